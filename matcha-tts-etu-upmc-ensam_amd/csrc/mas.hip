@@ -1,0 +1,460 @@
+// Monotonic Alignment Search on gfx950 (MI355X).
+//
+// Replaces the reference's host round trip  (matcha/utils/monotonic_align/__init__.py:40-55:
+// D2H copy -> Cython DP core.pyx:16-96 under OpenMP prange core.pyx:121 -> H2D copy) with two
+// stream-ordered kernels:
+//
+//   mas_dp_kernel<K,...>   one wave64 per utterance (the DP is a T_y-long dependency chain, so one
+//                          utterance never benefits from more than one wave).  Lane l owns the K
+//                          consecutive text rows x = l*K .. l*K+K-1 of the column; the x-1 neighbour
+//                          of row l*K comes from lane l-1 with one DPP `wave_shr:1` (no LDS, no
+//                          barrier).  The lattice streams through registers in chunks of C columns
+//                          (K*C = 32 cells per lane per chunk), double-buffered so chunk k+1 is in
+//                          flight while chunk k is computed; value*mask is formed on arrival.
+//                          Backpointers are bit-packed per row, 32 columns per word (bit 31-j =
+//                          column j of the word), in LDS when they fit and in the workspace
+//                          otherwise.  The backtrack walks rows, not columns: for the current row
+//                          it jumps straight to the highest diagonal bit at or below y with one
+//                          s_ff1, so it costs O(t_x + t_y/32) scalar steps instead of t_y dependent
+//                          loads.  Output: per-row start column (a monotone path is one contiguous
+//                          run per row).
+//   mas_expand_kernel      full-chip, coalesced float4 writer of the dense [B,Tx,Ty] path
+//                          (12 B/cell algorithmic traffic is dominated by this write + the reads).
+//
+// Numerics (bit-exact with the Cython): this file is compiled with -ffp-contract=off; value*mask is
+// one fp32 multiply (__init__.py:45), `best + score` one fp32 add (core.pyx:80), ties take the
+// diagonal (`from_prev >= from_same or x == y`, core.pyx:73), out-of-band cells hold max_neg_val.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "mtts_common.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kLdsBitsLimit = 48 * 1024;  // LDS bytes for backpointer words (total stays <= 64 KiB)
+
+struct MasArgs {
+    const float *value;     // [B,Tx,Ty]
+    const float *mask;      // [B,Tx,Ty] or null (lengths given explicitly)
+    const int32_t *t_xs;    // [B] or null (then from mask)
+    const int32_t *t_ys;    // [B] or null
+    int32_t *lengths;       // [B,2] (workspace or caller)
+    int32_t *row_start;     // [B,Tx]
+    uint32_t *bits;         // [B, nch, Txp] (global-bits mode only)
+    float *dp_out;          // [B,Tx,Ty] reference-mutated lattice, or null
+    int Tx, Ty, Txp, nch;
+    int premasked;
+    float neg;
+};
+
+__device__ __forceinline__ float dpp_wave_shr1(float src, float lane0_value) {
+    // lane l <- lane l-1; lane 0 keeps lane0_value (bound_ctrl = 0 disables the write there).
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, lane0_value),
+                                           __builtin_bit_cast(int, src), 0x138 /*wave_shr:1*/,
+                                           0xf, 0xf, false));
+}
+
+// Loads N consecutive floats of one lattice row.  Plain global loads: on ROCm 7.2 clang the
+// __builtin_amdgcn_raw_buffer_load_b64/_b128 builtins lower to a single dword load and alias every
+// component to element 0 (checked in the emitted IR), so the buffer-resource path is not used.
+// `eoff` is clamped so a load never leaves the utterance (columns past Ty are never consumed).
+template <int N, bool VEC>
+__device__ __forceinline__ void load_row_segment(const float *__restrict__ base, int eoff, int last,
+                                                 float (&dst)[N]) {
+    if constexpr (VEC && N % 4 == 0) {
+#pragma unroll
+        for (int q = 0; q < N / 4; ++q) {
+            const int o = min(eoff + 4 * q, last - 3);
+            const float4 v = *reinterpret_cast<const float4 *>(base + o);
+            dst[4 * q + 0] = v.x;
+            dst[4 * q + 1] = v.y;
+            dst[4 * q + 2] = v.z;
+            dst[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < N; ++q) dst[q] = base[min(eoff + q, last)];
+    }
+}
+
+template <int K, int C, bool VEC, bool LDS_BITS, bool DP_OUT>
+__global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
+    extern __shared__ uint32_t smem[];
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int Tx = a.Tx, Ty = a.Ty, Txp = a.Txp;
+    const size_t ubase = (size_t)b * Tx * Ty;
+    const float neg = a.neg;
+
+    // ---- lengths: explicit (core.pyx API) or from the mask (__init__.py:52-53) ----
+    int t_x, t_y;
+    if (a.t_xs) {
+        t_x = a.t_xs[b];
+        t_y = a.t_ys[b];
+    } else {
+        const float *m = a.mask + ubase;
+        float sx = 0.f, sy = 0.f;
+        for (int x = lane; x < Tx; x += kWave) sx += m[(size_t)x * Ty];
+        for (int y = lane; y < Ty; y += kWave) sy += m[y];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            sx += __shfl_xor(sx, off);
+            sy += __shfl_xor(sy, off);
+        }
+        t_x = (int)sx;
+        t_y = (int)sy;
+    }
+    t_x = __builtin_amdgcn_readfirstlane(t_x);
+    t_y = __builtin_amdgcn_readfirstlane(t_y);
+    if (lane == 0) {
+        a.lengths[2 * b] = t_x;
+        a.lengths[2 * b + 1] = t_y;
+    }
+
+    int32_t *rs = reinterpret_cast<int32_t *>(smem);  // [Txp] row starts
+    uint32_t *bits_l = smem + Txp;                      // [nch][Txp] (LDS mode)
+    uint32_t *bits_g = a.bits + (size_t)b * a.nch * Txp;
+    for (int x = lane; x < Txp; x += kWave) rs[x] = -1;
+
+    const bool valid = t_x >= 1 && t_y >= 1 && t_x <= t_y && t_x <= Tx && t_y <= Ty;
+    if (valid) {
+        // ------------------------------- forward DP -------------------------------
+        const int x0 = lane * K;
+        const unsigned span = (unsigned)(t_y - t_x);
+        int roff[K];  // element offset of each owned row (clamped into the utterance for loads)
+#pragma unroll
+        for (int i = 0; i < K; ++i) roff[i] = min(x0 + i, Tx - 1) * Ty;
+        const int last = Tx * Ty - 1;
+        const float *vbase = a.value + ubase;
+        const float *mbase = a.premasked ? vbase : a.mask + ubase;
+        const bool use_mask = !a.premasked;
+
+        float dp[K];
+        uint32_t R[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            dp[i] = neg;  // core.pyx:52-53
+            R[i] = 0u;
+        }
+
+        float va[K][C], ma[K][C], vb[K][C], mb[K][C];
+
+        auto load_chunk = [&](float (&vv)[K][C], float (&mm)[K][C], int y0) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) load_row_segment<C, VEC>(vbase, roff[i] + y0, last, vv[i]);
+            if (use_mask) {
+#pragma unroll
+                for (int i = 0; i < K; ++i) load_row_segment<C, VEC>(mbase, roff[i] + y0, last, mm[i]);
+            }
+        };
+
+        auto flush_bits = [&](int word_idx, int shift) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const uint32_t w = R[i] << shift;
+                if constexpr (LDS_BITS) {
+                    bits_l[word_idx * Txp + x0 + i] = w;
+                } else {
+                    bits_g[(size_t)word_idx * Txp + x0 + i] = w;
+                }
+                R[i] = 0u;
+            }
+        };
+
+        auto process_chunk = [&](float (&vv)[K][C], float (&mm)[K][C], int y0) {
+#pragma unroll
+            for (int j = 0; j < C; ++j) {
+                const int y = y0 + j;
+                if (y < t_y) {
+                    float s[K];
+#pragma unroll
+                    for (int i = 0; i < K; ++i) s[i] = use_mask ? vv[i][j] * mm[i][j] : vv[i][j];
+                    // x == 0 predecessor: 0 at y == 0, max_neg_val after (core.pyx:63-64)
+                    const float nb = dpp_wave_shr1(dp[K - 1], y == 0 ? 0.0f : neg);
+                    float ndp[K];
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        const float fp = (i == 0) ? nb : dp[i - 1];  // core.pyx:65-66
+                        const float fs = dp[i];                      // core.pyx:70-71 (dp init = neg)
+                        const int d = y - (x0 + i);
+                        const bool diag = (fp >= fs) || (d == 0);    // core.pyx:73
+                        const float best = diag ? fp : fs;
+                        const float v = best + s[i];                 // core.pyx:80
+                        ndp[i] = ((unsigned)d <= span) ? v : neg;    // band x_min..x_max, :59-62
+                        R[i] = (R[i] << 1) | (diag ? 1u : 0u);
+                    }
+#pragma unroll
+                    for (int i = 0; i < K; ++i) dp[i] = ndp[i];
+                    if constexpr (DP_OUT) {
+#pragma unroll
+                        for (int i = 0; i < K; ++i)
+                            if (x0 + i < t_x) a.dp_out[ubase + (size_t)(x0 + i) * Ty + y] = ndp[i];
+                    }
+                    if ((y & 31) == 31) flush_bits(y >> 5, 0);
+                }
+            }
+        };
+
+        const int nload = (t_y + C - 1) / C;
+        load_chunk(va, ma, 0);
+        for (int c = 0; c < nload; c += 2) {
+            if (c + 1 < nload) load_chunk(vb, mb, (c + 1) * C);
+            process_chunk(va, ma, c * C);
+            if (c + 1 >= nload) break;
+            if (c + 2 < nload) load_chunk(va, ma, (c + 2) * C);
+            process_chunk(vb, mb, (c + 1) * C);
+        }
+        if (t_y & 31) flush_bits(t_y >> 5, 32 - (t_y & 31));
+
+        if constexpr (!LDS_BITS) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        if constexpr (!LDS_BITS) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+
+        // ------------------------------- backtrack -------------------------------
+        // Row idx occupies columns [ydec, y]; ydec = the highest column <= y whose diagonal bit is
+        // set, or idx itself (forced diagonal at x == y, core.pyx:91).  Registers hold one chunk of
+        // words slot-major: W[r] lane l = row r*64 + l, so the row select is static per r-segment.
+        int idx = t_x - 1;
+        int y = t_y - 1;
+        int cur_c = -1;
+        uint32_t W[K];
+#pragma unroll
+        for (int r = 0; r < K; ++r) W[r] = 0u;
+        bool done = false;
+#pragma unroll
+        for (int r = K - 1; r >= 0; --r) {
+            while (!done && idx >= kWave * r) {
+                if (idx == 0) {  // row 0 runs down to column 0 (core.pyx:89-91: idx > 0 test)
+                    if (lane == 0) rs[0] = 0;
+                    done = true;
+                    break;
+                }
+                if (idx >= y) {  // on the diagonal: every remaining step is forced
+                    for (int x = lane; x <= idx; x += kWave) rs[x] = x;
+                    done = true;
+                    break;
+                }
+                const int c = y >> 5;
+                if (c != cur_c) {
+#pragma unroll
+                    for (int rr = 0; rr < K; ++rr) {
+                        if constexpr (LDS_BITS) {
+                            W[rr] = bits_l[c * Txp + rr * kWave + lane];
+                        } else {
+                            W[rr] = bits_g[(size_t)c * Txp + rr * kWave + lane];
+                        }
+                    }
+                    cur_c = c;
+                }
+                const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)W[r], idx & (kWave - 1));
+                const int base = c << 5;
+                uint32_t m = word & (0xFFFFFFFFu << (31 - (y - base)));  // columns <= y
+                if (idx >= base) m &= 0xFFFFFFFFu >> (idx - base);       // columns >= idx (in band)
+                int ydec;
+                if (m) {
+                    ydec = base + 31 - __builtin_ctz(m);
+                } else if (idx >= base) {
+                    ydec = idx;
+                } else {
+                    y = base - 1;
+                    continue;
+                }
+                if (lane == 0) rs[idx] = ydec;
+                idx -= 1;
+                y = ydec - 1;
+            }
+        }
+    }
+    __syncthreads();
+    int32_t *rs_out = a.row_start + (size_t)b * Tx;
+    for (int x = lane; x < Tx; x += kWave) rs_out[x] = rs[x];
+}
+
+// Dense writer: path[b,x,y] = 1 iff row_start[b,x] <= y <= row_end[b,x].  One block per (b, x,
+// 1024-column slab); float4 stores when rows are 16-byte aligned.
+template <typename T, bool SET_ONLY>
+__global__ __launch_bounds__(256) void mas_expand_kernel(const int32_t *__restrict__ row_start,
+                                                         const int32_t *__restrict__ lengths,
+                                                         T *__restrict__ path, int Tx, int Ty,
+                                                         int vec4) {
+    const int b = blockIdx.z, x = blockIdx.y;
+    const int t_x = lengths[2 * b], t_y = lengths[2 * b + 1];
+    const int32_t *rsb = row_start + (size_t)b * Tx;
+    int s = rsb[x];
+    int e = -1;
+    if (s >= 0) e = (x == t_x - 1) ? t_y - 1 : rsb[x + 1] - 1;
+    if (s < 0) s = 1;  // empty range
+    T *row = path + ((size_t)b * Tx + x) * Ty;
+    const int y0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (y0 >= Ty) return;
+    if constexpr (SET_ONLY) {
+        for (int k = 0; k < 4 && y0 + k < Ty; ++k)
+            if (y0 + k >= s && y0 + k <= e) row[y0 + k] = (T)1;
+    } else {
+        if (vec4 && y0 + 3 < Ty) {
+            float4 v;
+            v.x = (y0 + 0 >= s && y0 + 0 <= e) ? 1.f : 0.f;
+            v.y = (y0 + 1 >= s && y0 + 1 <= e) ? 1.f : 0.f;
+            v.z = (y0 + 2 >= s && y0 + 2 <= e) ? 1.f : 0.f;
+            v.w = (y0 + 3 >= s && y0 + 3 <= e) ? 1.f : 0.f;
+            *reinterpret_cast<float4 *>(row + y0) = v;
+        } else {
+            for (int k = 0; k < 4 && y0 + k < Ty; ++k)
+                row[y0 + k] = (y0 + k >= s && y0 + k <= e) ? (T)1 : (T)0;
+        }
+    }
+}
+
+struct WsLayout {
+    size_t lengths, row_start, bits, total;
+    int K, Txp, nch;
+    bool lds_bits;
+};
+
+WsLayout ws_layout(int B, int Tx, int Ty) {
+    WsLayout w{};
+    w.K = Tx <= 64 ? 1 : Tx <= 128 ? 2 : Tx <= 256 ? 4 : 8;
+    w.Txp = kWave * w.K;
+    w.nch = (Ty + 31) / 32;
+    w.lds_bits = (size_t)w.Txp * w.nch * 4 <= (size_t)kLdsBitsLimit;
+    size_t off = 0;
+    w.lengths = off;
+    off = mtts::align_up(off + (size_t)B * 2 * 4, 256);
+    w.row_start = off;
+    off = mtts::align_up(off + (size_t)B * Tx * 4, 256);
+    w.bits = off;
+    if (!w.lds_bits) off = mtts::align_up(off + (size_t)B * w.nch * w.Txp * 4, 256);
+    w.total = off;
+    return w;
+}
+
+template <int K, int C>
+int launch_dp_k(const MasArgs &a, int B, bool vec, bool lds_bits, bool dp_out, size_t shmem,
+                hipStream_t st) {
+    dim3 grid(B), block(kWave);
+#define MTTS_MAS_LAUNCH(V, L, D) \
+    hipLaunchKernelGGL((mas_dp_kernel<K, C, V, L, D>), grid, block, shmem, st, a)
+    if (vec) {
+        if (lds_bits) {
+            if (dp_out) MTTS_MAS_LAUNCH(true, true, true); else MTTS_MAS_LAUNCH(true, true, false);
+        } else {
+            if (dp_out) MTTS_MAS_LAUNCH(true, false, true); else MTTS_MAS_LAUNCH(true, false, false);
+        }
+    } else {
+        if (lds_bits) {
+            if (dp_out) MTTS_MAS_LAUNCH(false, true, true); else MTTS_MAS_LAUNCH(false, true, false);
+        } else {
+            if (dp_out) MTTS_MAS_LAUNCH(false, false, true); else MTTS_MAS_LAUNCH(false, false, false);
+        }
+    }
+#undef MTTS_MAS_LAUNCH
+    return mtts::check_launch("mas_dp_kernel");
+}
+
+int launch_dp(MasArgs a, int B, const WsLayout &w, bool vec, bool dp_out, hipStream_t st) {
+    size_t shmem = (size_t)w.Txp * 4 + (w.lds_bits ? (size_t)w.Txp * w.nch * 4 : 0);
+    switch (w.K) {
+        case 1: return launch_dp_k<1, 32>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+        case 2: return launch_dp_k<2, 16>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+        case 4: return launch_dp_k<4, 8>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+        default: return launch_dp_k<8, 4>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+    }
+}
+
+int check_shape(int B, int Tx, int Ty) {
+    if (B < 0 || Tx < 1 || Ty < 1) return mtts::fail(MTTS_ERR_INVALID_ARG, "maximum_path: bad shape");
+    if (Tx > MTTS_MAS_MAX_TX)
+        return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: Tx > MTTS_MAS_MAX_TX (512) is not supported");
+    if ((int64_t)Tx * Ty * 4 >= (int64_t)1 << 31)
+        return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: one utterance's lattice exceeds 2 GiB");
+    return MTTS_OK;
+}
+
+}  // namespace
+
+extern "C" size_t mtts_maximum_path_workspace_size(int32_t B, int32_t Tx, int32_t Ty) {
+    if (B < 0 || Tx < 1 || Ty < 1) return 0;
+    return ws_layout(B, Tx, Ty).total;
+}
+
+extern "C" int mtts_maximum_path_f32(const float *value, const float *mask, float *path, int32_t B,
+                                     int32_t Tx, int32_t Ty, int32_t flags, int32_t *lengths_out,
+                                     int32_t *row_start_out, void *workspace, size_t workspace_bytes,
+                                     void *hip_stream) {
+    int rc = check_shape(B, Tx, Ty);
+    if (rc) return rc;
+    MTTS_CHECK_ARG((flags & ~(MTTS_MAS_VALUE_PREMASKED | MTTS_MAS_NO_DENSE_PATH)) == 0,
+                   "maximum_path: unknown flag bits");
+    if (B == 0) return MTTS_OK;
+    MTTS_CHECK_ARG(value && mask, "maximum_path: value and mask are required");
+    MTTS_CHECK_ARG(path || (flags & MTTS_MAS_NO_DENSE_PATH), "maximum_path: path is null");
+    const WsLayout w = ws_layout(B, Tx, Ty);
+    if (!workspace || workspace_bytes < w.total)
+        return mtts::fail(MTTS_ERR_WORKSPACE, "maximum_path: workspace too small");
+    char *ws = static_cast<char *>(workspace);
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+
+    MasArgs a{};
+    a.value = value;
+    a.mask = mask;
+    a.lengths = lengths_out ? lengths_out : reinterpret_cast<int32_t *>(ws + w.lengths);
+    a.row_start = row_start_out ? row_start_out : reinterpret_cast<int32_t *>(ws + w.row_start);
+    a.bits = reinterpret_cast<uint32_t *>(ws + w.bits);
+    a.Tx = Tx;
+    a.Ty = Ty;
+    a.Txp = w.Txp;
+    a.nch = w.nch;
+    a.premasked = (flags & MTTS_MAS_VALUE_PREMASKED) ? 1 : 0;
+    a.neg = -1e9f;
+    const bool vec = (Ty % 4 == 0) && ((uintptr_t)value % 16 == 0) &&
+                     (a.premasked || (uintptr_t)mask % 16 == 0);
+    rc = launch_dp(a, B, w, vec, false, st);
+    if (rc || (flags & MTTS_MAS_NO_DENSE_PATH)) return rc;
+
+    dim3 grid((Ty + 1023) / 1024, Tx, B);
+    const int vec4 = (Ty % 4 == 0) && ((uintptr_t)path % 16 == 0);
+    hipLaunchKernelGGL((mas_expand_kernel<float, false>), grid, dim3(256), 0, st, a.row_start,
+                       a.lengths, path, Tx, Ty, vec4);
+    return mtts::check_launch("mas_expand_kernel");
+}
+
+extern "C" int mtts_compute_batch_alignments(int32_t *paths, float *values, const int32_t *t_xs,
+                                             const int32_t *t_ys, int32_t B, int32_t Tx, int32_t Ty,
+                                             float max_neg_val, void *workspace,
+                                             size_t workspace_bytes, void *hip_stream) {
+    int rc = check_shape(B, Tx, Ty);
+    if (rc) return rc;
+    if (B == 0) return MTTS_OK;
+    MTTS_CHECK_ARG(paths && values && t_xs && t_ys, "compute_batch_alignments: null pointer");
+    const WsLayout w = ws_layout(B, Tx, Ty);
+    if (!workspace || workspace_bytes < w.total)
+        return mtts::fail(MTTS_ERR_WORKSPACE, "compute_batch_alignments: workspace too small");
+    char *ws = static_cast<char *>(workspace);
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+
+    MasArgs a{};
+    a.value = values;
+    a.mask = nullptr;
+    a.t_xs = t_xs;
+    a.t_ys = t_ys;
+    a.lengths = reinterpret_cast<int32_t *>(ws + w.lengths);
+    a.row_start = reinterpret_cast<int32_t *>(ws + w.row_start);
+    a.bits = reinterpret_cast<uint32_t *>(ws + w.bits);
+    a.dp_out = values;  // in place, exactly like the Cython (core.pyx:83-85)
+    a.Tx = Tx;
+    a.Ty = Ty;
+    a.Txp = w.Txp;
+    a.nch = w.nch;
+    a.premasked = 1;
+    a.neg = max_neg_val;
+    const bool vec = (Ty % 4 == 0) && ((uintptr_t)values % 16 == 0);
+    rc = launch_dp(a, B, w, vec, true, st);
+    if (rc) return rc;
+    dim3 grid((Ty + 1023) / 1024, Tx, B);
+    hipLaunchKernelGGL((mas_expand_kernel<int32_t, true>), grid, dim3(256), 0, st, a.row_start,
+                       a.lengths, paths, Tx, Ty, 0);
+    return mtts::check_launch("mas_expand_kernel");
+}

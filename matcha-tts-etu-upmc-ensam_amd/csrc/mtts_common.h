@@ -1,0 +1,36 @@
+// Shared helpers for the libmtts_hip.so translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "mtts.h"
+
+namespace mtts {
+
+// Records a printf-style message in the calling thread's error slot (read by mtts_last_error).
+void set_error(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+
+inline int fail(int code, const char *msg) {
+    set_error("%s", msg);
+    return code;
+}
+
+inline int check_launch(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("%s: %s", what, hipGetErrorString(e));
+        return MTTS_ERR_HIP;
+    }
+    return MTTS_OK;
+}
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace mtts
+
+#define MTTS_CHECK_ARG(cond, msg)                                   \
+    do {                                                            \
+        if (!(cond)) return ::mtts::fail(MTTS_ERR_INVALID_ARG, msg); \
+    } while (0)
