@@ -1,0 +1,233 @@
+#!/usr/bin/env python
+"""Headline benchmark: Matcha-TTS training step on synthetic LJSpeech-shaped batches.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = forward (text encoder, fp32 log-prior lattice, HIP maximum_path, CFM decoder) + backward +
+grad-norm clip (1.0) + AdamW on B=32 utterances per GPU (Tx=120, Ty=600, 80 mels; BASELINE config 3,
+one process per GPU, data parallel over RCCL with DDP's bucketed all-reduce overlapped with
+backward).  Inputs are resident in HBM before the timed region.  Rank 0 prints ONE JSON line:
+value = utterances/s over all ranks (max-over-ranks wall time), plus maximum_path Mcells/s, the MAS
+kernel roofline (HIP events around every MAS launch in the timed region, on the launch stream) and,
+at N=1, the CPU baseline timed on this host (oracle restatement of the reference step, and the
+reference Cython MAS when oracle/_ref was built).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+PKG = ROOT / "matcha-tts-etu-upmc-ensam_amd"
+sys.path[:0] = [str(PKG), str(ROOT)]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BF16_DENSE_TFLOPS = 2500.0
+FP32_MFMA_TFLOPS = 157.3
+
+
+def decoder_train_flops(B: int, T: int) -> float:
+    """3 x (12.05e6 T + 3072 T^2) FLOPs per utterance per train step."""
+    return 3.0 * (12.05e6 * T + 3072.0 * T * T) * B
+
+
+def cpu_baseline(B_cpu: int, Tx: int, Ty: int, budget_s: float) -> dict:
+    """Reference CPU path timed on this host: the oracle's fp32 train step (train mode, dropout on)
+    + AdamW, and the MAS (reference Cython from oracle/_ref if built, else the C restatement)."""
+    import numpy as np
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    from oracle import matcha_oracle as MO  # cpu_baseline leg only
+    import oracle_bind as OB
+
+    def mp(value, mask):
+        path, _ = OB.maximum_path(value.detach().numpy(), mask.detach().numpy())
+        return torch.from_numpy(path)
+
+    threads = torch.get_num_threads()
+    torch.manual_seed(0)
+    model = MO.MatchaTTSOracle(150, 80, 192, maximum_path=mp)
+    model.train()
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, betas=(0.9, 0.999), weight_decay=1e-6)
+    from matcha.training import synthetic_batch
+
+    b = synthetic_batch(B_cpu, Tx, Ty, device="cpu")
+
+    def step():
+        dur, prior, diff, _ = model(b["x"], b["x_lengths"], b["y"], b["y_lengths"])
+        (dur + prior + diff).backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    step()
+    n, t0 = 0, time.perf_counter()
+    while n < 3 or (time.perf_counter() - t0 < budget_s and n < 20):
+        step()
+        n += 1
+    step_s = (time.perf_counter() - t0) / n
+    out = {"value": round(B_cpu / step_s, 3), "unit": "utterances/s", "cores": threads, "kind": "port",
+           "sample": f"{n} fp32 train steps (fwd+bwd+clip+AdamW, dropout on) of the oracle restatement "
+                     f"(oracle/matcha_oracle.py) at B={B_cpu}, Tx={Tx}, Ty={Ty}; {threads} torch threads"}
+    # MAS on the host: reference Cython when present (oracle/_ref), else the C restatement
+    rng = np.random.default_rng(0)
+    Bm = 32
+    value = rng.normal(-100.0, 10.0, size=(Bm, Tx, Ty)).astype(np.float32)
+    t_x = np.full(Bm, Tx, np.int32)
+    t_y = np.full(Bm, Ty, np.int32)
+    kind, fn = "port", None
+    so = sorted((ROOT / "oracle" / "_ref").glob("core*.so"))
+    if so:
+        import importlib.util
+
+        spec = importlib.util.spec_from_file_location("core", so[0])
+        core = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(core)
+        kind = "reference"
+
+        def fn():
+            p = np.zeros(value.shape, np.int32)
+            core.compute_batch_alignments(p, value.copy(), t_x, t_y)
+    else:
+        def fn():
+            OB.mas_batch(value, t_x, t_y)
+    fn()
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 3.0:
+        fn()
+        n += 1
+    ms = (time.perf_counter() - t0) / n * 1e3
+    out["mas"] = {"value": round(Bm * Tx * Ty / ms / 1e3, 1), "unit": "Mcells/s", "kind": kind,
+                  "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
+                  "sample": f"{n} x compute_batch_alignments B={Bm} {Tx}x{Ty} ({ms:.3f} ms each, incl. copy)"}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--tx", type=int, default=120)
+    ap.add_argument("--ty", type=int, default=600)
+    ap.add_argument("--precision", default="32-true", choices=["32-true", "bf16-mixed"])
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import matcha.utils.monotonic_align as MA
+    from matcha.models.matcha_tts import MatchaTTS
+    from matcha.training import TrainConfig, Trainer, synthetic_batch
+
+    torch.manual_seed(1234)  # identical init on every rank (DDP also broadcasts rank 0's weights)
+    model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(dev)
+    model.train()
+    trainer = Trainer(model, TrainConfig(precision=args.precision))
+    B, Tx, Ty = args.batch, args.tx, args.ty
+    batch = synthetic_batch(B, Tx, Ty, seed=1000 + rank, device=dev)
+
+    # HIP events around every maximum_path launch (recorded on torch's current stream, which is
+    # the stream mtts_maximum_path_f32 is launched on)
+    mas_events: list = []
+    record = {"on": False}
+    real_mp = MA.maximum_path
+
+    def timed_mp(value, mask, **kw):
+        if not record["on"]:
+            return real_mp(value, mask, **kw)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = real_mp(value, mask, **kw)
+        e1.record()
+        mas_events.append((e0, e1))
+        return out
+
+    MA.maximum_path = timed_mp
+
+    for _ in range(args.warmup):
+        trainer.step([batch])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    record["on"] = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.step([batch])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    record["on"] = False
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    losses = trainer.last_losses.tolist()
+
+    mas_ms = sum(a.elapsed_time(b) for a, b in mas_events) / max(len(mas_events), 1)
+    cells = B * Tx * Ty
+    mas_gbs = 12.0 * cells / (mas_ms * 1e-3) / 1e9
+    step_ms = elapsed / args.steps * 1e3
+    flops = decoder_train_flops(B, Ty)
+
+    if rank == 0:
+        rec = {
+            "metric": "training utterances/sec (whole node) + maximum_path Mcells/sec, LJSpeech batch=32",
+            "value": round(world * B * args.steps / elapsed, 2),
+            "unit": "utterances/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(step_ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if args.precision == "32-true" else "bf16",
+            "data": "synthetic LJSpeech-shaped batches (random tokens/mels, ragged lengths), random-init weights",
+            "config": {"workload": f"MatchaTTS train step (encoder + MAS + CFM decoder fwd/bwd + clip + AdamW), "
+                                   f"B={B}/GPU, Tx={Tx}, Ty={Ty}, 80 mels",
+                       "model": "MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192)",
+                       "global_batch": world * B, "seq_len": Ty, "text_len": Tx, "parallelism": f"dp{world}",
+                       "precision": args.precision},
+            "maximum_path": {"value": round(world * cells / mas_ms / 1e3, 1), "unit": "Mcells/s (whole node)",
+                             "ms_per_call": round(mas_ms, 4), "calls": len(mas_events)},
+            "roofline": {"kernel": "mas_dp_kernel + mas_expand_kernel (maximum_path)", "bound": "hbm",
+                         "achieved": round(mas_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(mas_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "algorithmic_bytes_per_launch": 12 * cells,
+                         "note": "12 B/cell (value+mask read, path write); chain-bound: one wave per utterance"},
+            "decoder_mfma": {"train_flops_per_step": flops,
+                             "achieved_tflops_step": round(flops / (step_ms * 1e-3) / 1e12, 2),
+                             "peak_tflops": FP32_MFMA_TFLOPS if args.precision == "32-true" else BF16_DENSE_TFLOPS},
+            "losses": [round(v, 5) for v in losses],
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(4, Tx, Ty, args.cpu_budget)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,234 @@
+"""CFM velocity estimator: 1-D U-Net of ResNet + transformer blocks (drop-in for
+matcha/models/components/decoder.py).
+
+Same constructor, same module tree and parameter names as the reference (decoder.py:118-253), same
+forward signature ``forward(x, mask, mu, t, cond=None)`` with channel-major [B, C, T] in/out.
+Internally the activations are token-major [B, T, C] from the input pack to the final projection
+(see _ops.py); the reference's semantics are kept exactly, including its padding-dependent quirks:
+GroupNorm statistics over the full padded length, the ResNet residual not re-masked (:85), the
+half-resolution mask as a prefix slice (:311-316), nearest interpolation for odd lengths (:338-339,
+:361-364), and the float 0/1 attention mask used as an additive bias.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from matcha.models.components import _ops as O
+from matcha.models.components.transformer import BasicTransformerBlock
+
+
+class SinusoidalPosEmb(nn.Module):
+    """decoder.py:8-31: t -> [sin(1000 t f_k), cos(1000 t f_k)], f_k = exp(-k ln(1e4)/(dim/2-1))."""
+
+    def __init__(self, dim):
+        super().__init__()
+        assert dim % 2 == 0, "SinusoidalPosEmb needs an even dimension"
+        self.dim = dim
+
+    def forward(self, x, scale=1000):
+        if x.ndim < 1:
+            x = x.unsqueeze(0)
+        half = self.dim // 2
+        step = math.log(10000.0) / (half - 1)
+        freq = torch.exp(torch.arange(half, device=x.device, dtype=torch.float32) * -step)
+        arg = scale * x.float().unsqueeze(1) * freq.unsqueeze(0)
+        return torch.cat((arg.sin(), arg.cos()), dim=-1)
+
+
+class TimeStepEmbeddingNet(nn.Module):
+    """decoder.py:33-49: Linear -> SiLU -> Linear on [B, in]."""
+
+    def __init__(self, in_channels, time_embed_dim):
+        super().__init__()
+        self.linear_1 = nn.Linear(in_channels, time_embed_dim)
+        self.act = nn.SiLU()
+        self.linear_2 = nn.Linear(time_embed_dim, time_embed_dim)
+
+    def forward(self, sample):
+        return self.linear_2(self.act(self.linear_1(sample)))
+
+
+class Block1D(nn.Module):
+    """decoder.py:51-66: mish(GN(conv3(x*m))) * m  -- token-major, GN+Mish+mask fused."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, padding=1, groups=8):
+        super().__init__()
+        self.block = nn.Sequential(
+            nn.Conv1d(in_channels, out_channels, kernel_size, padding=padding),
+            nn.GroupNorm(groups, out_channels),
+            nn.Mish(),
+        )
+
+    def forward_tm(self, x, mask, add=None):
+        conv, gn = self.block[0], self.block[1]
+        h = O.conv_tm(x, conv.weight, conv.bias, mask, padding=conv.padding[0])
+        return O.group_norm_mish_tm(h, gn.weight, gn.bias, gn.num_groups, mask, add, gn.eps)
+
+    def forward(self, x, mask):  # channel-major API of the reference
+        return self.forward_tm(x.transpose(1, 2), mask[:, 0]).transpose(1, 2)
+
+
+class Resnet1D(nn.Module):
+    """decoder.py:68-86: block2(block1(x) + mlp(t)) + res_conv(x*m); the result is not re-masked."""
+
+    def __init__(self, in_channels, out_channels, time_emb_dim, kernel_size=3, padding=1, groups=8):
+        super().__init__()
+        self.mlp = nn.Sequential(nn.Mish(), nn.Linear(time_emb_dim, out_channels))
+        self.block1 = Block1D(in_channels, out_channels, kernel_size, padding, groups)
+        self.block2 = Block1D(out_channels, out_channels, kernel_size, padding, groups)
+        self.res_conv = nn.Conv1d(in_channels, out_channels, 1)
+
+    def forward_tm(self, x, mask, time_emb):
+        h = self.block1.forward_tm(x, mask, add=self.mlp(time_emb))
+        h = self.block2.forward_tm(h, mask)
+        return O.conv_tm(x, self.res_conv.weight, self.res_conv.bias, mask, padding=0) + h
+
+    def forward(self, x, mask, time_emb):
+        return self.forward_tm(x.transpose(1, 2), mask[:, 0], time_emb).transpose(1, 2)
+
+
+class Downsample1D(nn.Module):
+    """decoder.py:88-98: Conv1d(k3, s2, p1) -> ceil(T/2) frames."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.conv = nn.Conv1d(dim, dim, kernel_size=3, stride=2, padding=1)
+
+    def forward_tm(self, x, mask):
+        return O.conv_tm(x, self.conv.weight, self.conv.bias, mask, stride=2, padding=1)
+
+    def forward(self, x):
+        return self.conv(x)
+
+
+class Upsample1D(nn.Module):
+    """decoder.py:100-116: ConvTranspose1d(k4, s2, p1) -> 2T frames."""
+
+    def __init__(self, channels, out_channels=None):
+        super().__init__()
+        self.channels = channels
+        self.out_channels = out_channels or channels
+        self.conv = nn.ConvTranspose1d(channels, self.out_channels, 4, 2, 1)
+
+    def forward_tm(self, x, mask):
+        return O.conv_transpose_tm(x, self.conv.weight, self.conv.bias, mask)
+
+    def forward(self, inputs):
+        assert inputs.shape[1] == self.channels
+        return self.conv(inputs)
+
+
+def _conv_tm(mod: nn.Conv1d, x, mask):
+    return O.conv_tm(x, mod.weight, mod.bias, mask, stride=mod.stride[0], padding=mod.padding[0])
+
+
+class Decoder(nn.Module):
+    """decoder.py:118-371.  channels=(256,256), 1 transformer per level, 2 mid blocks, 4 heads x 64."""
+
+    def __init__(self, in_channels, out_channels, channels=(256, 256), dropout=0.05, attention_head_dim=64,
+                 n_blocks=1, num_mid_blocks=2, num_heads=4):
+        super().__init__()
+        channels = tuple(channels)
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.time_embeddings = SinusoidalPosEmb(dim=in_channels)
+        time_embed_dim = channels[0] * 4
+        self.time_mlp = TimeStepEmbeddingNet(in_channels, time_embed_dim)
+
+        def tblocks(dim):
+            return nn.ModuleList([
+                BasicTransformerBlock(dim=dim, num_attention_heads=num_heads, attention_head_dim=attention_head_dim,
+                                      dropout=dropout, activation_fn="gelu")
+                for _ in range(n_blocks)])
+
+        self.Downsampling_Blocks = nn.ModuleList([])
+        self.Mid_Blocks = nn.ModuleList([])
+        self.Upsampling_Blocks = nn.ModuleList([])
+        out_c = in_channels
+        for i, c in enumerate(channels):
+            in_c, out_c = out_c, c
+            last = i == len(channels) - 1
+            down = nn.Conv1d(out_c, out_c, kernel_size=3, padding=1) if last else Downsample1D(out_c)
+            self.Downsampling_Blocks.append(nn.ModuleList([Resnet1D(in_c, out_c, time_embed_dim), tblocks(out_c), down]))
+        for _ in range(num_mid_blocks):
+            self.Mid_Blocks.append(nn.ModuleList([Resnet1D(channels[-1], channels[-1], time_embed_dim),
+                                                  tblocks(channels[-1])]))
+        rev = channels[::-1] + (channels[0],)
+        for i in range(len(rev) - 1):
+            last = i == len(rev) - 2
+            up = nn.Conv1d(rev[i + 1], rev[i + 1], kernel_size=3, padding=1) if last else Upsample1D(rev[i + 1])
+            self.Upsampling_Blocks.append(nn.ModuleList([Resnet1D(2 * rev[i], rev[i + 1], time_embed_dim),
+                                                         tblocks(rev[i + 1]), up]))
+        self.final_conv = nn.Conv1d(channels[0], channels[0], kernel_size=3, padding=1)
+        self.final_norm = nn.GroupNorm(8, channels[0])
+        self.final_act = nn.Mish()
+        self.final_proj = nn.Conv1d(channels[0], self.out_channels, kernel_size=1)
+        self.initialize_weights()
+
+    def initialize_weights(self):
+        """decoder.py:255-268 (kaiming-normal convs/linears, zero biases, unit GroupNorm)."""
+        for m in self.modules():
+            if isinstance(m, (nn.Conv1d, nn.Linear)):
+                nn.init.kaiming_normal_(m.weight, nonlinearity="relu")
+                if m.bias is not None:
+                    nn.init.constant_(m.bias, 0)
+            elif isinstance(m, nn.GroupNorm):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+
+    @staticmethod
+    def _transformers(blocks, x, mask):
+        for blk in blocks:
+            x = blk.forward_tm(x, mask)
+        return x
+
+    def forward_tm(self, x, mask, mu, t):
+        """x, mu: [B, T, C] token-major; mask [B, T]; t [B] -> [B, T, out] token-major."""
+        temb = self.time_mlp(self.time_embeddings(t))
+        h = torch.cat([x, mu], dim=-1)  # einops pack "b * t" on channels (:288)
+        skips, masks = [], [mask]
+        for resnet, tfs, down in self.Downsampling_Blocks:
+            m = masks[-1]
+            h = self._transformers(tfs, resnet.forward_tm(h, m, temb), m)
+            skips.append(h)
+            if isinstance(down, Downsample1D):
+                h = down.forward_tm(h, m)
+                masks.append(m[:, : (m.shape[-1] + 1) // 2])  # prefix slice (:311-316)
+            else:
+                h = _conv_tm(down, h, m)
+                masks.append(m)
+        masks = masks[:-1]
+        m = masks[-1]
+        for resnet, tfs in self.Mid_Blocks:
+            h = self._transformers(tfs, resnet.forward_tm(h, m, temb), m)
+        for resnet, tfs, up in self.Upsampling_Blocks:
+            m = masks.pop()
+            skip = skips.pop()
+            if h.shape[1] != skip.shape[1]:  # odd T: nearest to the skip length (:338-339)
+                h = F.interpolate(h.transpose(1, 2), size=skip.shape[1], mode="nearest").transpose(1, 2)
+            h = torch.cat([h, skip], dim=-1)
+            h = self._transformers(tfs, resnet.forward_tm(h, m, temb), m)
+            if isinstance(up, Upsample1D):
+                h = up.forward_tm(h, m)
+                new = m.shape[-1] * 2
+            else:
+                h = _conv_tm(up, h, m)
+                new = h.shape[1]
+            if new > m.shape[-1]:
+                m = F.interpolate(m.unsqueeze(1), size=new, mode="nearest")[:, 0]
+            else:
+                m = m[:, :new]
+        h = _conv_tm(self.final_conv, h, m)
+        h = O.group_norm_mish_tm(h, self.final_norm.weight, self.final_norm.bias, self.final_norm.num_groups,
+                                 torch.ones_like(m), None, self.final_norm.eps)
+        out = _conv_tm(self.final_proj, h, m)
+        return out * mask.unsqueeze(-1)
+
+    def forward(self, x, mask, mu, t, cond=None):
+        """Reference signature: x, mu [B, C, T]; mask [B, 1, T]; t [B] -> [B, out, T]."""
+        out = self.forward_tm(x.transpose(1, 2), mask[:, 0], mu.transpose(1, 2), t)
+        return out.transpose(1, 2)

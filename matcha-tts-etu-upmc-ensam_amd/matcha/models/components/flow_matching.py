@@ -1,0 +1,71 @@
+"""Conditional flow matching: training loss and Euler sampler (drop-in for
+matcha/models/components/flow_matching.py).
+
+Reference: BaseConditionalFlowMatching flow_matching.py:12-151, ConditionalFlowMatching :154-189.
+compute_loss keeps the reference's RNG order (t = rand([B,1,1]) then z = randn_like(x1), :130,:133),
+its unmasked velocity target (:142) and its sum / (sum(mask) * n_feats) normalisation (:148-149).
+Keyword-only ``t``/``z`` let parity tests inject the randomness.
+"""
+from __future__ import annotations
+
+from abc import ABC
+
+import torch
+import torch.nn as nn
+
+from matcha.models.components.decoder import Decoder
+
+
+class BaseConditionalFlowMatching(nn.Module, ABC):
+    def __init__(self, n_feats, cfm_params, n_spks=1, spk_emb_dim=128):
+        super().__init__()
+        self.n_feats = n_feats
+        self.n_spks = n_spks
+        self.spk_emb_dim = spk_emb_dim
+        self.solver = getattr(cfm_params, "solver", "euler")
+        self.sigma_min = getattr(cfm_params, "sigma_min", 1e-4)
+        self.estimator = None
+
+    @torch.inference_mode()
+    def forward(self, mu, mask, n_timesteps, temperature=1.0, spks=None, cond=None):
+        """flow_matching.py:42-65: Euler integration of the learned velocity from N(0, T^2)."""
+        z = torch.randn_like(mu) * temperature
+        t_span = torch.linspace(0, 1, n_timesteps + 1, device=mu.device)
+        return self.solve_ode_euler(z, t_span, mu, mask, spks, cond)
+
+    def solve_ode_euler(self, x, t_span, mu, mask, spks, cond):
+        """flow_matching.py:67-104 (same t/dt recurrence)."""
+        t = t_span[0]
+        dt = t_span[1] - t_span[0]
+        for step in range(1, len(t_span)):
+            x = x + dt * self.estimator(x, mask, mu, t.expand(x.shape[0]), cond)
+            t = t + dt
+            if step < len(t_span) - 1:
+                dt = t_span[step + 1] - t
+        return x
+
+    def compute_loss(self, x1, mask, mu, spks=None, cond=None, *, t=None, z=None):
+        """Returns (loss, phi_t).  x1/mu [B, n_feats, T], mask [B, 1, T]."""
+        b = mu.shape[0]
+        if t is None:
+            t = torch.rand([b, 1, 1], device=mu.device, dtype=mu.dtype)
+        if z is None:
+            z = torch.randn_like(x1)
+        s = self.sigma_min
+        phi_t = (1 - (1 - s) * t) * z + t * x1
+        u_target = x1 - (1 - s) * z
+        u_pred = self.estimator.forward_tm(phi_t.transpose(1, 2), mask[:, 0], mu.transpose(1, 2),
+                                           t.reshape(b))
+        loss = torch.sum((u_pred - u_target.transpose(1, 2)) ** 2) / (torch.sum(mask) * u_target.shape[1])
+        return loss, phi_t
+
+
+class ConditionalFlowMatching(BaseConditionalFlowMatching):
+    def __init__(self, in_channels, out_channel, cfm_params, decoder_params, n_spks=1, spk_emb_dim=64):
+        super().__init__(n_feats=in_channels, cfm_params=cfm_params, n_spks=n_spks, spk_emb_dim=spk_emb_dim)
+        if n_spks > 1:
+            in_channels = in_channels + spk_emb_dim
+        self.estimator = Decoder(in_channels=in_channels, out_channels=out_channel, **decoder_params)
+
+
+CFM = ConditionalFlowMatching

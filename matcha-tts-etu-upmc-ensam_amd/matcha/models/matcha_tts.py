@@ -1,0 +1,130 @@
+"""Matcha-TTS model (drop-in for matcha/models/matcha_tts.py).
+
+Reference: MatchaTTS :219-325 (simple-params init :294-366, synthesise :368-435, forward :437-515).
+The train-step forward keeps the reference's order and arithmetic; the monotonic alignment runs on
+the GPU (matcha.utils.monotonic_align.maximum_path -> csrc/mas.hip) instead of the reference's
+device->host->device Cython round trip, so the step never synchronises with the host.  The log-prior
+lattice is computed in fp32 with autocast disabled: maximum_path is bit-exact only on the identical
+fp32 lattice.
+"""
+from __future__ import annotations
+
+import datetime as dt
+import math
+import random
+from types import SimpleNamespace
+
+import torch
+
+import matcha.utils.monotonic_align as monotonic_align
+from matcha.models.baselightningmodule import BaseLightningClass
+from matcha.models.components.flow_matching import ConditionalFlowMatching as CFM
+from matcha.models.components.text_encoder import TextEncoder
+from matcha.utils.model import denormalize, duration_loss, fix_len_compatibility, generate_path, sequence_mask
+
+
+class MatchaTTS(BaseLightningClass):
+    def __init__(self, n_vocab, n_feats=None, encoder=None, decoder=None, cfm=None, data_statistics=None,
+                 out_size=None, optimizer=None, scheduler=None, prior_loss=True, use_precomputed_durations=False,
+                 out_channels=None, hidden_channels=None):
+        super().__init__()
+        self.n_vocab = n_vocab
+        self.n_spks = 1
+        self.out_size = out_size
+        self.prior_loss = prior_loss
+        self.use_precomputed_durations = use_precomputed_durations
+        self.scheduler_config = scheduler
+        if encoder is not None and decoder is not None and cfm is not None:  # :264-292
+            self.n_feats = n_feats
+            self.encoder = TextEncoder(encoder.encoder_type, encoder.encoder_params,
+                                       encoder.duration_predictor_params, n_vocab)
+            self.decoder = CFM(in_channels=2 * encoder.encoder_params.n_feats,
+                               out_channel=encoder.encoder_params.n_feats, cfm_params=cfm, decoder_params=decoder)
+        else:  # :294-366
+            if out_channels is None or hidden_channels is None:
+                raise ValueError("give either (encoder, decoder, cfm) configs or (out_channels, hidden_channels)")
+            self.n_feats = out_channels
+            enc = SimpleNamespace(
+                encoder_type="transformer",
+                encoder_params=SimpleNamespace(n_feats=out_channels, n_channels=hidden_channels, filter_channels=768,
+                                               n_heads=2, n_layers=6, kernel_size=3, p_dropout=0.1, prenet=True),
+                duration_predictor_params=SimpleNamespace(filter_channels_dp=256, kernel_size=3, p_dropout=0.1))
+            self.encoder = TextEncoder(enc.encoder_type, enc.encoder_params, enc.duration_predictor_params, n_vocab)
+            self.decoder = CFM(in_channels=2 * out_channels, out_channel=out_channels,
+                               cfm_params=SimpleNamespace(solver="euler", sigma_min=1e-4),
+                               decoder_params={"channels": (256, 256), "dropout": 0.05, "attention_head_dim": 64,
+                                               "n_blocks": 1, "num_mid_blocks": 2, "num_heads": 4})
+        if data_statistics is None:
+            data_statistics = {"mel_mean": 0.0, "mel_std": 1.0}
+        self.update_data_statistics(data_statistics)
+
+    @torch.inference_mode()
+    def synthesise(self, x, x_lengths, n_timesteps, temperature=1.0, length_scale=1.0):
+        """matcha_tts.py:368-435."""
+        t0 = dt.datetime.now()
+        mu_x, logw, x_mask = self.encoder(x, x_lengths)
+        w_ceil = torch.ceil(torch.exp(logw) * x_mask) * length_scale
+        y_lengths = torch.clamp_min(torch.sum(w_ceil, [1, 2]), 1).long()
+        y_max_length = y_lengths.max()
+        y_max_length_ = fix_len_compatibility(y_max_length)
+        y_mask = sequence_mask(y_lengths, y_max_length_).unsqueeze(1).to(x_mask.dtype)
+        attn_mask = x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)
+        attn = generate_path(w_ceil.squeeze(1), attn_mask.squeeze(1)).unsqueeze(1)
+        mu_y = torch.matmul(attn.squeeze(1).transpose(1, 2), mu_x.transpose(1, 2)).transpose(1, 2)
+        decoder_outputs = self.decoder(mu_y, y_mask, n_timesteps, temperature)[:, :, :y_max_length]
+        rtf = (dt.datetime.now() - t0).total_seconds() * 22050 / (decoder_outputs.shape[-1] * 256)
+        return {"encoder_outputs": mu_y[:, :, :y_max_length], "decoder_outputs": decoder_outputs,
+                "attn": attn[:, :, :y_max_length], "mel": denormalize(decoder_outputs, self.mel_mean, self.mel_std),
+                "mel_lengths": y_lengths, "rtf": rtf}
+
+    def log_prior(self, mu_x, y):
+        """matcha_tts.py:467-472 in fp32: -1/2 sum y^2 + sum mu*y - 1/2 sum mu^2 - n/2 log(2 pi)."""
+        with torch.autocast(device_type=mu_x.device.type, enabled=False):
+            mu_x = mu_x.float()
+            y = y.float()
+            const = -0.5 * math.log(2 * math.pi) * self.n_feats
+            factor = -0.5 * torch.ones(mu_x.shape, dtype=mu_x.dtype, device=mu_x.device)
+            y_square = torch.matmul(factor.transpose(1, 2), y ** 2)
+            y_mu_double = torch.matmul(2.0 * (factor * mu_x).transpose(1, 2), y)
+            mu_square = torch.sum(factor * (mu_x ** 2), 1).unsqueeze(-1)
+            return y_square - y_mu_double + mu_square + const
+
+    def forward(self, x, x_lengths, y, y_lengths, out_size=None, cond=None, durations=None, *, t=None, z=None):
+        """Returns (dur_loss, prior_loss, diff_loss, attn) -- matcha_tts.py:437-515.  ``t``/``z``
+        (keyword-only) inject the CFM randomness for parity tests."""
+        mu_x, logw, x_mask = self.encoder(x, x_lengths)
+        y_max_length = y.shape[-1]
+        y_mask = sequence_mask(y_lengths, y_max_length).unsqueeze(1).to(x_mask)
+        attn_mask = x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)
+        if self.use_precomputed_durations:
+            attn = generate_path(durations.squeeze(1), attn_mask.squeeze(1))
+        else:
+            with torch.no_grad():
+                lp = self.log_prior(mu_x.detach(), y)
+                attn = monotonic_align.maximum_path(lp, attn_mask.squeeze(1)).detach()
+        logw_ = torch.log(1e-8 + torch.sum(attn.unsqueeze(1), -1)) * x_mask
+        dur_loss = duration_loss(logw, logw_, x_lengths)
+        if out_size is not None:  # :480-502 (host-side random crop, as the reference)
+            max_offset = (y_lengths - out_size).clamp(0)
+            offset_ranges = list(zip([0] * max_offset.shape[0], max_offset.cpu().numpy()))
+            out_offset = torch.LongTensor([random.choice(range(s, e)) if e > s else 0
+                                           for s, e in offset_ranges]).to(y_lengths)
+            attn_cut = torch.zeros(attn.shape[0], attn.shape[1], out_size, dtype=attn.dtype, device=attn.device)
+            y_cut = torch.zeros(y.shape[0], self.n_feats, out_size, dtype=y.dtype, device=y.device)
+            y_cut_lengths = []
+            for i, (y_, off) in enumerate(zip(y, out_offset)):
+                L = out_size + (y_lengths[i] - out_size).clamp(None, 0)
+                y_cut_lengths.append(L)
+                y_cut[i, :, :L] = y_[:, off:off + L]
+                attn_cut[i, :, :L] = attn[i, :, off:off + L]
+            y_cut_lengths = torch.LongTensor(y_cut_lengths)
+            y_mask = sequence_mask(y_cut_lengths).unsqueeze(1).to(y_mask)
+            attn, y = attn_cut, y_cut
+        mu_y = torch.matmul(attn.squeeze(1).transpose(1, 2), mu_x.transpose(1, 2)).transpose(1, 2)
+        diff_loss, _ = self.decoder.compute_loss(x1=y, mask=y_mask, mu=mu_y, cond=cond, t=t, z=z)
+        if self.prior_loss:
+            prior_loss = torch.sum(0.5 * ((y - mu_y) ** 2 + math.log(2 * math.pi)) * y_mask)
+            prior_loss = prior_loss / (torch.sum(y_mask) * self.n_feats)
+        else:
+            prior_loss = 0
+        return dur_loss, prior_loss, diff_loss, attn

@@ -11,6 +11,8 @@ training forward:
   model forward  /root/reference/matcha/models/matcha_tts.py:437-515 (simple-params init :294-366)
   utilities      /root/reference/matcha/utils/model.py:13-135
 Parameter names equal the reference's, so a state_dict moves between reference, oracle and product.
+Dropout layers sit where the reference has them (decoder 0.05, encoder 0.1) and are active only in
+train mode: parity tests run eval(); bench.py's cpu_baseline times the train-mode step.
 MAS inside MatchaTTSOracle.forward is the C oracle (oracle/mas_oracle.c) via tests/oracle_bind.py.
 
 Pinned by tests/test_oracle_golden.py / tests/test_model_oracle.py against decoder_golden.npz and
@@ -90,14 +92,14 @@ class Up(nn.Module):  # Upsample1D, decoder.py:100-116
 class Attn(nn.Module):
     """diffusers 0.25 Attention + AttnProcessor2_0 as used by transformer.py:251-259, 320-325."""
 
-    def __init__(self, dim, heads, dim_head):
+    def __init__(self, dim, heads, dim_head, dropout=0.0):
         super().__init__()
         inner = heads * dim_head
         self.heads = heads
         self.to_q = nn.Linear(dim, inner, bias=False)
         self.to_k = nn.Linear(dim, inner, bias=False)
         self.to_v = nn.Linear(dim, inner, bias=False)
-        self.to_out = nn.ModuleList([nn.Linear(inner, dim), nn.Identity()])
+        self.to_out = nn.ModuleList([nn.Linear(inner, dim), nn.Dropout(dropout)])
 
     def forward(self, h, key_mask):
         B, T, _ = h.shape
@@ -108,7 +110,7 @@ class Attn(nn.Module):
         s = q @ k.transpose(-1, -2) / math.sqrt(q.shape[-1])
         s = s + key_mask[:, None, None, :]  # float 0/1 mask added, not masked
         o = torch.softmax(s, dim=-1) @ v
-        return self.to_out[0](o.transpose(1, 2).reshape(B, T, -1))
+        return self.to_out[1](self.to_out[0](o.transpose(1, 2).reshape(B, T, -1)))
 
 
 class GELUProj(nn.Module):  # diffusers GELU(dim, inner) : Linear + erf gelu
@@ -121,21 +123,21 @@ class GELUProj(nn.Module):  # diffusers GELU(dim, inner) : Linear + erf gelu
 
 
 class FF(nn.Module):  # FeedForward, transformer.py:105-188 (net = [GELU, Dropout, Linear])
-    def __init__(self, dim, mult=4):
+    def __init__(self, dim, mult=4, dropout=0.0):
         super().__init__()
-        self.net = nn.ModuleList([GELUProj(dim, dim * mult), nn.Identity(), nn.Linear(dim * mult, dim)])
+        self.net = nn.ModuleList([GELUProj(dim, dim * mult), nn.Dropout(dropout), nn.Linear(dim * mult, dim)])
 
     def forward(self, x):
-        return self.net[2](self.net[0](x))
+        return self.net[2](self.net[1](self.net[0](x)))
 
 
 class TBlock(nn.Module):  # BasicTransformerBlock (diffusers branch), transformer.py:297-370
-    def __init__(self, dim, heads, dim_head):
+    def __init__(self, dim, heads, dim_head, dropout=0.0):
         super().__init__()
         self.norm1 = nn.LayerNorm(dim)
-        self.attn1 = Attn(dim, heads, dim_head)
+        self.attn1 = Attn(dim, heads, dim_head, dropout)
         self.norm3 = nn.LayerNorm(dim)
-        self.ff = FF(dim)
+        self.ff = FF(dim, dropout=dropout)
 
     def forward(self, h, key_mask):
         h = self.attn1(self.norm1(h), key_mask) + h
@@ -154,7 +156,7 @@ class DecoderOracle(nn.Module):
         self.time_mlp = TimeMLP(in_channels, tdim)
 
         def tblocks(c):
-            return nn.ModuleList([TBlock(c, num_heads, attention_head_dim) for _ in range(n_blocks)])
+            return nn.ModuleList([TBlock(c, num_heads, attention_head_dim, dropout) for _ in range(n_blocks)])
 
         self.Downsampling_Blocks = nn.ModuleList()
         cout = in_channels
@@ -244,8 +246,9 @@ def sequence_mask(lengths, max_len=None):  # model.py:13-34
 
 
 class ConvReluNormO(nn.Module):  # text_encoder.py:17-57
-    def __init__(self, c, k=5, n=3):
+    def __init__(self, c, k=5, n=3, p=0.1):
         super().__init__()
+        self.drop = nn.Dropout(p)
         self.convolutions = nn.ModuleList([nn.Conv1d(c, c, k, padding=k // 2) for _ in range(n)])
         self.normalizations = nn.ModuleList([nn.LayerNorm(c) for _ in range(n)])
         self.projection = nn.Conv1d(c, c, 1)
@@ -253,13 +256,14 @@ class ConvReluNormO(nn.Module):  # text_encoder.py:17-57
     def forward(self, x, m):
         r = x
         for conv, ln in zip(self.convolutions, self.normalizations):
-            x = F.relu(ln(conv(x * m).transpose(1, 2)).transpose(1, 2))
+            x = self.drop(F.relu(ln(conv(x * m).transpose(1, 2)).transpose(1, 2)))
         return (r + self.projection(x)) * m
 
 
 class DurationPredictorO(nn.Module):  # text_encoder.py:60-96
-    def __init__(self, cin, cf, k):
+    def __init__(self, cin, cf, k, p=0.1):
         super().__init__()
+        self.drop = nn.Dropout(p)
         self.conv_layer_1 = nn.Conv1d(cin, cf, k, padding=k // 2)
         self.norm_layer_1 = nn.LayerNorm(cf)
         self.conv_layer_2 = nn.Conv1d(cf, cf, k, padding=k // 2)
@@ -267,8 +271,8 @@ class DurationPredictorO(nn.Module):  # text_encoder.py:60-96
         self.output_projection = nn.Conv1d(cf, 1, 1)
 
     def forward(self, x, m):
-        x = self.norm_layer_1(torch.relu(self.conv_layer_1(x * m)).transpose(1, 2)).transpose(1, 2)
-        x = self.norm_layer_2(torch.relu(self.conv_layer_2(x * m)).transpose(1, 2)).transpose(1, 2)
+        x = self.drop(self.norm_layer_1(torch.relu(self.conv_layer_1(x * m)).transpose(1, 2)).transpose(1, 2))
+        x = self.drop(self.norm_layer_2(torch.relu(self.conv_layer_2(x * m)).transpose(1, 2)).transpose(1, 2))
         return self.output_projection(x * m) * m
 
 
@@ -286,9 +290,10 @@ def rope(x: torch.Tensor, rot_dim: int) -> torch.Tensor:
 
 
 class MHAO(nn.Module):  # text_encoder.py:146-230
-    def __init__(self, c, heads):
+    def __init__(self, c, heads, p=0.1):
         super().__init__()
         self.heads = heads
+        self.drop = nn.Dropout(p)
         self.query_conv = nn.Conv1d(c, c, 1)
         self.key_conv = nn.Conv1d(c, c, 1)
         self.value_conv = nn.Conv1d(c, c, 1)
@@ -305,15 +310,15 @@ class MHAO(nn.Module):  # text_encoder.py:146-230
         q, k = rope(q, rd), rope(k, rd)
         s = (q @ k.transpose(-1, -2)) / math.sqrt(d)
         s = s.masked_fill(amask == 0, -1e4)
-        o = torch.softmax(s, dim=-1) @ v
+        o = self.drop(torch.softmax(s, dim=-1)) @ v
         return self.output_conv(o.transpose(2, 3).contiguous().view(B, C, T))
 
 
 class FFNO(nn.Module):  # text_encoder.py:235-253
-    def __init__(self, c, cf, k):
+    def __init__(self, c, cf, k, p=0.1):
         super().__init__()
-        self.conv_net = nn.Sequential(nn.Conv1d(c, cf, k, padding=k // 2), nn.ReLU(), nn.Identity(),
-                                      nn.Conv1d(cf, c, k, padding=k // 2), nn.Identity())
+        self.conv_net = nn.Sequential(nn.Conv1d(c, cf, k, padding=k // 2), nn.ReLU(), nn.Dropout(p),
+                                      nn.Conv1d(cf, c, k, padding=k // 2), nn.Dropout(p))
 
     def forward(self, x, m):
         return self.conv_net(x * m) * m
@@ -326,13 +331,14 @@ class EncoderO(nn.Module):  # text_encoder.py:256-322
         self.norm_layers_1 = nn.ModuleList([nn.LayerNorm(c) for _ in range(layers)])
         self.ffn_layers = nn.ModuleList([FFNO(c, cf, k) for _ in range(layers)])
         self.norm_layers_2 = nn.ModuleList([nn.LayerNorm(c) for _ in range(layers)])
+        self.drop = nn.Dropout(0.1)
 
     def forward(self, x, m):
         amask = m.unsqueeze(2) * m.unsqueeze(-1)
         for att, n1, ffn, n2 in zip(self.attention_layers, self.norm_layers_1, self.ffn_layers, self.norm_layers_2):
             x = x * m
-            x = n1((x + att(x, amask)).transpose(1, 2)).transpose(1, 2)
-            x = n2((x + ffn(x, m)).transpose(1, 2)).transpose(1, 2)
+            x = n1((x + self.drop(att(x, amask))).transpose(1, 2)).transpose(1, 2)
+            x = n2((x + self.drop(ffn(x, m))).transpose(1, 2)).transpose(1, 2)
         return x * m
 
 

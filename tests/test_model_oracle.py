@@ -29,7 +29,7 @@ def oracle_maximum_path(value: torch.Tensor, mask: torch.Tensor) -> torch.Tensor
 def build_cfm(params, n_feats, seed):
     cfm = MO.CFMOracle(2 * n_feats, n_feats, SimpleNamespace(sigma_min=1e-4), params)
     apply_recipe(cfm, seed)
-    return cfm
+    return cfm.eval()
 
 
 def rel(a, b):
@@ -65,6 +65,7 @@ def test_matcha_forward_losses_and_alignment():
     torch.set_num_threads(8)
     model = MO.MatchaTTSOracle(150, 80, 192, maximum_path=oracle_maximum_path)
     apply_recipe(model, 13)
+    model.eval()
     assert [n for n, _ in model.named_parameters()] == list(GM["m_param_names"])
     enc = sum(p.numel() for p in model.encoder.parameters())
     dec = sum(p.numel() for p in model.decoder.parameters())
