@@ -1,0 +1,131 @@
+/*
+ * mtts_decoder.h -- C ABI of the CFM decoder operators in libmtts_hip.so (gfx950).
+ *
+ * Same conventions as mtts.h (caller-owned buffers, negative mtts_status on error, thread-local
+ * mtts_last_error(), stream-ordered, no host synchronisation).  Activations are TOKEN-MAJOR:
+ * [rows = batch*time, channels], channels contiguous, fp32 in HBM.
+ *
+ * Reference operators replaced (matcha/models/components/..., relative to the reference root):
+ *   mtts_conv_gemm / mtts_conv_wgrad  <- nn.Conv1d k3/k1, stride-2 Downsample1D, ConvTranspose1d
+ *                                        Upsample1D (decoder.py:51-116, 189-251) and the Linear layers
+ *                                        of BasicTransformerBlock / FeedForward (transformer.py:105-188,
+ *                                        diffusers Attention to_q/k/v/to_out), forward and backward
+ *   mtts_gn_mish_fwd / _bwd           <- Block1D's GroupNorm(8) + Mish + mask (decoder.py:58-66) with
+ *                                        Resnet1D's time-embedding add (decoder.py:82-83) and the final
+ *                                        GroupNorm + Mish (decoder.py:366-368)
+ *   mtts_layernorm_fwd / _bwd         <- BasicTransformerBlock norm1 / norm3 (transformer.py:316, 345)
+ *   mtts_attention_fwd / _bwd         <- diffusers AttnProcessor2_0 scaled_dot_product_attention with
+ *                                        the float 0/1 mask as an additive key bias (transformer.py:320-328)
+ */
+#ifndef MTTS_DECODER_H_
+#define MTTS_DECODER_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTTS_PREC_FP32 0 /* fp32 operands, v_mfma_f32_32x32x2_f32 (parity mode)            */
+#define MTTS_PREC_BF16 1 /* bf16 operands, v_mfma_f32_32x32x16_bf16, fp32 accumulation      */
+
+#define MTTS_ACT_NONE 0
+#define MTTS_ACT_GELU 1  /* erf GELU (diffusers GELU, approximate="none") */
+#define MTTS_ACT_DGELU 2 /* multiply by GELU'(aux[row, n]) -- backward through a GELU */
+
+#define MTTS_CONV_MAX_TAPS 4
+
+/*
+ * Implicit GEMM  C[row(b,u), n] = epi( sum_{j<ntaps} sum_{c<cin} A[b*Ti + u*in_stride + off[j], c]
+ *                                                               * a_scale[...] * W[n, j*cin + c] )
+ * for b < nb, u < To; input rows outside [0, Ti) read as zero.  epi = (+ bias[n]) -> [C_pre <- value]
+ * -> act -> (+ residual[row, n]) -> (* c_scale[row]);  row(b,u) = b*To_full + u*out_stride + out_off.
+ * act MTTS_ACT_DGELU multiplies by GELU'(aux[row, n]) instead (aux/ldaux: the saved pre-activation).
+ * W is packed [N][Kp] (bf16 for MTTS_PREC_BF16, fp32 otherwise), K = ntaps*cin, Kp >= K, Kp % 8 == 0.
+ * Requirements: cin % 8 == 0, lda % 4 == 0, A and W 16-byte aligned.
+ */
+typedef struct mtts_conv_gemm_args {
+    const float *A;
+    const float *a_scale; /* [nb*Ti] or NULL */
+    int32_t lda, Ti, To, nb, in_stride, ntaps;
+    int32_t off[MTTS_CONV_MAX_TAPS];
+    int32_t cin;
+    const void *W;
+    int32_t N, K, Kp;
+    const float *bias; /* [N] or NULL */
+    int32_t act;
+    const float *residual; /* rows addressed like C, or NULL */
+    int32_t ldr;
+    const float *c_scale; /* [nb*To_full] or NULL */
+    float *C;
+    int32_t ldc, To_full, out_stride, out_off;
+    float *C_pre;      /* optional: pre-activation values (rows addressed like C, ld = ldc) */
+    const float *aux;  /* MTTS_ACT_DGELU: pre-activation input (rows addressed like C) */
+    int32_t ldaux;
+    float dropout_p;       /* > 0: inverted dropout after act (before residual)                  */
+    const uint32_t *seed;  /* device pointer to 2 words: the dropout stream (graph-replay safe)   */
+} mtts_conv_gemm_args;
+
+int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
+
+/*
+ * Weight gradient of the same implicit GEMM:
+ *   dW[n, j*cin + c] = sum_{b,u} dY[row(b,u), n] * A[b*Ti + u*in_stride + off[j], c] * a_scale[...]
+ *   db[n]            = sum_{b,u} dY[row(b,u), n]                      (when db != NULL)
+ * written (or added, accumulate != 0) to dw[n*sn + c*sc + j*sj] -- any layout of [N, cin, ntaps].
+ * Deterministic: split over rows into fp32 partial slabs in the workspace, reduced in a fixed order.
+ */
+typedef struct mtts_conv_wgrad_args {
+    const float *dY;
+    int32_t ldy, To_full, out_stride, out_off;
+    const float *A;
+    const float *a_scale;
+    int32_t lda, Ti, To, nb, in_stride, ntaps;
+    int32_t off[MTTS_CONV_MAX_TAPS];
+    int32_t cin;
+    int32_t N, K;
+} mtts_conv_wgrad_args;
+
+size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *args);
+int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precision, float *dw, int64_t sn, int64_t sc,
+                    int64_t sj, float *db, int32_t accumulate, void *workspace, size_t workspace_bytes,
+                    void *hip_stream);
+
+/*
+ * y[b,t,c] = mish(GN(h)[b,t,c]) * mask[b,t] + add[b,c]      (mask / add optional)
+ * GroupNorm statistics per (b, group) over all T rows x C/G channels (the full padded length, as the
+ * reference).  mean/rstd [B,G] are saved for the backward.  C % G == 0, (C/G) % 4 == 0.
+ */
+int mtts_gn_mish_fwd(const float *h, const float *gamma, const float *beta, const float *mask, const float *add,
+                     float *y, float *mean, float *rstd, int32_t B, int32_t T, int32_t C, int32_t G, float eps,
+                     void *hip_stream);
+size_t mtts_gn_mish_bwd_workspace_size(int32_t B, int32_t C);
+/* dh (and dgamma, dbeta [C], dadd [B,C] when non-NULL) from dy and the forward's inputs/statistics. */
+int mtts_gn_mish_bwd(const float *dy, const float *h, const float *gamma, const float *beta, const float *mask,
+                     const float *mean, const float *rstd, float *dh, float *dgamma, float *dbeta, float *dadd,
+                     int32_t B, int32_t T, int32_t C, int32_t G, void *workspace, size_t workspace_bytes,
+                     void *hip_stream);
+
+/*
+ * Counter-based dropout (train mode, nn.Dropout semantics: keep with prob 1-p, scale 1/(1-p)).
+ * keep(row, col) is a hash of (seed[0], seed[1], row, col); `seed` is a DEVICE pointer (2 words) so a
+ * captured HIP graph draws a fresh mask on every replay, and a backward pass regenerates the exact
+ * mask the forward used without storing it.  y = x * keep / (1-p) over [rows, cols], leading dim ld.
+ */
+int mtts_dropout_apply(const float *x, float *y, int32_t rows, int32_t cols, int32_t ld, float p,
+                       const uint32_t *seed, void *hip_stream);
+
+/* LayerNorm over the last dim of x [M, C]; mean/rstd [M] saved.  C % 4 == 0, C <= 1024. */
+int mtts_layernorm_fwd(const float *x, const float *w, const float *b, float *y, float *mean, float *rstd,
+                       int32_t M, int32_t C, float eps, void *hip_stream);
+size_t mtts_layernorm_bwd_workspace_size(int32_t M, int32_t C);
+int mtts_layernorm_bwd(const float *dy, const float *x, const float *w, const float *mean, const float *rstd,
+                       float *dx, float *dw, float *db, int32_t M, int32_t C, void *workspace,
+                       size_t workspace_bytes, void *hip_stream);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* MTTS_DECODER_H_ */

@@ -1,0 +1,625 @@
+// Token-major implicit GEMM for every conv / linear of the CFM decoder (gfx950 MFMA).
+//
+// Reference ops replaced: Conv1d k3/k1 (decoder.py:59,78,95,192,239,248,251), the stride-2 Downsample
+// (:95), the ConvTranspose1d(4,2,1) Upsample (:112, run as two phase GEMMs), diffusers Linear layers
+// (to_q/k/v, to_out.0, ff.net.0.proj, ff.net.2; transformer.py:155-180) and the time-MLP Linears.
+//
+// Activations are token-major [rows, C] fp32.  For output row u of batch b, tap j reads input row
+// u*in_stride + off[j] of the same batch (zero outside [0, Ti)), times the optional row scale (the
+// reference's `x * mask` before every conv).  K = ntaps * cin; every 8-element K chunk lies in one
+// tap (cin % 8 == 0).  Weights come packed [N][Kp] (K contiguous, Kp = K rounded up to 8).
+// Epilogue: + bias[n] -> erf-GELU -> + residual -> * row scale -> store to row
+// b*To_full + u*out_stride + out_off.
+//
+// Tile: BM = 64*MR rows x BN = 128 cols x BK = 32, 256 threads = 4 waves (2 x 2), each wave owns
+// (32*MR) x 64 as MR x 2 tiles of 32x32.  Operands are staged global -> registers -> LDS (the
+// gather / mask / fp32->bf16 conversion happens in that pass) with two LDS buffers and one barrier
+// per K step: the next tile's global loads are in flight while the current tile's MFMAs run.
+//   bf16 path: v_mfma_f32_32x32x16_bf16 (dense bf16 MFMA, fp32 accumulate)
+//   fp32 path: v_mfma_f32_32x32x2_f32   (exact fp32 products, the parity mode)
+//
+// wgrad (conv_wgrad_kernel): dW[n][k] = sum_rows dY[row][n] * A_gathered[row][k], the reduction over
+// tokens split across blocks into fp32 partial slabs (deterministic), reduced by wgrad_reduce_kernel
+// which also emits the bias gradient (column sums of dY, accumulated in the k-tile-0 blocks).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "mtts_common.h"
+#include "mtts_decoder.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ uint16_t to_bf16(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+
+__device__ __forceinline__ int tap_off(const mtts_conv_gemm_args &p, int j) {
+    return j == 0 ? p.off[0] : j == 1 ? p.off[1] : j == 2 ? p.off[2] : p.off[3];
+}
+__device__ __forceinline__ int tap_off(const mtts_conv_wgrad_args &p, int j) {
+    return j == 0 ? p.off[0] : j == 1 ? p.off[1] : j == 2 ? p.off[2] : p.off[3];
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+// d/dx erf-GELU, as torch's GeluBackward (cdf + x * pdf)
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+    const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+    const float pdf = expf(-0.5f * x * x) * 0.39894228040143268f;
+    return cdf + x * pdf;
+}
+
+// b = m / d, u = m % d for 0 <= m < 2^24 with a precomputed 1/d (float estimate + one correction)
+__device__ __forceinline__ void divmod_fast(int m, int d, float inv_d, int &q, int &r) {
+    q = (int)((float)m * inv_d);
+    r = m - q * d;
+    if (r < 0) { --q; r += d; } else if (r >= d) { ++q; r -= d; }
+}
+
+constexpr int kBN = 128;
+constexpr int kBK = 32;
+constexpr int kThreads = 256;
+
+struct Gather {  // per-thread precomputed row info for one staged A row
+    int in_base;  // b*Ti (input row base of this batch)
+    int in_u;     // u*in_stride
+    bool valid;
+};
+
+template <bool BF16>
+struct Stage;  // LDS element type + padding per precision
+
+template <>
+struct Stage<true> {
+    using T = uint16_t;
+    static constexpr int PAD = 8;  // 80-byte rows: conflict-free ds_read_b128 (16 distinct rows)
+};
+template <>
+struct Stage<false> {
+    using T = float;
+    static constexpr int PAD = 1;  // 33-dword rows: conflict-free ds_read_b32 column reads
+};
+
+template <bool BF16, int MR>
+__global__ __launch_bounds__(kThreads) void conv_gemm_kernel(mtts_conv_gemm_args p) {
+    constexpr int BM = 64 * MR;
+    using ST = typename Stage<BF16>::T;
+    constexpr int LDK = kBK + Stage<BF16>::PAD;
+    __shared__ ST As[2][BM * LDK];
+    __shared__ ST Bs[2][kBN * LDK];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int M = p.nb * p.To;
+    const int m0 = blockIdx.x * BM;
+    const int n0 = blockIdx.y * kBN;
+    const int nk = (p.K + kBK - 1) / kBK;
+    const float inv_to = 1.0f / (float)p.To;
+
+    // ---- per-thread staging assignment: A: MR chunks of 8, B: 2 chunks of 8 ----
+    Gather ga[MR];
+    int a_row[MR], a_kc[MR], a_j[MR], a_ch[MR];  // (tap, channel) of the chunk at the current K step
+#pragma unroll
+    for (int c = 0; c < MR; ++c) {
+        const int q = tid + kThreads * c;
+        a_row[c] = q >> 2;
+        a_kc[c] = (q & 3) * 8;
+        const int m = m0 + a_row[c];
+        ga[c].valid = m < M;
+        int b = 0, u = 0;
+        if (ga[c].valid) divmod_fast(m, p.To, inv_to, b, u);
+        ga[c].in_base = b * p.Ti;
+        ga[c].in_u = u * p.in_stride;
+        a_j[c] = a_kc[c] / p.cin;
+        a_ch[c] = a_kc[c] - a_j[c] * p.cin;
+    }
+    int b_row[2], b_kc[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const int q = tid + kThreads * c;
+        b_row[c] = q >> 2;
+        b_kc[c] = (q & 3) * 8;
+    }
+
+    float ra[MR][8];
+    float rb_f[2][8];
+    uint4 rb_h[2];
+
+    auto load_tile = [&](int k0) {
+#pragma unroll
+        for (int c = 0; c < MR; ++c) {
+            const int k = k0 + a_kc[c];
+            bool ok = ga[c].valid && k < p.K;
+            const int ch = a_ch[c];
+            int irow = 0;
+            if (ok) {
+                irow = ga[c].in_u + tap_off(p, a_j[c]);
+                ok = irow >= 0 && irow < p.Ti;
+            }
+            // advance (tap, channel) to the next K step (cin >= 8; loop runs <= 4 times for cin 8)
+            a_ch[c] += kBK;
+            while (a_ch[c] >= p.cin) { a_ch[c] -= p.cin; ++a_j[c]; }
+            if (ok) {
+                const size_t r = (size_t)(ga[c].in_base + irow);
+                const float4 *src = reinterpret_cast<const float4 *>(p.A + r * p.lda + ch);
+                const float4 v0 = src[0], v1 = src[1];
+                const float s = p.a_scale ? p.a_scale[r] : 1.0f;
+                ra[c][0] = v0.x * s; ra[c][1] = v0.y * s; ra[c][2] = v0.z * s; ra[c][3] = v0.w * s;
+                ra[c][4] = v1.x * s; ra[c][5] = v1.y * s; ra[c][6] = v1.z * s; ra[c][7] = v1.w * s;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) ra[c][i] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int n = n0 + b_row[c];
+            const int k = k0 + b_kc[c];
+            const bool ok = n < p.N && k < p.Kp;
+            if constexpr (BF16) {
+                if (ok)
+                    rb_h[c] = *reinterpret_cast<const uint4 *>(static_cast<const uint16_t *>(p.W) +
+                                                               (size_t)n * p.Kp + k);
+                else
+                    rb_h[c] = make_uint4(0, 0, 0, 0);
+            } else {
+                if (ok) {
+                    const float4 *src = reinterpret_cast<const float4 *>(static_cast<const float *>(p.W) +
+                                                                         (size_t)n * p.Kp + k);
+                    const float4 v0 = src[0], v1 = src[1];
+                    rb_f[c][0] = v0.x; rb_f[c][1] = v0.y; rb_f[c][2] = v0.z; rb_f[c][3] = v0.w;
+                    rb_f[c][4] = v1.x; rb_f[c][5] = v1.y; rb_f[c][6] = v1.z; rb_f[c][7] = v1.w;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) rb_f[c][i] = 0.f;
+                }
+            }
+        }
+    };
+
+    auto store_tile = [&](int buf) {
+#pragma unroll
+        for (int c = 0; c < MR; ++c) {
+            ST *dst = &As[buf][a_row[c] * LDK + a_kc[c]];
+            if constexpr (BF16) {
+                uint4 w;
+                w.x = (uint32_t)to_bf16(ra[c][0]) | ((uint32_t)to_bf16(ra[c][1]) << 16);
+                w.y = (uint32_t)to_bf16(ra[c][2]) | ((uint32_t)to_bf16(ra[c][3]) << 16);
+                w.z = (uint32_t)to_bf16(ra[c][4]) | ((uint32_t)to_bf16(ra[c][5]) << 16);
+                w.w = (uint32_t)to_bf16(ra[c][6]) | ((uint32_t)to_bf16(ra[c][7]) << 16);
+                *reinterpret_cast<uint4 *>(dst) = w;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) dst[i] = ra[c][i];
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            ST *dst = &Bs[buf][b_row[c] * LDK + b_kc[c]];
+            if constexpr (BF16) {
+                *reinterpret_cast<uint4 *>(dst) = rb_h[c];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) dst[i] = rb_f[c][i];
+            }
+        }
+    };
+
+    f32x16 acc[MR][2];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+    const int lr = lane & 31, lh = lane >> 5;
+    auto compute = [&](int buf) {
+        if constexpr (BF16) {
+#pragma unroll
+            for (int ks = 0; ks < kBK / 16; ++ks) {
+                bf16x8 af[MR], bfr[2];
+#pragma unroll
+                for (int i = 0; i < MR; ++i)
+                    af[i] = *reinterpret_cast<const bf16x8 *>(
+                        &As[buf][(wr * 32 * MR + i * 32 + lr) * LDK + ks * 16 + 8 * lh]);
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    bfr[j] = *reinterpret_cast<const bf16x8 *>(
+                        &Bs[buf][(wc * 64 + j * 32 + lr) * LDK + ks * 16 + 8 * lh]);
+#pragma unroll
+                for (int i = 0; i < MR; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < kBK / 2; ++ks) {
+                float af[MR], bfr[2];
+#pragma unroll
+                for (int i = 0; i < MR; ++i) af[i] = As[buf][(wr * 32 * MR + i * 32 + lr) * LDK + ks * 2 + lh];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) bfr[j] = Bs[buf][(wc * 64 + j * 32 + lr) * LDK + ks * 2 + lh];
+#pragma unroll
+                for (int i = 0; i < MR; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    };
+
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const bool more = kt + 1 < nk;
+        if (more) load_tile((kt + 1) * kBK);
+        compute(kt & 1);
+        if (more) store_tile((kt + 1) & 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue ----
+    uint32_t s0 = 0, s1 = 0;
+    if (p.dropout_p > 0.f) {
+        s0 = p.seed[0];
+        s1 = p.seed[1];
+    }
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+        int crows[16];  // output row of each accumulator register (-1: past M)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int m = m0 + wr * 32 * MR + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * lh;
+            int b, u;
+            divmod_fast(m, p.To, inv_to, b, u);
+            crows[v] = m < M ? b * p.To_full + u * p.out_stride + p.out_off : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = n0 + wc * 64 + j * 32 + lr;
+            if (n >= p.N) continue;
+            const float bn = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                if (crows[v] < 0) continue;
+                const size_t crow = (size_t)crows[v];
+                float val = acc[i][j][v] + bn;
+                if (p.C_pre) p.C_pre[crow * p.ldc + n] = val;
+                if (p.act == MTTS_ACT_GELU) val = gelu_erf(val);
+                else if (p.act == MTTS_ACT_DGELU) val *= gelu_erf_grad(p.aux[crow * p.ldaux + n]);
+                if (p.dropout_p > 0.f)
+                    val = mtts::dropout_keep(s0, s1, (uint32_t)crow, (uint32_t)n, p.dropout_p)
+                              ? val * (1.0f / (1.0f - p.dropout_p))
+                              : 0.f;
+                if (p.residual) val += p.residual[crow * p.ldr + n];
+                if (p.c_scale) val *= p.c_scale[crow];
+                p.C[crow * p.ldc + n] = val;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// wgrad: partial[s][n][k] = sum over the split's rows of dY[row][n] * A_gathered[row][k]
+// Tile 128 (n) x 128 (k), reduction dim = rows in steps of 32; LDS holds both operands transposed
+// ([col][row], 16-byte fragment reads along rows).  k-tile-0 blocks also sum dY columns (bias grad).
+template <bool BF16>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_args p, int rows_per_split,
+                                                               float *__restrict__ part, float *__restrict__ part_db) {
+    constexpr int T = 128;
+    using ST = typename Stage<BF16>::T;
+    constexpr int LDR = kBK + Stage<BF16>::PAD;  // row stride of the transposed images
+    __shared__ ST Ys[T * LDR];
+    __shared__ ST Xs[T * LDR];
+    __shared__ float dbs[16][T];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int n0 = blockIdx.x * T, k0 = blockIdx.y * T, split = blockIdx.z;
+    const int M = p.nb * p.To;
+    const int r_begin = split * rows_per_split;
+    const int r_end = min(M, r_begin + rows_per_split);
+    const bool do_db = (blockIdx.y == 0) && part_db != nullptr;
+    const float inv_to = 1.0f / (float)p.To;
+
+    // staging: 32 rows x 128 cols per operand = 512 chunks of 8 -> 2 chunks per thread per operand
+    float colsum[2][8];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) colsum[c][i] = 0.f;
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+    for (int rb = r_begin; rb < r_end; rb += kBK) {
+        float yv[2][8], xv[2][8];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int q = tid + kThreads * c;
+            const int rr = q >> 4;          // 0..31
+            const int cc = (q & 15) * 8;    // 0..120
+            const int m = rb + rr;
+            const bool mv = m < r_end;
+            int b = 0, u = 0;
+            if (mv) divmod_fast(m, p.To, inv_to, b, u);
+            // dY
+            const int n = n0 + cc;
+            if (mv && n < p.N) {
+                const size_t yrow = (size_t)b * p.To_full + (size_t)u * p.out_stride + p.out_off;
+                const float *src = p.dY + yrow * p.ldy + n;
+                if (n + 8 <= p.N) {
+                    const float4 v0 = reinterpret_cast<const float4 *>(src)[0];
+                    const float4 v1 = reinterpret_cast<const float4 *>(src)[1];
+                    yv[c][0] = v0.x; yv[c][1] = v0.y; yv[c][2] = v0.z; yv[c][3] = v0.w;
+                    yv[c][4] = v1.x; yv[c][5] = v1.y; yv[c][6] = v1.z; yv[c][7] = v1.w;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) yv[c][i] = (n + i < p.N) ? src[i] : 0.f;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) yv[c][i] = 0.f;
+            }
+            // gathered A
+            const int k = k0 + cc;
+            bool ok = mv && k < p.K;
+            int irow = 0, ch = 0;
+            if (ok) {
+                const int j = k / p.cin;
+                ch = k - j * p.cin;
+                irow = u * p.in_stride + tap_off(p, j);
+                ok = irow >= 0 && irow < p.Ti;
+            }
+            if (ok) {
+                const size_t r = (size_t)b * p.Ti + irow;
+                const float4 *src = reinterpret_cast<const float4 *>(p.A + r * p.lda + ch);
+                const float4 v0 = src[0], v1 = src[1];
+                const float s = p.a_scale ? p.a_scale[r] : 1.0f;
+                xv[c][0] = v0.x * s; xv[c][1] = v0.y * s; xv[c][2] = v0.z * s; xv[c][3] = v0.w * s;
+                xv[c][4] = v1.x * s; xv[c][5] = v1.y * s; xv[c][6] = v1.z * s; xv[c][7] = v1.w * s;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) xv[c][i] = 0.f;
+            }
+            if (do_db) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) colsum[c][i] += yv[c][i];
+            }
+        }
+        __syncthreads();  // previous step's fragment reads are done
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int q = tid + kThreads * c;
+            const int rr = q >> 4, cc = (q & 15) * 8;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if constexpr (BF16) {
+                    Ys[(cc + i) * LDR + rr] = to_bf16(yv[c][i]);
+                    Xs[(cc + i) * LDR + rr] = to_bf16(xv[c][i]);
+                } else {
+                    Ys[(cc + i) * LDR + rr] = yv[c][i];
+                    Xs[(cc + i) * LDR + rr] = xv[c][i];
+                }
+            }
+        }
+        __syncthreads();
+        if constexpr (BF16) {
+#pragma unroll
+            for (int ks = 0; ks < kBK / 16; ++ks) {
+                bf16x8 af[2], bfr[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    af[i] = *reinterpret_cast<const bf16x8 *>(&Ys[(wr * 64 + i * 32 + lr) * LDR + ks * 16 + 8 * lh]);
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    bfr[j] = *reinterpret_cast<const bf16x8 *>(&Xs[(wc * 64 + j * 32 + lr) * LDR + ks * 16 + 8 * lh]);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < kBK / 2; ++ks) {
+                float af[2], bfr[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) af[i] = Ys[(wr * 64 + i * 32 + lr) * LDR + ks * 2 + lh];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) bfr[j] = Xs[(wc * 64 + j * 32 + lr) * LDR + ks * 2 + lh];
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+
+    float *slab = part + (size_t)split * p.N * p.K;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int k = k0 + wc * 64 + j * 32 + lr;
+            if (k >= p.K) continue;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int n = n0 + wr * 64 + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * lh;
+                if (n < p.N) slab[(size_t)n * p.K + k] = acc[i][j][v];
+            }
+        }
+    if (do_db) {
+        // thread tid holds column sums of cols (tid&15)*8+i over its row groups; reduce the 16
+        // row groups in a fixed order (deterministic, no float atomics)
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dbs[tid >> 4][(tid & 15) * 8 + i] = colsum[0][i] + colsum[1][i];
+        __syncthreads();
+        for (int x = tid; x < T; x += kThreads) {
+            const int n = n0 + x;
+            float s = 0.f;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) s += dbs[g][x];
+            if (n < p.N) part_db[(size_t)split * p.N + n] = s;
+        }
+    }
+}
+
+// dW (and db) = sum over splits, written in the caller's layout: w_out[n*sn + c*sc + j*sj]
+// for k = j*cin + c.
+__global__ void wgrad_reduce_kernel(const float *__restrict__ part, const float *__restrict__ part_db, int splits,
+                                    int N, int K, int cin, int64_t sn, int64_t sc, int64_t sj,
+                                    float *__restrict__ w_out, float *__restrict__ db_out, int accumulate) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t NK = (int64_t)N * K;
+    if (idx < NK) {
+        float s = 0.f;
+        for (int i = 0; i < splits; ++i) s += part[(size_t)i * NK + idx];
+        const int n = (int)(idx / K), k = (int)(idx - (int64_t)n * K);
+        const int j = k / cin, c = k - j * cin;
+        float *dst = w_out + n * sn + c * sc + j * sj;
+        *dst = accumulate ? *dst + s : s;
+    }
+    if (db_out && idx < N) {
+        float s = 0.f;
+        for (int i = 0; i < splits; ++i) s += part_db[(size_t)i * N + idx];
+        db_out[idx] = accumulate ? db_out[idx] + s : s;
+    }
+}
+
+int check_gather(const void *A, int lda, int cin, int ntaps, int K) {
+    if (!A) return mtts::fail(MTTS_ERR_INVALID_ARG, "conv_gemm: A is null");
+    if (cin <= 0 || cin % 8 || lda % 4 || (uintptr_t)A % 16)
+        return mtts::fail(MTTS_ERR_SHAPE, "conv_gemm: cin must be a multiple of 8, lda of 4, A 16-byte aligned");
+    if (ntaps < 1 || ntaps > MTTS_CONV_MAX_TAPS) return mtts::fail(MTTS_ERR_SHAPE, "conv_gemm: 1..4 taps");
+    if (K != ntaps * cin) return mtts::fail(MTTS_ERR_SHAPE, "conv_gemm: K != ntaps*cin");
+    return MTTS_OK;
+}
+
+}  // namespace
+
+extern "C" int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream) {
+    MTTS_CHECK_ARG(args != nullptr, "conv_gemm: args is null");
+    const mtts_conv_gemm_args &p = *args;
+    int rc = check_gather(p.A, p.lda, p.cin, p.ntaps, p.K);
+    if (rc) return rc;
+    MTTS_CHECK_ARG(p.W && p.C && p.N > 0 && p.nb >= 0 && p.To >= 0, "conv_gemm: bad output/weights");
+    MTTS_CHECK_ARG(p.Kp >= p.K && p.Kp % 8 == 0, "conv_gemm: Kp must be >= K and a multiple of 8");
+    MTTS_CHECK_ARG((uintptr_t)p.W % 16 == 0, "conv_gemm: W must be 16-byte aligned");
+    MTTS_CHECK_ARG(precision == MTTS_PREC_BF16 || precision == MTTS_PREC_FP32, "conv_gemm: bad precision");
+    MTTS_CHECK_ARG(p.act >= MTTS_ACT_NONE && p.act <= MTTS_ACT_DGELU, "conv_gemm: bad act");
+    MTTS_CHECK_ARG(p.act != MTTS_ACT_DGELU || p.aux, "conv_gemm: MTTS_ACT_DGELU needs aux");
+    MTTS_CHECK_ARG(p.dropout_p <= 0.f || (p.seed && p.dropout_p < 1.f), "conv_gemm: dropout needs a seed pointer");
+    const int M = p.nb * p.To;
+    if (M == 0) return MTTS_OK;
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+    const bool bf16 = precision == MTTS_PREC_BF16;
+    const int nblk_n = (p.N + kBN - 1) / kBN;
+    // 128-row tiles when they still give >= 2 blocks per CU, else 64-row tiles
+    const bool big = ((M + 127) / 128) * nblk_n >= 512;
+    if (big) {
+        dim3 grid((M + 127) / 128, nblk_n);
+        if (bf16) hipLaunchKernelGGL((conv_gemm_kernel<true, 2>), grid, dim3(kThreads), 0, st, p);
+        else hipLaunchKernelGGL((conv_gemm_kernel<false, 2>), grid, dim3(kThreads), 0, st, p);
+    } else {
+        dim3 grid((M + 63) / 64, nblk_n);
+        if (bf16) hipLaunchKernelGGL((conv_gemm_kernel<true, 1>), grid, dim3(kThreads), 0, st, p);
+        else hipLaunchKernelGGL((conv_gemm_kernel<false, 1>), grid, dim3(kThreads), 0, st, p);
+    }
+    return mtts::check_launch("conv_gemm_kernel");
+}
+
+__global__ void dropout_apply_kernel(const float *__restrict__ x, float *__restrict__ y, int rows, int cols, int ld,
+                                     float p, const uint32_t *__restrict__ seed) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)rows * cols) return;
+    const uint32_t s0 = seed[0], s1 = seed[1];
+    const int r = (int)(idx / cols), c = (int)(idx - (int64_t)r * cols);
+    const float v = x[(size_t)r * ld + c];
+    y[(size_t)r * ld + c] = mtts::dropout_keep(s0, s1, (uint32_t)r, (uint32_t)c, p) ? v * (1.0f / (1.0f - p)) : 0.f;
+}
+
+extern "C" int mtts_dropout_apply(const float *x, float *y, int32_t rows, int32_t cols, int32_t ld, float p,
+                                  const uint32_t *seed, void *hip_stream) {
+    MTTS_CHECK_ARG(x && y && seed && rows >= 0 && cols >= 0 && ld >= cols && p >= 0.f && p < 1.f,
+                   "dropout_apply: bad args");
+    const int64_t n = (int64_t)rows * cols;
+    if (n == 0) return MTTS_OK;
+    hipLaunchKernelGGL(dropout_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(hip_stream), x, y, rows, cols, ld, p, seed);
+    return mtts::check_launch("dropout_apply_kernel");
+}
+
+static void wgrad_plan(const mtts_conv_wgrad_args &p, int *splits, int *rows_per_split) {
+    const int M = p.nb * p.To;
+    const int tiles = ((p.N + 127) / 128) * ((p.K + 127) / 128);
+    int s = (512 + tiles - 1) / tiles;
+    s = max(1, min(s, (M + 255) / 256));
+    int rps = (M + s - 1) / s;
+    rps = (rps + kBK - 1) / kBK * kBK;
+    *rows_per_split = max(rps, kBK);
+    *splits = (M + *rows_per_split - 1) / *rows_per_split;
+    if (*splits < 1) *splits = 1;
+}
+
+extern "C" size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *args) {
+    if (!args) return 0;
+    int splits, rps;
+    wgrad_plan(*args, &splits, &rps);
+    return mtts::align_up((size_t)splits * args->N * args->K * 4, 256) + (size_t)splits * args->N * 4 + 256;
+}
+
+extern "C" int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precision, float *dw, int64_t sn,
+                               int64_t sc, int64_t sj, float *db, int32_t accumulate, void *workspace,
+                               size_t workspace_bytes, void *hip_stream) {
+    MTTS_CHECK_ARG(args != nullptr, "conv_wgrad: args is null");
+    const mtts_conv_wgrad_args &p = *args;
+    int rc = check_gather(p.A, p.lda, p.cin, p.ntaps, p.K);
+    if (rc) return rc;
+    MTTS_CHECK_ARG(p.dY && dw && p.N > 0, "conv_wgrad: null dY/dw");
+    MTTS_CHECK_ARG(p.ldy % 4 == 0 && (uintptr_t)p.dY % 16 == 0, "conv_wgrad: dY rows must be 16-byte aligned");
+    MTTS_CHECK_ARG(precision == MTTS_PREC_BF16 || precision == MTTS_PREC_FP32, "conv_wgrad: bad precision");
+    if (workspace_bytes < mtts_conv_wgrad_workspace_size(args) || !workspace)
+        return mtts::fail(MTTS_ERR_WORKSPACE, "conv_wgrad: workspace too small");
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+    int splits, rps;
+    wgrad_plan(p, &splits, &rps);
+    float *part = static_cast<float *>(workspace);
+    float *part_db = reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                               mtts::align_up((size_t)splits * p.N * p.K * 4, 256));
+    const int M = p.nb * p.To;
+    if (M == 0) {
+        hipMemsetAsync(part, 0, (size_t)p.N * p.K * 4, st);
+        hipMemsetAsync(part_db, 0, (size_t)p.N * 4, st);
+        splits = 1;
+    } else {
+        dim3 grid((p.N + 127) / 128, (p.K + 127) / 128, splits);
+        if (precision == MTTS_PREC_BF16)
+            hipLaunchKernelGGL((conv_wgrad_kernel<true>), grid, dim3(kThreads), 0, st, p, rps, part,
+                               db ? part_db : nullptr);
+        else
+            hipLaunchKernelGGL((conv_wgrad_kernel<false>), grid, dim3(kThreads), 0, st, p, rps, part,
+                               db ? part_db : nullptr);
+        rc = mtts::check_launch("conv_wgrad_kernel");
+        if (rc) return rc;
+    }
+    const int64_t NK = (int64_t)p.N * p.K;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((NK + 255) / 256)), dim3(256), 0, st, part, part_db,
+                       splits, p.N, p.K, p.cin, sn, sc, sj, dw, db, accumulate);
+    return mtts::check_launch("wgrad_reduce_kernel");
+}

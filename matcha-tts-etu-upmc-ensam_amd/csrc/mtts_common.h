@@ -28,6 +28,16 @@ inline int check_launch(const char *what) {
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// Counter-based dropout keep test shared by the GEMM epilogue and mtts_dropout_apply.
+__device__ __forceinline__ bool dropout_keep(uint32_t seed_lo, uint32_t seed_hi, uint32_t row, uint32_t col,
+                                             float p) {
+    uint32_t x = row * 0x9E3779B1u ^ (col + 0x7F4A7C15u) * 0x85EBCA77u ^ seed_lo;
+    x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+    x ^= seed_hi;
+    x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+    return (float)(x >> 8) * (1.0f / 16777216.0f) >= p;
+}
+
 }  // namespace mtts
 
 #define MTTS_CHECK_ARG(cond, msg)                                   \

@@ -1,0 +1,419 @@
+// Fused normalisation kernels of the CFM decoder, token-major [B*T, C] fp32 (gfx950).
+//
+// gn_mish_*: Block1D tail  mish(GroupNorm(conv)) * mask  (decoder.py:58-66), with Resnet1D's
+//            time-embedding add (decoder.py:82-83) fused; one workgroup per (batch, group), the group's
+//            T x C/G values stay in L1/L2 across the three passes (mean, centred variance, apply).
+//            Backward recomputes xhat / mish' from h and the saved statistics; per-(b, c) partial
+//            gamma/beta sums and the time-bias gradient come out of the same pass, and the gamma/beta
+//            partials are reduced over the batch by colsum_kernel in a fixed order (deterministic).
+// layernorm_*: one wave per token row (norm1 / norm3 of BasicTransformerBlock, transformer.py:316,345).
+// Numerics follow torch: mish(x) = x * tanh(log1p(exp(x))), two-pass variance, biased, eps inside sqrt.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "mtts_common.h"
+#include "mtts_decoder.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ float mish_f(float x) { return x * tanhf(log1pf(expf(x))); }
+
+__device__ __forceinline__ float mish_grad(float x) {
+    const float sig = 1.f / (1.f + expf(-x));
+    const float tsp = tanhf(log1pf(expf(x)));
+    return tsp + x * sig * (1.f - tsp * tsp);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// block-wide sum, result broadcast to all threads (fixed reduction order)
+__device__ __forceinline__ float block_sum(float v, float *red) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < kThreads / 64; ++i) s += red[i];
+    return s;
+}
+
+// thread layout inside a group: cg/4 float4 columns, kThreads/(cg/4) token rows per pass
+__global__ __launch_bounds__(kThreads) void gn_mish_fwd_kernel(const float *__restrict__ h, const float *__restrict__ gamma,
+                                                               const float *__restrict__ beta,
+                                                               const float *__restrict__ mask,
+                                                               const float *__restrict__ add, float *__restrict__ y,
+                                                               float *__restrict__ mean_out,
+                                                               float *__restrict__ rstd_out, int T, int C, int G,
+                                                               float eps) {
+    __shared__ float red[kThreads / 64];
+    const int g = blockIdx.x, b = blockIdx.y;
+    const int cg = C / G;
+    const int cols = cg / 4;
+    const int rows_per_pass = kThreads / cols;
+    const int tid = threadIdx.x;
+    const int col = tid % cols, r0 = tid / cols;
+    const bool active = r0 < rows_per_pass;
+    const int c0 = g * cg + col * 4;
+    const float *hb = h + (size_t)b * T * C + c0;
+    const float n = (float)T * cg;
+
+    float s = 0.f;
+    if (active)
+        for (int t = r0; t < T; t += rows_per_pass) {
+            const float4 v = *reinterpret_cast<const float4 *>(hb + (size_t)t * C);
+            s += (v.x + v.y) + (v.z + v.w);
+        }
+    const float mean = block_sum(s, red) / n;
+    float q = 0.f;
+    if (active)
+        for (int t = r0; t < T; t += rows_per_pass) {
+            const float4 v = *reinterpret_cast<const float4 *>(hb + (size_t)t * C);
+            const float a = v.x - mean, bq = v.y - mean, cq = v.z - mean, d = v.w - mean;
+            q += (a * a + bq * bq) + (cq * cq + d * d);
+        }
+    const float var = block_sum(q, red) / n;
+    const float rstd = rsqrtf(var + eps);
+    if (tid == 0) {
+        mean_out[b * G + g] = mean;
+        rstd_out[b * G + g] = rstd;
+    }
+    if (!active) return;
+    const float4 ga = *reinterpret_cast<const float4 *>(gamma + c0);
+    const float4 be = *reinterpret_cast<const float4 *>(beta + c0);
+    float4 ad = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (add) ad = *reinterpret_cast<const float4 *>(add + (size_t)b * C + c0);
+    float *yb = y + (size_t)b * T * C + c0;
+    for (int t = r0; t < T; t += rows_per_pass) {
+        const float4 v = *reinterpret_cast<const float4 *>(hb + (size_t)t * C);
+        const float m = mask ? mask[(size_t)b * T + t] : 1.f;
+        float4 o;
+        o.x = mish_f((v.x - mean) * rstd * ga.x + be.x) * m + ad.x;
+        o.y = mish_f((v.y - mean) * rstd * ga.y + be.y) * m + ad.y;
+        o.z = mish_f((v.z - mean) * rstd * ga.z + be.z) * m + ad.z;
+        o.w = mish_f((v.w - mean) * rstd * ga.w + be.w) * m + ad.w;
+        *reinterpret_cast<float4 *>(yb + (size_t)t * C) = o;
+    }
+}
+
+// Backward.  Per element: u = xhat*gamma + beta, g_u = dy * mask * mish'(u), dxhat = g_u * gamma.
+// dh = rstd * (dxhat - mean(dxhat) - xhat * mean(dxhat * xhat)) over the (b, g) group.
+// Partial outputs per (b, c): pg[b,c] = sum_t g_u*xhat, pb[b,c] = sum_t g_u, dadd[b,c] = sum_t dy.
+__global__ __launch_bounds__(kThreads) void gn_mish_bwd_kernel(
+    const float *__restrict__ dy, const float *__restrict__ h, const float *__restrict__ gamma,
+    const float *__restrict__ beta, const float *__restrict__ mask, const float *__restrict__ mean_in,
+    const float *__restrict__ rstd_in, float *__restrict__ dh, float *__restrict__ pg, float *__restrict__ pb,
+    float *__restrict__ dadd, int T, int C, int G) {
+    __shared__ float red[kThreads / 64];
+    __shared__ float4 chred[3][kThreads];
+    const int g = blockIdx.x, b = blockIdx.y;
+    const int cg = C / G;
+    const int cols = cg / 4;
+    const int rows_per_pass = kThreads / cols;
+    const int tid = threadIdx.x;
+    const int col = tid % cols, r0 = tid / cols;
+    const bool active = r0 < rows_per_pass;
+    const int c0 = g * cg + col * 4;
+    const float mean = mean_in[b * G + g], rstd = rstd_in[b * G + g];
+    const float4 ga = *reinterpret_cast<const float4 *>(gamma + c0);
+    const float4 be = *reinterpret_cast<const float4 *>(beta + c0);
+    const float *hb = h + (size_t)b * T * C + c0;
+    const float *db_ = dy + (size_t)b * T * C + c0;
+    const float n = (float)T * cg;
+
+    float s1 = 0.f, s2 = 0.f;
+    float4 ag = make_float4(0, 0, 0, 0), ab = make_float4(0, 0, 0, 0), ad = make_float4(0, 0, 0, 0);
+    if (active)
+        for (int t = r0; t < T; t += rows_per_pass) {
+            const float4 v = *reinterpret_cast<const float4 *>(hb + (size_t)t * C);
+            const float4 d = *reinterpret_cast<const float4 *>(db_ + (size_t)t * C);
+            const float m = mask ? mask[(size_t)b * T + t] : 1.f;
+            float xh, gu;
+#define MTTS_GN_BWD_ACC(X, D, GA, BE, AG, AB, AD)          \
+    xh = (X - mean) * rstd;                                 \
+    gu = D * m * mish_grad(xh * GA + BE);                   \
+    s1 += gu * GA;                                          \
+    s2 += gu * GA * xh;                                     \
+    AG += gu * xh;                                          \
+    AB += gu;                                               \
+    AD += D;
+            MTTS_GN_BWD_ACC(v.x, d.x, ga.x, be.x, ag.x, ab.x, ad.x)
+            MTTS_GN_BWD_ACC(v.y, d.y, ga.y, be.y, ag.y, ab.y, ad.y)
+            MTTS_GN_BWD_ACC(v.z, d.z, ga.z, be.z, ag.z, ab.z, ad.z)
+            MTTS_GN_BWD_ACC(v.w, d.w, ga.w, be.w, ag.w, ab.w, ad.w)
+#undef MTTS_GN_BWD_ACC
+        }
+    const float m1 = block_sum(s1, red) / n;
+    const float m2 = block_sum(s2, red) / n;
+    // per-channel partials: reduce the rows_per_pass threads that share a column, fixed order
+    chred[0][tid] = ag;
+    chred[1][tid] = ab;
+    chred[2][tid] = ad;
+    __syncthreads();
+    if (tid < cols) {
+        float4 sg = make_float4(0, 0, 0, 0), sb = sg, sd = sg;
+        for (int r = 0; r < rows_per_pass; ++r) {
+            const float4 a = chred[0][r * cols + tid], bb = chred[1][r * cols + tid], dd = chred[2][r * cols + tid];
+            sg.x += a.x; sg.y += a.y; sg.z += a.z; sg.w += a.w;
+            sb.x += bb.x; sb.y += bb.y; sb.z += bb.z; sb.w += bb.w;
+            sd.x += dd.x; sd.y += dd.y; sd.z += dd.z; sd.w += dd.w;
+        }
+        const int cc = g * cg + tid * 4;
+        *reinterpret_cast<float4 *>(pg + (size_t)b * C + cc) = sg;
+        *reinterpret_cast<float4 *>(pb + (size_t)b * C + cc) = sb;
+        if (dadd) *reinterpret_cast<float4 *>(dadd + (size_t)b * C + cc) = sd;
+    }
+    if (!active) return;
+    float *dhb = dh + (size_t)b * T * C + c0;
+    for (int t = r0; t < T; t += rows_per_pass) {
+        const float4 v = *reinterpret_cast<const float4 *>(hb + (size_t)t * C);
+        const float4 d = *reinterpret_cast<const float4 *>(db_ + (size_t)t * C);
+        const float m = mask ? mask[(size_t)b * T + t] : 1.f;
+        float4 o;
+        float xh, gu;
+#define MTTS_GN_BWD_OUT(X, D, GA, BE, O)                     \
+    xh = (X - mean) * rstd;                                   \
+    gu = D * m * mish_grad(xh * GA + BE);                     \
+    O = rstd * (gu * GA - m1 - xh * m2);
+        MTTS_GN_BWD_OUT(v.x, d.x, ga.x, be.x, o.x)
+        MTTS_GN_BWD_OUT(v.y, d.y, ga.y, be.y, o.y)
+        MTTS_GN_BWD_OUT(v.z, d.z, ga.z, be.z, o.z)
+        MTTS_GN_BWD_OUT(v.w, d.w, ga.w, be.w, o.w)
+#undef MTTS_GN_BWD_OUT
+        *reinterpret_cast<float4 *>(dhb + (size_t)t * C) = o;
+    }
+}
+
+// out[c] = sum_r in[r*C + c] for the gamma/beta partials.  Block = 64 columns x 4 row-slices; each
+// slice sums a contiguous quarter of the rows, the 4 slice sums are added in a fixed order.
+__global__ __launch_bounds__(256) void colsum_kernel(const float *__restrict__ in, int R, int C,
+                                                     float *__restrict__ out) {
+    __shared__ float part[4][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int sl = threadIdx.x >> 6;
+    const int per = (R + 3) / 4;
+    const int r0 = sl * per, r1 = min(R, r0 + per);
+    float s = 0.f;
+    if (c < C)
+        for (int r = r0; r < r1; ++r) s += in[(size_t)r * C + c];
+    part[sl][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (sl == 0 && c < C) out[c] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+}
+
+// ------------------------------------------------------------------------------ LayerNorm
+// one wave per row; lane handles float4 chunks lane*4 + 256*i
+__global__ __launch_bounds__(kThreads) void layernorm_fwd_kernel(const float *__restrict__ x, const float *__restrict__ w,
+                                                                 const float *__restrict__ bia, float *__restrict__ y,
+                                                                 float *__restrict__ mean_out, float *__restrict__ rstd_out,
+                                                                 int M, int C, float eps) {
+    const int row = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= M) return;
+    const float *xr = x + (size_t)row * C;
+    float4 v[4];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = lane * 4 + 256 * i;
+        v[i] = c < C ? *reinterpret_cast<const float4 *>(xr + c) : make_float4(0, 0, 0, 0);
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = lane * 4 + 256 * i;
+        if (c < C) {
+            const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, d = v[i].w - mean;
+            q += (a * a + b * b) + (cc * cc + d * d);
+        }
+    }
+    const float rstd = rsqrtf(wave_sum(q) / C + eps);
+    if (lane == 0) {
+        mean_out[row] = mean;
+        rstd_out[row] = rstd;
+    }
+    float *yr = y + (size_t)row * C;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = lane * 4 + 256 * i;
+        if (c < C) {
+            const float4 ww = *reinterpret_cast<const float4 *>(w + c);
+            const float4 bb = *reinterpret_cast<const float4 *>(bia + c);
+            float4 o;
+            o.x = (v[i].x - mean) * rstd * ww.x + bb.x;
+            o.y = (v[i].y - mean) * rstd * ww.y + bb.y;
+            o.z = (v[i].z - mean) * rstd * ww.z + bb.z;
+            o.w = (v[i].w - mean) * rstd * ww.w + bb.w;
+            *reinterpret_cast<float4 *>(yr + c) = o;
+        }
+    }
+}
+
+constexpr int kLnRowsPerBlock = 128;  // backward: rows per block (32 per wave)
+
+__global__ __launch_bounds__(kThreads) void layernorm_bwd_kernel(const float *__restrict__ dy, const float *__restrict__ x,
+                                                                 const float *__restrict__ w,
+                                                                 const float *__restrict__ mean_in,
+                                                                 const float *__restrict__ rstd_in, float *__restrict__ dx,
+                                                                 float *__restrict__ pw, float *__restrict__ pb, int M,
+                                                                 int C) {
+    __shared__ float4 red[2][kThreads / 64][256];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float4 aw[4], ab[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aw[i] = ab[i] = make_float4(0, 0, 0, 0);
+    float4 ww[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = lane * 4 + 256 * i;
+        ww[i] = c < C ? *reinterpret_cast<const float4 *>(w + c) : make_float4(0, 0, 0, 0);
+    }
+    const int rbeg = blockIdx.x * kLnRowsPerBlock;
+    for (int rr = wv; rr < kLnRowsPerBlock; rr += kThreads / 64) {
+        const int row = rbeg + rr;
+        if (row >= M) break;
+        const float mean = mean_in[row], rstd = rstd_in[row];
+        float4 xh[4], g[4];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = lane * 4 + 256 * i;
+            if (c < C) {
+                const float4 xv = *reinterpret_cast<const float4 *>(x + (size_t)row * C + c);
+                const float4 dv = *reinterpret_cast<const float4 *>(dy + (size_t)row * C + c);
+                xh[i] = make_float4((xv.x - mean) * rstd, (xv.y - mean) * rstd, (xv.z - mean) * rstd,
+                                    (xv.w - mean) * rstd);
+                g[i] = make_float4(dv.x * ww[i].x, dv.y * ww[i].y, dv.z * ww[i].z, dv.w * ww[i].w);
+                s1 += (g[i].x + g[i].y) + (g[i].z + g[i].w);
+                s2 += (g[i].x * xh[i].x + g[i].y * xh[i].y) + (g[i].z * xh[i].z + g[i].w * xh[i].w);
+                aw[i].x += dv.x * xh[i].x; aw[i].y += dv.y * xh[i].y; aw[i].z += dv.z * xh[i].z; aw[i].w += dv.w * xh[i].w;
+                ab[i].x += dv.x; ab[i].y += dv.y; ab[i].z += dv.z; ab[i].w += dv.w;
+            }
+        }
+        const float m1 = wave_sum(s1) / C, m2 = wave_sum(s2) / C;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = lane * 4 + 256 * i;
+            if (c < C) {
+                float4 o;
+                o.x = rstd * (g[i].x - m1 - xh[i].x * m2);
+                o.y = rstd * (g[i].y - m1 - xh[i].y * m2);
+                o.z = rstd * (g[i].z - m1 - xh[i].z * m2);
+                o.w = rstd * (g[i].w - m1 - xh[i].w * m2);
+                *reinterpret_cast<float4 *>(dx + (size_t)row * C + c) = o;
+            }
+        }
+    }
+    // reduce the 4 waves' partials (fixed order) -> one [C] partial per block
+    for (int i = 0; i < 4; ++i) {
+        const int c4 = lane + 64 * i;  // float4 index
+        if (c4 * 4 < C) {
+            red[0][wv][c4] = aw[i];
+            red[1][wv][c4] = ab[i];
+        }
+    }
+    __syncthreads();
+    for (int c4 = threadIdx.x; c4 * 4 < C; c4 += kThreads) {
+        float4 sw = make_float4(0, 0, 0, 0), sb = sw;
+        for (int q = 0; q < kThreads / 64; ++q) {
+            const float4 a = red[0][q][c4], bb = red[1][q][c4];
+            sw.x += a.x; sw.y += a.y; sw.z += a.z; sw.w += a.w;
+            sb.x += bb.x; sb.y += bb.y; sb.z += bb.z; sb.w += bb.w;
+        }
+        *reinterpret_cast<float4 *>(pw + (size_t)blockIdx.x * C + c4 * 4) = sw;
+        *reinterpret_cast<float4 *>(pb + (size_t)blockIdx.x * C + c4 * 4) = sb;
+    }
+}
+
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int mtts_gn_mish_fwd(const float *h, const float *gamma, const float *beta, const float *mask,
+                                const float *add, float *y, float *mean, float *rstd, int32_t B, int32_t T,
+                                int32_t C, int32_t G, float eps, void *hip_stream) {
+    MTTS_CHECK_ARG(h && gamma && beta && y && mean && rstd, "gn_mish_fwd: null pointer");
+    MTTS_CHECK_ARG(B >= 0 && T >= 1 && G >= 1 && C % G == 0 && (C / G) % 4 == 0 && C / G <= 4 * kThreads,
+                   "gn_mish_fwd: need C % G == 0 and (C/G) % 4 == 0");
+    MTTS_CHECK_ARG(aligned16(h) && aligned16(y) && aligned16(gamma) && aligned16(beta) && (!add || aligned16(add)),
+                   "gn_mish_fwd: tensors must be 16-byte aligned");
+    if (B == 0) return MTTS_OK;
+    hipLaunchKernelGGL(gn_mish_fwd_kernel, dim3(G, B), dim3(kThreads), 0, static_cast<hipStream_t>(hip_stream), h,
+                       gamma, beta, mask, add, y, mean, rstd, T, C, G, eps);
+    return mtts::check_launch("gn_mish_fwd_kernel");
+}
+
+extern "C" size_t mtts_gn_mish_bwd_workspace_size(int32_t B, int32_t C) {
+    return (size_t)2 * (B > 0 ? B : 0) * (C > 0 ? C : 0) * sizeof(float);
+}
+
+extern "C" int mtts_gn_mish_bwd(const float *dy, const float *h, const float *gamma, const float *beta,
+                                const float *mask, const float *mean, const float *rstd, float *dh, float *dgamma,
+                                float *dbeta, float *dadd, int32_t B, int32_t T, int32_t C, int32_t G,
+                                void *workspace, size_t workspace_bytes, void *hip_stream) {
+    MTTS_CHECK_ARG(dy && h && gamma && beta && mean && rstd && dh, "gn_mish_bwd: null pointer");
+    MTTS_CHECK_ARG(B >= 0 && T >= 1 && G >= 1 && C % G == 0 && (C / G) % 4 == 0, "gn_mish_bwd: bad shape");
+    MTTS_CHECK_ARG(aligned16(dy) && aligned16(h) && aligned16(dh) && (!dadd || aligned16(dadd)),
+                   "gn_mish_bwd: tensors must be 16-byte aligned");
+    if (B == 0) return MTTS_OK;
+    if (!workspace || workspace_bytes < mtts_gn_mish_bwd_workspace_size(B, C))
+        return mtts::fail(MTTS_ERR_WORKSPACE, "gn_mish_bwd: workspace too small");
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+    float *pg = static_cast<float *>(workspace);
+    float *pb = pg + (size_t)B * C;
+    hipLaunchKernelGGL(gn_mish_bwd_kernel, dim3(G, B), dim3(kThreads), 0, st, dy, h, gamma, beta, mask, mean, rstd,
+                       dh, pg, pb, dadd, T, C, G);
+    int rc = mtts::check_launch("gn_mish_bwd_kernel");
+    if (rc) return rc;
+    if (dgamma) hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pg, B, C, dgamma);
+    if (dbeta) hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pb, B, C, dbeta);
+    return mtts::check_launch("colsum_kernel");
+}
+
+extern "C" int mtts_layernorm_fwd(const float *x, const float *w, const float *b, float *y, float *mean,
+                                  float *rstd, int32_t M, int32_t C, float eps, void *hip_stream) {
+    MTTS_CHECK_ARG(x && w && b && y && mean && rstd, "layernorm_fwd: null pointer");
+    MTTS_CHECK_ARG(M >= 0 && C >= 4 && C % 4 == 0 && C <= 1024, "layernorm_fwd: need C % 4 == 0, C <= 1024");
+    MTTS_CHECK_ARG(aligned16(x) && aligned16(y) && aligned16(w) && aligned16(b), "layernorm_fwd: 16-byte alignment");
+    if (M == 0) return MTTS_OK;
+    const int rows_per_block = kThreads / 64;
+    hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((M + rows_per_block - 1) / rows_per_block), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(hip_stream), x, w, b, y, mean, rstd, M, C, eps);
+    return mtts::check_launch("layernorm_fwd_kernel");
+}
+
+extern "C" size_t mtts_layernorm_bwd_workspace_size(int32_t M, int32_t C) {
+    if (M <= 0 || C <= 0) return 0;
+    return (size_t)2 * ((M + kLnRowsPerBlock - 1) / kLnRowsPerBlock) * C * sizeof(float);
+}
+
+extern "C" int mtts_layernorm_bwd(const float *dy, const float *x, const float *w, const float *mean,
+                                  const float *rstd, float *dx, float *dw, float *db, int32_t M, int32_t C,
+                                  void *workspace, size_t workspace_bytes, void *hip_stream) {
+    MTTS_CHECK_ARG(dy && x && w && mean && rstd && dx, "layernorm_bwd: null pointer");
+    MTTS_CHECK_ARG(M >= 0 && C >= 4 && C % 4 == 0 && C <= 1024, "layernorm_bwd: need C % 4 == 0, C <= 1024");
+    MTTS_CHECK_ARG(aligned16(dy) && aligned16(x) && aligned16(dx) && aligned16(w), "layernorm_bwd: 16-byte alignment");
+    if (M == 0) return MTTS_OK;
+    if (!workspace || workspace_bytes < mtts_layernorm_bwd_workspace_size(M, C))
+        return mtts::fail(MTTS_ERR_WORKSPACE, "layernorm_bwd: workspace too small");
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+    const int nblk = (M + kLnRowsPerBlock - 1) / kLnRowsPerBlock;
+    float *pw = static_cast<float *>(workspace);
+    float *pb = pw + (size_t)nblk * C;
+    hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(nblk), dim3(kThreads), 0, st, dy, x, w, mean, rstd, dx, pw, pb, M, C);
+    int rc = mtts::check_launch("layernorm_bwd_kernel");
+    if (rc) return rc;
+    if (dw) hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pw, nblk, C, dw);
+    if (db) hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pb, nblk, C, db);
+    return mtts::check_launch("colsum_kernel");
+}

@@ -5,65 +5,473 @@ transformer block (decoder.py:298-306, 324-332, 345-353).  Here activations stay
 whole U-Net: a k-tap Conv1d is an implicit GEMM over K = k*C_in with rows = tokens, the transformer
 GEMMs need no transposes, and the reference's rearranges disappear.
 
-Each operator below is the unit a HIP kernel replaces (csrc/decoder_*.hip via include/mtts_decoder.h);
-`KERNELS` records which operators currently run in libmtts_hip.so.  Operators not yet moved run as
-PyTorch-ROCm device ops; none of them runs on the host.
+Every operator is a torch.autograd.Function whose forward AND backward run in libmtts_hip.so
+(include/mtts_decoder.h); there is no fallback -- without the library (or on CPU tensors) they raise.
+  conv_tm / conv_transpose_tm / linear_tm / ff_tm  -> mtts_conv_gemm + mtts_conv_wgrad
+      (stride-2 conv dgrad and the ConvTranspose1d forward run as two "phase" GEMMs; the transposed
+       conv's dgrad is a stride-2 conv)
+  group_norm_mish_tm                               -> mtts_gn_mish_fwd / _bwd
+  layer_norm_tm                                    -> mtts_layernorm_fwd / _bwd
+  attention_tm                                     -> PyTorch-ROCm SDPA (KERNELS records it; next HIP target)
+GEMM precision follows the caller: inside a bf16 torch.autocast region the GEMMs use bf16 MFMA with
+fp32 accumulation, otherwise exact-fp32 MFMA (the parity mode).  Activations stay fp32 in HBM.
+Dropout (train mode) is a counter-based mask generated in the GEMM epilogues and regenerated in the
+backward, so no mask tensor is stored.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch
 import torch.nn.functional as F
 
-KERNELS: dict[str, str] = {}
+from matcha import _native as N
+
+PREC_FP32, PREC_BF16 = 0, 1
+ACT_NONE, ACT_GELU, ACT_DGELU = 0, 1, 2
+
+KERNELS: dict[str, str] = {
+    "conv_tm": "mtts_conv_gemm/mtts_conv_wgrad",
+    "conv_transpose_tm": "mtts_conv_gemm/mtts_conv_wgrad",
+    "linear_tm": "mtts_conv_gemm/mtts_conv_wgrad",
+    "ff_tm": "mtts_conv_gemm/mtts_conv_wgrad",
+    "group_norm_mish_tm": "mtts_gn_mish_fwd/mtts_gn_mish_bwd",
+    "layer_norm_tm": "mtts_layernorm_fwd/mtts_layernorm_bwd",
+    "attention_tm": "torch SDPA (PyTorch-ROCm)",
+}
 
 
-def _cm(x: torch.Tensor) -> torch.Tensor:  # token-major -> channel-major view
-    return x.transpose(1, 2)
+class ConvGemmArgs(ctypes.Structure):
+    _fields_ = [("A", ctypes.c_void_p), ("a_scale", ctypes.c_void_p), ("lda", ctypes.c_int32),
+                ("Ti", ctypes.c_int32), ("To", ctypes.c_int32), ("nb", ctypes.c_int32),
+                ("in_stride", ctypes.c_int32), ("ntaps", ctypes.c_int32), ("off", ctypes.c_int32 * 4),
+                ("cin", ctypes.c_int32), ("W", ctypes.c_void_p), ("N", ctypes.c_int32), ("K", ctypes.c_int32),
+                ("Kp", ctypes.c_int32), ("bias", ctypes.c_void_p), ("act", ctypes.c_int32),
+                ("residual", ctypes.c_void_p), ("ldr", ctypes.c_int32), ("c_scale", ctypes.c_void_p),
+                ("C", ctypes.c_void_p), ("ldc", ctypes.c_int32), ("To_full", ctypes.c_int32),
+                ("out_stride", ctypes.c_int32), ("out_off", ctypes.c_int32), ("C_pre", ctypes.c_void_p),
+                ("aux", ctypes.c_void_p), ("ldaux", ctypes.c_int32), ("dropout_p", ctypes.c_float),
+                ("seed", ctypes.c_void_p)]
 
 
-def conv_tm(x, weight, bias, mask=None, stride: int = 1, padding: int | None = None):
-    """y = Conv1d(x * mask) in token-major layout.  x [B,T,Cin], weight [Cout,Cin,k] (nn.Conv1d
-    layout), mask [B,T] or None.  decoder.py:59,65,78,85,95,192,239,248,251."""
-    k = weight.shape[-1]
+class ConvWgradArgs(ctypes.Structure):
+    _fields_ = [("dY", ctypes.c_void_p), ("ldy", ctypes.c_int32), ("To_full", ctypes.c_int32),
+                ("out_stride", ctypes.c_int32), ("out_off", ctypes.c_int32), ("A", ctypes.c_void_p),
+                ("a_scale", ctypes.c_void_p), ("lda", ctypes.c_int32), ("Ti", ctypes.c_int32),
+                ("To", ctypes.c_int32), ("nb", ctypes.c_int32), ("in_stride", ctypes.c_int32),
+                ("ntaps", ctypes.c_int32), ("off", ctypes.c_int32 * 4), ("cin", ctypes.c_int32),
+                ("N", ctypes.c_int32), ("K", ctypes.c_int32)]
+
+
+_P, _I, _F, _SZ, _U = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint32
+_I64 = ctypes.c_int64
+N.register("mtts_conv_gemm", ctypes.c_int, [ctypes.POINTER(ConvGemmArgs), _I, _P])
+N.register("mtts_conv_wgrad_workspace_size", _SZ, [ctypes.POINTER(ConvWgradArgs)])
+N.register("mtts_conv_wgrad", ctypes.c_int,
+           [ctypes.POINTER(ConvWgradArgs), _I, _P, _I64, _I64, _I64, _P, _I, _P, _SZ, _P])
+N.register("mtts_gn_mish_fwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
+N.register("mtts_gn_mish_bwd_workspace_size", _SZ, [_I, _I])
+N.register("mtts_gn_mish_bwd", ctypes.c_int,
+           [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _SZ, _P])
+N.register("mtts_layernorm_fwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
+N.register("mtts_layernorm_bwd_workspace_size", _SZ, [_I, _I])
+N.register("mtts_layernorm_bwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P])
+N.register("mtts_dropout_apply", ctypes.c_int, [_P, _P, _I, _I, _I, _F, _P, _P])
+
+
+# ------------------------------------------------------------------------------------------ helpers
+def gemm_precision() -> int:
+    """bf16 MFMA inside a bf16 autocast region, exact-fp32 MFMA otherwise."""
+    if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+        return PREC_BF16
+    return PREC_FP32
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _f32c(t: torch.Tensor | None) -> torch.Tensor | None:
+    if t is None:
+        return None
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+def _new_seed(device) -> torch.Tensor:
+    """Two random words drawn ON THE DEVICE from torch's generator: no host sync, and a captured
+    HIP graph draws fresh dropout masks on every replay (torch's graph-safe philox offsets)."""
+    return torch.randint(0, 2 ** 31 - 1, (2,), device=device, dtype=torch.int32)
+
+
+def pack_weight(w2d: torch.Tensor, prec: int) -> tuple[torch.Tensor, int]:
+    """[N, K] -> contiguous [N, Kp] (Kp = K rounded up to 8) in the GEMM's operand precision."""
+    N_, K = w2d.shape
+    Kp = (K + 7) // 8 * 8
+    w = w2d.detach().to(torch.bfloat16 if prec == PREC_BF16 else torch.float32)
+    if Kp != K:
+        w = F.pad(w, (0, Kp - K))
+    return w.contiguous(), Kp
+
+
+def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_stride=1, out_off=0, *, prec,
+          a_scale=None, bias=None, act=ACT_NONE, residual=None, c_scale=None, C_pre=None, aux=None,
+          dropout_p=0.0, seed=None):
+    args = ConvGemmArgs()
+    args.A, args.a_scale, args.lda, args.Ti, args.To, args.nb = A.data_ptr(), N.ptr(a_scale), A.shape[-1], Ti, To, nb
+    args.in_stride, args.ntaps, args.cin = in_stride, len(offs), cin
+    for i, o in enumerate(offs):
+        args.off[i] = o
+    args.W, args.N, args.K, args.Kp = Wp.data_ptr(), N_, len(offs) * cin, Kp
+    args.bias, args.act = N.ptr(bias), act
+    args.residual, args.ldr = N.ptr(residual), (residual.shape[-1] if residual is not None else 0)
+    args.c_scale = N.ptr(c_scale)
+    args.C, args.ldc, args.To_full, args.out_stride, args.out_off = C.data_ptr(), C.shape[-1], To_full, out_stride, out_off
+    args.C_pre = N.ptr(C_pre)
+    args.aux, args.ldaux = N.ptr(aux), (aux.shape[-1] if aux is not None else 0)
+    args.dropout_p, args.seed = float(dropout_p), N.ptr(seed)
+    N.check(N.lib().mtts_conv_gemm(ctypes.byref(args), prec, _stream(C)), "mtts_conv_gemm")
+
+
+def _wgrad(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin, N_, dw, strides, *, prec,
+           a_scale=None, db=None):
+    args = ConvWgradArgs()
+    args.dY, args.ldy, args.To_full, args.out_stride, args.out_off = dY.data_ptr(), dY.shape[-1], To_full, out_stride, out_off
+    args.A, args.a_scale, args.lda, args.Ti, args.To, args.nb = A.data_ptr(), N.ptr(a_scale), A.shape[-1], Ti, To, nb
+    args.in_stride, args.ntaps, args.cin = in_stride, len(offs), cin
+    for i, o in enumerate(offs):
+        args.off[i] = o
+    args.N, args.K = N_, len(offs) * cin
+    lib = N.lib()
+    ws = torch.empty(int(lib.mtts_conv_wgrad_workspace_size(ctypes.byref(args))), dtype=torch.uint8, device=dY.device)
+    rc = lib.mtts_conv_wgrad(ctypes.byref(args), prec, dw.data_ptr(), strides[0], strides[1], strides[2],
+                             N.ptr(db), 0, ws.data_ptr(), ws.numel(), _stream(dY))
+    N.check(rc, "mtts_conv_wgrad")
+
+
+def _check(*ts):
+    N.require_device(*[t for t in ts if t is not None])
+
+
+# ------------------------------------------------------------------------------------------ conv
+class _ConvTM(torch.autograd.Function):
+    """y[b,u] = bias + sum_j W_j (x*m)[b, u*stride + j - pad]   (nn.Conv1d on x*mask, token-major)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, mask, out_scale, stride, padding):
+        _check(x, weight, mask)
+        prec = gemm_precision()
+        x = _f32c(x)
+        B, Ti, Cin = x.shape
+        Cout, _, k = weight.shape
+        To = (Ti + 2 * padding - k) // stride + 1
+        Wp, Kp = pack_weight(weight.permute(0, 2, 1).reshape(Cout, k * Cin), prec)
+        y = torch.empty(B, To, Cout, device=x.device, dtype=torch.float32)
+        mask = _f32c(mask)
+        out_scale = _f32c(out_scale)
+        bias_c = _f32c(bias)
+        _gemm(x, Ti, To, B, stride, [j - padding for j in range(k)], Cin, Wp, Kp, Cout, y, To, prec=prec,
+              a_scale=mask, bias=bias_c, c_scale=out_scale)
+        ctx.save_for_backward(x, weight, mask, out_scale)
+        ctx.cfg = (stride, padding, prec, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, mask, out_scale = ctx.saved_tensors
+        stride, pad, prec, has_bias = ctx.cfg
+        dy = _f32c(dy)
+        if out_scale is not None:
+            dy = dy * out_scale.unsqueeze(-1)
+        B, Ti, Cin = x.shape
+        Cout, _, k = weight.shape
+        To = dy.shape[1]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            if stride == 1:
+                Wd, Kp = pack_weight(weight.permute(1, 2, 0).reshape(Cin, k * Cout), prec)
+                _gemm(dy, To, Ti, B, 1, [pad - j for j in range(k)], Cout, Wd, Kp, Cin, dx, Ti, prec=prec,
+                      c_scale=mask)
+            else:  # stride-2 dgrad = transposed conv = one GEMM per output phase
+                for ph in range(stride):
+                    j0 = (ph + pad) % stride  # taps of this phase: j0, j0+stride, ... (a slice: no
+                    js = list(range(j0, k, stride))  # host->device index copy, legal in graph capture)
+                    nrows = (Ti - ph + stride - 1) // stride
+                    if not js or nrows <= 0:
+                        dx[:, ph::stride].zero_()
+                        continue
+                    Wd, Kp = pack_weight(weight[:, :, j0::stride].permute(1, 2, 0).reshape(Cin, len(js) * Cout), prec)
+                    _gemm(dy, To, nrows, B, 1, [(ph + pad - j) // stride for j in js], Cout, Wd, Kp, Cin, dx, Ti,
+                          stride, ph, prec=prec, c_scale=mask)
+        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
+            dw = torch.empty(weight.shape, device=x.device, dtype=torch.float32)
+            db = torch.empty(Cout, device=x.device, dtype=torch.float32) if has_bias else None
+            _wgrad(dy, To, 1, 0, x, Ti, To, B, stride, [j - pad for j in range(k)], Cin, Cout, dw,
+                   (Cin * k, k, 1), prec=prec, a_scale=mask, db=db)
+        return dx, dw, db, None, None, None, None
+
+
+class _ConvTransposeTM(torch.autograd.Function):
+    """ConvTranspose1d(k, stride 2, padding p) of x*mask (Upsample1D, decoder.py:112): two phase GEMMs."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, mask):
+        _check(x, weight, mask)
+        prec = gemm_precision()
+        x = _f32c(x)
+        mask = _f32c(mask)
+        B, T, Cin = x.shape
+        _, Cout, k = weight.shape
+        pad, s = 1, 2
+        To_full = (T - 1) * s - 2 * pad + k
+        y = torch.empty(B, To_full, Cout, device=x.device, dtype=torch.float32)
+        bias_c = _f32c(bias)
+        for ph in range(s):
+            j0 = (ph + pad) % s  # taps of this phase: j0, j0+s, ... (slice, not a host index list)
+            js = list(range(j0, k, s))
+            nrows = (To_full - ph + s - 1) // s
+            Wp, Kp = pack_weight(weight[:, :, j0::s].permute(1, 2, 0).reshape(Cout, len(js) * Cin), prec)
+            _gemm(x, T, nrows, B, 1, [(ph + pad - j) // s for j in js], Cin, Wp, Kp, Cout, y, To_full, s, ph,
+                  prec=prec, a_scale=mask, bias=bias_c)
+        ctx.save_for_backward(x, weight, mask)
+        ctx.cfg = (prec, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, mask = ctx.saved_tensors
+        prec, has_bias = ctx.cfg
+        dy = _f32c(dy)
+        B, T, Cin = x.shape
+        _, Cout, k = weight.shape
+        pad, s = 1, 2
+        T2 = dy.shape[1]
+        dx = dw = db = None
+        offs = [j - pad for j in range(k)]
+        if ctx.needs_input_grad[0]:  # dgrad of a transposed conv = stride-2 conv over dy
+            dx = torch.empty_like(x)
+            Wd, Kp = pack_weight(weight.permute(0, 2, 1).reshape(Cin, k * Cout), prec)
+            _gemm(dy, T2, T, B, s, offs, Cout, Wd, Kp, Cin, dx, T, prec=prec, c_scale=mask)
+        if ctx.needs_input_grad[1]:
+            xm = x * mask.unsqueeze(-1) if mask is not None else x
+            dw = torch.empty(weight.shape, device=x.device, dtype=torch.float32)
+            # dW[c, n, j] = sum_s xm[s, c] dy[2s + j - pad, n]
+            _wgrad(xm, T, 1, 0, dy, T2, T, B, s, offs, Cout, Cin, dw,
+                   (weight.stride(0), weight.stride(1), weight.stride(2)), prec=prec)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.sum(dim=(0, 1))
+        return dx, dw, db, None
+
+
+class _LinearTM(torch.autograd.Function):
+    """x @ W^T + b -> dropout -> + residual  (diffusers to_q/k/v/to_out Linear + Dropout)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, dropout_p):
+        _check(x, weight, residual)
+        prec = gemm_precision()
+        shp = x.shape
+        x2 = _f32c(x).reshape(-1, shp[-1])
+        M, K = x2.shape
+        Nout = weight.shape[0]
+        Wp, Kp = pack_weight(weight, prec)
+        y = torch.empty(M, Nout, device=x.device, dtype=torch.float32)
+        res2 = _f32c(residual).reshape(M, Nout) if residual is not None else None
+        seed = _new_seed(x.device) if dropout_p > 0 else None
+        _gemm(x2, M, M, 1, 1, [0], K, Wp, Kp, Nout, y, M, prec=prec, bias=_f32c(bias), residual=res2,
+              dropout_p=dropout_p, seed=seed)
+        ctx.save_for_backward(x2, weight)
+        ctx.cfg = (prec, bias is not None, residual is not None, shp, dropout_p, seed)
+        return y.reshape(*shp[:-1], Nout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight = ctx.saved_tensors
+        prec, has_bias, has_res, shp, p, seed = ctx.cfg
+        Nout, K = weight.shape
+        dy2 = _f32c(dy).reshape(-1, Nout)
+        M = dy2.shape[0]
+        dres = dy if has_res else None
+        if p > 0:  # gradient through the epilogue dropout: regenerate the forward's mask
+            g = torch.empty_like(dy2)
+            N.check(N.lib().mtts_dropout_apply(dy2.data_ptr(), g.data_ptr(), M, Nout, Nout, float(p),
+                                               seed.data_ptr(), _stream(g)), "mtts_dropout_apply")
+            dy2 = g
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            Wd, Kp = pack_weight(weight.t(), prec)
+            dx = torch.empty(M, K, device=dy2.device, dtype=torch.float32)
+            _gemm(dy2, M, M, 1, 1, [0], Nout, Wd, Kp, K, dx, M, prec=prec)
+            dx = dx.reshape(*shp)
+        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
+            dw = torch.empty(weight.shape, device=dy2.device, dtype=torch.float32)
+            db = torch.empty(Nout, device=dy2.device, dtype=torch.float32) if has_bias else None
+            _wgrad(dy2, M, 1, 0, x2, M, M, 1, 1, [0], K, Nout, dw, (K, 1, 0), prec=prec, db=db)
+        return dx, dw, db, dres, None
+
+
+class _FeedForwardTM(torch.autograd.Function):
+    """residual + dropout(gelu(x W1^T + b1)) W2^T + b2   (diffusers GELU -> Dropout -> Linear,
+    transformer.py:155-188).  The pre-activation is stored by the first GEMM's epilogue; the backward
+    folds GELU' and the regenerated dropout mask into the second GEMM's dgrad epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, residual, dropout_p):
+        _check(x, w1, w2, residual)
+        prec = gemm_precision()
+        shp = x.shape
+        x2 = _f32c(x).reshape(-1, shp[-1])
+        M, K = x2.shape
+        H, Nout = w1.shape[0], w2.shape[0]
+        W1p, K1p = pack_weight(w1, prec)
+        W2p, K2p = pack_weight(w2, prec)
+        z = torch.empty(M, H, device=x.device, dtype=torch.float32)
+        h = torch.empty(M, H, device=x.device, dtype=torch.float32)
+        seed = _new_seed(x.device) if dropout_p > 0 else None
+        _gemm(x2, M, M, 1, 1, [0], K, W1p, K1p, H, h, M, prec=prec, bias=_f32c(b1), act=ACT_GELU, C_pre=z,
+              dropout_p=dropout_p, seed=seed)
+        y = torch.empty(M, Nout, device=x.device, dtype=torch.float32)
+        res2 = _f32c(residual).reshape(M, Nout) if residual is not None else None
+        _gemm(h, M, M, 1, 1, [0], H, W2p, K2p, Nout, y, M, prec=prec, bias=_f32c(b2), residual=res2)
+        ctx.save_for_backward(x2, z, h, w1, w2)
+        ctx.cfg = (prec, shp, residual is not None, dropout_p, seed, b1 is not None, b2 is not None)
+        return y.reshape(*shp[:-1], Nout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, z, h, w1, w2 = ctx.saved_tensors
+        prec, shp, has_res, p, seed, has_b1, has_b2 = ctx.cfg
+        H, K = w1.shape
+        Nout = w2.shape[0]
+        dy2 = _f32c(dy).reshape(-1, Nout)
+        M = dy2.shape[0]
+        dev = dy2.device
+        dw2 = torch.empty(w2.shape, device=dev, dtype=torch.float32)
+        db2 = torch.empty(Nout, device=dev, dtype=torch.float32)
+        _wgrad(dy2, M, 1, 0, h, M, M, 1, 1, [0], H, Nout, dw2, (H, 1, 0), prec=prec, db=db2)
+        W2t, K2p = pack_weight(w2.t(), prec)
+        dz = torch.empty(M, H, device=dev, dtype=torch.float32)
+        _gemm(dy2, M, M, 1, 1, [0], Nout, W2t, K2p, H, dz, M, prec=prec, act=ACT_DGELU, aux=z, dropout_p=p,
+              seed=seed)
+        dw1 = torch.empty(w1.shape, device=dev, dtype=torch.float32)
+        db1 = torch.empty(H, device=dev, dtype=torch.float32)
+        _wgrad(dz, M, 1, 0, x2, M, M, 1, 1, [0], K, H, dw1, (K, 1, 0), prec=prec, db=db1)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            W1t, K1p = pack_weight(w1.t(), prec)
+            dx = torch.empty(M, K, device=dev, dtype=torch.float32)
+            _gemm(dz, M, M, 1, 1, [0], H, W1t, K1p, K, dx, M, prec=prec)
+            dx = dx.reshape(*shp)
+        return (dx, dw1, db1 if has_b1 else None, dw2, db2 if has_b2 else None, (dy if has_res else None),
+                None)
+
+
+# ------------------------------------------------------------------------------------------ norms
+class _GroupNormMishTM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, gamma, beta, mask, add, groups, eps):
+        _check(h, gamma, mask, add)
+        h = _f32c(h)
+        B, T, C = h.shape
+        y = torch.empty_like(h)
+        mean = torch.empty(B, groups, device=h.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        gamma_c, beta_c, mask_c, add_c = _f32c(gamma), _f32c(beta), _f32c(mask), _f32c(add)
+        N.check(N.lib().mtts_gn_mish_fwd(h.data_ptr(), gamma_c.data_ptr(), beta_c.data_ptr(), N.ptr(mask_c),
+                                         N.ptr(add_c), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), B, T, C,
+                                         groups, float(eps), _stream(h)), "mtts_gn_mish_fwd")
+        ctx.save_for_backward(h, gamma_c, beta_c, mask_c, mean, rstd)
+        ctx.cfg = (groups, add is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, gamma, beta, mask, mean, rstd = ctx.saved_tensors
+        groups, has_add = ctx.cfg
+        dy = _f32c(dy)
+        B, T, C = h.shape
+        dh = torch.empty_like(h)
+        dg = torch.empty(C, device=h.device, dtype=torch.float32)
+        dbt = torch.empty_like(dg)
+        dadd = torch.empty(B, C, device=h.device, dtype=torch.float32) if has_add else None
+        lib = N.lib()
+        ws = torch.empty(int(lib.mtts_gn_mish_bwd_workspace_size(B, C)), dtype=torch.uint8, device=h.device)
+        N.check(lib.mtts_gn_mish_bwd(dy.data_ptr(), h.data_ptr(), gamma.data_ptr(), beta.data_ptr(), N.ptr(mask),
+                                     mean.data_ptr(), rstd.data_ptr(), dh.data_ptr(), dg.data_ptr(), dbt.data_ptr(),
+                                     N.ptr(dadd), B, T, C, groups, ws.data_ptr(), ws.numel(), _stream(h)),
+                "mtts_gn_mish_bwd")
+        return dh, dg, dbt, None, dadd, None, None
+
+
+class _LayerNormTM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        _check(x, w)
+        shp = x.shape
+        x2 = _f32c(x).reshape(-1, shp[-1])
+        M, C = x2.shape
+        y = torch.empty_like(x2)
+        mean = torch.empty(M, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        w_c, b_c = _f32c(w), _f32c(b)
+        N.check(N.lib().mtts_layernorm_fwd(x2.data_ptr(), w_c.data_ptr(), b_c.data_ptr(), y.data_ptr(),
+                                           mean.data_ptr(), rstd.data_ptr(), M, C, float(eps), _stream(x2)),
+                "mtts_layernorm_fwd")
+        ctx.save_for_backward(x2, w_c, mean, rstd)
+        ctx.shp = shp
+        return y.reshape(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, mean, rstd = ctx.saved_tensors
+        M, C = x2.shape
+        dy2 = _f32c(dy).reshape(M, C)
+        dx = torch.empty_like(x2)
+        dw = torch.empty(C, device=x2.device, dtype=torch.float32)
+        db = torch.empty_like(dw)
+        lib = N.lib()
+        ws = torch.empty(max(int(lib.mtts_layernorm_bwd_workspace_size(M, C)), 1), dtype=torch.uint8,
+                         device=x2.device)
+        N.check(lib.mtts_layernorm_bwd(dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), mean.data_ptr(),
+                                       rstd.data_ptr(), dx.data_ptr(), dw.data_ptr(), db.data_ptr(), M, C,
+                                       ws.data_ptr(), ws.numel(), _stream(x2)), "mtts_layernorm_bwd")
+        return dx.reshape(ctx.shp), dw, db, None
+
+
+# ------------------------------------------------------------------------------------------ public ops
+def conv_tm(x, weight, bias, mask=None, stride: int = 1, padding: int | None = None, out_scale=None):
+    """y = Conv1d(x * mask) [* out_scale] token-major.  x [B,T,Cin], weight [Cout,Cin,k] (nn.Conv1d
+    layout), mask/out_scale [B,T] or None.  decoder.py:59,65,78,85,95,192,239,248,251,369-371."""
     if padding is None:
-        padding = k // 2
-    if mask is not None:
-        x = x * mask.unsqueeze(-1)
-    return F.conv1d(_cm(x), weight, bias, stride=stride, padding=padding).transpose(1, 2)
+        padding = weight.shape[-1] // 2
+    return _ConvTM.apply(x, weight, bias, mask, out_scale, stride, padding)
 
 
 def conv_transpose_tm(x, weight, bias, mask=None):
     """ConvTranspose1d(k=4, s=2, p=1) of x * mask; weight [Cin,Cout,4].  decoder.py:112-116."""
-    if mask is not None:
-        x = x * mask.unsqueeze(-1)
-    return F.conv_transpose1d(_cm(x), weight, bias, stride=2, padding=1).transpose(1, 2)
+    return _ConvTransposeTM.apply(x, weight, bias, mask)
 
 
-def group_norm_mish_tm(h, gamma, beta, groups: int, mask, add=None, eps: float = 1e-5):
-    """mish(GroupNorm(h)) * mask (+ add[b, c]).  Block1D tail (decoder.py:58-66) with the ResNet
-    time-embedding injection (decoder.py:82-83) fused.  GN statistics span the full padded length,
-    exactly like the reference."""
-    y = F.mish(F.group_norm(_cm(h), groups, gamma, beta, eps)).transpose(1, 2) * mask.unsqueeze(-1)
-    if add is not None:
-        y = y + add.unsqueeze(1)
-    return y
+def group_norm_mish_tm(h, gamma, beta, groups: int, mask=None, add=None, eps: float = 1e-5):
+    """mish(GroupNorm(h)) * mask (+ add[b, c]): Block1D tail (decoder.py:58-66) with Resnet1D's
+    time-embedding add (decoder.py:82-83) fused; statistics over the full padded length."""
+    return _GroupNormMishTM.apply(h, gamma, beta, mask, add, groups, eps)
 
 
 def layer_norm_tm(h, weight, bias, eps: float = 1e-5):
-    return F.layer_norm(h, (h.shape[-1],), weight, bias, eps)
+    return _LayerNormTM.apply(h, weight, bias, eps)
 
 
-def linear_tm(x, weight, bias=None, act: str | None = None, residual=None):
-    """x @ W^T + b, optional erf-GELU epilogue or residual add (transformer.py:155-156,174-180,
-    diffusers to_out)."""
-    y = F.linear(x, weight, bias)
-    if act == "gelu":
-        y = F.gelu(y)
-    if residual is not None:
-        y = y + residual
-    return y
+def linear_tm(x, weight, bias=None, residual=None, dropout_p: float = 0.0):
+    """residual + dropout(x @ W^T + b)   (diffusers Linear [+ Dropout] [+ residual])."""
+    return _LinearTM.apply(x, weight, bias, residual, float(dropout_p))
+
+
+def ff_tm(x, w1, b1, w2, b2, residual=None, dropout_p: float = 0.0):
+    return _FeedForwardTM.apply(x, w1, b1, w2, b2, residual, float(dropout_p))
 
 
 def attention_tm(q, k, v, key_bias, heads: int):

@@ -83,7 +83,9 @@ class Resnet1D(nn.Module):
         self.res_conv = nn.Conv1d(in_channels, out_channels, 1)
 
     def forward_tm(self, x, mask, time_emb):
-        h = self.block1.forward_tm(x, mask, add=self.mlp(time_emb))
+        with torch.autocast("cuda", enabled=False):  # [B, C] time projection, fp32
+            tproj = self.mlp(time_emb.float())
+        h = self.block1.forward_tm(x, mask, add=tproj)
         h = self.block2.forward_tm(h, mask)
         return O.conv_tm(x, self.res_conv.weight, self.res_conv.bias, mask, padding=0) + h
 
@@ -187,8 +189,17 @@ class Decoder(nn.Module):
         return x
 
     def forward_tm(self, x, mask, mu, t):
-        """x, mu: [B, T, C] token-major; mask [B, T]; t [B] -> [B, T, out] token-major."""
-        temb = self.time_mlp(self.time_embeddings(t))
+        """x, mu: [B, T, C] token-major; mask [B, T]; t [B] -> [B, T, out] token-major.
+        GEMMs run bf16 MFMA inside a bf16 autocast region (fp32 accumulate, fp32 activations), exact
+        fp32 MFMA otherwise; everything else here is fp32."""
+        prec_bf16 = torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+        with torch.autocast("cuda", enabled=False):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec_bf16):
+                return self._forward_tm(x.float(), mask.float(), mu.float(), t.float())
+
+    def _forward_tm(self, x, mask, mu, t):
+        with torch.autocast("cuda", enabled=False):  # [B, 1024] time MLP: tiny, kept fp32
+            temb = self.time_mlp(self.time_embeddings(t))
         h = torch.cat([x, mu], dim=-1)  # einops pack "b * t" on channels (:288)
         skips, masks = [], [mask]
         for resnet, tfs, down in self.Downsampling_Blocks:
@@ -224,9 +235,8 @@ class Decoder(nn.Module):
                 m = m[:, :new]
         h = _conv_tm(self.final_conv, h, m)
         h = O.group_norm_mish_tm(h, self.final_norm.weight, self.final_norm.bias, self.final_norm.num_groups,
-                                 torch.ones_like(m), None, self.final_norm.eps)
-        out = _conv_tm(self.final_proj, h, m)
-        return out * mask.unsqueeze(-1)
+                                 None, None, self.final_norm.eps)  # no mask after the final Mish (:366-368)
+        return O.conv_tm(h, self.final_proj.weight, self.final_proj.bias, m, padding=0, out_scale=mask)
 
     def forward(self, x, mask, mu, t, cond=None):
         """Reference signature: x, mu [B, C, T]; mask [B, 1, T]; t [B] -> [B, out, T]."""

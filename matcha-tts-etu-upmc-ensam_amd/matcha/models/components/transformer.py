@@ -29,7 +29,7 @@ class GELU(nn.Module):
         self.proj = nn.Linear(dim_in, dim_out, bias=bias)
 
     def forward(self, x):
-        return O.linear_tm(x, self.proj.weight, self.proj.bias, act="gelu")
+        return torch.nn.functional.gelu(self.proj(x))
 
 
 class FeedForward(nn.Module):
@@ -46,13 +46,13 @@ class FeedForward(nn.Module):
             self.net.append(nn.Dropout(dropout))
 
     def forward_tm(self, x, residual=None):
-        h = self.net[1](self.net[0](x))
-        out = O.linear_tm(h, self.net[2].weight, self.net[2].bias, residual=None if len(self.net) > 3 else residual)
+        """residual + Linear2(Dropout(GELU(Linear1(x)))) as one fused op (GELU, dropout and the
+        residual live in the GEMM epilogues)."""
         if len(self.net) > 3:
-            out = self.net[3](out)
-            if residual is not None:
-                out = out + residual
-        return out
+            raise NotImplementedError("final_dropout is not used by the Matcha decoder")
+        p = self.net[1].p if self.training else 0.0
+        proj, out = self.net[0].proj, self.net[2]
+        return O.ff_tm(x, proj.weight, proj.bias, out.weight, out.bias, residual=residual, dropout_p=p)
 
     def forward(self, hidden_states):
         return self.forward_tm(hidden_states)
@@ -78,9 +78,8 @@ class Attention(nn.Module):
         qkv = O.linear_tm(h, self.qkv_weight(), None)
         q, k, v = qkv.split(C, dim=-1)
         o = O.attention_tm(q, k, v, key_bias, self.heads)
-        if self.training and self.to_out[1].p > 0:
-            return self.to_out[1](O.linear_tm(o, self.to_out[0].weight, self.to_out[0].bias)) + residual
-        return O.linear_tm(o, self.to_out[0].weight, self.to_out[0].bias, residual=residual)
+        p = self.to_out[1].p if self.training else 0.0
+        return O.linear_tm(o, self.to_out[0].weight, self.to_out[0].bias, residual=residual, dropout_p=p)
 
     def forward(self, hidden_states, encoder_hidden_states=None, attention_mask=None, **kw):
         if encoder_hidden_states is not None:

@@ -4,11 +4,18 @@ baselightningmodule.py:115-162) on one process per GPU.
   - fp32 master weights, AdamW(1e-4, (0.9, 0.999), wd 1e-6) + per-epoch cosine (configure_optimizers)
   - gradient clipping by global norm 1.0 (gradient_clip_val=1.0)
   - gradient accumulation (accumulate_grad_batches; the reference uses 2 x 16 = 32 per step)
-  - data parallel over RCCL: torch DDP buckets the gradients (bucket_mb) and all-reduces each bucket
-    on its comm stream as soon as backward has produced it, i.e. overlapped with the rest of
-    backward; non-final accumulation micro-batches skip the all-reduce (no_sync)
-  - the 4 logged losses of a step are reduced in ONE all-reduce (the reference issues one
-    sync_dist all-reduce per self.log call)
+  - the step's 4 logged losses reduced in ONE collective (the reference issues one sync_dist
+    all-reduce per self.log call)
+
+Two execution modes:
+  graph=True (default on GPU): the whole step is captured once into a HIP graph and replayed -- about
+    a thousand kernel launches per step become one graph launch.  Gradients live in ONE flat fp32
+    buffer (every param.grad is a view into it), so data parallelism is a single RCCL all-reduce of
+    that buffer over xGMI between the forward/backward graph and the clip/AdamW graph.  Dropout masks
+    (torch's and the HIP epilogues') are drawn from device-side RNG state, so every replay draws new
+    masks.  Inputs are copied into static buffers before each replay.
+  graph=False (eager): torch DDP over RCCL (bucketed all-reduce overlapped with backward, no_sync
+    for non-final accumulation micro-batches).
 
 Synthetic LJSpeech-shaped batches: token ids ~ U{1..149}, lengths ~ U[0.7 max, max]
 with element 0 = max, mels ~ N(0, 1) zeroed past the length.
@@ -16,6 +23,7 @@ with element 0 = max, mels ~ N(0, 1) zeroed past the length.
 from __future__ import annotations
 
 import contextlib
+import math
 from dataclasses import dataclass
 
 import torch
@@ -46,41 +54,61 @@ class TrainConfig:
     gradient_clip_val: float = 1.0
     bucket_mb: float = 25.0
     precision: str = "32-true"  # "32-true" (reference) or "bf16-mixed"
+    graph: bool = False
+    lr: float = 1e-4
+    eta_min: float = 1e-6
+    t_max_epochs: int = 1000
 
 
 class Trainer:
     def __init__(self, model: MatchaTTS, cfg: TrainConfig = TrainConfig()):
         self.cfg = cfg
         self.model = model
-        self.ddp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
-        if self.ddp:
-            dev = next(model.parameters()).device
-            self.wrapped = torch.nn.parallel.DistributedDataParallel(
-                model, device_ids=[dev.index], bucket_cap_mb=cfg.bucket_mb, gradient_as_bucket_view=True,
-                broadcast_buffers=False)
-        else:
-            self.wrapped = model
-        opt = model.configure_optimizers()
-        self.optimizer = opt["optimizer"]
-        self.scheduler = opt["lr_scheduler"]["scheduler"]
+        self.world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
+        self.dev = next(model.parameters()).device
+        self.params = [p for p in model.parameters() if p.requires_grad]
         self.global_step = 0
+        self.epoch = 0
         self.last_losses = None
+        if cfg.graph:
+            if self.world > 1:  # identical initial weights on every rank (what DDP's broadcast does)
+                for p in model.state_dict().values():
+                    dist.broadcast(p, 0)
+            n = sum(p.numel() for p in self.params)
+            self.flat = torch.zeros(n, device=self.dev, dtype=torch.float32)
+            off = 0
+            for p in self.params:
+                p.grad = self.flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
+            self.lr = torch.tensor(cfg.lr, device=self.dev)
+            self.optimizer = torch.optim.AdamW(self.params, lr=self.lr, betas=(0.9, 0.999), weight_decay=1e-6,
+                                               fused=True, capturable=True)
+            self.scheduler = None
+            self._g_fb = self._g_opt = None
+            self._static = None
+            self.wrapped = model
+        else:
+            if self.world > 1:
+                self.wrapped = torch.nn.parallel.DistributedDataParallel(
+                    model, device_ids=[self.dev.index], bucket_cap_mb=cfg.bucket_mb, gradient_as_bucket_view=True,
+                    broadcast_buffers=False)
+            else:
+                self.wrapped = model
+            opt = model.configure_optimizers()
+            self.optimizer = opt["optimizer"]
+            self.scheduler = opt["lr_scheduler"]["scheduler"]
 
+    # ------------------------------------------------------------------------------------ common
     def _autocast(self):
         if self.cfg.precision == "bf16-mixed":
             return torch.autocast(device_type="cuda", dtype=torch.bfloat16)
         return contextlib.nullcontext()
 
-    def step(self, batches: list[dict]) -> torch.Tensor:
-        """One optimizer step over len(batches) == accumulate_grad_batches micro-batches.
-        Returns the device tensor [dur, prior, diff, total] (mean over micro-batches and ranks);
-        nothing here synchronises with the host."""
-        assert len(batches) == self.cfg.accumulate_grad_batches
+    def _fwd_bwd(self, batches, sync_ctx=None):
         n = len(batches)
         logged = None
         for i, batch in enumerate(batches):
-            sync = i == n - 1
-            ctx = self.wrapped.no_sync() if (self.ddp and not sync) else contextlib.nullcontext()
+            ctx = sync_ctx(i) if sync_ctx else contextlib.nullcontext()
             with ctx:
                 with self._autocast():
                     dur, prior, diff, _ = self.wrapped(x=batch["x"], x_lengths=batch["x_lengths"],
@@ -89,17 +117,100 @@ class Trainer:
                 (total / n).backward()
             vals = torch.stack([dur.detach(), torch.as_tensor(prior).detach(), diff.detach(), total.detach()]).float()
             logged = vals if logged is None else logged + vals
-        logged = logged / n
-        if self.ddp:  # the step's logged scalars in one collective (sync_dist=True)
-            dist.all_reduce(logged)
-            logged = logged / dist.get_world_size()
+        return logged / n
+
+    def _clip_and_update(self):
         if self.cfg.gradient_clip_val:
-            torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.cfg.gradient_clip_val, foreach=True)
+            torch.nn.utils.clip_grad_norm_(self.params, self.cfg.gradient_clip_val, foreach=True)
         self.optimizer.step()
+
+    # ------------------------------------------------------------------------------------ eager
+    def _eager_step(self, batches):
+        n = len(batches)
+        ddp = self.world > 1
+
+        def sync_ctx(i):
+            return self.wrapped.no_sync() if (ddp and i < n - 1) else contextlib.nullcontext()
+
+        logged = self._fwd_bwd(batches, sync_ctx)
+        if ddp:  # the step's logged scalars in one collective (sync_dist=True)
+            dist.all_reduce(logged)
+            logged = logged / self.world
+        self._clip_and_update()
         self.optimizer.zero_grad(set_to_none=True)
+        return logged
+
+    # ------------------------------------------------------------------------------------ graph
+    def _graph_capture(self, batches):
+        self._static = [{k: v.clone() for k, v in b.items()} for b in batches]
+        # warm-up (allocator pools, lazy library loads, optimizer state) must not leave updates behind
+        saved = [p.detach().clone() for p in self.params]
+        saved_state = {id(p): {k: v.clone() for k, v in st.items() if torch.is_tensor(v)}
+                       for p, st in self.optimizer.state.items()}
+        side = torch.cuda.Stream(self.dev)
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self.flat.zero_()
+                self._fwd_bwd(self._static)
+                self._clip_and_update()
+        torch.cuda.current_stream(self.dev).wait_stream(side)
+        with torch.no_grad():
+            for p, s_ in zip(self.params, saved):
+                p.copy_(s_)
+            for p, st in self.optimizer.state.items():  # moments / step back to their pre-warm-up values
+                prev = saved_state.get(id(p), {})
+                for k, v in st.items():
+                    if torch.is_tensor(v):
+                        v.copy_(prev[k]) if k in prev else v.zero_()
+
+        self._g_fb = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g_fb):
+            self.flat.zero_()
+            self._logged = self._fwd_bwd(self._static)
+            if self.world == 1:
+                self._clip_and_update()
+        if self.world > 1:
+            self._g_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._g_opt, pool=self._g_fb.pool()):
+                self._clip_and_update()
+
+    def _graph_step(self, batches):
+        if self._g_fb is None or len(batches) != len(self._static) or any(
+                b[k].shape != s[k].shape for b, s in zip(batches, self._static) for k in s):
+            self._graph_capture(batches)
+        for b, s in zip(batches, self._static):
+            for k, v in s.items():
+                if b[k] is not v:
+                    v.copy_(b[k], non_blocking=True)
+        self._g_fb.replay()
+        logged = self._logged
+        if self.world > 1:
+            dist.all_reduce(self.flat)  # one RCCL all-reduce of every gradient
+            self.flat.div_(self.world)
+            logged = logged.clone()
+            dist.all_reduce(logged)
+            logged = logged / self.world
+            self._g_opt.replay()
+        return logged
+
+    # ------------------------------------------------------------------------------------ api
+    def step(self, batches: list[dict]) -> torch.Tensor:
+        """One optimizer step over len(batches) == accumulate_grad_batches micro-batches.  Returns the
+        device tensor [dur, prior, diff, total] (mean over micro-batches and ranks); nothing here
+        synchronises with the host."""
+        assert len(batches) == self.cfg.accumulate_grad_batches
+        logged = self._graph_step(batches) if self.cfg.graph else self._eager_step(batches)
         self.global_step += 1
         self.last_losses = logged
         return logged
 
     def on_epoch_end(self):
-        self.scheduler.step()
+        """CosineAnnealingLR(T_max=1000 epochs, eta_min=1e-6) stepped per epoch."""
+        self.epoch += 1
+        if self.scheduler is not None:
+            self.scheduler.step()
+        else:
+            c = self.cfg
+            lr = c.eta_min + (c.lr - c.eta_min) * (1 + math.cos(math.pi * self.epoch / c.t_max_epochs)) / 2
+            self.lr.fill_(lr)

@@ -1,0 +1,196 @@
+"""Each fused decoder operator (HIP, token-major) against a plain PyTorch fp32 reference of the same
+op, forward and backward.  Tolerances (relative L2): fp32 MFMA mode 2e-5 fwd / 1e-4 grads; bf16 MFMA
+mode 1.5e-2 (bf16 operand rounding, fp32 accumulation)."""
+from __future__ import annotations
+
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+TOL = {"fp32": (2e-5, 1e-4), "bf16": (1.5e-2, 1.5e-2)}
+
+
+def rel(a, b):
+    return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
+
+
+def _ctx(prec):
+    return torch.autocast("cuda", dtype=torch.bfloat16, enabled=(prec == "bf16"))
+
+
+def _mask(B, T, lengths):
+    m = torch.zeros(B, T, device=DEV)
+    for b, L in enumerate(lengths):
+        m[b, :L] = 1
+    return m
+
+
+def _run(fn, ref, inputs, prec):
+    """fn/ref take the same leaf tensors; compares outputs and all input grads."""
+    torch.manual_seed(0)
+    xs = [t.detach().clone().requires_grad_(t.requires_grad) for t in inputs]
+    rs = [t.detach().clone().requires_grad_(t.requires_grad) for t in inputs]
+    with _ctx(prec):
+        y = fn(*xs)
+    yr = ref(*rs)
+    g = torch.randn_like(yr)
+    (y * g).sum().backward()
+    (yr * g).sum().backward()
+    ftol, gtol = TOL[prec]
+    assert rel(y, yr) < ftol, rel(y, yr)
+    for a, b in zip(xs, rs):
+        if b.grad is not None:
+            assert a.grad is not None
+            assert rel(a.grad, b.grad) < gtol, (tuple(b.shape), rel(a.grad, b.grad))
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("B,T,Cin,Cout,k,stride,pad,masked", [
+    (2, 37, 32, 64, 3, 1, 1, True), (3, 64, 160, 256, 3, 1, 1, True), (2, 40, 64, 48, 1, 1, 0, True),
+    (2, 41, 32, 32, 3, 2, 1, True), (2, 64, 256, 256, 3, 2, 1, True), (1, 300, 512, 256, 3, 1, 1, False),
+    (2, 33, 256, 80, 1, 1, 0, True)])
+def test_conv_tm(prec, B, T, Cin, Cout, k, stride, pad, masked):
+    from matcha.models.components._ops import conv_tm
+
+    x = torch.randn(B, T, Cin, device=DEV, requires_grad=True)
+    w = (torch.randn(Cout, Cin, k, device=DEV) / math.sqrt(Cin * k)).requires_grad_(True)
+    b = torch.randn(Cout, device=DEV, requires_grad=True)
+    m = _mask(B, T, [T - 5 * i for i in range(B)]) if masked else None
+
+    def ref(x, w, b):
+        xx = x * m.unsqueeze(-1) if m is not None else x
+        return F.conv1d(xx.transpose(1, 2), w, b, stride=stride, padding=pad).transpose(1, 2)
+
+    _run(lambda x, w, b: conv_tm(x, w, b, m, stride=stride, padding=pad), ref, [x, w, b], prec)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_conv_tm_out_scale(prec):
+    from matcha.models.components._ops import conv_tm
+
+    B, T = 2, 50
+    x = torch.randn(B, T, 256, device=DEV, requires_grad=True)
+    w = (torch.randn(80, 256, 1, device=DEV) / 16).requires_grad_(True)
+    b = torch.randn(80, device=DEV, requires_grad=True)
+    m = _mask(B, T, [50, 31])
+    ref = lambda x, w, b: (F.conv1d((x * m[..., None]).transpose(1, 2), w, b).transpose(1, 2) * m[..., None])
+    _run(lambda x, w, b: conv_tm(x, w, b, m, padding=0, out_scale=m), ref, [x, w, b], prec)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("B,T,C", [(2, 19, 32), (3, 150, 256)])
+def test_conv_transpose_tm(prec, B, T, C):
+    from matcha.models.components._ops import conv_transpose_tm
+
+    x = torch.randn(B, T, C, device=DEV, requires_grad=True)
+    w = (torch.randn(C, C, 4, device=DEV) / math.sqrt(C * 2)).requires_grad_(True)
+    b = torch.randn(C, device=DEV, requires_grad=True)
+    m = _mask(B, T, [T - 3 * i for i in range(B)])
+    ref = lambda x, w, b: F.conv_transpose1d((x * m[..., None]).transpose(1, 2), w, b, 2, 1).transpose(1, 2)
+    _run(lambda x, w, b: conv_transpose_tm(x, w, b, m), ref, [x, w, b], prec)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("M,K,Nn,res", [(300, 256, 768, False), (4800, 256, 256, True), (77, 32, 96, True)])
+def test_linear_tm(prec, M, K, Nn, res):
+    from matcha.models.components._ops import linear_tm
+
+    x = torch.randn(2, M // 2 if M % 2 == 0 else M, K, device=DEV, requires_grad=True)
+    w = (torch.randn(Nn, K, device=DEV) / math.sqrt(K)).requires_grad_(True)
+    b = torch.randn(Nn, device=DEV, requires_grad=True)
+    r = torch.randn(*x.shape[:-1], Nn, device=DEV, requires_grad=True)
+    if res:
+        _run(lambda x, w, b, r: linear_tm(x, w, b, residual=r), lambda x, w, b, r: F.linear(x, w, b) + r,
+             [x, w, b, r], prec)
+    else:
+        _run(lambda x, w, b: linear_tm(x, w, b), lambda x, w, b: F.linear(x, w, b), [x, w, b], prec)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("M,C", [(600, 256), (130, 32)])
+def test_ff_tm(prec, M, C):
+    from matcha.models.components._ops import ff_tm
+
+    x = torch.randn(M, C, device=DEV, requires_grad=True)
+    w1 = (torch.randn(4 * C, C, device=DEV) / math.sqrt(C)).requires_grad_(True)
+    b1 = torch.randn(4 * C, device=DEV, requires_grad=True)
+    w2 = (torch.randn(C, 4 * C, device=DEV) / math.sqrt(4 * C)).requires_grad_(True)
+    b2 = torch.randn(C, device=DEV, requires_grad=True)
+    r = torch.randn(M, C, device=DEV, requires_grad=True)
+    ref = lambda x, w1, b1, w2, b2, r: F.linear(F.gelu(F.linear(x, w1, b1)), w2, b2) + r
+    _run(lambda x, w1, b1, w2, b2, r: ff_tm(x, w1, b1, w2, b2, residual=r), ref, [x, w1, b1, w2, b2, r], prec)
+
+
+def test_dropout_epilogues_consistent():
+    """Train-mode dropout: about p of the outputs dropped, survivors scaled 1/(1-p), and the backward
+    regenerates the same mask (checked against an explicit-mask torch computation)."""
+    from matcha.models.components._ops import ff_tm, linear_tm
+
+    torch.manual_seed(1)
+    M, K, Nn, p = 2048, 256, 256, 0.25
+    x = torch.randn(M, K, device=DEV, requires_grad=True)
+    w = (torch.randn(Nn, K, device=DEV) / 16).requires_grad_(True)
+    y = linear_tm(x, w, None, dropout_p=p)
+    full = F.linear(x.detach(), w.detach())
+    keep = y.detach() != 0
+    frac = 1 - keep.float().mean().item()
+    assert abs(frac - p) < 0.01, frac
+    torch.testing.assert_close(y.detach()[keep], full[keep] / (1 - p), rtol=1e-5, atol=1e-5)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    exp_dx = (g * keep / (1 - p)) @ w.detach()
+    assert rel(x.grad, exp_dx) < 1e-5
+    # FF: dropout between GELU and the second Linear
+    w1 = (torch.randn(4 * K, K, device=DEV) / 16).requires_grad_(True)
+    w2 = (torch.randn(K, 4 * K, device=DEV) / 32).requires_grad_(True)
+    xx = torch.randn(M, K, device=DEV, requires_grad=True)
+    y2 = ff_tm(xx, w1, None, w2, None, dropout_p=p)
+    (y2 * g).sum().backward()
+    h = F.gelu(F.linear(xx.detach(), w1.detach()))
+    # recover the mask from a second forward with the same seed is not possible; check statistics
+    assert torch.isfinite(xx.grad).all() and torch.isfinite(w1.grad).all()
+    assert (y2 - F.linear(h, w2.detach())).abs().mean() > 0  # dropout did something
+
+
+@pytest.mark.parametrize("B,T,C,G,masked,add", [(2, 37, 32, 8, True, True), (3, 600, 256, 8, True, True),
+                                                 (2, 300, 256, 8, False, False), (1, 5, 64, 8, True, False)])
+def test_group_norm_mish_tm(B, T, C, G, masked, add):
+    from matcha.models.components._ops import group_norm_mish_tm
+
+    h = (torch.randn(B, T, C, device=DEV) * 3 + 1).requires_grad_(True)
+    gam = (1 + 0.1 * torch.randn(C, device=DEV)).requires_grad_(True)
+    bet = (0.1 * torch.randn(C, device=DEV)).requires_grad_(True)
+    m = _mask(B, T, [T - 2 * i for i in range(B)]) if masked else None
+    a = torch.randn(B, C, device=DEV, requires_grad=True)
+
+    def ref(h, gam, bet, a):
+        y = F.mish(F.group_norm(h.transpose(1, 2), G, gam, bet, 1e-5)).transpose(1, 2)
+        if m is not None:
+            y = y * m[..., None]
+        return y + a[:, None, :] if add else y
+
+    _run(lambda h, gam, bet, a: group_norm_mish_tm(h, gam, bet, G, m, a if add else None), ref, [h, gam, bet, a],
+         "fp32")
+
+
+@pytest.mark.parametrize("M,C", [(19200, 256), (77, 32), (5, 1024)])
+def test_layer_norm_tm(M, C):
+    from matcha.models.components._ops import layer_norm_tm
+
+    x = (torch.randn(M, C, device=DEV) * 2 + 0.5).requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(C, device=DEV)).requires_grad_(True)
+    b = (0.1 * torch.randn(C, device=DEV)).requires_grad_(True)
+    _run(lambda x, w, b: layer_norm_tm(x, w, b), lambda x, w, b: F.layer_norm(x, (C,), w, b, 1e-5), [x, w, b],
+         "fp32")
+
+
+def test_ops_refuse_cpu_and_never_fall_back():
+    from matcha import _native as N
+    from matcha.models.components._ops import conv_tm
+
+    with pytest.raises(N.NativeError):
+        conv_tm(torch.randn(1, 4, 8), torch.randn(8, 8, 3), None)
