@@ -90,8 +90,8 @@ class Trainer:
         else:
             if self.world > 1:
                 self.wrapped = torch.nn.parallel.DistributedDataParallel(
-                    model, device_ids=[self.dev.index], bucket_cap_mb=cfg.bucket_mb, gradient_as_bucket_view=True,
-                    broadcast_buffers=False)
+                    model, device_ids=[self.dev.index] if self.dev.type == "cuda" else None,
+                    bucket_cap_mb=cfg.bucket_mb, gradient_as_bucket_view=True, broadcast_buffers=False)
             else:
                 self.wrapped = model
             opt = model.configure_optimizers()
@@ -100,7 +100,7 @@ class Trainer:
 
     # ------------------------------------------------------------------------------------ common
     def _autocast(self):
-        if self.cfg.precision == "bf16-mixed":
+        if self.cfg.precision == "bf16-mixed" and self.dev.type == "cuda":
             return torch.autocast(device_type="cuda", dtype=torch.bfloat16)
         return contextlib.nullcontext()
 
