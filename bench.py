@@ -6,13 +6,16 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 A step = forward (text encoder, fp32 log-prior lattice, HIP maximum_path, CFM decoder) + backward +
-grad-norm clip (1.0) + AdamW on B=32 utterances per GPU (Tx=120, Ty=600, 80 mels; BASELINE config 3,
-one process per GPU, data parallel over RCCL with DDP's bucketed all-reduce overlapped with
-backward).  Inputs are resident in HBM before the timed region.  Rank 0 prints ONE JSON line:
-value = utterances/s over all ranks (max-over-ranks wall time), plus maximum_path Mcells/s, the MAS
-kernel roofline (HIP events around every MAS launch in the timed region, on the launch stream) and,
-at N=1, the CPU baseline timed on this host (oracle restatement of the reference step, and the
-reference Cython MAS when oracle/_ref was built).
+grad-norm clip (1.0) + AdamW on B=32 utterances per GPU (Tx=120, Ty=600, 80 mels; BASELINE config 3),
+one process per GPU, data parallel over RCCL.  By default the whole step is one captured HIP graph
+replay (N>1: graph fwd+bwd, one RCCL all-reduce of the flat gradient buffer, graph clip+AdamW);
+--no-graph runs it eagerly under DDP.  Inputs are resident in HBM before the timed region.
+Rank 0 prints ONE JSON line: value = utterances/s over all ranks (max-over-ranks wall time), plus
+  roofline      the dominant kernel (decoder conv_gemm_kernel): HIP events around each of its launches
+                on the launch stream during one extra eager fwd+bwd after the timed region;
+  maximum_path  Mcells/s and roofline_mas (HIP events around maximum_path on the batch's own lattice);
+  cpu_baseline  (N=1) the oracle restatement of the reference step and the reference Cython MAS
+                (oracle/_ref when built) timed on this host's cores.
 """
 from __future__ import annotations
 
@@ -206,11 +209,28 @@ def main():
                 e1.record()
                 mas_events.append((e0, e1))
         torch.cuda.synchronize()
+    # dominant kernel: the decoder's implicit-GEMM conv/linear (conv_gemm_kernel, fwd + dgrad).  One
+    # more eager fwd+bwd of the same batch (after the timed region, results discarded) with HIP events
+    # around every launch on its stream; algorithmic FLOPs = 2*M*N*K per launch.
+    from matcha.models.components import _ops as OPS
+
+    for rep in range(2):
+        OPS.LAUNCH_LOG = []
+        trainer._fwd_bwd([batch])
+        torch.cuda.synchronize()
+    gemm_log, OPS.LAUNCH_LOG = OPS.LAUNCH_LOG, None
+    model.zero_grad(set_to_none=False)
+    gemm_ms = [a.elapsed_time(b) for a, b, _, _ in gemm_log]
+    gemm_flops = sum(f for _, _, f, _ in gemm_log)
+    gemm_avg_us = sum(gemm_ms) / max(len(gemm_ms), 1) * 1e3
+    gemm_tflops = gemm_flops / (sum(gemm_ms) * 1e-3) / 1e12 if gemm_ms else 0.0
+
     mas_ms = sum(a.elapsed_time(b) for a, b in mas_events) / max(len(mas_events), 1)
     cells = B * Tx * Ty
     mas_gbs = 12.0 * cells / (mas_ms * 1e-3) / 1e9
     step_ms = elapsed / args.steps * 1e3
     flops = decoder_train_flops(B, Ty)
+    gemm_peak = FP32_MFMA_TFLOPS if args.precision == "32-true" else BF16_DENSE_TFLOPS
 
     if rank == 0:
         rec = {
@@ -233,11 +253,18 @@ def main():
                        "precision": args.precision, "hip_graph": graph},
             "maximum_path": {"value": round(world * cells / mas_ms / 1e3, 1), "unit": "Mcells/s (whole node)",
                              "ms_per_call": round(mas_ms, 4), "calls": len(mas_events)},
-            "roofline": {"kernel": "mas_dp_kernel + mas_expand_kernel (maximum_path)", "bound": "hbm",
-                         "achieved": round(mas_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(mas_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                         "algorithmic_bytes_per_launch": 12 * cells,
-                         "note": "12 B/cell (value+mask read, path write); chain-bound: one wave per utterance"},
+            "roofline": {"kernel": "conv_gemm_kernel (decoder implicit-GEMM conv/linear, fwd + dgrad)",
+                         "bound": "mfma", "achieved": round(gemm_tflops, 1), "peak": gemm_peak, "unit": "TFLOP/s",
+                         "frac": round(gemm_tflops / gemm_peak, 4), "traffic": None,
+                         "launches_per_step": len(gemm_log), "avg_launch_us": round(gemm_avg_us, 2),
+                         "algorithmic_flops_per_step": gemm_flops,
+                         "note": "achieved = sum(2*M*N*K) / sum(launch durations), HIP events on the launch "
+                                 "stream over one eager fwd+bwd of the bench batch"},
+            "roofline_mas": {"kernel": "mas_dp_kernel + mas_expand_kernel (maximum_path)", "bound": "hbm",
+                             "achieved": round(mas_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(mas_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                             "algorithmic_bytes_per_launch": 12 * cells,
+                             "note": "12 B/cell (value+mask read, path write); chain-bound: one wave per utterance"},
             "decoder_mfma": {"train_flops_per_step": flops,
                              "achieved_tflops_step": round(flops / (step_ms * 1e-3) / 1e12, 2),
                              "peak_tflops": FP32_MFMA_TFLOPS if args.precision == "32-true" else BF16_DENSE_TFLOPS},

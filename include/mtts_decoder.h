@@ -35,6 +35,7 @@ extern "C" {
 #define MTTS_ACT_DGELU 2 /* multiply by GELU'(aux[row, n]) -- backward through a GELU */
 
 #define MTTS_CONV_MAX_TAPS 4
+#define MTTS_GEMM_PANEL 64 /* mtts_conv_gemm_tile schedule id of the panel kernel */
 
 /*
  * Implicit GEMM  C[row(b,u), n] = epi( sum_{j<ntaps} sum_{c<cin} A[b*Ti + u*in_stride + off[j], c]
@@ -68,6 +69,11 @@ typedef struct mtts_conv_gemm_args {
 } mtts_conv_gemm_args;
 
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
+/* Same, with an explicit schedule: 0..10 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;
+ * 8..10 are bf16-only 64-wide K steps), MTTS_GEMM_PANEL = the bf16 A-resident panel schedule
+ * (csrc/conv_gemm_panel.hip), -1 = heuristic.
+ * For tuning and tests; mtts_conv_gemm picks the configuration itself. */
+int mtts_conv_gemm_tile(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg, void *hip_stream);
 
 /*
  * Weight gradient of the same implicit GEMM:

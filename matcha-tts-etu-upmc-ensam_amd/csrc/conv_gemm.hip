@@ -82,34 +82,44 @@ struct Stage<false> {
     static constexpr int PAD = 1;  // 33-dword rows: conflict-free ds_read_b32 column reads
 };
 
-template <bool BF16, int MR>
-__global__ __launch_bounds__(kThreads) void conv_gemm_kernel(mtts_conv_gemm_args p) {
-    constexpr int BM = 64 * MR;
+// Block = WM x WN waves; each wave owns TM x TN MFMA tiles of 32x32 -> block tile
+// BM = 32*WM*TM rows x BN = 32*WN*TN cols, K step KB (32, or 64 for bf16: each step is one global
+// round trip, so a longer step halves the exposed latency per MFMA).
+template <bool BF16, int WM, int WN, int TM, int TN, int KB = kBK>
+__global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_args p) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN;
+    constexpr int KC = KB / 8;                    // 8-element chunks per staged row
+    constexpr int CA = (BM * KC + NT - 1) / NT;  // A chunks per thread per K step
+    constexpr int CB = (BN * KC + NT - 1) / NT;  // B chunks per thread per K step
+    static_assert(BM * KC % NT == 0 || NT % (BM * KC) == 0, "tile/threads mismatch");
+    static_assert(BF16 || KB == kBK, "fp32 path uses 32-wide K steps");
     using ST = typename Stage<BF16>::T;
-    constexpr int LDK = kBK + Stage<BF16>::PAD;
+    constexpr int LDK = KB + Stage<BF16>::PAD;
     __shared__ ST As[2][BM * LDK];
-    __shared__ ST Bs[2][kBN * LDK];
+    __shared__ ST Bs[2][BN * LDK];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int wr = wave >> 1, wc = wave & 1;
+    const int wr = wave / WN, wc = wave % WN;
     const int M = p.nb * p.To;
     const int m0 = blockIdx.x * BM;
-    const int n0 = blockIdx.y * kBN;
-    const int nk = (p.K + kBK - 1) / kBK;
+    const int n0 = blockIdx.y * BN;
+    const int nk = (p.K + KB - 1) / KB;
     const float inv_to = 1.0f / (float)p.To;
 
-    // ---- per-thread staging assignment: A: MR chunks of 8, B: 2 chunks of 8 ----
-    Gather ga[MR];
-    int a_row[MR], a_kc[MR], a_j[MR], a_ch[MR];  // (tap, channel) of the chunk at the current K step
+    Gather ga[CA];
+    int a_row[CA], a_kc[CA], a_j[CA], a_ch[CA];  // (tap, channel) of the chunk at the current K step
+    bool a_on[CA];                               // this thread stages an A chunk (tiles with BM*4 < NT)
 #pragma unroll
-    for (int c = 0; c < MR; ++c) {
-        const int q = tid + kThreads * c;
-        a_row[c] = q >> 2;
-        a_kc[c] = (q & 3) * 8;
+    for (int c = 0; c < CA; ++c) {
+        const int q = tid + NT * c;
+        a_on[c] = q < BM * KC;
+        a_row[c] = a_on[c] ? q / KC : 0;
+        a_kc[c] = (q % KC) * 8;
         const int m = m0 + a_row[c];
-        ga[c].valid = m < M;
+        ga[c].valid = a_on[c] && m < M;
         int b = 0, u = 0;
         if (ga[c].valid) divmod_fast(m, p.To, inv_to, b, u);
         ga[c].in_base = b * p.Ti;
@@ -117,21 +127,23 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(mtts_conv_gemm_args
         a_j[c] = a_kc[c] / p.cin;
         a_ch[c] = a_kc[c] - a_j[c] * p.cin;
     }
-    int b_row[2], b_kc[2];
+    int b_row[CB], b_kc[CB];
+    bool b_on[CB];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        const int q = tid + kThreads * c;
-        b_row[c] = q >> 2;
-        b_kc[c] = (q & 3) * 8;
+    for (int c = 0; c < CB; ++c) {
+        const int q = tid + NT * c;
+        b_on[c] = q < BN * KC;
+        b_row[c] = b_on[c] ? q / KC : 0;
+        b_kc[c] = (q % KC) * 8;
     }
 
-    float ra[MR][8];
-    float rb_f[2][8];
-    uint4 rb_h[2];
+    float ra[CA][8];
+    float rb_f[CB][8];
+    uint4 rb_h[CB];
 
     auto load_tile = [&](int k0) {
 #pragma unroll
-        for (int c = 0; c < MR; ++c) {
+        for (int c = 0; c < CA; ++c) {
             const int k = k0 + a_kc[c];
             bool ok = ga[c].valid && k < p.K;
             const int ch = a_ch[c];
@@ -140,8 +152,7 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(mtts_conv_gemm_args
                 irow = ga[c].in_u + tap_off(p, a_j[c]);
                 ok = irow >= 0 && irow < p.Ti;
             }
-            // advance (tap, channel) to the next K step (cin >= 8; loop runs <= 4 times for cin 8)
-            a_ch[c] += kBK;
+            a_ch[c] += KB;  // advance (tap, channel) to the next K step
             while (a_ch[c] >= p.cin) { a_ch[c] -= p.cin; ++a_j[c]; }
             if (ok) {
                 const size_t r = (size_t)(ga[c].in_base + irow);
@@ -156,10 +167,10 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(mtts_conv_gemm_args
             }
         }
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
+        for (int c = 0; c < CB; ++c) {
             const int n = n0 + b_row[c];
             const int k = k0 + b_kc[c];
-            const bool ok = n < p.N && k < p.Kp;
+            const bool ok = b_on[c] && n < p.N && k < p.Kp;
             if constexpr (BF16) {
                 if (ok)
                     rb_h[c] = *reinterpret_cast<const uint4 *>(static_cast<const uint16_t *>(p.W) +
@@ -183,7 +194,8 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(mtts_conv_gemm_args
 
     auto store_tile = [&](int buf) {
 #pragma unroll
-        for (int c = 0; c < MR; ++c) {
+        for (int c = 0; c < CA; ++c) {
+            if (!a_on[c]) continue;
             ST *dst = &As[buf][a_row[c] * LDK + a_kc[c]];
             if constexpr (BF16) {
                 uint4 w;
@@ -198,7 +210,8 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(mtts_conv_gemm_args
             }
         }
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
+        for (int c = 0; c < CB; ++c) {
+            if (!b_on[c]) continue;
             ST *dst = &Bs[buf][b_row[c] * LDK + b_kc[c]];
             if constexpr (BF16) {
                 *reinterpret_cast<uint4 *>(dst) = rb_h[c];
@@ -209,11 +222,11 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(mtts_conv_gemm_args
         }
     };
 
-    f32x16 acc[MR][2];
+    f32x16 acc[TM][TN];
 #pragma unroll
-    for (int i = 0; i < MR; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
@@ -221,34 +234,34 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(mtts_conv_gemm_args
     auto compute = [&](int buf) {
         if constexpr (BF16) {
 #pragma unroll
-            for (int ks = 0; ks < kBK / 16; ++ks) {
-                bf16x8 af[MR], bfr[2];
+            for (int ks = 0; ks < KB / 16; ++ks) {
+                bf16x8 af[TM], bfr[TN];
 #pragma unroll
-                for (int i = 0; i < MR; ++i)
+                for (int i = 0; i < TM; ++i)
                     af[i] = *reinterpret_cast<const bf16x8 *>(
-                        &As[buf][(wr * 32 * MR + i * 32 + lr) * LDK + ks * 16 + 8 * lh]);
+                        &As[buf][(wr * 32 * TM + i * 32 + lr) * LDK + ks * 16 + 8 * lh]);
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
+                for (int j = 0; j < TN; ++j)
                     bfr[j] = *reinterpret_cast<const bf16x8 *>(
-                        &Bs[buf][(wc * 64 + j * 32 + lr) * LDK + ks * 16 + 8 * lh]);
+                        &Bs[buf][(wc * 32 * TN + j * 32 + lr) * LDK + ks * 16 + 8 * lh]);
 #pragma unroll
-                for (int i = 0; i < MR; ++i)
+                for (int i = 0; i < TM; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j)
+                    for (int j = 0; j < TN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
             }
         } else {
 #pragma unroll
             for (int ks = 0; ks < kBK / 2; ++ks) {
-                float af[MR], bfr[2];
+                float af[TM], bfr[TN];
 #pragma unroll
-                for (int i = 0; i < MR; ++i) af[i] = As[buf][(wr * 32 * MR + i * 32 + lr) * LDK + ks * 2 + lh];
+                for (int i = 0; i < TM; ++i) af[i] = As[buf][(wr * 32 * TM + i * 32 + lr) * LDK + ks * 2 + lh];
 #pragma unroll
-                for (int j = 0; j < 2; ++j) bfr[j] = Bs[buf][(wc * 64 + j * 32 + lr) * LDK + ks * 2 + lh];
+                for (int j = 0; j < TN; ++j) bfr[j] = Bs[buf][(wc * 32 * TN + j * 32 + lr) * LDK + ks * 2 + lh];
 #pragma unroll
-                for (int i = 0; i < MR; ++i)
+                for (int i = 0; i < TM; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j)
+                    for (int j = 0; j < TN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
             }
         }
@@ -259,7 +272,7 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(mtts_conv_gemm_args
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const bool more = kt + 1 < nk;
-        if (more) load_tile((kt + 1) * kBK);
+        if (more) load_tile((kt + 1) * KB);
         compute(kt & 1);
         if (more) store_tile((kt + 1) & 1);
         __syncthreads();
@@ -272,18 +285,18 @@ __global__ __launch_bounds__(kThreads) void conv_gemm_kernel(mtts_conv_gemm_args
         s1 = p.seed[1];
     }
 #pragma unroll
-    for (int i = 0; i < MR; ++i) {
+    for (int i = 0; i < TM; ++i) {
         int crows[16];  // output row of each accumulator register (-1: past M)
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
-            const int m = m0 + wr * 32 * MR + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * lh;
+            const int m = m0 + wr * 32 * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * lh;
             int b, u;
             divmod_fast(m, p.To, inv_to, b, u);
             crows[v] = m < M ? b * p.To_full + u * p.out_stride + p.out_off : -1;
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int n = n0 + wc * 64 + j * 32 + lr;
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wc * 32 * TN + j * 32 + lr;
             if (n >= p.N) continue;
             const float bn = p.bias ? p.bias[n] : 0.f;
 #pragma unroll
@@ -513,7 +526,62 @@ int check_gather(const void *A, int lda, int cin, int ntaps, int K) {
 
 }  // namespace
 
-extern "C" int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream) {
+// Tile configurations: {WM, WN, TM, TN} -> BM x BN = 32*WM*TM x 32*WN*TN, 64*WM*WN threads.
+struct TileCfg {
+    int wm, wn, tm, tn, kb;
+};
+constexpr TileCfg kCfgs[] = {
+    {2, 2, 1, 2, 32},  // 0: 64 x 128, 256 thr (round-1 default)
+    {2, 2, 2, 2, 32},  // 1: 128 x 128, 256 thr
+    {1, 2, 1, 1, 32},  // 2: 32 x 64, 128 thr
+    {2, 2, 1, 1, 32},  // 3: 64 x 64, 256 thr
+    {1, 4, 1, 2, 32},  // 4: 32 x 256, 256 thr
+    {2, 4, 1, 2, 32},  // 5: 64 x 256, 512 thr
+    {1, 2, 1, 2, 32},  // 6: 32 x 128, 128 thr
+    {1, 4, 1, 1, 32},  // 7: 32 x 128, 256 thr (one 32x32 tile per wave)
+    {1, 4, 1, 1, 64},  // 8: config 7 with 64-wide K steps (bf16)
+    {2, 4, 1, 2, 64},  // 9: config 5 with 64-wide K steps (bf16)
+    {2, 2, 1, 2, 64},  // 10: config 0 with 64-wide K steps (bf16)
+};
+constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+
+template <bool BF16, int C>
+static void launch_cfg(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    constexpr TileCfg c = kCfgs[C];
+    constexpr int BM = 32 * c.wm * c.tm, BN = 32 * c.wn * c.tn;
+    dim3 grid((M + BM - 1) / BM, (p.N + BN - 1) / BN);
+    hipLaunchKernelGGL((conv_gemm_kernel<BF16, c.wm, c.wn, c.tm, c.tn, (BF16 ? c.kb : kBK)>), grid,
+                       dim3(64 * c.wm * c.wn), 0, st, p);
+}
+
+template <bool BF16>
+static void launch_by_id(int id, const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    switch (id) {
+        case 0: launch_cfg<BF16, 0>(p, M, st); break;
+        case 1: launch_cfg<BF16, 1>(p, M, st); break;
+        case 2: launch_cfg<BF16, 2>(p, M, st); break;
+        case 3: launch_cfg<BF16, 3>(p, M, st); break;
+        case 4: launch_cfg<BF16, 4>(p, M, st); break;
+        case 5: launch_cfg<BF16, 5>(p, M, st); break;
+        case 6: launch_cfg<BF16, 6>(p, M, st); break;
+        case 7: launch_cfg<BF16, 7>(p, M, st); break;
+        case 8: launch_cfg<BF16, 8>(p, M, st); break;
+        case 9: launch_cfg<BF16, 9>(p, M, st); break;
+        default: launch_cfg<BF16, 10>(p, M, st); break;
+    }
+}
+
+// From the tile sweep on the train step's shapes (tools/gemm_sweep.py, profiles/r01/gemm_sweep_bf16.log):
+// 32 x 128 tiles (config 7) are best or within 10% everywhere; when that grid is small (<= 3 blocks
+// per CU: half-resolution and narrow GEMMs) the same tile with 64-wide K steps (config 8) is 10-35%
+// faster because each block then waits on half as many global round trips.
+static int pick_cfg(const mtts_conv_gemm_args &p, int M, bool bf16) {
+    if (!bf16) return 7;
+    const long blocks = (long)((M + 31) / 32) * ((p.N + 127) / 128);
+    return blocks <= 768 ? 8 : 7;
+}
+
+static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, int cfg, void *hip_stream) {
     MTTS_CHECK_ARG(args != nullptr, "conv_gemm: args is null");
     const mtts_conv_gemm_args &p = *args;
     int rc = check_gather(p.A, p.lda, p.cin, p.ntaps, p.K);
@@ -525,23 +593,30 @@ extern "C" int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision
     MTTS_CHECK_ARG(p.act >= MTTS_ACT_NONE && p.act <= MTTS_ACT_DGELU, "conv_gemm: bad act");
     MTTS_CHECK_ARG(p.act != MTTS_ACT_DGELU || p.aux, "conv_gemm: MTTS_ACT_DGELU needs aux");
     MTTS_CHECK_ARG(p.dropout_p <= 0.f || (p.seed && p.dropout_p < 1.f), "conv_gemm: dropout needs a seed pointer");
+    MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || cfg == MTTS_GEMM_PANEL, "conv_gemm: bad tile config");
     const int M = p.nb * p.To;
     if (M == 0) return MTTS_OK;
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
     const bool bf16 = precision == MTTS_PREC_BF16;
-    const int nblk_n = (p.N + kBN - 1) / kBN;
-    // 128-row tiles when they still give >= 2 blocks per CU, else 64-row tiles
-    const bool big = ((M + 127) / 128) * nblk_n >= 512;
-    if (big) {
-        dim3 grid((M + 127) / 128, nblk_n);
-        if (bf16) hipLaunchKernelGGL((conv_gemm_kernel<true, 2>), grid, dim3(kThreads), 0, st, p);
-        else hipLaunchKernelGGL((conv_gemm_kernel<false, 2>), grid, dim3(kThreads), 0, st, p);
-    } else {
-        dim3 grid((M + 63) / 64, nblk_n);
-        if (bf16) hipLaunchKernelGGL((conv_gemm_kernel<true, 1>), grid, dim3(kThreads), 0, st, p);
-        else hipLaunchKernelGGL((conv_gemm_kernel<false, 1>), grid, dim3(kThreads), 0, st, p);
+    // bf16: the A-resident panel schedule (conv_gemm_panel.hip) when its LDS panel fits
+    if (cfg == MTTS_GEMM_PANEL) {
+        if (!bf16) return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: panel schedule is bf16 only");
+        if (mtts::conv_gemm_panel_launch(p, st) == 0) return mtts::check_launch("conv_gemm_panel_kernel");
+        return mtts::fail(MTTS_ERR_SHAPE, "conv_gemm: panel schedule does not fit");
     }
+    if (cfg < 0) cfg = pick_cfg(p, M, bf16);
+    if (bf16) launch_by_id<true>(cfg, p, M, st);
+    else launch_by_id<false>(cfg, p, M, st);
     return mtts::check_launch("conv_gemm_kernel");
+}
+
+extern "C" int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream) {
+    return conv_gemm_impl(args, precision, -1, hip_stream);
+}
+
+extern "C" int mtts_conv_gemm_tile(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg,
+                                   void *hip_stream) {
+    return conv_gemm_impl(args, precision, tile_cfg, hip_stream);
 }
 
 __global__ void dropout_apply_kernel(const float *__restrict__ x, float *__restrict__ y, int rows, int cols, int ld,
@@ -604,8 +679,9 @@ extern "C" int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precisi
                                                mtts::align_up((size_t)splits * p.N * p.K * 4, 256));
     const int M = p.nb * p.To;
     if (M == 0) {
-        hipMemsetAsync(part, 0, (size_t)p.N * p.K * 4, st);
-        hipMemsetAsync(part_db, 0, (size_t)p.N * 4, st);
+        if (hipMemsetAsync(part, 0, (size_t)p.N * p.K * 4, st) != hipSuccess ||
+            hipMemsetAsync(part_db, 0, (size_t)p.N * 4, st) != hipSuccess)
+            return mtts::fail(MTTS_ERR_HIP, "conv_wgrad: memset failed");
         splits = 1;
     } else {
         dim3 grid((p.N + 127) / 128, (p.K + 127) / 128, splits);

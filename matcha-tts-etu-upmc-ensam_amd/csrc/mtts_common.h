@@ -40,6 +40,12 @@ __device__ __forceinline__ bool dropout_keep(uint32_t seed_lo, uint32_t seed_hi,
 
 }  // namespace mtts
 
+struct mtts_conv_gemm_args;
+namespace mtts {
+// conv_gemm_panel.hip: A-resident bf16 schedule; returns 0 if launched, 1 if it does not apply.
+int conv_gemm_panel_launch(const mtts_conv_gemm_args &p, hipStream_t st);
+}  // namespace mtts
+
 #define MTTS_CHECK_ARG(cond, msg)                                   \
     do {                                                            \
         if (!(cond)) return ::mtts::fail(MTTS_ERR_INVALID_ARG, msg); \

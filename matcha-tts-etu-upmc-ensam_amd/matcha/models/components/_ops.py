@@ -67,6 +67,7 @@ class ConvWgradArgs(ctypes.Structure):
 _P, _I, _F, _SZ, _U = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint32
 _I64 = ctypes.c_int64
 N.register("mtts_conv_gemm", ctypes.c_int, [ctypes.POINTER(ConvGemmArgs), _I, _P])
+N.register("mtts_conv_gemm_tile", ctypes.c_int, [ctypes.POINTER(ConvGemmArgs), _I, _I, _P])
 N.register("mtts_conv_wgrad_workspace_size", _SZ, [ctypes.POINTER(ConvWgradArgs)])
 N.register("mtts_conv_wgrad", ctypes.c_int,
            [ctypes.POINTER(ConvWgradArgs), _I, _P, _I64, _I64, _I64, _P, _I, _P, _SZ, _P])
@@ -116,9 +117,14 @@ def pack_weight(w2d: torch.Tensor, prec: int) -> tuple[torch.Tensor, int]:
     return w.contiguous(), Kp
 
 
+# Per-launch timing for bench.py's roofline leg: when set to a list, every mtts_conv_gemm launch appends
+# (start_event, end_event, algorithmic_flops, precision), events recorded on the launch stream.
+LAUNCH_LOG: list | None = None
+
+
 def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_stride=1, out_off=0, *, prec,
           a_scale=None, bias=None, act=ACT_NONE, residual=None, c_scale=None, C_pre=None, aux=None,
-          dropout_p=0.0, seed=None):
+          dropout_p=0.0, seed=None, tile_cfg=-1):
     args = ConvGemmArgs()
     args.A, args.a_scale, args.lda, args.Ti, args.To, args.nb = A.data_ptr(), N.ptr(a_scale), A.shape[-1], Ti, To, nb
     args.in_stride, args.ntaps, args.cin = in_stride, len(offs), cin
@@ -132,7 +138,15 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     args.C_pre = N.ptr(C_pre)
     args.aux, args.ldaux = N.ptr(aux), (aux.shape[-1] if aux is not None else 0)
     args.dropout_p, args.seed = float(dropout_p), N.ptr(seed)
-    N.check(N.lib().mtts_conv_gemm(ctypes.byref(args), prec, _stream(C)), "mtts_conv_gemm")
+    log = LAUNCH_LOG
+    if log is not None:
+        st = torch.cuda.current_stream(C.device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+    N.check(N.lib().mtts_conv_gemm_tile(ctypes.byref(args), prec, tile_cfg, _stream(C)), "mtts_conv_gemm")
+    if log is not None:
+        e1.record(st)
+        log.append((e0, e1, 2.0 * nb * To * N_ * args.K, prec))
 
 
 def _wgrad(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin, N_, dw, strides, *, prec,

@@ -34,15 +34,20 @@ def test_graph_step_matches_eager_step(precision):
     le = te.step([b]).clone()
     lg = tg.step([b]).clone()
     torch.cuda.synchronize()
-    torch.testing.assert_close(lg, le, rtol=1e-5, atol=1e-6)  # same weights -> same losses
+    # same weights -> same losses.  fp32: 1e-5.  bf16: library kernels outside libmtts (torch SDPA under
+    # autocast, MIOpen encoder convs) may select other algorithms under stream capture, and bf16 rounding
+    # amplifies that; the north-star loss tolerance (1e-4 relative) applies.
+    rtol = 1e-5 if precision == "32-true" else 1e-4
+    torch.testing.assert_close(lg, le, rtol=rtol, atol=1e-6)
     for _ in range(2):
         te.step([b])
         tg.step([b])
     torch.cuda.synchronize()
     # torch's embedding backward (text encoder) accumulates with atomics, and AdamW turns tiny
-    # gradient differences into steps of up to ~lr: compare updates at lr scale
+    # gradient differences into steps of up to ~lr each: a near-zero gradient whose sign differs moves
+    # the two copies apart by at most 2*lr per step -> 3 steps * 2 * 1e-4
     for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
-        assert (p2 - p1).abs().max().item() <= 3e-4, n
+        assert (p2 - p1).abs().max().item() <= 6e-4, n
     p0 = dict(_model().named_parameters())
     moved = [(p1 - p0[n]).abs().max().item() for n, p1 in m1.named_parameters()]
     assert max(moved) > 1e-5  # the optimizer actually stepped
