@@ -130,6 +130,38 @@ int mtts_layernorm_bwd(const float *dy, const float *x, const float *w, const fl
                        float *dx, float *dw, float *db, int32_t M, int32_t C, void *workspace,
                        size_t workspace_bytes, void *hip_stream);
 
+/*
+ * Flash attention of the decoder's transformer blocks (transformer.py:191-370: diffusers Attention,
+ * 4 heads x 64, AttnProcessor2_0 -> F.scaled_dot_product_attention with the FLOAT 0/1 mask, i.e. an
+ * additive per-key bias).  scores[b,h,i,j] = scale * q_i.k_j + key_bias[b,j]; o = softmax(scores) v.
+ * Token-major rows (row = b*T + t), head h at columns [h*D, h*D+D): q/k/v may be column slices of one
+ * fused QKV buffer (shared row stride ldq).  D: a multiple of 8 up to 96 (the decoder uses 64).  lse [B,H,T] receives log2(sum_j 2^(scores*log2 e))
+ * for the backward.  Rows and strides: 16-byte aligned pointers, strides multiples of 4 floats.
+ */
+typedef struct mtts_attn_args {
+    const float *q, *k, *v;
+    int32_t ldq;
+    const float *key_bias; /* [B*T] or NULL (no bias) */
+    float *o;
+    int32_t ldo;
+    float *lse;
+    int32_t B, T, H, D;
+    float scale;
+} mtts_attn_args;
+
+typedef struct mtts_attn_grads {
+    const float *dout; /* dL/do, row stride lddo */
+    int32_t lddo;
+    float *dq, *dk, *dv; /* written (not accumulated), shared row stride ldd */
+    int32_t ldd;
+} mtts_attn_grads;
+
+int mtts_attention_fwd(const mtts_attn_args *args, int32_t precision, void *hip_stream);
+size_t mtts_attention_bwd_workspace_size(int32_t B, int32_t T, int32_t H);
+/* Deterministic backward (no atomics): a dQ pass (also forms rowsum(dO*O)) then a dK/dV pass. */
+int mtts_attention_bwd(const mtts_attn_args *args, const mtts_attn_grads *grads, int32_t precision,
+                       void *workspace, size_t workspace_bytes, void *hip_stream);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

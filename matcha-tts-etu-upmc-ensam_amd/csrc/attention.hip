@@ -1,0 +1,616 @@
+// Flash attention (forward + deterministic backward) for the decoder's transformer blocks on gfx950
+// MFMA.  Reference: transformer.py:191-370 (diffusers Attention, 4 heads x 64; head dims 32/64/96
+// are built) whose mask reaches
+// F.scaled_dot_product_attention as a FLOAT tensor, i.e. an additive per-key bias (the 0/1 mask
+// itself: +1 on valid keys, +0 on padding -- padded keys are NOT excluded).  scores = q.k*scale + bias.
+//
+// Layout: q/k/v/o and their gradients are token-major rows (row = b*T + t) with head h at columns
+// [h*64, h*64+64) -- the fused QKV projection's output is consumed in place, no transposes.
+//
+// Orientation trick.  A 32x32 MFMA tile's C layout gives lane l the column (l & 31) and 16 rows
+// {(v&3) + 8(v>>2) + 4(l>>5)}.  The forward and dQ kernels compute S^T = K Q^T, so a lane owns ONE
+// query and 16 keys of the tile (its partner lane l^32 the other 16): the row softmax is 16 in-lane
+// values + one lane^32 exchange, the online-softmax rescale is a per-lane scalar, and P^T feeds the
+// next MFMA (O^T += V^T P^T) straight from registers because the V^T fragment is read from LDS in the
+// same key order the lane holds.  The dK/dV kernel uses the mirrored orientation (a lane owns one key).
+// Softmax runs in the log2 domain; the saved row statistic is lse2 = log2(sum_j 2^(s2_ij)).
+//
+// Precision: BF16 = bf16 MFMA (32x32x16) operands, fp32 accumulation and softmax (bf16-mixed mode);
+// FP32 = exact-fp32 MFMA (32x32x2) -- the parity mode.  Inputs/outputs are fp32 in HBM either way.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <type_traits>
+
+#include "mtts_common.h"
+#include "mtts_decoder.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kTile = 64;           // keys (fwd, dQ) or queries (dKV) per LDS stage
+constexpr int kRowsPerBlock = 128;  // queries (fwd, dQ) or keys (dKV) per block: 4 waves x 32
+constexpr int kThreads = 256;
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr size_t kLdsMax = 160 * 1024;
+
+// Geometry per (precision, compiled head dim D in {32, 64, 96}; a runtime head dim dh <= D runs with
+// zero-filled columns dh..D-1).  Row tiles are [64 rows][D + pad] (fragment
+// reads along the head dim), transposed tiles [D][64 + pad] (fragment reads along the rows).
+template <bool BF16, int D>
+struct G {
+    static_assert(D % 32 == 0 && D <= 96, "head dim 32, 64 or 96");
+    using T = std::conditional_t<BF16, uint16_t, float>;
+    static constexpr int PAD = BF16 ? 8 : 1;  // bf16: 16-byte-aligned rows, conflict-free b128 reads
+    static constexpr int LDR = D + PAD;
+    static constexpr int LDT = kTile + PAD;
+    static constexpr int RE = kTile * LDR;  // elements of a row tile
+    static constexpr int TE = D * LDT;      // elements of a transposed tile
+    static constexpr int NT = D / 32;       // 32-wide MFMA tiles over the head dim
+    static constexpr int F4 = kTile * D / 4 / kThreads;  // float4 per thread to stage one tile
+};
+
+__device__ __forceinline__ uint16_t to_bf16(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+    return (uint32_t)to_bf16(a) | ((uint32_t)to_bf16(b) << 16);
+}
+// bf16 fragments are always assembled from 32-bit words: element-wise construction of bf16 / u16
+// vectors from LDS loads miscompiles here (every element comes back as element 0), like the
+// raw_buffer_load_b64 builtin (toolchain findings).
+__device__ __forceinline__ bf16x8 frag8(const float *e) {
+    const uint4 w = make_uint4(pack2(e[0], e[1]), pack2(e[2], e[3]), pack2(e[4], e[5]), pack2(e[6], e[7]));
+    return __builtin_bit_cast(bf16x8, w);
+}
+
+__device__ __forceinline__ int crow(int v, int lh) { return (v & 3) + 8 * (v >> 2) + 4 * lh; }
+
+// B-operand fragments held in registers for one row (a query or a key) of the lane: the row's D
+// dims in MFMA k-step order.
+template <bool BF16, int D>
+struct RowFrag;
+template <int D>
+struct RowFrag<true, D> {
+    bf16x8 f[D / 16];
+    __device__ void load(const float *row, bool ok, int lh, int dh) {
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) {
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+            const int c = 16 * ks + 8 * lh;
+            if (ok && c < dh) a = *reinterpret_cast<const float4 *>(row + c);
+            if (ok && c + 4 < dh) b = *reinterpret_cast<const float4 *>(row + c + 4);
+            const float e[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            f[ks] = frag8(e);
+        }
+    }
+};
+template <int D>
+struct RowFrag<false, D> {
+    float f[D / 2];
+    __device__ void load(const float *row, bool ok, int lh, int dh) {
+#pragma unroll
+        for (int ks = 0; ks < D / 2; ++ks) f[ks] = (ok && 2 * ks + lh < dh) ? row[2 * ks + lh] : 0.f;
+    }
+};
+
+// acc += A(LDS row tile, row r, contiguous over the head dim) x B(register row fragment)
+template <bool BF16, int D>
+__device__ __forceinline__ void mma_rows(f32x16 &acc, const typename G<BF16, D>::T *tile, int r, int lh,
+                                         const RowFrag<BF16, D> &bf) {
+    constexpr int LD = G<BF16, D>::LDR;
+    if constexpr (BF16) {
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) {
+            const bf16x8 a = *reinterpret_cast<const bf16x8 *>(tile + r * LD + 16 * ks + 8 * lh);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bf.f[ks], acc, 0, 0, 0);
+        }
+    } else {
+#pragma unroll
+        for (int ks = 0; ks < D / 2; ++ks)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(tile[r * LD + 2 * ks + lh], bf.f[ks], acc, 0, 0, 0);
+    }
+}
+
+// acc += A(LDS transposed tile: row = head dim d, columns = the 32 rows of sub-tile `sub`, read in
+// the C-layout order this lane holds) x B(the lane's 16 C-layout values `s`)
+template <bool BF16, int D>
+__device__ __forceinline__ void mma_perm(f32x16 &acc, const typename G<BF16, D>::T *tileT, int d, int sub, int lh,
+                                         const float (&s)[16]) {
+    constexpr int LD = G<BF16, D>::LDT;
+    if constexpr (BF16) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int c0 = sub * 32 + 16 * ks + 4 * lh;
+            const uint2 lo = *reinterpret_cast<const uint2 *>(tileT + d * LD + c0);
+            const uint2 hi = *reinterpret_cast<const uint2 *>(tileT + d * LD + c0 + 8);
+            const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+            const bf16x8 b = frag8(s + 8 * ks);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+        }
+    } else {
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(tileT[d * LD + sub * 32 + crow(v, lh)], s[v], acc, 0, 0, 0);
+    }
+}
+
+// Staging of a 64-row tile of one head (rows r0.. of batch b) into LDS: row layout and/or transposed.
+// Rows >= T are zero.
+template <bool BF16, int D>
+struct TileLoader {
+    using Gm = G<BF16, D>;
+    float4 v[Gm::F4];
+    __device__ void load(const float *base, int ld, int b, int T, int r0, int tid, int dh) {
+#pragma unroll
+        for (int i = 0; i < Gm::F4; ++i) {
+            const int idx = tid + kThreads * i;
+            const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
+            v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r0 + r < T && c < dh) v[i] = *reinterpret_cast<const float4 *>(base + ((size_t)b * T + r0 + r) * ld + c);
+        }
+    }
+    __device__ void store(typename Gm::T *rowt, typename Gm::T *trt, int tid) const {
+#pragma unroll
+        for (int i = 0; i < Gm::F4; ++i) {
+            const int idx = tid + kThreads * i;
+            const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
+            const float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+            if constexpr (BF16) {
+                if (rowt)
+                    *reinterpret_cast<uint2 *>(rowt + r * Gm::LDR + c) = make_uint2(pack2(e[0], e[1]), pack2(e[2], e[3]));
+                if (trt) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) trt[(c + j) * Gm::LDT + r] = to_bf16(e[j]);
+                }
+            } else {
+                if (rowt) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) rowt[r * Gm::LDR + c + j] = e[j];
+                }
+                if (trt) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) trt[(c + j) * Gm::LDT + r] = e[j];
+                }
+            }
+        }
+    }
+};
+
+// LDS bytes per stage; kernels double-buffer when two stages fit in 160 KB, else single-buffer.
+template <bool BF16, int D>
+constexpr size_t fwd_stage() {  // K rows + V transposed + bias
+    return (size_t)(G<BF16, D>::RE + G<BF16, D>::TE) * sizeof(typename G<BF16, D>::T) + kTile * sizeof(float);
+}
+template <bool BF16, int D>
+constexpr size_t dq_stage() {  // K rows + V rows + K transposed + bias
+    return (size_t)(2 * G<BF16, D>::RE + G<BF16, D>::TE) * sizeof(typename G<BF16, D>::T) + kTile * sizeof(float);
+}
+template <bool BF16, int D>
+constexpr size_t dkv_stage() {  // Q rows + dO rows + Q transposed + dO transposed + lse + Drow
+    return (size_t)(2 * G<BF16, D>::RE + 2 * G<BF16, D>::TE) * sizeof(typename G<BF16, D>::T) +
+           2 * kTile * sizeof(float);
+}
+constexpr int nbuf(size_t stage) { return 2 * stage <= kLdsMax ? 2 : 1; }
+
+template <typename T>
+__device__ __forceinline__ T *carve(unsigned char *&p, size_t n) {
+    T *r = reinterpret_cast<T *>(p);
+    p += (n * sizeof(T) + 15) / 16 * 16;
+    return r;
+}
+
+// The shared K-tile loop: stage 0, then per tile prefetch the next into registers, compute, and
+// publish it (double buffer: into the other stage, one barrier; single buffer: two barriers).
+template <int NB, typename Load, typename Store, typename Compute>
+__device__ __forceinline__ void tile_loop(int ntiles, Load &&load, Store &&store, Compute &&compute) {
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int it = 0; it < ntiles; ++it) {
+        const int buf = NB == 2 ? (it & 1) : 0;
+        const bool more = it + 1 < ntiles;
+        if (more) load((it + 1) * kTile);
+        compute(buf);
+        if constexpr (NB == 2) {
+            if (more) store(buf ^ 1);
+            __syncthreads();
+        } else {
+            __syncthreads();
+            if (more) {
+                store(0);
+                __syncthreads();
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward: grid (ceil(T/128), H, B); lane = query
+template <bool BF16, int D>
+__global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
+    using Gm = G<BF16, D>;
+    using ST = typename Gm::T;
+    constexpr int NB = nbuf(fwd_stage<BF16, D>());
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char *sp = smem;
+    ST *Ks = carve<ST>(sp, NB * Gm::RE);  // [NB][64 keys][LDR]
+    ST *Vt = carve<ST>(sp, NB * Gm::TE);  // [NB][D][LDT] (V transposed)
+    float *bias_s = carve<float>(sp, NB * kTile);  // log2 domain; -inf past T
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
+    const int q = blockIdx.x * kRowsPerBlock + wave * 32 + lr;
+    const bool q_ok = q < T;
+    const float *Kb = p.k + h * dh, *Vb = p.v + h * dh;
+
+    RowFrag<BF16, D> qf;
+    qf.load(p.q + h * dh + ((size_t)b * T + (q_ok ? q : 0)) * p.ldq, q_ok, lh, dh);
+    const float sl2 = p.scale * kLog2e;
+
+    f32x16 acc[Gm::NT];
+#pragma unroll
+    for (int t = 0; t < Gm::NT; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
+    float m = -INFINITY, l = 0.f;
+
+    TileLoader<BF16, D> lk, lv;
+    float bias_r = 0.f;
+    auto load = [&](int k0) {
+        lk.load(Kb, p.ldq, b, T, k0, tid, dh);
+        lv.load(Vb, p.ldq, b, T, k0, tid, dh);
+        if (tid < kTile) {
+            const int key = k0 + tid;
+            bias_r = key < T ? (p.key_bias ? p.key_bias[(size_t)b * T + key] * kLog2e : 0.f) : -INFINITY;
+        }
+    };
+    auto store = [&](int buf) {
+        lk.store(Ks + buf * Gm::RE, nullptr, tid);
+        lv.store(nullptr, Vt + buf * Gm::TE, tid);
+        if (tid < kTile) bias_s[buf * kTile + tid] = bias_r;
+    };
+    auto compute = [&](int buf) {
+        const ST *K_ = Ks + buf * Gm::RE, *V_ = Vt + buf * Gm::TE;
+        const float *bs = bias_s + buf * kTile;
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+            f32x16 sacc;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) sacc[v] = 0.f;
+            mma_rows<BF16, D>(sacc, K_, sub * 32 + lr, lh, qf);  // S^T: rows = keys, col = this lane's query
+            float s[16], mx = -INFINITY;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                s[v] = sacc[v] * sl2 + bs[sub * 32 + crow(v, lh)];
+                mx = fmaxf(mx, s[v]);
+            }
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            const float m_new = fmaxf(m, mx);
+            const float corr = exp2f(m - m_new);  // m = -inf on the first tile -> 0
+            float rs = 0.f;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                s[v] = exp2f(s[v] - m_new);
+                rs += s[v];
+            }
+            rs += __shfl_xor(rs, 32);
+            l = l * corr + rs;
+            m = m_new;
+#pragma unroll
+            for (int t = 0; t < Gm::NT; ++t) {
+#pragma unroll
+                for (int v = 0; v < 16; ++v) acc[t][v] *= corr;
+                mma_perm<BF16, D>(acc[t], V_, t * 32 + lr, sub, lh, s);  // O^T += V^T P^T
+            }
+        }
+    };
+    tile_loop<NB>((T + kTile - 1) / kTile, load, store, compute);
+
+    if (q_ok) {
+        const float inv = 1.f / l;
+        float *orow = p.o + ((size_t)b * T + q) * p.ldo + h * dh;
+#pragma unroll
+        for (int t = 0; t < Gm::NT; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                if (t * 32 + 8 * g + 4 * lh < dh)
+                *reinterpret_cast<float4 *>(orow + t * 32 + 8 * g + 4 * lh) =
+                    make_float4(acc[t][4 * g] * inv, acc[t][4 * g + 1] * inv, acc[t][4 * g + 2] * inv,
+                                acc[t][4 * g + 3] * inv);
+        if (lh == 0) p.lse[((size_t)b * p.H + h) * T + q] = m + log2f(l);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward, dQ: grid (ceil(T/128), H, B); lane = query.  Also writes Drow = rowsum(dO * O) for dKV.
+template <bool BF16, int D>
+__global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p, mtts_attn_grads g, float *Drow) {
+    using Gm = G<BF16, D>;
+    using ST = typename Gm::T;
+    constexpr int NB = nbuf(dq_stage<BF16, D>());
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char *sp = smem;
+    ST *Ks = carve<ST>(sp, NB * Gm::RE);
+    ST *Vs = carve<ST>(sp, NB * Gm::RE);
+    ST *Kt = carve<ST>(sp, NB * Gm::TE);
+    float *bias_s = carve<float>(sp, NB * kTile);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
+    const int q = blockIdx.x * kRowsPerBlock + wave * 32 + lr;
+    const bool q_ok = q < T;
+    const size_t qrow = (size_t)b * T + (q_ok ? q : 0);
+    const float *Kb = p.k + h * dh, *Vb = p.v + h * dh;
+
+    RowFrag<BF16, D> qf, gf;
+    qf.load(p.q + h * dh + qrow * p.ldq, q_ok, lh, dh);
+    gf.load(g.dout + h * dh + qrow * g.lddo, q_ok, lh, dh);
+    // Drow[q] = sum_d dO[q,d] * O[q,d]: each half-wave lane sums D/2 dims
+    float dsum = 0.f;
+    if (q_ok) {
+        const float *orow = p.o + qrow * p.ldo + h * dh + (D / 2) * lh;
+        const float *grow = g.dout + qrow * g.lddo + h * dh + (D / 2) * lh;
+#pragma unroll
+        for (int i = 0; i < D / 2; i += 4) {
+            if ((D / 2) * lh + i >= dh) break;
+            const float4 a = *reinterpret_cast<const float4 *>(orow + i);
+            const float4 c = *reinterpret_cast<const float4 *>(grow + i);
+            dsum += a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
+        }
+    }
+    dsum += __shfl_xor(dsum, 32);
+    const size_t srow = ((size_t)b * p.H + h) * T + (q_ok ? q : 0);
+    const float lse2 = q_ok ? p.lse[srow] : 0.f;
+    if (q_ok && lh == 0) Drow[srow] = dsum;
+    const float sl2 = p.scale * kLog2e;
+
+    f32x16 acc[Gm::NT];
+#pragma unroll
+    for (int t = 0; t < Gm::NT; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
+
+    TileLoader<BF16, D> lk, lv;
+    float bias_r = 0.f;
+    auto load = [&](int k0) {
+        lk.load(Kb, p.ldq, b, T, k0, tid, dh);
+        lv.load(Vb, p.ldq, b, T, k0, tid, dh);
+        if (tid < kTile) {
+            const int key = k0 + tid;
+            bias_r = key < T ? (p.key_bias ? p.key_bias[(size_t)b * T + key] * kLog2e : 0.f) : -INFINITY;
+        }
+    };
+    auto store = [&](int buf) {
+        lk.store(Ks + buf * Gm::RE, Kt + buf * Gm::TE, tid);
+        lv.store(Vs + buf * Gm::RE, nullptr, tid);
+        if (tid < kTile) bias_s[buf * kTile + tid] = bias_r;
+    };
+    auto compute = [&](int buf) {
+        const ST *K_ = Ks + buf * Gm::RE, *V_ = Vs + buf * Gm::RE, *KT_ = Kt + buf * Gm::TE;
+        const float *bs = bias_s + buf * kTile;
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+            f32x16 sacc, pacc;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) sacc[v] = pacc[v] = 0.f;
+            mma_rows<BF16, D>(sacc, K_, sub * 32 + lr, lh, qf);  // S^T
+            mma_rows<BF16, D>(pacc, V_, sub * 32 + lr, lh, gf);  // dP^T = V dO^T
+            float ds[16];
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const float pr = exp2f(sacc[v] * sl2 + bs[sub * 32 + crow(v, lh)] - lse2);
+                ds[v] = pr * (pacc[v] - dsum);
+            }
+#pragma unroll
+            for (int t = 0; t < Gm::NT; ++t) mma_perm<BF16, D>(acc[t], KT_, t * 32 + lr, sub, lh, ds);  // dQ^T += K^T dS^T
+        }
+    };
+    tile_loop<NB>((T + kTile - 1) / kTile, load, store, compute);
+
+    if (q_ok) {
+        float *drow = g.dq + ((size_t)b * T + q) * g.ldd + h * dh;
+        const float sc = p.scale;
+#pragma unroll
+        for (int t = 0; t < Gm::NT; ++t)
+#pragma unroll
+            for (int gi = 0; gi < 4; ++gi)
+                if (t * 32 + 8 * gi + 4 * lh < dh)
+                *reinterpret_cast<float4 *>(drow + t * 32 + 8 * gi + 4 * lh) =
+                    make_float4(acc[t][4 * gi] * sc, acc[t][4 * gi + 1] * sc, acc[t][4 * gi + 2] * sc,
+                                acc[t][4 * gi + 3] * sc);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward, dK/dV: grid (ceil(T/128), H, B); lane = key.  C layout: rows = queries, col = key.
+template <bool BF16, int D>
+__global__ __launch_bounds__(kThreads) void attn_bwd_dkv_kernel(mtts_attn_args p, mtts_attn_grads g,
+                                                                const float *Drow) {
+    using Gm = G<BF16, D>;
+    using ST = typename Gm::T;
+    constexpr int NB = nbuf(dkv_stage<BF16, D>());
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char *sp = smem;
+    ST *Qs = carve<ST>(sp, NB * Gm::RE);
+    ST *Gs = carve<ST>(sp, NB * Gm::RE);  // dO rows
+    ST *Qt = carve<ST>(sp, NB * Gm::TE);
+    ST *Gt = carve<ST>(sp, NB * Gm::TE);  // dO transposed
+    float *lse_s = carve<float>(sp, NB * kTile);  // +inf past T
+    float *d_s = carve<float>(sp, NB * kTile);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
+    const int key = blockIdx.x * kRowsPerBlock + wave * 32 + lr;
+    const bool k_ok = key < T;
+    const size_t krow = (size_t)b * T + (k_ok ? key : 0);
+
+    RowFrag<BF16, D> kf, vf;
+    kf.load(p.k + h * dh + krow * p.ldq, k_ok, lh, dh);
+    vf.load(p.v + h * dh + krow * p.ldq, k_ok, lh, dh);
+    const float sl2 = p.scale * kLog2e;
+    const float bias2 = (k_ok && p.key_bias) ? p.key_bias[krow] * kLog2e : 0.f;
+    const float *Qb = p.q + h * dh, *Gb = g.dout + h * dh;
+    const size_t sbase = ((size_t)b * p.H + h) * T;
+
+    f32x16 dk[Gm::NT], dv[Gm::NT];
+#pragma unroll
+    for (int t = 0; t < Gm::NT; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) dk[t][v] = dv[t][v] = 0.f;
+
+    TileLoader<BF16, D> lq, lg;
+    float lse_r = 0.f, d_r = 0.f;
+    auto load = [&](int q0) {
+        lq.load(Qb, p.ldq, b, T, q0, tid, dh);
+        lg.load(Gb, g.lddo, b, T, q0, tid, dh);
+        if (tid < kTile) {
+            const int qq = q0 + tid;
+            lse_r = qq < T ? p.lse[sbase + qq] : INFINITY;
+            d_r = qq < T ? Drow[sbase + qq] : 0.f;
+        }
+    };
+    auto store = [&](int buf) {
+        lq.store(Qs + buf * Gm::RE, Qt + buf * Gm::TE, tid);
+        lg.store(Gs + buf * Gm::RE, Gt + buf * Gm::TE, tid);
+        if (tid < kTile) {
+            lse_s[buf * kTile + tid] = lse_r;
+            d_s[buf * kTile + tid] = d_r;
+        }
+    };
+    auto compute = [&](int buf) {
+        const ST *Q_ = Qs + buf * Gm::RE, *G_ = Gs + buf * Gm::RE, *QT_ = Qt + buf * Gm::TE, *GT_ = Gt + buf * Gm::TE;
+        const float *ls = lse_s + buf * kTile, *dd = d_s + buf * kTile;
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+            f32x16 sacc, pacc;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) sacc[v] = pacc[v] = 0.f;
+            mma_rows<BF16, D>(sacc, Q_, sub * 32 + lr, lh, kf);  // S = Q K^T (rows q, col = this key)
+            mma_rows<BF16, D>(pacc, G_, sub * 32 + lr, lh, vf);  // dP = dO V^T
+            float pr[16], ds[16];
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int qi = sub * 32 + crow(v, lh);
+                pr[v] = exp2f(sacc[v] * sl2 + bias2 - ls[qi]);
+                ds[v] = pr[v] * (pacc[v] - dd[qi]);
+            }
+#pragma unroll
+            for (int t = 0; t < Gm::NT; ++t) {
+                mma_perm<BF16, D>(dv[t], GT_, t * 32 + lr, sub, lh, pr);  // dV^T += dO^T P
+                mma_perm<BF16, D>(dk[t], QT_, t * 32 + lr, sub, lh, ds);  // dK^T += Q^T dS
+            }
+        }
+    };
+    tile_loop<NB>((T + kTile - 1) / kTile, load, store, compute);
+
+    if (k_ok) {
+        float *dkr = g.dk + krow * g.ldd + h * dh;
+        float *dvr = g.dv + krow * g.ldd + h * dh;
+        const float sc = p.scale;
+#pragma unroll
+        for (int t = 0; t < Gm::NT; ++t)
+#pragma unroll
+            for (int gi = 0; gi < 4; ++gi) {
+                const int c = t * 32 + 8 * gi + 4 * lh;
+                if (c >= dh) continue;
+                *reinterpret_cast<float4 *>(dkr + c) = make_float4(dk[t][4 * gi] * sc, dk[t][4 * gi + 1] * sc,
+                                                                   dk[t][4 * gi + 2] * sc, dk[t][4 * gi + 3] * sc);
+                *reinterpret_cast<float4 *>(dvr + c) =
+                    make_float4(dv[t][4 * gi], dv[t][4 * gi + 1], dv[t][4 * gi + 2], dv[t][4 * gi + 3]);
+            }
+    }
+}
+
+constexpr size_t lds_bytes(size_t stage) { return nbuf(stage) * (stage + 64); }  // + carve alignment slack
+
+template <typename K>
+bool set_lds(K kernel, size_t bytes) {
+    if (bytes <= 64 * 1024) return true;
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bytes) == hipSuccess;
+}
+
+bool aligned16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
+
+int check_args(const mtts_attn_args *p, int precision) {
+    MTTS_CHECK_ARG(p, "attention: null args");
+    MTTS_CHECK_ARG(precision == MTTS_PREC_FP32 || precision == MTTS_PREC_BF16, "attention: bad precision");
+    MTTS_CHECK_ARG(p->D >= 8 && p->D <= 96 && p->D % 8 == 0, "attention: head dim must be a multiple of 8 in [8, 96]");
+    MTTS_CHECK_ARG(p->B >= 0 && p->T >= 0 && p->H >= 1, "attention: bad shape");
+    MTTS_CHECK_ARG(p->q && p->k && p->v && p->o && p->lse, "attention: null tensor");
+    MTTS_CHECK_ARG(p->ldq % 4 == 0 && p->ldo % 4 == 0 && p->ldq >= p->H * p->D && p->ldo >= p->H * p->D,
+                   "attention: row strides must be multiples of 4 and cover H*D");
+    MTTS_CHECK_ARG(aligned16(p->q) && aligned16(p->k) && aligned16(p->v) && aligned16(p->o),
+                   "attention: q/k/v/o must be 16-byte aligned");
+    MTTS_CHECK_ARG(p->scale > 0.f, "attention: scale must be positive");
+    return MTTS_OK;
+}
+
+template <bool BF16, int D>
+int fwd_launch(const mtts_attn_args &p, hipStream_t st) {
+    constexpr size_t lds = lds_bytes(fwd_stage<BF16, D>());
+    static_assert(lds <= kLdsMax, "attention fwd LDS");
+    if (!set_lds(attn_fwd_kernel<BF16, D>, lds)) return mtts::fail(MTTS_ERR_HIP, "attention: LDS attribute");
+    dim3 grid((p.T + kRowsPerBlock - 1) / kRowsPerBlock, p.H, p.B);
+    hipLaunchKernelGGL((attn_fwd_kernel<BF16, D>), grid, dim3(kThreads), lds, st, p);
+    return mtts::check_launch("attn_fwd_kernel");
+}
+
+template <bool BF16, int D>
+int bwd_launch(const mtts_attn_args &p, const mtts_attn_grads &g, float *Drow, hipStream_t st) {
+    constexpr size_t lq = lds_bytes(dq_stage<BF16, D>()), lkv = lds_bytes(dkv_stage<BF16, D>());
+    static_assert(lq <= kLdsMax && lkv <= kLdsMax, "attention bwd LDS");
+    if (!set_lds(attn_bwd_dq_kernel<BF16, D>, lq) || !set_lds(attn_bwd_dkv_kernel<BF16, D>, lkv))
+        return mtts::fail(MTTS_ERR_HIP, "attention_bwd: LDS attribute");
+    dim3 grid((p.T + kRowsPerBlock - 1) / kRowsPerBlock, p.H, p.B);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<BF16, D>), grid, dim3(kThreads), lq, st, p, g, Drow);
+    if (int rc = mtts::check_launch("attn_bwd_dq_kernel")) return rc;
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<BF16, D>), grid, dim3(kThreads), lkv, st, p, g, (const float *)Drow);
+    return mtts::check_launch("attn_bwd_dkv_kernel");
+}
+
+template <bool BF16>
+int fwd_dispatch(const mtts_attn_args &p, hipStream_t st) {
+    return p.D <= 32 ? fwd_launch<BF16, 32>(p, st) : p.D <= 64 ? fwd_launch<BF16, 64>(p, st) : fwd_launch<BF16, 96>(p, st);
+}
+template <bool BF16>
+int bwd_dispatch(const mtts_attn_args &p, const mtts_attn_grads &g, float *Drow, hipStream_t st) {
+    return p.D <= 32   ? bwd_launch<BF16, 32>(p, g, Drow, st)
+           : p.D <= 64 ? bwd_launch<BF16, 64>(p, g, Drow, st)
+                       : bwd_launch<BF16, 96>(p, g, Drow, st);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mtts_attention_fwd(const mtts_attn_args *p, int32_t precision, void *hip_stream) {
+    if (int rc = check_args(p, precision)) return rc;
+    if (p->B == 0 || p->T == 0) return MTTS_OK;
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+    return precision == MTTS_PREC_BF16 ? fwd_dispatch<true>(*p, st) : fwd_dispatch<false>(*p, st);
+}
+
+size_t mtts_attention_bwd_workspace_size(int32_t B, int32_t T, int32_t H) {
+    return mtts::align_up((size_t)B * H * T * sizeof(float), 256);
+}
+
+int mtts_attention_bwd(const mtts_attn_args *p, const mtts_attn_grads *g, int32_t precision, void *workspace,
+                       size_t workspace_bytes, void *hip_stream) {
+    if (int rc = check_args(p, precision)) return rc;
+    MTTS_CHECK_ARG(g && g->dout && g->dq && g->dk && g->dv, "attention_bwd: null gradient tensor");
+    MTTS_CHECK_ARG(g->lddo % 4 == 0 && g->ldd % 4 == 0 && g->lddo >= p->H * p->D && g->ldd >= p->H * p->D,
+                   "attention_bwd: gradient row strides must be multiples of 4 and cover H*D");
+    MTTS_CHECK_ARG(aligned16(g->dout) && aligned16(g->dq) && aligned16(g->dk) && aligned16(g->dv),
+                   "attention_bwd: gradients must be 16-byte aligned");
+    if (p->B == 0 || p->T == 0) return MTTS_OK;
+    if (workspace_bytes < mtts_attention_bwd_workspace_size(p->B, p->T, p->H) || !workspace)
+        return mtts::fail(MTTS_ERR_WORKSPACE, "attention_bwd: workspace too small");
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+    float *Drow = static_cast<float *>(workspace);
+    return precision == MTTS_PREC_BF16 ? bwd_dispatch<true>(*p, *g, Drow, st) : bwd_dispatch<false>(*p, *g, Drow, st);
+}
+
+}  // extern "C"

@@ -12,7 +12,7 @@ Every operator is a torch.autograd.Function whose forward AND backward run in li
        conv's dgrad is a stride-2 conv)
   group_norm_mish_tm                               -> mtts_gn_mish_fwd / _bwd
   layer_norm_tm                                    -> mtts_layernorm_fwd / _bwd
-  attention_tm                                     -> PyTorch-ROCm SDPA (KERNELS records it; next HIP target)
+  attention_tm                                     -> mtts_attention_fwd / _bwd (flash attention)
 GEMM precision follows the caller: inside a bf16 torch.autocast region the GEMMs use bf16 MFMA with
 fp32 accumulation, otherwise exact-fp32 MFMA (the parity mode).  Activations stay fp32 in HBM.
 Dropout (train mode) is a counter-based mask generated in the GEMM epilogues and regenerated in the
@@ -38,7 +38,7 @@ KERNELS: dict[str, str] = {
     "ff_tm": "mtts_conv_gemm/mtts_conv_wgrad",
     "group_norm_mish_tm": "mtts_gn_mish_fwd/mtts_gn_mish_bwd",
     "layer_norm_tm": "mtts_layernorm_fwd/mtts_layernorm_bwd",
-    "attention_tm": "torch SDPA (PyTorch-ROCm)",
+    "attention_tm": "mtts_attention_fwd/mtts_attention_bwd",
 }
 
 
@@ -64,6 +64,18 @@ class ConvWgradArgs(ctypes.Structure):
                 ("N", ctypes.c_int32), ("K", ctypes.c_int32)]
 
 
+class AttnArgs(ctypes.Structure):
+    _fields_ = [("q", ctypes.c_void_p), ("k", ctypes.c_void_p), ("v", ctypes.c_void_p), ("ldq", ctypes.c_int32),
+                ("key_bias", ctypes.c_void_p), ("o", ctypes.c_void_p), ("ldo", ctypes.c_int32),
+                ("lse", ctypes.c_void_p), ("B", ctypes.c_int32), ("T", ctypes.c_int32), ("H", ctypes.c_int32),
+                ("D", ctypes.c_int32), ("scale", ctypes.c_float)]
+
+
+class AttnGrads(ctypes.Structure):
+    _fields_ = [("dout", ctypes.c_void_p), ("lddo", ctypes.c_int32), ("dq", ctypes.c_void_p),
+                ("dk", ctypes.c_void_p), ("dv", ctypes.c_void_p), ("ldd", ctypes.c_int32)]
+
+
 _P, _I, _F, _SZ, _U = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint32
 _I64 = ctypes.c_int64
 N.register("mtts_conv_gemm", ctypes.c_int, [ctypes.POINTER(ConvGemmArgs), _I, _P])
@@ -79,6 +91,9 @@ N.register("mtts_layernorm_fwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _I, 
 N.register("mtts_layernorm_bwd_workspace_size", _SZ, [_I, _I])
 N.register("mtts_layernorm_bwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P])
 N.register("mtts_dropout_apply", ctypes.c_int, [_P, _P, _I, _I, _I, _F, _P, _P])
+N.register("mtts_attention_fwd", ctypes.c_int, [ctypes.POINTER(AttnArgs), _I, _P])
+N.register("mtts_attention_bwd_workspace_size", _SZ, [_I, _I, _I])
+N.register("mtts_attention_bwd", ctypes.c_int, [ctypes.POINTER(AttnArgs), ctypes.POINTER(AttnGrads), _I, _P, _SZ, _P])
 
 
 # ------------------------------------------------------------------------------------------ helpers
@@ -488,15 +503,59 @@ def ff_tm(x, w1, b1, w2, b2, residual=None, dropout_p: float = 0.0):
     return _FeedForwardTM.apply(x, w1, b1, w2, b2, residual, float(dropout_p))
 
 
-def attention_tm(q, k, v, key_bias, heads: int):
-    """softmax(q k^T / sqrt(d) + key_bias[b, key]) v per head.  q/k/v [B,T,H*d], key_bias [B,T]:
-    the reference's float 0/1 mask is ADDED to the scores (diffusers AttnProcessor2_0 +
-    prepare_attention_mask), so padded keys are down-weighted, not removed."""
-    B, T, C = q.shape
-    d = C // heads
-    qh = q.view(B, T, heads, d).transpose(1, 2)
-    kh = k.view(B, T, heads, d).transpose(1, 2)
-    vh = v.view(B, T, heads, d).transpose(1, 2)
-    bias = key_bias.to(q.dtype)[:, None, None, :].expand(B, heads, T, T)
-    o = F.scaled_dot_product_attention(qh, kh, vh, attn_mask=bias, scale=1.0 / math.sqrt(d))
-    return o.transpose(1, 2).reshape(B, T, C)
+class _AttentionTM(torch.autograd.Function):
+    """Multi-head attention over a fused token-major QKV buffer [B, T, 3C] -> o [B, T, C]."""
+
+    @staticmethod
+    def _args(qkv, bias, o, lse, heads):
+        B, T, C3 = qkv.shape
+        C = C3 // 3
+        a = AttnArgs()
+        base, es = qkv.data_ptr(), qkv.element_size()
+        a.q, a.k, a.v, a.ldq = base, base + C * es, base + 2 * C * es, C3
+        a.key_bias, a.o, a.ldo, a.lse = N.ptr(bias), o.data_ptr(), C, lse.data_ptr()
+        a.B, a.T, a.H, a.D = B, T, heads, C // heads
+        a.scale = 1.0 / math.sqrt(C // heads)
+        return a
+
+    @staticmethod
+    def forward(ctx, qkv, key_bias, heads):
+        _check(qkv, key_bias)
+        prec = gemm_precision()
+        qkv = _f32c(qkv)
+        bias = _f32c(key_bias)
+        B, T, C3 = qkv.shape
+        o = torch.empty(B, T, C3 // 3, device=qkv.device, dtype=torch.float32)
+        lse = torch.empty(B, heads, T, device=qkv.device, dtype=torch.float32)
+        a = _AttentionTM._args(qkv, bias, o, lse, heads)
+        N.check(N.lib().mtts_attention_fwd(ctypes.byref(a), prec, _stream(qkv)), "mtts_attention_fwd")
+        ctx.save_for_backward(qkv, bias, o, lse)
+        ctx.heads, ctx.prec = heads, prec
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, bias, o, lse = ctx.saved_tensors
+        do = _f32c(do)
+        B, T, C3 = qkv.shape
+        C = C3 // 3
+        dqkv = torch.empty_like(qkv)
+        a = _AttentionTM._args(qkv, bias, o, lse, ctx.heads)
+        g = AttnGrads()
+        g.dout, g.lddo = do.data_ptr(), C
+        base, es = dqkv.data_ptr(), dqkv.element_size()
+        g.dq, g.dk, g.dv, g.ldd = base, base + C * es, base + 2 * C * es, C3
+        lib = N.lib()
+        ws = torch.empty(int(lib.mtts_attention_bwd_workspace_size(B, T, ctx.heads)), dtype=torch.uint8,
+                         device=qkv.device)
+        N.check(lib.mtts_attention_bwd(ctypes.byref(a), ctypes.byref(g), ctx.prec, ws.data_ptr(), ws.numel(),
+                                       _stream(qkv)), "mtts_attention_bwd")
+        return dqkv, None, None
+
+
+def attention_tm(qkv, key_bias, heads: int):
+    """softmax(q k^T / sqrt(d) + key_bias[b, key]) v per head, from the fused projection qkv [B,T,3C]
+    (q | k | v column blocks, head h at [h*d, h*d+d) of each); key_bias [B,T].  The reference's float
+    0/1 mask is ADDED to the scores (diffusers AttnProcessor2_0 + prepare_attention_mask),
+    so padded keys are down-weighted, not removed.  Returns o [B, T, C] token-major."""
+    return _AttentionTM.apply(qkv, key_bias, heads)

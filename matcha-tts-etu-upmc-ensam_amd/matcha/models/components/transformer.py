@@ -74,10 +74,8 @@ class Attention(nn.Module):
         return torch.cat([self.to_q.weight, self.to_k.weight, self.to_v.weight], dim=0)
 
     def forward_tm(self, h, key_bias, residual=None):
-        C = self.to_q.weight.shape[0]
-        qkv = O.linear_tm(h, self.qkv_weight(), None)
-        q, k, v = qkv.split(C, dim=-1)
-        o = O.attention_tm(q, k, v, key_bias, self.heads)
+        qkv = O.linear_tm(h, self.qkv_weight(), None)  # [B, T, 3C]: q | k | v
+        o = O.attention_tm(qkv, key_bias, self.heads)
         p = self.to_out[1].p if self.training else 0.0
         return O.linear_tm(o, self.to_out[0].weight, self.to_out[0].bias, residual=residual, dropout_p=p)
 
