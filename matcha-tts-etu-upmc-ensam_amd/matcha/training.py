@@ -9,9 +9,12 @@ baselightningmodule.py:115-162) on one process per GPU.
 
 Two execution modes:
   graph=True (default on GPU): the whole step is captured once into a HIP graph and replayed -- about
-    a thousand kernel launches per step become one graph launch.  Gradients live in ONE flat fp32
-    buffer (every param.grad is a view into it), so data parallelism is a single RCCL all-reduce of
-    that buffer over xGMI between the forward/backward graph and the clip/AdamW graph.  Dropout masks
+    a thousand kernel launches per step become one graph launch.  Gradients are NOT pre-allocated:
+    param.grad is None when backward starts, so autograd hands each parameter its freshly computed
+    gradient tensor (no per-parameter accumulate kernel).  N=1: clip + AdamW read those tensors inside
+    the same graph.  N>1: one batched copy packs them into a flat fp32 buffer, data parallelism is a
+    single RCCL all-reduce of that buffer over xGMI, and a second graph runs clip + AdamW on views of
+    it.  Dropout masks
     (torch's and the HIP epilogues') are drawn from device-side RNG state, so every replay draws new
     masks.  Inputs are copied into static buffers before each replay.
   graph=False (eager): torch DDP over RCCL (bucketed all-reduce overlapped with backward, no_sync
@@ -74,12 +77,9 @@ class Trainer:
             if self.world > 1:  # identical initial weights on every rank (what DDP's broadcast does)
                 for p in model.state_dict().values():
                     dist.broadcast(p, 0)
-            n = sum(p.numel() for p in self.params)
-            self.flat = torch.zeros(n, device=self.dev, dtype=torch.float32)
-            off = 0
+            self.flat = None  # N>1: packed gradients for the all-reduce (sized at capture)
             for p in self.params:
-                p.grad = self.flat[off:off + p.numel()].view_as(p)
-                off += p.numel()
+                p.grad = None
             self.lr = torch.tensor(cfg.lr, device=self.dev)
             self.optimizer = torch.optim.AdamW(self.params, lr=self.lr, betas=(0.9, 0.999), weight_decay=1e-6,
                                                fused=True, capturable=True)
@@ -151,10 +151,12 @@ class Trainer:
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):
             for _ in range(2):
-                self.flat.zero_()
+                for p in self.params:
+                    p.grad = None
                 self._fwd_bwd(self._static)
                 self._clip_and_update()
         torch.cuda.current_stream(self.dev).wait_stream(side)
+        gparams = [p for p in self.params if p.grad is not None]  # parameters the step differentiates
         with torch.no_grad():
             for p, s_ in zip(self.params, saved):
                 p.copy_(s_)
@@ -164,13 +166,23 @@ class Trainer:
                     if torch.is_tensor(v):
                         v.copy_(prev[k]) if k in prev else v.zero_()
 
+        if self.world > 1:
+            self.flat = torch.zeros(sum(p.numel() for p in gparams), device=self.dev, dtype=torch.float32)
         self._g_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_fb):
-            self.flat.zero_()
+            for p in self.params:
+                p.grad = None  # autograd hands over each fresh gradient: no accumulate kernels
             self._logged = self._fwd_bwd(self._static)
             if self.world == 1:
                 self._clip_and_update()
+            else:
+                torch.cat([p.grad.reshape(-1) for p in gparams], out=self.flat)
         if self.world > 1:
+            self._fb_grads = [p.grad for p in gparams]  # graph-pool outputs, kept alive with the graph
+            off = 0
+            for p in gparams:  # the optimizer graph reads the all-reduced flat buffer
+                p.grad = self.flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
             self._g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._g_opt, pool=self._g_fb.pool()):
                 self._clip_and_update()
