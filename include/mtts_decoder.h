@@ -131,6 +131,26 @@ int mtts_layernorm_bwd(const float *dy, const float *x, const float *w, const fl
                        size_t workspace_bytes, void *hip_stream);
 
 /*
+ * Batched weight packing (csrc/pack.hip): each job is one affine gather of an fp32 torch weight into
+ * (a column block of) a GEMM operand with row stride ld (bf16 or fp32 per `precision`), K ordered
+ * tap-major / channel-minor:
+ *     dst[r*ld + j*C + c] = src[r*sr + c*sc + (j0 + j*js)*sj]  for j < ntaps, c < C;
+ *     dst[r*ld + k'] = 0 for C*ntaps <= k' < Kp  (Kp = columns this job writes).
+ * Covers Conv1d forward / dgrad / stride-2 phase layouts, ConvTranspose1d phases and stacked Linear
+ * weights (row blocks, or column blocks of the transposed stack).  Kp % 8 == 0, ld % 8 == 0, dst
+ * 16-byte aligned.  `jobs` is a HOST array.
+ */
+typedef struct mtts_pack_job {
+    const float *src;
+    void *dst;
+    int32_t rows, C, ntaps, Kp, ld;
+    int64_t sr, sc, sj;
+    int32_t j0, js;
+} mtts_pack_job;
+
+int mtts_pack_weights(const mtts_pack_job *jobs, int32_t njobs, int32_t precision, void *hip_stream);
+
+/*
  * Flash attention of the decoder's transformer blocks (transformer.py:191-370: diffusers Attention,
  * 4 heads x 64, AttnProcessor2_0 -> F.scaled_dot_product_attention with the FLOAT 0/1 mask, i.e. an
  * additive per-key bias).  scores[b,h,i,j] = scale * q_i.k_j + key_bias[b,j]; o = softmax(scores) v.

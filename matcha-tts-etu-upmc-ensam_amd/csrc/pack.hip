@@ -1,0 +1,92 @@
+// Batched weight packing: every GEMM operand layout the decoder step needs, in a few launches.
+//
+// The implicit-GEMM kernels read weights as [rows][ld] with K ordered tap-major / channel-minor
+// (k' = j*C + c) in the operand precision.  torch keeps Conv1d weights [Cout][Cin][k], ConvTranspose1d
+// [Cin][Cout][k] and Linear [N][K] in fp32; the forward, the dgrad (transposed) and the stride-2
+// phase GEMMs each need their own gather of them.  One job = one affine gather
+//     dst[r*ld + j*C + c] = src[r*sr + c*sc + (j0 + j*js)*sj],   zero for k' in [C*ntaps, Kp),
+// and a launch runs up to kJobsPerLaunch jobs (blockIdx.y = job), each thread producing 8
+// consecutive k' (one 16-byte bf16 store, or two float4).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "mtts_common.h"
+#include "mtts_decoder.h"
+
+namespace {
+
+constexpr int kJobsPerLaunch = 32;
+constexpr int kThreads = 256;
+
+struct JobBatch {
+    mtts_pack_job job[kJobsPerLaunch];
+};
+
+template <bool BF16>
+__global__ __launch_bounds__(kThreads) void pack_kernel(JobBatch jb) {
+    const mtts_pack_job &j = jb.job[blockIdx.y];
+    const int groups = j.Kp / 8;
+    const long total = (long)j.rows * groups;
+    const int K = j.C * j.ntaps;
+    for (long gi = (long)blockIdx.x * kThreads + threadIdx.x; gi < total; gi += (long)gridDim.x * kThreads) {
+        const int r = (int)(gi / groups);
+        const int k0 = (int)(gi - (long)r * groups) * 8;
+        int tap = k0 / j.C, c = k0 - tap * j.C;
+        float e[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            e[i] = k0 + i < K ? j.src[(int64_t)r * j.sr + (int64_t)c * j.sc + (int64_t)(j.j0 + tap * j.js) * j.sj]
+                              : 0.f;
+            if (++c == j.C) {
+                c = 0;
+                ++tap;
+            }
+        }
+        if constexpr (BF16) {
+            uint32_t w[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                w[i] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)e[2 * i]) |
+                       ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)e[2 * i + 1]) << 16);
+            *reinterpret_cast<uint4 *>(static_cast<uint16_t *>(j.dst) + (size_t)r * j.ld + k0) =
+                make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+            float4 *d = reinterpret_cast<float4 *>(static_cast<float *>(j.dst) + (size_t)r * j.ld + k0);
+            d[0] = make_float4(e[0], e[1], e[2], e[3]);
+            d[1] = make_float4(e[4], e[5], e[6], e[7]);
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int mtts_pack_weights(const mtts_pack_job *jobs, int32_t njobs, int32_t precision, void *hip_stream) {
+    MTTS_CHECK_ARG(njobs >= 0 && (jobs || njobs == 0), "pack_weights: bad job list");
+    MTTS_CHECK_ARG(precision == MTTS_PREC_FP32 || precision == MTTS_PREC_BF16, "pack_weights: bad precision");
+    long max_groups = 0;
+    for (int i = 0; i < njobs; ++i) {
+        const mtts_pack_job &j = jobs[i];
+        MTTS_CHECK_ARG(j.src && j.dst, "pack_weights: null pointer");
+        MTTS_CHECK_ARG(j.rows >= 0 && j.C >= 1 && j.ntaps >= 1 && j.Kp % 8 == 0 && j.Kp >= j.C * j.ntaps &&
+                           j.ld % 8 == 0 && j.ld >= j.Kp,
+                       "pack_weights: bad job shape (Kp, ld multiples of 8, Kp >= C*ntaps, ld >= Kp)");
+        MTTS_CHECK_ARG((reinterpret_cast<uintptr_t>(j.dst) & 15) == 0, "pack_weights: dst must be 16-byte aligned");
+        const long g = (long)j.rows * (j.Kp / 8);
+        max_groups = g > max_groups ? g : max_groups;
+    }
+    if (njobs == 0 || max_groups == 0) return MTTS_OK;
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+    const int gx = (int)((max_groups + kThreads - 1) / kThreads < 256 ? (max_groups + kThreads - 1) / kThreads : 256);
+    for (int base = 0; base < njobs; base += kJobsPerLaunch) {
+        const int n = njobs - base < kJobsPerLaunch ? njobs - base : kJobsPerLaunch;
+        JobBatch jb;
+        for (int i = 0; i < n; ++i) jb.job[i] = jobs[base + i];
+        if (precision == MTTS_PREC_BF16)
+            hipLaunchKernelGGL(pack_kernel<true>, dim3(gx, n), dim3(kThreads), 0, st, jb);
+        else
+            hipLaunchKernelGGL(pack_kernel<false>, dim3(gx, n), dim3(kThreads), 0, st, jb);
+        if (int rc = mtts::check_launch("pack_kernel")) return rc;
+    }
+    return MTTS_OK;
+}

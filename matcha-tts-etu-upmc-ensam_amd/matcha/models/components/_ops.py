@@ -20,6 +20,8 @@ backward, so no mask tensor is stored.
 """
 from __future__ import annotations
 
+import contextlib
+import contextvars
 import ctypes
 import math
 
@@ -76,6 +78,12 @@ class AttnGrads(ctypes.Structure):
                 ("dk", ctypes.c_void_p), ("dv", ctypes.c_void_p), ("ldd", ctypes.c_int32)]
 
 
+class PackJob(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("rows", ctypes.c_int32), ("C", ctypes.c_int32),
+                ("ntaps", ctypes.c_int32), ("Kp", ctypes.c_int32), ("ld", ctypes.c_int32), ("sr", ctypes.c_int64),
+                ("sc", ctypes.c_int64), ("sj", ctypes.c_int64), ("j0", ctypes.c_int32), ("js", ctypes.c_int32)]
+
+
 _P, _I, _F, _SZ, _U = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint32
 _I64 = ctypes.c_int64
 N.register("mtts_conv_gemm", ctypes.c_int, [ctypes.POINTER(ConvGemmArgs), _I, _P])
@@ -91,6 +99,7 @@ N.register("mtts_layernorm_fwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _I, 
 N.register("mtts_layernorm_bwd_workspace_size", _SZ, [_I, _I])
 N.register("mtts_layernorm_bwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P])
 N.register("mtts_dropout_apply", ctypes.c_int, [_P, _P, _I, _I, _I, _F, _P, _P])
+N.register("mtts_pack_weights", ctypes.c_int, [ctypes.POINTER(PackJob), _I, _I, _P])
 N.register("mtts_attention_fwd", ctypes.c_int, [ctypes.POINTER(AttnArgs), _I, _P])
 N.register("mtts_attention_bwd_workspace_size", _SZ, [_I, _I, _I])
 N.register("mtts_attention_bwd", ctypes.c_int, [ctypes.POINTER(AttnArgs), ctypes.POINTER(AttnGrads), _I, _P, _SZ, _P])
@@ -130,6 +139,132 @@ def pack_weight(w2d: torch.Tensor, prec: int) -> tuple[torch.Tensor, int]:
     if Kp != K:
         w = F.pad(w, (0, Kp - K))
     return w.contiguous(), Kp
+
+
+# ------------------------------------------------------------------------------------------ weight packing
+# A GEMM operand layout of one or more fp32 weights: [rows][Kp] in the operand precision, built by
+# mtts_pack_weights jobs (include/mtts_decoder.h).  job = (src, row0, rows, col0, Kp_job, C, ntaps,
+# sr, sc, sj, j0, js): dst[row0 + r][col0 + j*C + c] = src[r*sr + c*sc + (j0 + j*js)*sj].
+class PackSpec:
+    __slots__ = ("key", "rows", "Kp", "jobs", "dgrad")
+
+    def __init__(self, key, rows, Kp, jobs, dgrad):
+        self.key, self.rows, self.Kp, self.jobs, self.dgrad = key, rows, Kp, jobs, dgrad
+
+
+def _r8(n):
+    return (n + 7) // 8 * 8
+
+
+def spec_linear(ws, dgrad=False):
+    """Linear weights [N_i, K] stacked along N -> [sum N_i, Kp] (forward); dgrad: the transpose
+    [K, sum N_i] (column blocks; each N_i % 8 == 0 when stacking)."""
+    ws = tuple(ws)
+    K = ws[0].shape[1]
+    if not dgrad:
+        jobs, r0 = [], 0
+        for w in ws:
+            jobs.append((w, r0, w.shape[0], 0, _r8(K), K, 1, K, 1, 0, 0, 1))
+            r0 += w.shape[0]
+        return PackSpec(("lin",) + tuple(id(w) for w in ws), r0, _r8(K), jobs, False)
+    ntot = sum(w.shape[0] for w in ws)
+    jobs, c0 = [], 0
+    for i, w in enumerate(ws):
+        last = i == len(ws) - 1
+        jobs.append((w, 0, K, c0, (_r8(ntot) - c0) if last else w.shape[0], w.shape[0], 1, 1, K, 0, 0, 1))
+        c0 += w.shape[0]
+    return PackSpec(("lin_t",) + tuple(id(w) for w in ws), K, _r8(ntot), jobs, True)
+
+
+def spec_conv_fwd(w):
+    """Conv1d weight [Cout, Cin, k] -> [Cout][j*Cin + c]."""
+    Cout, Cin, k = w.shape
+    return PackSpec(("conv", id(w)), Cout, _r8(k * Cin), [(w, 0, Cout, 0, _r8(k * Cin), Cin, k, Cin * k, k, 1, 0, 1)],
+                    False)
+
+
+def spec_conv_dgrad(w, j0=0, js=1):
+    """Conv1d dgrad operand: [Cin][jj*Cout + n] = w[n, c, j0 + jj*js] (all taps, or one stride phase)."""
+    Cout, Cin, k = w.shape
+    nt = len(range(j0, k, js))
+    return PackSpec(("conv_d", id(w), j0, js), Cin, _r8(nt * Cout),
+                    [(w, 0, Cin, 0, _r8(nt * Cout), Cout, nt, k, Cin * k, 1, j0, js)], True)
+
+
+def spec_convT_fwd(w, j0, js):
+    """ConvTranspose1d weight [Cin, Cout, k], output phase taps j0::js -> [Cout][jj*Cin + c]."""
+    Cin, Cout, k = w.shape
+    nt = len(range(j0, k, js))
+    return PackSpec(("convT", id(w), j0, js), Cout, _r8(nt * Cin),
+                    [(w, 0, Cout, 0, _r8(nt * Cin), Cin, nt, k, Cout * k, 1, j0, js)], False)
+
+
+def spec_convT_dgrad(w):
+    """ConvTranspose1d dgrad operand (a stride-2 conv over dy): [Cin][j*Cout + n] = w[c, n, j]."""
+    Cin, Cout, k = w.shape
+    return PackSpec(("convT_d", id(w)), Cin, _r8(k * Cout), [(w, 0, Cin, 0, _r8(k * Cout), Cout, k, Cout * k, k, 1, 0, 1)],
+                    True)
+
+
+def _run_pack(specs, prec):
+    dev = specs[0].jobs[0][0].device
+    dt = torch.bfloat16 if prec == PREC_BF16 else torch.float32
+    outs = [torch.empty(sp.rows, sp.Kp, device=dev, dtype=dt) for sp in specs]
+    njobs = sum(len(sp.jobs) for sp in specs)
+    arr = (PackJob * njobs)()
+    i = 0
+    keep = []
+    for sp, out in zip(specs, outs):
+        es = out.element_size()
+        for (w, r0, rows, c0, kpj, C, nt, sr, sc, sj, j0, js) in sp.jobs:
+            src = _f32c(w)
+            keep.append(src)
+            j = arr[i]
+            j.src, j.dst = src.data_ptr(), out.data_ptr() + (r0 * sp.Kp + c0) * es
+            j.rows, j.C, j.ntaps, j.Kp, j.ld = rows, C, nt, kpj, sp.Kp
+            j.sr, j.sc, j.sj, j.j0, j.js = sr, sc, sj, j0, js
+            i += 1
+    N.check(N.lib().mtts_pack_weights(arr, njobs, prec, torch.cuda.current_stream(dev).cuda_stream),
+            "mtts_pack_weights")
+    return outs
+
+
+_PACK_SCOPE: contextvars.ContextVar = contextvars.ContextVar("mtts_pack_scope", default=None)
+
+
+@contextlib.contextmanager
+def weight_pack_scope(owner: torch.nn.Module):
+    """Packs, in a few launches, every operand layout `owner`'s previous forward asked for (the
+    backward's transposed layouts too when grad is enabled), and serves the ops inside the scope
+    from that cache.  Layouts requested for the first time are packed on demand and remembered."""
+    prec = gemm_precision()
+    plan = owner.__dict__.setdefault("_mtts_pack_plan", {})
+    grad = torch.is_grad_enabled()
+    specs = [sp for key, sp in plan.items() if key[0] == prec and (grad or not sp.dgrad)]
+    cache = {}
+    if specs:
+        for sp, t in zip(specs, _run_pack(specs, prec)):
+            cache[(prec,) + sp.key] = t
+    tok = _PACK_SCOPE.set((plan, cache, prec))
+    try:
+        yield
+    finally:
+        _PACK_SCOPE.reset(tok)
+
+
+def packed(spec: PackSpec, prec: int) -> tuple[torch.Tensor, int]:
+    """(operand, Kp) for `spec`, from the active weight_pack_scope when there is one."""
+    act = _PACK_SCOPE.get()
+    if act is not None and act[2] == prec:
+        plan, cache, _ = act
+        key = (prec,) + spec.key
+        t = cache.get(key)
+        if t is None:
+            t = _run_pack([spec], prec)[0]
+            cache[key] = t
+            plan[key] = spec
+        return t, spec.Kp
+    return _run_pack([spec], prec)[0], spec.Kp
 
 
 # Per-launch timing for bench.py's roofline leg: when set to a list, every mtts_conv_gemm launch appends
@@ -196,7 +331,13 @@ class _ConvTM(torch.autograd.Function):
         B, Ti, Cin = x.shape
         Cout, _, k = weight.shape
         To = (Ti + 2 * padding - k) // stride + 1
-        Wp, Kp = pack_weight(weight.permute(0, 2, 1).reshape(Cout, k * Cin), prec)
+        Wp, Kp = packed(spec_conv_fwd(weight), prec)
+        # the backward's dgrad operands come from the same packing pass (weight_pack_scope)
+        ctx.wd = None
+        if ctx.needs_input_grad[0]:
+            ctx.wd = [packed(spec_conv_dgrad(weight), prec)] if stride == 1 else \
+                [packed(spec_conv_dgrad(weight, (ph + padding) % stride, stride), prec)
+                 if len(range((ph + padding) % stride, k, stride)) else None for ph in range(stride)]
         y = torch.empty(B, To, Cout, device=x.device, dtype=torch.float32)
         mask = _f32c(mask)
         out_scale = _f32c(out_scale)
@@ -221,7 +362,7 @@ class _ConvTM(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             if stride == 1:
-                Wd, Kp = pack_weight(weight.permute(1, 2, 0).reshape(Cin, k * Cout), prec)
+                Wd, Kp = ctx.wd[0]
                 _gemm(dy, To, Ti, B, 1, [pad - j for j in range(k)], Cout, Wd, Kp, Cin, dx, Ti, prec=prec,
                       c_scale=mask)
             else:  # stride-2 dgrad = transposed conv = one GEMM per output phase
@@ -232,7 +373,7 @@ class _ConvTM(torch.autograd.Function):
                     if not js or nrows <= 0:
                         dx[:, ph::stride].zero_()
                         continue
-                    Wd, Kp = pack_weight(weight[:, :, j0::stride].permute(1, 2, 0).reshape(Cin, len(js) * Cout), prec)
+                    Wd, Kp = ctx.wd[ph]
                     _gemm(dy, To, nrows, B, 1, [(ph + pad - j) // stride for j in js], Cout, Wd, Kp, Cin, dx, Ti,
                           stride, ph, prec=prec, c_scale=mask)
         if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
@@ -262,9 +403,10 @@ class _ConvTransposeTM(torch.autograd.Function):
             j0 = (ph + pad) % s  # taps of this phase: j0, j0+s, ... (slice, not a host index list)
             js = list(range(j0, k, s))
             nrows = (To_full - ph + s - 1) // s
-            Wp, Kp = pack_weight(weight[:, :, j0::s].permute(1, 2, 0).reshape(Cout, len(js) * Cin), prec)
+            Wp, Kp = packed(spec_convT_fwd(weight, j0, s), prec)
             _gemm(x, T, nrows, B, 1, [(ph + pad - j) // s for j in js], Cin, Wp, Kp, Cout, y, To_full, s, ph,
                   prec=prec, a_scale=mask, bias=bias_c)
+        ctx.wd = packed(spec_convT_dgrad(weight), prec) if ctx.needs_input_grad[0] else None
         ctx.save_for_backward(x, weight, mask)
         ctx.cfg = (prec, bias is not None)
         return y
@@ -282,7 +424,7 @@ class _ConvTransposeTM(torch.autograd.Function):
         offs = [j - pad for j in range(k)]
         if ctx.needs_input_grad[0]:  # dgrad of a transposed conv = stride-2 conv over dy
             dx = torch.empty_like(x)
-            Wd, Kp = pack_weight(weight.permute(0, 2, 1).reshape(Cin, k * Cout), prec)
+            Wd, Kp = ctx.wd
             _gemm(dy, T2, T, B, s, offs, Cout, Wd, Kp, Cin, dx, T, prec=prec, c_scale=mask)
         if ctx.needs_input_grad[1]:
             xm = x * mask.unsqueeze(-1) if mask is not None else x
@@ -296,31 +438,34 @@ class _ConvTransposeTM(torch.autograd.Function):
 
 
 class _LinearTM(torch.autograd.Function):
-    """x @ W^T + b -> dropout -> + residual  (diffusers to_q/k/v/to_out Linear + Dropout)."""
+    """x @ W^T + b -> dropout -> + residual  (diffusers to_q/k/v/to_out Linear + Dropout).  W may be
+    several weights stacked along N (the fused q|k|v projection), each receiving its own gradient."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, dropout_p):
-        _check(x, weight, residual)
+    def forward(ctx, x, bias, residual, dropout_p, *weights):
+        _check(x, residual, *weights)
         prec = gemm_precision()
         shp = x.shape
         x2 = _f32c(x).reshape(-1, shp[-1])
         M, K = x2.shape
-        Nout = weight.shape[0]
-        Wp, Kp = pack_weight(weight, prec)
+        Nout = sum(w.shape[0] for w in weights)
+        Wp, Kp = packed(spec_linear(weights), prec)
+        ctx.wd = packed(spec_linear(weights, dgrad=True), prec) if ctx.needs_input_grad[0] else None
         y = torch.empty(M, Nout, device=x.device, dtype=torch.float32)
         res2 = _f32c(residual).reshape(M, Nout) if residual is not None else None
         seed = _new_seed(x.device) if dropout_p > 0 else None
         _gemm(x2, M, M, 1, 1, [0], K, Wp, Kp, Nout, y, M, prec=prec, bias=_f32c(bias), residual=res2,
               dropout_p=dropout_p, seed=seed)
-        ctx.save_for_backward(x2, weight)
-        ctx.cfg = (prec, bias is not None, residual is not None, shp, dropout_p, seed)
+        ctx.save_for_backward(x2)
+        ctx.cfg = (prec, bias is not None, residual is not None, shp, dropout_p, seed,
+                   [w.shape[0] for w in weights], K)
         return y.reshape(*shp[:-1], Nout)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, weight = ctx.saved_tensors
-        prec, has_bias, has_res, shp, p, seed = ctx.cfg
-        Nout, K = weight.shape
+        (x2,) = ctx.saved_tensors
+        prec, has_bias, has_res, shp, p, seed, rows, K = ctx.cfg
+        Nout = sum(rows)
         dy2 = _f32c(dy).reshape(-1, Nout)
         M = dy2.shape[0]
         dres = dy if has_res else None
@@ -329,17 +474,19 @@ class _LinearTM(torch.autograd.Function):
             N.check(N.lib().mtts_dropout_apply(dy2.data_ptr(), g.data_ptr(), M, Nout, Nout, float(p),
                                                seed.data_ptr(), _stream(g)), "mtts_dropout_apply")
             dy2 = g
-        dx = dw = db = None
+        dx = db = None
+        dws = [None] * len(rows)
         if ctx.needs_input_grad[0]:
-            Wd, Kp = pack_weight(weight.t(), prec)
+            Wd, Kp = ctx.wd
             dx = torch.empty(M, K, device=dy2.device, dtype=torch.float32)
             _gemm(dy2, M, M, 1, 1, [0], Nout, Wd, Kp, K, dx, M, prec=prec)
             dx = dx.reshape(*shp)
-        if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
-            dw = torch.empty(weight.shape, device=dy2.device, dtype=torch.float32)
+        if any(ctx.needs_input_grad[4:]) or (has_bias and ctx.needs_input_grad[1]):
+            dw = torch.empty(Nout, K, device=dy2.device, dtype=torch.float32)
             db = torch.empty(Nout, device=dy2.device, dtype=torch.float32) if has_bias else None
             _wgrad(dy2, M, 1, 0, x2, M, M, 1, 1, [0], K, Nout, dw, (K, 1, 0), prec=prec, db=db)
-        return dx, dw, db, dres, None
+            dws = list(dw.split(rows, dim=0))
+        return (dx, db, dres, None, *dws)
 
 
 class _FeedForwardTM(torch.autograd.Function):
@@ -355,8 +502,10 @@ class _FeedForwardTM(torch.autograd.Function):
         x2 = _f32c(x).reshape(-1, shp[-1])
         M, K = x2.shape
         H, Nout = w1.shape[0], w2.shape[0]
-        W1p, K1p = pack_weight(w1, prec)
-        W2p, K2p = pack_weight(w2, prec)
+        W1p, K1p = packed(spec_linear((w1,)), prec)
+        W2p, K2p = packed(spec_linear((w2,)), prec)
+        ctx.w2t = packed(spec_linear((w2,), dgrad=True), prec) if any(ctx.needs_input_grad) else None
+        ctx.w1t = packed(spec_linear((w1,), dgrad=True), prec) if ctx.needs_input_grad[0] else None
         z = torch.empty(M, H, device=x.device, dtype=torch.float32)
         h = torch.empty(M, H, device=x.device, dtype=torch.float32)
         seed = _new_seed(x.device) if dropout_p > 0 else None
@@ -381,7 +530,7 @@ class _FeedForwardTM(torch.autograd.Function):
         dw2 = torch.empty(w2.shape, device=dev, dtype=torch.float32)
         db2 = torch.empty(Nout, device=dev, dtype=torch.float32)
         _wgrad(dy2, M, 1, 0, h, M, M, 1, 1, [0], H, Nout, dw2, (H, 1, 0), prec=prec, db=db2)
-        W2t, K2p = pack_weight(w2.t(), prec)
+        W2t, K2p = ctx.w2t
         dz = torch.empty(M, H, device=dev, dtype=torch.float32)
         _gemm(dy2, M, M, 1, 1, [0], Nout, W2t, K2p, H, dz, M, prec=prec, act=ACT_DGELU, aux=z, dropout_p=p,
               seed=seed)
@@ -390,7 +539,7 @@ class _FeedForwardTM(torch.autograd.Function):
         _wgrad(dz, M, 1, 0, x2, M, M, 1, 1, [0], K, H, dw1, (K, 1, 0), prec=prec, db=db1)
         dx = None
         if ctx.needs_input_grad[0]:
-            W1t, K1p = pack_weight(w1.t(), prec)
+            W1t, K1p = ctx.w1t
             dx = torch.empty(M, K, device=dev, dtype=torch.float32)
             _gemm(dz, M, M, 1, 1, [0], H, W1t, K1p, K, dx, M, prec=prec)
             dx = dx.reshape(*shp)
@@ -495,8 +644,10 @@ def layer_norm_tm(h, weight, bias, eps: float = 1e-5):
 
 
 def linear_tm(x, weight, bias=None, residual=None, dropout_p: float = 0.0):
-    """residual + dropout(x @ W^T + b)   (diffusers Linear [+ Dropout] [+ residual])."""
-    return _LinearTM.apply(x, weight, bias, residual, float(dropout_p))
+    """residual + dropout(x @ W^T + b)   (diffusers Linear [+ Dropout] [+ residual]).  `weight` may be
+    a tuple of weights stacked along the output dim (one GEMM, one gradient per weight)."""
+    ws = tuple(weight) if isinstance(weight, (tuple, list)) else (weight,)
+    return _LinearTM.apply(x, bias, residual, float(dropout_p), *ws)
 
 
 def ff_tm(x, w1, b1, w2, b2, residual=None, dropout_p: float = 0.0):

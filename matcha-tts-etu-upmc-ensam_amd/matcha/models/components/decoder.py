@@ -194,7 +194,7 @@ class Decoder(nn.Module):
         fp32 MFMA otherwise; everything else here is fp32."""
         prec_bf16 = torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
         with torch.autocast("cuda", enabled=False):
-            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec_bf16):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec_bf16), O.weight_pack_scope(self):
                 return self._forward_tm(x.float(), mask.float(), mu.float(), t.float())
 
     def _forward_tm(self, x, mask, mu, t):

@@ -74,7 +74,7 @@ class Attention(nn.Module):
         return torch.cat([self.to_q.weight, self.to_k.weight, self.to_v.weight], dim=0)
 
     def forward_tm(self, h, key_bias, residual=None):
-        qkv = O.linear_tm(h, self.qkv_weight(), None)  # [B, T, 3C]: q | k | v
+        qkv = O.linear_tm(h, (self.to_q.weight, self.to_k.weight, self.to_v.weight), None)  # [B,T,3C] q|k|v
         o = O.attention_tm(qkv, key_bias, self.heads)
         p = self.to_out[1].p if self.training else 0.0
         return O.linear_tm(o, self.to_out[0].weight, self.to_out[0].bias, residual=residual, dropout_p=p)
