@@ -33,8 +33,10 @@ extern "C" {
 #define MTTS_ACT_NONE 0
 #define MTTS_ACT_GELU 1  /* erf GELU (diffusers GELU, approximate="none") */
 #define MTTS_ACT_DGELU 2 /* multiply by GELU'(aux[row, n]) -- backward through a GELU */
+#define MTTS_ACT_RELU 3  /* max(x, 0) */
+#define MTTS_ACT_DRELU 4 /* zero where aux[row, n] <= 0 -- backward through a ReLU (aux: its output) */
 
-#define MTTS_CONV_MAX_TAPS 4
+#define MTTS_CONV_MAX_TAPS 8
 #define MTTS_GEMM_PANEL 64 /* mtts_conv_gemm_tile schedule id of the panel kernel */
 
 /*
@@ -121,14 +123,25 @@ int mtts_gn_mish_bwd(const float *dy, const float *h, const float *gamma, const 
  */
 int mtts_dropout_apply(const float *x, float *y, int32_t rows, int32_t cols, int32_t ld, float p,
                        const uint32_t *seed, void *hip_stream);
+/* Backward of an epilogue "act -> dropout" from the forward OUTPUT y: dx = dy * [y > 0] (act
+ * MTTS_ACT_RELU) * keep(seed, r, c) / (1-p) (p > 0).  Rows/cols index like mtts_dropout_apply. */
+int mtts_act_dropout_bwd(const float *dy, const float *y, float *dx, int32_t rows, int32_t cols, int32_t ld,
+                         int32_t act, float p, const uint32_t *seed, void *hip_stream);
 
-/* LayerNorm over the last dim of x [M, C]; mean/rstd [M] saved.  C % 4 == 0, C <= 1024. */
+/* LayerNorm over the last dim of x [M, C]; mean/rstd [M] saved.  C % 4 == 0, C <= 1024.  Optional
+ * fused tail applied to the normalized output: act MTTS_ACT_RELU, then dropout(p) with the
+ * counter-based mask keyed (seed, row, channel) -- the text encoder's LN -> ReLU -> Dropout
+ * (text_encoder.py:48-55) and LN -> Dropout (:81-95).  act = MTTS_ACT_NONE, p = 0: plain LayerNorm. */
 int mtts_layernorm_fwd(const float *x, const float *w, const float *b, float *y, float *mean, float *rstd,
-                       int32_t M, int32_t C, float eps, void *hip_stream);
+                       int32_t M, int32_t C, float eps, int32_t act, float dropout_p, const uint32_t *seed,
+                       void *hip_stream);
 size_t mtts_layernorm_bwd_workspace_size(int32_t M, int32_t C);
-int mtts_layernorm_bwd(const float *dy, const float *x, const float *w, const float *mean, const float *rstd,
-                       float *dx, float *dw, float *db, int32_t M, int32_t C, void *workspace,
-                       size_t workspace_bytes, void *hip_stream);
+/* dx (and dw, db when non-NULL) from dy w.r.t. the forward's (tail) output; the same act / p / seed as
+ * the forward (b is needed for the ReLU gate). */
+int mtts_layernorm_bwd(const float *dy, const float *x, const float *w, const float *b, const float *mean,
+                       const float *rstd, float *dx, float *dw, float *db, int32_t M, int32_t C, int32_t act,
+                       float dropout_p, const uint32_t *seed, void *workspace, size_t workspace_bytes,
+                       void *hip_stream);
 
 /*
  * Batched weight packing (csrc/pack.hip): each job is one affine gather of an fp32 torch weight into
@@ -167,6 +180,8 @@ typedef struct mtts_attn_args {
     float *lse;
     int32_t B, T, H, D;
     float scale;
+    float dropout_p;      /* dropout on the probabilities (text encoder, text_encoder.py:222); 0 = off */
+    const uint32_t *seed; /* device pointer (2 words), keyed (seed, (b*H+h)*T + q, key) */
 } mtts_attn_args;
 
 typedef struct mtts_attn_grads {
@@ -181,6 +196,14 @@ size_t mtts_attention_bwd_workspace_size(int32_t B, int32_t T, int32_t H);
 /* Deterministic backward (no atomics): a dQ pass (also forms rowsum(dO*O)) then a dK/dV pass. */
 int mtts_attention_bwd(const mtts_attn_args *args, const mtts_attn_grads *grads, int32_t precision,
                        void *workspace, size_t workspace_bytes, void *hip_stream);
+
+/* Rotary position embedding of the text encoder's attention (text_encoder.py:99-143): on the q and
+ * k column blocks of a fused token-major projection x [rows = B*T, 3C] (H heads of C/H dims), the first
+ * rope_dims dims of every head are rotated by position t = row % T in rotate-half form with
+ * cos_t/sin_t [T][rope_dims/2]; the v block is copied.  inverse = 1 applies R^T (the backward).
+ * Out of place (x != y). */
+int mtts_rope_qk(const float *x, float *y, int32_t rows, int32_t T, int32_t C, int32_t H, int32_t rope_dims,
+                 const float *cos_t, const float *sin_t, int32_t inverse, void *hip_stream);
 
 #ifdef __cplusplus
 } /* extern "C" */

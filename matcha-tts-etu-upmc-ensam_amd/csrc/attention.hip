@@ -212,7 +212,7 @@ __device__ __forceinline__ void tile_loop(int ntiles, Load &&load, Store &&store
         const int buf = NB == 2 ? (it & 1) : 0;
         const bool more = it + 1 < ntiles;
         if (more) load((it + 1) * kTile);
-        compute(buf);
+        compute(buf, it * kTile);
         if constexpr (NB == 2) {
             if (more) store(buf ^ 1);
             __syncthreads();
@@ -271,7 +271,15 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
         lv.store(nullptr, Vt + buf * Gm::TE, tid);
         if (tid < kTile) bias_s[buf * kTile + tid] = bias_r;
     };
-    auto compute = [&](int buf) {
+    const bool drop = p.dropout_p > 0.f;
+    uint32_t s0 = 0, s1 = 0;
+    if (drop) {
+        s0 = p.seed[0];
+        s1 = p.seed[1];
+    }
+    const float inv_keep = 1.f / (1.f - p.dropout_p);
+    const uint32_t prow = (uint32_t)(((size_t)b * p.H + h) * T + q);  // dropout row key of this query
+    auto compute = [&](int buf, int k0) {
         const ST *K_ = Ks + buf * Gm::RE, *V_ = Vt + buf * Gm::TE;
         const float *bs = bias_s + buf * kTile;
 #pragma unroll
@@ -298,6 +306,13 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
             rs += __shfl_xor(rs, 32);
             l = l * corr + rs;
             m = m_new;
+            if (drop) {  // dropout on the probabilities (the normalizer l keeps the undropped sum)
+#pragma unroll
+                for (int v = 0; v < 16; ++v)
+                    s[v] = mtts::dropout_keep(s0, s1, prow, (uint32_t)(k0 + sub * 32 + crow(v, lh)), p.dropout_p)
+                               ? s[v] * inv_keep
+                               : 0.f;
+            }
 #pragma unroll
             for (int t = 0; t < Gm::NT; ++t) {
 #pragma unroll
@@ -387,7 +402,15 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p,
         lv.store(Vs + buf * Gm::RE, nullptr, tid);
         if (tid < kTile) bias_s[buf * kTile + tid] = bias_r;
     };
-    auto compute = [&](int buf) {
+    const bool drop = p.dropout_p > 0.f;
+    uint32_t s0 = 0, s1 = 0;
+    if (drop) {
+        s0 = p.seed[0];
+        s1 = p.seed[1];
+    }
+    const float inv_keep = 1.f / (1.f - p.dropout_p);
+    const uint32_t prow = (uint32_t)srow;
+    auto compute = [&](int buf, int k0) {
         const ST *K_ = Ks + buf * Gm::RE, *V_ = Vs + buf * Gm::RE, *KT_ = Kt + buf * Gm::TE;
         const float *bs = bias_s + buf * kTile;
 #pragma unroll
@@ -401,7 +424,12 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p,
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 const float pr = exp2f(sacc[v] * sl2 + bs[sub * 32 + crow(v, lh)] - lse2);
-                ds[v] = pr * (pacc[v] - dsum);
+                float dp = pacc[v];  // dL/d(dropped P) -> dL/dP through the regenerated mask
+                if (drop)
+                    dp = mtts::dropout_keep(s0, s1, prow, (uint32_t)(k0 + sub * 32 + crow(v, lh)), p.dropout_p)
+                             ? dp * inv_keep
+                             : 0.f;
+                ds[v] = pr * (dp - dsum);
             }
 #pragma unroll
             for (int t = 0; t < Gm::NT; ++t) mma_perm<BF16, D>(acc[t], KT_, t * 32 + lr, sub, lh, ds);  // dQ^T += K^T dS^T
@@ -479,7 +507,14 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkv_kernel(mtts_attn_args p
             d_s[buf * kTile + tid] = d_r;
         }
     };
-    auto compute = [&](int buf) {
+    const bool drop = p.dropout_p > 0.f;
+    uint32_t s0 = 0, s1 = 0;
+    if (drop) {
+        s0 = p.seed[0];
+        s1 = p.seed[1];
+    }
+    const float inv_keep = 1.f / (1.f - p.dropout_p);
+    auto compute = [&](int buf, int q0) {
         const ST *Q_ = Qs + buf * Gm::RE, *G_ = Gs + buf * Gm::RE, *QT_ = Qt + buf * Gm::TE, *GT_ = Gt + buf * Gm::TE;
         const float *ls = lse_s + buf * kTile, *dd = d_s + buf * kTile;
 #pragma unroll
@@ -493,8 +528,15 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkv_kernel(mtts_attn_args p
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 const int qi = sub * 32 + crow(v, lh);
-                pr[v] = exp2f(sacc[v] * sl2 + bias2 - ls[qi]);
-                ds[v] = pr[v] * (pacc[v] - dd[qi]);
+                const float pv = exp2f(sacc[v] * sl2 + bias2 - ls[qi]);
+                float dp = pacc[v];
+                pr[v] = pv;
+                if (drop) {  // P feeds dV through the forward's dropout mask
+                    const bool keep = mtts::dropout_keep(s0, s1, (uint32_t)(sbase + q0 + qi), (uint32_t)key, p.dropout_p);
+                    pr[v] = keep ? pv * inv_keep : 0.f;
+                    dp = keep ? dp * inv_keep : 0.f;
+                }
+                ds[v] = pv * (dp - dd[qi]);
             }
 #pragma unroll
             for (int t = 0; t < Gm::NT; ++t) {
@@ -545,6 +587,8 @@ int check_args(const mtts_attn_args *p, int precision) {
     MTTS_CHECK_ARG(aligned16(p->q) && aligned16(p->k) && aligned16(p->v) && aligned16(p->o),
                    "attention: q/k/v/o must be 16-byte aligned");
     MTTS_CHECK_ARG(p->scale > 0.f, "attention: scale must be positive");
+    MTTS_CHECK_ARG(p->dropout_p >= 0.f && p->dropout_p < 1.f && (p->dropout_p == 0.f || p->seed),
+                   "attention: dropout_p in [0, 1) with a seed");
     return MTTS_OK;
 }
 
@@ -582,9 +626,46 @@ int bwd_dispatch(const mtts_attn_args &p, const mtts_attn_grads &g, float *Drow,
                        : bwd_launch<BF16, 96>(p, g, Drow, st);
 }
 
+// RoPE (text_encoder.py:99-143, rotate-half form) on the q and k column blocks of a fused [rows, 3C]
+// projection, v copied: one thread per element.  Head dim D, rotated dims [0, R) of each head, half = R/2,
+// cos/sin [T][half].  forward: y_d = x_d cos - x_{d+half} sin (d < half), x_d cos + x_{d-half} sin;
+// inverse (the backward, R^T): the signs of the sin terms flip.
+__global__ void rope_qk_kernel(const float *__restrict__ x, float *__restrict__ y, int rows, int T, int C, int D, int R,
+                               const float *__restrict__ cs, const float *__restrict__ sn, float sgn) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int W = 3 * C;
+    if (idx >= (int64_t)rows * W) return;
+    const int r = (int)(idx / W), col = (int)(idx - (int64_t)r * W);
+    const float *xr = x + (size_t)r * W;
+    float v = xr[col];
+    const int d = (col % C) % D;
+    if (col < 2 * C && d < R) {
+        const int half = R / 2, t = r % T;
+        const int i = d < half ? d : d - half;
+        const float c = cs[t * half + i], s = sn[t * half + i];
+        v = d < half ? v * c - sgn * xr[col + half] * s : v * c + sgn * xr[col - half] * s;
+    }
+    y[(size_t)r * W + col] = v;
+}
+
 }  // namespace
 
 extern "C" {
+
+int mtts_rope_qk(const float *x, float *y, int32_t rows, int32_t T, int32_t C, int32_t H, int32_t rope_dims,
+                 const float *cos_t, const float *sin_t, int32_t inverse, void *hip_stream) {
+    MTTS_CHECK_ARG(x && y && cos_t && sin_t && x != y, "rope_qk: null or aliased pointer");
+    MTTS_CHECK_ARG(rows >= 0 && T >= 1 && rows % T == 0 && H >= 1 && C % H == 0 && rope_dims % 2 == 0 &&
+                       rope_dims >= 0 && rope_dims <= C / H,
+                   "rope_qk: bad shape");
+    const int64_t n = (int64_t)rows * 3 * C;
+    if (n == 0) return MTTS_OK;
+    hipLaunchKernelGGL(rope_qk_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(hip_stream), x, y, rows, T, C, C / H, rope_dims, cos_t, sin_t,
+                       inverse ? -1.f : 1.f);
+    return mtts::check_launch("rope_qk_kernel");
+}
+
 
 int mtts_attention_fwd(const mtts_attn_args *p, int32_t precision, void *hip_stream) {
     if (int rc = check_args(p, precision)) return rc;

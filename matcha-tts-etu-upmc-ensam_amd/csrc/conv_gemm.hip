@@ -35,21 +35,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ uint16_t to_bf16(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
-__device__ __forceinline__ int tap_off(const mtts_conv_gemm_args &p, int j) {
-    return j == 0 ? p.off[0] : j == 1 ? p.off[1] : j == 2 ? p.off[2] : p.off[3];
-}
-__device__ __forceinline__ int tap_off(const mtts_conv_wgrad_args &p, int j) {
-    return j == 0 ? p.off[0] : j == 1 ? p.off[1] : j == 2 ? p.off[2] : p.off[3];
-}
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
-// d/dx erf-GELU, as torch's GeluBackward (cdf + x * pdf)
-__device__ __forceinline__ float gelu_erf_grad(float x) {
-    const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-    const float pdf = expf(-0.5f * x * x) * 0.39894228040143268f;
-    return cdf + x * pdf;
-}
 
 // b = m / d, u = m % d for 0 <= m < 2^24 with a precomputed 1/d (float estimate + one correction)
 __device__ __forceinline__ void divmod_fast(int m, int d, float inv_d, int &q, int &r) {
@@ -149,7 +136,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
             const int ch = a_ch[c];
             int irow = 0;
             if (ok) {
-                irow = ga[c].in_u + tap_off(p, a_j[c]);
+                irow = ga[c].in_u + mtts::tap_off(p, a_j[c]);
                 ok = irow >= 0 && irow < p.Ti;
             }
             a_ch[c] += KB;  // advance (tap, channel) to the next K step
@@ -305,8 +292,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
                 const size_t crow = (size_t)crows[v];
                 float val = acc[i][j][v] + bn;
                 if (p.C_pre) p.C_pre[crow * p.ldc + n] = val;
-                if (p.act == MTTS_ACT_GELU) val = gelu_erf(val);
-                else if (p.act == MTTS_ACT_DGELU) val *= gelu_erf_grad(p.aux[crow * p.ldaux + n]);
+                if (p.act) val = mtts::epi_act(p.act, val, p.aux + crow * p.ldaux + n);
                 if (p.dropout_p > 0.f)
                     val = mtts::dropout_keep(s0, s1, (uint32_t)crow, (uint32_t)n, p.dropout_p)
                               ? val * (1.0f / (1.0f - p.dropout_p))
@@ -394,7 +380,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
             if (ok) {
                 const int j = k / p.cin;
                 ch = k - j * p.cin;
-                irow = u * p.in_stride + tap_off(p, j);
+                irow = u * p.in_stride + mtts::tap_off(p, j);
                 ok = irow >= 0 && irow < p.Ti;
             }
             if (ok) {
@@ -519,7 +505,7 @@ int check_gather(const void *A, int lda, int cin, int ntaps, int K) {
     if (!A) return mtts::fail(MTTS_ERR_INVALID_ARG, "conv_gemm: A is null");
     if (cin <= 0 || cin % 8 || lda % 4 || (uintptr_t)A % 16)
         return mtts::fail(MTTS_ERR_SHAPE, "conv_gemm: cin must be a multiple of 8, lda of 4, A 16-byte aligned");
-    if (ntaps < 1 || ntaps > MTTS_CONV_MAX_TAPS) return mtts::fail(MTTS_ERR_SHAPE, "conv_gemm: 1..4 taps");
+    if (ntaps < 1 || ntaps > MTTS_CONV_MAX_TAPS) return mtts::fail(MTTS_ERR_SHAPE, "conv_gemm: 1..8 taps");
     if (K != ntaps * cin) return mtts::fail(MTTS_ERR_SHAPE, "conv_gemm: K != ntaps*cin");
     return MTTS_OK;
 }
@@ -590,8 +576,9 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     MTTS_CHECK_ARG(p.Kp >= p.K && p.Kp % 8 == 0, "conv_gemm: Kp must be >= K and a multiple of 8");
     MTTS_CHECK_ARG((uintptr_t)p.W % 16 == 0, "conv_gemm: W must be 16-byte aligned");
     MTTS_CHECK_ARG(precision == MTTS_PREC_BF16 || precision == MTTS_PREC_FP32, "conv_gemm: bad precision");
-    MTTS_CHECK_ARG(p.act >= MTTS_ACT_NONE && p.act <= MTTS_ACT_DGELU, "conv_gemm: bad act");
-    MTTS_CHECK_ARG(p.act != MTTS_ACT_DGELU || p.aux, "conv_gemm: MTTS_ACT_DGELU needs aux");
+    MTTS_CHECK_ARG(p.act >= MTTS_ACT_NONE && p.act <= MTTS_ACT_DRELU, "conv_gemm: bad act");
+    MTTS_CHECK_ARG((p.act != MTTS_ACT_DGELU && p.act != MTTS_ACT_DRELU) || p.aux,
+                   "conv_gemm: MTTS_ACT_DGELU / MTTS_ACT_DRELU need aux");
     MTTS_CHECK_ARG(p.dropout_p <= 0.f || (p.seed && p.dropout_p < 1.f), "conv_gemm: dropout needs a seed pointer");
     MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || cfg == MTTS_GEMM_PANEL, "conv_gemm: bad tile config");
     const int M = p.nb * p.To;
@@ -638,6 +625,32 @@ extern "C" int mtts_dropout_apply(const float *x, float *y, int32_t rows, int32_
     hipLaunchKernelGGL(dropout_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(hip_stream), x, y, rows, cols, ld, p, seed);
     return mtts::check_launch("dropout_apply_kernel");
+}
+
+// dx = dy * [y > 0] (act RELU) * keep(seed, r, c) / (1-p) (p > 0): the backward of a GEMM epilogue
+// "ReLU -> dropout" from its output y (kept and positive <=> pre-activation positive).
+__global__ void act_dropout_bwd_kernel(const float *__restrict__ dy, const float *__restrict__ y, float *__restrict__ dx,
+                                       int rows, int cols, int ld, int act, float p, const uint32_t *__restrict__ seed) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)rows * cols) return;
+    const int r = (int)(idx / cols), c = (int)(idx - (int64_t)r * cols);
+    const size_t o = (size_t)r * ld + c;
+    float v = dy[o];
+    if (act == MTTS_ACT_RELU && !(y[o] > 0.f)) v = 0.f;
+    if (p > 0.f) v = mtts::dropout_keep(seed[0], seed[1], (uint32_t)r, (uint32_t)c, p) ? v * (1.0f / (1.0f - p)) : 0.f;
+    dx[o] = v;
+}
+
+extern "C" int mtts_act_dropout_bwd(const float *dy, const float *y, float *dx, int32_t rows, int32_t cols, int32_t ld,
+                                    int32_t act, float p, const uint32_t *seed, void *hip_stream) {
+    MTTS_CHECK_ARG(dy && dx && rows >= 0 && cols >= 0 && ld >= cols && p >= 0.f && p < 1.f && (p == 0.f || seed),
+                   "act_dropout_bwd: bad args");
+    MTTS_CHECK_ARG(act == MTTS_ACT_NONE || (act == MTTS_ACT_RELU && y), "act_dropout_bwd: act NONE, or RELU with y");
+    const int64_t n = (int64_t)rows * cols;
+    if (n == 0) return MTTS_OK;
+    hipLaunchKernelGGL(act_dropout_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(hip_stream), dy, y, dx, rows, cols, ld, act, p, seed);
+    return mtts::check_launch("act_dropout_bwd_kernel");
 }
 
 static void wgrad_plan(const mtts_conv_wgrad_args &p, int *splits, int *rows_per_split) {

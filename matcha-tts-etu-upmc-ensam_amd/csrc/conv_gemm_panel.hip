@@ -37,14 +37,6 @@ constexpr int kWChunks = kBN * kBK / 8 / kThreads;  // 16-byte W chunks per thre
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
     return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)b) << 16);
 }
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_erf_grad(float x) {
-    const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-    return cdf + x * expf(-0.5f * x * x) * 0.39894228040143268f;
-}
-__device__ __forceinline__ int tap_off(const mtts_conv_gemm_args &p, int j) {
-    return j == 0 ? p.off[0] : j == 1 ? p.off[1] : j == 2 ? p.off[2] : p.off[3];
-}
 
 struct PanelGeom {
     int min_off, span, R, ld;  // panel rows R, LDS row length ld (bf16 elements)
@@ -179,7 +171,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_panel_kernel(mtts_conv_
                 const int kk = k0 + ks * 16 + 8 * lh;
                 bf16x8 af;
                 if (kk < p.K) {
-                    const int prow = lr * p.in_stride + tap_off(p, tj[ks]) - g.min_off;
+                    const int prow = lr * p.in_stride + mtts::tap_off(p, tj[ks]) - g.min_off;
                     af = *reinterpret_cast<const bf16x8 *>(panel + (size_t)prow * g.ld + tc[ks]);
                 } else {
                     af = bf16x8{};
@@ -227,8 +219,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_gemm_panel_kernel(mtts_conv_
                 const int dr = r * p.out_stride;
                 float val = acc[t][v] + bn;
                 if (p.C_pre) p.C_pre[row0 * p.ldc + dr * p.ldc + n] = val;
-                if (p.act == MTTS_ACT_GELU) val = gelu_erf(val);
-                else if (p.act == MTTS_ACT_DGELU) val *= gelu_erf_grad(p.aux[row0 * p.ldaux + dr * p.ldaux + n]);
+                if (p.act) val = mtts::epi_act(p.act, val, p.aux + row0 * p.ldaux + dr * p.ldaux + n);
                 if (p.dropout_p > 0.f)
                     val = mtts::dropout_keep(s0, s1, (uint32_t)row0 + (uint32_t)dr, (uint32_t)n, p.dropout_p)
                               ? val * (1.0f / (1.0f - p.dropout_p))

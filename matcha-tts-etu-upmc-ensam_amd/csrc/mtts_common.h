@@ -6,6 +6,7 @@
 #include <cstdint>
 
 #include "mtts.h"
+#include "mtts_decoder.h"
 
 namespace mtts {
 
@@ -36,6 +37,35 @@ __device__ __forceinline__ bool dropout_keep(uint32_t seed_lo, uint32_t seed_hi,
     x ^= seed_hi;
     x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
     return (float)(x >> 8) * (1.0f / 16777216.0f) >= p;
+}
+
+// Tap offset j of a conv argument struct (static indexing only: no private-memory copy of off[]).
+template <class P>
+__device__ __forceinline__ int tap_off(const P &p, int j) {
+    int o = p.off[0];
+#pragma unroll
+    for (int i = 1; i < MTTS_CONV_MAX_TAPS; ++i) o = j == i ? p.off[i] : o;
+    return o;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+// d/dx erf-GELU, as torch's GeluBackward (cdf + x * pdf)
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+    const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+    const float pdf = expf(-0.5f * x * x) * 0.39894228040143268f;
+    return cdf + x * pdf;
+}
+
+// GEMM epilogue activation (include/mtts_decoder.h MTTS_ACT_*); aux is read only by the D-variants.
+__device__ __forceinline__ float epi_act(int act, float v, const float *aux) {
+    switch (act) {
+        case MTTS_ACT_GELU: return gelu_erf(v);
+        case MTTS_ACT_DGELU: return v * gelu_erf_grad(*aux);
+        case MTTS_ACT_RELU: return fmaxf(v, 0.f);
+        case MTTS_ACT_DRELU: return *aux > 0.f ? v : 0.f;
+        default: return v;
+    }
 }
 
 }  // namespace mtts

@@ -214,7 +214,8 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float *__restrict__ i
 __global__ __launch_bounds__(kThreads) void layernorm_fwd_kernel(const float *__restrict__ x, const float *__restrict__ w,
                                                                  const float *__restrict__ bia, float *__restrict__ y,
                                                                  float *__restrict__ mean_out, float *__restrict__ rstd_out,
-                                                                 int M, int C, float eps) {
+                                                                 int M, int C, float eps, int act, float p,
+                                                                 const uint32_t *__restrict__ seed) {
     const int row = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= M) return;
@@ -243,18 +244,28 @@ __global__ __launch_bounds__(kThreads) void layernorm_fwd_kernel(const float *__
         rstd_out[row] = rstd;
     }
     float *yr = y + (size_t)row * C;
+    uint32_t sd0 = 0, sd1 = 0;  // dropout seed words
+    if (p > 0.f) {
+        sd0 = seed[0];
+        sd1 = seed[1];
+    }
+    const float inv_keep = 1.f / (1.f - p);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int c = lane * 4 + 256 * i;
         if (c < C) {
             const float4 ww = *reinterpret_cast<const float4 *>(w + c);
             const float4 bb = *reinterpret_cast<const float4 *>(bia + c);
-            float4 o;
-            o.x = (v[i].x - mean) * rstd * ww.x + bb.x;
-            o.y = (v[i].y - mean) * rstd * ww.y + bb.y;
-            o.z = (v[i].z - mean) * rstd * ww.z + bb.z;
-            o.w = (v[i].w - mean) * rstd * ww.w + bb.w;
-            *reinterpret_cast<float4 *>(yr + c) = o;
+            float o[4] = {(v[i].x - mean) * rstd * ww.x + bb.x, (v[i].y - mean) * rstd * ww.y + bb.y,
+                          (v[i].z - mean) * rstd * ww.z + bb.z, (v[i].w - mean) * rstd * ww.w + bb.w};
+            if (act == MTTS_ACT_RELU || p > 0.f) {  // fused tail: ReLU then dropout (ConvReluNorm order)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (act == MTTS_ACT_RELU) o[j] = fmaxf(o[j], 0.f);
+                    if (p > 0.f) o[j] = mtts::dropout_keep(sd0, sd1, (uint32_t)row, (uint32_t)(c + j), p) ? o[j] * inv_keep : 0.f;
+                }
+            }
+            *reinterpret_cast<float4 *>(yr + c) = make_float4(o[0], o[1], o[2], o[3]);
         }
     }
 }
@@ -262,22 +273,30 @@ __global__ __launch_bounds__(kThreads) void layernorm_fwd_kernel(const float *__
 constexpr int kLnRowsPerBlock = 128;  // backward: rows per block (32 per wave)
 
 __global__ __launch_bounds__(kThreads) void layernorm_bwd_kernel(const float *__restrict__ dy, const float *__restrict__ x,
-                                                                 const float *__restrict__ w,
+                                                                 const float *__restrict__ w, const float *__restrict__ bia,
                                                                  const float *__restrict__ mean_in,
                                                                  const float *__restrict__ rstd_in, float *__restrict__ dx,
                                                                  float *__restrict__ pw, float *__restrict__ pb, int M,
-                                                                 int C) {
+                                                                 int C, int act, float p, const uint32_t *__restrict__ seed) {
     __shared__ float4 red[2][kThreads / 64][256];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float4 aw[4], ab[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) aw[i] = ab[i] = make_float4(0, 0, 0, 0);
-    float4 ww[4];
+    float4 ww[4], bb[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int c = lane * 4 + 256 * i;
         ww[i] = c < C ? *reinterpret_cast<const float4 *>(w + c) : make_float4(0, 0, 0, 0);
+        bb[i] = (c < C && act == MTTS_ACT_RELU) ? *reinterpret_cast<const float4 *>(bia + c) : make_float4(0, 0, 0, 0);
     }
+    const bool tail = act == MTTS_ACT_RELU || p > 0.f;
+    uint32_t sd0 = 0, sd1 = 0;  // dropout seed words
+    if (p > 0.f) {
+        sd0 = seed[0];
+        sd1 = seed[1];
+    }
+    const float inv_keep = 1.f / (1.f - p);
     const int rbeg = blockIdx.x * kLnRowsPerBlock;
     for (int rr = wv; rr < kLnRowsPerBlock; rr += kThreads / 64) {
         const int row = rbeg + rr;
@@ -290,9 +309,22 @@ __global__ __launch_bounds__(kThreads) void layernorm_bwd_kernel(const float *__
             const int c = lane * 4 + 256 * i;
             if (c < C) {
                 const float4 xv = *reinterpret_cast<const float4 *>(x + (size_t)row * C + c);
-                const float4 dv = *reinterpret_cast<const float4 *>(dy + (size_t)row * C + c);
+                float4 dv = *reinterpret_cast<const float4 *>(dy + (size_t)row * C + c);
                 xh[i] = make_float4((xv.x - mean) * rstd, (xv.y - mean) * rstd, (xv.z - mean) * rstd,
                                     (xv.w - mean) * rstd);
+                if (tail) {  // through the fused tail: regenerate the dropout mask, ReLU gate from the LN output
+                    float d4[4] = {dv.x, dv.y, dv.z, dv.w};
+                    const float xs[4] = {xh[i].x, xh[i].y, xh[i].z, xh[i].w};
+                    const float w4[4] = {ww[i].x, ww[i].y, ww[i].z, ww[i].w};
+                    const float b4[4] = {bb[i].x, bb[i].y, bb[i].z, bb[i].w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (p > 0.f)
+                            d4[j] = mtts::dropout_keep(sd0, sd1, (uint32_t)row, (uint32_t)(c + j), p) ? d4[j] * inv_keep : 0.f;
+                        if (act == MTTS_ACT_RELU && xs[j] * w4[j] + b4[j] <= 0.f) d4[j] = 0.f;
+                    }
+                    dv = make_float4(d4[0], d4[1], d4[2], d4[3]);
+                }
                 g[i] = make_float4(dv.x * ww[i].x, dv.y * ww[i].y, dv.z * ww[i].z, dv.w * ww[i].w);
                 s1 += (g[i].x + g[i].y) + (g[i].z + g[i].w);
                 s2 += (g[i].x * xh[i].x + g[i].y * xh[i].y) + (g[i].z * xh[i].z + g[i].w * xh[i].w);
@@ -381,14 +413,17 @@ extern "C" int mtts_gn_mish_bwd(const float *dy, const float *h, const float *ga
 }
 
 extern "C" int mtts_layernorm_fwd(const float *x, const float *w, const float *b, float *y, float *mean,
-                                  float *rstd, int32_t M, int32_t C, float eps, void *hip_stream) {
+                                  float *rstd, int32_t M, int32_t C, float eps, int32_t act, float dropout_p,
+                                  const uint32_t *seed, void *hip_stream) {
     MTTS_CHECK_ARG(x && w && b && y && mean && rstd, "layernorm_fwd: null pointer");
+    MTTS_CHECK_ARG(act == MTTS_ACT_NONE || act == MTTS_ACT_RELU, "layernorm_fwd: act must be NONE or RELU");
+    MTTS_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed), "layernorm_fwd: bad dropout");
     MTTS_CHECK_ARG(M >= 0 && C >= 4 && C % 4 == 0 && C <= 1024, "layernorm_fwd: need C % 4 == 0, C <= 1024");
     MTTS_CHECK_ARG(aligned16(x) && aligned16(y) && aligned16(w) && aligned16(b), "layernorm_fwd: 16-byte alignment");
     if (M == 0) return MTTS_OK;
     const int rows_per_block = kThreads / 64;
     hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((M + rows_per_block - 1) / rows_per_block), dim3(kThreads), 0,
-                       static_cast<hipStream_t>(hip_stream), x, w, b, y, mean, rstd, M, C, eps);
+                       static_cast<hipStream_t>(hip_stream), x, w, b, y, mean, rstd, M, C, eps, act, dropout_p, seed);
     return mtts::check_launch("layernorm_fwd_kernel");
 }
 
@@ -397,10 +432,13 @@ extern "C" size_t mtts_layernorm_bwd_workspace_size(int32_t M, int32_t C) {
     return (size_t)2 * ((M + kLnRowsPerBlock - 1) / kLnRowsPerBlock) * C * sizeof(float);
 }
 
-extern "C" int mtts_layernorm_bwd(const float *dy, const float *x, const float *w, const float *mean,
+extern "C" int mtts_layernorm_bwd(const float *dy, const float *x, const float *w, const float *b, const float *mean,
                                   const float *rstd, float *dx, float *dw, float *db, int32_t M, int32_t C,
-                                  void *workspace, size_t workspace_bytes, void *hip_stream) {
+                                  int32_t act, float dropout_p, const uint32_t *seed, void *workspace,
+                                  size_t workspace_bytes, void *hip_stream) {
     MTTS_CHECK_ARG(dy && x && w && mean && rstd && dx, "layernorm_bwd: null pointer");
+    MTTS_CHECK_ARG(act == MTTS_ACT_NONE || (act == MTTS_ACT_RELU && b), "layernorm_bwd: act RELU needs b");
+    MTTS_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed), "layernorm_bwd: bad dropout");
     MTTS_CHECK_ARG(M >= 0 && C >= 4 && C % 4 == 0 && C <= 1024, "layernorm_bwd: need C % 4 == 0, C <= 1024");
     MTTS_CHECK_ARG(aligned16(dy) && aligned16(x) && aligned16(dx) && aligned16(w), "layernorm_bwd: 16-byte alignment");
     if (M == 0) return MTTS_OK;
@@ -410,7 +448,8 @@ extern "C" int mtts_layernorm_bwd(const float *dy, const float *x, const float *
     const int nblk = (M + kLnRowsPerBlock - 1) / kLnRowsPerBlock;
     float *pw = static_cast<float *>(workspace);
     float *pb = pw + (size_t)nblk * C;
-    hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(nblk), dim3(kThreads), 0, st, dy, x, w, mean, rstd, dx, pw, pb, M, C);
+    hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(nblk), dim3(kThreads), 0, st, dy, x, w, b, mean, rstd, dx, pw, pb, M,
+                       C, act, dropout_p, seed);
     int rc = mtts::check_launch("layernorm_bwd_kernel");
     if (rc) return rc;
     if (dw) hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pw, nblk, C, dw);

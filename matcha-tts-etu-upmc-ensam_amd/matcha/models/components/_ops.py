@@ -31,7 +31,7 @@ import torch.nn.functional as F
 from matcha import _native as N
 
 PREC_FP32, PREC_BF16 = 0, 1
-ACT_NONE, ACT_GELU, ACT_DGELU = 0, 1, 2
+ACT_NONE, ACT_GELU, ACT_DGELU, ACT_RELU, ACT_DRELU = 0, 1, 2, 3, 4
 
 KERNELS: dict[str, str] = {
     "conv_tm": "mtts_conv_gemm/mtts_conv_wgrad",
@@ -40,6 +40,8 @@ KERNELS: dict[str, str] = {
     "ff_tm": "mtts_conv_gemm/mtts_conv_wgrad",
     "group_norm_mish_tm": "mtts_gn_mish_fwd/mtts_gn_mish_bwd",
     "layer_norm_tm": "mtts_layernorm_fwd/mtts_layernorm_bwd",
+    "conv_ffn_tm": "mtts_conv_gemm/mtts_conv_wgrad/mtts_act_dropout_bwd",
+    "rope_tm": "mtts_rope_qk",
     "attention_tm": "mtts_attention_fwd/mtts_attention_bwd",
 }
 
@@ -47,7 +49,7 @@ KERNELS: dict[str, str] = {
 class ConvGemmArgs(ctypes.Structure):
     _fields_ = [("A", ctypes.c_void_p), ("a_scale", ctypes.c_void_p), ("lda", ctypes.c_int32),
                 ("Ti", ctypes.c_int32), ("To", ctypes.c_int32), ("nb", ctypes.c_int32),
-                ("in_stride", ctypes.c_int32), ("ntaps", ctypes.c_int32), ("off", ctypes.c_int32 * 4),
+                ("in_stride", ctypes.c_int32), ("ntaps", ctypes.c_int32), ("off", ctypes.c_int32 * 8),
                 ("cin", ctypes.c_int32), ("W", ctypes.c_void_p), ("N", ctypes.c_int32), ("K", ctypes.c_int32),
                 ("Kp", ctypes.c_int32), ("bias", ctypes.c_void_p), ("act", ctypes.c_int32),
                 ("residual", ctypes.c_void_p), ("ldr", ctypes.c_int32), ("c_scale", ctypes.c_void_p),
@@ -62,7 +64,7 @@ class ConvWgradArgs(ctypes.Structure):
                 ("out_stride", ctypes.c_int32), ("out_off", ctypes.c_int32), ("A", ctypes.c_void_p),
                 ("a_scale", ctypes.c_void_p), ("lda", ctypes.c_int32), ("Ti", ctypes.c_int32),
                 ("To", ctypes.c_int32), ("nb", ctypes.c_int32), ("in_stride", ctypes.c_int32),
-                ("ntaps", ctypes.c_int32), ("off", ctypes.c_int32 * 4), ("cin", ctypes.c_int32),
+                ("ntaps", ctypes.c_int32), ("off", ctypes.c_int32 * 8), ("cin", ctypes.c_int32),
                 ("N", ctypes.c_int32), ("K", ctypes.c_int32)]
 
 
@@ -70,7 +72,8 @@ class AttnArgs(ctypes.Structure):
     _fields_ = [("q", ctypes.c_void_p), ("k", ctypes.c_void_p), ("v", ctypes.c_void_p), ("ldq", ctypes.c_int32),
                 ("key_bias", ctypes.c_void_p), ("o", ctypes.c_void_p), ("ldo", ctypes.c_int32),
                 ("lse", ctypes.c_void_p), ("B", ctypes.c_int32), ("T", ctypes.c_int32), ("H", ctypes.c_int32),
-                ("D", ctypes.c_int32), ("scale", ctypes.c_float)]
+                ("D", ctypes.c_int32), ("scale", ctypes.c_float), ("dropout_p", ctypes.c_float),
+                ("seed", ctypes.c_void_p)]
 
 
 class AttnGrads(ctypes.Structure):
@@ -95,10 +98,13 @@ N.register("mtts_gn_mish_fwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I
 N.register("mtts_gn_mish_bwd_workspace_size", _SZ, [_I, _I])
 N.register("mtts_gn_mish_bwd", ctypes.c_int,
            [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _SZ, _P])
-N.register("mtts_layernorm_fwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
+N.register("mtts_layernorm_fwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _I, _F, _I, _F, _P, _P])
 N.register("mtts_layernorm_bwd_workspace_size", _SZ, [_I, _I])
-N.register("mtts_layernorm_bwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P])
+N.register("mtts_layernorm_bwd", ctypes.c_int,
+           [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _SZ, _P])
 N.register("mtts_dropout_apply", ctypes.c_int, [_P, _P, _I, _I, _I, _F, _P, _P])
+N.register("mtts_act_dropout_bwd", ctypes.c_int, [_P, _P, _P, _I, _I, _I, _I, _F, _P, _P])
+N.register("mtts_rope_qk", ctypes.c_int, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P])
 N.register("mtts_pack_weights", ctypes.c_int, [ctypes.POINTER(PackJob), _I, _I, _P])
 N.register("mtts_attention_fwd", ctypes.c_int, [ctypes.POINTER(AttnArgs), _I, _P])
 N.register("mtts_attention_bwd_workspace_size", _SZ, [_I, _I, _I])
@@ -160,7 +166,7 @@ def spec_linear(ws, dgrad=False):
     """Linear weights [N_i, K] stacked along N -> [sum N_i, Kp] (forward); dgrad: the transpose
     [K, sum N_i] (column blocks; each N_i % 8 == 0 when stacking)."""
     ws = tuple(ws)
-    K = ws[0].shape[1]
+    K = ws[0].shape[1]  # nn.Conv1d 1x1 weights [N, K, 1] have the Linear layout
     if not dgrad:
         jobs, r0 = [], 0
         for w in ws:
@@ -321,11 +327,13 @@ def _check(*ts):
 
 # ------------------------------------------------------------------------------------------ conv
 class _ConvTM(torch.autograd.Function):
-    """y[b,u] = bias + sum_j W_j (x*m)[b, u*stride + j - pad]   (nn.Conv1d on x*mask, token-major)."""
+    """y[b,u] = (residual + dropout(act(bias + sum_j W_j (x*m)[b, u*stride + j - pad]))) * out_scale
+    (nn.Conv1d on x*mask, token-major; act None or ReLU; residual only without act/dropout)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, mask, out_scale, stride, padding):
-        _check(x, weight, mask)
+    def forward(ctx, x, weight, bias, mask, out_scale, stride, padding, act, dropout_p, residual):
+        _check(x, weight, mask, residual)
+        assert residual is None or (act == ACT_NONE and dropout_p == 0.0)
         prec = gemm_precision()
         x = _f32c(x)
         B, Ti, Cin = x.shape
@@ -342,19 +350,28 @@ class _ConvTM(torch.autograd.Function):
         mask = _f32c(mask)
         out_scale = _f32c(out_scale)
         bias_c = _f32c(bias)
+        seed = _new_seed(x.device) if dropout_p > 0 else None
         _gemm(x, Ti, To, B, stride, [j - padding for j in range(k)], Cin, Wp, Kp, Cout, y, To, prec=prec,
-              a_scale=mask, bias=bias_c, c_scale=out_scale)
-        ctx.save_for_backward(x, weight, mask, out_scale)
-        ctx.cfg = (stride, padding, prec, bias is not None)
+              a_scale=mask, bias=bias_c, c_scale=out_scale, act=act, dropout_p=dropout_p, seed=seed,
+              residual=_f32c(residual))
+        ctx.save_for_backward(x, weight, mask, out_scale, y if act != ACT_NONE else None)
+        ctx.cfg = (stride, padding, prec, bias is not None, act, dropout_p, seed, residual is not None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, mask, out_scale = ctx.saved_tensors
-        stride, pad, prec, has_bias = ctx.cfg
+        x, weight, mask, out_scale, y = ctx.saved_tensors
+        stride, pad, prec, has_bias, act, p, seed, has_res = ctx.cfg
         dy = _f32c(dy)
         if out_scale is not None:
             dy = dy * out_scale.unsqueeze(-1)
+        dres = dy if has_res else None
+        if act != ACT_NONE or p > 0:  # through the epilogue ReLU / dropout (gate from the output y)
+            g = torch.empty_like(dy)
+            N.check(N.lib().mtts_act_dropout_bwd(dy.data_ptr(), N.ptr(y), g.data_ptr(), dy.shape[0] * dy.shape[1],
+                                                 dy.shape[2], dy.shape[2], act, float(p), N.ptr(seed), _stream(g)),
+                    "mtts_act_dropout_bwd")
+            dy = g
         B, Ti, Cin = x.shape
         Cout, _, k = weight.shape
         To = dy.shape[1]
@@ -381,7 +398,7 @@ class _ConvTM(torch.autograd.Function):
             db = torch.empty(Cout, device=x.device, dtype=torch.float32) if has_bias else None
             _wgrad(dy, To, 1, 0, x, Ti, To, B, stride, [j - pad for j in range(k)], Cin, Cout, dw,
                    (Cin * k, k, 1), prec=prec, a_scale=mask, db=db)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, dres
 
 
 class _ConvTransposeTM(torch.autograd.Function):
@@ -442,33 +459,39 @@ class _LinearTM(torch.autograd.Function):
     several weights stacked along N (the fused q|k|v projection), each receiving its own gradient."""
 
     @staticmethod
-    def forward(ctx, x, bias, residual, dropout_p, *weights):
-        _check(x, residual, *weights)
+    def forward(ctx, x, bias, residual, dropout_p, in_scale, out_scale, *weights):
+        _check(x, residual, in_scale, out_scale, *weights)
         prec = gemm_precision()
         shp = x.shape
         x2 = _f32c(x).reshape(-1, shp[-1])
         M, K = x2.shape
         Nout = sum(w.shape[0] for w in weights)
+        assert all(w.dim() == 2 or (w.dim() == 3 and w.shape[2] == 1) for w in weights)
         Wp, Kp = packed(spec_linear(weights), prec)
         ctx.wd = packed(spec_linear(weights, dgrad=True), prec) if ctx.needs_input_grad[0] else None
         y = torch.empty(M, Nout, device=x.device, dtype=torch.float32)
         res2 = _f32c(residual).reshape(M, Nout) if residual is not None else None
         seed = _new_seed(x.device) if dropout_p > 0 else None
+        ins = _f32c(in_scale).reshape(M) if in_scale is not None else None
+        outs = _f32c(out_scale).reshape(M) if out_scale is not None else None
         _gemm(x2, M, M, 1, 1, [0], K, Wp, Kp, Nout, y, M, prec=prec, bias=_f32c(bias), residual=res2,
-              dropout_p=dropout_p, seed=seed)
-        ctx.save_for_backward(x2)
+              dropout_p=dropout_p, seed=seed, a_scale=ins, c_scale=outs)
+        ctx.save_for_backward(x2, ins, outs)
         ctx.cfg = (prec, bias is not None, residual is not None, shp, dropout_p, seed,
                    [w.shape[0] for w in weights], K)
+        ctx.wshapes = [w.shape for w in weights]
         return y.reshape(*shp[:-1], Nout)
 
     @staticmethod
     def backward(ctx, dy):
-        (x2,) = ctx.saved_tensors
+        x2, ins, outs = ctx.saved_tensors
         prec, has_bias, has_res, shp, p, seed, rows, K = ctx.cfg
         Nout = sum(rows)
         dy2 = _f32c(dy).reshape(-1, Nout)
         M = dy2.shape[0]
-        dres = dy if has_res else None
+        if outs is not None:  # y = (residual + z) * out_scale
+            dy2 = dy2 * outs.unsqueeze(-1)
+        dres = dy2.reshape(dy.shape) if has_res else None
         if p > 0:  # gradient through the epilogue dropout: regenerate the forward's mask
             g = torch.empty_like(dy2)
             N.check(N.lib().mtts_dropout_apply(dy2.data_ptr(), g.data_ptr(), M, Nout, Nout, float(p),
@@ -476,17 +499,23 @@ class _LinearTM(torch.autograd.Function):
             dy2 = g
         dx = db = None
         dws = [None] * len(rows)
+        Np = _r8(Nout)
+        if Np != Nout:  # narrow outputs (the duration predictor's 1-channel projection): zero-pad dy to 8
+            dyp = torch.zeros(M, Np, device=dy2.device, dtype=torch.float32)  # columns; W^T is packed with
+            dyp[:, :Nout] = dy2  # zero columns to Np already, so dgrad is exact; dW/db keep rows < Nout
+            dy2 = dyp
         if ctx.needs_input_grad[0]:
             Wd, Kp = ctx.wd
             dx = torch.empty(M, K, device=dy2.device, dtype=torch.float32)
-            _gemm(dy2, M, M, 1, 1, [0], Nout, Wd, Kp, K, dx, M, prec=prec)
+            _gemm(dy2, M, M, 1, 1, [0], Np, Wd, Kp, K, dx, M, prec=prec, c_scale=ins)
             dx = dx.reshape(*shp)
-        if any(ctx.needs_input_grad[4:]) or (has_bias and ctx.needs_input_grad[1]):
-            dw = torch.empty(Nout, K, device=dy2.device, dtype=torch.float32)
-            db = torch.empty(Nout, device=dy2.device, dtype=torch.float32) if has_bias else None
-            _wgrad(dy2, M, 1, 0, x2, M, M, 1, 1, [0], K, Nout, dw, (K, 1, 0), prec=prec, db=db)
-            dws = list(dw.split(rows, dim=0))
-        return (dx, db, dres, None, *dws)
+        if any(ctx.needs_input_grad[6:]) or (has_bias and ctx.needs_input_grad[1]):
+            dw = torch.empty(Np, K, device=dy2.device, dtype=torch.float32)
+            db = torch.empty(Np, device=dy2.device, dtype=torch.float32) if has_bias else None
+            _wgrad(dy2, M, 1, 0, x2, M, M, 1, 1, [0], K, Np, dw, (K, 1, 0), prec=prec, db=db, a_scale=ins)
+            dws = [d.view(w_shape) for d, w_shape in zip(dw[:Nout].split(rows, dim=0), ctx.wshapes)]
+            db = db[:Nout] if db is not None else None
+        return (dx, db, dres, None, None, None, *dws)
 
 
 class _FeedForwardTM(torch.autograd.Function):
@@ -547,6 +576,83 @@ class _FeedForwardTM(torch.autograd.Function):
                 None)
 
 
+class _ConvFFNTM(torch.autograd.Function):
+    """The text encoder's FFN + residual (text_encoder.py:235-253, 307-313), token-major:
+        h = dropout_in(relu(conv1(x * m)))              (epilogue ReLU + dropout, h stored)
+        y = (residual + dropout_out(conv2(h))) * m       (epilogue dropout, residual, row mask)
+    The reference masks only the FFN's input and output (conv_net(x * x_mask) * x_mask): conv2 reads
+    the UNMASKED h, so rows next to the padding see the padded rows' relu(bias + leakage).
+    dropout_out is the FFN's own Dropout followed by the Encoder's self.dropout: two independent
+    Bernoulli(1-p) masks are one Bernoulli((1-p)^2) mask with scale 1/(1-p)^2 -- same distribution.
+    Backward: regenerated masks; ReLU' folded into conv2's dgrad epilogue (gate = h > 0)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, mask, residual, p_in, p_out):
+        _check(x, w1, w2, mask, residual)
+        prec = gemm_precision()
+        x = _f32c(x)
+        B, T, Cin = x.shape
+        F_, _, k = w1.shape
+        Cout = w2.shape[0]
+        pad = k // 2
+        offs = [j - pad for j in range(k)]
+        m = _f32c(mask)
+        W1p, K1p = packed(spec_conv_fwd(w1), prec)
+        W2p, K2p = packed(spec_conv_fwd(w2), prec)
+        ctx.w2d = packed(spec_conv_dgrad(w2), prec) if any(ctx.needs_input_grad) else None
+        ctx.w1d = packed(spec_conv_dgrad(w1), prec) if ctx.needs_input_grad[0] else None
+        s1 = _new_seed(x.device) if p_in > 0 else None
+        s2 = _new_seed(x.device) if p_out > 0 else None
+        h = torch.empty(B, T, F_, device=x.device, dtype=torch.float32)
+        _gemm(x, T, T, B, 1, offs, Cin, W1p, K1p, F_, h, T, prec=prec, a_scale=m, bias=_f32c(b1), act=ACT_RELU,
+              dropout_p=p_in, seed=s1)
+        y = torch.empty(B, T, Cout, device=x.device, dtype=torch.float32)
+        _gemm(h, T, T, B, 1, offs, F_, W2p, K2p, Cout, y, T, prec=prec, bias=_f32c(b2), dropout_p=p_out,
+              seed=s2, residual=_f32c(residual), c_scale=m)
+        ctx.save_for_backward(x, h, m)
+        ctx.cfg = (prec, k, p_in, p_out, s1, s2, residual is not None, w1.shape, w2.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, h, m = ctx.saved_tensors
+        prec, k, p_in, p_out, s1, s2, has_res, w1s, w2s = ctx.cfg
+        B, T, Cin = x.shape
+        F_, Cout = w1s[0], w2s[0]
+        pad = k // 2
+        offs = [j - pad for j in range(k)]
+        doffs = [pad - j for j in range(k)]
+        g = _f32c(dy) * m.unsqueeze(-1)
+        dres = g if has_res else None
+        dz2 = g
+        if p_out > 0:
+            dz2 = torch.empty_like(g)
+            N.check(N.lib().mtts_act_dropout_bwd(g.data_ptr(), None, dz2.data_ptr(), B * T, Cout, Cout, ACT_NONE,
+                                                 float(p_out), s2.data_ptr(), _stream(g)), "mtts_act_dropout_bwd")
+        dw2 = torch.empty(w2s, device=x.device, dtype=torch.float32)
+        db2 = torch.empty(Cout, device=x.device, dtype=torch.float32)
+        _wgrad(dz2, T, 1, 0, h, T, T, B, 1, offs, F_, Cout, dw2, (F_ * k, k, 1), prec=prec, db=db2)
+        W2d, K2d = ctx.w2d
+        dz1 = torch.empty_like(h)  # d(conv1 pre-activation) = dgrad * [h > 0] * keep_in / (1 - p_in)
+        _gemm(dz2, T, T, B, 1, doffs, Cout, W2d, K2d, F_, dz1, T, prec=prec, act=ACT_DRELU, aux=h,
+              dropout_p=p_in, seed=s1)
+        dw1 = torch.empty(w1s, device=x.device, dtype=torch.float32)
+        db1 = torch.empty(F_, device=x.device, dtype=torch.float32)
+        _wgrad(dz1, T, 1, 0, x, T, T, B, 1, offs, Cin, F_, dw1, (Cin * k, k, 1), prec=prec, a_scale=m, db=db1)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            W1d, K1d = ctx.w1d
+            dx = torch.empty_like(x)
+            _gemm(dz1, T, T, B, 1, doffs, F_, W1d, K1d, Cin, dx, T, prec=prec, c_scale=m)
+        return dx, dw1, db1, dw2, db2, None, dres, None, None
+
+
+def conv_ffn_tm(x, w1, b1, w2, b2, mask, residual=None, p_in: float = 0.0, p_out: float = 0.0):
+    """(residual + dropout_out(conv2(dropout_in(relu(conv1(x*m)))))) * m, token-major (text encoder
+    FFN, text_encoder.py:235-253); conv weights [F, Cin, k] / [Cout, F, k], odd k <= 8."""
+    return _ConvFFNTM.apply(x, w1, b1, w2, b2, mask, residual, float(p_in), float(p_out))
+
+
 # ------------------------------------------------------------------------------------------ norms
 class _GroupNormMishTM(torch.autograd.Function):
     @staticmethod
@@ -585,8 +691,11 @@ class _GroupNormMishTM(torch.autograd.Function):
 
 
 class _LayerNormTM(torch.autograd.Function):
+    """LayerNorm over the last dim, optionally followed by a fused ReLU and/or dropout (the text
+    encoder's LN -> ReLU -> Dropout and LN -> Dropout, text_encoder.py:48-55, 81-95)."""
+
     @staticmethod
-    def forward(ctx, x, w, b, eps):
+    def forward(ctx, x, w, b, eps, act, dropout_p):
         _check(x, w)
         shp = x.shape
         x2 = _f32c(x).reshape(-1, shp[-1])
@@ -595,16 +704,18 @@ class _LayerNormTM(torch.autograd.Function):
         mean = torch.empty(M, device=x.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
         w_c, b_c = _f32c(w), _f32c(b)
+        seed = _new_seed(x.device) if dropout_p > 0 else None
         N.check(N.lib().mtts_layernorm_fwd(x2.data_ptr(), w_c.data_ptr(), b_c.data_ptr(), y.data_ptr(),
-                                           mean.data_ptr(), rstd.data_ptr(), M, C, float(eps), _stream(x2)),
-                "mtts_layernorm_fwd")
-        ctx.save_for_backward(x2, w_c, mean, rstd)
-        ctx.shp = shp
+                                           mean.data_ptr(), rstd.data_ptr(), M, C, float(eps), act, float(dropout_p),
+                                           N.ptr(seed), _stream(x2)), "mtts_layernorm_fwd")
+        ctx.save_for_backward(x2, w_c, b_c, mean, rstd)
+        ctx.cfg = (shp, act, float(dropout_p), seed)
         return y.reshape(shp)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, w, mean, rstd = ctx.saved_tensors
+        x2, w, b, mean, rstd = ctx.saved_tensors
+        shp, act, p, seed = ctx.cfg
         M, C = x2.shape
         dy2 = _f32c(dy).reshape(M, C)
         dx = torch.empty_like(x2)
@@ -613,19 +724,22 @@ class _LayerNormTM(torch.autograd.Function):
         lib = N.lib()
         ws = torch.empty(max(int(lib.mtts_layernorm_bwd_workspace_size(M, C)), 1), dtype=torch.uint8,
                          device=x2.device)
-        N.check(lib.mtts_layernorm_bwd(dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), mean.data_ptr(),
-                                       rstd.data_ptr(), dx.data_ptr(), dw.data_ptr(), db.data_ptr(), M, C,
-                                       ws.data_ptr(), ws.numel(), _stream(x2)), "mtts_layernorm_bwd")
-        return dx.reshape(ctx.shp), dw, db, None
+        N.check(lib.mtts_layernorm_bwd(dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), b.data_ptr(), mean.data_ptr(),
+                                       rstd.data_ptr(), dx.data_ptr(), dw.data_ptr(), db.data_ptr(), M, C, act, p,
+                                       N.ptr(seed), ws.data_ptr(), ws.numel(), _stream(x2)), "mtts_layernorm_bwd")
+        return dx.reshape(shp), dw, db, None, None, None
 
 
 # ------------------------------------------------------------------------------------------ public ops
-def conv_tm(x, weight, bias, mask=None, stride: int = 1, padding: int | None = None, out_scale=None):
-    """y = Conv1d(x * mask) [* out_scale] token-major.  x [B,T,Cin], weight [Cout,Cin,k] (nn.Conv1d
-    layout), mask/out_scale [B,T] or None.  decoder.py:59,65,78,85,95,192,239,248,251,369-371."""
+def conv_tm(x, weight, bias, mask=None, stride: int = 1, padding: int | None = None, out_scale=None,
+            relu: bool = False, dropout_p: float = 0.0, residual=None):
+    """y = (residual + dropout(relu(Conv1d(x * mask)))) * out_scale, token-major.  x [B,T,Cin], weight
+    [Cout,Cin,k] (nn.Conv1d layout, k <= 8), mask/out_scale [B,T] or None.
+    decoder.py:59,65,78,85,95,192,239,248,251,369-371; text_encoder.py:48-57, 81-96."""
     if padding is None:
         padding = weight.shape[-1] // 2
-    return _ConvTM.apply(x, weight, bias, mask, out_scale, stride, padding)
+    return _ConvTM.apply(x, weight, bias, mask, out_scale, stride, padding, ACT_RELU if relu else ACT_NONE,
+                         float(dropout_p), residual)
 
 
 def conv_transpose_tm(x, weight, bias, mask=None):
@@ -639,15 +753,18 @@ def group_norm_mish_tm(h, gamma, beta, groups: int, mask=None, add=None, eps: fl
     return _GroupNormMishTM.apply(h, gamma, beta, mask, add, groups, eps)
 
 
-def layer_norm_tm(h, weight, bias, eps: float = 1e-5):
-    return _LayerNormTM.apply(h, weight, bias, eps)
+def layer_norm_tm(h, weight, bias, eps: float = 1e-5, relu: bool = False, dropout_p: float = 0.0):
+    """LayerNorm over the last dim [-> ReLU] [-> dropout(p)], one kernel each way."""
+    return _LayerNormTM.apply(h, weight, bias, eps, ACT_RELU if relu else ACT_NONE, float(dropout_p))
 
 
-def linear_tm(x, weight, bias=None, residual=None, dropout_p: float = 0.0):
-    """residual + dropout(x @ W^T + b)   (diffusers Linear [+ Dropout] [+ residual]).  `weight` may be
-    a tuple of weights stacked along the output dim (one GEMM, one gradient per weight)."""
+def linear_tm(x, weight, bias=None, residual=None, dropout_p: float = 0.0, in_scale=None, out_scale=None):
+    """(residual + dropout((x * in_scale) @ W^T + b)) * out_scale   (diffusers Linear [+ Dropout]
+    [+ residual]; the text encoder's masked 1x1 convs).  `weight` may be a tuple of weights stacked along
+    the output dim (one GEMM, one gradient per weight); a weight may be an nn.Conv1d weight [N, K, 1].
+    in_scale / out_scale: per-row [B, T] (or [M]) scales, e.g. the sequence mask."""
     ws = tuple(weight) if isinstance(weight, (tuple, list)) else (weight,)
-    return _LinearTM.apply(x, bias, residual, float(dropout_p), *ws)
+    return _LinearTM.apply(x, bias, residual, float(dropout_p), in_scale, out_scale, *ws)
 
 
 def ff_tm(x, w1, b1, w2, b2, residual=None, dropout_p: float = 0.0):
@@ -658,7 +775,7 @@ class _AttentionTM(torch.autograd.Function):
     """Multi-head attention over a fused token-major QKV buffer [B, T, 3C] -> o [B, T, C]."""
 
     @staticmethod
-    def _args(qkv, bias, o, lse, heads):
+    def _args(qkv, bias, o, lse, heads, dropout_p=0.0, seed=None):
         B, T, C3 = qkv.shape
         C = C3 // 3
         a = AttnArgs()
@@ -667,10 +784,11 @@ class _AttentionTM(torch.autograd.Function):
         a.key_bias, a.o, a.ldo, a.lse = N.ptr(bias), o.data_ptr(), C, lse.data_ptr()
         a.B, a.T, a.H, a.D = B, T, heads, C // heads
         a.scale = 1.0 / math.sqrt(C // heads)
+        a.dropout_p, a.seed = float(dropout_p), N.ptr(seed)
         return a
 
     @staticmethod
-    def forward(ctx, qkv, key_bias, heads):
+    def forward(ctx, qkv, key_bias, heads, dropout_p):
         _check(qkv, key_bias)
         prec = gemm_precision()
         qkv = _f32c(qkv)
@@ -678,10 +796,11 @@ class _AttentionTM(torch.autograd.Function):
         B, T, C3 = qkv.shape
         o = torch.empty(B, T, C3 // 3, device=qkv.device, dtype=torch.float32)
         lse = torch.empty(B, heads, T, device=qkv.device, dtype=torch.float32)
-        a = _AttentionTM._args(qkv, bias, o, lse, heads)
+        seed = _new_seed(qkv.device) if dropout_p > 0 else None
+        a = _AttentionTM._args(qkv, bias, o, lse, heads, dropout_p, seed)
         N.check(N.lib().mtts_attention_fwd(ctypes.byref(a), prec, _stream(qkv)), "mtts_attention_fwd")
         ctx.save_for_backward(qkv, bias, o, lse)
-        ctx.heads, ctx.prec = heads, prec
+        ctx.heads, ctx.prec, ctx.drop = heads, prec, (dropout_p, seed)
         return o
 
     @staticmethod
@@ -691,7 +810,7 @@ class _AttentionTM(torch.autograd.Function):
         B, T, C3 = qkv.shape
         C = C3 // 3
         dqkv = torch.empty_like(qkv)
-        a = _AttentionTM._args(qkv, bias, o, lse, ctx.heads)
+        a = _AttentionTM._args(qkv, bias, o, lse, ctx.heads, *ctx.drop)
         g = AttnGrads()
         g.dout, g.lddo = do.data_ptr(), C
         base, es = dqkv.data_ptr(), dqkv.element_size()
@@ -701,12 +820,44 @@ class _AttentionTM(torch.autograd.Function):
                          device=qkv.device)
         N.check(lib.mtts_attention_bwd(ctypes.byref(a), ctypes.byref(g), ctx.prec, ws.data_ptr(), ws.numel(),
                                        _stream(qkv)), "mtts_attention_bwd")
-        return dqkv, None, None
+        return dqkv, None, None, None
 
 
-def attention_tm(qkv, key_bias, heads: int):
+def attention_tm(qkv, key_bias, heads: int, dropout_p: float = 0.0):
     """softmax(q k^T / sqrt(d) + key_bias[b, key]) v per head, from the fused projection qkv [B,T,3C]
     (q | k | v column blocks, head h at [h*d, h*d+d) of each); key_bias [B,T].  The reference's float
     0/1 mask is ADDED to the scores (diffusers AttnProcessor2_0 + prepare_attention_mask),
     so padded keys are down-weighted, not removed.  Returns o [B, T, C] token-major."""
-    return _AttentionTM.apply(qkv, key_bias, heads)
+    return _AttentionTM.apply(qkv, key_bias, heads, float(dropout_p))
+
+
+class _RopeTM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, heads, rope_dims):
+        _check(qkv, cos, sin)
+        qkv, cos, sin = _f32c(qkv), _f32c(cos), _f32c(sin)  # the kernel reads fp32 tables [T, rope_dims/2]
+        assert cos.shape == sin.shape == (qkv.shape[1], rope_dims // 2)
+        B, T, C3 = qkv.shape
+        out = torch.empty_like(qkv)
+        N.check(N.lib().mtts_rope_qk(qkv.data_ptr(), out.data_ptr(), B * T, T, C3 // 3, heads, rope_dims,
+                                     cos.data_ptr(), sin.data_ptr(), 0, _stream(qkv)), "mtts_rope_qk")
+        ctx.save_for_backward(cos, sin)
+        ctx.cfg = (heads, rope_dims)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        cos, sin = ctx.saved_tensors
+        heads, rope_dims = ctx.cfg
+        dout = _f32c(dout)
+        B, T, C3 = dout.shape
+        dx = torch.empty_like(dout)
+        N.check(N.lib().mtts_rope_qk(dout.data_ptr(), dx.data_ptr(), B * T, T, C3 // 3, heads, rope_dims,
+                                     cos.data_ptr(), sin.data_ptr(), 1, _stream(dout)), "mtts_rope_qk")
+        return dx, None, None, None, None
+
+
+def rope_tm(qkv, cos, sin, heads: int, rope_dims: int):
+    """Rotary embedding of the q and k blocks of a fused [B, T, 3C] projection (first rope_dims dims of
+    each head, rotate-half form; cos/sin [T, rope_dims/2]); v passes through."""
+    return _RopeTM.apply(qkv, cos, sin, heads, rope_dims)

@@ -2,10 +2,22 @@
 
 Reference: ConvReluNorm :17-57, DurationPredictor :60-96, RotaryPositionalEmbeddings :99-143,
 MultiHeadAttention :146-230, FFN :235-253, Encoder :256-322, TextEncoder :325-402.  Same module tree
-and parameter names.  Not a kernel target in this tier: it runs as PyTorch-ROCm
-device ops, with the q/k/v 1x1 convs fused into one GEMM and scaled-dot-product attention (the
-reference's masked_fill(-1e4) becomes an additive -1e4 bias; identical on valid query rows, where
-both underflow to exactly 0, and padded rows are zeroed by the following x*mask).
+and parameter names (a reference checkpoint loads unchanged).
+
+Runs token-major ([B, T, C]) on the same libmtts_hip kernels as the decoder:
+  * every Conv1d is an implicit GEMM with the input mask as a row scale, ReLU / dropout / residual /
+    output mask in the GEMM epilogue (k = 5 prenet convs included);
+  * the prenet's LN -> ReLU -> Dropout and the duration predictor's LN -> Dropout are one LayerNorm
+    kernel each way;
+  * q/k/v are one GEMM over the stacked 1x1 conv weights, RoPE is one elementwise kernel on the fused
+    projection, attention is the flash kernel (head dim 96) with dropout on the probabilities;
+  * the FFN (conv k3 -> ReLU -> Dropout -> conv k3 -> Dropout, then the Encoder's Dropout and the
+    residual) is two GEMMs (conv_ffn_tm).
+Masking: the reference's masked_fill(mask == 0, -1e4) on the scores becomes an additive key bias
+of -1e4 on padded keys.  On valid query rows the two are identical (both weights underflow to
+exactly 0 in fp32); padded query rows differ, and padded rows are dead: every consumer masks them
+(x * mask at each layer's input and at the end, the FFN and projections' masked inputs, -1e4 keys),
+so no loss or gradient depends on them.  For the same reason residual adds use the unmasked input.
 """
 from __future__ import annotations
 
@@ -13,19 +25,16 @@ import math
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
+from matcha.models.components import _ops as O
 from matcha.utils.model import sequence_mask
-
-
-def _ln_c(x, ln: nn.LayerNorm):  # LayerNorm over channels of a [B, C, T] tensor
-    return F.layer_norm(x.transpose(1, 2), ln.normalized_shape, ln.weight, ln.bias, ln.eps).transpose(1, 2)
 
 
 class ConvReluNorm(nn.Module):
     def __init__(self, input_channels, hidden_channels, output_channels, kernel_size, num_layers, dropout_rate):
         super().__init__()
         pad = kernel_size // 2
+        self.dropout_rate = dropout_rate
         self.convolutions = nn.ModuleList(
             [nn.Conv1d(input_channels if i == 0 else hidden_channels, hidden_channels, kernel_size, padding=pad)
              for i in range(num_layers)])
@@ -35,17 +44,24 @@ class ConvReluNorm(nn.Module):
         self.projection.weight.data.zero_()
         self.projection.bias.data.zero_()
 
-    def forward(self, x, x_mask):
-        res = x
+    def forward_tm(self, x, m):
+        """x [B, T, C], m [B, T] -> (x + proj(h)) * m  (text_encoder.py:48-57)."""
+        p = self.dropout_rate if self.training else 0.0
+        h = x
         for conv, ln in zip(self.convolutions, self.normalizations):
-            x = self.activation_dropout(_ln_c(conv(x * x_mask), ln))
-        return (res + self.projection(x)) * x_mask
+            h = O.conv_tm(h, conv.weight, conv.bias, mask=m)
+            h = O.layer_norm_tm(h, ln.weight, ln.bias, ln.eps, relu=True, dropout_p=p)
+        return O.linear_tm(h, self.projection.weight, self.projection.bias, residual=x, out_scale=m)
+
+    def forward(self, x, x_mask):
+        return self.forward_tm(x.transpose(1, 2), x_mask[:, 0]).transpose(1, 2)
 
 
 class DurationPredictor(nn.Module):
     def __init__(self, input_channels, filter_channels, kernel_size, dropout_rate):
         super().__init__()
         pad = kernel_size // 2
+        self.dropout_rate = dropout_rate
         self.dropout = nn.Dropout(dropout_rate)
         self.conv_layer_1 = nn.Conv1d(input_channels, filter_channels, kernel_size, padding=pad)
         self.norm_layer_1 = nn.LayerNorm(filter_channels)
@@ -53,14 +69,21 @@ class DurationPredictor(nn.Module):
         self.norm_layer_2 = nn.LayerNorm(filter_channels)
         self.output_projection = nn.Conv1d(filter_channels, 1, 1)
 
+    def forward_tm(self, x, m):
+        """text_encoder.py:81-96: (conv -> ReLU -> LN -> Dropout) x 2 -> 1x1 conv, masked; -> [B, T, 1]."""
+        p = self.dropout_rate if self.training else 0.0
+        for conv, ln in ((self.conv_layer_1, self.norm_layer_1), (self.conv_layer_2, self.norm_layer_2)):
+            x = O.conv_tm(x, conv.weight, conv.bias, mask=m, relu=True)
+            x = O.layer_norm_tm(x, ln.weight, ln.bias, ln.eps, dropout_p=p)
+        return O.linear_tm(x, self.output_projection.weight, self.output_projection.bias, in_scale=m, out_scale=m)
+
     def forward(self, x, x_mask):
-        x = self.dropout(_ln_c(torch.relu(self.conv_layer_1(x * x_mask)), self.norm_layer_1))
-        x = self.dropout(_ln_c(torch.relu(self.conv_layer_2(x * x_mask)), self.norm_layer_2))
-        return self.output_projection(x * x_mask) * x_mask
+        return self.forward_tm(x.transpose(1, 2), x_mask[:, 0]).transpose(1, 2)
 
 
 class RotaryPositionalEmbeddings(nn.Module):
-    """Rotates the first ``feature_dim`` features of [B, H, T, d] (neg-half form, base 1e4)."""
+    """cos/sin tables of the reference's partial RoPE (text_encoder.py:99-143): the first feature_dim
+    features of every head, rotate-half form, base 1e4.  The rotation itself is mtts_rope_qk."""
 
     def __init__(self, feature_dim, base_freq=10_000):
         super().__init__()
@@ -68,23 +91,17 @@ class RotaryPositionalEmbeddings(nn.Module):
         self.feature_dim = int(feature_dim)
         self._cache = None
 
-    def _tables(self, T, device):
+    def tables(self, T: int, device) -> tuple[torch.Tensor, torch.Tensor]:
+        """cos, sin [T, feature_dim / 2], the reference's fp32 formula (:109-126)."""
         c = self._cache
         if c is None or c[0].shape[0] < T or c[0].device != device:
-            theta = 1.0 / (self.base_freq ** (torch.arange(0, self.feature_dim, 2, device=device).float()
-                                              / self.feature_dim))
-            ang = torch.arange(T, device=device).float()[:, None] * theta[None, :]
-            ang = torch.cat([ang, ang], dim=1)
-            self._cache = c = (ang.cos(), ang.sin())
+            # fp32 even inside a bf16 autocast region (autocast would run the einsum in bf16)
+            with torch.autocast(device_type=device.type, enabled=False):
+                theta = 1.0 / (self.base_freq ** (torch.arange(0, self.feature_dim, 2).float()
+                                                  / self.feature_dim)).to(device)
+                ang = torch.einsum("n,d->nd", torch.arange(T, device=device).float(), theta)
+                self._cache = c = (ang.cos().float().contiguous(), ang.sin().float().contiguous())
         return c[0][:T], c[1][:T]
-
-    def forward(self, x):
-        d = self.feature_dim
-        cos, sin = self._tables(x.shape[2], x.device)
-        xr, xp = x[..., :d], x[..., d:]
-        h = d // 2
-        neg = torch.cat([-xr[..., h:], xr[..., :h]], dim=-1)
-        return torch.cat([xr * cos + neg * sin, xp], dim=-1)
 
 
 class MultiHeadAttention(nn.Module):
@@ -94,6 +111,7 @@ class MultiHeadAttention(nn.Module):
         assert channels % num_heads == 0
         if proximal_bias:
             raise NotImplementedError("proximal_bias is not used by the Matcha encoder")
+        self.channels = channels
         self.num_heads = num_heads
         self.head_dim = channels // num_heads
         self.dropout_rate = dropout_rate
@@ -103,6 +121,7 @@ class MultiHeadAttention(nn.Module):
         self.query_rope = RotaryPositionalEmbeddings(self.head_dim * 0.5)
         self.key_rope = RotaryPositionalEmbeddings(self.head_dim * 0.5)
         self.output_conv = nn.Conv1d(channels, output_channels, 1)
+        self.dropout = nn.Dropout(dropout_rate)
         nn.init.xavier_uniform_(self.query_conv.weight)
         nn.init.xavier_uniform_(self.key_conv.weight)
         if proximal_init:
@@ -110,31 +129,44 @@ class MultiHeadAttention(nn.Module):
             self.key_conv.bias.data.copy_(self.query_conv.bias.data)
         nn.init.xavier_uniform_(self.value_conv.weight)
 
-    def forward(self, x, context, attention_bias):
-        """x [B, C, T]; attention_bias [B, 1, T, T] additive (0 valid, -1e4 masked)."""
-        B, C, T = x.shape
-        H, d = self.num_heads, self.head_dim
-        w = torch.cat([self.query_conv.weight, self.key_conv.weight, self.value_conv.weight], 0)[..., 0]
-        b = torch.cat([self.query_conv.bias, self.key_conv.bias, self.value_conv.bias], 0)
-        qkv = F.linear(x.transpose(1, 2), w, b)  # [B, T, 3C]
-        q, k, v = (t.view(B, T, H, d).transpose(1, 2) for t in qkv.split(C, dim=-1))
-        q, k = self.query_rope(q), self.key_rope(k)
-        o = F.scaled_dot_product_attention(q, k, v, attn_mask=attention_bias,
-                                           dropout_p=self.dropout_rate if self.training else 0.0)
-        o = o.transpose(1, 2).reshape(B, T, C)
-        return F.linear(o, self.output_conv.weight[..., 0], self.output_conv.bias).transpose(1, 2)
+    def attend_tm(self, x, m, key_bias):
+        """softmax-attention output [B, T, C] of (x * m) before output_conv (text_encoder.py:188-230)."""
+        T = x.shape[1]
+        qkv = O.linear_tm(x, (self.query_conv.weight, self.key_conv.weight, self.value_conv.weight),
+                          torch.cat([self.query_conv.bias, self.key_conv.bias, self.value_conv.bias]), in_scale=m)
+        cos, sin = self.query_rope.tables(T, x.device)  # query_rope and key_rope are the same rotation
+        qkv = O.rope_tm(qkv, cos, sin, self.num_heads, self.query_rope.feature_dim)
+        p = self.dropout_rate if self.training else 0.0
+        return O.attention_tm(qkv, key_bias, self.num_heads, dropout_p=p)
+
+    def forward(self, x, context, attention_mask=None):
+        """Reference API: x [B, C, T] (context must be x: self-attention), attention_mask [B, 1, T, T]
+        = x_mask_q * x_mask_k."""
+        assert context is x, "the encoder uses self-attention only"
+        m = attention_mask[:, 0].amax(dim=1) if attention_mask is not None else \
+            torch.ones(x.shape[0], x.shape[2], device=x.device)
+        o = self.attend_tm(x.transpose(1, 2), torch.ones_like(m), (m - 1.0) * 1e4)
+        return O.linear_tm(o, self.output_conv.weight, self.output_conv.bias).transpose(1, 2)
 
 
 class FFN(nn.Module):
     def __init__(self, input_channels, output_channels, filter_channels, kernel_size, dropout_rate=0.0):
         super().__init__()
         pad = kernel_size // 2
+        self.dropout_rate = dropout_rate
         self.conv_net = nn.Sequential(
             nn.Conv1d(input_channels, filter_channels, kernel_size, padding=pad), nn.ReLU(), nn.Dropout(dropout_rate),
             nn.Conv1d(filter_channels, output_channels, kernel_size, padding=pad), nn.Dropout(dropout_rate))
 
+    def forward_tm(self, x, m, residual=None, extra_dropout: float = 0.0):
+        """(residual + Dropout_extra(FFN(x, m))) * m, token-major (text_encoder.py:247-253, 307-313)."""
+        p = self.dropout_rate if self.training else 0.0
+        keep_out = (1.0 - p) * (1.0 - extra_dropout)
+        c1, c2 = self.conv_net[0], self.conv_net[3]
+        return O.conv_ffn_tm(x, c1.weight, c1.bias, c2.weight, c2.bias, m, residual, p_in=p, p_out=1.0 - keep_out)
+
     def forward(self, x, x_mask):
-        return self.conv_net(x * x_mask) * x_mask
+        return self.forward_tm(x.transpose(1, 2), x_mask[:, 0]).transpose(1, 2)
 
 
 class Encoder(nn.Module):
@@ -142,6 +174,7 @@ class Encoder(nn.Module):
                  **kwargs):
         super().__init__()
         self.num_layers = num_layers
+        self.dropout_rate = dropout_rate
         self.dropout = nn.Dropout(dropout_rate)
         self.attention_layers = nn.ModuleList(
             [MultiHeadAttention(hidden_channels, hidden_channels, num_heads, dropout_rate=dropout_rate)
@@ -152,16 +185,22 @@ class Encoder(nn.Module):
              for _ in range(num_layers)])
         self.norm_layers_2 = nn.ModuleList([nn.LayerNorm(hidden_channels) for _ in range(num_layers)])
 
+    def forward_tm(self, h, m):
+        """text_encoder.py:296-322, token-major; returns the UNMASKED last LayerNorm output (callers
+        apply the final x * mask through their input row scale)."""
+        p = self.dropout_rate if self.training else 0.0
+        key_bias = (m - 1.0) * 1e4  # masked_fill(-1e4) on padded keys
+        for attn, ln1, ffn, ln2 in zip(self.attention_layers, self.norm_layers_1, self.ffn_layers, self.norm_layers_2):
+            o = attn.attend_tm(h, m, key_bias)
+            x = O.linear_tm(o, attn.output_conv.weight, attn.output_conv.bias, residual=h, dropout_p=p)
+            x = O.layer_norm_tm(x, ln1.weight, ln1.bias, ln1.eps)
+            x = ffn.forward_tm(x, m, residual=x, extra_dropout=p)
+            h = O.layer_norm_tm(x, ln2.weight, ln2.bias, ln2.eps)
+        return h
+
     def forward(self, x, x_mask):
-        m2 = x_mask.unsqueeze(2) * x_mask.unsqueeze(-1)  # [B, 1, T, T]
-        bias = torch.zeros_like(m2).masked_fill(m2 == 0, -1e4)
-        for i in range(self.num_layers):
-            x = x * x_mask
-            a = self.dropout(self.attention_layers[i](x, x, bias))
-            x = _ln_c(x + a, self.norm_layers_1[i])
-            f = self.dropout(self.ffn_layers[i](x, x_mask))
-            x = _ln_c(x + f, self.norm_layers_2[i])
-        return x * x_mask
+        m = x_mask[:, 0]
+        return (self.forward_tm(x.transpose(1, 2), m) * m.unsqueeze(-1)).transpose(1, 2)
 
 
 class TextEncoder(nn.Module):
@@ -177,7 +216,7 @@ class TextEncoder(nn.Module):
             self.prenet = ConvReluNorm(self.channel_dim, self.channel_dim, self.channel_dim, kernel_size=5,
                                        num_layers=3, dropout_rate=0.1)
         else:
-            self.prenet = lambda x, x_mask: x
+            self.prenet = None
         self.encoder = Encoder(self.channel_dim, encoder_params.filter_channels, encoder_params.n_heads,
                                encoder_params.n_layers, encoder_params.kernel_size, encoder_params.p_dropout)
         self.mean_projection = nn.Conv1d(self.channel_dim, self.feature_dim, 1)
@@ -186,9 +225,12 @@ class TextEncoder(nn.Module):
                                                     duration_predictor_params.p_dropout)
 
     def forward(self, text_input, text_lengths):
-        emb = (self.embedding(text_input) * math.sqrt(self.channel_dim)).transpose(1, -1)
-        mask = sequence_mask(text_lengths, emb.size(2)).unsqueeze(1).to(emb.dtype)
-        h = self.encoder(self.prenet(emb, mask), mask)
-        mu = self.mean_projection(h) * mask
-        logw = self.duration_predictor(h.detach(), mask)
-        return mu, logw, mask
+        """text_encoder.py:376-402 -> (mu [B, n_feats, T], logw [B, 1, T], x_mask [B, 1, T])."""
+        with O.weight_pack_scope(self):
+            emb = self.embedding(text_input) * math.sqrt(self.channel_dim)  # [B, T, C]: token-major already
+            m = sequence_mask(text_lengths, emb.size(1)).to(emb.dtype)
+            h = self.prenet.forward_tm(emb, m) if self.prenet is not None else emb
+            h = self.encoder.forward_tm(h, m)
+            mu = O.linear_tm(h, self.mean_projection.weight, self.mean_projection.bias, in_scale=m, out_scale=m)
+            logw = self.duration_predictor.forward_tm(h.detach(), m)
+        return mu.transpose(1, 2), logw.transpose(1, 2), m.unsqueeze(1)

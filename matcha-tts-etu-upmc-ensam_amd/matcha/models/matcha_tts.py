@@ -92,10 +92,9 @@ class MatchaTTS(BaseLightningClass):
     def forward(self, x, x_lengths, y, y_lengths, out_size=None, cond=None, durations=None, *, t=None, z=None):
         """Returns (dur_loss, prior_loss, diff_loss, attn) -- matcha_tts.py:437-515.  ``t``/``z``
         (keyword-only) inject the CFM randomness for parity tests."""
-        # The text encoder (PyTorch-ROCm, not a kernel target this tier) stays fp32 even in a bf16
-        # autocast region: MIOpen has only naive kernels for its bf16 k=5 / k=3 convs.
-        with torch.autocast(device_type=x.device.type, enabled=False):
-            mu_x, logw, x_mask = self.encoder(x, x_lengths)
+        # the text encoder runs on the same HIP GEMM/attention kernels as the decoder and follows the
+        # caller's precision (bf16 MFMA operands inside a bf16 autocast region)
+        mu_x, logw, x_mask = self.encoder(x, x_lengths)
         y_max_length = y.shape[-1]
         y_mask = sequence_mask(y_lengths, y_max_length).unsqueeze(1).to(x_mask)
         attn_mask = x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)

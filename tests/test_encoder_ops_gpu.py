@@ -1,0 +1,204 @@
+"""Text-encoder operators on the GPU (train mode): RoPE against the reference formula, and every
+dropout-carrying op's backward against central differences of its own forward with the dropout masks
+replayed (same device RNG state -> same seeds -> same counter-based masks).  Exact-fp32 MFMA path."""
+from __future__ import annotations
+
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _dirderiv_check(fn, inputs, rtol=2e-3, eps=1e-3, seed=7):
+    """<grad f . v> (analytic, one backward) vs (f(x+eps v) - f(x-eps v)) / 2eps for a random direction v
+    over every floating input, with the op's RNG draws replayed for each evaluation."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    dirs = [torch.randn(x.shape, generator=g).to(DEV) for x in inputs]
+    w = None
+
+    def run(xs):
+        torch.cuda.manual_seed(1234)
+        return fn(*xs)
+
+    xs = [x.detach().clone().requires_grad_(True) for x in inputs]
+    y = run(xs)
+    w = torch.randn(y.shape, generator=g).to(DEV)
+    (y * w).sum().backward()
+    analytic = sum((x.grad * d).sum().item() for x, d in zip(xs, dirs))
+    with torch.no_grad():
+        yp = run([x + eps * d for x, d in zip(inputs, dirs)])
+        ym = run([x - eps * d for x, d in zip(inputs, dirs)])
+        numeric = ((yp - ym) * w).sum().item() / (2 * eps)
+    assert abs(analytic - numeric) <= rtol * max(abs(numeric), 1.0), (analytic, numeric)
+    return y
+
+
+def _mask(B, T, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    lens = torch.randint(T // 2, T + 1, (B,), generator=g)
+    lens[0] = T
+    return (torch.arange(T)[None] < lens[:, None]).float().to(DEV)
+
+
+def test_rope_matches_reference_formula():
+    from matcha.models.components import _ops as O
+    from matcha.models.components.text_encoder import RotaryPositionalEmbeddings
+
+    B, T, H, d = 3, 37, 2, 96
+    qkv = torch.randn(B, T, 3 * H * d, device=DEV, requires_grad=True)
+    rp = RotaryPositionalEmbeddings(d * 0.5)
+    cos, sin = rp.tables(T, DEV)
+    out = O.rope_tm(qkv, cos, sin, H, rp.feature_dim)
+    # reference (text_encoder.py:128-143) on [B, H, T, d]
+    x = qkv.detach().clone().requires_grad_(True)
+    q, k, v = x.split(H * d, dim=-1)
+    R, half = rp.feature_dim, rp.feature_dim // 2
+    cc, ss = torch.cat([cos, cos], 1)[:, None, :], torch.cat([sin, sin], 1)[:, None, :]
+
+    def ref(t):
+        t = t.view(B, T, H, d)
+        tr, tp = t[..., :R], t[..., R:]
+        neg = torch.cat([-tr[..., half:], tr[..., :half]], -1)
+        return torch.cat([tr * cc + neg * ss, tp], -1).reshape(B, T, H * d)
+
+    expect = torch.cat([ref(q), ref(k), v], -1)
+    torch.testing.assert_close(out, expect, rtol=1e-6, atol=1e-6)
+    gout = torch.randn_like(out)
+    out.backward(gout)
+    expect.backward(gout)
+    torch.testing.assert_close(qkv.grad, x.grad, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("relu,p", [(True, 0.1), (False, 0.1), (True, 0.0)])
+def test_layer_norm_tail_grad(relu, p):
+    from matcha.models.components import _ops as O
+
+    M, C = 300, 192
+    x = torch.randn(M, C, device=DEV)
+    # ReLU inputs kept away from the kink (finite differences across it are meaningless): |xhat*w| < 3
+    # and b = +-3 fixes the gate -- half the channels pass, half are cut
+    w = (torch.rand(C, device=DEV) * 0.2 + 0.1) * torch.sign(torch.randn(C, device=DEV))
+    b = torch.where(torch.arange(C, device=DEV) % 2 == 0, 3.0, -3.0)
+    y = _dirderiv_check(lambda x_, w_, b_: O.layer_norm_tm(x_, w_, b_, 1e-5, relu=relu, dropout_p=p), [x, w, b])
+    if p > 0 and not relu:
+        frac = (y == 0).float().mean().item()
+        assert abs(frac - p) < 0.02
+
+
+@pytest.mark.parametrize("k", [5, 3])
+def test_conv_relu_dropout_grad(k):
+    from matcha.models.components import _ops as O
+
+    B, T, Cin, Cout = 3, 50, 64, 96
+    x = torch.randn(B, T, Cin, device=DEV)
+    w = torch.randn(Cout, Cin, k, device=DEV) / math.sqrt(Cin * k) * 0.2  # |w.x| << 3: no ReLU kink crossing
+    b = torch.where(torch.arange(Cout, device=DEV) % 2 == 0, 3.0, -3.0)
+    m = _mask(B, T)
+    _dirderiv_check(lambda x_, w_, b_: O.conv_tm(x_, w_, b_, mask=m, relu=True, dropout_p=0.1), [x, w, b])
+
+
+def test_conv_residual_out_scale_grad():
+    from matcha.models.components import _ops as O
+
+    B, T, C = 2, 40, 64
+    x = torch.randn(B, T, C, device=DEV)
+    r = torch.randn(B, T, C, device=DEV)
+    w = torch.randn(C, C, 1, device=DEV) / 8
+    b = torch.randn(C, device=DEV)
+    m = _mask(B, T, 1)
+    _dirderiv_check(lambda x_, r_, w_, b_: O.conv_tm(x_, w_, b_, residual=r_, out_scale=m), [x, r, w, b])
+
+
+def test_conv_ffn_grad_and_reference_eval():
+    from matcha.models.components import _ops as O
+
+    B, T, C, F_ = 3, 45, 64, 128
+    x = torch.randn(B, T, C, device=DEV)
+    w1 = torch.randn(F_, C, 3, device=DEV) / math.sqrt(3 * C) * 0.2  # ReLU away from its kink
+    b1 = torch.where(torch.arange(F_, device=DEV) % 2 == 0, 3.0, -3.0)
+    w2 = torch.randn(C, F_, 3, device=DEV) / math.sqrt(3 * F_)
+    b2 = torch.randn(C, device=DEV) * 0.1
+    m = _mask(B, T, 2)
+    # eval semantics against the reference FFN (text_encoder.py:247-253): conv_net(x*m)*m, the inner conv
+    # reading the unmasked ReLU output; plus the Encoder's residual and the row mask
+    y = O.conv_ffn_tm(x, w1, b1, w2, b2, m, residual=x)
+    mc = m[:, None, :]
+    xc = x.transpose(1, 2)
+    h = torch.relu(torch.nn.functional.conv1d(xc * mc, w1, b1, padding=1))
+    f = torch.nn.functional.conv1d(h, w2, b2, padding=1) * mc
+    torch.testing.assert_close(y, ((xc + f) * mc).transpose(1, 2), rtol=1e-4, atol=1e-4)
+    _dirderiv_check(lambda x_, a, bb, c, d: O.conv_ffn_tm(x_, a, bb, c, d, m, residual=x_, p_in=0.1, p_out=0.19),
+                    [x, w1, b1, w2, b2])
+
+
+def test_attention_dropout_grad_and_rate():
+    from matcha.models.components import _ops as O
+
+    B, T, H, d = 2, 70, 2, 96
+    qkv = torch.randn(B, T, 3 * H * d, device=DEV)
+    m = _mask(B, T, 3)
+    bias = (m - 1) * 1e4
+    _dirderiv_check(lambda q: O.attention_tm(q, bias, H, dropout_p=0.1), [qkv])
+    # rate: with v = one-hot key rows the output row is the dropped probability row
+    qkv2 = torch.zeros(1, 64, 3 * 96, device=DEV)
+    qkv2[0, :, :192] = torch.randn(64, 192, device=DEV)
+    qkv2[0, :, 192:256] = torch.eye(64, device=DEV)
+    o = O.attention_tm(qkv2, torch.zeros(1, 64, device=DEV), 1, dropout_p=0.25)
+    frac = (o[0, :, :64] == 0).float().mean().item()
+    assert abs(frac - 0.25) < 0.04
+
+
+def test_linear_row_scales_grad():
+    from matcha.models.components import _ops as O
+
+    B, T, K, N_ = 2, 33, 64, 48
+    x = torch.randn(B, T, K, device=DEV)
+    w = torch.randn(N_, K, 1, device=DEV) / 8
+    b = torch.randn(N_, device=DEV)
+    r = torch.randn(B, T, N_, device=DEV)
+    m = _mask(B, T, 4)
+    _dirderiv_check(lambda x_, w_, b_, r_: O.linear_tm(x_, w_, b_, residual=r_, dropout_p=0.1, in_scale=m,
+                                                       out_scale=m), [x, w, b, r])
+
+
+def test_linear_one_channel_output_grad():
+    """The duration predictor's 1-channel projection (gradient padded to 8 columns inside)."""
+    from matcha.models.components import _ops as O
+
+    B, T, K = 2, 29, 256
+    x = torch.randn(B, T, K, device=DEV)
+    w = torch.randn(1, K, 1, device=DEV) / 16
+    b = torch.randn(1, device=DEV)
+    m = _mask(B, T, 5)
+    _dirderiv_check(lambda x_, w_, b_: O.linear_tm(x_, w_, b_, in_scale=m, out_scale=m), [x, w, b])
+
+
+def test_rope_tables_are_fp32_under_autocast():
+    """Regression: the tables are built with einsum, which a bf16 autocast region would run in bf16;
+    the kernel reads fp32."""
+    from matcha.models.components.text_encoder import RotaryPositionalEmbeddings
+
+    rp = RotaryPositionalEmbeddings(48)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        cos, sin = rp.tables(20, DEV)
+    assert cos.dtype == sin.dtype == torch.float32 and cos.is_contiguous() and cos.shape == (20, 24)
+
+
+def test_encoder_bf16_deterministic():
+    """Two bf16 forwards of the whole text encoder are bit-identical (the second served by the
+    batched weight-packing plan the first one recorded)."""
+    from matcha.models.matcha_tts import MatchaTTS
+    from matcha.training import synthetic_batch
+
+    torch.manual_seed(0)
+    m = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(DEV).eval()
+    b = synthetic_batch(4, 20, 80, device=DEV)
+    outs = []
+    for _ in range(2):
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            mu, logw, _ = m.encoder(b["x"], b["x_lengths"])
+        outs.append((mu.clone(), logw.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
