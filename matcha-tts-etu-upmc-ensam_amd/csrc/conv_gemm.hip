@@ -23,6 +23,8 @@
 // which also emits the bias gradient (column sums of dY, accumulated in the k-tile-0 blocks).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cstdint>
 
 #include "mtts_common.h"
@@ -307,17 +309,31 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
 
 // ------------------------------------------------------------------------------------------------
 // wgrad: partial[s][n][k] = sum over the split's rows of dY[row][n] * A_gathered[row][k]
-// Tile 128 (n) x 128 (k), reduction dim = rows in steps of 32; LDS holds both operands transposed
-// ([col][row], 16-byte fragment reads along rows).  k-tile-0 blocks also sum dY columns (bias grad).
-template <bool BF16>
+// Tile 128 (n) x 128 (k), 4 waves of 64 x 64; the reduction dim (token rows) advances KB rows per
+// step.  Both operands are staged transposed in LDS ([col][row], 16-byte fragment reads along rows),
+// double-buffered with a one-step register prefetch (one barrier per step).  A thread stages row PAIRS
+// x 4 columns so the transposed bf16 writes are packed 32-bit stores.  k-tile-0 blocks also sum dY
+// columns (bias grad) in a fixed order.
+template <bool BF16, int KB>
+struct WgradGeom {
+    static constexpr int T = 128;
+    static constexpr int LDR = KB + Stage<BF16>::PAD;  // row stride of the transposed images
+    static constexpr int CH = KB * 16 / kThreads;       // (2 rows x 4 cols) chunks per thread per operand
+    using ST = typename Stage<BF16>::T;
+    static constexpr size_t kBufBytes = (size_t)2 * T * LDR * sizeof(ST);  // Ys + Xs of one stage
+    static constexpr size_t kLds = 2 * kBufBytes;
+    static_assert((size_t)(KB / 2) * T * sizeof(float) <= kLds, "db scratch fits the operand buffers");
+};
+
+template <bool BF16, int KB>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_args p, int rows_per_split,
                                                                float *__restrict__ part, float *__restrict__ part_db) {
-    constexpr int T = 128;
-    using ST = typename Stage<BF16>::T;
-    constexpr int LDR = kBK + Stage<BF16>::PAD;  // row stride of the transposed images
-    __shared__ ST Ys[T * LDR];
-    __shared__ ST Xs[T * LDR];
-    __shared__ float dbs[16][T];
+    using Gm = WgradGeom<BF16, KB>;
+    using ST = typename Gm::ST;
+    constexpr int T = Gm::T, LDR = Gm::LDR, CH = Gm::CH;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    ST *Ybuf = reinterpret_cast<ST *>(smem);  // [2][T][LDR] then Xs [2][T][LDR]
+    ST *Xbuf = Ybuf + 2 * T * LDR;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
@@ -329,12 +345,95 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
     const bool do_db = (blockIdx.y == 0) && part_db != nullptr;
     const float inv_to = 1.0f / (float)p.To;
 
-    // staging: 32 rows x 128 cols per operand = 512 chunks of 8 -> 2 chunks per thread per operand
-    float colsum[2][8];
+    // per-chunk constants: row pair, column group, and the A gather's (tap offset, channel) -- k is
+    // fixed per chunk, so no division in the loop
+    int c_rp[CH], c_cc[CH], c_toff[CH], c_ch[CH];
+    bool c_kok[CH], c_nok[CH], c_nfull[CH];
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c < CH; ++c) {
+        const int q = tid + kThreads * c;
+        c_rp[c] = q >> 5;
+        c_cc[c] = (q & 31) * 4;
+        const int k = k0 + c_cc[c], n = n0 + c_cc[c];
+        c_kok[c] = k < p.K;
+        const int j = c_kok[c] ? k / p.cin : 0;
+        c_ch[c] = k - j * p.cin;
+        c_toff[c] = mtts::tap_off(p, j);
+        c_nok[c] = n < p.N;
+        c_nfull[c] = n + 4 <= p.N;
+    }
+
+    float yv[CH][2][4], xv[CH][2][4];
+    float colsum[CH][4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) colsum[c][i] = 0.f;
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) colsum[c][i] = 0.f;
+
+    auto load = [&](int rb) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int m = rb + 2 * c_rp[c] + h;
+                const bool mv = m < r_end;
+                int b = 0, u = 0;
+                if (mv) divmod_fast(m, p.To, inv_to, b, u);
+                float4 y4 = make_float4(0.f, 0.f, 0.f, 0.f), x4 = y4;
+                if (mv && c_nok[c]) {
+                    const float *src =
+                        p.dY + ((size_t)b * p.To_full + (size_t)u * p.out_stride + p.out_off) * p.ldy + n0 + c_cc[c];
+                    if (c_nfull[c]) {
+                        y4 = *reinterpret_cast<const float4 *>(src);
+                    } else {
+                        const int n = n0 + c_cc[c];
+                        y4.x = src[0];
+                        y4.y = n + 1 < p.N ? src[1] : 0.f;
+                        y4.z = n + 2 < p.N ? src[2] : 0.f;
+                        y4.w = n + 3 < p.N ? src[3] : 0.f;
+                    }
+                }
+                const int irow = u * p.in_stride + c_toff[c];
+                if (mv && c_kok[c] && irow >= 0 && irow < p.Ti) {
+                    const size_t r = (size_t)b * p.Ti + irow;
+                    x4 = *reinterpret_cast<const float4 *>(p.A + r * p.lda + c_ch[c]);
+                    if (p.a_scale) {
+                        const float sc = p.a_scale[r];
+                        x4.x *= sc; x4.y *= sc; x4.z *= sc; x4.w *= sc;
+                    }
+                }
+                yv[c][h][0] = y4.x; yv[c][h][1] = y4.y; yv[c][h][2] = y4.z; yv[c][h][3] = y4.w;
+                xv[c][h][0] = x4.x; xv[c][h][1] = x4.y; xv[c][h][2] = x4.z; xv[c][h][3] = x4.w;
+            }
+        if (do_db) {
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) colsum[c][i] += yv[c][0][i] + yv[c][1][i];
+        }
+    };
+    auto store = [&](int buf) {
+        ST *Ys = Ybuf + buf * T * LDR, *Xs = Xbuf + buf * T * LDR;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int r2 = 2 * c_rp[c];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int col = c_cc[c] + i;
+                if constexpr (BF16) {
+                    *reinterpret_cast<uint32_t *>(&Ys[col * LDR + r2]) =
+                        (uint32_t)to_bf16(yv[c][0][i]) | ((uint32_t)to_bf16(yv[c][1][i]) << 16);
+                    *reinterpret_cast<uint32_t *>(&Xs[col * LDR + r2]) =
+                        (uint32_t)to_bf16(xv[c][0][i]) | ((uint32_t)to_bf16(xv[c][1][i]) << 16);
+                } else {
+                    Ys[col * LDR + r2] = yv[c][0][i];
+                    Ys[col * LDR + r2 + 1] = yv[c][1][i];
+                    Xs[col * LDR + r2] = xv[c][0][i];
+                    Xs[col * LDR + r2 + 1] = xv[c][1][i];
+                }
+            }
+        }
+    };
 
     f32x16 acc[2][2];
 #pragma unroll
@@ -344,81 +443,11 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
 #pragma unroll
             for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
-    for (int rb = r_begin; rb < r_end; rb += kBK) {
-        float yv[2][8], xv[2][8];
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const int q = tid + kThreads * c;
-            const int rr = q >> 4;          // 0..31
-            const int cc = (q & 15) * 8;    // 0..120
-            const int m = rb + rr;
-            const bool mv = m < r_end;
-            int b = 0, u = 0;
-            if (mv) divmod_fast(m, p.To, inv_to, b, u);
-            // dY
-            const int n = n0 + cc;
-            if (mv && n < p.N) {
-                const size_t yrow = (size_t)b * p.To_full + (size_t)u * p.out_stride + p.out_off;
-                const float *src = p.dY + yrow * p.ldy + n;
-                if (n + 8 <= p.N) {
-                    const float4 v0 = reinterpret_cast<const float4 *>(src)[0];
-                    const float4 v1 = reinterpret_cast<const float4 *>(src)[1];
-                    yv[c][0] = v0.x; yv[c][1] = v0.y; yv[c][2] = v0.z; yv[c][3] = v0.w;
-                    yv[c][4] = v1.x; yv[c][5] = v1.y; yv[c][6] = v1.z; yv[c][7] = v1.w;
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) yv[c][i] = (n + i < p.N) ? src[i] : 0.f;
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) yv[c][i] = 0.f;
-            }
-            // gathered A
-            const int k = k0 + cc;
-            bool ok = mv && k < p.K;
-            int irow = 0, ch = 0;
-            if (ok) {
-                const int j = k / p.cin;
-                ch = k - j * p.cin;
-                irow = u * p.in_stride + mtts::tap_off(p, j);
-                ok = irow >= 0 && irow < p.Ti;
-            }
-            if (ok) {
-                const size_t r = (size_t)b * p.Ti + irow;
-                const float4 *src = reinterpret_cast<const float4 *>(p.A + r * p.lda + ch);
-                const float4 v0 = src[0], v1 = src[1];
-                const float s = p.a_scale ? p.a_scale[r] : 1.0f;
-                xv[c][0] = v0.x * s; xv[c][1] = v0.y * s; xv[c][2] = v0.z * s; xv[c][3] = v0.w * s;
-                xv[c][4] = v1.x * s; xv[c][5] = v1.y * s; xv[c][6] = v1.z * s; xv[c][7] = v1.w * s;
-            } else {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) xv[c][i] = 0.f;
-            }
-            if (do_db) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) colsum[c][i] += yv[c][i];
-            }
-        }
-        __syncthreads();  // previous step's fragment reads are done
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const int q = tid + kThreads * c;
-            const int rr = q >> 4, cc = (q & 15) * 8;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                if constexpr (BF16) {
-                    Ys[(cc + i) * LDR + rr] = to_bf16(yv[c][i]);
-                    Xs[(cc + i) * LDR + rr] = to_bf16(xv[c][i]);
-                } else {
-                    Ys[(cc + i) * LDR + rr] = yv[c][i];
-                    Xs[(cc + i) * LDR + rr] = xv[c][i];
-                }
-            }
-        }
-        __syncthreads();
+    auto compute = [&](int buf) {
+        const ST *Ys = Ybuf + buf * T * LDR, *Xs = Xbuf + buf * T * LDR;
         if constexpr (BF16) {
 #pragma unroll
-            for (int ks = 0; ks < kBK / 16; ++ks) {
+            for (int ks = 0; ks < KB / 16; ++ks) {
                 bf16x8 af[2], bfr[2];
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
@@ -434,7 +463,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
             }
         } else {
 #pragma unroll
-            for (int ks = 0; ks < kBK / 2; ++ks) {
+            for (int ks = 0; ks < KB / 2; ++ks) {
                 float af[2], bfr[2];
 #pragma unroll
                 for (int i = 0; i < 2; ++i) af[i] = Ys[(wr * 64 + i * 32 + lr) * LDR + ks * 2 + lh];
@@ -446,6 +475,18 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
                     for (int j = 0; j < 2; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
             }
+        }
+    };
+
+    if (r_begin < r_end) {
+        load(r_begin);
+        int buf = 0;
+        for (int rb = r_begin; rb < r_end; rb += KB) {
+            store(buf);  // buf was last read two steps ago, before the previous barrier
+            __syncthreads();
+            if (rb + KB < r_end) load(rb + KB);
+            compute(buf);
+            buf ^= 1;
         }
     }
 
@@ -463,41 +504,65 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
             }
         }
     if (do_db) {
-        // thread tid holds column sums of cols (tid&15)*8+i over its row groups; reduce the 16
-        // row groups in a fixed order (deterministic, no float atomics)
+        // (row pair, column) partial sums -> LDS scratch (reusing the operand buffers), then a fixed-order
+        // sum over the KB/2 row pairs (deterministic, no float atomics)
+        float *dbs = reinterpret_cast<float *>(smem);  // [KB/2][T]
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 8; ++i) dbs[tid >> 4][(tid & 15) * 8 + i] = colsum[0][i] + colsum[1][i];
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dbs[c_rp[c] * T + c_cc[c] + i] = colsum[c][i];
         __syncthreads();
         for (int x = tid; x < T; x += kThreads) {
             const int n = n0 + x;
-            float s = 0.f;
-#pragma unroll
-            for (int g = 0; g < 16; ++g) s += dbs[g][x];
-            if (n < p.N) part_db[(size_t)split * p.N + n] = s;
+            float sacc = 0.f;
+            for (int g = 0; g < KB / 2; ++g) sacc += dbs[g * T + x];
+            if (n < p.N) part_db[(size_t)split * p.N + n] = sacc;
         }
     }
 }
 
 // dW (and db) = sum over splits, written in the caller's layout: w_out[n*sn + c*sc + j*sj]
-// for k = j*cin + c.
+// for k = j*cin + c.  Each thread owns 4 consecutive (n, k) (float4 slab reads, NK % 4 == 0); the
+// splits are summed in 4 interleaved chains combined in a fixed order (deterministic).
 __global__ void wgrad_reduce_kernel(const float *__restrict__ part, const float *__restrict__ part_db, int splits,
                                     int N, int K, int cin, int64_t sn, int64_t sc, int64_t sj,
                                     float *__restrict__ w_out, float *__restrict__ db_out, int accumulate) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t NK = (int64_t)N * K;
-    if (idx < NK) {
-        float s = 0.f;
-        for (int i = 0; i < splits; ++i) s += part[(size_t)i * NK + idx];
-        const int n = (int)(idx / K), k = (int)(idx - (int64_t)n * K);
-        const int j = k / cin, c = k - j * cin;
-        float *dst = w_out + n * sn + c * sc + j * sj;
-        *dst = accumulate ? *dst + s : s;
+    if (q * 4 < NK) {
+        float4 a[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 *src = reinterpret_cast<const float4 *>(part) + q;
+        const int64_t step = NK / 4;
+        int i = 0;
+        for (; i + 3 < splits; i += 4) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float4 v = src[(int64_t)(i + c) * step];
+                a[c].x += v.x; a[c].y += v.y; a[c].z += v.z; a[c].w += v.w;
+            }
+        }
+        for (; i < splits; ++i) {
+            const float4 v = src[(int64_t)i * step];
+            a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
+        }
+        const float r[4] = {(a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y),
+                            (a[0].z + a[1].z) + (a[2].z + a[3].z), (a[0].w + a[1].w) + (a[2].w + a[3].w)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t idx = q * 4 + e;
+            const int n = (int)(idx / K), k = (int)(idx - (int64_t)n * K);
+            const int j = k / cin, c = k - j * cin;
+            float *dst = w_out + n * sn + c * sc + j * sj;
+            *dst = accumulate ? *dst + r[e] : r[e];
+        }
     }
-    if (db_out && idx < N) {
+    if (db_out && q < N) {
         float s = 0.f;
-        for (int i = 0; i < splits; ++i) s += part_db[(size_t)i * N + idx];
-        db_out[idx] = accumulate ? db_out[idx] + s : s;
+        for (int i = 0; i < splits; ++i) s += part_db[(size_t)i * N + q];
+        db_out[q] = accumulate ? db_out[q] + s : s;
     }
 }
 
@@ -653,28 +718,46 @@ extern "C" int mtts_act_dropout_bwd(const float *dy, const float *y, float *dx, 
     return mtts::check_launch("act_dropout_bwd_kernel");
 }
 
-static void wgrad_plan(const mtts_conv_wgrad_args &p, int *splits, int *rows_per_split) {
+// Split of the token rows over blocks: about target_blocks blocks in total, whole KB-row steps.
+constexpr int kWgradMaxTarget = 1024;
+static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks, int *splits, int *rows_per_split) {
     const int M = p.nb * p.To;
     const int tiles = ((p.N + 127) / 128) * ((p.K + 127) / 128);
-    int s = (512 + tiles - 1) / tiles;
-    s = max(1, min(s, (M + 255) / 256));
+    int s = (target_blocks + tiles - 1) / tiles;
+    s = max(1, min(s, (M + 4 * kb - 1) / (4 * kb)));  // at least 4 steps per split
     int rps = (M + s - 1) / s;
-    rps = (rps + kBK - 1) / kBK * kBK;
-    *rows_per_split = max(rps, kBK);
-    *splits = (M + *rows_per_split - 1) / *rows_per_split;
-    if (*splits < 1) *splits = 1;
+    rps = (rps + kb - 1) / kb * kb;
+    *rows_per_split = max(rps, kb);
+    *splits = max(1, (M + *rows_per_split - 1) / *rows_per_split);
 }
 
 extern "C" size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *args) {
     if (!args) return 0;
     int splits, rps;
-    wgrad_plan(*args, &splits, &rps);
+    wgrad_plan(*args, 32, kWgradMaxTarget, &splits, &rps);  // upper bound over every schedule
     return mtts::align_up((size_t)splits * args->N * args->K * 4, 256) + (size_t)splits * args->N * 4 + 256;
 }
 
-extern "C" int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precision, float *dw, int64_t sn,
-                               int64_t sc, int64_t sj, float *db, int32_t accumulate, void *workspace,
-                               size_t workspace_bytes, void *hip_stream) {
+template <bool BF16, int KB>
+static int wgrad_launch(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
+                        hipStream_t st) {
+    using Gm = WgradGeom<BF16, KB>;
+    static bool attr_set = false;
+    if (Gm::kLds > 64 * 1024 && !attr_set) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(conv_wgrad_kernel<BF16, KB>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)Gm::kLds) != hipSuccess)
+            return mtts::fail(MTTS_ERR_HIP, "conv_wgrad: LDS attribute");
+        attr_set = true;
+    }
+    dim3 grid((p.N + 127) / 128, (p.K + 127) / 128, splits);
+    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB>), grid, dim3(kThreads), Gm::kLds, st, p, rps, part, part_db);
+    return mtts::check_launch("conv_wgrad_kernel");
+}
+
+// rows_per_step: 32 or 64 (bf16 only), -1 = default; target_blocks: 64..1024, -1 = default
+static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, int rows_per_step, int target_blocks,
+                           float *dw, int64_t sn, int64_t sc, int64_t sj, float *db, int32_t accumulate,
+                           void *workspace, size_t workspace_bytes, void *hip_stream) {
     MTTS_CHECK_ARG(args != nullptr, "conv_wgrad: args is null");
     const mtts_conv_wgrad_args &p = *args;
     int rc = check_gather(p.A, p.lda, p.cin, p.ntaps, p.K);
@@ -682,11 +765,16 @@ extern "C" int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precisi
     MTTS_CHECK_ARG(p.dY && dw && p.N > 0, "conv_wgrad: null dY/dw");
     MTTS_CHECK_ARG(p.ldy % 4 == 0 && (uintptr_t)p.dY % 16 == 0, "conv_wgrad: dY rows must be 16-byte aligned");
     MTTS_CHECK_ARG(precision == MTTS_PREC_BF16 || precision == MTTS_PREC_FP32, "conv_wgrad: bad precision");
+    const bool bf16 = precision == MTTS_PREC_BF16;
+    if (rows_per_step < 0) rows_per_step = 32;
+    if (target_blocks < 0) target_blocks = 512;
+    MTTS_CHECK_ARG(rows_per_step == 32 || (rows_per_step == 64 && bf16), "conv_wgrad: rows_per_step 32 (or 64 bf16)");
+    MTTS_CHECK_ARG(target_blocks >= 64 && target_blocks <= kWgradMaxTarget, "conv_wgrad: target_blocks 64..1024");
     if (workspace_bytes < mtts_conv_wgrad_workspace_size(args) || !workspace)
         return mtts::fail(MTTS_ERR_WORKSPACE, "conv_wgrad: workspace too small");
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
     int splits, rps;
-    wgrad_plan(p, &splits, &rps);
+    wgrad_plan(p, rows_per_step, target_blocks, &splits, &rps);
     float *part = static_cast<float *>(workspace);
     float *part_db = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                                mtts::align_up((size_t)splits * p.N * p.K * 4, 256));
@@ -697,18 +785,29 @@ extern "C" int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precisi
             return mtts::fail(MTTS_ERR_HIP, "conv_wgrad: memset failed");
         splits = 1;
     } else {
-        dim3 grid((p.N + 127) / 128, (p.K + 127) / 128, splits);
-        if (precision == MTTS_PREC_BF16)
-            hipLaunchKernelGGL((conv_wgrad_kernel<true>), grid, dim3(kThreads), 0, st, p, rps, part,
-                               db ? part_db : nullptr);
-        else
-            hipLaunchKernelGGL((conv_wgrad_kernel<false>), grid, dim3(kThreads), 0, st, p, rps, part,
-                               db ? part_db : nullptr);
-        rc = mtts::check_launch("conv_wgrad_kernel");
+        float *pdb = db ? part_db : nullptr;
+        rc = !bf16 ? wgrad_launch<false, 32>(p, splits, rps, part, pdb, st)
+             : rows_per_step == 64 ? wgrad_launch<true, 64>(p, splits, rps, part, pdb, st)
+                                   : wgrad_launch<true, 32>(p, splits, rps, part, pdb, st);
         if (rc) return rc;
     }
-    const int64_t NK = (int64_t)p.N * p.K;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((NK + 255) / 256)), dim3(256), 0, st, part, part_db,
+    const int64_t NK = (int64_t)p.N * p.K;  // K % 8 == 0 (cin % 8): float4 groups never straddle rows
+    const int64_t nthr = std::max<int64_t>(NK / 4, p.N);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, st, part, part_db,
                        splits, p.N, p.K, p.cin, sn, sc, sj, dw, db, accumulate);
     return mtts::check_launch("wgrad_reduce_kernel");
+}
+
+extern "C" int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precision, float *dw, int64_t sn,
+                               int64_t sc, int64_t sj, float *db, int32_t accumulate, void *workspace,
+                               size_t workspace_bytes, void *hip_stream) {
+    return conv_wgrad_impl(args, precision, -1, -1, dw, sn, sc, sj, db, accumulate, workspace, workspace_bytes,
+                           hip_stream);
+}
+
+extern "C" int mtts_conv_wgrad_tile(const mtts_conv_wgrad_args *args, int32_t precision, int32_t rows_per_step,
+                                    int32_t target_blocks, float *dw, int64_t sn, int64_t sc, int64_t sj, float *db,
+                                    int32_t accumulate, void *workspace, size_t workspace_bytes, void *hip_stream) {
+    return conv_wgrad_impl(args, precision, rows_per_step, target_blocks, dw, sn, sc, sj, db, accumulate, workspace,
+                           workspace_bytes, hip_stream);
 }

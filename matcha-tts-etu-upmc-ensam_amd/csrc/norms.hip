@@ -33,7 +33,8 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-// block-wide sum, result broadcast to all threads (fixed reduction order)
+// block-wide sum over NT threads, result broadcast to all threads (fixed reduction order)
+template <int NT = kThreads>
 __device__ __forceinline__ float block_sum(float v, float *red) {
     v = wave_sum(v);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -42,23 +43,27 @@ __device__ __forceinline__ float block_sum(float v, float *red) {
     __syncthreads();
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < kThreads / 64; ++i) s += red[i];
+    for (int i = 0; i < NT / 64; ++i) s += red[i];
     return s;
 }
 
+// GroupNorm kernels: one 16-wave workgroup per (batch, group), so the three streaming passes over
+// the group's T x C/G values keep enough loads in flight (256 workgroups fill the 256 CUs)
+constexpr int kGnThreads = 1024;
+
 // thread layout inside a group: cg/4 float4 columns, kThreads/(cg/4) token rows per pass
-__global__ __launch_bounds__(kThreads) void gn_mish_fwd_kernel(const float *__restrict__ h, const float *__restrict__ gamma,
+__global__ __launch_bounds__(kGnThreads) void gn_mish_fwd_kernel(const float *__restrict__ h, const float *__restrict__ gamma,
                                                                const float *__restrict__ beta,
                                                                const float *__restrict__ mask,
                                                                const float *__restrict__ add, float *__restrict__ y,
                                                                float *__restrict__ mean_out,
                                                                float *__restrict__ rstd_out, int T, int C, int G,
                                                                float eps) {
-    __shared__ float red[kThreads / 64];
+    __shared__ float red[kGnThreads / 64];
     const int g = blockIdx.x, b = blockIdx.y;
     const int cg = C / G;
     const int cols = cg / 4;
-    const int rows_per_pass = kThreads / cols;
+    const int rows_per_pass = kGnThreads / cols;
     const int tid = threadIdx.x;
     const int col = tid % cols, r0 = tid / cols;
     const bool active = r0 < rows_per_pass;
@@ -72,7 +77,7 @@ __global__ __launch_bounds__(kThreads) void gn_mish_fwd_kernel(const float *__re
             const float4 v = *reinterpret_cast<const float4 *>(hb + (size_t)t * C);
             s += (v.x + v.y) + (v.z + v.w);
         }
-    const float mean = block_sum(s, red) / n;
+    const float mean = block_sum<kGnThreads>(s, red) / n;
     float q = 0.f;
     if (active)
         for (int t = r0; t < T; t += rows_per_pass) {
@@ -80,7 +85,7 @@ __global__ __launch_bounds__(kThreads) void gn_mish_fwd_kernel(const float *__re
             const float a = v.x - mean, bq = v.y - mean, cq = v.z - mean, d = v.w - mean;
             q += (a * a + bq * bq) + (cq * cq + d * d);
         }
-    const float var = block_sum(q, red) / n;
+    const float var = block_sum<kGnThreads>(q, red) / n;
     const float rstd = rsqrtf(var + eps);
     if (tid == 0) {
         mean_out[b * G + g] = mean;
@@ -107,17 +112,17 @@ __global__ __launch_bounds__(kThreads) void gn_mish_fwd_kernel(const float *__re
 // Backward.  Per element: u = xhat*gamma + beta, g_u = dy * mask * mish'(u), dxhat = g_u * gamma.
 // dh = rstd * (dxhat - mean(dxhat) - xhat * mean(dxhat * xhat)) over the (b, g) group.
 // Partial outputs per (b, c): pg[b,c] = sum_t g_u*xhat, pb[b,c] = sum_t g_u, dadd[b,c] = sum_t dy.
-__global__ __launch_bounds__(kThreads) void gn_mish_bwd_kernel(
+__global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_kernel(
     const float *__restrict__ dy, const float *__restrict__ h, const float *__restrict__ gamma,
     const float *__restrict__ beta, const float *__restrict__ mask, const float *__restrict__ mean_in,
     const float *__restrict__ rstd_in, float *__restrict__ dh, float *__restrict__ pg, float *__restrict__ pb,
     float *__restrict__ dadd, int T, int C, int G) {
-    __shared__ float red[kThreads / 64];
-    __shared__ float4 chred[3][kThreads];
+    __shared__ float red[kGnThreads / 64];
+    __shared__ float4 chred[3][kGnThreads];
     const int g = blockIdx.x, b = blockIdx.y;
     const int cg = C / G;
     const int cols = cg / 4;
-    const int rows_per_pass = kThreads / cols;
+    const int rows_per_pass = kGnThreads / cols;
     const int tid = threadIdx.x;
     const int col = tid % cols, r0 = tid / cols;
     const bool active = r0 < rows_per_pass;
@@ -151,8 +156,8 @@ __global__ __launch_bounds__(kThreads) void gn_mish_bwd_kernel(
             MTTS_GN_BWD_ACC(v.w, d.w, ga.w, be.w, ag.w, ab.w, ad.w)
 #undef MTTS_GN_BWD_ACC
         }
-    const float m1 = block_sum(s1, red) / n;
-    const float m2 = block_sum(s2, red) / n;
+    const float m1 = block_sum<kGnThreads>(s1, red) / n;
+    const float m2 = block_sum<kGnThreads>(s2, red) / n;
     // per-channel partials: reduce the rows_per_pass threads that share a column, fixed order
     chred[0][tid] = ag;
     chred[1][tid] = ab;
@@ -192,21 +197,40 @@ __global__ __launch_bounds__(kThreads) void gn_mish_bwd_kernel(
     }
 }
 
-// out[c] = sum_r in[r*C + c] for the gamma/beta partials.  Block = 64 columns x 4 row-slices; each
-// slice sums a contiguous quarter of the rows, the 4 slice sums are added in a fixed order.
-__global__ __launch_bounds__(256) void colsum_kernel(const float *__restrict__ in, int R, int C,
-                                                     float *__restrict__ out) {
-    __shared__ float part[4][64];
+// out[c] = sum_r in[r*C + c] (and out2 from in2 when given) for the gamma/beta partials.  Block = 64
+// columns x 16 row-slices (1024 threads); each slice sums an interleaved 1/16 of the rows (4-way
+// unrolled, independent loads in flight), the 16 slice sums are added in a fixed order.
+constexpr int kColsumSlices = 16;
+__global__ __launch_bounds__(64 * kColsumSlices) void colsum_kernel(const float *__restrict__ in,
+                                                                    const float *__restrict__ in2, int R, int C,
+                                                                    float *__restrict__ out, float *__restrict__ out2) {
+    __shared__ float part[2][kColsumSlices][64];
     const int c = blockIdx.x * 64 + (threadIdx.x & 63);
     const int sl = threadIdx.x >> 6;
-    const int per = (R + 3) / 4;
-    const int r0 = sl * per, r1 = min(R, r0 + per);
-    float s = 0.f;
-    if (c < C)
-        for (int r = r0; r < r1; ++r) s += in[(size_t)r * C + c];
-    part[sl][threadIdx.x & 63] = s;
+    float s[2] = {0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+        const float *src = w ? in2 : in;
+        if (!src || c >= C) continue;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        int r = sl;
+        for (; r + 3 * kColsumSlices < R; r += 4 * kColsumSlices) {
+            a0 += src[(size_t)r * C + c];
+            a1 += src[(size_t)(r + kColsumSlices) * C + c];
+            a2 += src[(size_t)(r + 2 * kColsumSlices) * C + c];
+            a3 += src[(size_t)(r + 3 * kColsumSlices) * C + c];
+        }
+        for (; r < R; r += kColsumSlices) a0 += src[(size_t)r * C + c];
+        s[w] = (a0 + a1) + (a2 + a3);
+    }
+    part[0][sl][threadIdx.x & 63] = s[0];
+    part[1][sl][threadIdx.x & 63] = s[1];
     __syncthreads();
-    if (sl == 0 && c < C) out[c] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+    if (sl < 2 && c < C && (sl ? out2 : out)) {
+        float t = 0.f;
+        for (int i = 0; i < kColsumSlices; ++i) t += part[sl][i][threadIdx.x & 63];
+        (sl ? out2 : out)[c] = t;
+    }
 }
 
 // ------------------------------------------------------------------------------ LayerNorm
@@ -270,14 +294,21 @@ __global__ __launch_bounds__(kThreads) void layernorm_fwd_kernel(const float *__
     }
 }
 
-constexpr int kLnRowsPerBlock = 128;  // backward: rows per block (32 per wave)
+// backward: rows per block, sized for ~512 blocks (4..128 rows, a multiple of the 4 waves): the
+// encoder's 3840-row LayerNorms would otherwise run on 30 blocks
+inline int ln_rows_per_block(int M) {
+    int r = (M + 511) / 512;
+    r = (r + 3) / 4 * 4;
+    return r < 4 ? 4 : (r > 128 ? 128 : r);
+}
 
 __global__ __launch_bounds__(kThreads) void layernorm_bwd_kernel(const float *__restrict__ dy, const float *__restrict__ x,
                                                                  const float *__restrict__ w, const float *__restrict__ bia,
                                                                  const float *__restrict__ mean_in,
                                                                  const float *__restrict__ rstd_in, float *__restrict__ dx,
                                                                  float *__restrict__ pw, float *__restrict__ pb, int M,
-                                                                 int C, int act, float p, const uint32_t *__restrict__ seed) {
+                                                                 int C, int act, float p, const uint32_t *__restrict__ seed,
+                                                                 int rows_per_block) {
     __shared__ float4 red[2][kThreads / 64][256];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float4 aw[4], ab[4];
@@ -297,8 +328,8 @@ __global__ __launch_bounds__(kThreads) void layernorm_bwd_kernel(const float *__
         sd1 = seed[1];
     }
     const float inv_keep = 1.f / (1.f - p);
-    const int rbeg = blockIdx.x * kLnRowsPerBlock;
-    for (int rr = wv; rr < kLnRowsPerBlock; rr += kThreads / 64) {
+    const int rbeg = blockIdx.x * rows_per_block;
+    for (int rr = wv; rr < rows_per_block; rr += kThreads / 64) {
         const int row = rbeg + rr;
         if (row >= M) break;
         const float mean = mean_in[row], rstd = rstd_in[row];
@@ -375,12 +406,12 @@ extern "C" int mtts_gn_mish_fwd(const float *h, const float *gamma, const float 
                                 const float *add, float *y, float *mean, float *rstd, int32_t B, int32_t T,
                                 int32_t C, int32_t G, float eps, void *hip_stream) {
     MTTS_CHECK_ARG(h && gamma && beta && y && mean && rstd, "gn_mish_fwd: null pointer");
-    MTTS_CHECK_ARG(B >= 0 && T >= 1 && G >= 1 && C % G == 0 && (C / G) % 4 == 0 && C / G <= 4 * kThreads,
+    MTTS_CHECK_ARG(B >= 0 && T >= 1 && G >= 1 && C % G == 0 && (C / G) % 4 == 0 && C / G <= 4 * kGnThreads,
                    "gn_mish_fwd: need C % G == 0 and (C/G) % 4 == 0");
     MTTS_CHECK_ARG(aligned16(h) && aligned16(y) && aligned16(gamma) && aligned16(beta) && (!add || aligned16(add)),
                    "gn_mish_fwd: tensors must be 16-byte aligned");
     if (B == 0) return MTTS_OK;
-    hipLaunchKernelGGL(gn_mish_fwd_kernel, dim3(G, B), dim3(kThreads), 0, static_cast<hipStream_t>(hip_stream), h,
+    hipLaunchKernelGGL(gn_mish_fwd_kernel, dim3(G, B), dim3(kGnThreads), 0, static_cast<hipStream_t>(hip_stream), h,
                        gamma, beta, mask, add, y, mean, rstd, T, C, G, eps);
     return mtts::check_launch("gn_mish_fwd_kernel");
 }
@@ -403,12 +434,13 @@ extern "C" int mtts_gn_mish_bwd(const float *dy, const float *h, const float *ga
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
     float *pg = static_cast<float *>(workspace);
     float *pb = pg + (size_t)B * C;
-    hipLaunchKernelGGL(gn_mish_bwd_kernel, dim3(G, B), dim3(kThreads), 0, st, dy, h, gamma, beta, mask, mean, rstd,
+    hipLaunchKernelGGL(gn_mish_bwd_kernel, dim3(G, B), dim3(kGnThreads), 0, st, dy, h, gamma, beta, mask, mean, rstd,
                        dh, pg, pb, dadd, T, C, G);
     int rc = mtts::check_launch("gn_mish_bwd_kernel");
     if (rc) return rc;
-    if (dgamma) hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pg, B, C, dgamma);
-    if (dbeta) hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pb, B, C, dbeta);
+    if (dgamma || dbeta)
+        hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(64 * kColsumSlices), 0, st, dgamma ? pg : nullptr,
+                           dbeta ? pb : nullptr, B, C, dgamma, dbeta);
     return mtts::check_launch("colsum_kernel");
 }
 
@@ -429,7 +461,8 @@ extern "C" int mtts_layernorm_fwd(const float *x, const float *w, const float *b
 
 extern "C" size_t mtts_layernorm_bwd_workspace_size(int32_t M, int32_t C) {
     if (M <= 0 || C <= 0) return 0;
-    return (size_t)2 * ((M + kLnRowsPerBlock - 1) / kLnRowsPerBlock) * C * sizeof(float);
+    const int rpb = ln_rows_per_block(M);
+    return (size_t)2 * ((M + rpb - 1) / rpb) * C * sizeof(float);
 }
 
 extern "C" int mtts_layernorm_bwd(const float *dy, const float *x, const float *w, const float *b, const float *mean,
@@ -445,14 +478,16 @@ extern "C" int mtts_layernorm_bwd(const float *dy, const float *x, const float *
     if (!workspace || workspace_bytes < mtts_layernorm_bwd_workspace_size(M, C))
         return mtts::fail(MTTS_ERR_WORKSPACE, "layernorm_bwd: workspace too small");
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
-    const int nblk = (M + kLnRowsPerBlock - 1) / kLnRowsPerBlock;
+    const int rpb = ln_rows_per_block(M);
+    const int nblk = (M + rpb - 1) / rpb;
     float *pw = static_cast<float *>(workspace);
     float *pb = pw + (size_t)nblk * C;
     hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(nblk), dim3(kThreads), 0, st, dy, x, w, b, mean, rstd, dx, pw, pb, M,
-                       C, act, dropout_p, seed);
+                       C, act, dropout_p, seed, rpb);
     int rc = mtts::check_launch("layernorm_bwd_kernel");
     if (rc) return rc;
-    if (dw) hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pw, nblk, C, dw);
-    if (db) hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(256), 0, st, pb, nblk, C, db);
+    if (dw || db)
+        hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(64 * kColsumSlices), 0, st, dw ? pw : nullptr,
+                           db ? pb : nullptr, nblk, C, dw, db);
     return mtts::check_launch("colsum_kernel");
 }
