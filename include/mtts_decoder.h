@@ -71,8 +71,8 @@ typedef struct mtts_conv_gemm_args {
 } mtts_conv_gemm_args;
 
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
-/* Same, with an explicit schedule: 0..10 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;
- * 8..10 are bf16-only 64-wide K steps), MTTS_GEMM_PANEL = the bf16 A-resident panel schedule
+/* Same, with an explicit schedule: 0..13 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;
+ * 8..13 bf16-only: 64-wide K steps, two K steps in flight), MTTS_GEMM_PANEL = the bf16 A-resident panel schedule
  * (csrc/conv_gemm_panel.hip), -1 = heuristic.
  * For tuning and tests; mtts_conv_gemm picks the configuration itself. */
 int mtts_conv_gemm_tile(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg, void *hip_stream);

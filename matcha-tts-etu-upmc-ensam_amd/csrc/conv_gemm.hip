@@ -74,7 +74,7 @@ struct Stage<false> {
 // Block = WM x WN waves; each wave owns TM x TN MFMA tiles of 32x32 -> block tile
 // BM = 32*WM*TM rows x BN = 32*WN*TN cols, K step KB (32, or 64 for bf16: each step is one global
 // round trip, so a longer step halves the exposed latency per MFMA).
-template <bool BF16, int WM, int WN, int TM, int TN, int KB = kBK>
+template <bool BF16, int WM, int WN, int TM, int TN, int KB = kBK, int DEPTH = 1>
 __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_args p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN;
@@ -85,8 +85,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
     static_assert(BF16 || KB == kBK, "fp32 path uses 32-wide K steps");
     using ST = typename Stage<BF16>::T;
     constexpr int LDK = KB + Stage<BF16>::PAD;
-    __shared__ ST As[2][BM * LDK];
-    __shared__ ST Bs[2][BN * LDK];
+    __shared__ ST As[2][(BM + 1) * LDK];  // + one dummy row: staging target of threads without an A chunk
+    __shared__ ST Bs[2][(BN + 1) * LDK];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -99,13 +99,23 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
     const float inv_to = 1.0f / (float)p.To;
 
     Gather ga[CA];
-    int a_row[CA], a_kc[CA], a_j[CA], a_ch[CA];  // (tap, channel) of the chunk at the current K step
+    // tap offsets in registers (a select over kernel-argument loads would become a dependent load)
+    int offr[MTTS_CONV_MAX_TAPS];
+#pragma unroll
+    for (int i = 0; i < MTTS_CONV_MAX_TAPS; ++i) offr[i] = p.off[i];
+    auto toff_of = [&](int j) {
+        int o = offr[0];
+#pragma unroll
+        for (int i = 1; i < MTTS_CONV_MAX_TAPS; ++i) o = j == i ? offr[i] : o;
+        return o;
+    };
+    int a_row[CA], a_kc[CA], a_j[CA], a_ch[CA], a_toff[CA];  // (tap, channel, tap offset) at the current step
     bool a_on[CA];                               // this thread stages an A chunk (tiles with BM*4 < NT)
 #pragma unroll
     for (int c = 0; c < CA; ++c) {
         const int q = tid + NT * c;
         a_on[c] = q < BM * KC;
-        a_row[c] = a_on[c] ? q / KC : 0;
+        a_row[c] = a_on[c] ? q / KC : BM;  // BM: the dummy row
         a_kc[c] = (q % KC) * 8;
         const int m = m0 + a_row[c];
         ga[c].valid = a_on[c] && m < M;
@@ -115,6 +125,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
         ga[c].in_u = u * p.in_stride;
         a_j[c] = a_kc[c] / p.cin;
         a_ch[c] = a_kc[c] - a_j[c] * p.cin;
+        a_toff[c] = toff_of(a_j[c]);
     }
     int b_row[CB], b_kc[CB];
     bool b_on[CB];
@@ -122,91 +133,90 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
     for (int c = 0; c < CB; ++c) {
         const int q = tid + NT * c;
         b_on[c] = q < BN * KC;
-        b_row[c] = b_on[c] ? q / KC : 0;
+        b_row[c] = b_on[c] ? q / KC : BN;  // BN: the dummy row
         b_kc[c] = (q % KC) * 8;
     }
 
-    float ra[CA][8];
-    float rb_f[CB][8];
-    uint4 rb_h[CB];
+    // One staged K step.  Loads are issued unconditionally from clamped (always valid) addresses and
+    // the validity / row-mask scale is applied only when the registers are written to LDS: no branch
+    // around a load and no use of a loaded value before store_tile, so the loads stay in flight
+    // through the compute phase and across the LDS-only barrier (counted vmcnt waits, not vmcnt(0)).
+    struct Regs {
+        float4 a[CA][2];
+        float as[CA];   // raw a_scale value (or junk when a_scale is null)
+        bool aok[CA];
+        float4 bf[CB][2];
+        uint4 bh[CB];
+        bool bok[CB];
+    };
+    Regs R0, R1;  // two steps in flight for DEPTH == 2
 
-    auto load_tile = [&](int k0) {
+    auto load_tile = [&](Regs &R, int k0) {
 #pragma unroll
         for (int c = 0; c < CA; ++c) {
             const int k = k0 + a_kc[c];
-            bool ok = ga[c].valid && k < p.K;
-            const int ch = a_ch[c];
-            int irow = 0;
-            if (ok) {
-                irow = ga[c].in_u + mtts::tap_off(p, a_j[c]);
-                ok = irow >= 0 && irow < p.Ti;
-            }
+            const int irow = ga[c].in_u + a_toff[c];
+            const bool ok = ga[c].valid && k < p.K && irow >= 0 && irow < p.Ti;
+            const size_t r = ok ? (size_t)(ga[c].in_base + irow) : 0;
+            const int ch = ok ? a_ch[c] : 0;
             a_ch[c] += KB;  // advance (tap, channel) to the next K step
-            while (a_ch[c] >= p.cin) { a_ch[c] -= p.cin; ++a_j[c]; }
-            if (ok) {
-                const size_t r = (size_t)(ga[c].in_base + irow);
-                const float4 *src = reinterpret_cast<const float4 *>(p.A + r * p.lda + ch);
-                const float4 v0 = src[0], v1 = src[1];
-                const float s = p.a_scale ? p.a_scale[r] : 1.0f;
-                ra[c][0] = v0.x * s; ra[c][1] = v0.y * s; ra[c][2] = v0.z * s; ra[c][3] = v0.w * s;
-                ra[c][4] = v1.x * s; ra[c][5] = v1.y * s; ra[c][6] = v1.z * s; ra[c][7] = v1.w * s;
-            } else {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) ra[c][i] = 0.f;
+            if (a_ch[c] >= p.cin) {
+                while (a_ch[c] >= p.cin) { a_ch[c] -= p.cin; ++a_j[c]; }
+                a_toff[c] = toff_of(a_j[c]);
             }
+            const float4 *src = reinterpret_cast<const float4 *>(p.A + r * p.lda + ch);
+            R.a[c][0] = src[0];
+            R.a[c][1] = src[1];
+            R.as[c] = *(p.a_scale ? p.a_scale + r : p.A);
+            R.aok[c] = ok;
         }
 #pragma unroll
         for (int c = 0; c < CB; ++c) {
             const int n = n0 + b_row[c];
             const int k = k0 + b_kc[c];
             const bool ok = b_on[c] && n < p.N && k < p.Kp;
+            const size_t off = ok ? (size_t)n * p.Kp + k : 0;
             if constexpr (BF16) {
-                if (ok)
-                    rb_h[c] = *reinterpret_cast<const uint4 *>(static_cast<const uint16_t *>(p.W) +
-                                                               (size_t)n * p.Kp + k);
-                else
-                    rb_h[c] = make_uint4(0, 0, 0, 0);
+                R.bh[c] = *reinterpret_cast<const uint4 *>(static_cast<const uint16_t *>(p.W) + off);
             } else {
-                if (ok) {
-                    const float4 *src = reinterpret_cast<const float4 *>(static_cast<const float *>(p.W) +
-                                                                         (size_t)n * p.Kp + k);
-                    const float4 v0 = src[0], v1 = src[1];
-                    rb_f[c][0] = v0.x; rb_f[c][1] = v0.y; rb_f[c][2] = v0.z; rb_f[c][3] = v0.w;
-                    rb_f[c][4] = v1.x; rb_f[c][5] = v1.y; rb_f[c][6] = v1.z; rb_f[c][7] = v1.w;
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) rb_f[c][i] = 0.f;
-                }
+                const float4 *src = reinterpret_cast<const float4 *>(static_cast<const float *>(p.W) + off);
+                R.bf[c][0] = src[0];
+                R.bf[c][1] = src[1];
             }
+            R.bok[c] = ok;
         }
     };
 
-    auto store_tile = [&](int buf) {
+    auto store_tile = [&](const Regs &R, int buf) {
 #pragma unroll
-        for (int c = 0; c < CA; ++c) {
-            if (!a_on[c]) continue;
+        for (int c = 0; c < CA; ++c) {  // unconditional (threads without a chunk write the dummy row)
+            const float sc = R.aok[c] ? (p.a_scale ? R.as[c] : 1.0f) : 0.0f;
+            const float e[8] = {R.a[c][0].x * sc, R.a[c][0].y * sc, R.a[c][0].z * sc, R.a[c][0].w * sc,
+                                R.a[c][1].x * sc, R.a[c][1].y * sc, R.a[c][1].z * sc, R.a[c][1].w * sc};
             ST *dst = &As[buf][a_row[c] * LDK + a_kc[c]];
             if constexpr (BF16) {
                 uint4 w;
-                w.x = (uint32_t)to_bf16(ra[c][0]) | ((uint32_t)to_bf16(ra[c][1]) << 16);
-                w.y = (uint32_t)to_bf16(ra[c][2]) | ((uint32_t)to_bf16(ra[c][3]) << 16);
-                w.z = (uint32_t)to_bf16(ra[c][4]) | ((uint32_t)to_bf16(ra[c][5]) << 16);
-                w.w = (uint32_t)to_bf16(ra[c][6]) | ((uint32_t)to_bf16(ra[c][7]) << 16);
+                w.x = (uint32_t)to_bf16(e[0]) | ((uint32_t)to_bf16(e[1]) << 16);
+                w.y = (uint32_t)to_bf16(e[2]) | ((uint32_t)to_bf16(e[3]) << 16);
+                w.z = (uint32_t)to_bf16(e[4]) | ((uint32_t)to_bf16(e[5]) << 16);
+                w.w = (uint32_t)to_bf16(e[6]) | ((uint32_t)to_bf16(e[7]) << 16);
                 *reinterpret_cast<uint4 *>(dst) = w;
             } else {
 #pragma unroll
-                for (int i = 0; i < 8; ++i) dst[i] = ra[c][i];
+                for (int i = 0; i < 8; ++i) dst[i] = e[i];
             }
         }
 #pragma unroll
         for (int c = 0; c < CB; ++c) {
-            if (!b_on[c]) continue;
             ST *dst = &Bs[buf][b_row[c] * LDK + b_kc[c]];
             if constexpr (BF16) {
-                *reinterpret_cast<uint4 *>(dst) = rb_h[c];
+                *reinterpret_cast<uint4 *>(dst) = R.bok[c] ? R.bh[c] : make_uint4(0, 0, 0, 0);
             } else {
+                const float m = R.bok[c] ? 1.f : 0.f;
+                const float e[8] = {R.bf[c][0].x * m, R.bf[c][0].y * m, R.bf[c][0].z * m, R.bf[c][0].w * m,
+                                    R.bf[c][1].x * m, R.bf[c][1].y * m, R.bf[c][1].z * m, R.bf[c][1].w * m};
 #pragma unroll
-                for (int i = 0; i < 8; ++i) dst[i] = rb_f[c][i];
+                for (int i = 0; i < 8; ++i) dst[i] = e[i];
             }
         }
     };
@@ -256,15 +266,36 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
         }
     };
 
-    load_tile(0);
-    store_tile(0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const bool more = kt + 1 < nk;
-        if (more) load_tile((kt + 1) * KB);
-        compute(kt & 1);
-        if (more) store_tile((kt + 1) & 1);
-        __syncthreads();
+    if constexpr (BF16 && DEPTH == 2) {
+        // two K steps in flight: the loads of step kt+2 are issued before computing step kt, stored to
+        // LDS after computing step kt+1 -- two compute phases cover each global round trip
+        load_tile(R0, 0);
+        store_tile(R0, 0);
+        load_tile(R1, KB);
+        mtts::lds_barrier();
+        for (int kt = 0; kt < nk; kt += 2) {
+            load_tile(R0, (kt + 2) * KB);
+            compute(0);
+            store_tile(R1, 1);
+            mtts::lds_barrier();
+            if (kt + 1 >= nk) break;
+            load_tile(R1, (kt + 3) * KB);
+            compute(1);
+            store_tile(R0, 0);
+            mtts::lds_barrier();
+        }
+    } else {
+        // branch-free body (no phi copies of in-flight registers): the step after the last one loads
+        // clamped addresses with every chunk masked off and stores into the unused buffer
+        load_tile(R0, 0);
+        store_tile(R0, 0);
+        mtts::lds_barrier();
+        for (int kt = 0; kt < nk; ++kt) {
+            load_tile(R0, (kt + 1) * KB);
+            compute(kt & 1);
+            store_tile(R0, (kt + 1) & 1);
+            mtts::lds_barrier();
+        }
     }
 
     // ---- epilogue ----
@@ -348,7 +379,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
     // per-chunk constants: row pair, column group, and the A gather's (tap offset, channel) -- k is
     // fixed per chunk, so no division in the loop
     int c_rp[CH], c_cc[CH], c_toff[CH], c_ch[CH];
-    bool c_kok[CH], c_nok[CH], c_nfull[CH];
+    bool c_kok[CH], c_nok[CH];
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
         const int q = tid + kThreads * c;
@@ -359,11 +390,17 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
         const int j = c_kok[c] ? k / p.cin : 0;
         c_ch[c] = k - j * p.cin;
         c_toff[c] = mtts::tap_off(p, j);
-        c_nok[c] = n < p.N;
-        c_nfull[c] = n + 4 <= p.N;
+        c_nok[c] = n < p.N;  // N % 4 == 0: a 4-column group is all in or all out
     }
 
-    float yv[CH][2][4], xv[CH][2][4];
+    // One staged step, loaded unconditionally from clamped addresses; validity, the row mask and the
+    // bias column sums are applied at store time so the loads stay in flight through the compute.
+    struct Regs {
+        float4 y[CH][2], x[CH][2];
+        float xs[CH][2];
+        bool yok[CH][2], xok[CH][2];
+    };
+    Regs R;
     float colsum[CH][4];
 #pragma unroll
     for (int c = 0; c < CH; ++c)
@@ -378,58 +415,51 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
                 const int m = rb + 2 * c_rp[c] + h;
                 const bool mv = m < r_end;
                 int b = 0, u = 0;
-                if (mv) divmod_fast(m, p.To, inv_to, b, u);
-                float4 y4 = make_float4(0.f, 0.f, 0.f, 0.f), x4 = y4;
-                if (mv && c_nok[c]) {
-                    const float *src =
-                        p.dY + ((size_t)b * p.To_full + (size_t)u * p.out_stride + p.out_off) * p.ldy + n0 + c_cc[c];
-                    if (c_nfull[c]) {
-                        y4 = *reinterpret_cast<const float4 *>(src);
-                    } else {
-                        const int n = n0 + c_cc[c];
-                        y4.x = src[0];
-                        y4.y = n + 1 < p.N ? src[1] : 0.f;
-                        y4.z = n + 2 < p.N ? src[2] : 0.f;
-                        y4.w = n + 3 < p.N ? src[3] : 0.f;
-                    }
-                }
+                divmod_fast(mv ? m : 0, p.To, inv_to, b, u);
+                const bool yok = mv && c_nok[c];
+                const size_t yrow = yok ? (size_t)b * p.To_full + (size_t)u * p.out_stride + p.out_off : 0;
+                R.y[c][h] = *reinterpret_cast<const float4 *>(p.dY + yrow * p.ldy + (yok ? n0 + c_cc[c] : 0));
+                R.yok[c][h] = yok;
                 const int irow = u * p.in_stride + c_toff[c];
-                if (mv && c_kok[c] && irow >= 0 && irow < p.Ti) {
-                    const size_t r = (size_t)b * p.Ti + irow;
-                    x4 = *reinterpret_cast<const float4 *>(p.A + r * p.lda + c_ch[c]);
-                    if (p.a_scale) {
-                        const float sc = p.a_scale[r];
-                        x4.x *= sc; x4.y *= sc; x4.z *= sc; x4.w *= sc;
-                    }
-                }
-                yv[c][h][0] = y4.x; yv[c][h][1] = y4.y; yv[c][h][2] = y4.z; yv[c][h][3] = y4.w;
-                xv[c][h][0] = x4.x; xv[c][h][1] = x4.y; xv[c][h][2] = x4.z; xv[c][h][3] = x4.w;
+                const bool xok = mv && c_kok[c] && irow >= 0 && irow < p.Ti;
+                const size_t r = xok ? (size_t)b * p.Ti + irow : 0;
+                R.x[c][h] = *reinterpret_cast<const float4 *>(p.A + r * p.lda + (xok ? c_ch[c] : 0));
+                R.xs[c][h] = *(p.a_scale ? p.a_scale + r : p.A);
+                R.xok[c][h] = xok;
             }
-        if (do_db) {
-#pragma unroll
-            for (int c = 0; c < CH; ++c)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) colsum[c][i] += yv[c][0][i] + yv[c][1][i];
-        }
     };
     auto store = [&](int buf) {
         ST *Ys = Ybuf + buf * T * LDR, *Xs = Xbuf + buf * T * LDR;
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
+            float yv[2][4], xv[2][4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const float ym = R.yok[c][h] ? 1.f : 0.f;
+                const float xm = R.xok[c][h] ? (p.a_scale ? R.xs[c][h] : 1.f) : 0.f;
+                yv[h][0] = R.y[c][h].x * ym; yv[h][1] = R.y[c][h].y * ym;
+                yv[h][2] = R.y[c][h].z * ym; yv[h][3] = R.y[c][h].w * ym;
+                xv[h][0] = R.x[c][h].x * xm; xv[h][1] = R.x[c][h].y * xm;
+                xv[h][2] = R.x[c][h].z * xm; xv[h][3] = R.x[c][h].w * xm;
+            }
+            if (do_db) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) colsum[c][i] += yv[0][i] + yv[1][i];
+            }
             const int r2 = 2 * c_rp[c];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int col = c_cc[c] + i;
                 if constexpr (BF16) {
                     *reinterpret_cast<uint32_t *>(&Ys[col * LDR + r2]) =
-                        (uint32_t)to_bf16(yv[c][0][i]) | ((uint32_t)to_bf16(yv[c][1][i]) << 16);
+                        (uint32_t)to_bf16(yv[0][i]) | ((uint32_t)to_bf16(yv[1][i]) << 16);
                     *reinterpret_cast<uint32_t *>(&Xs[col * LDR + r2]) =
-                        (uint32_t)to_bf16(xv[c][0][i]) | ((uint32_t)to_bf16(xv[c][1][i]) << 16);
+                        (uint32_t)to_bf16(xv[0][i]) | ((uint32_t)to_bf16(xv[1][i]) << 16);
                 } else {
-                    Ys[col * LDR + r2] = yv[c][0][i];
-                    Ys[col * LDR + r2 + 1] = yv[c][1][i];
-                    Xs[col * LDR + r2] = xv[c][0][i];
-                    Xs[col * LDR + r2 + 1] = xv[c][1][i];
+                    Ys[col * LDR + r2] = yv[0][i];
+                    Ys[col * LDR + r2 + 1] = yv[1][i];
+                    Xs[col * LDR + r2] = xv[0][i];
+                    Xs[col * LDR + r2 + 1] = xv[1][i];
                 }
             }
         }
@@ -483,8 +513,8 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
         int buf = 0;
         for (int rb = r_begin; rb < r_end; rb += KB) {
             store(buf);  // buf was last read two steps ago, before the previous barrier
-            __syncthreads();
-            if (rb + KB < r_end) load(rb + KB);
+            mtts::lds_barrier();
+            load(rb + KB);  // unconditional: past r_end every row is masked off (branch-free body)
             compute(buf);
             buf ^= 1;
         }
@@ -579,7 +609,7 @@ int check_gather(const void *A, int lda, int cin, int ntaps, int K) {
 
 // Tile configurations: {WM, WN, TM, TN} -> BM x BN = 32*WM*TM x 32*WN*TN, 64*WM*WN threads.
 struct TileCfg {
-    int wm, wn, tm, tn, kb;
+    int wm, wn, tm, tn, kb, depth = 1;  // depth: K steps in flight in registers (2: bf16 only)
 };
 constexpr TileCfg kCfgs[] = {
     {2, 2, 1, 2, 32},  // 0: 64 x 128, 256 thr (round-1 default)
@@ -593,6 +623,9 @@ constexpr TileCfg kCfgs[] = {
     {1, 4, 1, 1, 64},  // 8: config 7 with 64-wide K steps (bf16)
     {2, 4, 1, 2, 64},  // 9: config 5 with 64-wide K steps (bf16)
     {2, 2, 1, 2, 64},  // 10: config 0 with 64-wide K steps (bf16)
+    {1, 4, 1, 1, 32, 2},  // 11: config 7, two K steps in flight (bf16)
+    {1, 4, 1, 1, 64, 2},  // 12: config 8, two K steps in flight (bf16)
+    {2, 4, 1, 2, 64, 2},  // 13: config 9, two K steps in flight (bf16)
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -601,7 +634,7 @@ static void launch_cfg(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
     constexpr TileCfg c = kCfgs[C];
     constexpr int BM = 32 * c.wm * c.tm, BN = 32 * c.wn * c.tn;
     dim3 grid((M + BM - 1) / BM, (p.N + BN - 1) / BN);
-    hipLaunchKernelGGL((conv_gemm_kernel<BF16, c.wm, c.wn, c.tm, c.tn, (BF16 ? c.kb : kBK)>), grid,
+    hipLaunchKernelGGL((conv_gemm_kernel<BF16, c.wm, c.wn, c.tm, c.tn, (BF16 ? c.kb : kBK), (BF16 ? c.depth : 1)>), grid,
                        dim3(64 * c.wm * c.wn), 0, st, p);
 }
 
@@ -618,18 +651,21 @@ static void launch_by_id(int id, const mtts_conv_gemm_args &p, int M, hipStream_
         case 7: launch_cfg<BF16, 7>(p, M, st); break;
         case 8: launch_cfg<BF16, 8>(p, M, st); break;
         case 9: launch_cfg<BF16, 9>(p, M, st); break;
-        default: launch_cfg<BF16, 10>(p, M, st); break;
+        case 10: launch_cfg<BF16, 10>(p, M, st); break;
+        case 11: launch_cfg<BF16, 11>(p, M, st); break;
+        case 12: launch_cfg<BF16, 12>(p, M, st); break;
+        default: launch_cfg<BF16, 13>(p, M, st); break;
     }
 }
 
-// From the tile sweep on the train step's shapes (tools/gemm_sweep.py, profiles/r01/gemm_sweep_bf16.log):
-// 32 x 128 tiles (config 7) are best or within 10% everywhere; when that grid is small (<= 3 blocks
-// per CU: half-resolution and narrow GEMMs) the same tile with 64-wide K steps (config 8) is 10-35%
-// faster because each block then waits on half as many global round trips.
+// From the tile sweep on the train step's shapes (tools/gemm_sweep.py, profiles/r01/gemm_sweep_bf16.log;
+// graph-timed): with branch-free staging, 32 x 128 tiles with 64-wide K steps and two K steps in
+// flight (config 12) are best or within ~5% wherever K >= 384; short reductions (K <= 256: at most
+// four 64-wide steps) keep 32-wide steps (config 7).  fp32 (parity mode) uses config 7.
 static int pick_cfg(const mtts_conv_gemm_args &p, int M, bool bf16) {
+    (void)M;
     if (!bf16) return 7;
-    const long blocks = (long)((M + 31) / 32) * ((p.N + 127) / 128);
-    return blocks <= 768 ? 8 : 7;
+    return p.K >= 384 ? 12 : 7;
 }
 
 static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, int cfg, void *hip_stream) {
@@ -720,10 +756,13 @@ extern "C" int mtts_act_dropout_bwd(const float *dy, const float *y, float *dx, 
 
 // Split of the token rows over blocks: about target_blocks blocks in total, whole KB-row steps.
 constexpr int kWgradMaxTarget = 1024;
+// target_blocks < 0: the sweep's rule (tools/wgrad_sweep.py) -- about 768 rows per split (long enough
+// to amortize the pipeline and the split's slab write) but never fewer than 256 blocks.
 static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks, int *splits, int *rows_per_split) {
     const int M = p.nb * p.To;
     const int tiles = ((p.N + 127) / 128) * ((p.K + 127) / 128);
-    int s = (target_blocks + tiles - 1) / tiles;
+    int s = target_blocks > 0 ? (target_blocks + tiles - 1) / tiles
+                              : max((256 + tiles - 1) / tiles, (M + 384) / 768);
     s = max(1, min(s, (M + 4 * kb - 1) / (4 * kb)));  // at least 4 steps per split
     int rps = (M + s - 1) / s;
     rps = (rps + kb - 1) / kb * kb;
@@ -734,7 +773,10 @@ static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks,
 extern "C" size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *args) {
     if (!args) return 0;
     int splits, rps;
-    wgrad_plan(*args, 32, kWgradMaxTarget, &splits, &rps);  // upper bound over every schedule
+    int s2, r2;  // upper bound over every schedule (explicit targets and the default rule)
+    wgrad_plan(*args, 32, kWgradMaxTarget, &splits, &rps);
+    wgrad_plan(*args, 32, -1, &s2, &r2);
+    splits = max(splits, s2);
     return mtts::align_up((size_t)splits * args->N * args->K * 4, 256) + (size_t)splits * args->N * 4 + 256;
 }
 
@@ -762,14 +804,14 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
     const mtts_conv_wgrad_args &p = *args;
     int rc = check_gather(p.A, p.lda, p.cin, p.ntaps, p.K);
     if (rc) return rc;
-    MTTS_CHECK_ARG(p.dY && dw && p.N > 0, "conv_wgrad: null dY/dw");
+    MTTS_CHECK_ARG(p.dY && dw && p.N > 0 && p.N % 4 == 0, "conv_wgrad: null dY/dw or N % 4 != 0");
     MTTS_CHECK_ARG(p.ldy % 4 == 0 && (uintptr_t)p.dY % 16 == 0, "conv_wgrad: dY rows must be 16-byte aligned");
     MTTS_CHECK_ARG(precision == MTTS_PREC_BF16 || precision == MTTS_PREC_FP32, "conv_wgrad: bad precision");
     const bool bf16 = precision == MTTS_PREC_BF16;
     if (rows_per_step < 0) rows_per_step = 32;
-    if (target_blocks < 0) target_blocks = 512;
     MTTS_CHECK_ARG(rows_per_step == 32 || (rows_per_step == 64 && bf16), "conv_wgrad: rows_per_step 32 (or 64 bf16)");
-    MTTS_CHECK_ARG(target_blocks >= 64 && target_blocks <= kWgradMaxTarget, "conv_wgrad: target_blocks 64..1024");
+    MTTS_CHECK_ARG(target_blocks < 0 || (target_blocks >= 64 && target_blocks <= kWgradMaxTarget),
+                   "conv_wgrad: target_blocks 64..1024 (or -1)");
     if (workspace_bytes < mtts_conv_wgrad_workspace_size(args) || !workspace)
         return mtts::fail(MTTS_ERR_WORKSPACE, "conv_wgrad: workspace too small");
     hipStream_t st = static_cast<hipStream_t>(hip_stream);

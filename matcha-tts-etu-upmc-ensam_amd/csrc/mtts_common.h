@@ -39,6 +39,15 @@ __device__ __forceinline__ bool dropout_keep(uint32_t seed_lo, uint32_t seed_hi,
     return (float)(x >> 8) * (1.0f / 16777216.0f) >= p;
 }
 
+// Workgroup barrier for an LDS hand-off only: waits for this wave's LDS operations, NOT for its
+// outstanding global loads.  __syncthreads() carries a fence that makes hipcc drain vmcnt before the
+// s_barrier, which would turn every register prefetch into a synchronous load.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // Tap offset j of a conv argument struct (static indexing only: no private-memory copy of off[]).
 template <class P>
 __device__ __forceinline__ int tap_off(const P &p, int j) {
