@@ -142,13 +142,17 @@ template <bool BF16, int D>
 struct TileLoader {
     using Gm = G<BF16, D>;
     float4 v[Gm::F4];
+    bool ok[Gm::F4];
+    // unconditional loads from clamped addresses (validity applied in store): no branch around a load,
+    // so the loads stay in flight through the compute phase
     __device__ void load(const float *base, int ld, int b, int T, int r0, int tid, int dh) {
 #pragma unroll
         for (int i = 0; i < Gm::F4; ++i) {
             const int idx = tid + kThreads * i;
             const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
-            v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (r0 + r < T && c < dh) v[i] = *reinterpret_cast<const float4 *>(base + ((size_t)b * T + r0 + r) * ld + c);
+            ok[i] = r0 + r < T && c < dh;
+            const size_t off = ok[i] ? ((size_t)b * T + r0 + r) * ld + c : (size_t)b * T * ld;
+            v[i] = *reinterpret_cast<const float4 *>(base + off);
         }
     }
     __device__ void store(typename Gm::T *rowt, typename Gm::T *trt, int tid) const {
@@ -156,7 +160,8 @@ struct TileLoader {
         for (int i = 0; i < Gm::F4; ++i) {
             const int idx = tid + kThreads * i;
             const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
-            const float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+            const float m = ok[i] ? 1.f : 0.f;
+            const float e[4] = {v[i].x * m, v[i].y * m, v[i].z * m, v[i].w * m};
             if constexpr (BF16) {
                 if (rowt)
                     *reinterpret_cast<uint2 *>(rowt + r * Gm::LDR + c) = make_uint2(pack2(e[0], e[1]), pack2(e[2], e[3]));
@@ -205,22 +210,23 @@ __device__ __forceinline__ T *carve(unsigned char *&p, size_t n) {
 // publish it (double buffer: into the other stage, one barrier; single buffer: two barriers).
 template <int NB, typename Load, typename Store, typename Compute>
 __device__ __forceinline__ void tile_loop(int ntiles, Load &&load, Store &&store, Compute &&compute) {
+    // LDS-only barriers (mtts::lds_barrier): the next tile's global loads stay in flight across them
     load(0);
     store(0);
-    __syncthreads();
+    mtts::lds_barrier();
     for (int it = 0; it < ntiles; ++it) {
         const int buf = NB == 2 ? (it & 1) : 0;
         const bool more = it + 1 < ntiles;
-        if (more) load((it + 1) * kTile);
+        load((it + 1) * kTile);  // past the last tile every row is masked off (branch-free body)
         compute(buf, it * kTile);
         if constexpr (NB == 2) {
-            if (more) store(buf ^ 1);
-            __syncthreads();
+            store(buf ^ 1);
+            mtts::lds_barrier();
         } else {
-            __syncthreads();
+            mtts::lds_barrier();
             if (more) {
                 store(0);
-                __syncthreads();
+                mtts::lds_barrier();
             }
         }
     }
@@ -261,9 +267,10 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
     auto load = [&](int k0) {
         lk.load(Kb, p.ldq, b, T, k0, tid, dh);
         lv.load(Vb, p.ldq, b, T, k0, tid, dh);
-        if (tid < kTile) {
-            const int key = k0 + tid;
-            bias_r = key < T ? (p.key_bias ? p.key_bias[(size_t)b * T + key] * kLog2e : 0.f) : -INFINITY;
+        {
+            const int key = k0 + (tid & (kTile - 1));
+            const float raw = *(p.key_bias ? p.key_bias + (size_t)b * T + min(key, T - 1) : p.q);
+            bias_r = key < T ? (p.key_bias ? raw * kLog2e : 0.f) : -INFINITY;
         }
     };
     auto store = [&](int buf) {
@@ -392,9 +399,10 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p,
     auto load = [&](int k0) {
         lk.load(Kb, p.ldq, b, T, k0, tid, dh);
         lv.load(Vb, p.ldq, b, T, k0, tid, dh);
-        if (tid < kTile) {
-            const int key = k0 + tid;
-            bias_r = key < T ? (p.key_bias ? p.key_bias[(size_t)b * T + key] * kLog2e : 0.f) : -INFINITY;
+        {
+            const int key = k0 + (tid & (kTile - 1));
+            const float raw = *(p.key_bias ? p.key_bias + (size_t)b * T + min(key, T - 1) : p.q);
+            bias_r = key < T ? (p.key_bias ? raw * kLog2e : 0.f) : -INFINITY;
         }
     };
     auto store = [&](int buf) {
@@ -493,10 +501,11 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkv_kernel(mtts_attn_args p
     auto load = [&](int q0) {
         lq.load(Qb, p.ldq, b, T, q0, tid, dh);
         lg.load(Gb, g.lddo, b, T, q0, tid, dh);
-        if (tid < kTile) {
-            const int qq = q0 + tid;
-            lse_r = qq < T ? p.lse[sbase + qq] : INFINITY;
-            d_r = qq < T ? Drow[sbase + qq] : 0.f;
+        {
+            const int qq = q0 + (tid & (kTile - 1));
+            const float l_raw = p.lse[sbase + min(qq, T - 1)], d_raw = Drow[sbase + min(qq, T - 1)];
+            lse_r = qq < T ? l_raw : INFINITY;
+            d_r = qq < T ? d_raw : 0.f;
         }
     };
     auto store = [&](int buf) {
