@@ -134,8 +134,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # MTTS_BENCH_SHARED_GPU=1: every rank on cuda:0 over gloo -- rehearses the multi-rank graph path on
+        # a one-GPU box (RCCL refuses two ranks on one device); never used for reported numbers
+        if os.environ.get("MTTS_BENCH_SHARED_GPU") == "1":
+            local = 0
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 

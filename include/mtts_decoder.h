@@ -100,10 +100,11 @@ int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precision, float *
                     int64_t sj, float *db, int32_t accumulate, void *workspace, size_t workspace_bytes,
                     void *hip_stream);
 /* Same, with an explicit schedule: rows_per_step 32 (or 64, bf16), target_blocks 64..1024 for the
- * row split (-1 = defaults).  For tuning; mtts_conv_wgrad_workspace_size covers every schedule. */
+ * row split, depth 1 (or 2, bf16) row steps in flight (-1 = defaults).  For tuning;
+ * mtts_conv_wgrad_workspace_size covers every schedule. */
 int mtts_conv_wgrad_tile(const mtts_conv_wgrad_args *args, int32_t precision, int32_t rows_per_step,
-                         int32_t target_blocks, float *dw, int64_t sn, int64_t sc, int64_t sj, float *db,
-                         int32_t accumulate, void *workspace, size_t workspace_bytes, void *hip_stream);
+                         int32_t target_blocks, int32_t depth, float *dw, int64_t sn, int64_t sc, int64_t sj,
+                         float *db, int32_t accumulate, void *workspace, size_t workspace_bytes, void *hip_stream);
 
 /*
  * y[b,t,c] = mish(GN(h)[b,t,c]) * mask[b,t] + add[b,c]      (mask / add optional)

@@ -356,7 +356,7 @@ struct WgradGeom {
     static_assert((size_t)(KB / 2) * T * sizeof(float) <= kLds, "db scratch fits the operand buffers");
 };
 
-template <bool BF16, int KB>
+template <bool BF16, int KB, int DEPTH>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_args p, int rows_per_split,
                                                                float *__restrict__ part, float *__restrict__ part_db) {
     using Gm = WgradGeom<BF16, KB>;
@@ -400,14 +400,14 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
         float xs[CH][2];
         bool yok[CH][2], xok[CH][2];
     };
-    Regs R;
+    Regs R0, R1;  // DEPTH 2: two row steps in flight
     float colsum[CH][4];
 #pragma unroll
     for (int c = 0; c < CH; ++c)
 #pragma unroll
         for (int i = 0; i < 4; ++i) colsum[c][i] = 0.f;
 
-    auto load = [&](int rb) {
+    auto load = [&](Regs &R, int rb) {
 #pragma unroll
         for (int c = 0; c < CH; ++c)
 #pragma unroll
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
                 R.xok[c][h] = xok;
             }
     };
-    auto store = [&](int buf) {
+    auto store = [&](const Regs &R, int buf) {
         ST *Ys = Ybuf + buf * T * LDR, *Xs = Xbuf + buf * T * LDR;
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
@@ -509,14 +509,32 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
     };
 
     if (r_begin < r_end) {
-        load(r_begin);
-        int buf = 0;
-        for (int rb = r_begin; rb < r_end; rb += KB) {
-            store(buf);  // buf was last read two steps ago, before the previous barrier
+        if constexpr (DEPTH == 2) {
+            load(R0, r_begin);
+            load(R1, r_begin + KB);
+            store(R0, 0);
             mtts::lds_barrier();
-            load(rb + KB);  // unconditional: past r_end every row is masked off (branch-free body)
-            compute(buf);
-            buf ^= 1;
+            for (int rb = r_begin; rb < r_end; rb += 2 * KB) {
+                load(R0, rb + 2 * KB);
+                compute(0);
+                store(R1, 1);
+                mtts::lds_barrier();
+                if (rb + KB >= r_end) break;
+                load(R1, rb + 3 * KB);
+                compute(1);
+                store(R0, 0);
+                mtts::lds_barrier();
+            }
+        } else {
+            load(R0, r_begin);
+            int buf = 0;
+            for (int rb = r_begin; rb < r_end; rb += KB) {
+                store(R0, buf);  // buf was last read two steps ago, before the previous barrier
+                mtts::lds_barrier();
+                load(R0, rb + KB);  // unconditional: past r_end every row is masked off (branch-free body)
+                compute(buf);
+                buf ^= 1;
+            }
         }
     }
 
@@ -780,24 +798,26 @@ extern "C" size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *arg
     return mtts::align_up((size_t)splits * args->N * args->K * 4, 256) + (size_t)splits * args->N * 4 + 256;
 }
 
-template <bool BF16, int KB>
+template <bool BF16, int KB, int DEPTH>
 static int wgrad_launch(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
                         hipStream_t st) {
     using Gm = WgradGeom<BF16, KB>;
     static bool attr_set = false;
     if (Gm::kLds > 64 * 1024 && !attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(conv_wgrad_kernel<BF16, KB>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(conv_wgrad_kernel<BF16, KB, DEPTH>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)Gm::kLds) != hipSuccess)
             return mtts::fail(MTTS_ERR_HIP, "conv_wgrad: LDS attribute");
         attr_set = true;
     }
     dim3 grid((p.N + 127) / 128, (p.K + 127) / 128, splits);
-    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB>), grid, dim3(kThreads), Gm::kLds, st, p, rps, part, part_db);
+    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH>), grid, dim3(kThreads), Gm::kLds, st, p, rps, part, part_db);
     return mtts::check_launch("conv_wgrad_kernel");
 }
 
-// rows_per_step: 32 or 64 (bf16 only), -1 = default; target_blocks: 64..1024, -1 = default
+// rows_per_step: 32 or 64 (bf16 only), -1 = default; target_blocks: 64..1024, -1 = default;
+// depth: row steps in flight, 1 or 2 (bf16 only), -1 = default
 static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, int rows_per_step, int target_blocks,
+                           int depth,
                            float *dw, int64_t sn, int64_t sc, int64_t sj, float *db, int32_t accumulate,
                            void *workspace, size_t workspace_bytes, void *hip_stream) {
     MTTS_CHECK_ARG(args != nullptr, "conv_wgrad: args is null");
@@ -809,7 +829,9 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
     MTTS_CHECK_ARG(precision == MTTS_PREC_BF16 || precision == MTTS_PREC_FP32, "conv_wgrad: bad precision");
     const bool bf16 = precision == MTTS_PREC_BF16;
     if (rows_per_step < 0) rows_per_step = 32;
+    if (depth < 0) depth = 1;
     MTTS_CHECK_ARG(rows_per_step == 32 || (rows_per_step == 64 && bf16), "conv_wgrad: rows_per_step 32 (or 64 bf16)");
+    MTTS_CHECK_ARG(depth == 1 || (depth == 2 && bf16), "conv_wgrad: depth 1 (or 2 bf16)");
     MTTS_CHECK_ARG(target_blocks < 0 || (target_blocks >= 64 && target_blocks <= kWgradMaxTarget),
                    "conv_wgrad: target_blocks 64..1024 (or -1)");
     if (workspace_bytes < mtts_conv_wgrad_workspace_size(args) || !workspace)
@@ -828,9 +850,11 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
         splits = 1;
     } else {
         float *pdb = db ? part_db : nullptr;
-        rc = !bf16 ? wgrad_launch<false, 32>(p, splits, rps, part, pdb, st)
-             : rows_per_step == 64 ? wgrad_launch<true, 64>(p, splits, rps, part, pdb, st)
-                                   : wgrad_launch<true, 32>(p, splits, rps, part, pdb, st);
+        rc = !bf16 ? wgrad_launch<false, 32, 1>(p, splits, rps, part, pdb, st)
+             : rows_per_step == 64 ? (depth == 2 ? wgrad_launch<true, 64, 2>(p, splits, rps, part, pdb, st)
+                                                 : wgrad_launch<true, 64, 1>(p, splits, rps, part, pdb, st))
+                                   : (depth == 2 ? wgrad_launch<true, 32, 2>(p, splits, rps, part, pdb, st)
+                                                 : wgrad_launch<true, 32, 1>(p, splits, rps, part, pdb, st));
         if (rc) return rc;
     }
     const int64_t NK = (int64_t)p.N * p.K;  // K % 8 == 0 (cin % 8): float4 groups never straddle rows
@@ -843,13 +867,14 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
 extern "C" int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precision, float *dw, int64_t sn,
                                int64_t sc, int64_t sj, float *db, int32_t accumulate, void *workspace,
                                size_t workspace_bytes, void *hip_stream) {
-    return conv_wgrad_impl(args, precision, -1, -1, dw, sn, sc, sj, db, accumulate, workspace, workspace_bytes,
+    return conv_wgrad_impl(args, precision, -1, -1, -1, dw, sn, sc, sj, db, accumulate, workspace, workspace_bytes,
                            hip_stream);
 }
 
 extern "C" int mtts_conv_wgrad_tile(const mtts_conv_wgrad_args *args, int32_t precision, int32_t rows_per_step,
-                                    int32_t target_blocks, float *dw, int64_t sn, int64_t sc, int64_t sj, float *db,
-                                    int32_t accumulate, void *workspace, size_t workspace_bytes, void *hip_stream) {
-    return conv_wgrad_impl(args, precision, rows_per_step, target_blocks, dw, sn, sc, sj, db, accumulate, workspace,
-                           workspace_bytes, hip_stream);
+                                    int32_t target_blocks, int32_t depth, float *dw, int64_t sn, int64_t sc, int64_t sj,
+                                    float *db, int32_t accumulate, void *workspace, size_t workspace_bytes,
+                                    void *hip_stream) {
+    return conv_wgrad_impl(args, precision, rows_per_step, target_blocks, depth, dw, sn, sc, sj, db, accumulate,
+                           workspace, workspace_bytes, hip_stream);
 }

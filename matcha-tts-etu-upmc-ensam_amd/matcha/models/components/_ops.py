@@ -95,7 +95,7 @@ N.register("mtts_conv_wgrad_workspace_size", _SZ, [ctypes.POINTER(ConvWgradArgs)
 N.register("mtts_conv_wgrad", ctypes.c_int,
            [ctypes.POINTER(ConvWgradArgs), _I, _P, _I64, _I64, _I64, _P, _I, _P, _SZ, _P])
 N.register("mtts_conv_wgrad_tile", ctypes.c_int,
-           [ctypes.POINTER(ConvWgradArgs), _I, _I, _I, _P, _I64, _I64, _I64, _P, _I, _P, _SZ, _P])
+           [ctypes.POINTER(ConvWgradArgs), _I, _I, _I, _I, _P, _I64, _I64, _I64, _P, _I, _P, _SZ, _P])
 N.register("mtts_gn_mish_fwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
 N.register("mtts_gn_mish_bwd_workspace_size", _SZ, [_I, _I])
 N.register("mtts_gn_mish_bwd", ctypes.c_int,
@@ -308,7 +308,7 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
 
 
 def _wgrad(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin, N_, dw, strides, *, prec,
-           a_scale=None, db=None, rows_per_step=-1, target_blocks=-1):
+           a_scale=None, db=None, rows_per_step=-1, target_blocks=-1, depth=-1):
     args = ConvWgradArgs()
     args.dY, args.ldy, args.To_full, args.out_stride, args.out_off = dY.data_ptr(), dY.shape[-1], To_full, out_stride, out_off
     args.A, args.a_scale, args.lda, args.Ti, args.To, args.nb = A.data_ptr(), N.ptr(a_scale), A.shape[-1], Ti, To, nb
@@ -318,7 +318,7 @@ def _wgrad(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin
     args.N, args.K = N_, len(offs) * cin
     lib = N.lib()
     ws = torch.empty(int(lib.mtts_conv_wgrad_workspace_size(ctypes.byref(args))), dtype=torch.uint8, device=dY.device)
-    rc = lib.mtts_conv_wgrad_tile(ctypes.byref(args), prec, rows_per_step, target_blocks, dw.data_ptr(), strides[0],
+    rc = lib.mtts_conv_wgrad_tile(ctypes.byref(args), prec, rows_per_step, target_blocks, depth, dw.data_ptr(), strides[0],
                                   strides[1], strides[2], N.ptr(db), 0, ws.data_ptr(), ws.numel(), _stream(dY))
     N.check(rc, "mtts_conv_wgrad")
 

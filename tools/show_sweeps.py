@@ -9,6 +9,6 @@ for s,v in d.items(): print(f"  {s:20s}", "  ".join(f"c{c}:{u:6.1f}" for c,u in 
 d = defaultdict(dict); errs = []
 for l in open("gpurun_out/wgrad_sweep_bf16.log"):
     if not l.startswith("{"): continue
-    r = json.loads(l); d[r["shape"]][(r["kb"], r["target"])] = r["us"]; errs.append(max(r["rel_err"], r["db_err"]))
+    r = json.loads(l); d[r["shape"]][(r["kb"], r["target"], r.get("depth", 1))] = r["us"]; errs.append(max(r["rel_err"], r["db_err"]))
 print("wgrad max err", max(errs))
-for s, v in d.items(): print(f"  {s:20s}", "  ".join(f"{kb}/{t}:{u:6.1f}" for (kb, t), u in v.items()))
+for s, v in d.items(): print(f"  {s:20s}", "  ".join(f"{kb}/{t}/d{dp}:{u:6.1f}" for (kb, t, dp), u in v.items()))

@@ -30,7 +30,7 @@ def t_ev(fn, iters=20):
 
 prec_name = sys.argv[1] if len(sys.argv) > 1 else "bf16"
 prec = O.PREC_BF16 if prec_name == "bf16" else O.PREC_FP32
-scheds = [(32, -1), (32, 256), (32, 512), (32, 1024), (64, 256), (64, 512)] if prec_name == "bf16" else [(32, -1), (32, 256), (32, 512), (32, 1024)]
+scheds = [(32, -1, 1), (32, -1, 2), (64, -1, 1), (64, -1, 2), (32, 512, 2), (64, 512, 2)] if prec_name == "bf16" else [(32, -1, 1), (32, 512, 1)]
 shapes = [("conv3_full_256", 32, 600, 256, 256, 3), ("conv3_half_256", 32, 300, 256, 256, 3),
           ("conv3_full_512", 32, 600, 512, 256, 3), ("lin_full_256_1024", 32, 600, 256, 1024, 1),
           ("lin_full_1024_256", 32, 600, 1024, 256, 1), ("lin_full_256_768", 32, 600, 256, 768, 1),
@@ -45,12 +45,12 @@ for name, B, T, Cin, Cout, k in shapes:
     dw = torch.empty(Cout, Cin, k, device=dev)
     db = torch.empty(Cout, device=dev)
     flops = 2.0 * B * T * Cout * Cin * k
-    for kb, tb in scheds:
+    for kb, tb, dp in scheds:
         run = lambda: O._wgrad(dy, T, 1, 0, x, T, T, B, 1, [j - pad for j in range(k)], Cin, Cout, dw, (Cin * k, k, 1),
-                               prec=prec, db=db, rows_per_step=kb, target_blocks=tb)
+                               prec=prec, db=db, rows_per_step=kb, target_blocks=tb, depth=dp)
         run(); torch.cuda.synchronize()
         err = ((dw - ref).norm() / ref.norm()).item()
         errb = ((db - refb).norm() / refb.norm()).item()
         us = t_ev(run)
-        print(json.dumps({"shape": name, "kb": kb, "target": tb, "us": round(us, 1), "tflops": round(flops / us / 1e6, 1),
+        print(json.dumps({"shape": name, "kb": kb, "target": tb, "depth": dp, "us": round(us, 1), "tflops": round(flops / us / 1e6, 1),
                           "rel_err": float(f"{err:.2e}"), "db_err": float(f"{errb:.2e}")}), flush=True)
