@@ -227,8 +227,9 @@ def main():
         torch.cuda.synchronize()
     gemm_log, OPS.LAUNCH_LOG = OPS.LAUNCH_LOG, None
     model.zero_grad(set_to_none=False)
-    gemm_ms = [a.elapsed_time(b) for a, b, _, _ in gemm_log]
-    gemm_flops = sum(f for _, _, f, _ in gemm_log)
+    gemm_ms = [a.elapsed_time(b) for a, b, _, _, _ in gemm_log]
+    gemm_flops = sum(f for _, _, f, _, _ in gemm_log)
+    gemm_bytes = sum(nb for _, _, _, _, nb in gemm_log)
     gemm_avg_us = sum(gemm_ms) / max(len(gemm_ms), 1) * 1e3
     gemm_tflops = gemm_flops / (sum(gemm_ms) * 1e-3) / 1e12 if gemm_ms else 0.0
 
@@ -237,6 +238,14 @@ def main():
     mas_gbs = 12.0 * cells / (mas_ms * 1e-3) / 1e9
     step_ms = elapsed / args.steps * 1e3
     flops = decoder_train_flops(B, Ty)
+    # roofline.traffic: PMC-measured HBM bytes per conv_gemm launch on THIS workload (tools/pmc_traffic.sh
+    # -> profiles/<round>/conv_gemm_traffic.json); PMC passes serialize kernels, so not collected here
+    traffic, traffic_src = None, None
+    if (B, Tx, Ty, args.precision) == (32, 120, 600, "bf16-mixed"):
+        found = sorted(ROOT.glob("profiles/r*/conv_gemm_traffic.json"))
+        if found:
+            traffic = json.loads(found[-1].read_text())["traffic_bytes_per_launch"]
+            traffic_src = str(found[-1].relative_to(ROOT))
     gemm_peak = FP32_MFMA_TFLOPS if args.precision == "32-true" else BF16_DENSE_TFLOPS
 
     if rank == 0:
@@ -260,9 +269,12 @@ def main():
                        "precision": args.precision, "hip_graph": graph},
             "maximum_path": {"value": round(world * cells / mas_ms / 1e3, 1), "unit": "Mcells/s (whole node)",
                              "ms_per_call": round(mas_ms, 4), "calls": len(mas_events)},
-            "roofline": {"kernel": "conv_gemm_kernel (decoder implicit-GEMM conv/linear, fwd + dgrad)",
+            "roofline": {"kernel": "conv_gemm_kernel (decoder + encoder implicit-GEMM conv/linear, fwd + dgrad)",
                          "bound": "mfma", "achieved": round(gemm_tflops, 1), "peak": gemm_peak, "unit": "TFLOP/s",
-                         "frac": round(gemm_tflops / gemm_peak, 4), "traffic": None,
+                         "frac": round(gemm_tflops / gemm_peak, 4), "traffic": traffic,
+                         "traffic_unit": "HBM bytes per launch (PMC, FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": round(gemm_bytes / max(len(gemm_log), 1)),
                          "launches_per_step": len(gemm_log), "avg_launch_us": round(gemm_avg_us, 2),
                          "algorithmic_flops_per_step": gemm_flops,
                          "note": "achieved = sum(2*M*N*K) / sum(launch durations), HIP events on the launch "

@@ -276,7 +276,9 @@ def packed(spec: PackSpec, prec: int) -> tuple[torch.Tensor, int]:
 
 
 # Per-launch timing for bench.py's roofline leg: when set to a list, every mtts_conv_gemm launch appends
-# (start_event, end_event, algorithmic_flops, precision), events recorded on the launch stream.
+# (start_event, end_event, algorithmic_flops, precision, algorithmic_bytes), events recorded on the
+# launch stream.  Algorithmic bytes: the unique input rows once (nb*Ti*cin*4), the packed weights,
+# the output, and the residual / aux / pre-activation tensors the epilogue touches.
 LAUNCH_LOG: list | None = None
 
 
@@ -304,7 +306,10 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     N.check(N.lib().mtts_conv_gemm_tile(ctypes.byref(args), prec, tile_cfg, _stream(C)), "mtts_conv_gemm")
     if log is not None:
         e1.record(st)
-        log.append((e0, e1, 2.0 * nb * To * N_ * args.K, prec))
+        M_ = nb * To
+        nbytes = nb * Ti * cin * 4 + N_ * Kp * Wp.element_size() + M_ * N_ * 4
+        nbytes += sum(M_ * N_ * 4 for t in (residual, aux, C_pre) if t is not None)
+        log.append((e0, e1, 2.0 * M_ * N_ * args.K, prec, nbytes))
 
 
 def _wgrad(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin, N_, dw, strides, *, prec,
