@@ -44,9 +44,11 @@ extern "C" {
  *                                                               * a_scale[...] * W[n, j*cin + c] )
  * for b < nb, u < To; input rows outside [0, Ti) read as zero.  epi = (+ bias[n]) -> [C_pre <- value]
  * -> act -> (+ residual[row, n]) -> (* c_scale[row]);  row(b,u) = b*To_full + u*out_stride + out_off.
- * act MTTS_ACT_DGELU multiplies by GELU'(aux[row, n]) instead (aux/ldaux: the saved pre-activation).
+ * act MTTS_ACT_DGELU / MTTS_ACT_DRELU multiply by GELU'(aux) / [aux > 0] instead (aux/ldaux: the saved
+ * pre-activation / activation output).
  * W is packed [N][Kp] (bf16 for MTTS_PREC_BF16, fp32 otherwise), K = ntaps*cin, Kp >= K, Kp % 8 == 0.
- * Requirements: cin % 8 == 0, lda % 4 == 0, A and W 16-byte aligned.
+ * Requirements: cin % 8 == 0, lda % 4 == 0, A and W 16-byte aligned, and off[] an arithmetic
+ * progression (off[j] = off[0] + j*(off[1]-off[0]): every conv, dgrad and stride-phase GEMM is one).
  */
 typedef struct mtts_conv_gemm_args {
     const float *A;
@@ -71,8 +73,8 @@ typedef struct mtts_conv_gemm_args {
 } mtts_conv_gemm_args;
 
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
-/* Same, with an explicit schedule: 0..13 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;
- * 8..13 bf16-only: 64-wide K steps, two K steps in flight), MTTS_GEMM_PANEL = the bf16 A-resident panel schedule
+/* Same, with an explicit schedule: 0..17 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;
+ * 8..17 bf16-only: 64-wide K steps, two K steps in flight), MTTS_GEMM_PANEL = the bf16 A-resident panel schedule
  * (csrc/conv_gemm_panel.hip), -1 = heuristic.
  * For tuning and tests; mtts_conv_gemm picks the configuration itself. */
 int mtts_conv_gemm_tile(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg, void *hip_stream);

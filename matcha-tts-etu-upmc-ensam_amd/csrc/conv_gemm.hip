@@ -99,16 +99,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
     const float inv_to = 1.0f / (float)p.To;
 
     Gather ga[CA];
-    // tap offsets in registers (a select over kernel-argument loads would become a dependent load)
-    int offr[MTTS_CONV_MAX_TAPS];
-#pragma unroll
-    for (int i = 0; i < MTTS_CONV_MAX_TAPS; ++i) offr[i] = p.off[i];
-    auto toff_of = [&](int j) {
-        int o = offr[0];
-#pragma unroll
-        for (int i = 1; i < MTTS_CONV_MAX_TAPS; ++i) o = j == i ? offr[i] : o;
-        return o;
-    };
+    // tap offsets form an arithmetic progression (checked at launch): off_j = off_0 + j*step in scalar
+    // registers -- a lookup table (select chain or array) was compiled to a scratch / kernarg load per
+    // tap change inside the K loop
+    const int off0 = p.off[0], offstep = p.ntaps > 1 ? p.off[1] - p.off[0] : 0;
+    auto toff_of = [&](int j) { return off0 + j * offstep; };
     int a_row[CA], a_kc[CA], a_j[CA], a_ch[CA], a_toff[CA];  // (tap, channel, tap offset) at the current step
     bool a_on[CA];                               // this thread stages an A chunk (tiles with BM*4 < NT)
 #pragma unroll
@@ -614,6 +609,13 @@ __global__ void wgrad_reduce_kernel(const float *__restrict__ part, const float 
     }
 }
 
+// The GEMM kernels compute tap offsets as off[0] + j*(off[1]-off[0]).
+bool taps_arithmetic(const int32_t *off, int ntaps) {
+    for (int j = 2; j < ntaps; ++j)
+        if (off[j] - off[j - 1] != off[1] - off[0]) return false;
+    return true;
+}
+
 int check_gather(const void *A, int lda, int cin, int ntaps, int K) {
     if (!A) return mtts::fail(MTTS_ERR_INVALID_ARG, "conv_gemm: A is null");
     if (cin <= 0 || cin % 8 || lda % 4 || (uintptr_t)A % 16)
@@ -644,6 +646,10 @@ constexpr TileCfg kCfgs[] = {
     {1, 4, 1, 1, 32, 2},  // 11: config 7, two K steps in flight (bf16)
     {1, 4, 1, 1, 64, 2},  // 12: config 8, two K steps in flight (bf16)
     {2, 4, 1, 2, 64, 2},  // 13: config 9, two K steps in flight (bf16)
+    {2, 2, 1, 2, 64, 2},  // 14: 64 x 128, K64, two steps in flight (bf16)
+    {1, 4, 1, 2, 64, 2},  // 15: 32 x 256, K64, two steps in flight (bf16)
+    {2, 2, 1, 1, 64, 2},  // 16: 64 x 64, K64, two steps in flight (bf16)
+    {1, 2, 1, 1, 64, 2},  // 17: 32 x 64 (128 threads), K64, two steps in flight (bf16)
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -672,7 +678,11 @@ static void launch_by_id(int id, const mtts_conv_gemm_args &p, int M, hipStream_
         case 10: launch_cfg<BF16, 10>(p, M, st); break;
         case 11: launch_cfg<BF16, 11>(p, M, st); break;
         case 12: launch_cfg<BF16, 12>(p, M, st); break;
-        default: launch_cfg<BF16, 13>(p, M, st); break;
+        case 13: launch_cfg<BF16, 13>(p, M, st); break;
+        case 14: launch_cfg<BF16, 14>(p, M, st); break;
+        case 15: launch_cfg<BF16, 15>(p, M, st); break;
+        case 16: launch_cfg<BF16, 16>(p, M, st); break;
+        default: launch_cfg<BF16, 17>(p, M, st); break;
     }
 }
 
@@ -691,6 +701,8 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     const mtts_conv_gemm_args &p = *args;
     int rc = check_gather(p.A, p.lda, p.cin, p.ntaps, p.K);
     if (rc) return rc;
+    if (!taps_arithmetic(p.off, p.ntaps))
+        return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: tap offsets must be an arithmetic progression");
     MTTS_CHECK_ARG(p.W && p.C && p.N > 0 && p.nb >= 0 && p.To >= 0, "conv_gemm: bad output/weights");
     MTTS_CHECK_ARG(p.Kp >= p.K && p.Kp % 8 == 0, "conv_gemm: Kp must be >= K and a multiple of 8");
     MTTS_CHECK_ARG((uintptr_t)p.W % 16 == 0, "conv_gemm: W must be 16-byte aligned");
