@@ -23,8 +23,12 @@ OBJ = PKG / "build" / "obj"
 LIB = PKG / "lib" / "libmtts_hip.so"
 ARCH = "gfx950"
 
+# -packed-fp32-ops: no v_pk_{add,mul,fma}_f32.  On the MI355X box, packed-fp32 VALU ops in the bf16
+# wgrad staging produced wrong low-half results in lanes 16-31 / 48-63 whenever several workgroups
+# shared a CU (nondeterministic dW/db; bit-exact with one workgroup per CU or with the feature off;
+# tools/wgrad_debug.py, DESIGN.md "Toolchain findings").  The host pass ignores the feature (warning).
 COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
-          "-Wall", "-Wno-unused-function"]
+          "-Wall", "-Wno-unused-function", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 # Per-file extra flags.  The MAS DP must not contract value*mask + best into an FMA (bit parity with
 # the Cython, core.pyx:80 / __init__.py:45).
 EXTRA = {
@@ -53,7 +57,8 @@ def _compile(src: Path, force: bool) -> Path:
     if not force and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _newest_header()):
         return obj
     lang = ["-x", "hip"] if src.suffix == ".hip" else ["-x", "hip"]
-    cmd = [_hipcc(), *COMMON, *EXTRA.get(src.name, []), *lang, "-c", str(src), "-o", str(obj)]
+    cmd = [_hipcc(), *COMMON, *EXTRA.get(src.name, []), *os.environ.get("MTTS_EXTRA_HIPCC_FLAGS", "").split(),
+           *lang, "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -34,6 +34,19 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p names row q / columns 4p..4p+3 of a 4 x 16 block of
+// 16-bit elements and receives column (lane & 15) of the block's 4 rows.  Two reads, rows r..r+3 and
+// r+4..r+7, give a lane the 8 reduction-index elements of a 32x32x16 MFMA operand that is stored
+// row-major along the reduction index.
+__device__ __forceinline__ bf16x8 tr_read8(const uint16_t *p, int row_stride) {
+    using LdsS4 = __attribute__((address_space(3))) s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LdsS4 *)(p));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LdsS4 *)(p + 4 * row_stride));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
 
 __device__ __forceinline__ uint16_t to_bf16(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
@@ -336,17 +349,21 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
 // ------------------------------------------------------------------------------------------------
 // wgrad: partial[s][n][k] = sum over the split's rows of dY[row][n] * A_gathered[row][k]
 // Tile 128 (n) x 128 (k), 4 waves of 64 x 64; the reduction dim (token rows) advances KB rows per
-// step.  Both operands are staged transposed in LDS ([col][row], 16-byte fragment reads along rows),
-// double-buffered with a one-step register prefetch (one barrier per step).  A thread stages row PAIRS
-// x 4 columns so the transposed bf16 writes are packed 32-bit stores.  k-tile-0 blocks also sum dY
-// columns (bias grad) in a fixed order.
+// step, double-buffered with a one-step register prefetch (one barrier per step).  A thread stages
+// row PAIRS x 4 columns.  bf16: both operands are staged row-major ([row][col], one conflict-free
+// ds_write_b64 per row and operand) with 80-dword rows and read with ds_read_b64_tr_b16 (row stride
+// = 16 mod 64 dwords: the 4 rows a 32-lane half reads sit on disjoint banks).  fp32: staged
+// transposed ([col][row], 33-dword rows, conflict-free ds_read_b32 column reads).  k-tile-0 blocks
+// also sum dY columns (bias grad) in a fixed order.
 template <bool BF16, int KB>
 struct WgradGeom {
     static constexpr int T = 128;
-    static constexpr int LDR = KB + Stage<BF16>::PAD;  // row stride of the transposed images
+    static constexpr int LDR = KB + Stage<BF16>::PAD;  // fp32: row stride of the transposed images
+    static constexpr int LDW = T + 32;                  // bf16: row stride of the row-major images
+    static constexpr int kImg = BF16 ? KB * LDW : T * LDR;  // elements per operand image
     static constexpr int CH = KB * 16 / kThreads;       // (2 rows x 4 cols) chunks per thread per operand
     using ST = typename Stage<BF16>::T;
-    static constexpr size_t kBufBytes = (size_t)2 * T * LDR * sizeof(ST);  // Ys + Xs of one stage
+    static constexpr size_t kBufBytes = (size_t)2 * kImg * sizeof(ST);  // Ys + Xs of one stage
     static constexpr size_t kLds = 2 * kBufBytes;
     static_assert((size_t)(KB / 2) * T * sizeof(float) <= kLds, "db scratch fits the operand buffers");
 };
@@ -356,10 +373,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
                                                                float *__restrict__ part, float *__restrict__ part_db) {
     using Gm = WgradGeom<BF16, KB>;
     using ST = typename Gm::ST;
-    constexpr int T = Gm::T, LDR = Gm::LDR, CH = Gm::CH;
+    constexpr int T = Gm::T, LDR = Gm::LDR, LDW = Gm::LDW, IMG = Gm::kImg, CH = Gm::CH;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    ST *Ybuf = reinterpret_cast<ST *>(smem);  // [2][T][LDR] then Xs [2][T][LDR]
-    ST *Xbuf = Ybuf + 2 * T * LDR;
+    ST *Ybuf = reinterpret_cast<ST *>(smem);  // [2][IMG] then Xs [2][IMG]
+    ST *Xbuf = Ybuf + 2 * IMG;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
@@ -424,7 +441,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
             }
     };
     auto store = [&](const Regs &R, int buf) {
-        ST *Ys = Ybuf + buf * T * LDR, *Xs = Xbuf + buf * T * LDR;
+        ST *Ys = Ybuf + buf * IMG, *Xs = Xbuf + buf * IMG;
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
             float yv[2][4], xv[2][4];
@@ -442,15 +459,19 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
                 for (int i = 0; i < 4; ++i) colsum[c][i] += yv[0][i] + yv[1][i];
             }
             const int r2 = 2 * c_rp[c];
+            if constexpr (BF16) {
+                auto pk = [](float a, float b) { return (uint32_t)to_bf16(a) | ((uint32_t)to_bf16(b) << 16); };
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int col = c_cc[c] + i;
-                if constexpr (BF16) {
-                    *reinterpret_cast<uint32_t *>(&Ys[col * LDR + r2]) =
-                        (uint32_t)to_bf16(yv[0][i]) | ((uint32_t)to_bf16(yv[1][i]) << 16);
-                    *reinterpret_cast<uint32_t *>(&Xs[col * LDR + r2]) =
-                        (uint32_t)to_bf16(xv[0][i]) | ((uint32_t)to_bf16(xv[1][i]) << 16);
-                } else {
+                for (int h = 0; h < 2; ++h) {
+                    *reinterpret_cast<uint2 *>(&Ys[(r2 + h) * LDW + c_cc[c]]) =
+                        make_uint2(pk(yv[h][0], yv[h][1]), pk(yv[h][2], yv[h][3]));
+                    *reinterpret_cast<uint2 *>(&Xs[(r2 + h) * LDW + c_cc[c]]) =
+                        make_uint2(pk(xv[h][0], xv[h][1]), pk(xv[h][2], xv[h][3]));
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int col = c_cc[c] + i;
                     Ys[col * LDR + r2] = yv[0][i];
                     Ys[col * LDR + r2 + 1] = yv[1][i];
                     Xs[col * LDR + r2] = xv[0][i];
@@ -469,17 +490,18 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
             for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
     auto compute = [&](int buf) {
-        const ST *Ys = Ybuf + buf * T * LDR, *Xs = Xbuf + buf * T * LDR;
+        const ST *Ys = Ybuf + buf * IMG, *Xs = Xbuf + buf * IMG;
         if constexpr (BF16) {
+            // this lane's tr-read address inside a 16-row x 32-column operand block
+            const int g = lane >> 4;
+            const int tro = (8 * (g >> 1) + ((lane >> 2) & 3)) * LDW + 16 * (g & 1) + 4 * (lane & 3);
 #pragma unroll
             for (int ks = 0; ks < KB / 16; ++ks) {
                 bf16x8 af[2], bfr[2];
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
-                    af[i] = *reinterpret_cast<const bf16x8 *>(&Ys[(wr * 64 + i * 32 + lr) * LDR + ks * 16 + 8 * lh]);
+                for (int i = 0; i < 2; ++i) af[i] = tr_read8(&Ys[ks * 16 * LDW + wr * 64 + i * 32 + tro], LDW);
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    bfr[j] = *reinterpret_cast<const bf16x8 *>(&Xs[(wc * 64 + j * 32 + lr) * LDR + ks * 16 + 8 * lh]);
+                for (int j = 0; j < 2; ++j) bfr[j] = tr_read8(&Xs[ks * 16 * LDW + wc * 64 + j * 32 + tro], LDW);
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll

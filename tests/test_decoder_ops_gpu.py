@@ -194,3 +194,61 @@ def test_ops_refuse_cpu_and_never_fall_back():
 
     with pytest.raises(N.NativeError):
         conv_tm(torch.randn(1, 4, 8), torch.randn(8, 8, 3), None)
+
+
+# Strict bf16 checks at the train step's full size (many workgroups per CU).  Operands are rounded to
+# bf16 up front, so the bf16 MFMA products are exact and only fp32 accumulation order separates the
+# kernels from a float64 reference: every entry must agree to 1e-5 of the output's scale, and repeated
+# calls must be bitwise identical.  The loose 1.5e-2 relative tolerance above let through a
+# packed-fp32 miscompute in the wgrad staging (wrong low halves in lanes 16-31/48-63 under CU
+# co-residency, relative error 3e-3..1e-2); these catch that class of error.
+BIG = [(32, 600, 256, 768, 1), (32, 600, 512, 256, 3), (32, 120, 192, 768, 3)]
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout,k", BIG)
+@pytest.mark.parametrize("rows_per_step,target_blocks,depth", [(32, -1, 1), (32, 1024, 1), (64, 1024, 1), (32, 512, 2)])
+def test_wgrad_bf16_exact_and_deterministic(B, T, Cin, Cout, k, rows_per_step, target_blocks, depth):
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator(device="cpu").manual_seed(B * T + Cin + Cout + k)
+    x = torch.randn(B, T, Cin, generator=g).bfloat16().float().to(DEV)
+    dy = torch.randn(B, T, Cout, generator=g).bfloat16().float().to(DEV)
+    pad = k // 2
+    ref = torch.nn.grad.conv1d_weight(x.double().transpose(1, 2), (Cout, Cin, k), dy.double().transpose(1, 2),
+                                      padding=pad)
+    refb = dy.double().sum((0, 1))
+    outs = []
+    for _ in range(3):
+        dw = torch.full((Cout, Cin, k), float("nan"), device=DEV)
+        db = torch.full((Cout,), float("nan"), device=DEV)
+        O._wgrad(dy, T, 1, 0, x, T, T, B, 1, [j - pad for j in range(k)], Cin, Cout, dw, (Cin * k, k, 1),
+                 prec=O.PREC_BF16, db=db, rows_per_step=rows_per_step, target_blocks=target_blocks, depth=depth)
+        outs.append((dw, db))
+    torch.cuda.synchronize()
+    dw, db = outs[0]
+    assert (dw.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+    assert (db.double() - refb).abs().max().item() <= 1e-5 * refb.abs().max().item()
+    for dw2, db2 in outs[1:]:
+        assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout,k", BIG)
+@pytest.mark.parametrize("cfg", [-1, 7, 12])
+def test_gemm_bf16_exact_and_deterministic(B, T, Cin, Cout, k, cfg):
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator(device="cpu").manual_seed(B * T + Cin + Cout + k + 1)
+    x = torch.randn(B, T, Cin, generator=g).bfloat16().float().to(DEV)
+    w = (torch.randn(Cout, Cin, k, generator=g) / math.sqrt(Cin * k)).bfloat16().float().to(DEV)
+    pad = k // 2
+    ref = F.conv1d(x.double().transpose(1, 2), w.double(), padding=pad).transpose(1, 2)
+    Wp, Kp = O.pack_weight(w.permute(0, 2, 1).reshape(Cout, k * Cin), O.PREC_BF16)
+    outs = []
+    for _ in range(3):
+        y = torch.full((B, T, Cout), float("nan"), device=DEV)
+        O._gemm(x, T, T, B, 1, [j - pad for j in range(k)], Cin, Wp, Kp, Cout, y, T, prec=O.PREC_BF16, tile_cfg=cfg)
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert (outs[0].double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+    for y2 in outs[1:]:
+        assert torch.equal(outs[0], y2)
