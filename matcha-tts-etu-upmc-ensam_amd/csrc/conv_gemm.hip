@@ -49,6 +49,12 @@ __device__ __forceinline__ bf16x8 tr_read8(const uint16_t *p, int row_stride) {
 }
 
 __device__ __forceinline__ uint16_t to_bf16(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// (a, b) -> one v_cvt_pk_bf16_f32 (two scalar to_bf16 + shift/or were compiled to SDWA repacks)
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
 
 
 
@@ -106,8 +112,20 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
     const int wave = tid >> 6;
     const int wr = wave / WN, wc = wave % WN;
     const int M = p.nb * p.To;
-    const int m0 = blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
+    // 1-D grid, XCD-contiguous: the dispatcher deals consecutive block ids round-robin over the 8 XCDs,
+    // so block id b is relabelled to the (b % 8)-th contiguous run of tiles (bijective for any grid
+    // size), and tiles are numbered N-fastest -- every column block of an A row panel runs on the same
+    // XCD at about the same time and reads the panel from that XCD's L2
+    int m0, n0;
+    {
+        const int nt = (p.N + BN - 1) / BN;
+        const int nwg = gridDim.x, orig = blockIdx.x;
+        const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+        const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+        const int mt = wgid / nt;
+        m0 = mt * BM;
+        n0 = (wgid - mt * nt) * BN;
+    }
     const int nk = (p.K + KB - 1) / KB;
     const float inv_to = 1.0f / (float)p.To;
 
@@ -368,7 +386,11 @@ struct WgradGeom {
     static_assert((size_t)(KB / 2) * T * sizeof(float) <= kLds, "db scratch fits the operand buffers");
 };
 
-template <bool BF16, int KB, int DEPTH>
+// INC: rows advance by exactly KB per load call, so each staged row's (u, dY offset, A row) is
+// updated incrementally -- an add and one wrap select instead of a division and 64-bit address math
+// per row and step (the loop was VALU-bound: ~365 VALU vs 8 MFMA per step).  Requires To >= KB (one
+// wrap per step) and 32-bit element offsets; the launcher picks the generic path otherwise.
+template <bool BF16, int KB, int DEPTH, bool INC>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_args p, int rows_per_split,
                                                                float *__restrict__ part, float *__restrict__ part_db) {
     using Gm = WgradGeom<BF16, KB>;
@@ -381,11 +403,24 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
     const int lr = lane & 31, lh = lane >> 5;
-    const int n0 = blockIdx.x * T, k0 = blockIdx.y * T, split = blockIdx.z;
+    // 1-D grid relabelled XCD-contiguous (as conv_gemm_kernel), tiles numbered n-fastest, then k, then
+    // split: the tiles of one split read the same token rows and now share one XCD's L2
+    int n0, k0, split, ktile;
+    {
+        const int ntn = (p.N + T - 1) / T, ntk = (p.K + T - 1) / T;
+        const int nwg = gridDim.x, orig = blockIdx.x;
+        const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+        const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+        split = wgid / (ntn * ntk);
+        const int t = wgid - split * ntn * ntk;
+        ktile = t / ntn;
+        n0 = (t - ktile * ntn) * T;
+        k0 = ktile * T;
+    }
     const int M = p.nb * p.To;
     const int r_begin = split * rows_per_split;
     const int r_end = min(M, r_begin + rows_per_split);
-    const bool do_db = (blockIdx.y == 0) && part_db != nullptr;
+    const bool do_db = (ktile == 0) && part_db != nullptr;
     const float inv_to = 1.0f / (float)p.To;
 
     // per-chunk constants: row pair, column group, and the A gather's (tap offset, channel) -- k is
@@ -400,10 +435,28 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
         const int k = k0 + c_cc[c], n = n0 + c_cc[c];
         c_kok[c] = k < p.K;
         const int j = c_kok[c] ? k / p.cin : 0;
-        c_ch[c] = k - j * p.cin;
+        c_ch[c] = c_kok[c] ? k - j * p.cin : 0;  // columns past K / N are never stored: any valid address
         c_toff[c] = mtts::tap_off(p, j);
         c_nok[c] = n < p.N;  // N % 4 == 0: a 4-column group is all in or all out
     }
+    // INC state of each staged row (chunk c, row h of the pair) for the NEXT load call
+    int s_u[CH][2], s_y[CH][2], s_x[CH][2], s_i[CH][2];
+    const int y_step = KB * p.out_stride * p.ldy, y_wrap = (p.To_full - p.To * p.out_stride) * p.ldy;
+    const int x_step = KB * p.in_stride, x_wrap = p.Ti - p.To * p.in_stride, i_wrap = -p.To * p.in_stride;
+    if constexpr (INC) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                int b = 0, u = 0;
+                divmod_fast(min(r_begin + 2 * c_rp[c] + h, M - 1), p.To, inv_to, b, u);
+                s_u[c][h] = u;
+                s_y[c][h] = (b * p.To_full + u * p.out_stride + p.out_off) * p.ldy;
+                s_i[c][h] = u * p.in_stride + c_toff[c];
+                s_x[c][h] = b * p.Ti + s_i[c][h];
+            }
+    }
+    const int y_col = min(n0 + c_cc[0], p.N - 4);  // per-chunk y column (chunks differ only in row pair)
 
     // One staged step, loaded unconditionally from clamped addresses; validity, the row mask and the
     // bias column sums are applied at store time so the loads stay in flight through the compute.
@@ -420,6 +473,29 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
         for (int i = 0; i < 4; ++i) colsum[c][i] = 0.f;
 
     auto load = [&](Regs &R, int rb) {
+        if constexpr (INC) {
+            const int rows_left = r_end - rb;
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const bool mv = 2 * c_rp[c] + h < rows_left;
+                    R.y[c][h] = *reinterpret_cast<const float4 *>(p.dY + (uint32_t)((mv ? s_y[c][h] : 0) + y_col));
+                    R.yok[c][h] = mv;
+                    const bool xok = mv && (unsigned)s_i[c][h] < (unsigned)p.Ti;
+                    const int xr = xok ? s_x[c][h] : 0;
+                    R.x[c][h] = *reinterpret_cast<const float4 *>(p.A + (uint32_t)(xr * p.lda + c_ch[c]));
+                    R.xs[c][h] = *(p.a_scale ? p.a_scale + (uint32_t)xr : p.A);
+                    R.xok[c][h] = xok;
+                    int u = s_u[c][h] + KB;
+                    const bool wrap = u >= p.To;
+                    s_u[c][h] = wrap ? u - p.To : u;
+                    s_y[c][h] += y_step + (wrap ? y_wrap : 0);
+                    s_x[c][h] += x_step + (wrap ? x_wrap : 0);
+                    s_i[c][h] += x_step + (wrap ? i_wrap : 0);
+                }
+            return;
+        }
 #pragma unroll
         for (int c = 0; c < CH; ++c)
 #pragma unroll
@@ -454,13 +530,12 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
                 xv[h][0] = R.x[c][h].x * xm; xv[h][1] = R.x[c][h].y * xm;
                 xv[h][2] = R.x[c][h].z * xm; xv[h][3] = R.x[c][h].w * xm;
             }
-            if (do_db) {
+            // unconditional (only k-tile-0 blocks store it): a select per element costs more than the add
 #pragma unroll
-                for (int i = 0; i < 4; ++i) colsum[c][i] += yv[0][i] + yv[1][i];
-            }
+            for (int i = 0; i < 4; ++i) colsum[c][i] += yv[0][i] + yv[1][i];
             const int r2 = 2 * c_rp[c];
             if constexpr (BF16) {
-                auto pk = [](float a, float b) { return (uint32_t)to_bf16(a) | ((uint32_t)to_bf16(b) << 16); };
+                auto pk = [](float a, float b) { return pack_bf16x2(a, b); };
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     *reinterpret_cast<uint2 *>(&Ys[(r2 + h) * LDW + c_cc[c]]) =
@@ -588,33 +663,48 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
 }
 
 // dW (and db) = sum over splits, written in the caller's layout: w_out[n*sn + c*sc + j*sj]
-// for k = j*cin + c.  Each thread owns 4 consecutive (n, k) (float4 slab reads, NK % 4 == 0); the
-// splits are summed in 4 interleaved chains combined in a fixed order (deterministic).
-__global__ void wgrad_reduce_kernel(const float *__restrict__ part, const float *__restrict__ part_db, int splits,
-                                    int N, int K, int cin, int64_t sn, int64_t sc, int64_t sj,
-                                    float *__restrict__ w_out, float *__restrict__ db_out, int accumulate) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t NK = (int64_t)N * K;
-    if (q * 4 < NK) {
-        float4 a[4];
+// for k = j*cin + c.  A block owns 64 float4 groups of the (n, k) slab (NK % 4 == 0); its 4 waves take
+// interleaved quarters of the splits (wave g: splits g, g+4, ...; four float4 loads in flight per
+// lane), and the quarters are combined through LDS in a fixed order -- deterministic, and 4x the
+// waves of one-thread-per-group so enough slab reads are in flight to stream at HBM rate.
+constexpr int kRedGroups = 64;
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restrict__ part,
+                                                           const float *__restrict__ part_db, int splits, int N,
+                                                           int K, int cin, int64_t sn, int64_t sc, int64_t sj,
+                                                           float *__restrict__ w_out, float *__restrict__ db_out,
+                                                           int accumulate) {
+    __shared__ float4 red[4][kRedGroups];
+    const int t = threadIdx.x & (kRedGroups - 1), g = threadIdx.x >> 6;
+    const int64_t q = (int64_t)blockIdx.x * kRedGroups + t;
+    const int64_t NK = (int64_t)N * K, step = NK / 4;
+    const bool on = q < step;
+    const float4 *src = reinterpret_cast<const float4 *>(part) + (on ? q : 0);
+    float4 a[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) a[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 *src = reinterpret_cast<const float4 *>(part) + q;
-        const int64_t step = NK / 4;
-        int i = 0;
-        for (; i + 3 < splits; i += 4) {
+    for (int c = 0; c < 4; ++c) a[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int i = g;
+    for (; i + 12 < splits; i += 16) {
+        float4 v[4];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float4 v = src[(int64_t)(i + c) * step];
-                a[c].x += v.x; a[c].y += v.y; a[c].z += v.z; a[c].w += v.w;
-            }
+        for (int c = 0; c < 4; ++c) v[c] = src[(int64_t)(i + 4 * c) * step];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            a[c].x += v[c].x; a[c].y += v[c].y; a[c].z += v[c].z; a[c].w += v[c].w;
         }
-        for (; i < splits; ++i) {
-            const float4 v = src[(int64_t)i * step];
-            a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c)  // i + 12 >= splits: at most 3 left
+        if (i + 4 * c < splits) {
+            const float4 v = src[(int64_t)(i + 4 * c) * step];
+            a[c].x += v.x; a[c].y += v.y; a[c].z += v.z; a[c].w += v.w;
         }
-        const float r[4] = {(a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y),
-                            (a[0].z + a[1].z) + (a[2].z + a[3].z), (a[0].w + a[1].w) + (a[2].w + a[3].w)};
+    red[g][t] = make_float4((a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y),
+                            (a[0].z + a[1].z) + (a[2].z + a[3].z), (a[0].w + a[1].w) + (a[2].w + a[3].w));
+    __syncthreads();
+    if (g == 0 && on) {
+        const float4 r0 = red[0][t], r1 = red[1][t], r2 = red[2][t], r3 = red[3][t];
+        const float r[4] = {(r0.x + r1.x) + (r2.x + r3.x), (r0.y + r1.y) + (r2.y + r3.y),
+                            (r0.z + r1.z) + (r2.z + r3.z), (r0.w + r1.w) + (r2.w + r3.w)};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int64_t idx = q * 4 + e;
@@ -624,9 +714,9 @@ __global__ void wgrad_reduce_kernel(const float *__restrict__ part, const float 
             *dst = accumulate ? *dst + r[e] : r[e];
         }
     }
-    if (db_out && q < N) {
+    if (db_out && g == 1 && q < N) {
         float s = 0.f;
-        for (int i = 0; i < splits; ++i) s += part_db[(size_t)i * N + q];
+        for (int z = 0; z < splits; ++z) s += part_db[(size_t)z * N + q];
         db_out[q] = accumulate ? db_out[q] + s : s;
     }
 }
@@ -679,7 +769,7 @@ template <bool BF16, int C>
 static void launch_cfg(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
     constexpr TileCfg c = kCfgs[C];
     constexpr int BM = 32 * c.wm * c.tm, BN = 32 * c.wn * c.tn;
-    dim3 grid((M + BM - 1) / BM, (p.N + BN - 1) / BN);
+    dim3 grid((unsigned)(((M + BM - 1) / BM) * ((p.N + BN - 1) / BN)));
     hipLaunchKernelGGL((conv_gemm_kernel<BF16, c.wm, c.wn, c.tm, c.tn, (BF16 ? c.kb : kBK), (BF16 ? c.depth : 1)>), grid,
                        dim3(64 * c.wm * c.wn), 0, st, p);
 }
@@ -832,20 +922,37 @@ extern "C" size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *arg
     return mtts::align_up((size_t)splits * args->N * args->K * 4, 256) + (size_t)splits * args->N * 4 + 256;
 }
 
-template <bool BF16, int KB, int DEPTH>
-static int wgrad_launch(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
-                        hipStream_t st) {
+template <bool BF16, int KB, int DEPTH, bool INC>
+static int wgrad_launch_k(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
+                          hipStream_t st) {
     using Gm = WgradGeom<BF16, KB>;
     static bool attr_set = false;
     if (Gm::kLds > 64 * 1024 && !attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(conv_wgrad_kernel<BF16, KB, DEPTH>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(conv_wgrad_kernel<BF16, KB, DEPTH, INC>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)Gm::kLds) != hipSuccess)
             return mtts::fail(MTTS_ERR_HIP, "conv_wgrad: LDS attribute");
         attr_set = true;
     }
-    dim3 grid((p.N + 127) / 128, (p.K + 127) / 128, splits);
-    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH>), grid, dim3(kThreads), Gm::kLds, st, p, rps, part, part_db);
+    dim3 grid((unsigned)(((p.N + 127) / 128) * ((p.K + 127) / 128) * splits));
+    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH, INC>), grid, dim3(kThreads), Gm::kLds, st, p, rps, part,
+                       part_db);
     return mtts::check_launch("conv_wgrad_kernel");
+}
+
+// The incremental row walk needs one wrap per step (To >= KB) and element offsets that stay inside
+// int32 even for the masked rows a split walks past its end (two extra sequences of margin).
+static bool wgrad_inc_ok(const mtts_conv_wgrad_args &p, int kb) {
+    const int64_t ymax = ((int64_t)p.nb + 2) * p.To_full * p.ldy;
+    const int64_t xmax = ((int64_t)p.nb + 2) * p.Ti * p.lda + (int64_t)(p.To + kb) * p.in_stride * p.lda;
+    return p.To >= kb && ymax < (int64_t(1) << 31) && xmax < (int64_t(1) << 31) && p.out_stride >= 1 &&
+           p.in_stride >= 1;
+}
+
+template <bool BF16, int KB, int DEPTH>
+static int wgrad_launch(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
+                        hipStream_t st) {
+    return wgrad_inc_ok(p, KB) ? wgrad_launch_k<BF16, KB, DEPTH, true>(p, splits, rps, part, part_db, st)
+                               : wgrad_launch_k<BF16, KB, DEPTH, false>(p, splits, rps, part, part_db, st);
 }
 
 // rows_per_step: 32 or 64 (bf16 only), -1 = default; target_blocks: 64..1024, -1 = default;
@@ -892,9 +999,9 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
         if (rc) return rc;
     }
     const int64_t NK = (int64_t)p.N * p.K;  // K % 8 == 0 (cin % 8): float4 groups never straddle rows
-    const int64_t nthr = std::max<int64_t>(NK / 4, p.N);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, st, part, part_db,
-                       splits, p.N, p.K, p.cin, sn, sc, sj, dw, db, accumulate);
+    const int64_t groups = std::max<int64_t>(NK / 4, p.N);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((groups + kRedGroups - 1) / kRedGroups)), dim3(256), 0, st,
+                       part, part_db, splits, p.N, p.K, p.cin, sn, sc, sj, dw, db, accumulate);
     return mtts::check_launch("wgrad_reduce_kernel");
 }
 
