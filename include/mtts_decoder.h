@@ -38,6 +38,7 @@ extern "C" {
 
 #define MTTS_CONV_MAX_TAPS 8
 #define MTTS_GEMM_PANEL 64 /* mtts_conv_gemm_tile schedule id of the panel kernel */
+#define MTTS_GEMM_GLDS 32  /* schedule ids 32.. : bf16 LDS-DMA kernels (csrc/conv_gemm_glds.hip)   */
 
 /*
  * Implicit GEMM  C[row(b,u), n] = epi( sum_{j<ntaps} sum_{c<cin} A[b*Ti + u*in_stride + off[j], c]
@@ -70,7 +71,12 @@ typedef struct mtts_conv_gemm_args {
     int32_t ldaux;
     float dropout_p;       /* > 0: inverted dropout after act (before residual)                  */
     const uint32_t *seed;  /* device pointer to 2 words: the dropout stream (graph-replay safe)   */
+    int32_t flags;         /* MTTS_GEMM_F_* */
 } mtts_conv_gemm_args;
+
+/* mtts_conv_gemm_args.flags */
+#define MTTS_GEMM_F_BINARY_SCALE 0x1 /* a_scale holds only 0 / 1 (a sequence mask): lets the bf16 path
+                                        stage A rows by LDS-DMA, reading zeros for masked rows */
 
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
 /* Same, with an explicit schedule: 0..17 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;

@@ -27,6 +27,7 @@
 
 #include <cstdint>
 
+#include "gemm_epilogue.h"
 #include "mtts_common.h"
 #include "mtts_decoder.h"
 
@@ -59,12 +60,7 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
 
 
 
-// b = m / d, u = m % d for 0 <= m < 2^24 with a precomputed 1/d (float estimate + one correction)
-__device__ __forceinline__ void divmod_fast(int m, int d, float inv_d, int &q, int &r) {
-    q = (int)((float)m * inv_d);
-    r = m - q * d;
-    if (r < 0) { --q; r += d; } else if (r >= d) { ++q; r -= d; }
-}
+using mtts::divmod_fast;
 
 constexpr int kBN = 128;
 constexpr int kBK = 32;
@@ -324,44 +320,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
         }
     }
 
-    // ---- epilogue ----
-    uint32_t s0 = 0, s1 = 0;
-    if (p.dropout_p > 0.f) {
-        s0 = p.seed[0];
-        s1 = p.seed[1];
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-        int crows[16];  // output row of each accumulator register (-1: past M)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-            const int m = m0 + wr * 32 * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * lh;
-            int b, u;
-            divmod_fast(m, p.To, inv_to, b, u);
-            crows[v] = m < M ? b * p.To_full + u * p.out_stride + p.out_off : -1;
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int n = n0 + wc * 32 * TN + j * 32 + lr;
-            if (n >= p.N) continue;
-            const float bn = p.bias ? p.bias[n] : 0.f;
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                if (crows[v] < 0) continue;
-                const size_t crow = (size_t)crows[v];
-                float val = acc[i][j][v] + bn;
-                if (p.C_pre) p.C_pre[crow * p.ldc + n] = val;
-                if (p.act) val = mtts::epi_act(p.act, val, p.aux + crow * p.ldaux + n);
-                if (p.dropout_p > 0.f)
-                    val = mtts::dropout_keep(s0, s1, (uint32_t)crow, (uint32_t)n, p.dropout_p)
-                              ? val * (1.0f / (1.0f - p.dropout_p))
-                              : 0.f;
-                if (p.residual) val += p.residual[crow * p.ldr + n];
-                if (p.c_scale) val *= p.c_scale[crow];
-                p.C[crow * p.ldc + n] = val;
-            }
+    // ---- epilogue ---- (the K loop ended with a barrier after every wave's last LDS access: Bs is free
+    // for the 16-byte-row epilogue's per-wave 4 KiB staging images when it is large enough)
+    if constexpr (sizeof(Bs) >= (size_t)WM * WN * 4096) {
+        if (mtts::gemm_epilogue_vec_ok(p)) {
+            mtts::gemm_epilogue_vec<TM, TN>(p, acc, reinterpret_cast<float *>(reinterpret_cast<unsigned char *>(&Bs[0][0]) + wave * 4096),
+                                            m0 + wr * 32 * TM, n0 + wc * 32 * TN, lane);
+            return;
         }
     }
+    mtts::gemm_epilogue<TM, TN>(p, acc, m0 + wr * 32 * TM, n0 + wc * 32 * TN, lr, lh);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -798,13 +766,16 @@ static void launch_by_id(int id, const mtts_conv_gemm_args &p, int M, hipStream_
     }
 }
 
-// From the tile sweep on the train step's shapes (tools/gemm_sweep.py, profiles/r01/gemm_sweep_bf16.log;
-// graph-timed): with branch-free staging, 32 x 128 tiles with 64-wide K steps and two K steps in
-// flight (config 12) are best or within ~5% wherever K >= 384; short reductions (K <= 256: at most
-// four 64-wide steps) keep 32-wide steps (config 7).  fp32 (parity mode) uses config 7.
+// From the tile sweeps on the train step's shapes (tools/gemm_sweep.py, graph-timed;
+// profiles/r01/gemm_sweep_glds.log): the LDS-DMA kernels (64 x 256 tiles, 512 threads) win by 5-20 %
+// wherever the reduction is long (K >= 512) or the output wide (N >= 768) -- three stages in flight
+// from K >= 768, two below; shorter / narrower GEMMs keep the register-staged 32 x 128 tiles: 64-wide
+// K steps with two in flight (config 12) for K >= 384, 32-wide (config 7) below.  fp32 (parity
+// mode) uses config 7.
 static int pick_cfg(const mtts_conv_gemm_args &p, int M, bool bf16) {
     (void)M;
     if (!bf16) return 7;
+    if ((p.K >= 512 || p.N >= 768) && mtts::conv_gemm_glds_applies(p)) return MTTS_GEMM_GLDS + (p.K >= 768 ? 10 : 9);
     return p.K >= 384 ? 12 : 7;
 }
 
@@ -823,7 +794,8 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     MTTS_CHECK_ARG((p.act != MTTS_ACT_DGELU && p.act != MTTS_ACT_DRELU) || p.aux,
                    "conv_gemm: MTTS_ACT_DGELU / MTTS_ACT_DRELU need aux");
     MTTS_CHECK_ARG(p.dropout_p <= 0.f || (p.seed && p.dropout_p < 1.f), "conv_gemm: dropout needs a seed pointer");
-    MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || cfg == MTTS_GEMM_PANEL, "conv_gemm: bad tile config");
+    const bool glds_id = cfg >= MTTS_GEMM_GLDS && cfg < MTTS_GEMM_GLDS + mtts::conv_gemm_glds_num_cfgs();
+    MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || cfg == MTTS_GEMM_PANEL || glds_id, "conv_gemm: bad tile config");
     const int M = p.nb * p.To;
     if (M == 0) return MTTS_OK;
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
@@ -834,7 +806,15 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
         if (mtts::conv_gemm_panel_launch(p, st) == 0) return mtts::check_launch("conv_gemm_panel_kernel");
         return mtts::fail(MTTS_ERR_SHAPE, "conv_gemm: panel schedule does not fit");
     }
-    if (cfg < 0) cfg = pick_cfg(p, M, bf16);
+    if (glds_id) {
+        if (!bf16 || !mtts::conv_gemm_glds_applies(p))
+            return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: LDS-DMA schedule needs bf16, cin >= 64 and a 0/1 a_scale");
+        return mtts::conv_gemm_glds_launch(cfg - MTTS_GEMM_GLDS, p, M, st);
+    }
+    if (cfg < 0) {
+        cfg = pick_cfg(p, M, bf16);
+        if (cfg >= MTTS_GEMM_GLDS) return mtts::conv_gemm_glds_launch(cfg - MTTS_GEMM_GLDS, p, M, st);
+    }
     if (bf16) launch_by_id<true>(cfg, p, M, st);
     else launch_by_id<false>(cfg, p, M, st);
     return mtts::check_launch("conv_gemm_kernel");

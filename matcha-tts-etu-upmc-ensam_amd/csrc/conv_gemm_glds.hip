@@ -1,0 +1,319 @@
+// bf16 implicit GEMM with LDS-DMA staging (global_load_lds_dwordx4) of both operands -- the default
+// bf16 schedule of mtts_conv_gemm for the decoder / encoder convs and linears.
+//
+// Same contract as conv_gemm_kernel (include/mtts_decoder.h), for precision MTTS_PREC_BF16 with
+// a_scale either NULL or a 0/1 row mask (MTTS_GEMM_F_BINARY_SCALE).  Why a second kernel: the
+// register-staged kernel spends ~45 VALU instructions per MFMA on staging (fp32 loads, row-mask
+// multiply, bf16 conversion, validity selects, LDS stores; SQ_INSTS_VALU / SQ_INSTS_MFMA on the step's
+// 19200 x 256 x 768 conv) and is issue-bound at ~9 % of MFMA peak.  Here the operands go
+// HBM/L2 -> LDS with no VGPR round trip:
+//   A (fp32 activations): each lane DMAs one 16-byte chunk (4 channels) of one tap row; a row that
+//     lies outside [0, Ti) or whose mask is 0 is read from a 16-byte zero constant instead, so the
+//     masked / zero-padded operand is formed by address selection alone.  The fp32 -> bf16 conversion
+//     moves to the fragment read (4 v_cvt_pk_bf16_f32 per 8 elements).
+//   W (packed bf16 [N][Kp]): DMA'd as is.
+// LDS images are XOR-swizzled through the per-lane SOURCE address (an LDS-DMA wave instruction fills
+// 1 KiB lane-linearly): A rows are 256 B (64 fp32 of one K step), 16-byte chunk c of row r sits at
+// c ^ (r & 15); W rows are 128 B, chunk c of row n at c ^ ((n >> 1) & 7).  Both make the MFMA
+// fragment reads (ds_read_b128, 16-lane groups) bank-conflict free.
+// Pipeline: STAGES LDS buffers, K step 64, loads for step kt + STAGES - 1 issued right after the
+// barrier that retires step kt - 1's reads; a counted s_waitcnt vmcnt (never 0 inside the loop) and a
+// raw s_barrier (no fence: __syncthreads() would drain the in-flight DMAs) order each buffer.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <type_traits>
+
+#include "gemm_epilogue.h"
+#include "mtts_common.h"
+#include "mtts_decoder.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+using mtts::f32x16;
+
+__device__ uint4 g_zero16 = {0u, 0u, 0u, 0u};  // never written: source of every masked / out-of-range chunk
+
+constexpr int kBK = 64;
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
+
+// One global_load_lds_dwordx4: 16 bytes per lane from `src` into LDS at lds_base + 16*lane.  Issued as
+// inline asm so hipcc's waitcnt pass does not see an LDS write it cannot disambiguate from the
+// fragment reads of the other stages (it inserted vmcnt(0) before them, draining every prefetch);
+// the kernel orders each buffer itself with counted vmcnt waits and barriers.  M0 holds the LDS base.
+__device__ __forceinline__ void glds16(const void *src, void *lds_base) {
+    const uint32_t lds = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)lds_base);
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(lds)
+        : "memory");
+}
+
+// s_waitcnt vmcnt(N) (expcnt / lgkmcnt left at their maxima; gfx9 encoding: vmcnt[3:0] | [15:14])
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+template <int WM, int WN, int TM, int TN, int STAGES>
+struct GldsGeom {
+    static constexpr int NT = 64 * WM * WN;
+    static constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN;
+    static constexpr int A_BYTES = BM * kBK * 4;  // fp32 rows of 256 B
+    static constexpr int W_BYTES = BN * kBK * 2;  // bf16 rows of 128 B
+    static constexpr int GA = A_BYTES / (NT * 16);  // DMA instructions per thread per K step
+    static constexpr int GW = W_BYTES / (NT * 16);
+    static_assert(A_BYTES % (NT * 16) == 0 && W_BYTES % (NT * 16) == 0, "tile / threads mismatch");
+};
+
+template <int WM, int WN, int TM, int TN, int STAGES>
+__global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_gemm_args p) {
+    using G = GldsGeom<WM, WN, TM, TN, STAGES>;
+    constexpr int NT = G::NT, BM = G::BM, BN = G::BN, GA = G::GA, GW = G::GW, NW = NT / 64;
+    // one __shared__ object per stage and operand, and a K loop unrolled by STAGES so every access
+    // names its buffer statically: hipcc then sees that a DMA into one buffer cannot alias the
+    // ds_reads of another and does not insert vmcnt(0) before them (one shared array with a runtime
+    // stage offset gets a full drain of the in-flight DMAs before every fragment read)
+    __shared__ __attribute__((aligned(1024))) unsigned char sA0[G::A_BYTES], sW0[G::W_BYTES];
+    __shared__ __attribute__((aligned(1024))) unsigned char sA1[G::A_BYTES], sW1[G::W_BYTES];
+    __shared__ __attribute__((aligned(1024))) unsigned char sA2[STAGES > 2 ? G::A_BYTES : 16],
+        sW2[STAGES > 2 ? G::W_BYTES : 16];
+    auto abuf = [&](auto S) -> unsigned char * {
+        if constexpr (decltype(S)::value == 0) return sA0;
+        else if constexpr (decltype(S)::value == 1) return sA1;
+        else return sA2;
+    };
+    auto wbuf = [&](auto S) -> unsigned char * {
+        if constexpr (decltype(S)::value == 0) return sW0;
+        else if constexpr (decltype(S)::value == 1) return sW1;
+        else return sW2;
+    };
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave / WN, wc = wave % WN;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int M = p.nb * p.To;
+    int m0, n0;
+    {
+        const int nt = (p.N + BN - 1) / BN;
+        const int t = mtts::xcd_relabel(blockIdx.x, gridDim.x);
+        const int mt = t / nt;
+        m0 = mt * BM;
+        n0 = (t - mt * nt) * BN;
+    }
+    const int nk = (p.K + kBK - 1) / kBK;
+    const float inv_to = 1.0f / (float)p.To;
+    const int off0 = p.off[0], offstep = p.ntaps > 1 ? p.off[1] - p.off[0] : 0;
+
+    // ---- A chunk state: DMA instruction i of this wave covers tile rows 4q..4q+3 (q = i*NW + wave);
+    // lane -> row 4q + lane/16, LDS slot lane%16 <- logical chunk (lane%16) ^ (row & 15)
+    const float *zero = reinterpret_cast<const float *>(&g_zero16);
+    const long long tap_delta = (long long)offstep * p.lda - p.cin;  // source step when a chunk changes tap
+    const float *a_src[GA];  // the lane's chunk in the current step (valid when its tap's bit is set)
+    int a_ch[GA], a_j[GA];   // channel of the lane's chunk within its tap, and the tap
+    uint32_t a_ok[GA];       // bit j: tap j's source row exists and is unmasked
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+        const int r = 4 * (i * NW + wave) + (lane >> 4);
+        const int lc = (lane & 15) ^ (r & 15);
+        const int m = m0 + r;
+        int b = 0, u = 0;
+        const bool mv = m < M;
+        mtts::divmod_fast(mv ? m : 0, p.To, inv_to, b, u);
+        uint32_t ok = 0;
+        for (int j = 0; j < p.ntaps; ++j) {
+            const int irow = u * p.in_stride + off0 + j * offstep;
+            bool v = mv && irow >= 0 && irow < p.Ti;
+            if (v && p.a_scale) v = p.a_scale[(size_t)b * p.Ti + irow] != 0.f;
+            ok |= (uint32_t)v << j;
+        }
+        a_ok[i] = ok;
+        const int k = lc * 4;  // the lane's element within the first K step
+        a_j[i] = k / p.cin;
+        a_ch[i] = k - a_j[i] * p.cin;
+        a_src[i] = p.A + (long long)(b * p.Ti + u * p.in_stride + off0 + a_j[i] * offstep) * p.lda + a_ch[i];
+    }
+    // ---- W chunk state: instruction i covers W rows 8q..8q+7; lane -> row 8q + lane/8, LDS slot lane%8
+    // <- logical chunk (lane%8) ^ ((row >> 1) & 7)
+    const uint16_t *w_ptr[GW];
+    int w_k[GW];
+    bool w_nok[GW];
+#pragma unroll
+    for (int i = 0; i < GW; ++i) {
+        const int n = 8 * (i * NW + wave) + (lane >> 3);
+        const int lc = (lane & 7) ^ ((n >> 1) & 7);
+        w_nok[i] = n0 + n < p.N;
+        w_k[i] = lc * 8;
+        w_ptr[i] = static_cast<const uint16_t *>(p.W) + (size_t)(w_nok[i] ? n0 + n : 0) * p.Kp + lc * 8;
+    }
+
+    auto issue = [&](auto S) {
+        unsigned char *abase = abuf(S);
+        unsigned char *wbase = wbuf(S);
+#pragma unroll
+        for (int i = 0; i < GA; ++i) {
+            const bool ok = (a_ok[i] >> min(a_j[i], 31)) & 1u;  // a_j >= ntaps (past K): bit is 0
+            glds16(ok ? a_src[i] : zero, abase + (i * NW + wave) * 1024);
+            a_ch[i] += kBK;
+            a_src[i] += kBK;
+            const bool w = a_ch[i] >= p.cin;  // cin >= 64: at most one tap change per step
+            a_ch[i] -= w ? p.cin : 0;
+            a_j[i] += w;
+            a_src[i] += w ? tap_delta : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < GW; ++i) {
+            const bool ok = w_nok[i] && w_k[i] < p.Kp;
+            glds16(ok ? static_cast<const void *>(w_ptr[i]) : static_cast<const void *>(zero),
+                   wbase + (i * NW + wave) * 1024);
+            w_ptr[i] += kBK;
+            w_k[i] += kBK;
+        }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+    auto compute = [&](auto S) {
+        const unsigned char *abase = abuf(S);
+        const unsigned char *wbase = wbuf(S);
+#pragma unroll
+        for (int ks = 0; ks < kBK / 16; ++ks) {
+            bf16x8 af[TM], bfr[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int r = wr * 32 * TM + i * 32 + lr;
+                const int c = 4 * ks + 2 * lh;
+                const float4 x0 = *reinterpret_cast<const float4 *>(abase + r * 256 + ((c ^ (r & 15)) << 4));
+                const float4 x1 = *reinterpret_cast<const float4 *>(abase + r * 256 + (((c + 1) ^ (r & 15)) << 4));
+                const uint4 w = make_uint4(pack2(x0.x, x0.y), pack2(x0.z, x0.w), pack2(x1.x, x1.y), pack2(x1.z, x1.w));
+                af[i] = __builtin_bit_cast(bf16x8, w);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int n = wc * 32 * TN + j * 32 + lr;
+                const int c = 2 * ks + lh;
+                bfr[j] = *reinterpret_cast<const bf16x8 *>(wbase + n * 128 + ((c ^ ((n >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+    };
+
+    // prologue: steps 0 .. STAGES-2 in flight (steps past nk DMA zeros into their buffer: harmless)
+    issue(std::integral_constant<int, 0>{});
+    if constexpr (STAGES > 2) issue(std::integral_constant<int, 1>{});
+    // step kt uses buffer kt % STAGES and refills buffer (kt + STAGES - 1) % STAGES, which step kt-1 read
+    auto step = [&](auto S) {
+        constexpr int cur = decltype(S)::value, nxt = (cur + STAGES - 1) % STAGES;
+        wait_vmcnt<(GA + GW) * (STAGES - 2)>();  // this wave's DMAs for step kt have landed
+        mtts::lds_barrier();                       // ... everyone's, and step kt-1's reads are done
+        issue(std::integral_constant<int, nxt>{});
+        compute(S);
+    };
+    for (int kt = 0; kt < nk; kt += STAGES) {
+        step(std::integral_constant<int, 0>{});
+        if (kt + 1 >= nk) break;
+        step(std::integral_constant<int, 1>{});
+        if constexpr (STAGES > 2) {
+            if (kt + 2 >= nk) break;
+            step(std::integral_constant<int, 2>{});
+        }
+    }
+    wait_vmcnt<0>();  // no DMA may still target this workgroup's LDS when it retires
+    if (mtts::gemm_epilogue_vec_ok(p)) {
+        mtts::lds_barrier();  // every wave is past its last fragment read: the buffers are free
+        unsigned char *stage = wave % 4 == 0 ? sA0 : wave % 4 == 1 ? sW0 : wave % 4 == 2 ? sA1 : sW1;
+        mtts::gemm_epilogue_vec<TM, TN>(p, acc, reinterpret_cast<float *>(stage + (wave / 4) * 4096),
+                                        m0 + wr * 32 * TM, n0 + wc * 32 * TN, lane);
+    } else {
+        mtts::gemm_epilogue<TM, TN>(p, acc, m0 + wr * 32 * TM, n0 + wc * 32 * TN, lr, lh);
+    }
+}
+
+struct GldsCfg {
+    int wm, wn, tm, tn, stages;
+};
+constexpr GldsCfg kGlds[] = {
+    {1, 4, 2, 2, 2},  // 32: 64 x 256, 256 thr, 2 stages (96 KiB)
+    {1, 4, 2, 2, 3},  // 33: 64 x 256, 3 stages (144 KiB)
+    {2, 2, 2, 2, 2},  // 34: 128 x 128, 2 stages (96 KiB)
+    {2, 2, 2, 2, 3},  // 35: 128 x 128, 3 stages (144 KiB)
+    {1, 4, 1, 2, 2},  // 36: 32 x 256, 2 stages (80 KiB)
+    {1, 4, 1, 2, 3},  // 37: 32 x 256, 3 stages (120 KiB)
+    {2, 2, 1, 2, 2},  // 38: 64 x 128, 2 stages (64 KiB)
+    {2, 2, 1, 2, 3},  // 39: 64 x 128, 3 stages (96 KiB)
+    {1, 4, 1, 1, 3},  // 40: 32 x 128, 3 stages (72 KiB)
+    {2, 4, 1, 2, 2},  // 41: 64 x 256, 512 thr (waves 32 x 64), 2 stages (96 KiB)
+    {2, 4, 1, 2, 3},  // 42: 64 x 256, 512 thr, 3 stages (144 KiB)
+    {1, 2, 2, 2, 3},  // 43: 64 x 128, 128 thr (waves 64 x 64), 3 stages (96 KiB)
+};
+constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
+
+template <int C>
+int launch_glds(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    constexpr GldsCfg c = kGlds[C];
+    using G = GldsGeom<c.wm, c.wn, c.tm, c.tn, c.stages>;
+    auto kern = conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages>;
+    dim3 grid((unsigned)(((M + G::BM - 1) / G::BM) * ((p.N + G::BN - 1) / G::BN)));
+    hipLaunchKernelGGL(kern, grid, dim3(G::NT), 0, st, p);
+    return mtts::check_launch("conv_gemm_glds");
+}
+
+}  // namespace
+
+namespace mtts {
+
+int conv_gemm_glds_num_cfgs() { return kNumGlds; }
+
+// Whether the LDS-DMA kernels can run this GEMM (bf16; 16-byte aligned rows; 0/1 row mask or none;
+// 32-bit element offsets).
+bool conv_gemm_glds_applies(const mtts_conv_gemm_args &p) {
+    if (p.a_scale && !(p.flags & MTTS_GEMM_F_BINARY_SCALE)) return false;
+    if (p.cin < kBK || p.cin % 4 || p.lda % 4 || p.Kp % 8) return false;
+    const long long arows = (long long)p.nb * p.Ti;
+    if (arows * p.lda >= (1ll << 31) - (1ll << 20)) return false;
+    return true;
+}
+
+int conv_gemm_glds_launch(int id, const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    switch (id) {
+        case 0: return launch_glds<0>(p, M, st);
+        case 1: return launch_glds<1>(p, M, st);
+        case 2: return launch_glds<2>(p, M, st);
+        case 3: return launch_glds<3>(p, M, st);
+        case 4: return launch_glds<4>(p, M, st);
+        case 5: return launch_glds<5>(p, M, st);
+        case 6: return launch_glds<6>(p, M, st);
+        case 7: return launch_glds<7>(p, M, st);
+        case 8: return launch_glds<8>(p, M, st);
+        case 9: return launch_glds<9>(p, M, st);
+        case 10: return launch_glds<10>(p, M, st);
+        default: return launch_glds<11>(p, M, st);
+    }
+}
+
+}  // namespace mtts

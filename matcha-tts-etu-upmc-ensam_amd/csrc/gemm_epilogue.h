@@ -1,0 +1,162 @@
+// Shared epilogue of the conv/linear implicit GEMMs (conv_gemm.hip, conv_gemm_glds.hip).
+//
+// One wave holds TM x TN accumulators of v_mfma_f32_32x32x16 / 32x32x2 layout: register v of lane
+// (lr = lane & 31, lh = lane >> 5) is C[row (v & 3) + 8 (v >> 2) + 4 lh][col lr] of its 32x32 tile.
+// Per element: + bias[n] -> (store pre-activation) -> act -> dropout -> + residual -> * c_scale ->
+// store at row b*To_full + u*out_stride + out_off of C.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "mtts_common.h"
+#include "mtts_decoder.h"
+
+namespace mtts {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// b = m / d, u = m % d for 0 <= m < 2^24 with a precomputed 1/d (float estimate + one correction)
+__device__ __forceinline__ void divmod_fast(int m, int d, float inv_d, int &q, int &r) {
+    q = (int)((float)m * inv_d);
+    r = m - q * d;
+    if (r < 0) { --q; r += d; } else if (r >= d) { ++q; r -= d; }
+}
+
+// XCD-contiguous relabelling of a 1-D grid: the dispatcher deals consecutive block ids round-robin
+// over the 8 XCDs, so block id b becomes the (b % 8)-th contiguous run of tiles (bijective for any
+// grid size); with tiles numbered N-fastest the column blocks of one row panel share an XCD's L2.
+__device__ __forceinline__ int xcd_relabel(int orig, int nwg) {
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void gemm_epilogue(const mtts_conv_gemm_args &p, f32x16 (&acc)[TM][TN], int row0,
+                                              int col0, int lr, int lh) {
+    const int M = p.nb * p.To;
+    const float inv_to = 1.0f / (float)p.To;
+    uint32_t s0 = 0, s1 = 0;
+    if (p.dropout_p > 0.f) {
+        s0 = p.seed[0];
+        s1 = p.seed[1];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        int crows[16];  // output row of each accumulator register (-1: past M)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int m = row0 + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * lh;
+            int b, u;
+            divmod_fast(m, p.To, inv_to, b, u);
+            crows[v] = m < M ? b * p.To_full + u * p.out_stride + p.out_off : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = col0 + j * 32 + lr;
+            if (n >= p.N) continue;
+            const float bn = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                if (crows[v] < 0) continue;
+                const size_t crow = (size_t)crows[v];
+                float val = acc[i][j][v] + bn;
+                if (p.C_pre) p.C_pre[crow * p.ldc + n] = val;
+                if (p.act) val = epi_act(p.act, val, p.aux + crow * p.ldaux + n);
+                if (p.dropout_p > 0.f)
+                    val = dropout_keep(s0, s1, (uint32_t)crow, (uint32_t)n, p.dropout_p)
+                              ? val * (1.0f / (1.0f - p.dropout_p))
+                              : 0.f;
+                if (p.residual) val += p.residual[crow * p.ldr + n];
+                if (p.c_scale) val *= p.c_scale[crow];
+                p.C[crow * p.ldc + n] = val;
+            }
+        }
+    }
+}
+
+// Epilogue over 16-byte rows: each 32x32 accumulator tile goes through a wave-private 4 KiB LDS
+// image (row-major, 32 floats per row -- conflict-free for both the ds_write_b32 of the MFMA layout and
+// the ds_read_b128 of the row chunks), then every lane finishes 4 consecutive columns of one row and
+// writes them (and reads bias / residual / aux) as float4.  The MFMA layout alone gives each lane one
+// column of 16 rows: 4-byte stores in 128-byte row pieces, which left the output-heavy GEMMs (the
+// 1024-wide FFN projection, K = 80 linears) running at ~1.5 TB/s.  Needs N, ldc, ldr, ldaux % 4 == 0
+// and 16-byte aligned C / C_pre / residual / aux (gemm_epilogue_vec_ok); the caller has retired every
+// other use of `stage` (a workgroup barrier after its last LDS read).
+__host__ __device__ inline bool gemm_epilogue_vec_ok(const mtts_conv_gemm_args &p) {
+    auto al = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
+    return p.N % 4 == 0 && p.ldc % 4 == 0 && al(p.C) && al(p.C_pre) && al(p.bias) && (!p.residual || (p.ldr % 4 == 0 && al(p.residual))) &&
+           (!p.aux || (p.ldaux % 4 == 0 && al(p.aux)));
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void gemm_epilogue_vec(const mtts_conv_gemm_args &p, f32x16 (&acc)[TM][TN], float *stage,
+                                                  int row0, int col0, int lane) {
+    const int M = p.nb * p.To;
+    const float inv_to = 1.0f / (float)p.To;
+    const int lr = lane & 31, lh = lane >> 5;
+    const bool drop = p.dropout_p > 0.f;
+    uint32_t s0 = 0, s1 = 0;
+    if (drop) {
+        s0 = p.seed[0];
+        s1 = p.seed[1];
+    }
+    const float keep_scale = drop ? 1.0f / (1.0f - p.dropout_p) : 1.0f;
+    const int rsub = lane >> 3, c4 = lane & 7;  // this lane's row within an 8-row slab and its column chunk
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        // output rows of the 4 slabs this lane finishes in tile row i (same for every j)
+        int crow[4];
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int m = row0 + i * 32 + it * 8 + rsub;
+            int b, u;
+            divmod_fast(m, p.To, inv_to, b, u);
+            crow[it] = m < M ? b * p.To_full + u * p.out_stride + p.out_off : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+#pragma unroll
+            for (int v = 0; v < 16; ++v) stage[((v & 3) + 8 * (v >> 2) + 4 * lh) * 32 + lr] = acc[i][j][v];
+            const int n = col0 + j * 32 + 4 * c4;
+            const bool nok = n < p.N;
+            float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (p.bias && nok) bn = *reinterpret_cast<const float4 *>(p.bias + n);
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                float4 x = reinterpret_cast<const float4 *>(stage)[(it * 8 + rsub) * 8 + c4];
+                if (crow[it] < 0 || !nok) continue;
+                const size_t off = (size_t)crow[it] * p.ldc + n;
+                float e[4] = {x.x + bn.x, x.y + bn.y, x.z + bn.z, x.w + bn.w};
+                if (p.C_pre) *reinterpret_cast<float4 *>(p.C_pre + off) = make_float4(e[0], e[1], e[2], e[3]);
+                if (p.act) {
+                    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (p.act == MTTS_ACT_DGELU || p.act == MTTS_ACT_DRELU)
+                        a = *reinterpret_cast<const float4 *>(p.aux + (size_t)crow[it] * p.ldaux + n);
+                    const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) e[q] = epi_act(p.act, e[q], &av[q]);
+                }
+                if (drop) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        e[q] = dropout_keep(s0, s1, (uint32_t)crow[it], (uint32_t)(n + q), p.dropout_p) ? e[q] * keep_scale
+                                                                                                     : 0.f;
+                }
+                if (p.residual) {
+                    const float4 r = *reinterpret_cast<const float4 *>(p.residual + (size_t)crow[it] * p.ldr + n);
+                    e[0] += r.x; e[1] += r.y; e[2] += r.z; e[3] += r.w;
+                }
+                if (p.c_scale) {
+                    const float cs = p.c_scale[crow[it]];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) e[q] *= cs;
+                }
+                *reinterpret_cast<float4 *>(p.C + off) = make_float4(e[0], e[1], e[2], e[3]);
+            }
+        }
+    }
+}
+
+}  // namespace mtts

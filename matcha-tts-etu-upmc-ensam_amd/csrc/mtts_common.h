@@ -83,6 +83,10 @@ struct mtts_conv_gemm_args;
 namespace mtts {
 // conv_gemm_panel.hip: A-resident bf16 schedule; returns 0 if launched, 1 if it does not apply.
 int conv_gemm_panel_launch(const mtts_conv_gemm_args &p, hipStream_t st);
+// conv_gemm_glds.hip: bf16 LDS-DMA schedules (ids MTTS_GEMM_GLDS + 0 .. num - 1)
+int conv_gemm_glds_num_cfgs();
+bool conv_gemm_glds_applies(const mtts_conv_gemm_args &p);
+int conv_gemm_glds_launch(int id, const mtts_conv_gemm_args &p, int M, hipStream_t st);
 }  // namespace mtts
 
 #define MTTS_CHECK_ARG(cond, msg)                                   \

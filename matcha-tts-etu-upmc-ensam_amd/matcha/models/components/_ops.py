@@ -46,6 +46,10 @@ KERNELS: dict[str, str] = {
 }
 
 
+GEMM_F_BINARY_SCALE = 0x1  # include/mtts_decoder.h MTTS_GEMM_F_BINARY_SCALE
+GEMM_GLDS = 32  # MTTS_GEMM_GLDS: first LDS-DMA schedule id
+
+
 class ConvGemmArgs(ctypes.Structure):
     _fields_ = [("A", ctypes.c_void_p), ("a_scale", ctypes.c_void_p), ("lda", ctypes.c_int32),
                 ("Ti", ctypes.c_int32), ("To", ctypes.c_int32), ("nb", ctypes.c_int32),
@@ -56,7 +60,7 @@ class ConvGemmArgs(ctypes.Structure):
                 ("C", ctypes.c_void_p), ("ldc", ctypes.c_int32), ("To_full", ctypes.c_int32),
                 ("out_stride", ctypes.c_int32), ("out_off", ctypes.c_int32), ("C_pre", ctypes.c_void_p),
                 ("aux", ctypes.c_void_p), ("ldaux", ctypes.c_int32), ("dropout_p", ctypes.c_float),
-                ("seed", ctypes.c_void_p)]
+                ("seed", ctypes.c_void_p), ("flags", ctypes.c_int32)]
 
 
 class ConvWgradArgs(ctypes.Structure):
@@ -284,7 +288,11 @@ LAUNCH_LOG: list | None = None
 
 def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_stride=1, out_off=0, *, prec,
           a_scale=None, bias=None, act=ACT_NONE, residual=None, c_scale=None, C_pre=None, aux=None,
-          dropout_p=0.0, seed=None, tile_cfg=-1):
+          dropout_p=0.0, seed=None, tile_cfg=-1, binary_scale=True):
+    """One mtts_conv_gemm launch.  Every row scale the model passes (a_scale) is a sequence mask
+    (matcha.utils.model.sequence_mask: 0/1 by construction, as the reference's x * mask), so
+    ``binary_scale`` defaults to True: the bf16 LDS-DMA schedule then reads masked rows as zeros
+    instead of multiplying.  Pass False for a general row scale."""
     args = ConvGemmArgs()
     args.A, args.a_scale, args.lda, args.Ti, args.To, args.nb = A.data_ptr(), N.ptr(a_scale), A.shape[-1], Ti, To, nb
     args.in_stride, args.ntaps, args.cin = in_stride, len(offs), cin
@@ -298,6 +306,7 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     args.C_pre = N.ptr(C_pre)
     args.aux, args.ldaux = N.ptr(aux), (aux.shape[-1] if aux is not None else 0)
     args.dropout_p, args.seed = float(dropout_p), N.ptr(seed)
+    args.flags = GEMM_F_BINARY_SCALE if (binary_scale and a_scale is not None) else 0
     log = LAUNCH_LOG
     if log is not None:
         st = torch.cuda.current_stream(C.device)
@@ -309,7 +318,10 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
         M_ = nb * To
         nbytes = nb * Ti * cin * 4 + N_ * Kp * Wp.element_size() + M_ * N_ * 4
         nbytes += sum(M_ * N_ * 4 for t in (residual, aux, C_pre) if t is not None)
-        log.append((e0, e1, 2.0 * M_ * N_ * args.K, prec, nbytes))
+        log.append((e0, e1, 2.0 * M_ * N_ * args.K, prec, nbytes,
+                    dict(M=M_, N=N_, K=args.K, cin=cin, ntaps=len(offs), in_stride=in_stride, res=residual is not None,
+                         act=act, pre=C_pre is not None, drop=dropout_p > 0, cs=c_scale is not None,
+                         asc=a_scale is not None, cfg=tile_cfg)))
 
 
 def _wgrad(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin, N_, dw, strides, *, prec,

@@ -57,7 +57,8 @@ if prec_name == "bf16":
         y = torch.zeros(B, 2 * T, Cout, device=dev)
         pre = torch.zeros(B, 2 * T, Cout, device=dev)
         O._gemm(x, T, T, B, 1, [-1, 0, 1], Cin, Wp, Kp, Cout, y, 2 * T, 2, 1, prec=prec, a_scale=msk, bias=bias,
-                act=1, residual=res, c_scale=cs, C_pre=pre, dropout_p=0.1, seed=seed, tile_cfg=cfg)
+                act=1, residual=res, c_scale=cs, C_pre=pre, dropout_p=0.1, seed=seed, tile_cfg=cfg,
+                binary_scale=True)
         torch.cuda.synchronize()
         outs[cfg] = (y, pre)
         e = max(((y - outs[7][0]).norm() / outs[7][0].norm()).item(), ((pre - outs[7][1]).norm() / outs[7][1].norm()).item())
