@@ -13,6 +13,9 @@
  *
  * Reference interfaces replaced (paths relative to the reference repository root):
  *   mtts_maximum_path_f32          <- matcha/utils/monotonic_align/__init__.py:40-55  maximum_path(value, mask)
+ *   mtts_prior_maximum_path        <- matcha/models/matcha_tts.py:461-478 (log-prior lattice + maximum_path +
+ *                                     the duration target), fused
+ *   mtts_expand_rows_fwd / _bwd    <- matcha/models/matcha_tts.py:504-505  mu_y = attn^T @ mu_x
  *   mtts_compute_batch_alignments  <- matcha/utils/monotonic_align/core.pyx:101-128   compute_batch_alignments(...)
  *                                     (bound as maximum_path_c, __init__.py:4-8)
  * Decoder / CFM operators (matcha/models/components/{decoder,transformer,flow_matching}.py) are
@@ -89,6 +92,36 @@ int mtts_compute_batch_alignments(int32_t *paths, float *values, const int32_t *
                                   const int32_t *t_ys, int32_t B, int32_t Tx, int32_t Ty,
                                   float max_neg_val, void *workspace, size_t workspace_bytes,
                                   void *hip_stream);
+
+/*
+ * Fused alignment of the training forward (matcha_tts.py:461-478):
+ *   lattice[b,i,j] = (log N(y[b,:,j]; mu_x[b,:,i], I)) * x_mask[b,i] * y_mask[b,j]   (matcha_tts.py:467-472,
+ *                    maximum_path's value*mask) with the masks from x_lengths / y_lengths (int64 [B]),
+ *   then the DP and backtrack of mtts_maximum_path_f32 on it (t_x = x_lengths, t_y = y_lengths).
+ *   mu_x : float32 [B, C, Tx], y : float32 [B, C, Ty] (channel-major, C-contiguous, device memory).
+ *   Outputs (each optional): path float32 [B,Tx,Ty] (dense hard attention), lengths_out int32 [B,2],
+ *   row_start_out int32 [B,Tx] (as mtts_maximum_path_f32), dur_out float32 [B,Tx] = sum_j path[b,i,j],
+ *   col_row_out int32 [B,Ty] = the text row of frame j (-1 past t_y), lattice_out float32 [B,Tx,Ty]
+ *   (the masked lattice; otherwise it lives in the workspace).
+ *   The lattice sums run in ascending channel order, one fp32 operation each (bit-reproducible on the
+ *   host); the reference's torch matmuls use an implementation-defined order.
+ */
+size_t mtts_prior_maximum_path_workspace_size(int32_t B, int32_t Tx, int32_t Ty);
+int mtts_prior_maximum_path(const float *mu_x, const float *y, const int64_t *x_lengths, const int64_t *y_lengths,
+                            int32_t B, int32_t C, int32_t Tx, int32_t Ty, float *path, int32_t *lengths_out,
+                            int32_t *row_start_out, float *dur_out, int32_t *col_row_out, float *lattice_out,
+                            void *workspace, size_t workspace_bytes, void *hip_stream);
+
+/*
+ * mu_y = attn^T @ mu_x for a hard alignment (matcha_tts.py:504-505) as a gather, and its backward:
+ *   fwd: dst[b,c,j] = src[b,c,col_row[b,j]] (0 where col_row < 0); src [B,C,Tx], dst [B,C,Ty] float32.
+ *   bwd: dx[b,c,i] = sum over the frames j of row i (row_start / lengths of mtts_maximum_path_f32) of
+ *        dy[b,c,j], in ascending j (deterministic).
+ */
+int mtts_expand_rows_fwd(const float *src, const int32_t *col_row, int32_t B, int32_t C, int32_t Tx, int32_t Ty,
+                         float *dst, void *hip_stream);
+int mtts_expand_rows_bwd(const float *dy, const int32_t *row_start, const int32_t *lengths, int32_t B, int32_t C,
+                         int32_t Tx, int32_t Ty, float *dx, void *hip_stream);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -84,6 +84,16 @@ int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip
  * (csrc/conv_gemm_panel.hip), -1 = heuristic.
  * For tuning and tests; mtts_conv_gemm picks the configuration itself. */
 int mtts_conv_gemm_tile(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg, void *hip_stream);
+/* With a caller-owned workspace: lets the bf16 LDS-DMA schedules split K over several workgroups
+ * (fp32 partial slabs, combined in a fixed order by a second kernel that also runs the epilogue) when
+ * the output alone cannot fill the chip (e.g. the text encoder's 3840-row GEMMs).  tile_cfg as above
+ * (-1 = heuristic); splits: 0 = heuristic, 1 = never, >= 2 = that many (LDS-DMA schedules only).
+ * mtts_conv_gemm_workspace_size returns the bytes the same (args, precision, tile_cfg, splits) needs
+ * (0: no split); a smaller workspace runs the GEMM unsplit. */
+size_t mtts_conv_gemm_workspace_size(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg,
+                                     int32_t splits);
+int mtts_conv_gemm_ws(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg, int32_t splits,
+                      void *workspace, size_t workspace_bytes, void *hip_stream);
 
 /*
  * Weight gradient of the same implicit GEMM:

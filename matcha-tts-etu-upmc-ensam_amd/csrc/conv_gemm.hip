@@ -766,20 +766,53 @@ static void launch_by_id(int id, const mtts_conv_gemm_args &p, int M, hipStream_
     }
 }
 
-// From the tile sweeps on the train step's shapes (tools/gemm_sweep.py, graph-timed;
-// profiles/r01/gemm_sweep_glds.log): the LDS-DMA kernels (64 x 256 tiles, 512 threads) win by 5-20 %
-// wherever the reduction is long (K >= 512) or the output wide (N >= 768) -- three stages in flight
-// from K >= 768, two below; shorter / narrower GEMMs keep the register-staged 32 x 128 tiles: 64-wide
-// K steps with two in flight (config 12) for K >= 384, 32-wide (config 7) below.  fp32 (parity
-// mode) uses config 7.
+// Schedule choice from graph-timed sweeps of the train step's GEMMs WITH their epilogues
+// (tools/gemm_sweep2.py -> profiles/r01/gemm_sweep2.log):
+//  * erf-GELU / GELU' epilogues (the FFN's 1024-wide projection and its dgrad) are epilogue-bound:
+//    the small register-staged 32 x 128 tiles (config 7) keep 3 workgroups per CU so one
+//    workgroup's epilogue overlaps another's main loop (75 vs 88 us at 19200 x 1024 x 256);
+//  * the LDS-DMA 64 x 256 kernel (3 stages) wins when its tiles fill the chip in ONE round
+//    (128..256 tiles, K >= 768: the half-resolution decoder GEMMs, 17.4 vs 19.0 us) -- at 300 tiles
+//    the second round's tail makes it lose to config 12;
+//  * long reductions on grids far below the CU count (the text encoder's 3840 x 192 x 2304 conv)
+//    split K four ways on that kernel (22 vs 29 us);
+//  * everything else: 32 x 128 register tiles, 64-wide K steps two in flight (config 12) from
+//    K >= 384, 32-wide (config 7) below.  fp32 (parity mode) uses config 7.
+static int glds_tiles(const mtts_conv_gemm_args &p, int M) { return ((M + 63) / 64) * ((p.N + 255) / 256); }
+
 static int pick_cfg(const mtts_conv_gemm_args &p, int M, bool bf16) {
-    (void)M;
     if (!bf16) return 7;
-    if ((p.K >= 512 || p.N >= 768) && mtts::conv_gemm_glds_applies(p)) return MTTS_GEMM_GLDS + (p.K >= 768 ? 10 : 9);
+    if (p.act == MTTS_ACT_GELU || p.act == MTTS_ACT_DGELU) return 7;
+    if (mtts::conv_gemm_glds_applies(p) && p.K >= 768) {
+        const int t = glds_tiles(p, M);
+        if ((t >= 128 && t <= 256) || (t < 128 && p.K >= 1536 && p.N % 4 == 0)) return MTTS_GEMM_GLDS + 10;
+    }
     return p.K >= 384 ? 12 : 7;
 }
 
-static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, int cfg, void *hip_stream) {
+// Split-K (LDS-DMA schedules, heuristic pick only): grids below half the chip with >= 24 K steps
+static int pick_splits(const mtts_conv_gemm_args &p, int M, int cfg, int splits) {
+    if (cfg < MTTS_GEMM_GLDS || p.N % 4) return 1;
+    if (splits > 0) return splits;
+    const int nk = (p.K + 63) / 64;
+    if (cfg != MTTS_GEMM_GLDS + 10 || glds_tiles(p, M) >= 128 || nk < 24) return 1;
+    return 4;
+}
+
+struct GemmPlan {
+    int cfg, splits;
+    size_t ws;
+};
+
+static GemmPlan plan_gemm(const mtts_conv_gemm_args &p, bool bf16, int cfg, int splits) {
+    const int M = p.nb * p.To;
+    if (cfg < 0) cfg = pick_cfg(p, M, bf16);
+    splits = pick_splits(p, M, cfg, splits);
+    return {cfg, splits, cfg >= MTTS_GEMM_GLDS ? mtts::conv_gemm_glds_splitk_bytes(p, splits) : 0};
+}
+
+static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, int cfg, int splits, void *ws,
+                          size_t ws_bytes, void *hip_stream) {
     MTTS_CHECK_ARG(args != nullptr, "conv_gemm: args is null");
     const mtts_conv_gemm_args &p = *args;
     int rc = check_gather(p.A, p.lda, p.cin, p.ntaps, p.K);
@@ -796,37 +829,47 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     MTTS_CHECK_ARG(p.dropout_p <= 0.f || (p.seed && p.dropout_p < 1.f), "conv_gemm: dropout needs a seed pointer");
     const bool glds_id = cfg >= MTTS_GEMM_GLDS && cfg < MTTS_GEMM_GLDS + mtts::conv_gemm_glds_num_cfgs();
     MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || cfg == MTTS_GEMM_PANEL || glds_id, "conv_gemm: bad tile config");
+    MTTS_CHECK_ARG(splits >= 0, "conv_gemm: bad split count");
     const int M = p.nb * p.To;
     if (M == 0) return MTTS_OK;
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
     const bool bf16 = precision == MTTS_PREC_BF16;
-    // bf16: the A-resident panel schedule (conv_gemm_panel.hip) when its LDS panel fits
     if (cfg == MTTS_GEMM_PANEL) {
         if (!bf16) return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: panel schedule is bf16 only");
         if (mtts::conv_gemm_panel_launch(p, st) == 0) return mtts::check_launch("conv_gemm_panel_kernel");
         return mtts::fail(MTTS_ERR_SHAPE, "conv_gemm: panel schedule does not fit");
     }
-    if (glds_id) {
-        if (!bf16 || !mtts::conv_gemm_glds_applies(p))
-            return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: LDS-DMA schedule needs bf16, cin >= 64 and a 0/1 a_scale");
-        return mtts::conv_gemm_glds_launch(cfg - MTTS_GEMM_GLDS, p, M, st);
+    if (glds_id && (!bf16 || !mtts::conv_gemm_glds_applies(p)))
+        return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: LDS-DMA schedule needs bf16, cin >= 64 and a 0/1 a_scale");
+    const GemmPlan pl = plan_gemm(p, bf16, cfg, splits);
+    if (pl.cfg >= MTTS_GEMM_GLDS) {
+        int s = pl.splits;
+        if (pl.ws > 0 && (!ws || ws_bytes < pl.ws || (uintptr_t)ws % 16)) s = 1;  // no workspace: unsplit
+        return mtts::conv_gemm_glds_launch(pl.cfg - MTTS_GEMM_GLDS, p, M, s, static_cast<float *>(ws), st);
     }
-    if (cfg < 0) {
-        cfg = pick_cfg(p, M, bf16);
-        if (cfg >= MTTS_GEMM_GLDS) return mtts::conv_gemm_glds_launch(cfg - MTTS_GEMM_GLDS, p, M, st);
-    }
-    if (bf16) launch_by_id<true>(cfg, p, M, st);
-    else launch_by_id<false>(cfg, p, M, st);
+    if (bf16) launch_by_id<true>(pl.cfg, p, M, st);
+    else launch_by_id<false>(pl.cfg, p, M, st);
     return mtts::check_launch("conv_gemm_kernel");
 }
 
 extern "C" int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream) {
-    return conv_gemm_impl(args, precision, -1, hip_stream);
+    return conv_gemm_impl(args, precision, -1, 1, nullptr, 0, hip_stream);
 }
 
 extern "C" int mtts_conv_gemm_tile(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg,
                                    void *hip_stream) {
-    return conv_gemm_impl(args, precision, tile_cfg, hip_stream);
+    return conv_gemm_impl(args, precision, tile_cfg, 1, nullptr, 0, hip_stream);
+}
+
+extern "C" size_t mtts_conv_gemm_workspace_size(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg,
+                                                int32_t splits) {
+    if (!args || args->nb * args->To == 0) return 0;
+    return plan_gemm(*args, precision == MTTS_PREC_BF16, tile_cfg, splits).ws;
+}
+
+extern "C" int mtts_conv_gemm_ws(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg, int32_t splits,
+                                 void *workspace, size_t workspace_bytes, void *hip_stream) {
+    return conv_gemm_impl(args, precision, tile_cfg, splits, workspace, workspace_bytes, hip_stream);
 }
 
 __global__ void dropout_apply_kernel(const float *__restrict__ x, float *__restrict__ y, int rows, int cols, int ld,

@@ -81,7 +81,7 @@ struct GldsGeom {
 };
 
 template <int WM, int WN, int TM, int TN, int STAGES>
-__global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_gemm_args p) {
+__global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_gemm_args p, int ksteps, float *part) {
     using G = GldsGeom<WM, WN, TM, TN, STAGES>;
     constexpr int NT = G::NT, BM = G::BM, BN = G::BN, GA = G::GA, GW = G::GW, NW = NT / 64;
     // one __shared__ object per stage and operand, and a K loop unrolled by STAGES so every access
@@ -108,15 +108,24 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
     const int wr = wave / WN, wc = wave % WN;
     const int lr = lane & 31, lh = lane >> 5;
     const int M = p.nb * p.To;
-    int m0, n0;
+    // split-K (part != NULL): grid = tiles x S, the S splits of a tile adjacent (same XCD); split s
+    // reduces K steps [s*ksteps, min(nk, (s+1)*ksteps)) and stores raw fp32 partials to part[s][M][N]
+    int m0, n0, kstep0 = 0, nk = (p.K + kBK - 1) / kBK;
     {
         const int nt = (p.N + BN - 1) / BN;
-        const int t = mtts::xcd_relabel(blockIdx.x, gridDim.x);
+        const int ntiles = ((M + BM - 1) / BM) * nt;
+        const int S = gridDim.x / ntiles;
+        int t = mtts::xcd_relabel(blockIdx.x, gridDim.x);
+        if (S > 1) {
+            const int tile = t / S, split = t - tile * S;
+            t = tile;
+            kstep0 = split * ksteps;
+            nk = min(ksteps, nk - kstep0);
+        }
         const int mt = t / nt;
         m0 = mt * BM;
         n0 = (t - mt * nt) * BN;
     }
-    const int nk = (p.K + kBK - 1) / kBK;
     const float inv_to = 1.0f / (float)p.To;
     const int off0 = p.off[0], offstep = p.ntaps > 1 ? p.off[1] - p.off[0] : 0;
 
@@ -143,7 +152,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
             ok |= (uint32_t)v << j;
         }
         a_ok[i] = ok;
-        const int k = lc * 4;  // the lane's element within the first K step
+        const int k = kstep0 * kBK + lc * 4;  // the lane's element within the first K step
         a_j[i] = k / p.cin;
         a_ch[i] = k - a_j[i] * p.cin;
         a_src[i] = p.A + (long long)(b * p.Ti + u * p.in_stride + off0 + a_j[i] * offstep) * p.lda + a_ch[i];
@@ -158,8 +167,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
         const int n = 8 * (i * NW + wave) + (lane >> 3);
         const int lc = (lane & 7) ^ ((n >> 1) & 7);
         w_nok[i] = n0 + n < p.N;
-        w_k[i] = lc * 8;
-        w_ptr[i] = static_cast<const uint16_t *>(p.W) + (size_t)(w_nok[i] ? n0 + n : 0) * p.Kp + lc * 8;
+        w_k[i] = kstep0 * kBK + lc * 8;
+        w_ptr[i] = static_cast<const uint16_t *>(p.W) + (size_t)(w_nok[i] ? n0 + n : 0) * p.Kp + w_k[i];
     }
 
     auto issue = [&](auto S) {
@@ -244,14 +253,46 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
         }
     }
     wait_vmcnt<0>();  // no DMA may still target this workgroup's LDS when it retires
-    if (mtts::gemm_epilogue_vec_ok(p)) {
+    if (part || mtts::gemm_epilogue_vec_ok(p)) {
         mtts::lds_barrier();  // every wave is past its last fragment read: the buffers are free
         unsigned char *stage = wave % 4 == 0 ? sA0 : wave % 4 == 1 ? sW0 : wave % 4 == 2 ? sA1 : sW1;
-        mtts::gemm_epilogue_vec<TM, TN>(p, acc, reinterpret_cast<float *>(stage + (wave / 4) * 4096),
-                                        m0 + wr * 32 * TM, n0 + wc * 32 * TN, lane);
+        float *st = reinterpret_cast<float *>(stage + (wave / 4) * 4096);
+        if (part)
+            mtts::gemm_store_partial<TM, TN>(p, acc, st, part + (size_t)(kstep0 / ksteps) * M * p.N,
+                                             m0 + wr * 32 * TM, n0 + wc * 32 * TN, lane);
+        else
+            mtts::gemm_epilogue_vec<TM, TN>(p, acc, st, m0 + wr * 32 * TM, n0 + wc * 32 * TN, lane);
     } else {
         mtts::gemm_epilogue<TM, TN>(p, acc, m0 + wr * 32 * TM, n0 + wc * 32 * TN, lr, lh);
     }
+}
+
+// Split-K combine: out = epilogue(sum_s part[s][m][n..n+3]) summed in split order (deterministic).
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(mtts_conv_gemm_args p, const float *__restrict__ part,
+                                                              int S) {
+    const int M = p.nb * p.To, n4 = p.N >> 2;
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long long)M * n4) return;
+    const int m = (int)(idx / n4), n = (int)(idx - (long long)m * n4) * 4;
+    const size_t slab = (size_t)M * p.N;
+    float4 a = *reinterpret_cast<const float4 *>(part + (size_t)m * p.N + n);
+    for (int s = 1; s < S; ++s) {
+        const float4 b = *reinterpret_cast<const float4 *>(part + s * slab + (size_t)m * p.N + n);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.bias) bn = *reinterpret_cast<const float4 *>(p.bias + n);
+    float e[4] = {a.x + bn.x, a.y + bn.y, a.z + bn.z, a.w + bn.w};
+    int b, u;
+    mtts::divmod_fast(m, p.To, 1.0f / (float)p.To, b, u);
+    uint32_t s0 = 0, s1 = 0;
+    float keep = 1.f;
+    if (p.dropout_p > 0.f) {
+        s0 = p.seed[0];
+        s1 = p.seed[1];
+        keep = 1.0f / (1.0f - p.dropout_p);
+    }
+    mtts::epilogue_row4(p, b * p.To_full + u * p.out_stride + p.out_off, n, e, s0, s1, keep);
 }
 
 struct GldsCfg {
@@ -270,17 +311,27 @@ constexpr GldsCfg kGlds[] = {
     {2, 4, 1, 2, 2},  // 41: 64 x 256, 512 thr (waves 32 x 64), 2 stages (96 KiB)
     {2, 4, 1, 2, 3},  // 42: 64 x 256, 512 thr, 3 stages (144 KiB)
     {1, 2, 2, 2, 3},  // 43: 64 x 128, 128 thr (waves 64 x 64), 3 stages (96 KiB)
+    {2, 2, 1, 1, 3},  // 44: 64 x 64, 3 stages (72 KiB)
+    {2, 2, 1, 1, 2},  // 45: 64 x 64, 2 stages (48 KiB)
 };
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
 
 template <int C>
-int launch_glds(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+int launch_glds(const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
     constexpr GldsCfg c = kGlds[C];
     using G = GldsGeom<c.wm, c.wn, c.tm, c.tn, c.stages>;
     auto kern = conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages>;
-    dim3 grid((unsigned)(((M + G::BM - 1) / G::BM) * ((p.N + G::BN - 1) / G::BN)));
-    hipLaunchKernelGGL(kern, grid, dim3(G::NT), 0, st, p);
-    return mtts::check_launch("conv_gemm_glds");
+    const int nk = (p.K + kBK - 1) / kBK;
+    const int ksteps = (nk + splits - 1) / splits;
+    const int S = splits > 1 ? (nk + ksteps - 1) / ksteps : 1;  // every split non-empty
+    dim3 grid((unsigned)(((M + G::BM - 1) / G::BM) * ((p.N + G::BN - 1) / G::BN) * S));
+    hipLaunchKernelGGL(kern, grid, dim3(G::NT), 0, st, p, ksteps, S > 1 ? part : nullptr);
+    int rc = mtts::check_launch("conv_gemm_glds");
+    if (rc || S == 1) return rc;
+    const long long n4 = (long long)M * (p.N / 4);
+    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, p,
+                       (const float *)part, S);
+    return mtts::check_launch("splitk_epilogue_kernel");
 }
 
 }  // namespace
@@ -299,20 +350,30 @@ bool conv_gemm_glds_applies(const mtts_conv_gemm_args &p) {
     return true;
 }
 
-int conv_gemm_glds_launch(int id, const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+size_t conv_gemm_glds_splitk_bytes(const mtts_conv_gemm_args &p, int splits) {
+    if (splits <= 1) return 0;
+    const int nk = (p.K + kBK - 1) / kBK;
+    const int ksteps = (nk + splits - 1) / splits;
+    const int S = (nk + ksteps - 1) / ksteps;
+    return S > 1 ? (size_t)S * p.nb * p.To * p.N * sizeof(float) : 0;
+}
+
+int conv_gemm_glds_launch(int id, const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
     switch (id) {
-        case 0: return launch_glds<0>(p, M, st);
-        case 1: return launch_glds<1>(p, M, st);
-        case 2: return launch_glds<2>(p, M, st);
-        case 3: return launch_glds<3>(p, M, st);
-        case 4: return launch_glds<4>(p, M, st);
-        case 5: return launch_glds<5>(p, M, st);
-        case 6: return launch_glds<6>(p, M, st);
-        case 7: return launch_glds<7>(p, M, st);
-        case 8: return launch_glds<8>(p, M, st);
-        case 9: return launch_glds<9>(p, M, st);
-        case 10: return launch_glds<10>(p, M, st);
-        default: return launch_glds<11>(p, M, st);
+        case 0: return launch_glds<0>(p, M, splits, part, st);
+        case 1: return launch_glds<1>(p, M, splits, part, st);
+        case 2: return launch_glds<2>(p, M, splits, part, st);
+        case 3: return launch_glds<3>(p, M, splits, part, st);
+        case 4: return launch_glds<4>(p, M, splits, part, st);
+        case 5: return launch_glds<5>(p, M, splits, part, st);
+        case 6: return launch_glds<6>(p, M, splits, part, st);
+        case 7: return launch_glds<7>(p, M, splits, part, st);
+        case 8: return launch_glds<8>(p, M, splits, part, st);
+        case 9: return launch_glds<9>(p, M, splits, part, st);
+        case 10: return launch_glds<10>(p, M, splits, part, st);
+        case 11: return launch_glds<11>(p, M, splits, part, st);
+        case 12: return launch_glds<12>(p, M, splits, part, st);
+        default: return launch_glds<13>(p, M, splits, part, st);
     }
 }
 

@@ -76,6 +76,59 @@ __device__ __forceinline__ void gemm_epilogue(const mtts_conv_gemm_args &p, f32x
     }
 }
 
+// Everything after the bias for 4 consecutive columns n..n+3 of output row crow (float4 I/O).
+__device__ __forceinline__ void epilogue_row4(const mtts_conv_gemm_args &p, int crow, int n, float (&e)[4],
+                                              uint32_t s0, uint32_t s1, float keep_scale) {
+    const size_t off = (size_t)crow * p.ldc + n;
+    if (p.C_pre) *reinterpret_cast<float4 *>(p.C_pre + off) = make_float4(e[0], e[1], e[2], e[3]);
+    if (p.act) {
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (p.act == MTTS_ACT_DGELU || p.act == MTTS_ACT_DRELU)
+            a = *reinterpret_cast<const float4 *>(p.aux + (size_t)crow * p.ldaux + n);
+        const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) e[q] = epi_act(p.act, e[q], &av[q]);
+    }
+    if (p.dropout_p > 0.f) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            e[q] = dropout_keep(s0, s1, (uint32_t)crow, (uint32_t)(n + q), p.dropout_p) ? e[q] * keep_scale : 0.f;
+    }
+    if (p.residual) {
+        const float4 r = *reinterpret_cast<const float4 *>(p.residual + (size_t)crow * p.ldr + n);
+        e[0] += r.x; e[1] += r.y; e[2] += r.z; e[3] += r.w;
+    }
+    if (p.c_scale) {
+        const float cs = p.c_scale[crow];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) e[q] *= cs;
+    }
+    *reinterpret_cast<float4 *>(p.C + off) = make_float4(e[0], e[1], e[2], e[3]);
+}
+
+// Split-K partial store: the raw accumulators of a wave's tiles into part[M][N] (row = GEMM row),
+// through the same per-wave LDS image as gemm_epilogue_vec.
+template <int TM, int TN>
+__device__ __forceinline__ void gemm_store_partial(const mtts_conv_gemm_args &p, f32x16 (&acc)[TM][TN], float *stage,
+                                                   float *part, int row0, int col0, int lane) {
+    const int M = p.nb * p.To;
+    const int lr = lane & 31, lh = lane >> 5, rsub = lane >> 3, c4 = lane & 7;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+#pragma unroll
+            for (int v = 0; v < 16; ++v) stage[((v & 3) + 8 * (v >> 2) + 4 * lh) * 32 + lr] = acc[i][j][v];
+            const int n = col0 + j * 32 + 4 * c4;
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const float4 x = reinterpret_cast<const float4 *>(stage)[(it * 8 + rsub) * 8 + c4];
+                const int m = row0 + i * 32 + it * 8 + rsub;
+                if (m < M && n < p.N) *reinterpret_cast<float4 *>(part + (size_t)m * p.N + n) = x;
+            }
+        }
+}
+
 // Epilogue over 16-byte rows: each 32x32 accumulator tile goes through a wave-private 4 KiB LDS
 // image (row-major, 32 floats per row -- conflict-free for both the ds_write_b32 of the MFMA layout and
 // the ds_read_b128 of the row chunks), then every lane finishes 4 consecutive columns of one row and
@@ -127,33 +180,8 @@ __device__ __forceinline__ void gemm_epilogue_vec(const mtts_conv_gemm_args &p, 
             for (int it = 0; it < 4; ++it) {
                 float4 x = reinterpret_cast<const float4 *>(stage)[(it * 8 + rsub) * 8 + c4];
                 if (crow[it] < 0 || !nok) continue;
-                const size_t off = (size_t)crow[it] * p.ldc + n;
                 float e[4] = {x.x + bn.x, x.y + bn.y, x.z + bn.z, x.w + bn.w};
-                if (p.C_pre) *reinterpret_cast<float4 *>(p.C_pre + off) = make_float4(e[0], e[1], e[2], e[3]);
-                if (p.act) {
-                    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (p.act == MTTS_ACT_DGELU || p.act == MTTS_ACT_DRELU)
-                        a = *reinterpret_cast<const float4 *>(p.aux + (size_t)crow[it] * p.ldaux + n);
-                    const float av[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) e[q] = epi_act(p.act, e[q], &av[q]);
-                }
-                if (drop) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        e[q] = dropout_keep(s0, s1, (uint32_t)crow[it], (uint32_t)(n + q), p.dropout_p) ? e[q] * keep_scale
-                                                                                                     : 0.f;
-                }
-                if (p.residual) {
-                    const float4 r = *reinterpret_cast<const float4 *>(p.residual + (size_t)crow[it] * p.ldr + n);
-                    e[0] += r.x; e[1] += r.y; e[2] += r.z; e[3] += r.w;
-                }
-                if (p.c_scale) {
-                    const float cs = p.c_scale[crow[it]];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) e[q] *= cs;
-                }
-                *reinterpret_cast<float4 *>(p.C + off) = make_float4(e[0], e[1], e[2], e[3]);
+                epilogue_row4(p, crow[it], n, e, s0, s1, keep_scale);
             }
         }
     }

@@ -26,6 +26,7 @@
 // diagonal (`from_prev >= from_same or x == y`, core.pyx:73), out-of-band cells hold max_neg_val.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdint>
 
 #include "mtts_common.h"
@@ -308,6 +309,155 @@ __global__ __launch_bounds__(256) void mas_expand_kernel(const int32_t *__restri
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Fused producer: the log-prior lattice of matcha_tts.py:467-472 (MatchaTTS.forward) computed
+// straight from mu_x [B,C,Tx] and y [B,C,Ty] (channel-major, as the encoder / data loader hold them)
+// and multiplied by the attention mask x_mask[i] * y_mask[j] (maximum_path's value*mask,
+// __init__.py:45), written once to HBM for the DP:
+//   ysq[j]   = sum_c -0.5 * (y[c,j] * y[c,j])            (y_square = factor^T @ y^2)
+//   ymu[i,j] = sum_c (-mu[c,i]) * y[c,j]                 (y_mu_double = (2 * factor * mu)^T @ y)
+//   musq[i]  = sum_c -0.5 * (mu[c,i] * mu[c,i])          (mu_square = sum(factor * mu^2, 1))
+//   lattice  = ((ysq[j] - ymu[i,j]) + musq[i]) + const,  const = -0.5 * log(2 pi) * C
+// Every product and sum is one fp32 operation in ascending c (-ffp-contract=off for this file): a
+// numpy restatement reproduces the lattice bit for bit (oracle/prior_oracle.py).  The reference's
+// torch matmuls sum in an implementation-defined order, so lattices agree to fp32 rounding, not bits.
+// Tile: 64 text rows x 64 frames per 256-thread block, 4 x 4 cells per thread, mu / y tiles staged
+// in LDS 16 channels at a time.  The block of tile (0, 0) also writes t_x / t_y as int32 for the DP.
+constexpr int kLpT = 64;
+constexpr int kLpC = 16;  // channels staged per LDS round
+
+__global__ __launch_bounds__(256) void log_prior_kernel(const float *__restrict__ mu, const float *__restrict__ y,
+                                                        const int64_t *__restrict__ xl, const int64_t *__restrict__ yl,
+                                                        int C, int Tx, int Ty, float cst, float *__restrict__ out,
+                                                        int32_t *__restrict__ txy) {
+    __shared__ __attribute__((aligned(16))) float smu[kLpC][kLpT];
+    __shared__ __attribute__((aligned(16))) float sy[kLpC][kLpT];
+    const int b = blockIdx.z, i0 = blockIdx.y * kLpT, j0 = blockIdx.x * kLpT;
+    const int tid = threadIdx.x, ti = (tid >> 4) * 4, tj = (tid & 15) * 4;
+    const int t_x = (int)min<int64_t>(max<int64_t>(xl[b], 0), Tx);
+    const int t_y = (int)min<int64_t>(max<int64_t>(yl[b], 0), Ty);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) {
+        txy[b] = t_x;
+        txy[gridDim.z + b] = t_y;
+    }
+    const float *mub = mu + (size_t)b * C * Tx, *yb = y + (size_t)b * C * Ty;
+    float ymu[4][4], ysq[4], musq[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        ysq[r] = 0.f;
+        musq[r] = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ymu[r][q] = 0.f;
+    }
+    for (int c0 = 0; c0 < C; c0 += kLpC) {
+        for (int e = tid; e < kLpC * kLpT; e += 256) {
+            const int c = c0 + e / kLpT, t = e % kLpT;
+            smu[e / kLpT][t] = (c < C && i0 + t < Tx) ? mub[(size_t)c * Tx + i0 + t] : 0.f;
+            sy[e / kLpT][t] = (c < C && j0 + t < Ty) ? yb[(size_t)c * Ty + j0 + t] : 0.f;
+        }
+        __syncthreads();
+        const int cn = min(kLpC, C - c0);
+        for (int c = 0; c < cn; ++c) {
+            const float4 m4 = *reinterpret_cast<const float4 *>(&smu[c][ti]);
+            const float4 y4 = *reinterpret_cast<const float4 *>(&sy[c][tj]);
+            const float mv[4] = {m4.x, m4.y, m4.z, m4.w}, yv[4] = {y4.x, y4.y, y4.z, y4.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                musq[r] = musq[r] + -0.5f * (mv[r] * mv[r]);
+                ysq[r] = ysq[r] + -0.5f * (yv[r] * yv[r]);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ymu[r][q] = ymu[r][q] + (-mv[r]) * yv[q];
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = i0 + ti + r;
+        if (i >= Tx) continue;
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = j0 + tj + q;
+            const float m = (i < t_x && j < t_y) ? 1.f : 0.f;  // x_mask[i] * y_mask[j]
+            v[q] = (((ysq[q] - ymu[r][q]) + musq[r]) + cst) * m;
+        }
+        float *row = out + ((size_t)b * Tx + i) * Ty + j0 + tj;
+        if ((Ty & 3) == 0 && j0 + tj + 3 < Ty) {
+            *reinterpret_cast<float4 *>(row) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (j0 + tj + q < Ty) row[q] = v[q];
+        }
+    }
+}
+
+// Alignment consumers from the row starts (matcha_tts.py:477-478, 504-505): durations
+// dur[b,x] = sum_y attn[b,x,y] (the run length of row x) and col_row[b,y] = the text row of frame y
+// (-1 past t_y), which turns mu_y = attn^T mu_x into a gather.  One block per utterance.
+__global__ __launch_bounds__(256) void mas_runs_kernel(const int32_t *__restrict__ row_start,
+                                                       const int32_t *__restrict__ lengths, int Tx, int Ty,
+                                                       float *__restrict__ dur, int32_t *__restrict__ col_row) {
+    const int b = blockIdx.x;
+    const int t_x = lengths[2 * b], t_y = lengths[2 * b + 1];
+    const int32_t *rs = row_start + (size_t)b * Tx;
+    for (int x = threadIdx.x; x < Tx; x += 256) {
+        const int s = rs[x];
+        int n = 0;
+        if (s >= 0) n = ((x == t_x - 1) ? t_y : rs[x + 1]) - s;
+        if (dur) dur[(size_t)b * Tx + x] = (float)n;
+    }
+    if (!col_row) return;
+    const bool any = t_x >= 1 && rs[0] >= 0;
+    for (int yy = threadIdx.x; yy < Ty; yy += 256) {
+        int row = -1;
+        if (any && yy < t_y) {  // last row whose start <= yy (starts increase along the path)
+            int lo = 0, hi = t_x - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (rs[mid] <= yy) lo = mid; else hi = mid - 1;
+            }
+            row = lo;
+        }
+        col_row[(size_t)b * Ty + yy] = row;
+    }
+}
+
+// mu_y[b,c,y] = mu_x[b,c,col_row[b,y]] (0 where col_row < 0): attn^T mu_x on a one-hot attn is exactly
+// this gather (every other term is 0 * finite).  Backward: dmu_x[b,c,x] = sum over the run of row x
+// of dmu_y[b,c,y], in ascending y (deterministic; no atomics).
+__global__ __launch_bounds__(256) void expand_rows_fwd_kernel(const float *__restrict__ src,
+                                                              const int32_t *__restrict__ col_row, int C, int Tx,
+                                                              int Ty, float *__restrict__ dst) {
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const int b = blockIdx.y;
+    if (idx >= (size_t)C * Ty) return;
+    const int c = (int)(idx / Ty), yy = (int)(idx - (size_t)c * Ty);
+    const int x = col_row[(size_t)b * Ty + yy];
+    dst[((size_t)b * C + c) * Ty + yy] = x >= 0 ? src[((size_t)b * C + c) * Tx + x] : 0.f;
+}
+
+__global__ __launch_bounds__(256) void expand_rows_bwd_kernel(const float *__restrict__ dy,
+                                                              const int32_t *__restrict__ row_start,
+                                                              const int32_t *__restrict__ lengths, int C, int Tx,
+                                                              int Ty, float *__restrict__ dx) {
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const int b = blockIdx.y;
+    if (idx >= (size_t)C * Tx) return;
+    const int c = (int)(idx / Tx), x = (int)(idx - (size_t)c * Tx);
+    const int t_x = lengths[2 * b], t_y = lengths[2 * b + 1];
+    const int32_t *rs = row_start + (size_t)b * Tx;
+    float acc = 0.f;
+    const int s = rs[x];
+    if (s >= 0) {
+        const int e = (x == t_x - 1) ? t_y : rs[x + 1];
+        const float *d = dy + ((size_t)b * C + c) * Ty;
+        for (int yy = s; yy < e; ++yy) acc += d[yy];
+    }
+    dx[((size_t)b * C + c) * Tx + x] = acc;
+}
+
 struct WsLayout {
     size_t lengths, row_start, bits, total;
     int K, Txp, nch;
@@ -419,6 +569,91 @@ extern "C" int mtts_maximum_path_f32(const float *value, const float *mask, floa
     hipLaunchKernelGGL((mas_expand_kernel<float, false>), grid, dim3(256), 0, st, a.row_start,
                        a.lengths, path, Tx, Ty, vec4);
     return mtts::check_launch("mas_expand_kernel");
+}
+
+extern "C" size_t mtts_prior_maximum_path_workspace_size(int32_t B, int32_t Tx, int32_t Ty) {
+    if (B < 0 || Tx < 1 || Ty < 1) return 0;
+    return mtts::align_up(ws_layout(B, Tx, Ty).total, 256) + mtts::align_up((size_t)B * 2 * 4, 256) +
+           (size_t)B * Tx * Ty * 4;
+}
+
+extern "C" int mtts_prior_maximum_path(const float *mu_x, const float *y, const int64_t *x_lengths,
+                                       const int64_t *y_lengths, int32_t B, int32_t C, int32_t Tx, int32_t Ty,
+                                       float *path, int32_t *lengths_out, int32_t *row_start_out, float *dur_out,
+                                       int32_t *col_row_out, float *lattice_out, void *workspace,
+                                       size_t workspace_bytes, void *hip_stream) {
+    int rc = check_shape(B, Tx, Ty);
+    if (rc) return rc;
+    if (B == 0) return MTTS_OK;
+    MTTS_CHECK_ARG(mu_x && y && x_lengths && y_lengths && C >= 1, "prior_maximum_path: null input or C < 1");
+    MTTS_CHECK_ARG(B <= 65535, "prior_maximum_path: B > 65535");
+    const WsLayout w = ws_layout(B, Tx, Ty);
+    if (!workspace || workspace_bytes < mtts_prior_maximum_path_workspace_size(B, Tx, Ty))
+        return mtts::fail(MTTS_ERR_WORKSPACE, "prior_maximum_path: workspace too small");
+    char *ws = static_cast<char *>(workspace);
+    const size_t o_txy = mtts::align_up(w.total, 256), o_lat = o_txy + mtts::align_up((size_t)B * 2 * 4, 256);
+    int32_t *txy = reinterpret_cast<int32_t *>(ws + o_txy);
+    float *lat = lattice_out ? lattice_out : reinterpret_cast<float *>(ws + o_lat);
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+
+    const float cst = (float)(-0.5 * std::log(2.0 * M_PI) * C);  // the Python scalar, rounded as torch does
+    dim3 lg((Ty + kLpT - 1) / kLpT, (Tx + kLpT - 1) / kLpT, B);
+    hipLaunchKernelGGL(log_prior_kernel, lg, dim3(256), 0, st, mu_x, y, x_lengths, y_lengths, C, Tx, Ty, cst, lat, txy);
+    rc = mtts::check_launch("log_prior_kernel");
+    if (rc) return rc;
+
+    MasArgs a{};
+    a.value = lat;
+    a.t_xs = txy;
+    a.t_ys = txy + B;
+    a.lengths = lengths_out ? lengths_out : reinterpret_cast<int32_t *>(ws + w.lengths);
+    a.row_start = row_start_out ? row_start_out : reinterpret_cast<int32_t *>(ws + w.row_start);
+    a.bits = reinterpret_cast<uint32_t *>(ws + w.bits);
+    a.Tx = Tx;
+    a.Ty = Ty;
+    a.Txp = w.Txp;
+    a.nch = w.nch;
+    a.premasked = 1;
+    a.neg = -1e9f;
+    const bool vec = (Ty % 4 == 0) && ((uintptr_t)lat % 16 == 0);
+    rc = launch_dp(a, B, w, vec, false, st);
+    if (rc) return rc;
+    if (path) {
+        dim3 grid((Ty + 1023) / 1024, Tx, B);
+        const int vec4 = (Ty % 4 == 0) && ((uintptr_t)path % 16 == 0);
+        hipLaunchKernelGGL((mas_expand_kernel<float, false>), grid, dim3(256), 0, st, a.row_start, a.lengths, path, Tx,
+                           Ty, vec4);
+        rc = mtts::check_launch("mas_expand_kernel");
+        if (rc) return rc;
+    }
+    if (dur_out || col_row_out) {
+        hipLaunchKernelGGL(mas_runs_kernel, dim3(B), dim3(256), 0, st, a.row_start, a.lengths, Tx, Ty, dur_out,
+                           col_row_out);
+        rc = mtts::check_launch("mas_runs_kernel");
+    }
+    return rc;
+}
+
+extern "C" int mtts_expand_rows_fwd(const float *src, const int32_t *col_row, int32_t B, int32_t C, int32_t Tx,
+                                    int32_t Ty, float *dst, void *hip_stream) {
+    MTTS_CHECK_ARG(src && col_row && dst && B >= 0 && C >= 0 && Tx >= 1 && Ty >= 0 && B <= 65535,
+                   "expand_rows_fwd: bad args");
+    if ((size_t)B * C * Ty == 0) return MTTS_OK;
+    dim3 grid((unsigned)(((size_t)C * Ty + 255) / 256), B);
+    hipLaunchKernelGGL(expand_rows_fwd_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(hip_stream), src, col_row,
+                       C, Tx, Ty, dst);
+    return mtts::check_launch("expand_rows_fwd_kernel");
+}
+
+extern "C" int mtts_expand_rows_bwd(const float *dy, const int32_t *row_start, const int32_t *lengths, int32_t B,
+                                    int32_t C, int32_t Tx, int32_t Ty, float *dx, void *hip_stream) {
+    MTTS_CHECK_ARG(dy && row_start && lengths && dx && B >= 0 && C >= 0 && Tx >= 1 && Ty >= 1 && B <= 65535,
+                   "expand_rows_bwd: bad args");
+    if ((size_t)B * C * Tx == 0) return MTTS_OK;
+    dim3 grid((unsigned)(((size_t)C * Tx + 255) / 256), B);
+    hipLaunchKernelGGL(expand_rows_bwd_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(hip_stream), dy, row_start,
+                       lengths, C, Tx, Ty, dx);
+    return mtts::check_launch("expand_rows_bwd_kernel");
 }
 
 extern "C" int mtts_compute_batch_alignments(int32_t *paths, float *values, const int32_t *t_xs,

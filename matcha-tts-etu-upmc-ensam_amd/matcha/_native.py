@@ -32,6 +32,11 @@ _SIGNATURES: dict[str, tuple] = {
     "mtts_last_error": (ctypes.c_char_p, []),
     "mtts_maximum_path_workspace_size": (_SZ, [_I32, _I32, _I32]),
     "mtts_maximum_path_f32": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _SZ, _P]),
+    "mtts_prior_maximum_path_workspace_size": (_SZ, [_I32, _I32, _I32]),
+    "mtts_prior_maximum_path": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P,
+                                               _SZ, _P]),
+    "mtts_expand_rows_fwd": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _P, _P]),
+    "mtts_expand_rows_bwd": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, _I32, _P, _P]),
     "mtts_compute_batch_alignments": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _SZ, _P]),
 }
 

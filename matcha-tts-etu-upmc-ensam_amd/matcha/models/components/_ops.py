@@ -95,6 +95,8 @@ _P, _I, _F, _SZ, _U = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float, ctypes.c_
 _I64 = ctypes.c_int64
 N.register("mtts_conv_gemm", ctypes.c_int, [ctypes.POINTER(ConvGemmArgs), _I, _P])
 N.register("mtts_conv_gemm_tile", ctypes.c_int, [ctypes.POINTER(ConvGemmArgs), _I, _I, _P])
+N.register("mtts_conv_gemm_workspace_size", _SZ, [ctypes.POINTER(ConvGemmArgs), _I, _I, _I])
+N.register("mtts_conv_gemm_ws", ctypes.c_int, [ctypes.POINTER(ConvGemmArgs), _I, _I, _I, _P, _SZ, _P])
 N.register("mtts_conv_wgrad_workspace_size", _SZ, [ctypes.POINTER(ConvWgradArgs)])
 N.register("mtts_conv_wgrad", ctypes.c_int,
            [ctypes.POINTER(ConvWgradArgs), _I, _P, _I64, _I64, _I64, _P, _I, _P, _SZ, _P])
@@ -137,9 +139,22 @@ def _f32c(t: torch.Tensor | None) -> torch.Tensor | None:
     return t.contiguous()
 
 
+_SEED_SCOPE: contextvars.ContextVar = contextvars.ContextVar("mtts_seed_scope", default=None)
+
+
 def _new_seed(device) -> torch.Tensor:
     """Two random words drawn ON THE DEVICE from torch's generator: no host sync, and a captured
-    HIP graph draws fresh dropout masks on every replay (torch's graph-safe philox offsets)."""
+    HIP graph draws fresh dropout masks on every replay (torch's graph-safe philox offsets).  Inside
+    a weight_pack_scope the words are slices of ONE pool drawn when the scope opens (sized by the
+    owner's previous forward): one generator launch per module forward instead of one per dropout."""
+    st = _SEED_SCOPE.get()
+    if st is not None:
+        st["used"] += 1
+        pool = st["pool"]
+        if pool is not None and pool.device == torch.device(device) and st["i"] + 2 <= pool.numel():
+            i = st["i"]
+            st["i"] = i + 2
+            return pool[i:i + 2]
     return torch.randint(0, 2 ** 31 - 1, (2,), device=device, dtype=torch.int32)
 
 
@@ -258,10 +273,18 @@ def weight_pack_scope(owner: torch.nn.Module):
         for sp, t in zip(specs, _run_pack(specs, prec)):
             cache[(prec,) + sp.key] = t
     tok = _PACK_SCOPE.set((plan, cache, prec))
+    nseed = owner.__dict__.get("_mtts_seed_count", 0)
+    dev = next(owner.parameters()).device
+    pool = (torch.randint(0, 2 ** 31 - 1, (2 * nseed,), device=dev, dtype=torch.int32)
+            if nseed and dev.type == "cuda" else None)
+    seeds = {"pool": pool, "i": 0, "used": 0}
+    stok = _SEED_SCOPE.set(seeds)
     try:
         yield
     finally:
+        _SEED_SCOPE.reset(stok)
         _PACK_SCOPE.reset(tok)
+        owner.__dict__["_mtts_seed_count"] = seeds["used"]
 
 
 def packed(spec: PackSpec, prec: int) -> tuple[torch.Tensor, int]:
@@ -288,7 +311,7 @@ LAUNCH_LOG: list | None = None
 
 def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_stride=1, out_off=0, *, prec,
           a_scale=None, bias=None, act=ACT_NONE, residual=None, c_scale=None, C_pre=None, aux=None,
-          dropout_p=0.0, seed=None, tile_cfg=-1, binary_scale=True):
+          dropout_p=0.0, seed=None, tile_cfg=-1, binary_scale=True, splits=0):
     """One mtts_conv_gemm launch.  Every row scale the model passes (a_scale) is a sequence mask
     (matcha.utils.model.sequence_mask: 0/1 by construction, as the reference's x * mask), so
     ``binary_scale`` defaults to True: the bf16 LDS-DMA schedule then reads masked rows as zeros
@@ -312,7 +335,11 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
         st = torch.cuda.current_stream(C.device)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
-    N.check(N.lib().mtts_conv_gemm_tile(ctypes.byref(args), prec, tile_cfg, _stream(C)), "mtts_conv_gemm")
+    lib = N.lib()
+    nws = int(lib.mtts_conv_gemm_workspace_size(ctypes.byref(args), prec, tile_cfg, splits))
+    ws = torch.empty(nws, dtype=torch.uint8, device=C.device) if nws else None
+    N.check(lib.mtts_conv_gemm_ws(ctypes.byref(args), prec, tile_cfg, splits, N.ptr(ws), nws, _stream(C)),
+            "mtts_conv_gemm")
     if log is not None:
         e1.record(st)
         M_ = nb * To

@@ -87,7 +87,8 @@ class Resnet1D(nn.Module):
             tproj = self.mlp(time_emb.float())
         h = self.block1.forward_tm(x, mask, add=tproj)
         h = self.block2.forward_tm(h, mask)
-        return O.conv_tm(x, self.res_conv.weight, self.res_conv.bias, mask, padding=0) + h
+        # res_conv(x*m) + h with the add in the GEMM epilogue ((acc + bias) + h, torch's order)
+        return O.conv_tm(x, self.res_conv.weight, self.res_conv.bias, mask, padding=0, residual=h)
 
     def forward(self, x, mask, time_emb):
         return self.forward_tm(x.transpose(1, 2), mask[:, 0], time_emb).transpose(1, 2)

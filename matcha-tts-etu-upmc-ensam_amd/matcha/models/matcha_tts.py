@@ -97,14 +97,19 @@ class MatchaTTS(BaseLightningClass):
         mu_x, logw, x_mask = self.encoder(x, x_lengths)
         y_max_length = y.shape[-1]
         y_mask = sequence_mask(y_lengths, y_max_length).unsqueeze(1).to(x_mask)
-        attn_mask = x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)
+        runs = None
         if self.use_precomputed_durations:
+            attn_mask = x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)
             attn = generate_path(durations.squeeze(1), attn_mask.squeeze(1))
+            dur = torch.sum(attn, -1)
         else:
+            # :461-478 fused on the GPU: lattice (log_prior) * attn_mask -> maximum_path -> sum(attn, -1),
+            # with the attention mask taken from the lengths (never materialised)
             with torch.no_grad():
-                lp = self.log_prior(mu_x.detach(), y)
-                attn = monotonic_align.maximum_path(lp, attn_mask.squeeze(1)).detach()
-        logw_ = torch.log(1e-8 + torch.sum(attn.unsqueeze(1), -1)) * x_mask
+                attn, dur, col_row, row_start, lens = monotonic_align.prior_maximum_path(mu_x, y, x_lengths,
+                                                                                          y_lengths)
+            runs = (col_row, row_start, lens)
+        logw_ = torch.log(1e-8 + dur.unsqueeze(1)) * x_mask
         dur_loss = duration_loss(logw, logw_, x_lengths)
         if out_size is not None:  # :480-502 (host-side random crop, as the reference)
             max_offset = (y_lengths - out_size).clamp(0)
@@ -122,7 +127,11 @@ class MatchaTTS(BaseLightningClass):
             y_cut_lengths = torch.LongTensor(y_cut_lengths)
             y_mask = sequence_mask(y_cut_lengths).unsqueeze(1).to(y_mask)
             attn, y = attn_cut, y_cut
-        mu_y = torch.matmul(attn.squeeze(1).transpose(1, 2), mu_x.transpose(1, 2)).transpose(1, 2)
+            runs = None
+        if runs is not None:  # attn^T @ mu_x on the one-hot attn == a gather (bitwise), segment-sum backward
+            mu_y = monotonic_align.expand_rows(mu_x, *runs)
+        else:
+            mu_y = torch.matmul(attn.squeeze(1).transpose(1, 2), mu_x.transpose(1, 2)).transpose(1, 2)
         diff_loss, _ = self.decoder.compute_loss(x1=y, mask=y_mask, mu=mu_y, cond=cond, t=t, z=z)
         if self.prior_loss:
             prior_loss = torch.sum(0.5 * ((y - mu_y) ** 2 + math.log(2 * math.pi)) * y_mask)

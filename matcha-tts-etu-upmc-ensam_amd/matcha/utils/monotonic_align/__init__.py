@@ -87,3 +87,76 @@ def maximum_path_c(paths: torch.Tensor, values: torch.Tensor, t_xs: torch.Tensor
 
 # the reference binds the compiled core as maximum_path_c (__init__.py:4-5)
 compute_batch_alignments = maximum_path_c
+
+
+def prior_maximum_path(mu_x: torch.Tensor, y: torch.Tensor, x_lengths: torch.Tensor, y_lengths: torch.Tensor, *,
+                       return_lattice: bool = False):
+    """The training forward's alignment step fused (matcha_tts.py:461-478, MatchaTTS.forward):
+    log-prior lattice from mu_x [B,C,Tx] and y [B,C,Ty] (fp32), masked by the length masks, Viterbi
+    max path, and the duration target -- one lattice write to HBM instead of two bmm's, their
+    elementwise tail, the [B,Tx,Ty] attention mask and a reduction over the dense path
+    (csrc/mas.hip: log_prior_kernel -> mas_dp_kernel -> mas_expand_kernel / mas_runs_kernel).
+
+    Returns (attn [B,Tx,Ty] fp32, dur [B,Tx] fp32 = attn.sum(-1), col_row [B,Ty] int32 = text row of
+    each frame (-1 past t_y), row_start [B,Tx] int32, lengths [B,2] int32) and, with
+    ``return_lattice``, the masked fp32 lattice [B,Tx,Ty] the DP ran on.  No gradient."""
+    N.require_device(mu_x, y, x_lengths, y_lengths)
+    if mu_x.dim() != 3 or y.dim() != 3 or mu_x.shape[:2] != y.shape[:2]:
+        raise ValueError(f"prior_maximum_path expects mu_x [B,C,Tx] and y [B,C,Ty], got {tuple(mu_x.shape)}, "
+                         f"{tuple(y.shape)}")
+    mu_x = mu_x.detach().to(torch.float32).contiguous()
+    y = y.detach().to(torch.float32).contiguous()
+    xl = x_lengths.detach().to(torch.int64).contiguous()
+    yl = y_lengths.detach().to(torch.int64).contiguous()
+    B, C, Tx = mu_x.shape
+    Ty = y.shape[2]
+    dev = mu_x.device
+    attn = torch.empty((B, Tx, Ty), dtype=torch.float32, device=dev)
+    dur = torch.empty((B, Tx), dtype=torch.float32, device=dev)
+    col_row = torch.empty((B, Ty), dtype=torch.int32, device=dev)
+    row_start = torch.empty((B, Tx), dtype=torch.int32, device=dev)
+    lengths = torch.empty((B, 2), dtype=torch.int32, device=dev)
+    lattice = torch.empty((B, Tx, Ty), dtype=torch.float32, device=dev) if return_lattice else None
+    ws = torch.empty(max(int(N.lib().mtts_prior_maximum_path_workspace_size(B, Tx, Ty)), 1), dtype=torch.uint8,
+                     device=dev)
+    with torch.cuda.device(dev):
+        rc = N.lib().mtts_prior_maximum_path(
+            N.ptr(mu_x), N.ptr(y), N.ptr(xl), N.ptr(yl), B, C, Tx, Ty, N.ptr(attn), N.ptr(lengths), N.ptr(row_start),
+            N.ptr(dur), N.ptr(col_row), N.ptr(lattice), N.ptr(ws), ws.numel(), N.stream_handle(dev))
+    N.check(rc, "mtts_prior_maximum_path")
+    out = (attn, dur, col_row, row_start, lengths)
+    return out + (lattice,) if return_lattice else out
+
+
+class _ExpandRows(torch.autograd.Function):
+    """mu_y = attn^T @ mu_x for a hard alignment (matcha_tts.py:504-505) as a gather of mu_x columns;
+    backward sums each text row's run of frames (deterministic segment sums, no atomics)."""
+
+    @staticmethod
+    def forward(ctx, mu_x, col_row, row_start, lengths):
+        mu_x = mu_x.to(torch.float32).contiguous()
+        B, C, Tx = mu_x.shape
+        Ty = col_row.shape[1]
+        out = torch.empty((B, C, Ty), dtype=torch.float32, device=mu_x.device)
+        N.check(N.lib().mtts_expand_rows_fwd(N.ptr(mu_x), N.ptr(col_row), B, C, Tx, Ty, N.ptr(out),
+                                             N.stream_handle(mu_x.device)), "mtts_expand_rows_fwd")
+        ctx.save_for_backward(row_start, lengths)
+        ctx.shape = (B, C, Tx, Ty)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        row_start, lengths = ctx.saved_tensors
+        B, C, Tx, Ty = ctx.shape
+        dy = dy.to(torch.float32).contiguous()
+        dx = torch.empty((B, C, Tx), dtype=torch.float32, device=dy.device)
+        N.check(N.lib().mtts_expand_rows_bwd(N.ptr(dy), N.ptr(row_start), N.ptr(lengths), B, C, Tx, Ty, N.ptr(dx),
+                                             N.stream_handle(dy.device)), "mtts_expand_rows_bwd")
+        return dx, None, None, None
+
+
+def expand_rows(mu_x: torch.Tensor, col_row: torch.Tensor, row_start: torch.Tensor, lengths: torch.Tensor):
+    """[B,C,Tx] -> [B,C,Ty]: attn^T @ mu_x for the alignment prior_maximum_path returned (bitwise
+    equal to the bmm on the one-hot attn: every other term is 0 * finite)."""
+    N.require_device(mu_x, col_row, row_start, lengths)
+    return _ExpandRows.apply(mu_x, col_row, row_start, lengths)

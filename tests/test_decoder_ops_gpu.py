@@ -233,7 +233,7 @@ def test_wgrad_bf16_exact_and_deterministic(B, T, Cin, Cout, k, rows_per_step, t
 
 
 @pytest.mark.parametrize("B,T,Cin,Cout,k", BIG)
-@pytest.mark.parametrize("cfg", [-1, 7, 12])
+@pytest.mark.parametrize("cfg", [-1, 7, 12, 41, 42, 44])
 def test_gemm_bf16_exact_and_deterministic(B, T, Cin, Cout, k, cfg):
     from matcha.models.components import _ops as O
 
@@ -252,3 +252,37 @@ def test_gemm_bf16_exact_and_deterministic(B, T, Cin, Cout, k, cfg):
     assert (outs[0].double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
     for y2 in outs[1:]:
         assert torch.equal(outs[0], y2)
+
+
+@pytest.mark.parametrize("cfg,splits", [(41, 1), (42, 3), (44, 1), (44, 4), (-1, 0)])
+@pytest.mark.parametrize("act,pre", [(0, False), (1, True)])
+def test_gemm_lds_dma_split_k_epilogue(cfg, splits, act, pre):
+    """LDS-DMA schedules (incl. split-K + combine pass) against the register-staged config 7 on the
+    whole epilogue: ragged 0/1 row mask (masked rows DMA'd from the zero chunk), bias, GELU with the
+    pre-activation store, dropout, residual, output row scale and a stride-2 output phase."""
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator(device="cpu").manual_seed(7 + splits + act)
+    B, T, Cin, Cout = 5, 77, 256, 320
+    x = torch.randn(B, T, Cin, generator=g).to(DEV)
+    msk = (torch.rand(B * T, generator=g) > 0.2).float().to(DEV)
+    w = (torch.randn(Cout, Cin * 3, generator=g) / math.sqrt(Cin * 3)).to(DEV)
+    Wp, Kp = O.pack_weight(w, O.PREC_BF16)
+    bias = torch.randn(Cout, generator=g).to(DEV)
+    res = torch.randn(B, 2 * T, Cout, generator=g).to(DEV)
+    cs = torch.rand(B * 2 * T, generator=g).to(DEV)
+    seed = torch.tensor([12345, 678], dtype=torch.int32, device=DEV)
+    outs = []
+    for c, sp in [(7, 1), (cfg, splits)]:
+        y = torch.zeros(B, 2 * T, Cout, device=DEV)
+        yp = torch.zeros(B, 2 * T, Cout, device=DEV) if pre else None
+        O._gemm(x, T, T, B, 1, [-1, 0, 1], Cin, Wp, Kp, Cout, y, 2 * T, 2, 1, prec=O.PREC_BF16, a_scale=msk,
+                bias=bias, act=act, residual=res, c_scale=cs, C_pre=yp, dropout_p=0.1, seed=seed, tile_cfg=c,
+                splits=sp)
+        outs.append((y, yp))
+    torch.cuda.synchronize()
+    (y0, p0), (y1, p1) = outs
+    assert (y1[:, 0::2] == 0).all()  # the other output phase is untouched
+    assert rel(y1, y0) < 1e-5, rel(y1, y0)
+    if pre:
+        assert rel(p1, p0) < 1e-5, rel(p1, p0)

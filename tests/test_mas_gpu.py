@@ -181,3 +181,75 @@ def test_no_host_sync_and_stream_ordering():
         p = maximum_path(v, m)
     s.synchronize()
     np.testing.assert_array_equal(p.cpu().numpy(), exp)
+
+
+# ---------------------------------------------------------------- fused prior lattice + MAS
+@pytest.mark.parametrize("B,C,Tx,Ty", [(4, 80, 13, 37), (3, 80, 64, 65), (2, 80, 200, 1000), (32, 80, 120, 600),
+                                       (2, 16, 1, 5), (3, 80, 300, 301)])
+def test_prior_maximum_path_vs_oracle(B, C, Tx, Ty):
+    """mtts_prior_maximum_path: the masked lattice is bit-identical to the numpy restatement of
+    matcha_tts.py:467-472 (oracle/prior_oracle.py), the path bit-identical to the CPU oracle's
+    maximum_path on that lattice, durations == path.sum(-1), col_row == the path's row per frame."""
+    from matcha.utils.monotonic_align import prior_maximum_path
+    from oracle import prior_oracle as PO
+
+    rng = np.random.default_rng(B * 1000 + Tx + Ty)
+    mu = rng.normal(0.0, 1.0, size=(B, C, Tx)).astype(np.float32)
+    y = rng.normal(0.0, 1.0, size=(B, C, Ty)).astype(np.float32)
+    xl = rng.integers(max(1, Tx // 2), Tx + 1, size=B).astype(np.int64)
+    yl = np.maximum(rng.integers(max(1, Ty // 2), Ty + 1, size=B), xl).astype(np.int64)
+    xl[0], yl[0] = Tx, Ty
+    d = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    attn, dur, col_row, rs, lens, lat = prior_maximum_path(d(mu), d(y), d(xl), d(yl), return_lattice=True)
+    torch.cuda.synchronize()
+    exp_lat, mask = PO.log_prior_lattice(mu, y, xl, yl)
+    np.testing.assert_array_equal(lat.cpu().numpy().view(np.uint32), exp_lat.view(np.uint32))
+    exp_path, exp_t = O.maximum_path(exp_lat, mask)
+    np.testing.assert_array_equal(attn.cpu().numpy(), exp_path)
+    np.testing.assert_array_equal(lens.cpu().numpy(), exp_t)
+    np.testing.assert_array_equal(dur.cpu().numpy(), PO.durations(exp_path))
+    np.testing.assert_array_equal(col_row.cpu().numpy(), PO.col_row(exp_path))
+
+
+def test_prior_lattice_matches_torch_formula():
+    """Against the reference's own formula (matcha_tts.py:467-472 in float64): fp32 rounding only."""
+    from matcha.utils.monotonic_align import prior_maximum_path
+
+    g = torch.Generator().manual_seed(5)
+    B, C, Tx, Ty = 4, 80, 50, 211
+    mu = torch.randn(B, C, Tx, generator=g)
+    y = torch.randn(B, C, Ty, generator=g)
+    xl = torch.tensor([50, 31, 17, 50])
+    yl = torch.tensor([211, 150, 99, 60])
+    *_, lat = prior_maximum_path(mu.to(DEV), y.to(DEV), xl.to(DEV), yl.to(DEV), return_lattice=True)
+    m, yy = mu.double(), y.double()
+    factor = -0.5 * torch.ones_like(m)
+    ref = (torch.matmul(factor.transpose(1, 2), yy ** 2) - torch.matmul(2.0 * (factor * m).transpose(1, 2), yy)
+           + torch.sum(factor * m ** 2, 1).unsqueeze(-1) - 0.5 * np.log(2 * np.pi) * C)
+    am = ((torch.arange(Tx)[None, :, None] < xl[:, None, None]) & (torch.arange(Ty)[None, None, :] < yl[:, None, None]))
+    ref = ref * am
+    err = (lat.cpu().double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-6, err
+
+
+def test_expand_rows_matches_bmm_and_its_gradient():
+    """mu_y = attn^T @ mu_x as a gather: forward bitwise equal to the bmm on the one-hot attn;
+    backward (segment sums) equal to the bmm's gradient in float64 to fp32 rounding."""
+    from matcha.utils.monotonic_align import expand_rows, prior_maximum_path
+
+    g = torch.Generator().manual_seed(9)
+    B, C, Tx, Ty = 5, 80, 40, 173
+    mu = torch.randn(B, C, Tx, generator=g).to(DEV)
+    y = torch.randn(B, C, Ty, generator=g).to(DEV)
+    xl = torch.tensor([40, 33, 1, 20, 39], device=DEV)
+    yl = torch.tensor([173, 100, 7, 20, 140], device=DEV)
+    attn, dur, col_row, rs, lens = prior_maximum_path(mu, y, xl, yl)
+    a = mu.clone().requires_grad_(True)
+    out = expand_rows(a, col_row, rs, lens)
+    ref = torch.matmul(attn.transpose(1, 2), mu.transpose(1, 2)).transpose(1, 2)
+    assert torch.equal(out, ref)
+    gy = torch.randn(B, C, Ty, generator=g).to(DEV)
+    (out * gy).sum().backward()
+    gref = torch.matmul(gy.double(), attn.double().transpose(1, 2))
+    err = (a.grad.double() - gref).abs().max().item() / gref.abs().max().item()
+    assert err < 1e-6, err
