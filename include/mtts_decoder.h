@@ -229,6 +229,28 @@ int mtts_attention_bwd(const mtts_attn_args *args, const mtts_attn_grads *grads,
 int mtts_rope_qk(const float *x, float *y, int32_t rows, int32_t T, int32_t C, int32_t H, int32_t rope_dims,
                  const float *cos_t, const float *sin_t, int32_t inverse, void *hip_stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Optimizer step: gradient-norm clipping + AdamW (train.py gradient_clip_val=1.0 ->
+ * torch.nn.utils.clip_grad_norm_; baselightningmodule.py:59-65 torch.optim.AdamW) over a flat fp32
+ * parameter array and its two flat moment arrays.  Gradients are read through a chunk table: chunk i
+ * covers grad[0 .. n) at flat offset `offset` (n <= 65536 recommended: one 256-thread block each).
+ *   coef = min(max_norm / (||g||_2 + 1e-6), 1) (max_norm <= 0: no clipping); t = *step + 1;
+ *   p *= 1 - lr*wd; m += (1-b1)(g*coef - m); v = b2 v + (1-b2)(g*coef)^2;
+ *   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps);  *step = t.
+ * lr and step are device scalars (graph-replay safe); the norm is reduced in a fixed order.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct mtts_adamw_chunk {
+    const float *grad;
+    int64_t offset;
+    int32_t n;
+    int32_t pad_;
+} mtts_adamw_chunk;
+
+size_t mtts_clip_adamw_workspace_size(int32_t nchunks);
+int mtts_clip_adamw(const mtts_adamw_chunk *chunks, int32_t nchunks, float *params, float *exp_avg,
+                    float *exp_avg_sq, const float *lr, float *step, float max_norm, float beta1, float beta2,
+                    float eps, float weight_decay, void *workspace, size_t workspace_bytes, void *hip_stream);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -357,6 +357,7 @@ __global__ __launch_bounds__(256) void log_prior_kernel(const float *__restrict_
         }
         __syncthreads();
         const int cn = min(kLpC, C - c0);
+#pragma unroll 4
         for (int c = 0; c < cn; ++c) {
             const float4 m4 = *reinterpret_cast<const float4 *>(&smu[c][ti]);
             const float4 y4 = *reinterpret_cast<const float4 *>(&sy[c][tj]);
@@ -438,24 +439,40 @@ __global__ __launch_bounds__(256) void expand_rows_fwd_kernel(const float *__res
     dst[((size_t)b * C + c) * Ty + yy] = x >= 0 ? src[((size_t)b * C + c) * Tx + x] : 0.f;
 }
 
+// one block per (utterance, 8 channels): the channels' dy rows are staged in LDS with coalesced
+// loads, then thread (channel, row x) sums its run from LDS -- a per-thread loop over global memory
+// serialised one HBM latency per frame (31 us at the bench shape)
+constexpr int kErC = 8;
+constexpr int kErMaxTy = 2048;
 __global__ __launch_bounds__(256) void expand_rows_bwd_kernel(const float *__restrict__ dy,
                                                               const int32_t *__restrict__ row_start,
                                                               const int32_t *__restrict__ lengths, int C, int Tx,
                                                               int Ty, float *__restrict__ dx) {
-    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
-    const int b = blockIdx.y;
-    if (idx >= (size_t)C * Tx) return;
-    const int c = (int)(idx / Tx), x = (int)(idx - (size_t)c * Tx);
+    __shared__ float sdy[kErC * kErMaxTy];
+    const int b = blockIdx.y, c0 = blockIdx.x * kErC;
+    const int nc = min(kErC, C - c0);
     const int t_x = lengths[2 * b], t_y = lengths[2 * b + 1];
     const int32_t *rs = row_start + (size_t)b * Tx;
-    float acc = 0.f;
-    const int s = rs[x];
-    if (s >= 0) {
-        const int e = (x == t_x - 1) ? t_y : rs[x + 1];
-        const float *d = dy + ((size_t)b * C + c) * Ty;
-        for (int yy = s; yy < e; ++yy) acc += d[yy];
+    for (int ty0 = 0; ty0 < Ty; ty0 += kErMaxTy) {  // frame slabs (one slab for Ty <= 2048)
+        const int tn = min(kErMaxTy, Ty - ty0);
+        __syncthreads();
+        for (int e = threadIdx.x; e < nc * tn; e += 256) {
+            const int c = e / tn, yy = e - c * tn;
+            sdy[c * kErMaxTy + yy] = dy[((size_t)b * C + c0 + c) * Ty + ty0 + yy];
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < nc * Tx; e += 256) {
+            const int c = e / Tx, x = e - c * Tx;
+            const int s = rs[x];
+            float acc = ty0 == 0 ? 0.f : dx[((size_t)b * C + c0 + c) * Tx + x];
+            if (s >= 0) {
+                const int en = (x == t_x - 1) ? t_y : rs[x + 1];
+                const int lo = max(s, ty0) - ty0, hi = min(en, ty0 + tn) - ty0;
+                for (int yy = lo; yy < hi; ++yy) acc += sdy[c * kErMaxTy + yy];
+            }
+            dx[((size_t)b * C + c0 + c) * Tx + x] = acc;
+        }
     }
-    dx[((size_t)b * C + c) * Tx + x] = acc;
 }
 
 struct WsLayout {
@@ -650,7 +667,7 @@ extern "C" int mtts_expand_rows_bwd(const float *dy, const int32_t *row_start, c
     MTTS_CHECK_ARG(dy && row_start && lengths && dx && B >= 0 && C >= 0 && Tx >= 1 && Ty >= 1 && B <= 65535,
                    "expand_rows_bwd: bad args");
     if ((size_t)B * C * Tx == 0) return MTTS_OK;
-    dim3 grid((unsigned)(((size_t)C * Tx + 255) / 256), B);
+    dim3 grid((unsigned)((C + kErC - 1) / kErC), B);
     hipLaunchKernelGGL(expand_rows_bwd_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(hip_stream), dy, row_start,
                        lengths, C, Tx, Ty, dx);
     return mtts::check_launch("expand_rows_bwd_kernel");

@@ -26,12 +26,14 @@ with element 0 = max, mels ~ N(0, 1) zeroed past the length.
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import math
 from dataclasses import dataclass
 
 import torch
 import torch.distributed as dist
 
+from matcha import _native as N
 from matcha.models.matcha_tts import MatchaTTS
 
 
@@ -49,6 +51,101 @@ def synthetic_batch(B: int, Tx: int, Ty: int, n_feats: int = 80, seed: int = 0, 
     x = x * (pos_x < x_lengths[:, None])
     y = y * (pos_y < y_lengths[:, None, None])
     return {k: v.to(device) for k, v in dict(x=x, x_lengths=x_lengths, y=y, y_lengths=y_lengths).items()}
+
+
+class _AdamWChunk(ctypes.Structure):  # include/mtts_decoder.h mtts_adamw_chunk
+    _fields_ = [("grad", ctypes.c_void_p), ("offset", ctypes.c_int64), ("n", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
+class _FlatClipAdamW:
+    """clip_grad_norm_(max_norm) + AdamW(lr, (0.9, 0.999), eps 1e-8, wd 1e-6) -- the reference step's
+    optimizer (baselightningmodule.py:59-65, train.py gradient_clip_val) -- as mtts_clip_adamw over a
+    flat parameter array.  lr is a device scalar (the cosine schedule writes it); the step count lives
+    on the device; the gradient table is rebuilt whenever the gradient tensors change (eager calls)
+    and frozen by bind_grads() for graph capture."""
+
+    CHUNK = 32768
+
+    def __init__(self, params, lr: torch.Tensor, max_norm: float, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-6):
+        self.params = list(params)
+        dev = self.params[0].device
+        offs, off = [], 0
+        for p in self.params:
+            offs.append(off)
+            off += (p.numel() + 3) // 4 * 4
+        self.flat = torch.zeros(off, device=dev, dtype=torch.float32)
+        with torch.no_grad():
+            for p, o in zip(self.params, offs):
+                self.flat[o:o + p.numel()].copy_(p.detach().reshape(-1))
+                p.data = self.flat[o:o + p.numel()].view_as(p)
+        self.offsets = offs
+        self.exp_avg = torch.zeros_like(self.flat)
+        self.exp_avg_sq = torch.zeros_like(self.flat)
+        self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)
+        self.lr, self.max_norm = lr, float(max_norm or 0.0)
+        self.betas, self.eps, self.wd = betas, eps, weight_decay
+        self._table = None
+        self._key = None
+        self._ws = None
+        self.state = {}  # (torch.optim API surface used by callers)
+
+    def _build(self):
+        key = tuple((p.grad.data_ptr() if p.grad is not None else 0) for p in self.params)
+        if key == self._key:
+            return
+        rows = []
+        for p, o in zip(self.params, self.offsets):
+            g = p.grad
+            if g is None:
+                continue
+            if g.dtype != torch.float32 or not g.is_contiguous():
+                raise RuntimeError("fused AdamW expects contiguous fp32 gradients")
+            n = g.numel()
+            for s in range(0, n, self.CHUNK):
+                rows.append((g.data_ptr() + 4 * s, o + s, min(self.CHUNK, n - s)))
+        arr = (_AdamWChunk * max(len(rows), 1))()
+        for i, (gp, o, n) in enumerate(rows):
+            arr[i].grad, arr[i].offset, arr[i].n = gp, o, n
+        host = torch.frombuffer(bytearray(arr), dtype=torch.uint8)
+        self._table = host.to(self.flat.device)
+        self._n = len(rows)
+        nws = int(N.lib().mtts_clip_adamw_workspace_size(self._n))
+        self._ws = torch.empty(max(nws, 4), dtype=torch.uint8, device=self.flat.device)
+        self._key = key
+
+    def bind_grads(self):
+        self._key = None
+        self._build()
+
+    def step(self):
+        if torch.cuda.is_current_stream_capturing():
+            if self._table is None:
+                raise RuntimeError("bind_grads() before capturing the optimizer step")
+        else:
+            self._build()
+        b1, b2 = self.betas
+        N.check(N.lib().mtts_clip_adamw(N.ptr(self._table), self._n, N.ptr(self.flat), N.ptr(self.exp_avg),
+                                        N.ptr(self.exp_avg_sq), N.ptr(self.lr), N.ptr(self.step_t), self.max_norm,
+                                        b1, b2, self.eps, self.wd, N.ptr(self._ws), self._ws.numel(),
+                                        torch.cuda.current_stream(self.flat.device).cuda_stream), "mtts_clip_adamw")
+
+    def state_snapshot(self):
+        return [t.clone() for t in (self.exp_avg, self.exp_avg_sq, self.step_t)]
+
+    def state_restore(self, snap):
+        for t, s_ in zip((self.exp_avg, self.exp_avg_sq, self.step_t), snap):
+            t.copy_(s_)
+
+    def zero_grad(self, set_to_none: bool = True):
+        for p in self.params:
+            p.grad = None
+
+
+N.register("mtts_clip_adamw_workspace_size", ctypes.c_size_t, [ctypes.c_int32])
+N.register("mtts_clip_adamw", ctypes.c_int,
+           [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p])
 
 
 @dataclass
@@ -81,8 +178,10 @@ class Trainer:
             for p in self.params:
                 p.grad = None
             self.lr = torch.tensor(cfg.lr, device=self.dev)
-            self.optimizer = torch.optim.AdamW(self.params, lr=self.lr, betas=(0.9, 0.999), weight_decay=1e-6,
-                                               fused=True, capturable=True)
+            # clip + AdamW as two HIP launches (csrc/optim.hip) over one flat fp32 parameter array:
+            # the parameters become views into it (names / state_dict unchanged), each region
+            # 16-byte aligned; the moments are flat arrays of the same layout
+            self.optimizer = _FlatClipAdamW(self.params, self.lr, cfg.gradient_clip_val)
             self.scheduler = None
             self._g_fb = self._g_opt = None
             self._static = None
@@ -120,6 +219,9 @@ class Trainer:
         return logged / n
 
     def _clip_and_update(self):
+        if isinstance(self.optimizer, _FlatClipAdamW):  # graph mode: clipping is inside the fused step
+            self.optimizer.step()
+            return
         if self.cfg.gradient_clip_val:
             torch.nn.utils.clip_grad_norm_(self.params, self.cfg.gradient_clip_val, foreach=True)
         self.optimizer.step()
@@ -145,8 +247,7 @@ class Trainer:
         self._static = [{k: v.clone() for k, v in b.items()} for b in batches]
         # warm-up (allocator pools, lazy library loads, optimizer state) must not leave updates behind
         saved = [p.detach().clone() for p in self.params]
-        saved_state = {id(p): {k: v.clone() for k, v in st.items() if torch.is_tensor(v)}
-                       for p, st in self.optimizer.state.items()}
+        saved_state = self.optimizer.state_snapshot()
         side = torch.cuda.Stream(self.dev)
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):
@@ -160,11 +261,7 @@ class Trainer:
         with torch.no_grad():
             for p, s_ in zip(self.params, saved):
                 p.copy_(s_)
-            for p, st in self.optimizer.state.items():  # moments / step back to their pre-warm-up values
-                prev = saved_state.get(id(p), {})
-                for k, v in st.items():
-                    if torch.is_tensor(v):
-                        v.copy_(prev[k]) if k in prev else v.zero_()
+            self.optimizer.state_restore(saved_state)  # moments / step back to their pre-warm-up values
 
         if self.world > 1:
             self.flat = torch.zeros(sum(p.numel() for p in gparams), device=self.dev, dtype=torch.float32)
@@ -173,19 +270,19 @@ class Trainer:
             for p in self.params:
                 p.grad = None  # autograd hands over each fresh gradient: no accumulate kernels
             self._logged = self._fwd_bwd(self._static)
-            if self.world == 1:
-                self._clip_and_update()
-            else:
+            if self.world > 1:
                 torch.cat([p.grad.reshape(-1) for p in gparams], out=self.flat)
+        self._fb_grads = [p.grad for p in gparams]  # graph-pool outputs, kept alive with the graph
         if self.world > 1:
-            self._fb_grads = [p.grad for p in gparams]  # graph-pool outputs, kept alive with the graph
             off = 0
             for p in gparams:  # the optimizer graph reads the all-reduced flat buffer
                 p.grad = self.flat[off:off + p.numel()].view_as(p)
                 off += p.numel()
-            self._g_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_opt, pool=self._g_fb.pool()):
-                self._clip_and_update()
+        # the optimizer graph: its gradient table points at the (fixed) graph-pool gradients
+        self.optimizer.bind_grads()
+        self._g_opt = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g_opt, pool=self._g_fb.pool()):
+            self._clip_and_update()
 
     def _graph_step(self, batches):
         if self._g_fb is None or len(batches) != len(self._static) or any(
@@ -203,7 +300,7 @@ class Trainer:
             logged = logged.clone()
             dist.all_reduce(logged)
             logged = logged / self.world
-            self._g_opt.replay()
+        self._g_opt.replay()
         return logged
 
     # ------------------------------------------------------------------------------------ api
