@@ -19,11 +19,26 @@ namespace {
 
 constexpr int kThreads = 256;
 
-__device__ __forceinline__ float mish_f(float x) { return x * tanhf(log1pf(expf(x))); }
+// mish(x) = x * tanh(softplus(x)) with ONE exponential: for e = exp(x), tanh(log(1 + e)) =
+// ((1+e)^2 - 1) / ((1+e)^2 + 1) = n / (n + 2), n = e (e + 2); sigmoid(x) = e / (1 + e).  x is clamped at
+// 15 (tanh(softplus(15)) rounds to 1 in fp32) so n never overflows.  Agrees with torch's
+// x * tanh(log1p(exp(x))) to a few ulp; the three-transcendental form made the GroupNorm backward
+// VALU-bound.
+__device__ __forceinline__ float tanh_softplus(float x, float &sig) {
+    const float e = __expf(fminf(x, 15.f));
+    const float n = e * (e + 2.f);
+    sig = e / (1.f + e);
+    return n / (n + 2.f);
+}
+
+__device__ __forceinline__ float mish_f(float x) {
+    float sig;
+    return x * tanh_softplus(x, sig);
+}
 
 __device__ __forceinline__ float mish_grad(float x) {
-    const float sig = 1.f / (1.f + expf(-x));
-    const float tsp = tanhf(log1pf(expf(x)));
+    float sig;
+    const float tsp = tanh_softplus(x, sig);
     return tsp + x * sig * (1.f - tsp * tsp);
 }
 
@@ -106,6 +121,151 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_fwd_kernel(const float *__
         o.z = mish_f((v.z - mean) * rstd * ga.z + be.z) * m + ad.z;
         o.w = mish_f((v.w - mean) * rstd * ga.w + be.w) * m + ad.w;
         *reinterpret_cast<float4 *>(yb + (size_t)t * C) = o;
+    }
+}
+
+// Register-resident variants (T <= P * rows_per_pass): the group's values are loaded ONCE into
+// registers -- one HBM read + one write per element instead of three / four streaming passes -- with
+// the same per-thread summation order as the streaming kernels.
+template <int P>
+__global__ __launch_bounds__(kGnThreads) void gn_mish_fwd_reg_kernel(const float *__restrict__ h, const float *__restrict__ gamma,
+                                                                   const float *__restrict__ beta,
+                                                                   const float *__restrict__ mask,
+                                                                   const float *__restrict__ add, float *__restrict__ y,
+                                                                   float *__restrict__ mean_out,
+                                                                   float *__restrict__ rstd_out, int T, int C, int G,
+                                                                   float eps) {
+    __shared__ float red[kGnThreads / 64];
+    const int g = blockIdx.x, b = blockIdx.y;
+    const int cg = C / G, cols = cg / 4, rpp = kGnThreads / cols;
+    const int tid = threadIdx.x, col = tid % cols, r0 = tid / cols;
+    const bool active = r0 < rpp;
+    const int c0 = g * cg + col * 4;
+    const float *hb = h + (size_t)b * T * C + c0;
+    const float n = (float)T * cg;
+    float4 v[P];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const int t = r0 + k * rpp;
+        v[k] = (active && t < T) ? *reinterpret_cast<const float4 *>(hb + (size_t)t * C) : make_float4(0.f, 0.f, 0.f, 0.f);
+        s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+    }
+    const float mean = block_sum<kGnThreads>(s, red) / n;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        if (!active || r0 + k * rpp >= T) continue;
+        const float a = v[k].x - mean, bq = v[k].y - mean, cq = v[k].z - mean, d = v[k].w - mean;
+        q += (a * a + bq * bq) + (cq * cq + d * d);
+    }
+    const float var = block_sum<kGnThreads>(q, red) / n;
+    const float rstd = rsqrtf(var + eps);
+    if (tid == 0) {
+        mean_out[b * G + g] = mean;
+        rstd_out[b * G + g] = rstd;
+    }
+    if (!active) return;
+    const float4 ga = *reinterpret_cast<const float4 *>(gamma + c0);
+    const float4 be = *reinterpret_cast<const float4 *>(beta + c0);
+    float4 ad = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (add) ad = *reinterpret_cast<const float4 *>(add + (size_t)b * C + c0);
+    float *yb = y + (size_t)b * T * C + c0;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const int t = r0 + k * rpp;
+        if (t >= T) continue;
+        const float m = mask ? mask[(size_t)b * T + t] : 1.f;
+        float4 o;
+        o.x = mish_f((v[k].x - mean) * rstd * ga.x + be.x) * m + ad.x;
+        o.y = mish_f((v[k].y - mean) * rstd * ga.y + be.y) * m + ad.y;
+        o.z = mish_f((v[k].z - mean) * rstd * ga.z + be.z) * m + ad.z;
+        o.w = mish_f((v[k].w - mean) * rstd * ga.w + be.w) * m + ad.w;
+        *reinterpret_cast<float4 *>(yb + (size_t)t * C) = o;
+    }
+}
+
+template <int P>
+__global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_reg_kernel(
+    const float *__restrict__ dy, const float *__restrict__ h, const float *__restrict__ gamma,
+    const float *__restrict__ beta, const float *__restrict__ mask, const float *__restrict__ mean_in,
+    const float *__restrict__ rstd_in, float *__restrict__ dh, float *__restrict__ pg, float *__restrict__ pb,
+    float *__restrict__ dadd, int T, int C, int G) {
+    __shared__ float red[kGnThreads / 64];
+    __shared__ float4 chred[3][kGnThreads];
+    const int g = blockIdx.x, b = blockIdx.y;
+    const int cg = C / G, cols = cg / 4, rpp = kGnThreads / cols;
+    const int tid = threadIdx.x, col = tid % cols, r0 = tid / cols;
+    const bool active = r0 < rpp;
+    const int c0 = g * cg + col * 4;
+    const float mean = mean_in[b * G + g], rstd = rstd_in[b * G + g];
+    const float4 ga = *reinterpret_cast<const float4 *>(gamma + c0);
+    const float4 be = *reinterpret_cast<const float4 *>(beta + c0);
+    const float *hb = h + (size_t)b * T * C + c0;
+    const float *db_ = dy + (size_t)b * T * C + c0;
+    const float n = (float)T * cg;
+    float4 v[P], gu[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const int t = r0 + k * rpp;
+        const bool ok = active && t < T;
+        v[k] = ok ? *reinterpret_cast<const float4 *>(hb + (size_t)t * C) : make_float4(0.f, 0.f, 0.f, 0.f);
+        gu[k] = ok ? *reinterpret_cast<const float4 *>(db_ + (size_t)t * C) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float s1 = 0.f, s2 = 0.f;
+    float4 ag = make_float4(0, 0, 0, 0), ab = make_float4(0, 0, 0, 0), ad = make_float4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const int t = r0 + k * rpp;
+        if (!active || t >= T) continue;
+        const float m = mask ? mask[(size_t)b * T + t] : 1.f;
+        float xh, d;
+#define MTTS_GN_BWD_ACC(X, G_, GA, BE, AG, AB, AD) \
+    xh = (X - mean) * rstd;                         \
+    d = G_;                                          \
+    G_ = d * m * mish_grad(xh * GA + BE);            \
+    s1 += G_ * GA;                                   \
+    s2 += G_ * GA * xh;                              \
+    AG += G_ * xh;                                   \
+    AB += G_;                                        \
+    AD += d;
+        MTTS_GN_BWD_ACC(v[k].x, gu[k].x, ga.x, be.x, ag.x, ab.x, ad.x)
+        MTTS_GN_BWD_ACC(v[k].y, gu[k].y, ga.y, be.y, ag.y, ab.y, ad.y)
+        MTTS_GN_BWD_ACC(v[k].z, gu[k].z, ga.z, be.z, ag.z, ab.z, ad.z)
+        MTTS_GN_BWD_ACC(v[k].w, gu[k].w, ga.w, be.w, ag.w, ab.w, ad.w)
+#undef MTTS_GN_BWD_ACC
+    }
+    const float m1 = block_sum<kGnThreads>(s1, red) / n;
+    const float m2 = block_sum<kGnThreads>(s2, red) / n;
+    chred[0][tid] = ag;
+    chred[1][tid] = ab;
+    chred[2][tid] = ad;
+    __syncthreads();
+    if (tid < cols) {
+        float4 sg = make_float4(0, 0, 0, 0), sb = sg, sd = sg;
+        for (int r = 0; r < rpp; ++r) {
+            const float4 a = chred[0][r * cols + tid], bb = chred[1][r * cols + tid], dd = chred[2][r * cols + tid];
+            sg.x += a.x; sg.y += a.y; sg.z += a.z; sg.w += a.w;
+            sb.x += bb.x; sb.y += bb.y; sb.z += bb.z; sb.w += bb.w;
+            sd.x += dd.x; sd.y += dd.y; sd.z += dd.z; sd.w += dd.w;
+        }
+        const int cc = g * cg + tid * 4;
+        *reinterpret_cast<float4 *>(pg + (size_t)b * C + cc) = sg;
+        *reinterpret_cast<float4 *>(pb + (size_t)b * C + cc) = sb;
+        if (dadd) *reinterpret_cast<float4 *>(dadd + (size_t)b * C + cc) = sd;
+    }
+    if (!active) return;
+    float *dhb = dh + (size_t)b * T * C + c0;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const int t = r0 + k * rpp;
+        if (t >= T) continue;
+        float4 o;
+        o.x = rstd * (gu[k].x * ga.x - m1 - (v[k].x - mean) * rstd * m2);
+        o.y = rstd * (gu[k].y * ga.y - m1 - (v[k].y - mean) * rstd * m2);
+        o.z = rstd * (gu[k].z * ga.z - m1 - (v[k].z - mean) * rstd * m2);
+        o.w = rstd * (gu[k].w * ga.w - m1 - (v[k].w - mean) * rstd * m2);
+        *reinterpret_cast<float4 *>(dhb + (size_t)t * C) = o;
     }
 }
 
@@ -411,8 +571,17 @@ extern "C" int mtts_gn_mish_fwd(const float *h, const float *gamma, const float 
     MTTS_CHECK_ARG(aligned16(h) && aligned16(y) && aligned16(gamma) && aligned16(beta) && (!add || aligned16(add)),
                    "gn_mish_fwd: tensors must be 16-byte aligned");
     if (B == 0) return MTTS_OK;
-    hipLaunchKernelGGL(gn_mish_fwd_kernel, dim3(G, B), dim3(kGnThreads), 0, static_cast<hipStream_t>(hip_stream), h,
-                       gamma, beta, mask, add, y, mean, rstd, T, C, G, eps);
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+    const int passes = (T + kGnThreads / (C / G / 4) - 1) / (kGnThreads / (C / G / 4));
+    if (passes <= 4)
+        hipLaunchKernelGGL(gn_mish_fwd_reg_kernel<4>, dim3(G, B), dim3(kGnThreads), 0, st, h, gamma, beta, mask, add, y,
+                           mean, rstd, T, C, G, eps);
+    else if (passes <= 8)
+        hipLaunchKernelGGL(gn_mish_fwd_reg_kernel<8>, dim3(G, B), dim3(kGnThreads), 0, st, h, gamma, beta, mask, add, y,
+                           mean, rstd, T, C, G, eps);
+    else
+        hipLaunchKernelGGL(gn_mish_fwd_kernel, dim3(G, B), dim3(kGnThreads), 0, st, h, gamma, beta, mask, add, y, mean,
+                           rstd, T, C, G, eps);
     return mtts::check_launch("gn_mish_fwd_kernel");
 }
 
@@ -434,8 +603,16 @@ extern "C" int mtts_gn_mish_bwd(const float *dy, const float *h, const float *ga
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
     float *pg = static_cast<float *>(workspace);
     float *pb = pg + (size_t)B * C;
-    hipLaunchKernelGGL(gn_mish_bwd_kernel, dim3(G, B), dim3(kGnThreads), 0, st, dy, h, gamma, beta, mask, mean, rstd,
-                       dh, pg, pb, dadd, T, C, G);
+    const int passes = (T + kGnThreads / (C / G / 4) - 1) / (kGnThreads / (C / G / 4));
+    if (passes <= 4)
+        hipLaunchKernelGGL(gn_mish_bwd_reg_kernel<4>, dim3(G, B), dim3(kGnThreads), 0, st, dy, h, gamma, beta, mask, mean,
+                           rstd, dh, pg, pb, dadd, T, C, G);
+    else if (passes <= 6)  // (8 spills at 1024 threads)
+        hipLaunchKernelGGL(gn_mish_bwd_reg_kernel<6>, dim3(G, B), dim3(kGnThreads), 0, st, dy, h, gamma, beta, mask, mean,
+                           rstd, dh, pg, pb, dadd, T, C, G);
+    else
+        hipLaunchKernelGGL(gn_mish_bwd_kernel, dim3(G, B), dim3(kGnThreads), 0, st, dy, h, gamma, beta, mask, mean, rstd,
+                           dh, pg, pb, dadd, T, C, G);
     int rc = mtts::check_launch("gn_mish_bwd_kernel");
     if (rc) return rc;
     if (dgamma || dbeta)
