@@ -27,22 +27,29 @@ class BaseConditionalFlowMatching(nn.Module, ABC):
         self.estimator = None
 
     @torch.inference_mode()
-    def forward(self, mu, mask, n_timesteps, temperature=1.0, spks=None, cond=None):
-        """flow_matching.py:42-65: Euler integration of the learned velocity from N(0, T^2)."""
-        z = torch.randn_like(mu) * temperature
+    def forward(self, mu, mask, n_timesteps, temperature=1.0, spks=None, cond=None, *, z=None):
+        """flow_matching.py:42-65: Euler integration of the learned velocity from N(0, T^2).
+        ``z`` (keyword-only) injects the initial noise for parity tests."""
+        if z is None:
+            z = torch.randn_like(mu) * temperature
         t_span = torch.linspace(0, 1, n_timesteps + 1, device=mu.device)
         return self.solve_ode_euler(z, t_span, mu, mask, spks, cond)
 
     def solve_ode_euler(self, x, t_span, mu, mask, spks, cond):
-        """flow_matching.py:67-104 (same t/dt recurrence)."""
+        """flow_matching.py:67-104 (same t/dt recurrence).  The velocity field runs token-major on the
+        HIP kernels (Decoder.forward_tm); the state stays [B, T, C] across the steps and is transposed
+        back once at the end."""
         t = t_span[0]
         dt = t_span[1] - t_span[0]
+        xt = x.transpose(1, 2).contiguous()
+        mu_t = mu.transpose(1, 2).contiguous()
+        m = mask[:, 0].contiguous()
         for step in range(1, len(t_span)):
-            x = x + dt * self.estimator(x, mask, mu, t.expand(x.shape[0]), cond)
+            xt = xt + dt * self.estimator.forward_tm(xt, m, mu_t, t.expand(x.shape[0]))
             t = t + dt
             if step < len(t_span) - 1:
                 dt = t_span[step + 1] - t
-        return x
+        return xt.transpose(1, 2)
 
     def compute_loss(self, x1, mask, mu, spks=None, cond=None, *, t=None, z=None):
         """Returns (loss, phi_t).  x1/mu [B, n_feats, T], mask [B, 1, T]."""

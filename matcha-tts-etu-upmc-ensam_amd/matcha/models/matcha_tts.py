@@ -59,8 +59,9 @@ class MatchaTTS(BaseLightningClass):
         self.update_data_statistics(data_statistics)
 
     @torch.inference_mode()
-    def synthesise(self, x, x_lengths, n_timesteps, temperature=1.0, length_scale=1.0):
-        """matcha_tts.py:368-435."""
+    def synthesise(self, x, x_lengths, n_timesteps, temperature=1.0, length_scale=1.0, *, z=None):
+        """matcha_tts.py:179-245 (reference fork).  ``z`` (keyword-only, [B, n_feats, y_max_length_])
+        injects the ODE's initial noise for parity tests."""
         t0 = dt.datetime.now()
         mu_x, logw, x_mask = self.encoder(x, x_lengths)
         w_ceil = torch.ceil(torch.exp(logw) * x_mask) * length_scale
@@ -71,7 +72,7 @@ class MatchaTTS(BaseLightningClass):
         attn_mask = x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)
         attn = generate_path(w_ceil.squeeze(1), attn_mask.squeeze(1)).unsqueeze(1)
         mu_y = torch.matmul(attn.squeeze(1).transpose(1, 2), mu_x.transpose(1, 2)).transpose(1, 2)
-        decoder_outputs = self.decoder(mu_y, y_mask, n_timesteps, temperature)[:, :, :y_max_length]
+        decoder_outputs = self.decoder(mu_y, y_mask, n_timesteps, temperature, z=z)[:, :, :y_max_length]
         rtf = (dt.datetime.now() - t0).total_seconds() * 22050 / (decoder_outputs.shape[-1] * 256)
         return {"encoder_outputs": mu_y[:, :, :y_max_length], "decoder_outputs": decoder_outputs,
                 "attn": attn[:, :, :y_max_length], "mel": denormalize(decoder_outputs, self.mel_mean, self.mel_std),

@@ -224,6 +224,20 @@ class CFMOracle(nn.Module):
         self.sigma_min = getattr(cfm_params, "sigma_min", 1e-4) if cfm_params is not None else 1e-4
         self.estimator = DecoderOracle(in_channels, out_channel, **(decoder_params or {}))
 
+    @torch.no_grad()
+    def forward(self, mu, mask, n_timesteps, temperature=1.0, spks=None, cond=None, z=None):
+        """flow_matching.py:42-65 + solve_ode_euler :67-104 (same t / dt recurrence); z injectable."""
+        if z is None:
+            z = torch.randn_like(mu) * temperature
+        t_span = torch.linspace(0, 1, n_timesteps + 1, device=mu.device)
+        x, t, dt = z, t_span[0], t_span[1] - t_span[0]
+        for step in range(1, len(t_span)):
+            x = x + dt * self.estimator(x, mask, mu, t, cond)
+            t = t + dt
+            if step < len(t_span) - 1:
+                dt = t_span[step + 1] - t
+        return x
+
     def compute_loss(self, x1, mask, mu, spks=None, cond=None, t=None, z=None):
         B = mu.shape[0]
         if t is None:
@@ -359,6 +373,19 @@ class TextEncoderO(nn.Module):  # text_encoder.py:325-402 (simple-params config,
         return self.mean_projection(h) * m, self.duration_predictor(h.detach(), m), m
 
 
+def generate_path(duration, mask):  # model.py:77-114 (build_alignment_path)
+    B, Tx, Ty = mask.shape
+    cum = torch.cumsum(duration, 1)
+    path = sequence_mask(cum.reshape(B * Tx), Ty).to(mask.dtype).view(B, Tx, Ty)
+    path = path - F.pad(path, (0, 0, 1, 0, 0, 0))[:, :-1]
+    return path * mask
+
+
+def fix_len_compatibility(length, num_downsamplings_in_unet=2):  # model.py:37-57
+    f = 2 ** num_downsamplings_in_unet
+    return int((torch.ceil(length / f) * f).item())
+
+
 class MatchaTTSOracle(nn.Module):
     """MatchaTTS(n_vocab, out_channels=80, hidden_channels=192) forward (matcha_tts.py:437-515)."""
 
@@ -371,6 +398,24 @@ class MatchaTTSOracle(nn.Module):
         self.register_buffer("mel_mean", torch.tensor(0.0))
         self.register_buffer("mel_std", torch.tensor(1.0))
         self._maximum_path = maximum_path
+
+    @torch.no_grad()
+    def synthesise(self, x, x_lengths, n_timesteps, temperature=1.0, length_scale=1.0, z=None):
+        """matcha_tts.py:179-245 (rtf omitted); ``z`` [B, n_feats, y_max_length_] injectable."""
+        mu_x, logw, x_mask = self.encoder(x, x_lengths)
+        w = torch.exp(logw) * x_mask
+        w_ceil = torch.ceil(w) * length_scale
+        y_lengths = torch.clamp_min(torch.sum(w_ceil, [1, 2]), 1).long()
+        y_max_length = y_lengths.max()
+        y_max_length_ = fix_len_compatibility(y_max_length)
+        y_mask = sequence_mask(y_lengths, y_max_length_).unsqueeze(1).to(x_mask.dtype)
+        attn_mask = x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)
+        attn = generate_path(w_ceil.squeeze(1), attn_mask.squeeze(1)).unsqueeze(1)
+        mu_y = torch.matmul(attn.squeeze(1).transpose(1, 2), mu_x.transpose(1, 2)).transpose(1, 2)
+        out = self.decoder(mu_y, y_mask, n_timesteps, temperature, z=z)
+        ym = int(y_max_length)
+        return {"encoder_outputs": mu_y[:, :, :ym], "decoder_outputs": out[:, :, :ym], "attn": attn[:, :, :ym],
+                "mel": out[:, :, :ym] * self.mel_std + self.mel_mean, "mel_lengths": y_lengths}
 
     def forward(self, x, x_lengths, y, y_lengths, out_size=None, cond=None, durations=None, t=None, z=None,
                 return_log_prior=False):
