@@ -127,6 +127,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="eager step (DDP) instead of the captured HIP graph")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-synth", action="store_true", help="skip the synthesise (inference) measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -233,6 +234,29 @@ def main():
     gemm_avg_us = sum(gemm_ms) / max(len(gemm_ms), 1) * 1e3
     gemm_tflops = gemm_flops / (sum(gemm_ms) * 1e-3) / 1e12 if gemm_ms else 0.0
 
+    # inference: MatchaTTS.synthesise on the same text batch, 10 Euler steps, the ODE
+    # replayed as one HIP graph; length_scale 5 gives LJSpeech-like ~5 frames per token
+    synth = None
+    if not args.no_synth:
+        model.eval()
+        with torch.inference_mode():
+            xs, xls = batch["x"], batch["x_lengths"]
+            for _ in range(2):
+                out = model.synthesise(xs, xls, 10, length_scale=5.0)
+            torch.cuda.synchronize()
+            reps, t0s = 5, time.perf_counter()
+            for _ in range(reps):
+                out = model.synthesise(xs, xls, 10, length_scale=5.0)
+            torch.cuda.synchronize()
+            syn_ms = (time.perf_counter() - t0s) / reps * 1e3
+        frames = int(out["mel_lengths"].sum().item())
+        audio_s = frames * 256 / 22050
+        synth = {"n_timesteps": 10, "batch": B, "frames": frames, "padded_frames": int(out["decoder_outputs"].shape[-1]),
+                 "ms_per_call": round(syn_ms, 2), "rtf": round(syn_ms / 1e3 / audio_s, 6),
+                 "frames_per_s": round(frames / (syn_ms / 1e3), 1),
+                 "note": "wall clock incl. host sync for the predicted lengths; random-init weights, length_scale 5"}
+        model.train()
+
     mas_ms = sum(a.elapsed_time(b) for a, b in mas_events) / max(len(mas_events), 1)
     cells = B * Tx * Ty
     mas_gbs = 12.0 * cells / (mas_ms * 1e-3) / 1e9
@@ -305,6 +329,7 @@ def main():
                              "achieved_tflops_step": round(flops / (step_ms * 1e-3) / 1e12, 2),
                              "peak_tflops": FP32_MFMA_TFLOPS if args.precision == "32-true" else BF16_DENSE_TFLOPS},
             "losses": [round(v, 5) for v in losses],
+            "synthesise": synth,
         }
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(4, Tx, Ty, args.cpu_budget)

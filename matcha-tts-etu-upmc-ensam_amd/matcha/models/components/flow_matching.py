@@ -35,10 +35,47 @@ class BaseConditionalFlowMatching(nn.Module, ABC):
         t_span = torch.linspace(0, 1, n_timesteps + 1, device=mu.device)
         return self.solve_ode_euler(z, t_span, mu, mask, spks, cond)
 
+    # the whole Euler solve of one (shape, n_timesteps) is captured once into a HIP graph and replayed:
+    # n_timesteps decoder forwards (~70 kernels each) become one graph launch.  Bounded cache.
+    graph_ode: bool = True
+    _GRAPH_CACHE_MAX = 8
+
     def solve_ode_euler(self, x, t_span, mu, mask, spks, cond):
         """flow_matching.py:67-104 (same t/dt recurrence).  The velocity field runs token-major on the
         HIP kernels (Decoder.forward_tm); the state stays [B, T, C] across the steps and is transposed
         back once at the end."""
+        if self.graph_ode and x.is_cuda and not torch.cuda.is_current_stream_capturing():
+            return self._solve_graph(x, t_span, mu, mask)
+        return self._solve_eager(x, t_span, mu, mask)
+
+    def _solve_graph(self, x, t_span, mu, mask):
+        cache = self.__dict__.setdefault("_ode_graphs", {})
+        key = (tuple(x.shape), tuple(mu.shape), t_span.numel(), x.dtype, x.device,
+               torch.is_autocast_enabled("cuda"), torch.get_autocast_dtype("cuda"))
+        ent = cache.get(key)
+        if ent is None:
+            if len(cache) >= self._GRAPH_CACHE_MAX:
+                cache.pop(next(iter(cache)))
+            sx, smu, sm, st = x.clone(), mu.clone(), mask.clone(), t_span.clone()
+            cur = torch.cuda.current_stream(x.device)
+            side = torch.cuda.Stream(x.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):  # warm-up: lazy loads, pack plans, allocator pools
+                self._solve_eager(sx, st, smu, sm)
+            cur.wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                out = self._solve_eager(sx, st, smu, sm)
+            ent = cache[key] = (g, sx, smu, sm, st, out)
+        g, sx, smu, sm, st, out = ent
+        sx.copy_(x)
+        smu.copy_(mu)
+        sm.copy_(mask)
+        st.copy_(t_span)
+        g.replay()
+        return out.clone()
+
+    def _solve_eager(self, x, t_span, mu, mask):
         t = t_span[0]
         dt = t_span[1] - t_span[0]
         xt = x.transpose(1, 2).contiguous()
