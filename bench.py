@@ -239,7 +239,8 @@ def main():
     synth = None
     if not args.no_synth:
         model.eval()
-        with torch.inference_mode():
+        amp = torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.precision == "bf16-mixed")
+        with torch.inference_mode(), amp:
             xs, xls = batch["x"], batch["x_lengths"]
             for _ in range(2):
                 out = model.synthesise(xs, xls, 10, length_scale=5.0)
@@ -254,6 +255,7 @@ def main():
         synth = {"n_timesteps": 10, "batch": B, "frames": frames, "padded_frames": int(out["decoder_outputs"].shape[-1]),
                  "ms_per_call": round(syn_ms, 2), "rtf": round(syn_ms / 1e3 / audio_s, 6),
                  "frames_per_s": round(frames / (syn_ms / 1e3), 1),
+                 "precision": args.precision,
                  "note": "wall clock incl. host sync for the predicted lengths; random-init weights, length_scale 5"}
         model.train()
 

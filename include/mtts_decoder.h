@@ -77,6 +77,9 @@ typedef struct mtts_conv_gemm_args {
 /* mtts_conv_gemm_args.flags */
 #define MTTS_GEMM_F_BINARY_SCALE 0x1 /* a_scale holds only 0 / 1 (a sequence mask): lets the bf16 path
                                         stage A rows by LDS-DMA, reading zeros for masked rows */
+#define MTTS_GEMM_F_A_BF16 0x2       /* A holds bf16 (lda in elements, lda % 8 == 0, cin % 8 == 0; bf16
+                                        precision only, LDS-DMA schedules) */
+#define MTTS_GEMM_F_C_BF16 0x4       /* C (not C_pre) is written as bf16 (ldc in elements) */
 
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
 /* Same, with an explicit schedule: 0..17 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;
@@ -111,6 +114,7 @@ typedef struct mtts_conv_wgrad_args {
     int32_t off[MTTS_CONV_MAX_TAPS];
     int32_t cin;
     int32_t N, K;
+    int32_t flags; /* MTTS_GEMM_F_A_BF16: A holds bf16 (lda in elements; bf16 precision only) */
 } mtts_conv_wgrad_args;
 
 size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *args);

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include <cstdint>
 
@@ -358,9 +359,13 @@ struct WgradGeom {
 // updated incrementally -- an add and one wrap select instead of a division and 64-bit address math
 // per row and step (the loop was VALU-bound: ~365 VALU vs 8 MFMA per step).  Requires To >= KB (one
 // wrap per step) and 32-bit element offsets; the launcher picks the generic path otherwise.
-template <bool BF16, int KB, int DEPTH, bool INC>
+// ABF16: A holds bf16 (MTTS_GEMM_F_A_BF16, bf16 precision only): 8-byte row chunks instead of 16, no
+// conversion on the way to LDS (the masked-row zeroing is a select).
+template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_args p, int rows_per_split,
                                                                float *__restrict__ part, float *__restrict__ part_db) {
+    static_assert(!ABF16 || BF16, "bf16 A needs the bf16 path");
+    const uint16_t *A16 = reinterpret_cast<const uint16_t *>(p.A);
     using Gm = WgradGeom<BF16, KB>;
     using ST = typename Gm::ST;
     constexpr int T = Gm::T, LDR = Gm::LDR, LDW = Gm::LDW, IMG = Gm::kImg, CH = Gm::CH;
@@ -430,6 +435,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
     // bias column sums are applied at store time so the loads stay in flight through the compute.
     struct Regs {
         float4 y[CH][2], x[CH][2];
+        uint2 x16[CH][2];  // ABF16: the 4 bf16 of the chunk
         float xs[CH][2];
         bool yok[CH][2], xok[CH][2];
     };
@@ -452,7 +458,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
                     R.yok[c][h] = mv;
                     const bool xok = mv && (unsigned)s_i[c][h] < (unsigned)p.Ti;
                     const int xr = xok ? s_x[c][h] : 0;
-                    R.x[c][h] = *reinterpret_cast<const float4 *>(p.A + (uint32_t)(xr * p.lda + c_ch[c]));
+                    if constexpr (ABF16)
+                        R.x16[c][h] = *reinterpret_cast<const uint2 *>(A16 + (uint32_t)(xr * p.lda + c_ch[c]));
+                    else
+                        R.x[c][h] = *reinterpret_cast<const float4 *>(p.A + (uint32_t)(xr * p.lda + c_ch[c]));
                     R.xs[c][h] = *(p.a_scale ? p.a_scale + (uint32_t)xr : p.A);
                     R.xok[c][h] = xok;
                     int u = s_u[c][h] + KB;
@@ -479,7 +488,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
                 const int irow = u * p.in_stride + c_toff[c];
                 const bool xok = mv && c_kok[c] && irow >= 0 && irow < p.Ti;
                 const size_t r = xok ? (size_t)b * p.Ti + irow : 0;
-                R.x[c][h] = *reinterpret_cast<const float4 *>(p.A + r * p.lda + (xok ? c_ch[c] : 0));
+                if constexpr (ABF16)
+                    R.x16[c][h] = *reinterpret_cast<const uint2 *>(A16 + r * p.lda + (xok ? c_ch[c] : 0));
+                else
+                    R.x[c][h] = *reinterpret_cast<const float4 *>(p.A + r * p.lda + (xok ? c_ch[c] : 0));
                 R.xs[c][h] = *(p.a_scale ? p.a_scale + r : p.A);
                 R.xok[c][h] = xok;
             }
@@ -495,8 +507,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
                 const float xm = R.xok[c][h] ? (p.a_scale ? R.xs[c][h] : 1.f) : 0.f;
                 yv[h][0] = R.y[c][h].x * ym; yv[h][1] = R.y[c][h].y * ym;
                 yv[h][2] = R.y[c][h].z * ym; yv[h][3] = R.y[c][h].w * ym;
-                xv[h][0] = R.x[c][h].x * xm; xv[h][1] = R.x[c][h].y * xm;
-                xv[h][2] = R.x[c][h].z * xm; xv[h][3] = R.x[c][h].w * xm;
+                if constexpr (!ABF16) {
+                    xv[h][0] = R.x[c][h].x * xm; xv[h][1] = R.x[c][h].y * xm;
+                    xv[h][2] = R.x[c][h].z * xm; xv[h][3] = R.x[c][h].w * xm;
+                }
             }
             // unconditional (only k-tile-0 blocks store it): a select per element costs more than the add
 #pragma unroll
@@ -508,8 +522,14 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
                 for (int h = 0; h < 2; ++h) {
                     *reinterpret_cast<uint2 *>(&Ys[(r2 + h) * LDW + c_cc[c]]) =
                         make_uint2(pk(yv[h][0], yv[h][1]), pk(yv[h][2], yv[h][3]));
-                    *reinterpret_cast<uint2 *>(&Xs[(r2 + h) * LDW + c_cc[c]]) =
-                        make_uint2(pk(xv[h][0], xv[h][1]), pk(xv[h][2], xv[h][3]));
+                    if constexpr (ABF16) {  // 0/1 row scale on bf16 A: keep or zero the raw bits
+                        const float xm = R.xok[c][h] ? (p.a_scale ? R.xs[c][h] : 1.f) : 0.f;
+                        *reinterpret_cast<uint2 *>(&Xs[(r2 + h) * LDW + c_cc[c]]) =
+                            xm != 0.f ? R.x16[c][h] : make_uint2(0u, 0u);
+                    } else {
+                        *reinterpret_cast<uint2 *>(&Xs[(r2 + h) * LDW + c_cc[c]]) =
+                            make_uint2(pk(xv[h][0], xv[h][1]), pk(xv[h][2], xv[h][3]));
+                    }
                 }
             } else {
 #pragma unroll
@@ -771,6 +791,9 @@ static void launch_by_id(int id, const mtts_conv_gemm_args &p, int M, hipStream_
 //  * erf-GELU / GELU' epilogues (the FFN's 1024-wide projection and its dgrad) are epilogue-bound:
 //    the small register-staged 32 x 128 tiles (config 7) keep 3 workgroups per CU so one
 //    workgroup's epilogue overlaps another's main loop (75 vs 88 us at 19200 x 1024 x 256);
+//  * the LDS-DMA 128 x 256 kernel (8 waves of 64 x 64, 2 stages) when ITS tiles fill the chip in one
+//    round and K >= 512 (the 19200-row N = 256 convs / FFN down-projection: 26.9 vs 29.8 us -- W is
+//    re-streamed by half as many row tiles);
 //  * the LDS-DMA 64 x 256 kernel (3 stages) wins when its tiles fill the chip in ONE round
 //    (128..256 tiles, K >= 768: the half-resolution decoder GEMMs, 17.4 vs 19.0 us) -- at 300 tiles
 //    the second round's tail makes it lose to config 12;
@@ -783,7 +806,17 @@ static int glds_tiles(const mtts_conv_gemm_args &p, int M) { return ((M + 63) / 
 static int pick_cfg(const mtts_conv_gemm_args &p, int M, bool bf16) {
     if (!bf16) return 7;
     if (p.act == MTTS_ACT_GELU || p.act == MTTS_ACT_DGELU) return 7;
-    if (mtts::conv_gemm_glds_applies(p) && p.K >= 768) {
+    static const int sched_mask = [] {  // MTTS_GEMM_SCHED_OFF bit mask: A/B switch for experiments
+        const char *e = getenv("MTTS_GEMM_SCHED_OFF");
+        return e ? atoi(e) : 0;
+    }();
+    // 128 x 256 LDS-DMA tiles won the isolated sweep on the 19200-row N = 256 GEMMs (26.9 vs 29.8 us) but
+    // LOST 0.33 ms per step in an in-step A/B on one box (tools/gpu_ab.sh: 2829 vs 2915 utt/s): opt-in
+    if ((sched_mask & 4) && mtts::conv_gemm_glds_applies(p) && p.K >= 512) {  // 128 x 256 tiles, one round
+        const int t = ((M + 127) / 128) * ((p.N + 255) / 256);
+        if (t >= 128 && t <= 256) return MTTS_GEMM_GLDS + 14;
+    }
+    if (!(sched_mask & 2) && mtts::conv_gemm_glds_applies(p) && p.K >= 768) {
         const int t = glds_tiles(p, M);
         if ((t >= 128 && t <= 256) || (t < 128 && p.K >= 1536 && p.N % 4 == 0)) return MTTS_GEMM_GLDS + 10;
     }
@@ -841,6 +874,17 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     }
     if (glds_id && (!bf16 || !mtts::conv_gemm_glds_applies(p)))
         return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: LDS-DMA schedule needs bf16, cin >= 64 and a 0/1 a_scale");
+    if (p.flags & MTTS_GEMM_F_A_BF16) {  // bf16 A operands exist only in the LDS-DMA kernels
+        if (!bf16 || !mtts::conv_gemm_glds_applies(p))
+            return mtts::fail(MTTS_ERR_UNSUPPORTED,
+                              "conv_gemm: a bf16 A needs bf16 precision, cin >= 64, cin / lda % 8 == 0, 0/1 a_scale");
+        if (cfg < 0) {
+            cfg = pick_cfg(p, M, bf16);
+            if (cfg < MTTS_GEMM_GLDS) cfg = MTTS_GEMM_GLDS + 9;
+        } else if (cfg < MTTS_GEMM_GLDS) {
+            return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: a bf16 A needs an LDS-DMA schedule");
+        }
+    }
     const GemmPlan pl = plan_gemm(p, bf16, cfg, splits);
     if (pl.cfg >= MTTS_GEMM_GLDS) {
         int s = pl.splits;
@@ -945,20 +989,20 @@ extern "C" size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *arg
     return mtts::align_up((size_t)splits * args->N * args->K * 4, 256) + (size_t)splits * args->N * 4 + 256;
 }
 
-template <bool BF16, int KB, int DEPTH, bool INC>
+template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false>
 static int wgrad_launch_k(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
                           hipStream_t st) {
     using Gm = WgradGeom<BF16, KB>;
     static bool attr_set = false;
     if (Gm::kLds > 64 * 1024 && !attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(conv_wgrad_kernel<BF16, KB, DEPTH, INC>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)Gm::kLds) != hipSuccess)
             return mtts::fail(MTTS_ERR_HIP, "conv_wgrad: LDS attribute");
         attr_set = true;
     }
     dim3 grid((unsigned)(((p.N + 127) / 128) * ((p.K + 127) / 128) * splits));
-    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH, INC>), grid, dim3(kThreads), Gm::kLds, st, p, rps, part,
-                       part_db);
+    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16>), grid, dim3(kThreads), Gm::kLds, st, p, rps,
+                       part, part_db);
     return mtts::check_launch("conv_wgrad_kernel");
 }
 
@@ -974,6 +1018,11 @@ static bool wgrad_inc_ok(const mtts_conv_wgrad_args &p, int kb) {
 template <bool BF16, int KB, int DEPTH>
 static int wgrad_launch(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
                         hipStream_t st) {
+    if constexpr (BF16 && KB == 32 && DEPTH == 1) {
+        if (p.flags & MTTS_GEMM_F_A_BF16)
+            return wgrad_inc_ok(p, KB) ? wgrad_launch_k<true, 32, 1, true, true>(p, splits, rps, part, part_db, st)
+                                       : wgrad_launch_k<true, 32, 1, false, true>(p, splits, rps, part, part_db, st);
+    }
     return wgrad_inc_ok(p, KB) ? wgrad_launch_k<BF16, KB, DEPTH, true>(p, splits, rps, part, part_db, st)
                                : wgrad_launch_k<BF16, KB, DEPTH, false>(p, splits, rps, part, part_db, st);
 }
@@ -994,6 +1043,10 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
     const bool bf16 = precision == MTTS_PREC_BF16;
     if (rows_per_step < 0) rows_per_step = 32;
     if (depth < 0) depth = 1;
+    if (p.flags & MTTS_GEMM_F_A_BF16) {
+        MTTS_CHECK_ARG(bf16 && rows_per_step == 32 && depth == 1 && p.lda % 4 == 0 && (uintptr_t)p.A % 8 == 0,
+                       "conv_wgrad: a bf16 A needs bf16 precision, the default schedule and 8-byte aligned rows");
+    }
     MTTS_CHECK_ARG(rows_per_step == 32 || (rows_per_step == 64 && bf16), "conv_wgrad: rows_per_step 32 (or 64 bf16)");
     MTTS_CHECK_ARG(depth == 1 || (depth == 2 && bf16), "conv_wgrad: depth 1 (or 2 bf16)");
     MTTS_CHECK_ARG(target_blocks < 0 || (target_blocks >= 64 && target_blocks <= kWgradMaxTarget),

@@ -69,20 +69,26 @@ __device__ __forceinline__ void wait_vmcnt() {
     __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-template <int WM, int WN, int TM, int TN, int STAGES>
+template <int WM, int WN, int TM, int TN, int STAGES, bool ABF16 = false>
 struct GldsGeom {
     static constexpr int NT = 64 * WM * WN;
     static constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN;
-    static constexpr int A_BYTES = BM * kBK * 4;  // fp32 rows of 256 B
+    static constexpr int A_BYTES = BM * kBK * (ABF16 ? 2 : 4);  // fp32 rows of 256 B / bf16 rows of 128 B
     static constexpr int W_BYTES = BN * kBK * 2;  // bf16 rows of 128 B
     static constexpr int GA = A_BYTES / (NT * 16);  // DMA instructions per thread per K step
     static constexpr int GW = W_BYTES / (NT * 16);
     static_assert(A_BYTES % (NT * 16) == 0 && W_BYTES % (NT * 16) == 0, "tile / threads mismatch");
 };
 
-template <int WM, int WN, int TM, int TN, int STAGES>
+// ABF16: A is bf16 in HBM (MTTS_GEMM_F_A_BF16): 128-byte rows, the same image and swizzle as W, and
+// the fragment read needs no conversion.
+template <int WM, int WN, int TM, int TN, int STAGES, bool ABF16>
 __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_gemm_args p, int ksteps, float *part) {
-    using G = GldsGeom<WM, WN, TM, TN, STAGES>;
+    using G = GldsGeom<WM, WN, TM, TN, STAGES, ABF16>;
+    constexpr int ES = ABF16 ? 2 : 4;        // bytes per A element
+    constexpr int RPI = ABF16 ? 8 : 4;       // A rows per 1 KiB DMA instruction
+    constexpr int CPR = ABF16 ? 8 : 16;      // 16-byte chunks per A row of one K step
+    constexpr int EPC = 16 / ES;             // A elements per chunk
     constexpr int NT = G::NT, BM = G::BM, BN = G::BN, GA = G::GA, GW = G::GW, NW = NT / 64;
     // one __shared__ object per stage and operand, and a K loop unrolled by STAGES so every access
     // names its buffer statically: hipcc then sees that a DMA into one buffer cannot alias the
@@ -132,14 +138,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
     // ---- A chunk state: DMA instruction i of this wave covers tile rows 4q..4q+3 (q = i*NW + wave);
     // lane -> row 4q + lane/16, LDS slot lane%16 <- logical chunk (lane%16) ^ (row & 15)
     const float *zero = reinterpret_cast<const float *>(&g_zero16);
-    const long long tap_delta = (long long)offstep * p.lda - p.cin;  // source step when a chunk changes tap
-    const float *a_src[GA];  // the lane's chunk in the current step (valid when its tap's bit is set)
+    const long long tap_delta = ((long long)offstep * p.lda - p.cin) * ES;  // source bytes when a chunk changes tap
+    const char *a_src[GA];   // the lane's chunk in the current step (valid when its tap's bit is set)
     int a_ch[GA], a_j[GA];   // channel of the lane's chunk within its tap, and the tap
     uint32_t a_ok[GA];       // bit j: tap j's source row exists and is unmasked
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
-        const int r = 4 * (i * NW + wave) + (lane >> 4);
-        const int lc = (lane & 15) ^ (r & 15);
+        const int r = RPI * (i * NW + wave) + lane / CPR;
+        const int lc = (lane % CPR) ^ (ABF16 ? ((r >> 1) & 7) : (r & 15));
         const int m = m0 + r;
         int b = 0, u = 0;
         const bool mv = m < M;
@@ -152,10 +158,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
             ok |= (uint32_t)v << j;
         }
         a_ok[i] = ok;
-        const int k = kstep0 * kBK + lc * 4;  // the lane's element within the first K step
+        const int k = kstep0 * kBK + lc * EPC;  // the lane's element within the first K step
         a_j[i] = k / p.cin;
         a_ch[i] = k - a_j[i] * p.cin;
-        a_src[i] = p.A + (long long)(b * p.Ti + u * p.in_stride + off0 + a_j[i] * offstep) * p.lda + a_ch[i];
+        a_src[i] = reinterpret_cast<const char *>(p.A) +
+                   ((long long)(b * p.Ti + u * p.in_stride + off0 + a_j[i] * offstep) * p.lda + a_ch[i]) * ES;
     }
     // ---- W chunk state: instruction i covers W rows 8q..8q+7; lane -> row 8q + lane/8, LDS slot lane%8
     // <- logical chunk (lane%8) ^ ((row >> 1) & 7)
@@ -177,9 +184,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
 #pragma unroll
         for (int i = 0; i < GA; ++i) {
             const bool ok = (a_ok[i] >> min(a_j[i], 31)) & 1u;  // a_j >= ntaps (past K): bit is 0
-            glds16(ok ? a_src[i] : zero, abase + (i * NW + wave) * 1024);
+            glds16(ok ? static_cast<const void *>(a_src[i]) : static_cast<const void *>(zero),
+                   abase + (i * NW + wave) * 1024);
             a_ch[i] += kBK;
-            a_src[i] += kBK;
+            a_src[i] += kBK * ES;
             const bool w = a_ch[i] >= p.cin;  // cin >= 64: at most one tap change per step
             a_ch[i] -= w ? p.cin : 0;
             a_j[i] += w;
@@ -212,11 +220,18 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 const int r = wr * 32 * TM + i * 32 + lr;
-                const int c = 4 * ks + 2 * lh;
-                const float4 x0 = *reinterpret_cast<const float4 *>(abase + r * 256 + ((c ^ (r & 15)) << 4));
-                const float4 x1 = *reinterpret_cast<const float4 *>(abase + r * 256 + (((c + 1) ^ (r & 15)) << 4));
-                const uint4 w = make_uint4(pack2(x0.x, x0.y), pack2(x0.z, x0.w), pack2(x1.x, x1.y), pack2(x1.z, x1.w));
-                af[i] = __builtin_bit_cast(bf16x8, w);
+                if constexpr (ABF16) {
+                    const int c = 2 * ks + lh;
+                    af[i] = *reinterpret_cast<const bf16x8 *>(abase + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+                } else {
+                    const int c = 4 * ks + 2 * lh;
+                    const float4 x0 = *reinterpret_cast<const float4 *>(abase + r * 256 + ((c ^ (r & 15)) << 4));
+                    const float4 x1 =
+                        *reinterpret_cast<const float4 *>(abase + r * 256 + (((c + 1) ^ (r & 15)) << 4));
+                    const uint4 w =
+                        make_uint4(pack2(x0.x, x0.y), pack2(x0.z, x0.w), pack2(x1.x, x1.y), pack2(x1.z, x1.w));
+                    af[i] = __builtin_bit_cast(bf16x8, w);
+                }
             }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
@@ -313,14 +328,16 @@ constexpr GldsCfg kGlds[] = {
     {1, 2, 2, 2, 3},  // 43: 64 x 128, 128 thr (waves 64 x 64), 3 stages (96 KiB)
     {2, 2, 1, 1, 3},  // 44: 64 x 64, 3 stages (72 KiB)
     {2, 2, 1, 1, 2},  // 45: 64 x 64, 2 stages (48 KiB)
+    {2, 4, 2, 2, 2},  // 46: 128 x 256, 512 thr (waves 64 x 64), 2 stages (128 KiB)
+    {4, 2, 1, 2, 2},  // 47: 128 x 128, 512 thr (waves 32 x 64), 2 stages (96 KiB)
 };
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
 
-template <int C>
-int launch_glds(const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
+template <int C, bool ABF16>
+int launch_glds_t(const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
     constexpr GldsCfg c = kGlds[C];
-    using G = GldsGeom<c.wm, c.wn, c.tm, c.tn, c.stages>;
-    auto kern = conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages>;
+    using G = GldsGeom<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16>;
+    auto kern = conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16>;
     const int nk = (p.K + kBK - 1) / kBK;
     const int ksteps = (nk + splits - 1) / splits;
     const int S = splits > 1 ? (nk + ksteps - 1) / ksteps : 1;  // every split non-empty
@@ -334,6 +351,17 @@ int launch_glds(const mtts_conv_gemm_args &p, int M, int splits, float *part, hi
     return mtts::check_launch("splitk_epilogue_kernel");
 }
 
+// bf16-A instantiations exist for the schedules the heuristic picks (64 x 256 two / three stages,
+// 64 x 64, 128 x 256); any other id with a bf16 A runs the 64 x 256 two-stage one
+template <int C>
+int launch_glds(const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
+    if (p.flags & MTTS_GEMM_F_A_BF16) {
+        if constexpr (C == 9 || C == 10 || C == 12 || C == 14) return launch_glds_t<C, true>(p, M, splits, part, st);
+        else return launch_glds_t<9, true>(p, M, splits, part, st);
+    }
+    return launch_glds_t<C, false>(p, M, splits, part, st);
+}
+
 }  // namespace
 
 namespace mtts {
@@ -345,6 +373,7 @@ int conv_gemm_glds_num_cfgs() { return kNumGlds; }
 bool conv_gemm_glds_applies(const mtts_conv_gemm_args &p) {
     if (p.a_scale && !(p.flags & MTTS_GEMM_F_BINARY_SCALE)) return false;
     if (p.cin < kBK || p.cin % 4 || p.lda % 4 || p.Kp % 8) return false;
+    if ((p.flags & MTTS_GEMM_F_A_BF16) && (p.cin % 8 || p.lda % 8 || (uintptr_t)p.A % 16)) return false;
     const long long arows = (long long)p.nb * p.Ti;
     if (arows * p.lda >= (1ll << 31) - (1ll << 20)) return false;
     return true;
@@ -373,7 +402,9 @@ int conv_gemm_glds_launch(int id, const mtts_conv_gemm_args &p, int M, int split
         case 10: return launch_glds<10>(p, M, splits, part, st);
         case 11: return launch_glds<11>(p, M, splits, part, st);
         case 12: return launch_glds<12>(p, M, splits, part, st);
-        default: return launch_glds<13>(p, M, splits, part, st);
+        case 13: return launch_glds<13>(p, M, splits, part, st);
+        case 14: return launch_glds<14>(p, M, splits, part, st);
+        default: return launch_glds<15>(p, M, splits, part, st);
     }
 }
 

@@ -70,7 +70,10 @@ __device__ __forceinline__ void gemm_epilogue(const mtts_conv_gemm_args &p, f32x
                               : 0.f;
                 if (p.residual) val += p.residual[crow * p.ldr + n];
                 if (p.c_scale) val *= p.c_scale[crow];
-                p.C[crow * p.ldc + n] = val;
+                if (p.flags & MTTS_GEMM_F_C_BF16)
+                    reinterpret_cast<__bf16 *>(p.C)[crow * p.ldc + n] = (__bf16)val;
+                else
+                    p.C[crow * p.ldc + n] = val;
             }
         }
     }
@@ -103,7 +106,15 @@ __device__ __forceinline__ void epilogue_row4(const mtts_conv_gemm_args &p, int 
 #pragma unroll
         for (int q = 0; q < 4; ++q) e[q] *= cs;
     }
-    *reinterpret_cast<float4 *>(p.C + off) = make_float4(e[0], e[1], e[2], e[3]);
+    if (p.flags & MTTS_GEMM_F_C_BF16) {
+        typedef float f32x2_ __attribute__((ext_vector_type(2)));
+        typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
+        const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_){e[0], e[1]}, bf16x2_));
+        const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_){e[2], e[3]}, bf16x2_));
+        *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(p.C) + off) = make_uint2(lo, hi);
+    } else {
+        *reinterpret_cast<float4 *>(p.C + off) = make_float4(e[0], e[1], e[2], e[3]);
+    }
 }
 
 // Split-K partial store: the raw accumulators of a wave's tiles into part[M][N] (row = GEMM row),

@@ -23,6 +23,7 @@ from __future__ import annotations
 import contextlib
 import contextvars
 import ctypes
+import os
 import math
 
 import torch
@@ -47,6 +48,8 @@ KERNELS: dict[str, str] = {
 
 
 GEMM_F_BINARY_SCALE = 0x1  # include/mtts_decoder.h MTTS_GEMM_F_BINARY_SCALE
+GEMM_F_A_BF16 = 0x2  # MTTS_GEMM_F_A_BF16: A operand stored bf16 (bf16-mixed activations)
+GEMM_F_C_BF16 = 0x4  # MTTS_GEMM_F_C_BF16: output stored bf16
 GEMM_GLDS = 32  # MTTS_GEMM_GLDS: first LDS-DMA schedule id
 
 
@@ -69,7 +72,7 @@ class ConvWgradArgs(ctypes.Structure):
                 ("a_scale", ctypes.c_void_p), ("lda", ctypes.c_int32), ("Ti", ctypes.c_int32),
                 ("To", ctypes.c_int32), ("nb", ctypes.c_int32), ("in_stride", ctypes.c_int32),
                 ("ntaps", ctypes.c_int32), ("off", ctypes.c_int32 * 8), ("cin", ctypes.c_int32),
-                ("N", ctypes.c_int32), ("K", ctypes.c_int32)]
+                ("N", ctypes.c_int32), ("K", ctypes.c_int32), ("flags", ctypes.c_int32)]
 
 
 class AttnArgs(ctypes.Structure):
@@ -329,7 +332,9 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     args.C_pre = N.ptr(C_pre)
     args.aux, args.ldaux = N.ptr(aux), (aux.shape[-1] if aux is not None else 0)
     args.dropout_p, args.seed = float(dropout_p), N.ptr(seed)
-    args.flags = GEMM_F_BINARY_SCALE if (binary_scale and a_scale is not None) else 0
+    args.flags = ((GEMM_F_BINARY_SCALE if (binary_scale and a_scale is not None) else 0)
+                  | (GEMM_F_A_BF16 if A.dtype == torch.bfloat16 else 0)
+                  | (GEMM_F_C_BF16 if C.dtype == torch.bfloat16 else 0))
     log = LAUNCH_LOG
     if log is not None:
         st = torch.cuda.current_stream(C.device)
@@ -343,7 +348,7 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     if log is not None:
         e1.record(st)
         M_ = nb * To
-        nbytes = nb * Ti * cin * 4 + N_ * Kp * Wp.element_size() + M_ * N_ * 4
+        nbytes = nb * Ti * cin * A.element_size() + N_ * Kp * Wp.element_size() + M_ * N_ * C.element_size()
         nbytes += sum(M_ * N_ * 4 for t in (residual, aux, C_pre) if t is not None)
         log.append((e0, e1, 2.0 * M_ * N_ * args.K, prec, nbytes,
                     dict(M=M_, N=N_, K=args.K, cin=cin, ntaps=len(offs), in_stride=in_stride, res=residual is not None,
@@ -360,6 +365,7 @@ def _wgrad(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin
     for i, o in enumerate(offs):
         args.off[i] = o
     args.N, args.K = N_, len(offs) * cin
+    args.flags = GEMM_F_A_BF16 if A.dtype == torch.bfloat16 else 0
     lib = N.lib()
     ws = torch.empty(int(lib.mtts_conv_wgrad_workspace_size(ctypes.byref(args))), dtype=torch.uint8, device=dY.device)
     rc = lib.mtts_conv_wgrad_tile(ctypes.byref(args), prec, rows_per_step, target_blocks, depth, dw.data_ptr(), strides[0],
@@ -582,7 +588,10 @@ class _FeedForwardTM(torch.autograd.Function):
         ctx.w2t = packed(spec_linear((w2,), dgrad=True), prec) if any(ctx.needs_input_grad) else None
         ctx.w1t = packed(spec_linear((w1,), dgrad=True), prec) if ctx.needs_input_grad[0] else None
         z = torch.empty(M, H, device=x.device, dtype=torch.float32)
-        h = torch.empty(M, H, device=x.device, dtype=torch.float32)
+        # bf16-mixed: the GELU output is only ever the next GEMM's (and its wgrad's) bf16 MFMA operand,
+        # so it is stored as bf16 -- half the bytes written here and read twice later
+        h16 = prec == PREC_BF16 and os.environ.get("MTTS_FF_FP32_HIDDEN") != "1"
+        h = torch.empty(M, H, device=x.device, dtype=torch.bfloat16 if h16 else torch.float32)
         seed = _new_seed(x.device) if dropout_p > 0 else None
         _gemm(x2, M, M, 1, 1, [0], K, W1p, K1p, H, h, M, prec=prec, bias=_f32c(b1), act=ACT_GELU, C_pre=z,
               dropout_p=dropout_p, seed=seed)

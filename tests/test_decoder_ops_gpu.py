@@ -286,3 +286,41 @@ def test_gemm_lds_dma_split_k_epilogue(cfg, splits, act, pre):
     assert rel(y1, y0) < 1e-5, rel(y1, y0)
     if pre:
         assert rel(p1, p0) < 1e-5, rel(p1, p0)
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout,k,cfg", [(32, 600, 1024, 256, 1, -1), (32, 300, 256, 256, 3, -1),
+                                                 (5, 77, 256, 320, 3, 44), (4, 120, 192, 768, 3, 42)])
+def test_bf16_operand_storage_bitwise(B, T, Cin, Cout, k, cfg):
+    """bf16-stored A (MTTS_GEMM_F_A_BF16) and bf16 C (MTTS_GEMM_F_C_BF16): the GEMM and the wgrad on a
+    bf16 A are bitwise equal to the fp32-A path on the same (bf16-representable) values, and a bf16 C
+    is the fp32 C rounded once."""
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator(device="cpu").manual_seed(B + T + Cin + Cout)
+    x = torch.randn(B, T, Cin, generator=g).bfloat16().to(DEV)
+    m = (torch.rand(B * T, generator=g) > 0.2).float().to(DEV)
+    w = (torch.randn(Cout, Cin * k, generator=g) / math.sqrt(Cin * k)).to(DEV)
+    Wp, Kp = O.pack_weight(w, O.PREC_BF16)
+    offs = [j - k // 2 for j in range(k)]
+    c_cfg = cfg if cfg >= 0 else 41
+    y32 = torch.empty(B, T, Cout, device=DEV)
+    O._gemm(x.float(), T, T, B, 1, offs, Cin, Wp, Kp, Cout, y32, T, prec=O.PREC_BF16, a_scale=m, tile_cfg=c_cfg)
+    y16a = torch.empty(B, T, Cout, device=DEV)
+    O._gemm(x, T, T, B, 1, offs, Cin, Wp, Kp, Cout, y16a, T, prec=O.PREC_BF16, a_scale=m, tile_cfg=cfg)
+    yc = torch.empty(B, T, Cout, device=DEV, dtype=torch.bfloat16)
+    O._gemm(x.float(), T, T, B, 1, offs, Cin, Wp, Kp, Cout, yc, T, prec=O.PREC_BF16, a_scale=m, tile_cfg=c_cfg)
+    torch.cuda.synchronize()
+    if cfg >= 0:
+        assert torch.equal(y16a, y32)
+    else:
+        assert rel(y16a, y32) < 1e-6  # the heuristic may pick another schedule for the bf16 A
+    assert torch.equal(yc, y32.bfloat16())
+    dy = torch.randn(B, T, Cout, generator=g).to(DEV)
+    outs = []
+    for xa in (x.float(), x):
+        dw = torch.empty(Cout, Cin, k, device=DEV)
+        db = torch.empty(Cout, device=DEV)
+        O._wgrad(dy, T, 1, 0, xa, T, T, B, 1, offs, Cin, Cout, dw, (Cin * k, k, 1), prec=O.PREC_BF16, a_scale=m, db=db)
+        outs.append((dw, db))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

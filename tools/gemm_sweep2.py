@@ -39,6 +39,9 @@ SHAPES = [
 ]
 cands = [(-1, 0), (7, 1), (12, 1), (41, 1), (42, 1), (38, 1), (44, 1), (45, 1), (41, 2), (42, 2), (44, 2), (42, 4),
          (44, 4)]
+only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
+if only:
+    SHAPES = [s_ for s_ in SHAPES if s_[0] in only]
 if len(sys.argv) > 1:
     cands = [tuple(int(v) for v in c.split(":")) for c in sys.argv[1].split(",")]
 seed = torch.tensor([12345, 678], dtype=torch.int32, device=dev)
