@@ -159,23 +159,8 @@ def main():
     B, Tx, Ty = args.batch, args.tx, args.ty
     batch = synthetic_batch(B, Tx, Ty, seed=1000 + rank, device=dev)
 
-    # HIP events around every maximum_path launch (recorded on torch's current stream, which is
-    # the stream mtts_maximum_path_f32 is launched on)
     mas_events: list = []
-    record = {"on": False}
     real_mp = MA.maximum_path
-
-    def timed_mp(value, mask, **kw):
-        if not record["on"] or graph:
-            return real_mp(value, mask, **kw)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        out = real_mp(value, mask, **kw)
-        e1.record()
-        mas_events.append((e0, e1))
-        return out
-
-    MA.maximum_path = timed_mp
 
     for _ in range(args.warmup):
         trainer.step([batch])
@@ -183,7 +168,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    record["on"] = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         trainer.step([batch])
@@ -191,32 +175,40 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    record["on"] = False
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
     losses = trainer.last_losses.tolist()
 
-    if graph:
-        # the step is one graph replay: time maximum_path with HIP events on THIS batch's fp32 lattice
-        # (same kernels, same stream), right after the timed region
-        from matcha.utils.model import sequence_mask
+    # time maximum_path with HIP events on THIS batch's fp32 lattice (same kernels, same stream),
+    # right after the timed region; the step itself runs the fused lattice + DP
+    # (prior_maximum_path), timed beside it
+    from matcha.utils.model import sequence_mask
 
-        with torch.no_grad():
-            mu_x, _, x_mask = model.encoder(batch["x"], batch["x_lengths"])
-            lp = model.log_prior(mu_x, batch["y"])
-            y_mask = sequence_mask(batch["y_lengths"], Ty).unsqueeze(1).float()
-            am = (x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)).squeeze(1).contiguous()
-            for _ in range(3):
-                real_mp(lp, am)
-            for _ in range(20):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                real_mp(lp, am)
-                e1.record()
-                mas_events.append((e0, e1))
-        torch.cuda.synchronize()
+    with torch.no_grad():
+        mu_x, _, x_mask = model.encoder(batch["x"], batch["x_lengths"])
+        lp = model.log_prior(mu_x, batch["y"])
+        y_mask = sequence_mask(batch["y_lengths"], Ty).unsqueeze(1).float()
+        am = (x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)).squeeze(1).contiguous()
+        for _ in range(3):
+            real_mp(lp, am)
+        mas_events.clear()
+        for _ in range(20):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            real_mp(lp, am)
+            e1.record()
+            mas_events.append((e0, e1))
+        fev = []
+        for _ in range(20):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            MA.prior_maximum_path(mu_x, batch["y"], batch["x_lengths"], batch["y_lengths"])
+            e1.record()
+            fev.append((e0, e1))
+    torch.cuda.synchronize()
+    fused_ms = sum(a.elapsed_time(b) for a, b in fev) / len(fev)
     # dominant kernel: the decoder's implicit-GEMM conv/linear (conv_gemm_kernel, fwd + dgrad).  One
     # more eager fwd+bwd of the same batch (after the timed region, results discarded) with HIP events
     # around every launch on its stream; algorithmic FLOPs = 2*M*N*K per launch.
@@ -320,7 +312,10 @@ def main():
                        "global_batch": world * B, "seq_len": Ty, "text_len": Tx, "parallelism": f"dp{world}",
                        "precision": args.precision, "hip_graph": graph},
             "maximum_path": {"value": round(world * cells / mas_ms / 1e3, 1), "unit": "Mcells/s (whole node)",
-                             "ms_per_call": round(mas_ms, 4), "calls": len(mas_events)},
+                             "ms_per_call": round(mas_ms, 4), "calls": len(mas_events),
+                             "fused_prior_maximum_path_ms": round(fused_ms, 4),
+                             "fused_note": "what the step runs: log-prior lattice from mu_x / y + DP + durations "
+                                           "+ frame rows (mtts_prior_maximum_path)"},
             "roofline": gemm_roofline,
             "roofline_mas": {"kernel": "mas_dp_kernel + mas_expand_kernel (maximum_path)", "bound": "hbm",
                              "achieved": round(mas_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
