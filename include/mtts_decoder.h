@@ -80,6 +80,7 @@ typedef struct mtts_conv_gemm_args {
 #define MTTS_GEMM_F_A_BF16 0x2       /* A holds bf16 (lda in elements, lda % 8 == 0, cin % 8 == 0; bf16
                                         precision only, LDS-DMA schedules) */
 #define MTTS_GEMM_F_C_BF16 0x4       /* C (not C_pre) is written as bf16 (ldc in elements) */
+#define MTTS_GEMM_F_FAST_ACT 0x8     /* GELU / GELU' with a 5e-7 (fp32-evaluated) erf approximation (bf16-mixed) */
 
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
 /* Same, with an explicit schedule: 0..17 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;

@@ -63,7 +63,7 @@ __device__ __forceinline__ void gemm_epilogue(const mtts_conv_gemm_args &p, f32x
                 const size_t crow = (size_t)crows[v];
                 float val = acc[i][j][v] + bn;
                 if (p.C_pre) p.C_pre[crow * p.ldc + n] = val;
-                if (p.act) val = epi_act(p.act, val, p.aux + crow * p.ldaux + n);
+                if (p.act) val = epi_act(p.act, val, p.aux + crow * p.ldaux + n, p.flags & MTTS_GEMM_F_FAST_ACT);
                 if (p.dropout_p > 0.f)
                     val = dropout_keep(s0, s1, (uint32_t)crow, (uint32_t)n, p.dropout_p)
                               ? val * (1.0f / (1.0f - p.dropout_p))
@@ -89,8 +89,9 @@ __device__ __forceinline__ void epilogue_row4(const mtts_conv_gemm_args &p, int 
         if (p.act == MTTS_ACT_DGELU || p.act == MTTS_ACT_DRELU)
             a = *reinterpret_cast<const float4 *>(p.aux + (size_t)crow * p.ldaux + n);
         const float av[4] = {a.x, a.y, a.z, a.w};
+        const bool fast = p.flags & MTTS_GEMM_F_FAST_ACT;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) e[q] = epi_act(p.act, e[q], &av[q]);
+        for (int q = 0; q < 4; ++q) e[q] = epi_act(p.act, e[q], &av[q], fast);
     }
     if (p.dropout_p > 0.f) {
 #pragma unroll

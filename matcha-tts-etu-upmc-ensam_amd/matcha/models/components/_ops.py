@@ -50,6 +50,8 @@ KERNELS: dict[str, str] = {
 GEMM_F_BINARY_SCALE = 0x1  # include/mtts_decoder.h MTTS_GEMM_F_BINARY_SCALE
 GEMM_F_A_BF16 = 0x2  # MTTS_GEMM_F_A_BF16: A operand stored bf16 (bf16-mixed activations)
 GEMM_F_C_BF16 = 0x4  # MTTS_GEMM_F_C_BF16: output stored bf16
+GEMM_F_FAST_ACT = 0x8  # MTTS_GEMM_F_FAST_ACT: 1.5e-7-accurate erf in GELU epilogues (bf16-mixed only)
+_FAST_ACT = os.environ.get("MTTS_EXACT_GELU") != "1"
 GEMM_GLDS = 32  # MTTS_GEMM_GLDS: first LDS-DMA schedule id
 
 
@@ -334,7 +336,8 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     args.dropout_p, args.seed = float(dropout_p), N.ptr(seed)
     args.flags = ((GEMM_F_BINARY_SCALE if (binary_scale and a_scale is not None) else 0)
                   | (GEMM_F_A_BF16 if A.dtype == torch.bfloat16 else 0)
-                  | (GEMM_F_C_BF16 if C.dtype == torch.bfloat16 else 0))
+                  | (GEMM_F_C_BF16 if C.dtype == torch.bfloat16 else 0)
+                  | (GEMM_F_FAST_ACT if (prec == PREC_BF16 and _FAST_ACT) else 0))
     log = LAUNCH_LOG
     if log is not None:
         st = torch.cuda.current_stream(C.device)
