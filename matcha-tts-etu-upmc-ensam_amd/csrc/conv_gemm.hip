@@ -970,8 +970,10 @@ constexpr int kWgradMaxTarget = 1024;
 static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks, int *splits, int *rows_per_split) {
     const int M = p.nb * p.To;
     const int tiles = ((p.N + 127) / 128) * ((p.K + 127) / 128);
+    static const int min_blocks = [] { const char *e = getenv("MTTS_WGRAD_MINBLK"); return e ? atoi(e) : 256; }();
+    static const int split_rows = [] { const char *e = getenv("MTTS_WGRAD_ROWS"); return e && atoi(e) > 0 ? atoi(e) : 768; }();
     int s = target_blocks > 0 ? (target_blocks + tiles - 1) / tiles
-                              : max((256 + tiles - 1) / tiles, (M + 384) / 768);
+                              : max((min_blocks + tiles - 1) / tiles, (M + split_rows / 2) / split_rows);
     s = max(1, min(s, (M + 4 * kb - 1) / (4 * kb)));  // at least 4 steps per split
     int rps = (M + s - 1) / s;
     rps = (rps + kb - 1) / kb * kb;

@@ -359,8 +359,59 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
                          asc=a_scale is not None, cfg=tile_cfg)))
 
 
+# Weight gradients off the critical path: inside side_stream_wgrad() every _wgrad launches on a
+# side stream (after the main stream's work so far), so a layer's wgrad + slab reduce overlap the
+# dgrad chain that the previous layer waits for -- the backward's kernels are latency-bound and leave
+# the chip under-filled one at a time.  Every tensor a side launch touches is kept alive until
+# join_side_streams() (the main stream then waits for the side stream), so the caching allocator
+# cannot hand its memory to the main stream early; and because that extra reference raises the
+# tensors' use count, autograd never accumulates into a pass-through gradient in place while the side
+# stream still reads it.  The outputs dw / db are NOT kept (AccumulateGrad then steals them without a
+# kernel); nothing on the main stream reads them before the join.  Only for steps where autograd does
+# not accumulate into existing .grad tensors (fresh gradients, one micro-batch): the Trainer's graph
+# step.
+_SIDE_WGRAD = {"on": False, "streams": {}, "keep": []}
+
+
+@contextlib.contextmanager
+def side_stream_wgrad(enabled: bool = True):
+    prev = _SIDE_WGRAD["on"]
+    _SIDE_WGRAD["on"] = enabled
+    try:
+        yield
+    finally:
+        _SIDE_WGRAD["on"] = prev
+        join_side_streams()
+
+
+def join_side_streams():
+    for dev, side in _SIDE_WGRAD["streams"].items():
+        torch.cuda.current_stream(dev).wait_stream(side)
+    _SIDE_WGRAD["keep"].clear()
+
+
 def _wgrad(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin, N_, dw, strides, *, prec,
            a_scale=None, db=None, rows_per_step=-1, target_blocks=-1, depth=-1):
+    if _SIDE_WGRAD["on"] and dY.is_cuda:
+        dev = dY.device
+        side = _SIDE_WGRAD["streams"].get(dev)
+        if side is None:
+            side = _SIDE_WGRAD["streams"][dev] = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        # inputs only: an extra reference to dw / db would make AccumulateGrad clone them on the main
+        # stream (it steals a gradient only at use count 1) -- reading them before the side stream wrote
+        _SIDE_WGRAD["keep"].extend(t for t in (dY, A, a_scale) if t is not None)
+        with torch.cuda.stream(side):
+            return _wgrad_launch(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin, N_, dw,
+                                 strides, prec=prec, a_scale=a_scale, db=db, rows_per_step=rows_per_step,
+                                 target_blocks=target_blocks, depth=depth)
+    return _wgrad_launch(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin, N_, dw, strides,
+                         prec=prec, a_scale=a_scale, db=db, rows_per_step=rows_per_step,
+                         target_blocks=target_blocks, depth=depth)
+
+
+def _wgrad_launch(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin, N_, dw, strides, *, prec,
+                  a_scale=None, db=None, rows_per_step=-1, target_blocks=-1, depth=-1):
     args = ConvWgradArgs()
     args.dY, args.ldy, args.To_full, args.out_stride, args.out_off = dY.data_ptr(), dY.shape[-1], To_full, out_stride, out_off
     args.A, args.a_scale, args.lda, args.Ti, args.To, args.nb = A.data_ptr(), N.ptr(a_scale), A.shape[-1], Ti, To, nb

@@ -28,12 +28,14 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import math
+import os
 from dataclasses import dataclass
 
 import torch
 import torch.distributed as dist
 
 from matcha import _native as N
+from matcha.models.components import _ops as OPS
 from matcha.models.matcha_tts import MatchaTTS
 
 
@@ -161,6 +163,10 @@ class TrainConfig:
 
 
 class Trainer:
+    # opt-in: measured in-step on MI355X the graph step got 0.25 ms SLOWER with weight gradients on a
+    # side stream (11.25 vs 11.01 ms): the ~100 cross-stream edges cost more than the overlap returns
+    side_stream_wgrad = os.environ.get("MTTS_SIDE_WGRAD", "0") == "1"
+
     def __init__(self, model: MatchaTTS, cfg: TrainConfig = TrainConfig()):
         self.cfg = cfg
         self.model = model
@@ -204,6 +210,16 @@ class Trainer:
         return contextlib.nullcontext()
 
     def _fwd_bwd(self, batches, sync_ctx=None):
+        n = len(batches)
+        # weight gradients on a side stream, overlapping the dgrad chain (components/_ops.py
+        # side_stream_wgrad): safe when autograd steals every fresh gradient (graph step, one
+        # micro-batch, gradients set to None first); joined before this returns
+        side = (self.cfg.graph and n == 1 and self.dev.type == "cuda" and self.side_stream_wgrad
+                and all(p.grad is None for p in self.params))
+        with OPS.side_stream_wgrad(side):
+            return self._fwd_bwd_body(batches, sync_ctx)
+
+    def _fwd_bwd_body(self, batches, sync_ctx=None):
         n = len(batches)
         logged = None
         for i, batch in enumerate(batches):

@@ -64,3 +64,32 @@ def test_graph_replays_draw_new_dropout_masks():
     torch.cuda.synchronize()
     assert torch.isfinite(losses).all()
     assert len({round(v, 6) for v in losses[:, 2].tolist()}) > 1  # diff loss changes (t, z, masks)
+
+
+def test_side_stream_wgrad_matches_main_stream():
+    """Weight gradients launched on the side stream (components/_ops.py side_stream_wgrad) equal the
+    main-stream ones: same kernels, same inputs -- only the ordering against the dgrad chain moves."""
+    from matcha.models.components import _ops as OPS
+    from matcha.training import synthetic_batch
+
+    b = synthetic_batch(4, 20, 80, device=DEV)
+    m = _model(2)
+    m.eval()
+    t = torch.rand(4, 1, 1, device=DEV)
+    z = torch.randn(4, 80, 80, device=DEV)
+
+    def grads(side):
+        m.zero_grad(set_to_none=True)
+        with OPS.side_stream_wgrad(side):
+            dur, prior, diff, _ = m(**b, t=t, z=z)
+            (dur + prior + diff).backward()
+        torch.cuda.synchronize()
+        return {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+
+    g0, g1 = grads(False), grads(True)
+    assert g0.keys() == g1.keys() and len(g0) > 100
+    for n in g0:  # the decoder runs on libmtts alone: bitwise.  The encoder's torch kernels (embedding
+        if n.startswith("decoder."):  # backward with atomics, library convs) need not be deterministic
+            assert torch.equal(g1[n], g0[n]), n
+        else:
+            torch.testing.assert_close(g1[n], g0[n], rtol=1e-4, atol=1e-6)
