@@ -40,18 +40,59 @@ constexpr size_t kLdsMax = 160 * 1024;
 // Geometry per (precision, compiled head dim D in {32, 64, 96}; a runtime head dim dh <= D runs with
 // zero-filled columns dh..D-1).  Row tiles are [64 rows][D + pad] (fragment
 // reads along the head dim), transposed tiles [D][64 + pad] (fragment reads along the rows).
+//
+// bf16: ONE swizzled image per tile, read by rows (ds_read_b128) for the MFMAs that sum over the head
+// dim and by columns (ds_read_b64_tr_b16, the gfx950 transposing LDS read) for the MFMAs that sum over
+// the tile's rows -- no transposed copy, every store a ds_write_b64.  The image is made of 8-row x
+// 32-column sub-tiles of 512 B ([row / 8][col / 32][row % 8][32 cols]); inside a sub-tile row the
+// 16-byte chunk ch sits at chunk ch ^ ((row >> 2) & 3).  With the staging map below (16 lanes = two
+// rows x 32 columns) the b64 stores, the b128 row reads and the transposing reads of the 32x32x16
+// operand maps are all bank-conflict free (checked exhaustively for D = 32 / 64 / 96 against the
+// lane groups of MI355X_MICROARCH.md's LDS table), and the per-lane read addresses differ only by
+// immediates across k-steps / sub-tiles but for the XOR's one varying bit (2 base registers each).
+// fp32 (parity mode): a padded row tile plus a transposed tile, scalar fragment reads.
 template <bool BF16, int D>
 struct G {
     static_assert(D % 32 == 0 && D <= 96, "head dim 32, 64 or 96");
     using T = std::conditional_t<BF16, uint16_t, float>;
-    static constexpr int PAD = BF16 ? 8 : 1;  // bf16: 16-byte-aligned rows, conflict-free b128 reads
-    static constexpr int LDR = D + PAD;
-    static constexpr int LDT = kTile + PAD;
-    static constexpr int RE = kTile * LDR;  // elements of a row tile
-    static constexpr int TE = D * LDT;      // elements of a transposed tile
-    static constexpr int NT = D / 32;       // 32-wide MFMA tiles over the head dim
+    static constexpr int LDR = D + 1;               // fp32 row tile pitch (elements)
+    static constexpr int LDT = kTile + 1;           // fp32 transposed tile pitch
+    static constexpr int RE = BF16 ? kTile * D : kTile * LDR;  // elements of a row tile / image
+    static constexpr int TE = BF16 ? 0 : D * LDT;   // elements of a transposed tile (fp32 only)
+    static constexpr int NT = D / 32;               // 32-wide MFMA tiles over the head dim
     static constexpr int F4 = kTile * D / 4 / kThreads;  // float4 per thread to stage one tile
 };
+
+// byte offset of elements (r, col .. col+3) in a bf16 image (col % 4 == 0)
+template <int D>
+__device__ __forceinline__ int img_off(int r, int col) {
+    return 16 * D * (r >> 3) + 512 * (col >> 5) + 64 * (r & 7) + 16 * (((col >> 3) & 3) ^ ((r >> 2) & 3)) +
+           8 * ((col >> 2) & 1);
+}
+
+// staging map of float4 number idx of a 64 x D tile: fp32 row-major; bf16 16-lane groups of two rows
+// x 32 columns (one 128-byte span of the image per group: conflict-free b64 stores)
+template <bool BF16, int D>
+__device__ __forceinline__ void stage_rc(int idx, int &r, int &c) {
+    if constexpr (BF16) {
+        constexpr int NT = D / 32;
+        const int cc = idx & 7, rr = (idx >> 3) & 1, g = idx >> 4;
+        r = 2 * (g / NT) + rr;
+        c = 32 * (g % NT) + 4 * cc;
+    } else {
+        r = idx / (D / 4);
+        c = (idx % (D / 4)) * 4;
+    }
+}
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+// ds_read_b64_tr_b16: in each 16-lane group, lane 4q+p addresses row q / columns 4p..4p+3 of a 4x16
+// block and lane i receives column i of the 4 rows (EXEC must be full: called outside divergence)
+__device__ __forceinline__ uint2 lds_tr16(const void *p) {
+    const v4i16 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4i16 *)(const_cast<void *>(p)));
+    return __builtin_bit_cast(uint2, v);
+}
 
 __device__ __forceinline__ uint16_t to_bf16(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
@@ -101,9 +142,10 @@ __device__ __forceinline__ void mma_rows(f32x16 &acc, const typename G<BF16, D>:
                                          const RowFrag<BF16, D> &bf) {
     constexpr int LD = G<BF16, D>::LDR;
     if constexpr (BF16) {
+        const char *img = reinterpret_cast<const char *>(tile);
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) {
-            const bf16x8 a = *reinterpret_cast<const bf16x8 *>(tile + r * LD + 16 * ks + 8 * lh);
+            const bf16x8 a = *reinterpret_cast<const bf16x8 *>(img + img_off<D>(r, 16 * ks + 8 * lh));
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bf.f[ks], acc, 0, 0, 0);
         }
     } else {
@@ -113,18 +155,24 @@ __device__ __forceinline__ void mma_rows(f32x16 &acc, const typename G<BF16, D>:
     }
 }
 
-// acc += A(LDS transposed tile: row = head dim d, columns = the 32 rows of sub-tile `sub`, read in
-// the C-layout order this lane holds) x B(the lane's 16 C-layout values `s`)
+// acc += A(the tile transposed: row = head dim d, columns = the 32 rows of sub-tile `sub`, read in
+// the C-layout order this lane holds) x B(the lane's 16 C-layout values `s`).  bf16: `tileT` is the
+// row image, read with the transposing LDS read; fp32: the transposed tile.
 template <bool BF16, int D>
 __device__ __forceinline__ void mma_perm(f32x16 &acc, const typename G<BF16, D>::T *tileT, int d, int sub, int lh,
                                          const float (&s)[16]) {
     constexpr int LD = G<BF16, D>::LDT;
     if constexpr (BF16) {
+        // lane's k-slots = rows {16ks + 4lh + 0..3, 16ks + 8 + 4lh + 0..3} of the sub-tile (the C-layout
+        // rows it holds in s[8ks .. 8ks+7]); group lane 4q+p addresses row q, columns 4p.. of its block
+        const char *img = reinterpret_cast<const char *>(tileT);
+        const int j = threadIdx.x & 15, g1 = (threadIdx.x >> 4) & 1;
+        const int col = (d & ~31) + 16 * g1 + 4 * (j & 3);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            const int c0 = sub * 32 + 16 * ks + 4 * lh;
-            const uint2 lo = *reinterpret_cast<const uint2 *>(tileT + d * LD + c0);
-            const uint2 hi = *reinterpret_cast<const uint2 *>(tileT + d * LD + c0 + 8);
+            const int r = sub * 32 + 16 * ks + 4 * lh + (j >> 2);
+            const uint2 lo = lds_tr16(img + img_off<D>(r, col));
+            const uint2 hi = lds_tr16(img + img_off<D>(r + 8, col));
             const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
             const bf16x8 b = frag8(s + 8 * ks);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
@@ -148,8 +196,8 @@ struct TileLoader {
     __device__ void load(const float *base, int ld, int b, int T, int r0, int tid, int dh) {
 #pragma unroll
         for (int i = 0; i < Gm::F4; ++i) {
-            const int idx = tid + kThreads * i;
-            const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
+            int r, c;
+            stage_rc<BF16, D>(tid + kThreads * i, r, c);
             ok[i] = r0 + r < T && c < dh;
             const size_t off = ok[i] ? ((size_t)b * T + r0 + r) * ld + c : (size_t)b * T * ld;
             v[i] = *reinterpret_cast<const float4 *>(base + off);
@@ -158,17 +206,15 @@ struct TileLoader {
     __device__ void store(typename Gm::T *rowt, typename Gm::T *trt, int tid) const {
 #pragma unroll
         for (int i = 0; i < Gm::F4; ++i) {
-            const int idx = tid + kThreads * i;
-            const int r = idx / (D / 4), c = (idx % (D / 4)) * 4;
+            int r, c;
+            stage_rc<BF16, D>(tid + kThreads * i, r, c);
             const float m = ok[i] ? 1.f : 0.f;
             const float e[4] = {v[i].x * m, v[i].y * m, v[i].z * m, v[i].w * m};
-            if constexpr (BF16) {
-                if (rowt)
-                    *reinterpret_cast<uint2 *>(rowt + r * Gm::LDR + c) = make_uint2(pack2(e[0], e[1]), pack2(e[2], e[3]));
-                if (trt) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) trt[(c + j) * Gm::LDT + r] = to_bf16(e[j]);
-                }
+            if constexpr (BF16) {  // one image serves both reads: `trt` names it when `rowt` is null
+                typename Gm::T *img = rowt ? rowt : trt;
+                if (img)
+                    *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(img) + img_off<D>(r, c)) =
+                        make_uint2(pack2(e[0], e[1]), pack2(e[2], e[3]));
             } else {
                 if (rowt) {
 #pragma unroll
@@ -185,8 +231,9 @@ struct TileLoader {
 
 // LDS bytes per stage; kernels double-buffer when two stages fit in 160 KB, else single-buffer.
 template <bool BF16, int D>
-constexpr size_t fwd_stage() {  // K rows + V transposed + bias
-    return (size_t)(G<BF16, D>::RE + G<BF16, D>::TE) * sizeof(typename G<BF16, D>::T) + kTile * sizeof(float);
+constexpr size_t fwd_stage() {  // K rows + V transposed (bf16: K and V images) + bias
+    return (size_t)(G<BF16, D>::RE + (BF16 ? G<BF16, D>::RE : G<BF16, D>::TE)) * sizeof(typename G<BF16, D>::T) +
+           kTile * sizeof(float);
 }
 template <bool BF16, int D>
 constexpr size_t dq_stage() {  // K rows + V rows + K transposed + bias
@@ -241,8 +288,8 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
     constexpr int NB = nbuf(fwd_stage<BF16, D>());
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char *sp = smem;
-    ST *Ks = carve<ST>(sp, NB * Gm::RE);  // [NB][64 keys][LDR]
-    ST *Vt = carve<ST>(sp, NB * Gm::TE);  // [NB][D][LDT] (V transposed)
+    ST *Ks = carve<ST>(sp, NB * Gm::RE);  // [NB][64 keys][LDR] (bf16: image)
+    ST *Vt = carve<ST>(sp, NB * (BF16 ? Gm::RE : Gm::TE));  // [NB][D][LDT] V transposed (bf16: V image)
     float *bias_s = carve<float>(sp, NB * kTile);  // log2 domain; -inf past T
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
@@ -275,7 +322,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
     };
     auto store = [&](int buf) {
         lk.store(Ks + buf * Gm::RE, nullptr, tid);
-        lv.store(nullptr, Vt + buf * Gm::TE, tid);
+        lv.store(nullptr, Vt + buf * (BF16 ? Gm::RE : Gm::TE), tid);
         if (tid < kTile) bias_s[buf * kTile + tid] = bias_r;
     };
     const bool drop = p.dropout_p > 0.f;
@@ -287,7 +334,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
     const float inv_keep = 1.f / (1.f - p.dropout_p);
     const uint32_t prow = (uint32_t)(((size_t)b * p.H + h) * T + q);  // dropout row key of this query
     auto compute = [&](int buf, int k0) {
-        const ST *K_ = Ks + buf * Gm::RE, *V_ = Vt + buf * Gm::TE;
+        const ST *K_ = Ks + buf * Gm::RE, *V_ = Vt + buf * (BF16 ? Gm::RE : Gm::TE);
         const float *bs = bias_s + buf * kTile;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
@@ -356,7 +403,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p,
     unsigned char *sp = smem;
     ST *Ks = carve<ST>(sp, NB * Gm::RE);
     ST *Vs = carve<ST>(sp, NB * Gm::RE);
-    ST *Kt = carve<ST>(sp, NB * Gm::TE);
+    ST *Kt = BF16 ? Ks : carve<ST>(sp, NB * Gm::TE);  // bf16: K^T is read from the K image
     float *bias_s = carve<float>(sp, NB * kTile);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
@@ -406,7 +453,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p,
         }
     };
     auto store = [&](int buf) {
-        lk.store(Ks + buf * Gm::RE, Kt + buf * Gm::TE, tid);
+        lk.store(Ks + buf * Gm::RE, BF16 ? nullptr : Kt + buf * Gm::TE, tid);
         lv.store(Vs + buf * Gm::RE, nullptr, tid);
         if (tid < kTile) bias_s[buf * kTile + tid] = bias_r;
     };
@@ -419,7 +466,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p,
     const float inv_keep = 1.f / (1.f - p.dropout_p);
     const uint32_t prow = (uint32_t)srow;
     auto compute = [&](int buf, int k0) {
-        const ST *K_ = Ks + buf * Gm::RE, *V_ = Vs + buf * Gm::RE, *KT_ = Kt + buf * Gm::TE;
+        const ST *K_ = Ks + buf * Gm::RE, *V_ = Vs + buf * Gm::RE, *KT_ = BF16 ? K_ : Kt + buf * Gm::TE;
         const float *bs = bias_s + buf * kTile;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
@@ -471,8 +518,8 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkv_kernel(mtts_attn_args p
     unsigned char *sp = smem;
     ST *Qs = carve<ST>(sp, NB * Gm::RE);
     ST *Gs = carve<ST>(sp, NB * Gm::RE);  // dO rows
-    ST *Qt = carve<ST>(sp, NB * Gm::TE);
-    ST *Gt = carve<ST>(sp, NB * Gm::TE);  // dO transposed
+    ST *Qt = BF16 ? Qs : carve<ST>(sp, NB * Gm::TE);  // bf16: transposed reads of the row images
+    ST *Gt = BF16 ? Gs : carve<ST>(sp, NB * Gm::TE);  // dO transposed
     float *lse_s = carve<float>(sp, NB * kTile);  // +inf past T
     float *d_s = carve<float>(sp, NB * kTile);
 
@@ -509,8 +556,8 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkv_kernel(mtts_attn_args p
         }
     };
     auto store = [&](int buf) {
-        lq.store(Qs + buf * Gm::RE, Qt + buf * Gm::TE, tid);
-        lg.store(Gs + buf * Gm::RE, Gt + buf * Gm::TE, tid);
+        lq.store(Qs + buf * Gm::RE, BF16 ? nullptr : Qt + buf * Gm::TE, tid);
+        lg.store(Gs + buf * Gm::RE, BF16 ? nullptr : Gt + buf * Gm::TE, tid);
         if (tid < kTile) {
             lse_s[buf * kTile + tid] = lse_r;
             d_s[buf * kTile + tid] = d_r;
@@ -524,7 +571,8 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkv_kernel(mtts_attn_args p
     }
     const float inv_keep = 1.f / (1.f - p.dropout_p);
     auto compute = [&](int buf, int q0) {
-        const ST *Q_ = Qs + buf * Gm::RE, *G_ = Gs + buf * Gm::RE, *QT_ = Qt + buf * Gm::TE, *GT_ = Gt + buf * Gm::TE;
+        const ST *Q_ = Qs + buf * Gm::RE, *G_ = Gs + buf * Gm::RE;
+        const ST *QT_ = BF16 ? Q_ : Qt + buf * Gm::TE, *GT_ = BF16 ? G_ : Gt + buf * Gm::TE;
         const float *ls = lse_s + buf * kTile, *dd = d_s + buf * kTile;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
