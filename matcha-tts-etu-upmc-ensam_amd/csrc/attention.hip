@@ -115,14 +115,16 @@ struct RowFrag;
 template <int D>
 struct RowFrag<true, D> {
     bf16x8 f[D / 16];
-    __device__ void load(const float *row, bool ok, int lh, int dh) {
+    // mul: a prescale folded into the operand before its bf16 rounding (the softmax scale * log2 e)
+    __device__ void load(const float *row, bool ok, int lh, int dh, float mul = 1.f) {
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) {
             float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
             const int c = 16 * ks + 8 * lh;
             if (ok && c < dh) a = *reinterpret_cast<const float4 *>(row + c);
             if (ok && c + 4 < dh) b = *reinterpret_cast<const float4 *>(row + c + 4);
-            const float e[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            const float e[8] = {a.x * mul, a.y * mul, a.z * mul, a.w * mul,
+                                b.x * mul, b.y * mul, b.z * mul, b.w * mul};
             f[ks] = frag8(e);
         }
     }
@@ -130,7 +132,7 @@ struct RowFrag<true, D> {
 template <int D>
 struct RowFrag<false, D> {
     float f[D / 2];
-    __device__ void load(const float *row, bool ok, int lh, int dh) {
+    __device__ void load(const float *row, bool ok, int lh, int dh, float = 1.f) {
 #pragma unroll
         for (int ks = 0; ks < D / 2; ++ks) f[ks] = (ok && 2 * ks + lh < dh) ? row[2 * ks + lh] : 0.f;
     }
@@ -190,26 +192,29 @@ template <bool BF16, int D>
 struct TileLoader {
     using Gm = G<BF16, D>;
     float4 v[Gm::F4];
-    bool ok[Gm::F4];
-    // unconditional loads from clamped addresses (validity applied in store): no branch around a load,
-    // so the loads stay in flight through the compute phase
+    bool narrow = false;  // runtime head dim dh < D: columns past dh are zeroed
+    // unconditional loads from clamped addresses: no branch around a load, so the loads stay in flight
+    // through the compute phase.  Rows past T are NOT zeroed: they hold finite data (row 0 of the
+    // batch) and every kernel gives them probability 0 (key bias -inf / query lse +inf), so they add
+    // exact zeros to every product.
     __device__ void load(const float *base, int ld, int b, int T, int r0, int tid, int dh) {
+        narrow = dh < D;
 #pragma unroll
         for (int i = 0; i < Gm::F4; ++i) {
             int r, c;
             stage_rc<BF16, D>(tid + kThreads * i, r, c);
-            ok[i] = r0 + r < T && c < dh;
-            const size_t off = ok[i] ? ((size_t)b * T + r0 + r) * ld + c : (size_t)b * T * ld;
+            const bool ok = r0 + r < T && c < dh;
+            const size_t off = ok ? ((size_t)b * T + r0 + r) * ld + c : (size_t)b * T * ld;
             v[i] = *reinterpret_cast<const float4 *>(base + off);
         }
     }
-    __device__ void store(typename Gm::T *rowt, typename Gm::T *trt, int tid) const {
+    __device__ void store(typename Gm::T *rowt, typename Gm::T *trt, int tid, int dh) const {
 #pragma unroll
         for (int i = 0; i < Gm::F4; ++i) {
             int r, c;
             stage_rc<BF16, D>(tid + kThreads * i, r, c);
-            const float m = ok[i] ? 1.f : 0.f;
-            const float e[4] = {v[i].x * m, v[i].y * m, v[i].z * m, v[i].w * m};
+            float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+            if (narrow && c >= dh) e[0] = e[1] = e[2] = e[3] = 0.f;
             if constexpr (BF16) {  // one image serves both reads: `trt` names it when `rowt` is null
                 typename Gm::T *img = rowt ? rowt : trt;
                 if (img)
@@ -253,6 +258,32 @@ __device__ __forceinline__ T *carve(unsigned char *&p, size_t n) {
     return r;
 }
 
+// The key bias enters shifted by the batch row's first bias c0 -- softmax is invariant to a per-row
+// constant, and the saved lse carries the shift consistently into the backward.  With the 0/1 key mask
+// every tile inside the valid keys is then all zeros: the stage's flag lets it skip the per-element
+// bias (wave 0 stages the 64 biases of a tile and votes).
+__device__ __forceinline__ float key_bias_c0(const mtts_attn_args &p, int b) {
+    return p.key_bias ? p.key_bias[(size_t)b * p.T] : 0.f;
+}
+__device__ __forceinline__ float stage_bias(const mtts_attn_args &p, int b, int key, float c0) {
+    const int T = p.T;
+    const float raw = *(p.key_bias ? p.key_bias + (size_t)b * T + min(key, T - 1) : p.q);
+    return key < T ? (p.key_bias ? (raw - c0) * kLog2e : 0.f) : -INFINITY;
+}
+__device__ __forceinline__ void store_bias(float *bias_s, int *flag_s, int buf, float bias_r, int tid) {
+    if (tid < kTile) {  // wave 0, all lanes
+        bias_s[buf * kTile + tid] = bias_r;
+        const bool nz = __any(bias_r != 0.f);
+        if (tid == 0) flag_s[buf] = nz;
+    }
+}
+
+// Online-softmax rescales are deferred while the running max grows by at most kDefer (log2 units):
+// the probabilities then stay <= 2^kDefer, exact in fp32 and harmless to bf16 (the normaliser l uses
+// the same stale max).  The decision is wave-uniform, so the 16 x NT accumulator multiplies are
+// skipped as a whole on most tiles.
+constexpr float kDefer = 8.f;
+
 // The shared K-tile loop: stage 0, then per tile prefetch the next into registers, compute, and
 // publish it (double buffer: into the other stage, one barrier; single buffer: two barriers).
 template <int NB, typename Load, typename Store, typename Compute>
@@ -290,17 +321,20 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
     unsigned char *sp = smem;
     ST *Ks = carve<ST>(sp, NB * Gm::RE);  // [NB][64 keys][LDR] (bf16: image)
     ST *Vt = carve<ST>(sp, NB * (BF16 ? Gm::RE : Gm::TE));  // [NB][D][LDT] V transposed (bf16: V image)
-    float *bias_s = carve<float>(sp, NB * kTile);  // log2 domain; -inf past T
+    float *bias_s = carve<float>(sp, NB * kTile);  // log2 domain, shifted by c0; -inf past T
+    int *flag_s = carve<int>(sp, NB);              // stage has a nonzero bias
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
     const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
     const int q = blockIdx.x * kRowsPerBlock + wave * 32 + lr;
     const bool q_ok = q < T;
     const float *Kb = p.k + h * dh, *Vb = p.v + h * dh;
+    const float c0 = key_bias_c0(p, b);
 
-    RowFrag<BF16, D> qf;
-    qf.load(p.q + h * dh + ((size_t)b * T + (q_ok ? q : 0)) * p.ldq, q_ok, lh, dh);
+    // bf16: q carries scale * log2 e (scores come out of the MFMA in the log2 domain)
     const float sl2 = p.scale * kLog2e;
+    RowFrag<BF16, D> qf;
+    qf.load(p.q + h * dh + ((size_t)b * T + (q_ok ? q : 0)) * p.ldq, q_ok, lh, dh, BF16 ? sl2 : 1.f);
 
     f32x16 acc[Gm::NT];
 #pragma unroll
@@ -314,16 +348,12 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
     auto load = [&](int k0) {
         lk.load(Kb, p.ldq, b, T, k0, tid, dh);
         lv.load(Vb, p.ldq, b, T, k0, tid, dh);
-        {
-            const int key = k0 + (tid & (kTile - 1));
-            const float raw = *(p.key_bias ? p.key_bias + (size_t)b * T + min(key, T - 1) : p.q);
-            bias_r = key < T ? (p.key_bias ? raw * kLog2e : 0.f) : -INFINITY;
-        }
+        bias_r = stage_bias(p, b, k0 + (tid & (kTile - 1)), c0);
     };
     auto store = [&](int buf) {
-        lk.store(Ks + buf * Gm::RE, nullptr, tid);
-        lv.store(nullptr, Vt + buf * (BF16 ? Gm::RE : Gm::TE), tid);
-        if (tid < kTile) bias_s[buf * kTile + tid] = bias_r;
+        lk.store(Ks + buf * Gm::RE, nullptr, tid, dh);
+        lv.store(nullptr, Vt + buf * (BF16 ? Gm::RE : Gm::TE), tid, dh);
+        store_bias(bias_s, flag_s, buf, bias_r, tid);
     };
     const bool drop = p.dropout_p > 0.f;
     uint32_t s0 = 0, s1 = 0;
@@ -336,6 +366,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
     auto compute = [&](int buf, int k0) {
         const ST *K_ = Ks + buf * Gm::RE, *V_ = Vt + buf * (BF16 ? Gm::RE : Gm::TE);
         const float *bs = bias_s + buf * kTile;
+        const bool tb = flag_s[buf] != 0;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
             f32x16 sacc;
@@ -345,21 +376,29 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
             float s[16], mx = -INFINITY;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
-                s[v] = sacc[v] * sl2 + bs[sub * 32 + crow(v, lh)];
+                s[v] = BF16 ? sacc[v] : sacc[v] * sl2;
+                if (tb) s[v] += bs[sub * 32 + crow(v, lh)];
                 mx = fmaxf(mx, s[v]);
             }
             mx = fmaxf(mx, __shfl_xor(mx, 32));
-            const float m_new = fmaxf(m, mx);
-            const float corr = exp2f(m - m_new);  // m = -inf on the first tile -> 0
+            if (__any(mx > m + kDefer)) {  // m = -inf before the first sub-tile: always taken there
+                const float m_new = fmaxf(m, mx);
+                const float corr = exp2f(m - m_new);
+                l *= corr;
+#pragma unroll
+                for (int t = 0; t < Gm::NT; ++t)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) acc[t][v] *= corr;
+                m = m_new;
+            }
             float rs = 0.f;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
-                s[v] = exp2f(s[v] - m_new);
+                s[v] = exp2f(s[v] - m);
                 rs += s[v];
             }
             rs += __shfl_xor(rs, 32);
-            l = l * corr + rs;
-            m = m_new;
+            l += rs;
             if (drop) {  // dropout on the probabilities (the normalizer l keeps the undropped sum)
 #pragma unroll
                 for (int v = 0; v < 16; ++v)
@@ -368,11 +407,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
                                : 0.f;
             }
 #pragma unroll
-            for (int t = 0; t < Gm::NT; ++t) {
-#pragma unroll
-                for (int v = 0; v < 16; ++v) acc[t][v] *= corr;
-                mma_perm<BF16, D>(acc[t], V_, t * 32 + lr, sub, lh, s);  // O^T += V^T P^T
-            }
+            for (int t = 0; t < Gm::NT; ++t) mma_perm<BF16, D>(acc[t], V_, t * 32 + lr, sub, lh, s);  // O^T += V^T P^T
         }
     };
     tile_loop<NB>((T + kTile - 1) / kTile, load, store, compute);
@@ -395,7 +430,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
 // ------------------------------------------------------------------------------------------------
 // backward, dQ: grid (ceil(T/128), H, B); lane = query.  Also writes Drow = rowsum(dO * O) for dKV.
 template <bool BF16, int D>
-__global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p, mtts_attn_grads g, float *Drow) {
+__global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(mtts_attn_args p, mtts_attn_grads g, float *Drow) {
     using Gm = G<BF16, D>;
     using ST = typename Gm::T;
     constexpr int NB = nbuf(dq_stage<BF16, D>());
@@ -405,6 +440,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p,
     ST *Vs = carve<ST>(sp, NB * Gm::RE);
     ST *Kt = BF16 ? Ks : carve<ST>(sp, NB * Gm::TE);  // bf16: K^T is read from the K image
     float *bias_s = carve<float>(sp, NB * kTile);
+    int *flag_s = carve<int>(sp, NB);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
     const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
@@ -413,8 +449,9 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p,
     const size_t qrow = (size_t)b * T + (q_ok ? q : 0);
     const float *Kb = p.k + h * dh, *Vb = p.v + h * dh;
 
+    const float sl2 = p.scale * kLog2e, c0 = key_bias_c0(p, b);
     RowFrag<BF16, D> qf, gf;
-    qf.load(p.q + h * dh + qrow * p.ldq, q_ok, lh, dh);
+    qf.load(p.q + h * dh + qrow * p.ldq, q_ok, lh, dh, BF16 ? sl2 : 1.f);  // as the forward's
     gf.load(g.dout + h * dh + qrow * g.lddo, q_ok, lh, dh);
     // Drow[q] = sum_d dO[q,d] * O[q,d]: each half-wave lane sums D/2 dims
     float dsum = 0.f;
@@ -433,7 +470,6 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p,
     const size_t srow = ((size_t)b * p.H + h) * T + (q_ok ? q : 0);
     const float lse2 = q_ok ? p.lse[srow] : 0.f;
     if (q_ok && lh == 0) Drow[srow] = dsum;
-    const float sl2 = p.scale * kLog2e;
 
     f32x16 acc[Gm::NT];
 #pragma unroll
@@ -446,16 +482,12 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p,
     auto load = [&](int k0) {
         lk.load(Kb, p.ldq, b, T, k0, tid, dh);
         lv.load(Vb, p.ldq, b, T, k0, tid, dh);
-        {
-            const int key = k0 + (tid & (kTile - 1));
-            const float raw = *(p.key_bias ? p.key_bias + (size_t)b * T + min(key, T - 1) : p.q);
-            bias_r = key < T ? (p.key_bias ? raw * kLog2e : 0.f) : -INFINITY;
-        }
+        bias_r = stage_bias(p, b, k0 + (tid & (kTile - 1)), c0);
     };
     auto store = [&](int buf) {
-        lk.store(Ks + buf * Gm::RE, BF16 ? nullptr : Kt + buf * Gm::TE, tid);
-        lv.store(Vs + buf * Gm::RE, nullptr, tid);
-        if (tid < kTile) bias_s[buf * kTile + tid] = bias_r;
+        lk.store(Ks + buf * Gm::RE, BF16 ? nullptr : Kt + buf * Gm::TE, tid, dh);
+        lv.store(Vs + buf * Gm::RE, nullptr, tid, dh);
+        store_bias(bias_s, flag_s, buf, bias_r, tid);
     };
     const bool drop = p.dropout_p > 0.f;
     uint32_t s0 = 0, s1 = 0;
@@ -465,26 +497,39 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p,
     }
     const float inv_keep = 1.f / (1.f - p.dropout_p);
     const uint32_t prow = (uint32_t)srow;
+    // bf16 without dropout: the row constants start the accumulators (S^T - lse, dP^T - D), so the
+    // chains end ready for exp2 and the product
+    const bool fold = BF16 && !drop;
     auto compute = [&](int buf, int k0) {
         const ST *K_ = Ks + buf * Gm::RE, *V_ = Vs + buf * Gm::RE, *KT_ = BF16 ? K_ : Kt + buf * Gm::TE;
         const float *bs = bias_s + buf * kTile;
+        const bool tb = flag_s[buf] != 0;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
             f32x16 sacc, pacc;
 #pragma unroll
-            for (int v = 0; v < 16; ++v) sacc[v] = pacc[v] = 0.f;
+            for (int v = 0; v < 16; ++v) {
+                sacc[v] = BF16 ? -lse2 : 0.f;
+                pacc[v] = fold ? -dsum : 0.f;
+            }
             mma_rows<BF16, D>(sacc, K_, sub * 32 + lr, lh, qf);  // S^T
             mma_rows<BF16, D>(pacc, V_, sub * 32 + lr, lh, gf);  // dP^T = V dO^T
             float ds[16];
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
-                const float pr = exp2f(sacc[v] * sl2 + bs[sub * 32 + crow(v, lh)] - lse2);
-                float dp = pacc[v];  // dL/d(dropped P) -> dL/dP through the regenerated mask
-                if (drop)
-                    dp = mtts::dropout_keep(s0, s1, prow, (uint32_t)(k0 + sub * 32 + crow(v, lh)), p.dropout_p)
-                             ? dp * inv_keep
-                             : 0.f;
-                ds[v] = pr * (dp - dsum);
+                float x = BF16 ? sacc[v] : sacc[v] * sl2 - lse2;
+                if (tb) x += bs[sub * 32 + crow(v, lh)];
+                const float pr = exp2f(x);
+                if (fold) {
+                    ds[v] = pr * pacc[v];
+                } else {
+                    float dp = pacc[v];  // dL/d(dropped P) -> dL/dP through the regenerated mask
+                    if (drop)
+                        dp = mtts::dropout_keep(s0, s1, prow, (uint32_t)(k0 + sub * 32 + crow(v, lh)), p.dropout_p)
+                                 ? dp * inv_keep
+                                 : 0.f;
+                    ds[v] = pr * (dp - dsum);
+                }
             }
 #pragma unroll
             for (int t = 0; t < Gm::NT; ++t) mma_perm<BF16, D>(acc[t], KT_, t * 32 + lr, sub, lh, ds);  // dQ^T += K^T dS^T
@@ -509,7 +554,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(mtts_attn_args p,
 // ------------------------------------------------------------------------------------------------
 // backward, dK/dV: grid (ceil(T/128), H, B); lane = key.  C layout: rows = queries, col = key.
 template <bool BF16, int D>
-__global__ __launch_bounds__(kThreads) void attn_bwd_dkv_kernel(mtts_attn_args p, mtts_attn_grads g,
+__global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_dkv_kernel(mtts_attn_args p, mtts_attn_grads g,
                                                                 const float *Drow) {
     using Gm = G<BF16, D>;
     using ST = typename Gm::T;
@@ -529,11 +574,11 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkv_kernel(mtts_attn_args p
     const bool k_ok = key < T;
     const size_t krow = (size_t)b * T + (k_ok ? key : 0);
 
+    const float sl2 = p.scale * kLog2e, c0 = key_bias_c0(p, b);
     RowFrag<BF16, D> kf, vf;
-    kf.load(p.k + h * dh + krow * p.ldq, k_ok, lh, dh);
+    kf.load(p.k + h * dh + krow * p.ldq, k_ok, lh, dh, BF16 ? sl2 : 1.f);  // bf16: S in the log2 domain
     vf.load(p.v + h * dh + krow * p.ldq, k_ok, lh, dh);
-    const float sl2 = p.scale * kLog2e;
-    const float bias2 = (k_ok && p.key_bias) ? p.key_bias[krow] * kLog2e : 0.f;
+    const float bias2 = (k_ok && p.key_bias) ? (p.key_bias[krow] - c0) * kLog2e : 0.f;
     const float *Qb = p.q + h * dh, *Gb = g.dout + h * dh;
     const size_t sbase = ((size_t)b * p.H + h) * T;
 
@@ -556,8 +601,8 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkv_kernel(mtts_attn_args p
         }
     };
     auto store = [&](int buf) {
-        lq.store(Qs + buf * Gm::RE, BF16 ? nullptr : Qt + buf * Gm::TE, tid);
-        lg.store(Gs + buf * Gm::RE, BF16 ? nullptr : Gt + buf * Gm::TE, tid);
+        lq.store(Qs + buf * Gm::RE, BF16 ? nullptr : Qt + buf * Gm::TE, tid, dh);
+        lg.store(Gs + buf * Gm::RE, BF16 ? nullptr : Gt + buf * Gm::TE, tid, dh);
         if (tid < kTile) {
             lse_s[buf * kTile + tid] = lse_r;
             d_s[buf * kTile + tid] = d_r;
@@ -570,6 +615,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkv_kernel(mtts_attn_args p
         s1 = p.seed[1];
     }
     const float inv_keep = 1.f / (1.f - p.dropout_p);
+    const bool fold = BF16 && !drop;  // row constants start the accumulators (as in the dQ kernel)
     auto compute = [&](int buf, int q0) {
         const ST *Q_ = Qs + buf * Gm::RE, *G_ = Gs + buf * Gm::RE;
         const ST *QT_ = BF16 ? Q_ : Qt + buf * Gm::TE, *GT_ = BF16 ? G_ : Gt + buf * Gm::TE;
@@ -578,22 +624,31 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkv_kernel(mtts_attn_args p
         for (int sub = 0; sub < 2; ++sub) {
             f32x16 sacc, pacc;
 #pragma unroll
-            for (int v = 0; v < 16; ++v) sacc[v] = pacc[v] = 0.f;
+            for (int v = 0; v < 16; ++v) {
+                const int qi = sub * 32 + crow(v, lh);
+                sacc[v] = BF16 ? bias2 - ls[qi] : 0.f;
+                pacc[v] = fold ? -dd[qi] : 0.f;
+            }
             mma_rows<BF16, D>(sacc, Q_, sub * 32 + lr, lh, kf);  // S = Q K^T (rows q, col = this key)
             mma_rows<BF16, D>(pacc, G_, sub * 32 + lr, lh, vf);  // dP = dO V^T
             float pr[16], ds[16];
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 const int qi = sub * 32 + crow(v, lh);
-                const float pv = exp2f(sacc[v] * sl2 + bias2 - ls[qi]);
-                float dp = pacc[v];
+                const float pv = exp2f(BF16 ? sacc[v] : sacc[v] * sl2 + bias2 - ls[qi]);
                 pr[v] = pv;
-                if (drop) {  // P feeds dV through the forward's dropout mask
-                    const bool keep = mtts::dropout_keep(s0, s1, (uint32_t)(sbase + q0 + qi), (uint32_t)key, p.dropout_p);
-                    pr[v] = keep ? pv * inv_keep : 0.f;
-                    dp = keep ? dp * inv_keep : 0.f;
+                if (fold) {
+                    ds[v] = pv * pacc[v];
+                } else {
+                    float dp = pacc[v];
+                    if (drop) {  // P feeds dV through the forward's dropout mask
+                        const bool keep =
+                            mtts::dropout_keep(s0, s1, (uint32_t)(sbase + q0 + qi), (uint32_t)key, p.dropout_p);
+                        pr[v] = keep ? pv * inv_keep : 0.f;
+                        dp = keep ? dp * inv_keep : 0.f;
+                    }
+                    ds[v] = pv * (dp - dd[qi]);
                 }
-                ds[v] = pv * (dp - dd[qi]);
             }
 #pragma unroll
             for (int t = 0; t < Gm::NT; ++t) {
