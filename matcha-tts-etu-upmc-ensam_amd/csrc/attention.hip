@@ -94,9 +94,11 @@ __device__ __forceinline__ uint2 lds_tr16(const void *p) {
     return __builtin_bit_cast(uint2, v);
 }
 
-__device__ __forceinline__ uint16_t to_bf16(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// (a, b) -> one v_cvt_pk_bf16_f32 (two scalar conversions + shift/or compile to 4 instructions)
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-    return (uint32_t)to_bf16(a) | ((uint32_t)to_bf16(b) << 16);
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
 }
 // bf16 fragments are always assembled from 32-bit words: element-wise construction of bf16 / u16
 // vectors from LDS loads miscompiles here (every element comes back as element 0), like the
@@ -107,6 +109,31 @@ __device__ __forceinline__ bf16x8 frag8(const float *e) {
 }
 
 __device__ __forceinline__ int crow(int v, int lh) { return (v & 3) + 8 * (v >> 2) + 4 * lh; }
+
+// The 16 C-layout rows a lane holds are 4 runs of 4: per-row LDS constants (key bias, lse, D) are
+// read as 4 float4 (ds_read_b128) instead of 16 scalars.
+__device__ __forceinline__ void crow_load16(const float *base, int lh, float (&out)[16]) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const float4 t = *reinterpret_cast<const float4 *>(base + 8 * g + 4 * lh);
+        out[4 * g] = t.x;
+        out[4 * g + 1] = t.y;
+        out[4 * g + 2] = t.z;
+        out[4 * g + 3] = t.w;
+    }
+}
+
+// x combined with the other 32-lane half's value of the same lane slot (v_permlane32_swap: no LDS)
+__device__ __forceinline__ float half_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float half_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// 2^x as the bare v_exp_f32: arguments are <= kDefer or -inf (-> 0); tiny results flush to zero
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // B-operand fragments held in registers for one row (a query or a key) of the lane: the row's D
 // dims in MFMA k-step order.
@@ -313,7 +340,7 @@ __device__ __forceinline__ void tile_loop(int ntiles, Load &&load, Store &&store
 // ------------------------------------------------------------------------------------------------
 // forward: grid (ceil(T/128), H, B); lane = query
 template <bool BF16, int D>
-__global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
+__global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_fwd_kernel(mtts_attn_args p) {
     using Gm = G<BF16, D>;
     using ST = typename Gm::T;
     constexpr int NB = nbuf(fwd_stage<BF16, D>());
@@ -363,27 +390,28 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
     }
     const float inv_keep = 1.f / (1.f - p.dropout_p);
     const uint32_t prow = (uint32_t)(((size_t)b * p.H + h) * T + q);  // dropout row key of this query
-    auto compute = [&](int buf, int k0) {
+    auto body = [&](int buf, int k0, auto has_bias) {
+        constexpr bool TB = decltype(has_bias)::value;
         const ST *K_ = Ks + buf * Gm::RE, *V_ = Vt + buf * (BF16 ? Gm::RE : Gm::TE);
         const float *bs = bias_s + buf * kTile;
-        const bool tb = flag_s[buf] != 0;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
             f32x16 sacc;
 #pragma unroll
             for (int v = 0; v < 16; ++v) sacc[v] = 0.f;
             mma_rows<BF16, D>(sacc, K_, sub * 32 + lr, lh, qf);  // S^T: rows = keys, col = this lane's query
-            float s[16], mx = -INFINITY;
+            float s[16], bv[16], mx = -INFINITY;
+            if constexpr (TB) crow_load16(bs + sub * 32, lh, bv);
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 s[v] = BF16 ? sacc[v] : sacc[v] * sl2;
-                if (tb) s[v] += bs[sub * 32 + crow(v, lh)];
+                if constexpr (TB) s[v] += bv[v];
                 mx = fmaxf(mx, s[v]);
             }
-            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            mx = half_max(mx);
             if (__any(mx > m + kDefer)) {  // m = -inf before the first sub-tile: always taken there
                 const float m_new = fmaxf(m, mx);
-                const float corr = exp2f(m - m_new);
+                const float corr = fast_exp2(m - m_new);
                 l *= corr;
 #pragma unroll
                 for (int t = 0; t < Gm::NT; ++t)
@@ -394,11 +422,10 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
             float rs = 0.f;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
-                s[v] = exp2f(s[v] - m);
+                s[v] = fast_exp2(s[v] - m);
                 rs += s[v];
             }
-            rs += __shfl_xor(rs, 32);
-            l += rs;
+            l += half_sum(rs);
             if (drop) {  // dropout on the probabilities (the normalizer l keeps the undropped sum)
 #pragma unroll
                 for (int v = 0; v < 16; ++v)
@@ -409,6 +436,12 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(mtts_attn_args p) {
 #pragma unroll
             for (int t = 0; t < Gm::NT; ++t) mma_perm<BF16, D>(acc[t], V_, t * 32 + lr, sub, lh, s);  // O^T += V^T P^T
         }
+    };
+    auto compute = [&](int buf, int k0) {  // tiles inside the valid keys skip the bias (wave-uniform)
+        if (flag_s[buf])
+            body(buf, k0, std::true_type{});
+        else
+            body(buf, k0, std::false_type{});
     };
     tile_loop<NB>((T + kTile - 1) / kTile, load, store, compute);
 
@@ -466,7 +499,7 @@ __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(
             dsum += a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
         }
     }
-    dsum += __shfl_xor(dsum, 32);
+    dsum = half_sum(dsum);
     const size_t srow = ((size_t)b * p.H + h) * T + (q_ok ? q : 0);
     const float lse2 = q_ok ? p.lse[srow] : 0.f;
     if (q_ok && lh == 0) Drow[srow] = dsum;
@@ -500,10 +533,10 @@ __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(
     // bf16 without dropout: the row constants start the accumulators (S^T - lse, dP^T - D), so the
     // chains end ready for exp2 and the product
     const bool fold = BF16 && !drop;
-    auto compute = [&](int buf, int k0) {
+    auto body = [&](int buf, int k0, auto has_bias) {
+        constexpr bool TB = decltype(has_bias)::value;
         const ST *K_ = Ks + buf * Gm::RE, *V_ = Vs + buf * Gm::RE, *KT_ = BF16 ? K_ : Kt + buf * Gm::TE;
         const float *bs = bias_s + buf * kTile;
-        const bool tb = flag_s[buf] != 0;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
             f32x16 sacc, pacc;
@@ -514,12 +547,13 @@ __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(
             }
             mma_rows<BF16, D>(sacc, K_, sub * 32 + lr, lh, qf);  // S^T
             mma_rows<BF16, D>(pacc, V_, sub * 32 + lr, lh, gf);  // dP^T = V dO^T
-            float ds[16];
+            float ds[16], bv[16];
+            if constexpr (TB) crow_load16(bs + sub * 32, lh, bv);
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 float x = BF16 ? sacc[v] : sacc[v] * sl2 - lse2;
-                if (tb) x += bs[sub * 32 + crow(v, lh)];
-                const float pr = exp2f(x);
+                if constexpr (TB) x += bv[v];
+                const float pr = fast_exp2(x);
                 if (fold) {
                     ds[v] = pr * pacc[v];
                 } else {
@@ -534,6 +568,12 @@ __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(
 #pragma unroll
             for (int t = 0; t < Gm::NT; ++t) mma_perm<BF16, D>(acc[t], KT_, t * 32 + lr, sub, lh, ds);  // dQ^T += K^T dS^T
         }
+    };
+    auto compute = [&](int buf, int k0) {
+        if (flag_s[buf])
+            body(buf, k0, std::true_type{});
+        else
+            body(buf, k0, std::false_type{});
     };
     tile_loop<NB>((T + kTile - 1) / kTile, load, store, compute);
 
@@ -623,11 +663,13 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
             f32x16 sacc, pacc;
+            float lv[16], dv16[16];
+            crow_load16(ls + sub * 32, lh, lv);
+            crow_load16(dd + sub * 32, lh, dv16);
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
-                const int qi = sub * 32 + crow(v, lh);
-                sacc[v] = BF16 ? bias2 - ls[qi] : 0.f;
-                pacc[v] = fold ? -dd[qi] : 0.f;
+                sacc[v] = BF16 ? bias2 - lv[v] : 0.f;
+                pacc[v] = fold ? -dv16[v] : 0.f;
             }
             mma_rows<BF16, D>(sacc, Q_, sub * 32 + lr, lh, kf);  // S = Q K^T (rows q, col = this key)
             mma_rows<BF16, D>(pacc, G_, sub * 32 + lr, lh, vf);  // dP = dO V^T
@@ -635,7 +677,7 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 const int qi = sub * 32 + crow(v, lh);
-                const float pv = exp2f(BF16 ? sacc[v] : sacc[v] * sl2 + bias2 - ls[qi]);
+                const float pv = fast_exp2(BF16 ? sacc[v] : sacc[v] * sl2 + bias2 - lv[v]);
                 pr[v] = pv;
                 if (fold) {
                     ds[v] = pv * pacc[v];
@@ -647,7 +689,7 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
                         pr[v] = keep ? pv * inv_keep : 0.f;
                         dp = keep ? dp * inv_keep : 0.f;
                     }
-                    ds[v] = pv * (dp - dd[qi]);
+                    ds[v] = pv * (dp - dv16[v]);
                 }
             }
 #pragma unroll

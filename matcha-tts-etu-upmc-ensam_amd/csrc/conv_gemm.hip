@@ -219,10 +219,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
             ST *dst = &As[buf][a_row[c] * LDK + a_kc[c]];
             if constexpr (BF16) {
                 uint4 w;
-                w.x = (uint32_t)to_bf16(e[0]) | ((uint32_t)to_bf16(e[1]) << 16);
-                w.y = (uint32_t)to_bf16(e[2]) | ((uint32_t)to_bf16(e[3]) << 16);
-                w.z = (uint32_t)to_bf16(e[4]) | ((uint32_t)to_bf16(e[5]) << 16);
-                w.w = (uint32_t)to_bf16(e[6]) | ((uint32_t)to_bf16(e[7]) << 16);
+                w.x = pack_bf16x2(e[0], e[1]);
+                w.y = pack_bf16x2(e[2], e[3]);
+                w.z = pack_bf16x2(e[4], e[5]);
+                w.w = pack_bf16x2(e[6], e[7]);
                 *reinterpret_cast<uint4 *>(dst) = w;
             } else {
 #pragma unroll

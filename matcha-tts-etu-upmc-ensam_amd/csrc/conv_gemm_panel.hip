@@ -34,8 +34,10 @@ constexpr int kWPad = 8;                     // bf16 elements of padding per W L
 constexpr int kWLd = kBK + kWPad;            // 40 -> 80-byte rows
 constexpr int kWChunks = kBN * kBK / 8 / kThreads;  // 16-byte W chunks per thread per K step (= 4)
 
-__device__ __forceinline__ uint32_t pack2(float a, float b) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)b) << 16);
+typedef float f32x2p __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2p __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack2(float a, float b) {  // one v_cvt_pk_bf16_f32
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2p){a, b}, bf16x2p));
 }
 
 struct PanelGeom {
