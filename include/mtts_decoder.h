@@ -256,6 +256,40 @@ int mtts_clip_adamw(const mtts_adamw_chunk *chunks, int32_t nchunks, float *para
                     float *exp_avg_sq, const float *lr, float *step, float max_norm, float beta1, float beta2,
                     float eps, float weight_decay, void *workspace, size_t workspace_bytes, void *hip_stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Partial-sum reductions of the parameter gradients, batched.
+ *
+ * The weight-gradient GEMMs (mtts_conv_wgrad*) and the norm backwards (mtts_layernorm_bwd,
+ * mtts_gn_mish_bwd) produce fp32 partial slabs and sum them in a fixed order (deterministic, no
+ * float atomics).  One job:
+ *     out[map(i)] (+)= sum_{s < splits} part[s * stride + i]      for i < n
+ * with map(i) = i (cols == 0), or for cols > 0 the weight-gradient layout: i = r*cols + k,
+ * k = j*cin + c -> r*sr + c*sc + j*sj.  mtts_reduce_partials runs the jobs now (one launch per 32).
+ *
+ * Deferral: between mtts_defer_reductions(1) and mtts_defer_reductions(0) the backward entry points
+ * queue their reduction jobs instead of launching them; mtts_flush_reductions(stream) then runs the
+ * whole queue as ONE batched launch (the ~120 per-layer reduce launches of a training step become a
+ * few), mtts_discard_reductions() drops it.  The caller keeps the producers' workspaces alive and
+ * reads none of the outputs until the flush, on a stream ordered after every producer.  Process-wide
+ * state (autograd runs backward functions on its own thread).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct mtts_reduce_job {
+    const float *part;
+    float *out;
+    int64_t stride; /* floats between consecutive slabs, >= n */
+    int64_t n;      /* elements per slab */
+    int32_t splits;
+    int32_t accumulate;
+    int32_t cols, cin; /* cols == 0: out[i]; else the weight layout above */
+    int64_t sr, sc, sj;
+} mtts_reduce_job;
+
+int mtts_reduce_partials(const mtts_reduce_job *jobs, int32_t njobs, void *hip_stream);
+void mtts_defer_reductions(int32_t on);
+int32_t mtts_pending_reductions(void);
+int mtts_flush_reductions(void *hip_stream);
+void mtts_discard_reductions(void);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

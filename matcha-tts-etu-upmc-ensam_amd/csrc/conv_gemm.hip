@@ -19,8 +19,9 @@
 //   fp32 path: v_mfma_f32_32x32x2_f32   (exact fp32 products, the parity mode)
 //
 // wgrad (conv_wgrad_kernel): dW[n][k] = sum_rows dY[row][n] * A_gathered[row][k], the reduction over
-// tokens split across blocks into fp32 partial slabs (deterministic), reduced by wgrad_reduce_kernel
-// which also emits the bias gradient (column sums of dY, accumulated in the k-tile-0 blocks).
+// tokens split across blocks into fp32 partial slabs (deterministic) that reduce.hip sums in a fixed
+// order -- at once, or batched with the step's other gradient sums -- together with the bias gradient
+// (column sums of dY, accumulated in the k-tile-0 blocks).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -650,65 +651,6 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
     }
 }
 
-// dW (and db) = sum over splits, written in the caller's layout: w_out[n*sn + c*sc + j*sj]
-// for k = j*cin + c.  A block owns 64 float4 groups of the (n, k) slab (NK % 4 == 0); its 4 waves take
-// interleaved quarters of the splits (wave g: splits g, g+4, ...; four float4 loads in flight per
-// lane), and the quarters are combined through LDS in a fixed order -- deterministic, and 4x the
-// waves of one-thread-per-group so enough slab reads are in flight to stream at HBM rate.
-constexpr int kRedGroups = 64;
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restrict__ part,
-                                                           const float *__restrict__ part_db, int splits, int N,
-                                                           int K, int cin, int64_t sn, int64_t sc, int64_t sj,
-                                                           float *__restrict__ w_out, float *__restrict__ db_out,
-                                                           int accumulate) {
-    __shared__ float4 red[4][kRedGroups];
-    const int t = threadIdx.x & (kRedGroups - 1), g = threadIdx.x >> 6;
-    const int64_t q = (int64_t)blockIdx.x * kRedGroups + t;
-    const int64_t NK = (int64_t)N * K, step = NK / 4;
-    const bool on = q < step;
-    const float4 *src = reinterpret_cast<const float4 *>(part) + (on ? q : 0);
-    float4 a[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) a[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-    int i = g;
-    for (; i + 12 < splits; i += 16) {
-        float4 v[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = src[(int64_t)(i + 4 * c) * step];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            a[c].x += v[c].x; a[c].y += v[c].y; a[c].z += v[c].z; a[c].w += v[c].w;
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < 3; ++c)  // i + 12 >= splits: at most 3 left
-        if (i + 4 * c < splits) {
-            const float4 v = src[(int64_t)(i + 4 * c) * step];
-            a[c].x += v.x; a[c].y += v.y; a[c].z += v.z; a[c].w += v.w;
-        }
-    red[g][t] = make_float4((a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y),
-                            (a[0].z + a[1].z) + (a[2].z + a[3].z), (a[0].w + a[1].w) + (a[2].w + a[3].w));
-    __syncthreads();
-    if (g == 0 && on) {
-        const float4 r0 = red[0][t], r1 = red[1][t], r2 = red[2][t], r3 = red[3][t];
-        const float r[4] = {(r0.x + r1.x) + (r2.x + r3.x), (r0.y + r1.y) + (r2.y + r3.y),
-                            (r0.z + r1.z) + (r2.z + r3.z), (r0.w + r1.w) + (r2.w + r3.w)};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int64_t idx = q * 4 + e;
-            const int n = (int)(idx / K), k = (int)(idx - (int64_t)n * K);
-            const int j = k / cin, c = k - j * cin;
-            float *dst = w_out + n * sn + c * sc + j * sj;
-            *dst = accumulate ? *dst + r[e] : r[e];
-        }
-    }
-    if (db_out && g == 1 && q < N) {
-        float s = 0.f;
-        for (int z = 0; z < splits; ++z) s += part_db[(size_t)z * N + q];
-        db_out[q] = accumulate ? db_out[q] + s : s;
-    }
-}
-
 // The GEMM kernels compute tap offsets as off[0] + j*(off[1]-off[0]).
 bool taps_arithmetic(const int32_t *off, int ntaps) {
     for (int j = 2; j < ntaps; ++j)
@@ -1076,11 +1018,29 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
                                                  : wgrad_launch<true, 32, 1>(p, splits, rps, part, pdb, st));
         if (rc) return rc;
     }
-    const int64_t NK = (int64_t)p.N * p.K;  // K % 8 == 0 (cin % 8): float4 groups never straddle rows
-    const int64_t groups = std::max<int64_t>(NK / 4, p.N);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((groups + kRedGroups - 1) / kRedGroups)), dim3(256), 0, st,
-                       part, part_db, splits, p.N, p.K, p.cin, sn, sc, sj, dw, db, accumulate);
-    return mtts::check_launch("wgrad_reduce_kernel");
+    // sum of the split slabs (reduce.hip: now, or queued for the step's batched launch)
+    const int64_t NK = (int64_t)p.N * p.K;
+    mtts_reduce_job jobs[2] = {};
+    jobs[0].part = part;
+    jobs[0].out = dw;
+    jobs[0].stride = NK;
+    jobs[0].n = NK;
+    jobs[0].splits = splits;
+    jobs[0].accumulate = accumulate;
+    jobs[0].cols = p.K;
+    jobs[0].cin = p.cin;
+    jobs[0].sr = sn;
+    jobs[0].sc = sc;
+    jobs[0].sj = sj;
+    if (db) {
+        jobs[1].part = part_db;
+        jobs[1].out = db;
+        jobs[1].stride = p.N;
+        jobs[1].n = p.N;
+        jobs[1].splits = splits;
+        jobs[1].accumulate = accumulate;
+    }
+    return mtts::submit_reductions(jobs, db ? 2 : 1, st);
 }
 
 extern "C" int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precision, float *dw, int64_t sn,

@@ -113,6 +113,12 @@ int conv_gemm_glds_launch(int id, const mtts_conv_gemm_args &p, int M, int split
 size_t conv_gemm_glds_splitk_bytes(const mtts_conv_gemm_args &p, int splits);
 }  // namespace mtts
 
+struct mtts_reduce_job;
+namespace mtts {
+// reduce.hip: runs the partial-sum jobs now, or queues them while deferral is on
+int submit_reductions(const mtts_reduce_job *jobs, int njobs, hipStream_t st);
+}  // namespace mtts
+
 #define MTTS_CHECK_ARG(cond, msg)                                   \
     do {                                                            \
         if (!(cond)) return ::mtts::fail(MTTS_ERR_INVALID_ARG, msg); \

@@ -5,7 +5,7 @@
 //            T x C/G values stay in L1/L2 across the three passes (mean, centred variance, apply).
 //            Backward recomputes xhat / mish' from h and the saved statistics; per-(b, c) partial
 //            gamma/beta sums and the time-bias gradient come out of the same pass, and the gamma/beta
-//            partials are reduced over the batch by colsum_kernel in a fixed order (deterministic).
+//            partials are reduced over the batch in a fixed order by reduce.hip (deterministic, batchable).
 // layernorm_*: one wave per token row (norm1 / norm3 of BasicTransformerBlock, transformer.py:316,345).
 // Numerics follow torch: mish(x) = x * tanh(log1p(exp(x))), two-pass variance, biased, eps inside sqrt.
 #include <hip/hip_runtime.h>
@@ -357,40 +357,22 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_kernel(
     }
 }
 
-// out[c] = sum_r in[r*C + c] (and out2 from in2 when given) for the gamma/beta partials.  Block = 64
-// columns x 16 row-slices (1024 threads); each slice sums an interleaved 1/16 of the rows (4-way
-// unrolled, independent loads in flight), the 16 slice sums are added in a fixed order.
-constexpr int kColsumSlices = 16;
-__global__ __launch_bounds__(64 * kColsumSlices) void colsum_kernel(const float *__restrict__ in,
-                                                                    const float *__restrict__ in2, int R, int C,
-                                                                    float *__restrict__ out, float *__restrict__ out2) {
-    __shared__ float part[2][kColsumSlices][64];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int sl = threadIdx.x >> 6;
-    float s[2] = {0.f, 0.f};
-#pragma unroll
+// gamma/beta gradients = fixed-order sums of the [R][C] per-block partials (reduce.hip: now, or
+// queued for the step's batched launch)
+int submit_param_sums(const float *pa, float *outa, const float *pb, float *outb, int R, int C, hipStream_t st) {
+    mtts_reduce_job jobs[2] = {};
+    int n = 0;
     for (int w = 0; w < 2; ++w) {
-        const float *src = w ? in2 : in;
-        if (!src || c >= C) continue;
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-        int r = sl;
-        for (; r + 3 * kColsumSlices < R; r += 4 * kColsumSlices) {
-            a0 += src[(size_t)r * C + c];
-            a1 += src[(size_t)(r + kColsumSlices) * C + c];
-            a2 += src[(size_t)(r + 2 * kColsumSlices) * C + c];
-            a3 += src[(size_t)(r + 3 * kColsumSlices) * C + c];
-        }
-        for (; r < R; r += kColsumSlices) a0 += src[(size_t)r * C + c];
-        s[w] = (a0 + a1) + (a2 + a3);
+        float *out = w ? outb : outa;
+        if (!out) continue;
+        jobs[n].part = w ? pb : pa;
+        jobs[n].out = out;
+        jobs[n].stride = C;
+        jobs[n].n = C;
+        jobs[n].splits = R;
+        ++n;
     }
-    part[0][sl][threadIdx.x & 63] = s[0];
-    part[1][sl][threadIdx.x & 63] = s[1];
-    __syncthreads();
-    if (sl < 2 && c < C && (sl ? out2 : out)) {
-        float t = 0.f;
-        for (int i = 0; i < kColsumSlices; ++i) t += part[sl][i][threadIdx.x & 63];
-        (sl ? out2 : out)[c] = t;
-    }
+    return n ? mtts::submit_reductions(jobs, n, st) : MTTS_OK;
 }
 
 // ------------------------------------------------------------------------------ LayerNorm
@@ -615,10 +597,7 @@ extern "C" int mtts_gn_mish_bwd(const float *dy, const float *h, const float *ga
                            dh, pg, pb, dadd, T, C, G);
     int rc = mtts::check_launch("gn_mish_bwd_kernel");
     if (rc) return rc;
-    if (dgamma || dbeta)
-        hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(64 * kColsumSlices), 0, st, dgamma ? pg : nullptr,
-                           dbeta ? pb : nullptr, B, C, dgamma, dbeta);
-    return mtts::check_launch("colsum_kernel");
+    return submit_param_sums(pg, dgamma, pb, dbeta, B, C, st);
 }
 
 extern "C" int mtts_layernorm_fwd(const float *x, const float *w, const float *b, float *y, float *mean,
@@ -663,8 +642,5 @@ extern "C" int mtts_layernorm_bwd(const float *dy, const float *x, const float *
                        C, act, dropout_p, seed, rpb);
     int rc = mtts::check_launch("layernorm_bwd_kernel");
     if (rc) return rc;
-    if (dw || db)
-        hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(64 * kColsumSlices), 0, st, dw ? pw : nullptr,
-                           db ? pb : nullptr, nblk, C, dw, db);
-    return mtts::check_launch("colsum_kernel");
+    return submit_param_sums(pw, dw, pb, db, nblk, C, st);
 }

@@ -23,6 +23,7 @@ from __future__ import annotations
 import contextlib
 import contextvars
 import ctypes
+import functools
 import os
 import math
 
@@ -122,6 +123,11 @@ N.register("mtts_pack_weights", ctypes.c_int, [ctypes.POINTER(PackJob), _I, _I, 
 N.register("mtts_attention_fwd", ctypes.c_int, [ctypes.POINTER(AttnArgs), _I, _P])
 N.register("mtts_attention_bwd_workspace_size", _SZ, [_I, _I, _I])
 N.register("mtts_attention_bwd", ctypes.c_int, [ctypes.POINTER(AttnArgs), ctypes.POINTER(AttnGrads), _I, _P, _SZ, _P])
+N.register("mtts_reduce_partials", ctypes.c_int, [_P, _I, _P])
+N.register("mtts_defer_reductions", None, [_I])
+N.register("mtts_pending_reductions", _I, [])
+N.register("mtts_flush_reductions", ctypes.c_int, [_P])
+N.register("mtts_discard_reductions", None, [])
 
 
 # ------------------------------------------------------------------------------------------ helpers
@@ -390,6 +396,63 @@ def join_side_streams():
     _SIDE_WGRAD["keep"].clear()
 
 
+# Parameter-gradient sums deferred to one batched launch (csrc/reduce.hip): inside
+# deferred_grad_sums() the weight-gradient GEMMs and the norm backwards only QUEUE the fixed-order sums
+# of their partial slabs; the context exit runs the queue as one launch instead of ~120 small ones.
+# The workspaces holding the partials are kept alive until then.  Valid only while nothing reads a
+# parameter gradient before the exit: fresh gradients (AccumulateGrad steals them, no copy kernel) of
+# LEAF weights -- a Function whose weights are not all leaves (ctx.leaf False) sums at once.
+_DEFER = {"on": False, "keep": []}
+
+
+def _leaves(*ts) -> bool:
+    return all(t is None or t.is_leaf for t in ts)
+
+
+def _keep_partials(*ts):
+    if _DEFER["on"]:
+        _DEFER["keep"].extend(t for t in ts if t is not None)
+
+
+@contextlib.contextmanager
+def deferred_grad_sums(enabled: bool = True):
+    if not enabled or _DEFER["on"]:
+        yield
+        return
+    lib = N.lib()
+    lib.mtts_defer_reductions(1)
+    _DEFER["on"] = True
+    ok = False
+    try:
+        yield
+        ok = True
+    finally:
+        lib.mtts_defer_reductions(0)
+        _DEFER["on"] = False
+        try:
+            if ok:
+                N.check(lib.mtts_flush_reductions(torch.cuda.current_stream().cuda_stream), "mtts_flush_reductions")
+            else:
+                lib.mtts_discard_reductions()
+        finally:
+            _DEFER["keep"].clear()  # stream-ordered frees, after the flush launch
+
+
+def _grad_sums(backward):
+    """Backward decorator: a Function with non-leaf weights sums its partials at once."""
+    @functools.wraps(backward)
+    def run(ctx, *grads):
+        if not _DEFER["on"] or getattr(ctx, "leaf", True):
+            return backward(ctx, *grads)
+        lib = N.lib()
+        lib.mtts_defer_reductions(0)
+        try:
+            return backward(ctx, *grads)
+        finally:
+            lib.mtts_defer_reductions(1)
+    return run
+
+
 def _wgrad(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin, N_, dw, strides, *, prec,
            a_scale=None, db=None, rows_per_step=-1, target_blocks=-1, depth=-1):
     if _SIDE_WGRAD["on"] and dY.is_cuda:
@@ -422,6 +485,7 @@ def _wgrad_launch(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, of
     args.flags = GEMM_F_A_BF16 if A.dtype == torch.bfloat16 else 0
     lib = N.lib()
     ws = torch.empty(int(lib.mtts_conv_wgrad_workspace_size(ctypes.byref(args))), dtype=torch.uint8, device=dY.device)
+    _keep_partials(ws)
     rc = lib.mtts_conv_wgrad_tile(ctypes.byref(args), prec, rows_per_step, target_blocks, depth, dw.data_ptr(), strides[0],
                                   strides[1], strides[2], N.ptr(db), 0, ws.data_ptr(), ws.numel(), _stream(dY))
     N.check(rc, "mtts_conv_wgrad")
@@ -461,10 +525,12 @@ class _ConvTM(torch.autograd.Function):
               a_scale=mask, bias=bias_c, c_scale=out_scale, act=act, dropout_p=dropout_p, seed=seed,
               residual=_f32c(residual))
         ctx.save_for_backward(x, weight, mask, out_scale, y if act != ACT_NONE else None)
+        ctx.leaf = _leaves(weight, bias)
         ctx.cfg = (stride, padding, prec, bias is not None, act, dropout_p, seed, residual is not None)
         return y
 
     @staticmethod
+    @_grad_sums
     def backward(ctx, dy):
         x, weight, mask, out_scale, y = ctx.saved_tensors
         stride, pad, prec, has_bias, act, p, seed, has_res = ctx.cfg
@@ -531,10 +597,12 @@ class _ConvTransposeTM(torch.autograd.Function):
                   prec=prec, a_scale=mask, bias=bias_c)
         ctx.wd = packed(spec_convT_dgrad(weight), prec) if ctx.needs_input_grad[0] else None
         ctx.save_for_backward(x, weight, mask)
+        ctx.leaf = _leaves(weight, bias)
         ctx.cfg = (prec, bias is not None)
         return y
 
     @staticmethod
+    @_grad_sums
     def backward(ctx, dy):
         x, weight, mask = ctx.saved_tensors
         prec, has_bias = ctx.cfg
@@ -583,12 +651,14 @@ class _LinearTM(torch.autograd.Function):
         _gemm(x2, M, M, 1, 1, [0], K, Wp, Kp, Nout, y, M, prec=prec, bias=_f32c(bias), residual=res2,
               dropout_p=dropout_p, seed=seed, a_scale=ins, c_scale=outs)
         ctx.save_for_backward(x2, ins, outs)
+        ctx.leaf = _leaves(bias, *weights)
         ctx.cfg = (prec, bias is not None, residual is not None, shp, dropout_p, seed,
                    [w.shape[0] for w in weights], K)
         ctx.wshapes = [w.shape for w in weights]
         return y.reshape(*shp[:-1], Nout)
 
     @staticmethod
+    @_grad_sums
     def backward(ctx, dy):
         x2, ins, outs = ctx.saved_tensors
         prec, has_bias, has_res, shp, p, seed, rows, K = ctx.cfg
@@ -653,10 +723,12 @@ class _FeedForwardTM(torch.autograd.Function):
         res2 = _f32c(residual).reshape(M, Nout) if residual is not None else None
         _gemm(h, M, M, 1, 1, [0], H, W2p, K2p, Nout, y, M, prec=prec, bias=_f32c(b2), residual=res2)
         ctx.save_for_backward(x2, z, h, w1, w2)
+        ctx.leaf = _leaves(w1, b1, w2, b2)
         ctx.cfg = (prec, shp, residual is not None, dropout_p, seed, b1 is not None, b2 is not None)
         return y.reshape(*shp[:-1], Nout)
 
     @staticmethod
+    @_grad_sums
     def backward(ctx, dy):
         x2, z, h, w1, w2 = ctx.saved_tensors
         prec, shp, has_res, p, seed, has_b1, has_b2 = ctx.cfg
@@ -719,10 +791,12 @@ class _ConvFFNTM(torch.autograd.Function):
         _gemm(h, T, T, B, 1, offs, F_, W2p, K2p, Cout, y, T, prec=prec, bias=_f32c(b2), dropout_p=p_out,
               seed=s2, residual=_f32c(residual), c_scale=m)
         ctx.save_for_backward(x, h, m)
+        ctx.leaf = _leaves(w1, b1, w2, b2)
         ctx.cfg = (prec, k, p_in, p_out, s1, s2, residual is not None, w1.shape, w2.shape)
         return y
 
     @staticmethod
+    @_grad_sums
     def backward(ctx, dy):
         x, h, m = ctx.saved_tensors
         prec, k, p_in, p_out, s1, s2, has_res, w1s, w2s = ctx.cfg
@@ -777,10 +851,12 @@ class _GroupNormMishTM(torch.autograd.Function):
                                          N.ptr(add_c), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), B, T, C,
                                          groups, float(eps), _stream(h)), "mtts_gn_mish_fwd")
         ctx.save_for_backward(h, gamma_c, beta_c, mask_c, mean, rstd)
+        ctx.leaf = _leaves(gamma, beta)
         ctx.cfg = (groups, add is not None)
         return y
 
     @staticmethod
+    @_grad_sums
     def backward(ctx, dy):
         h, gamma, beta, mask, mean, rstd = ctx.saved_tensors
         groups, has_add = ctx.cfg
@@ -792,6 +868,7 @@ class _GroupNormMishTM(torch.autograd.Function):
         dadd = torch.empty(B, C, device=h.device, dtype=torch.float32) if has_add else None
         lib = N.lib()
         ws = torch.empty(int(lib.mtts_gn_mish_bwd_workspace_size(B, C)), dtype=torch.uint8, device=h.device)
+        _keep_partials(ws)
         N.check(lib.mtts_gn_mish_bwd(dy.data_ptr(), h.data_ptr(), gamma.data_ptr(), beta.data_ptr(), N.ptr(mask),
                                      mean.data_ptr(), rstd.data_ptr(), dh.data_ptr(), dg.data_ptr(), dbt.data_ptr(),
                                      N.ptr(dadd), B, T, C, groups, ws.data_ptr(), ws.numel(), _stream(h)),
@@ -818,10 +895,12 @@ class _LayerNormTM(torch.autograd.Function):
                                            mean.data_ptr(), rstd.data_ptr(), M, C, float(eps), act, float(dropout_p),
                                            N.ptr(seed), _stream(x2)), "mtts_layernorm_fwd")
         ctx.save_for_backward(x2, w_c, b_c, mean, rstd)
+        ctx.leaf = _leaves(w, b)
         ctx.cfg = (shp, act, float(dropout_p), seed)
         return y.reshape(shp)
 
     @staticmethod
+    @_grad_sums
     def backward(ctx, dy):
         x2, w, b, mean, rstd = ctx.saved_tensors
         shp, act, p, seed = ctx.cfg
@@ -833,6 +912,7 @@ class _LayerNormTM(torch.autograd.Function):
         lib = N.lib()
         ws = torch.empty(max(int(lib.mtts_layernorm_bwd_workspace_size(M, C)), 1), dtype=torch.uint8,
                          device=x2.device)
+        _keep_partials(ws)
         N.check(lib.mtts_layernorm_bwd(dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), b.data_ptr(), mean.data_ptr(),
                                        rstd.data_ptr(), dx.data_ptr(), dw.data_ptr(), db.data_ptr(), M, C, act, p,
                                        N.ptr(seed), ws.data_ptr(), ws.numel(), _stream(x2)), "mtts_layernorm_bwd")

@@ -166,6 +166,7 @@ class Trainer:
     # opt-in: measured in-step on MI355X the graph step got 0.25 ms SLOWER with weight gradients on a
     # side stream (11.25 vs 11.01 ms): the ~100 cross-stream edges cost more than the overlap returns
     side_stream_wgrad = os.environ.get("MTTS_SIDE_WGRAD", "0") == "1"
+    defer_grad_sums = os.environ.get("MTTS_DEFER_GRAD_SUMS", "1") != "0"
 
     def __init__(self, model: MatchaTTS, cfg: TrainConfig = TrainConfig()):
         self.cfg = cfg
@@ -214,9 +215,13 @@ class Trainer:
         # weight gradients on a side stream, overlapping the dgrad chain (components/_ops.py
         # side_stream_wgrad): safe when autograd steals every fresh gradient (graph step, one
         # micro-batch, gradients set to None first); joined before this returns
-        side = (self.cfg.graph and n == 1 and self.dev.type == "cuda" and self.side_stream_wgrad
-                and all(p.grad is None for p in self.params))
-        with OPS.side_stream_wgrad(side):
+        fresh = n == 1 and self.dev.type == "cuda" and all(p.grad is None for p in self.params)
+        side = self.cfg.graph and fresh and self.side_stream_wgrad
+        # the parameter-gradient partial sums of the whole backward in one batched launch
+        # (components/_ops.py deferred_grad_sums): also needs fresh gradients, and no DDP hook
+        # reading them during the backward
+        defer = fresh and self.defer_grad_sums and not side and (self.cfg.graph or self.world == 1)
+        with OPS.deferred_grad_sums(defer), OPS.side_stream_wgrad(side):
             return self._fwd_bwd_body(batches, sync_ctx)
 
     def _fwd_bwd_body(self, batches, sync_ctx=None):

@@ -324,3 +324,45 @@ def test_bf16_operand_storage_bitwise(B, T, Cin, Cout, k, cfg):
         outs.append((dw, db))
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_reduce_partials_jobs():
+    """csrc/reduce.hip against torch sums: plain and weight-layout jobs, float4 and scalar paths (n % 4),
+    long narrow jobs (16 slices), accumulate, several jobs in one batched launch."""
+    import ctypes
+
+    from matcha import _native as N
+    from matcha.models.components import _ops as O  # registers the entry points
+
+    class Job(ctypes.Structure):
+        _fields_ = [("part", ctypes.c_void_p), ("out", ctypes.c_void_p), ("stride", ctypes.c_int64),
+                    ("n", ctypes.c_int64), ("splits", ctypes.c_int32), ("accumulate", ctypes.c_int32),
+                    ("cols", ctypes.c_int32), ("cin", ctypes.c_int32), ("sr", ctypes.c_int64),
+                    ("sc", ctypes.c_int64), ("sj", ctypes.c_int64)]
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    cases = []  # (part [S, stride], out tensor, expected, job)
+    # plain, vector path, accumulate
+    p0 = torch.randn(7, 1024, device=DEV, generator=g)
+    o0 = torch.randn(1024, device=DEV, generator=g)
+    cases.append((p0, o0, o0 + p0.sum(0), dict(stride=1024, n=1024, splits=7, accumulate=1)))
+    # plain, scalar path (n % 4 != 0, stride > n), long narrow (16 slices)
+    p1 = torch.randn(300, 258, device=DEV, generator=g)
+    o1 = torch.zeros(255, device=DEV)
+    cases.append((p1, o1, p1[:, :255].sum(0), dict(stride=258, n=255, splits=300, accumulate=0)))
+    # weight layout: slab [N][K], K = taps*cin -> out[n, c, j] of a [N][cin][taps] conv weight
+    Nn, cin, taps, S = 24, 16, 3, 5
+    p2 = torch.randn(S, Nn * cin * taps, device=DEV, generator=g)
+    o2 = torch.zeros(Nn, cin, taps, device=DEV)
+    e2 = p2.sum(0).view(Nn, taps, cin).permute(0, 2, 1)
+    cases.append((p2, o2, e2, dict(stride=Nn * cin * taps, n=Nn * cin * taps, splits=S, accumulate=0,
+                                   cols=cin * taps, cin=cin, sr=cin * taps, sc=taps, sj=1)))
+    jobs = (Job * len(cases))()
+    for i, (p, o, _, kw) in enumerate(cases):
+        jobs[i] = Job(part=p.data_ptr(), out=o.data_ptr(), **kw)
+    N.check(N.lib().mtts_reduce_partials(jobs, len(cases), torch.cuda.current_stream().cuda_stream),
+            "mtts_reduce_partials")
+    torch.cuda.synchronize()
+    for p, o, e, _ in cases:
+        torch.testing.assert_close(o, e, rtol=1e-5, atol=1e-4)
+    assert O is not None

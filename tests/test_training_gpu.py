@@ -93,3 +93,38 @@ def test_side_stream_wgrad_matches_main_stream():
             assert torch.equal(g1[n], g0[n]), n
         else:
             torch.testing.assert_close(g1[n], g0[n], rtol=1e-4, atol=1e-6)
+
+
+def test_deferred_grad_sums_match_immediate():
+    """The batched, deferred parameter-gradient sums (csrc/reduce.hip) equal the per-layer ones bitwise
+    on the decoder (same fixed-order sums, one launch instead of one per layer)."""
+    from matcha.models.components import _ops as OPS
+    from matcha.training import synthetic_batch
+
+    b = synthetic_batch(4, 20, 80, device=DEV)
+    m = _model(3)
+    m.eval()
+    t = torch.rand(4, 1, 1, device=DEV)
+    z = torch.randn(4, 80, 80, device=DEV)
+
+    def grads(defer):
+        m.zero_grad(set_to_none=True)
+        with OPS.deferred_grad_sums(defer):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                dur, prior, diff, _ = m(**b, t=t, z=z)
+            (dur + prior + diff).backward()
+            if defer:
+                assert N.lib().mtts_pending_reductions() > 50  # queued, not yet run
+        torch.cuda.synchronize()
+        return {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+
+    from matcha import _native as N
+
+    g0, g1 = grads(False), grads(True)
+    assert N.lib().mtts_pending_reductions() == 0
+    assert g0.keys() == g1.keys() and len(g0) > 100
+    for n in g0:
+        if n.startswith("decoder."):
+            assert torch.equal(g1[n], g0[n]), n
+        else:
+            torch.testing.assert_close(g1[n], g0[n], rtol=1e-4, atol=1e-6)
