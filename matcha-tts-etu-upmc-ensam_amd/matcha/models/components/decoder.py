@@ -82,9 +82,11 @@ class Resnet1D(nn.Module):
         self.block2 = Block1D(out_channels, out_channels, kernel_size, padding, groups)
         self.res_conv = nn.Conv1d(in_channels, out_channels, 1)
 
-    def forward_tm(self, x, mask, time_emb):
-        with torch.autocast("cuda", enabled=False):  # [B, C] time projection, fp32
-            tproj = self.mlp(time_emb.float())
+    def forward_tm(self, x, mask, time_emb, tproj=None):
+        """tproj: this block's mlp(time_emb) when the caller computed every block's at once."""
+        if tproj is None:
+            with torch.autocast("cuda", enabled=False):  # [B, C] time projection, fp32
+                tproj = self.mlp(time_emb.float())
         h = self.block1.forward_tm(x, mask, add=tproj)
         h = self.block2.forward_tm(h, mask)
         # res_conv(x*m) + h with the add in the GEMM epilogue ((acc + bias) + h, torch's order)
@@ -198,32 +200,48 @@ class Decoder(nn.Module):
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec_bf16), O.weight_pack_scope(self):
                 return self._forward_tm(x.float(), mask.float(), mu.float(), t.float())
 
+    def _time_projections(self, temb):
+        """Every ResnetBlock's mlp(temb) = Linear(Mish(temb)) (decoder.py:80-81) as ONE GEMM: the Mish of
+        the shared time embedding is computed once and the blocks' Linear weights are stacked along N
+        (their gradients come back as separate views), instead of 6 x (mish, addmm) forward and
+        6 x (mish', 2 mm, bias sum, accumulate) backward launches.  fp32, like the per-block path."""
+        resnets = ([r for r, *_ in self.Downsampling_Blocks] + [r for r, _ in self.Mid_Blocks]
+                   + [r for r, *_ in self.Upsampling_Blocks])
+        lins = [r.mlp[1] for r in resnets]
+        with torch.autocast("cuda", enabled=False):
+            act = F.mish(temb.float())
+            bias = torch.cat([lin.bias for lin in lins])
+            tp = O.linear_tm(act, tuple(lin.weight for lin in lins), bias)
+        return dict(zip(map(id, resnets), tp.split([lin.out_features for lin in lins], dim=-1)))
+
     def _forward_tm(self, x, mask, mu, t):
         with torch.autocast("cuda", enabled=False):  # [B, 1024] time MLP: tiny, kept fp32
             temb = self.time_mlp(self.time_embeddings(t))
+        tps = self._time_projections(temb)
         h = torch.cat([x, mu], dim=-1)  # einops pack "b * t" on channels (:288)
         skips, masks = [], [mask]
         for resnet, tfs, down in self.Downsampling_Blocks:
             m = masks[-1]
-            h = self._transformers(tfs, resnet.forward_tm(h, m, temb), m)
+            h = self._transformers(tfs, resnet.forward_tm(h, m, temb, tps[id(resnet)]), m)
             skips.append(h)
             if isinstance(down, Downsample1D):
                 h = down.forward_tm(h, m)
-                masks.append(m[:, : (m.shape[-1] + 1) // 2])  # prefix slice (:311-316)
+                # prefix slice (:311-316), made contiguous once (every op of the level reads it)
+                masks.append(m[:, : (m.shape[-1] + 1) // 2].contiguous())
             else:
                 h = _conv_tm(down, h, m)
                 masks.append(m)
         masks = masks[:-1]
         m = masks[-1]
         for resnet, tfs in self.Mid_Blocks:
-            h = self._transformers(tfs, resnet.forward_tm(h, m, temb), m)
+            h = self._transformers(tfs, resnet.forward_tm(h, m, temb, tps[id(resnet)]), m)
         for resnet, tfs, up in self.Upsampling_Blocks:
             m = masks.pop()
             skip = skips.pop()
             if h.shape[1] != skip.shape[1]:  # odd T: nearest to the skip length (:338-339)
                 h = F.interpolate(h.transpose(1, 2), size=skip.shape[1], mode="nearest").transpose(1, 2)
             h = torch.cat([h, skip], dim=-1)
-            h = self._transformers(tfs, resnet.forward_tm(h, m, temb), m)
+            h = self._transformers(tfs, resnet.forward_tm(h, m, temb, tps[id(resnet)]), m)
             if isinstance(up, Upsample1D):
                 h = up.forward_tm(h, m)
                 new = m.shape[-1] * 2
@@ -233,7 +251,7 @@ class Decoder(nn.Module):
             if new > m.shape[-1]:
                 m = F.interpolate(m.unsqueeze(1), size=new, mode="nearest")[:, 0]
             else:
-                m = m[:, :new]
+                m = m[:, :new].contiguous()
         h = _conv_tm(self.final_conv, h, m)
         h = O.group_norm_mish_tm(h, self.final_norm.weight, self.final_norm.bias, self.final_norm.num_groups,
                                  None, None, self.final_norm.eps)  # no mask after the final Mish (:366-368)
