@@ -28,12 +28,15 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
+#include <type_traits>
 
 #include "mtts_common.h"
 
 namespace {
 
 constexpr int kWave = 64;
+constexpr int kDefaultRing = 2;  // lattice chunks in the DP ring (premasked); 3 and 4 measured equal (DP is VALU-chain bound)
 constexpr int kLdsBitsLimit = 48 * 1024;  // LDS bytes for backpointer words (total stays <= 64 KiB)
 
 struct MasArgs {
@@ -81,7 +84,15 @@ __device__ __forceinline__ void load_row_segment(const float *__restrict__ base,
     }
 }
 
-template <int K, int C, bool VEC, bool LDS_BITS, bool DP_OUT>
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+template <int K, int C, int D, bool PM, bool VEC, bool LDS_BITS, bool DP_OUT>
 __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
     extern __shared__ uint32_t smem[];
     const int b = blockIdx.x;
@@ -130,8 +141,7 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
         for (int i = 0; i < K; ++i) roff[i] = min(x0 + i, Tx - 1) * Ty;
         const int last = Tx * Ty - 1;
         const float *vbase = a.value + ubase;
-        const float *mbase = a.premasked ? vbase : a.mask + ubase;
-        const bool use_mask = !a.premasked;
+        const float *mbase = PM ? vbase : a.mask + ubase;
 
         float dp[K];
         uint32_t R[K];
@@ -141,14 +151,20 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
             R[i] = 0u;
         }
 
-        float va[K][C], ma[K][C], vb[K][C], mb[K][C];
+        // D-deep ring of lattice chunks: chunk c+D-1 is requested while chunk c is processed, so D-1
+        // chunks (K*C*(D-1) cells per lane) are in flight -- at one wave per utterance nothing else
+        // hides the L2/MALL/HBM latency of the lattice stream.  Loads are unconditional (addresses are
+        // clamped into the utterance) so the waitcnt bookkeeping stays exact across the ring.
+        constexpr int MD = PM ? 1 : D;  // no mask registers when value is premasked
+        float vbuf[D][K][C], mbuf[MD][K][C];
 
-        auto load_chunk = [&](float (&vv)[K][C], float (&mm)[K][C], int y0) {
+        auto load_chunk = [&](auto slot, int y0) {
+            constexpr int sl = decltype(slot)::value;
 #pragma unroll
-            for (int i = 0; i < K; ++i) load_row_segment<C, VEC>(vbase, roff[i] + y0, last, vv[i]);
-            if (use_mask) {
+            for (int i = 0; i < K; ++i) load_row_segment<C, VEC>(vbase, roff[i] + y0, last, vbuf[sl][i]);
+            if constexpr (!PM) {
 #pragma unroll
-                for (int i = 0; i < K; ++i) load_row_segment<C, VEC>(mbase, roff[i] + y0, last, mm[i]);
+                for (int i = 0; i < K; ++i) load_row_segment<C, VEC>(mbase, roff[i] + y0, last, mbuf[sl][i]);
             }
         };
 
@@ -165,14 +181,18 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
             }
         };
 
-        auto process_chunk = [&](float (&vv)[K][C], float (&mm)[K][C], int y0) {
+        auto process_chunk = [&](auto slot, int y0) {
+            constexpr int sl = decltype(slot)::value;
 #pragma unroll
             for (int j = 0; j < C; ++j) {
                 const int y = y0 + j;
                 if (y < t_y) {
                     float s[K];
 #pragma unroll
-                    for (int i = 0; i < K; ++i) s[i] = use_mask ? vv[i][j] * mm[i][j] : vv[i][j];
+                    for (int i = 0; i < K; ++i) {
+                        if constexpr (PM) s[i] = vbuf[sl][i][j];
+                        else s[i] = vbuf[sl][i][j] * mbuf[sl][i][j];  // __init__.py:45
+                    }
                     // x == 0 predecessor: 0 at y == 0, max_neg_val after (core.pyx:63-64)
                     const float nb = dpp_wave_shr1(dp[K - 1], y == 0 ? 0.0f : neg);
                     float ndp[K];
@@ -200,13 +220,16 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
         };
 
         const int nload = (t_y + C - 1) / C;
-        load_chunk(va, ma, 0);
-        for (int c = 0; c < nload; c += 2) {
-            if (c + 1 < nload) load_chunk(vb, mb, (c + 1) * C);
-            process_chunk(va, ma, c * C);
-            if (c + 1 >= nload) break;
-            if (c + 2 < nload) load_chunk(va, ma, (c + 2) * C);
-            process_chunk(vb, mb, (c + 1) * C);
+        static_for<0, D - 1>([&](auto sl) { load_chunk(sl, decltype(sl)::value * C); });
+        for (int c0 = 0; c0 < nload; c0 += D) {
+            static_for<0, D>([&](auto sl) {
+                constexpr int si = decltype(sl)::value;
+                const int c = c0 + si;
+                if (c < nload) {
+                    load_chunk(std::integral_constant<int, (si + D - 1) % D>{}, (c + D - 1) * C);
+                    process_chunk(sl, c * C);
+                }
+            });
         }
         if (t_y & 31) flush_bits(t_y >> 5, 32 - (t_y & 31));
 
@@ -439,38 +462,62 @@ __global__ __launch_bounds__(256) void expand_rows_fwd_kernel(const float *__res
     dst[((size_t)b * C + c) * Ty + yy] = x >= 0 ? src[((size_t)b * C + c) * Tx + x] : 0.f;
 }
 
-// one block per (utterance, 8 channels): the channels' dy rows are staged in LDS with coalesced
-// loads, then thread (channel, row x) sums its run from LDS -- a per-thread loop over global memory
-// serialised one HBM latency per frame (31 us at the bench shape)
-constexpr int kErC = 8;
-constexpr int kErMaxTy = 2048;
+// one block per (utterance, 2 channels): the channels' dy rows are staged in LDS (16-byte coalesced
+// loads when the rows allow), then 16 lanes per (channel, row x) sum its run from LDS.  The
+// earlier 8-channel blocks gave B*10 workgroups -- 80 at the long-form shape (B=8, Ty=4096), 940 us per
+// call on a latency-bound load phase; 2 channels give 4x the workgroups and 16-byte loads.
+constexpr int kErC = 2;
+constexpr int kErMaxTy = 4096;
+template <bool kVec>
 __global__ __launch_bounds__(256) void expand_rows_bwd_kernel(const float *__restrict__ dy,
                                                               const int32_t *__restrict__ row_start,
                                                               const int32_t *__restrict__ lengths, int C, int Tx,
                                                               int Ty, float *__restrict__ dx) {
-    __shared__ float sdy[kErC * kErMaxTy];
+    __shared__ __attribute__((aligned(16))) float sdy[kErC * kErMaxTy];
     const int b = blockIdx.y, c0 = blockIdx.x * kErC;
     const int nc = min(kErC, C - c0);
     const int t_x = lengths[2 * b], t_y = lengths[2 * b + 1];
     const int32_t *rs = row_start + (size_t)b * Tx;
-    for (int ty0 = 0; ty0 < Ty; ty0 += kErMaxTy) {  // frame slabs (one slab for Ty <= 2048)
+    for (int ty0 = 0; ty0 < Ty; ty0 += kErMaxTy) {  // frame slabs (one slab for Ty <= 4096)
         const int tn = min(kErMaxTy, Ty - ty0);
         __syncthreads();
-        for (int e = threadIdx.x; e < nc * tn; e += 256) {
-            const int c = e / tn, yy = e - c * tn;
-            sdy[c * kErMaxTy + yy] = dy[((size_t)b * C + c0 + c) * Ty + ty0 + yy];
+        if (kVec) {  // Ty % 4 == 0, dy 16-byte aligned: every slab row starts 16-byte aligned
+            const int tn4 = tn >> 2;
+            for (int e = threadIdx.x; e < nc * tn4; e += 256) {
+                const int c = e / tn4, q = e - c * tn4;
+                const float4 v = *reinterpret_cast<const float4 *>(dy + ((size_t)b * C + c0 + c) * Ty + ty0 + 4 * q);
+                *reinterpret_cast<float4 *>(&sdy[c * kErMaxTy + 4 * q]) = v;
+            }
+        } else {
+            for (int e = threadIdx.x; e < nc * tn; e += 256) {
+                const int c = e / tn, yy = e - c * tn;
+                sdy[c * kErMaxTy + yy] = dy[((size_t)b * C + c0 + c) * Ty + ty0 + yy];
+            }
         }
         __syncthreads();
-        for (int e = threadIdx.x; e < nc * Tx; e += 256) {
+        // 16 lanes per row: a run is summed as 16 strided partial sums + a 4-step xor tree (fixed
+        // order, deterministic); a degenerate alignment (one row owning thousands of frames) costs
+        // run/16 dependent LDS reads instead of run.
+        const int l16 = threadIdx.x & 15;
+        for (int e = threadIdx.x >> 4; e < nc * Tx; e += 16) {
             const int c = e / Tx, x = e - c * Tx;
             const int s = rs[x];
-            float acc = ty0 == 0 ? 0.f : dx[((size_t)b * C + c0 + c) * Tx + x];
+            int lo = 0, hi = 0;
             if (s >= 0) {
                 const int en = (x == t_x - 1) ? t_y : rs[x + 1];
-                const int lo = max(s, ty0) - ty0, hi = min(en, ty0 + tn) - ty0;
-                for (int yy = lo; yy < hi; ++yy) acc += sdy[c * kErMaxTy + yy];
+                lo = max(s, ty0) - ty0;
+                hi = min(en, ty0 + tn) - ty0;
             }
-            dx[((size_t)b * C + c0 + c) * Tx + x] = acc;
+            float acc = 0.f;
+            for (int yy = lo + l16; yy < hi; yy += 16) acc += sdy[c * kErMaxTy + yy];
+            acc += __shfl_xor(acc, 8, 16);
+            acc += __shfl_xor(acc, 4, 16);
+            acc += __shfl_xor(acc, 2, 16);
+            acc += __shfl_xor(acc, 1, 16);
+            if (l16 == 0) {
+                float *o = dx + ((size_t)b * C + c0 + c) * Tx + x;
+                *o = ty0 == 0 ? acc : *o + acc;
+            }
         }
     }
 }
@@ -498,12 +545,11 @@ WsLayout ws_layout(int B, int Tx, int Ty) {
     return w;
 }
 
-template <int K, int C>
-int launch_dp_k(const MasArgs &a, int B, bool vec, bool lds_bits, bool dp_out, size_t shmem,
-                hipStream_t st) {
+template <int K, int C, int D, bool PM>
+int launch_dp_k(const MasArgs &a, int B, bool vec, bool lds_bits, bool dp_out, size_t shmem, hipStream_t st) {
     dim3 grid(B), block(kWave);
-#define MTTS_MAS_LAUNCH(V, L, D) \
-    hipLaunchKernelGGL((mas_dp_kernel<K, C, V, L, D>), grid, block, shmem, st, a)
+#define MTTS_MAS_LAUNCH(V, L, DO) \
+    hipLaunchKernelGGL((mas_dp_kernel<K, C, D, PM, V, L, DO && PM>), grid, block, shmem, st, a)
     if (vec) {
         if (lds_bits) {
             if (dp_out) MTTS_MAS_LAUNCH(true, true, true); else MTTS_MAS_LAUNCH(true, true, false);
@@ -521,13 +567,37 @@ int launch_dp_k(const MasArgs &a, int B, bool vec, bool lds_bits, bool dp_out, s
     return mtts::check_launch("mas_dp_kernel");
 }
 
+// Chunk shape and ring depth per rows-per-lane K: K*C = 32 cells per lane per chunk; the premasked
+// lattice (the fused training path and core.pyx's API) carries no mask registers, so it affords a
+// deeper ring.  MTTS_MAS_RING overrides the premasked depth (tuning).
+int ring_depth() {
+    static const int d = [] {
+        const char *e = getenv("MTTS_MAS_RING");
+        const int v = e ? atoi(e) : 0;
+        return (v == 2 || v == 3 || v == 4) ? v : 0;
+    }();
+    return d;
+}
+
+template <int K, int C>
+int launch_dp_kc(const MasArgs &a, int B, bool vec, bool lds_bits, bool dp_out, size_t shmem, hipStream_t st) {
+    if (!a.premasked) {
+        if (dp_out) return mtts::fail(MTTS_ERR_INVALID_ARG, "maximum_path: dp_out needs a premasked lattice");
+        return launch_dp_k<K, C, 2, false>(a, B, vec, lds_bits, false, shmem, st);
+    }
+    const int d = ring_depth() ? ring_depth() : kDefaultRing;
+    if (d == 2) return launch_dp_k<K, C, 2, true>(a, B, vec, lds_bits, dp_out, shmem, st);
+    if (d == 3) return launch_dp_k<K, C, 3, true>(a, B, vec, lds_bits, dp_out, shmem, st);
+    return launch_dp_k<K, C, 4, true>(a, B, vec, lds_bits, dp_out, shmem, st);
+}
+
 int launch_dp(MasArgs a, int B, const WsLayout &w, bool vec, bool dp_out, hipStream_t st) {
     size_t shmem = (size_t)w.Txp * 4 + (w.lds_bits ? (size_t)w.Txp * w.nch * 4 : 0);
     switch (w.K) {
-        case 1: return launch_dp_k<1, 32>(a, B, vec, w.lds_bits, dp_out, shmem, st);
-        case 2: return launch_dp_k<2, 16>(a, B, vec, w.lds_bits, dp_out, shmem, st);
-        case 4: return launch_dp_k<4, 8>(a, B, vec, w.lds_bits, dp_out, shmem, st);
-        default: return launch_dp_k<8, 4>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+        case 1: return launch_dp_kc<1, 32>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+        case 2: return launch_dp_kc<2, 16>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+        case 4: return launch_dp_kc<4, 8>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+        default: return launch_dp_kc<8, 4>(a, B, vec, w.lds_bits, dp_out, shmem, st);
     }
 }
 
@@ -668,8 +738,13 @@ extern "C" int mtts_expand_rows_bwd(const float *dy, const int32_t *row_start, c
                    "expand_rows_bwd: bad args");
     if ((size_t)B * C * Tx == 0) return MTTS_OK;
     dim3 grid((unsigned)((C + kErC - 1) / kErC), B);
-    hipLaunchKernelGGL(expand_rows_bwd_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(hip_stream), dy, row_start,
-                       lengths, C, Tx, Ty, dx);
+    const bool vec = (Ty % 4 == 0) && ((uintptr_t)dy % 16 == 0);
+    if (vec)
+        hipLaunchKernelGGL(expand_rows_bwd_kernel<true>, grid, dim3(256), 0, static_cast<hipStream_t>(hip_stream), dy,
+                           row_start, lengths, C, Tx, Ty, dx);
+    else
+        hipLaunchKernelGGL(expand_rows_bwd_kernel<false>, grid, dim3(256), 0, static_cast<hipStream_t>(hip_stream), dy,
+                           row_start, lengths, C, Tx, Ty, dx);
     return mtts::check_launch("expand_rows_bwd_kernel");
 }
 

@@ -31,6 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_every_declared_symbol_has_a_python_signature():
     import matcha.models.components._ops  # noqa: F401  (registers the decoder entry points)
+    import matcha.training  # noqa: F401  (registers the clip + AdamW entry points)
 
     missing = [s for s in declared_symbols() if s not in N._SIGNATURES]
     assert not missing, missing
