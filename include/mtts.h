@@ -18,6 +18,7 @@
  *   mtts_expand_rows_fwd / _bwd    <- matcha/models/matcha_tts.py:504-505  mu_y = attn^T @ mu_x
  *   mtts_compute_batch_alignments  <- matcha/utils/monotonic_align/core.pyx:101-128   compute_batch_alignments(...)
  *                                     (bound as maximum_path_c, __init__.py:4-8)
+ *   mtts_mel_log_fwd               <- matcha/utils/audio_process.py:62-72  MelSpectrogram.__call__ (after the STFT)
  * Decoder / CFM operators (matcha/models/components/{decoder,transformer,flow_matching}.py) are
  * declared in mtts_decoder.h.
  */
@@ -116,12 +117,27 @@ int mtts_prior_maximum_path(const float *mu_x, const float *y, const int64_t *x_
  * mu_y = attn^T @ mu_x for a hard alignment (matcha_tts.py:504-505) as a gather, and its backward:
  *   fwd: dst[b,c,j] = src[b,c,col_row[b,j]] (0 where col_row < 0); src [B,C,Tx], dst [B,C,Ty] float32.
  *   bwd: dx[b,c,i] = sum over the frames j of row i (row_start / lengths of mtts_maximum_path_f32) of
- *        dy[b,c,j], in ascending j (deterministic).
+ *        dy[b,c,j]: 16 strided partial sums (j = start + l + 16k, ascending k) combined by a fixed
+ *        xor tree (deterministic, no atomics).
  */
 int mtts_expand_rows_fwd(const float *src, const int32_t *col_row, int32_t B, int32_t C, int32_t Tx, int32_t Ty,
                          float *dst, void *hip_stream);
 int mtts_expand_rows_bwd(const float *dy, const int32_t *row_start, const int32_t *lengths, int32_t B, int32_t C,
                          int32_t Tx, int32_t Ty, float *dx, void *hip_stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Log-mel features of the data path (matcha/utils/audio_process.py:32-81, MelSpectrogram.__call__)
+ * ------------------------------------------------------------------------------------------- */
+/*
+ * out[b,m,f] = log(max(sum_{k in [band_lo[m], band_hi[m])} mel_w[m,k] * sqrt(re^2 + im^2 + 1e-9), clip))
+ *   spec : float32 [B, n_freq, F, 2] (torch.stft's complex output viewed as real, C-contiguous)
+ *   mel_w: float32 [n_mels, n_freq] (the librosa slaney basis); band_lo/hi int32 [n_mels]: the nonzero
+ *          bins of each filter (zero weights outside are skipped -- exact, they add +0).
+ *   out  : float32 [B, n_mels, F].  Bins are summed in ascending k (fixed order, deterministic).
+ */
+int mtts_mel_log_fwd(const float *spec, const float *mel_w, const int32_t *band_lo, const int32_t *band_hi,
+                     int32_t B, int32_t n_freq, int32_t F, int32_t n_mels, float clip_val, float *out,
+                     void *hip_stream);
 
 #ifdef __cplusplus
 } /* extern "C" */
