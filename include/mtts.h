@@ -18,6 +18,7 @@
  *   mtts_expand_rows_fwd / _bwd    <- matcha/models/matcha_tts.py:504-505  mu_y = attn^T @ mu_x
  *   mtts_compute_batch_alignments  <- matcha/utils/monotonic_align/core.pyx:101-128   compute_batch_alignments(...)
  *                                     (bound as maximum_path_c, __init__.py:4-8)
+ *   mtts_losses_fwd / _bwd         <- flow_matching.py:145-149 (CFM loss) + matcha_tts.py:319-323 (prior loss)
  *   mtts_mel_log_fwd               <- matcha/utils/audio_process.py:62-72  MelSpectrogram.__call__ (after the STFT)
  * Decoder / CFM operators (matcha/models/components/{decoder,transformer,flow_matching}.py) are
  * declared in mtts_decoder.h.
@@ -138,6 +139,25 @@ int mtts_expand_rows_bwd(const float *dy, const int32_t *row_start, const int32_
 int mtts_mel_log_fwd(const float *spec, const float *mel_w, const int32_t *band_lo, const int32_t *band_hi,
                      int32_t B, int32_t n_freq, int32_t F, int32_t n_mels, float clip_val, float *out,
                      void *hip_stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Training losses (flow_matching.py:145-149 CFM loss, matcha_tts.py:319-323 prior loss), fused
+ * ------------------------------------------------------------------------------------------- */
+/*
+ * out[0] = sum((u_pred - (x1 - (1 - sigma_min) z))^2) / D         (unmasked numerator, reference quirk)
+ * out[1] = sum(0.5 ((y - mu_y)^2 + log 2pi) * y_mask) / D,  D = out[2] = sum(y_mask) * C
+ *   u_pred token-major [B,T,C]; x1, z, y, mu_y channel-major [B,C,T]; y_mask float [B,T] (float32, device).  u_pred = NULL
+ *   skips the CFM term (out[0] = 0); mu_y = NULL skips the prior term.  C <= 128.  Deterministic.
+ * Backward: du_pred = 2 g_diff / D (u_pred - u) (token-major), dmu_y = -g_prior / D (y - mu_y) * y_mask
+ *   (channel-major); either output may be NULL.  fwd_out is the forward's out (D read from out[2]).
+ */
+size_t mtts_losses_workspace_size(int32_t B, int32_t T);
+int mtts_losses_fwd(const float *u_pred, const float *x1, const float *z, const float *y, const float *mu_y,
+                    const float *y_mask, int32_t B, int32_t C, int32_t T, float sigma_min, float *out,
+                    void *workspace, size_t workspace_bytes, void *hip_stream);
+int mtts_losses_bwd(const float *g_diff, const float *g_prior, const float *fwd_out, const float *u_pred, const float *x1, const float *z,
+                    const float *y, const float *mu_y, const float *y_mask, int32_t B, int32_t C, int32_t T,
+                    float sigma_min, float *du_pred, float *dmu_y, void *hip_stream);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -13,7 +13,63 @@ from abc import ABC
 import torch
 import torch.nn as nn
 
+from matcha import _native as N
 from matcha.models.components.decoder import Decoder
+
+
+class _FusedLosses(torch.autograd.Function):
+    """CFM loss (flow_matching.py:145-149) and prior loss (matcha_tts.py:319-323) with their backward
+    in three HIP launches (csrc/losses.hip: partials + finalize forward, one backward) instead of
+    ~30 elementwise / reduction kernels.  u_pred token-major [B,T,C] (or None: no CFM term);
+    mu_y [B,C,T] (or None: no prior term); x1 = y, z [B,C,T]; mask [B,T].  Returns two fp32 scalars."""
+
+    @staticmethod
+    def forward(ctx, u_pred, mu_y, x1, z, mask, sigma_min):
+        N.require_device(x1, mask)
+        f32 = lambda t: None if t is None else t.detach().to(torch.float32).contiguous()  # noqa: E731
+        u_c, mu_c, x1_c, z_c, m_c = f32(u_pred), f32(mu_y), f32(x1), f32(z), f32(mask)
+        B, C, T = x1_c.shape
+        if u_c is not None and (u_c.shape != (B, T, C) or z_c is None or z_c.shape != x1_c.shape):
+            raise ValueError("fused losses: u_pred must be [B, T, C] and z [B, C, T]")
+        if mu_c is not None and mu_c.shape != x1_c.shape:
+            raise ValueError("fused losses: mu_y must be [B, C, T]")
+        if m_c.shape != (B, T):
+            raise ValueError("fused losses: mask must be [B, T]")
+        dev = x1_c.device
+        out = torch.empty(3, dtype=torch.float32, device=dev)
+        ws = torch.empty(max(int(N.lib().mtts_losses_workspace_size(B, T)), 4), dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            N.check(N.lib().mtts_losses_fwd(N.ptr(u_c), N.ptr(x1_c), N.ptr(z_c), N.ptr(x1_c), N.ptr(mu_c), N.ptr(m_c),
+                                            B, C, T, float(sigma_min), N.ptr(out), N.ptr(ws), ws.numel(),
+                                            N.stream_handle(dev)), "mtts_losses_fwd")
+        ctx.save_for_backward(u_c, mu_c, x1_c, z_c, m_c, out)
+        ctx.sigma = float(sigma_min)
+        return out[0], out[1]
+
+    @staticmethod
+    def backward(ctx, g_diff, g_prior):
+        u_c, mu_c, x1_c, z_c, m_c, out = ctx.saved_tensors
+        B, C, T = x1_c.shape
+        need_u = ctx.needs_input_grad[0] and u_c is not None
+        need_mu = ctx.needs_input_grad[1] and mu_c is not None
+        du = torch.empty_like(u_c) if need_u else None
+        dmu = torch.empty_like(mu_c) if need_mu else None
+        gd = g_diff.detach().to(torch.float32).contiguous() if need_u else None
+        gp = g_prior.detach().to(torch.float32).contiguous() if need_mu else None
+        if need_u or need_mu:
+            dev = x1_c.device
+            with torch.cuda.device(dev):
+                N.check(N.lib().mtts_losses_bwd(N.ptr(gd), N.ptr(gp), N.ptr(out), N.ptr(u_c), N.ptr(x1_c), N.ptr(z_c),
+                                                N.ptr(x1_c), N.ptr(mu_c), N.ptr(m_c), B, C, T, ctx.sigma, N.ptr(du),
+                                                N.ptr(dmu), N.stream_handle(dev)), "mtts_losses_bwd")
+        return du, dmu, None, None, None, None
+
+
+def fused_losses(u_pred, mu_y, x1, z, mask, sigma_min):
+    """(diff_loss, prior_loss); see _FusedLosses.  mask [B, 1, T] or [B, T]."""
+    if mask.dim() == 3:
+        mask = mask[:, 0]
+    return _FusedLosses.apply(u_pred, mu_y, x1, z, mask, sigma_min)
 
 
 class BaseConditionalFlowMatching(nn.Module, ABC):
@@ -90,6 +146,12 @@ class BaseConditionalFlowMatching(nn.Module, ABC):
 
     def compute_loss(self, x1, mask, mu, spks=None, cond=None, *, t=None, z=None):
         """Returns (loss, phi_t).  x1/mu [B, n_feats, T], mask [B, 1, T]."""
+        loss, _, phi_t = self.compute_loss_and_prior(x1, mask, mu, None, t=t, z=z)
+        return loss, phi_t
+
+    def compute_loss_and_prior(self, x1, mask, mu, prior_mu, *, t=None, z=None):
+        """compute_loss plus, when prior_mu is given, MatchaTTS's prior loss on (x1, prior_mu) -- both
+        in one fused pass over the tensors (csrc/losses.hip).  Returns (diff_loss, prior_loss, phi_t)."""
         b = mu.shape[0]
         if t is None:
             t = torch.rand([b, 1, 1], device=mu.device, dtype=mu.dtype)
@@ -97,11 +159,11 @@ class BaseConditionalFlowMatching(nn.Module, ABC):
             z = torch.randn_like(x1)
         s = self.sigma_min
         phi_t = (1 - (1 - s) * t) * z + t * x1
-        u_target = x1 - (1 - s) * z
         u_pred = self.estimator.forward_tm(phi_t.transpose(1, 2), mask[:, 0], mu.transpose(1, 2),
                                            t.reshape(b))
-        loss = torch.sum((u_pred - u_target.transpose(1, 2)) ** 2) / (torch.sum(mask) * u_target.shape[1])
-        return loss, phi_t
+        # sum((u_pred - u)^2) / (sum(mask) * n_feats) and the prior loss, fused (flow_matching.py:145-149)
+        loss, prior = fused_losses(u_pred, prior_mu, x1, z, mask, s)
+        return loss, prior, phi_t
 
 
 class ConditionalFlowMatching(BaseConditionalFlowMatching):

@@ -133,10 +133,9 @@ class MatchaTTS(BaseLightningClass):
             mu_y = monotonic_align.expand_rows(mu_x, *runs)
         else:
             mu_y = torch.matmul(attn.squeeze(1).transpose(1, 2), mu_x.transpose(1, 2)).transpose(1, 2)
-        diff_loss, _ = self.decoder.compute_loss(x1=y, mask=y_mask, mu=mu_y, cond=cond, t=t, z=z)
-        if self.prior_loss:
-            prior_loss = torch.sum(0.5 * ((y - mu_y) ** 2 + math.log(2 * math.pi)) * y_mask)
-            prior_loss = prior_loss / (torch.sum(y_mask) * self.n_feats)
-        else:
+        # CFM loss (:506) and prior loss (:508-511) in one fused HIP pass (components/flow_matching.py)
+        diff_loss, prior_loss, _ = self.decoder.compute_loss_and_prior(y, y_mask, mu_y,
+                                                                       mu_y if self.prior_loss else None, t=t, z=z)
+        if not self.prior_loss:
             prior_loss = 0
         return dur_loss, prior_loss, diff_loss, attn

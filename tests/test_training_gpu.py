@@ -27,8 +27,9 @@ def test_graph_step_matches_eager_step(precision):
     m2.eval()
     t = torch.rand(4, 1, 1, device=DEV)
     z = torch.randn(4, 80, 80, device=DEV)
-    for m in (m1, m2):  # inject the CFM randomness identically
-        m.decoder.compute_loss = (lambda f: (lambda *a, **k: f(*a, **{**k, "t": t, "z": z})))(m.decoder.compute_loss)
+    for m in (m1, m2):  # inject the CFM randomness identically (MatchaTTS.forward's fused-loss entry)
+        m.decoder.compute_loss_and_prior = (lambda f: (lambda *a, **k: f(*a, **{**k, "t": t, "z": z})))(
+            m.decoder.compute_loss_and_prior)
     te = Trainer(m1, TrainConfig(precision=precision, graph=False))
     tg = Trainer(m2, TrainConfig(precision=precision, graph=True))
     le = te.step([b]).clone()
