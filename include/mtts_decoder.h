@@ -290,6 +290,18 @@ int32_t mtts_pending_reductions(void);
 int mtts_flush_reductions(void *hip_stream);
 void mtts_discard_reductions(void);
 
+/* ---------------------------------------------------------------------------------------------
+ * CFM decoder input (flow_matching.py:130-145, decoder.py:8-31 and :288), csrc/cfm_prep.hip
+ * ------------------------------------------------------------------------------------------- */
+/* packed[b,t,0:C] = (1 - (1 - sigma_min) t_b) z[b,:,t] + t_b x1[b,:,t];  packed[b,t,C:2C] = mu[b,:,t]
+ * (x1, z, mu channel-major [B,C,T]; t [B]; packed token-major [B,T,2C]; C <= 128; torch's fp32 order). */
+int mtts_cfm_pack_fwd(const float *x1, const float *z, const float *t, const float *mu, int32_t B, int32_t C,
+                      int32_t T, float sigma_min, float *packed, void *hip_stream);
+/* d_mu[b,c,t] = d_packed[b,t,C+c] */
+int mtts_cfm_pack_bwd(const float *d_packed, int32_t B, int32_t C, int32_t T, float *d_mu, void *hip_stream);
+/* SinusoidalPosEmb: out[b,k] = sin(scale t_b f_k), out[b,dim/2+k] = cos(...), f_k = exp(-k ln(1e4)/(dim/2-1)) */
+int mtts_time_embedding(const float *t, int32_t B, int32_t dim, float scale, float *out, void *hip_stream);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

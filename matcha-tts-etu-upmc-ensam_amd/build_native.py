@@ -33,6 +33,7 @@ COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", f"-I{INCLUDE}"
 # the Cython, core.pyx:80 / __init__.py:45).
 EXTRA = {
     "mas.hip": ["-ffp-contract=off"],
+    "cfm_prep.hip": ["-ffp-contract=off"],  # phi_t and the time embedding round like torch (no fma)
 }
 
 

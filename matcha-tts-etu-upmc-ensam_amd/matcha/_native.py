@@ -41,6 +41,9 @@ _SIGNATURES: dict[str, tuple] = {
     "mtts_losses_workspace_size": (_SZ, [_I32, _I32]),
     "mtts_losses_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P, _SZ, _P]),
     "mtts_losses_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P, _P]),
+    "mtts_cfm_pack_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _F, _P, _P]),
+    "mtts_cfm_pack_bwd": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
+    "mtts_time_embedding": (ctypes.c_int, [_P, _I32, _I32, _F, _P, _P]),
     "mtts_mel_log_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _I32, _F, _P, _P]),
 }
 

@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from matcha import _native as N
 from matcha.models.components import _ops as O
 from matcha.models.components.transformer import BasicTransformerBlock
 
@@ -32,11 +33,14 @@ class SinusoidalPosEmb(nn.Module):
     def forward(self, x, scale=1000):
         if x.ndim < 1:
             x = x.unsqueeze(0)
-        half = self.dim // 2
-        step = math.log(10000.0) / (half - 1)
-        freq = torch.exp(torch.arange(half, device=x.device, dtype=torch.float32) * -step)
-        arg = scale * x.float().unsqueeze(1) * freq.unsqueeze(0)
-        return torch.cat((arg.sin(), arg.cos()), dim=-1)
+        # one HIP launch (csrc/cfm_prep.hip) for arange / exp / mul / sin / cos / cat, torch's fp32 order
+        N.require_device(x)
+        xc = x.detach().float().reshape(-1).contiguous()
+        out = torch.empty((xc.numel(), self.dim), dtype=torch.float32, device=x.device)
+        with torch.cuda.device(x.device):
+            N.check(N.lib().mtts_time_embedding(N.ptr(xc), xc.numel(), self.dim, float(scale), N.ptr(out),
+                                                N.stream_handle(x.device)), "mtts_time_embedding")
+        return out
 
 
 class TimeStepEmbeddingNet(nn.Module):
@@ -200,6 +204,13 @@ class Decoder(nn.Module):
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec_bf16), O.weight_pack_scope(self):
                 return self._forward_tm(x.float(), mask.float(), mu.float(), t.float())
 
+    def forward_tm_packed(self, h, mask, t):
+        """forward_tm on the already packed input h = [x | mu] [B, T, 2C] (CFM's fused pack)."""
+        prec_bf16 = torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+        with torch.autocast("cuda", enabled=False):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec_bf16), O.weight_pack_scope(self):
+                return self._forward_tm(None, mask.float(), None, t.float(), packed=h)
+
     def _time_projections(self, temb):
         """Every ResnetBlock's mlp(temb) = Linear(Mish(temb)) (decoder.py:80-81) as ONE GEMM: the Mish of
         the shared time embedding is computed once and the blocks' Linear weights are stacked along N
@@ -214,11 +225,11 @@ class Decoder(nn.Module):
             tp = O.linear_tm(act, tuple(lin.weight for lin in lins), bias)
         return dict(zip(map(id, resnets), tp.split([lin.out_features for lin in lins], dim=-1)))
 
-    def _forward_tm(self, x, mask, mu, t):
+    def _forward_tm(self, x, mask, mu, t, packed=None):
         with torch.autocast("cuda", enabled=False):  # [B, 1024] time MLP: tiny, kept fp32
             temb = self.time_mlp(self.time_embeddings(t))
         tps = self._time_projections(temb)
-        h = torch.cat([x, mu], dim=-1)  # einops pack "b * t" on channels (:288)
+        h = torch.cat([x, mu], dim=-1) if packed is None else packed  # einops pack "b * t" on channels (:288)
         skips, masks = [], [mask]
         for resnet, tfs, down in self.Downsampling_Blocks:
             m = masks[-1]

@@ -65,6 +65,39 @@ class _FusedLosses(torch.autograd.Function):
         return du, dmu, None, None, None, None
 
 
+class _CfmPack(torch.autograd.Function):
+    """phi_t = (1 - (1 - sigma) t) z + t x1 (flow_matching.py:139) packed with mu into the decoder's
+    token-major input [B, T, 2C] (decoder.py:288) in one HIP pass (csrc/cfm_prep.hip); backward
+    returns mu's gradient (x1 = y, z and t carry none, as in the reference)."""
+
+    @staticmethod
+    def forward(ctx, x1, z, t, mu, sigma_min):
+        N.require_device(x1, z, t, mu)
+        x1c, zc, muc = (v.detach().to(torch.float32).contiguous() for v in (x1, z, mu))
+        tc = t.detach().to(torch.float32).reshape(-1).contiguous()
+        B, C, T = x1c.shape
+        if zc.shape != x1c.shape or muc.shape != x1c.shape or tc.numel() != B:
+            raise ValueError("cfm pack: x1, z, mu must be [B, C, T] and t [B]")
+        packed = torch.empty((B, T, 2 * C), dtype=torch.float32, device=x1c.device)
+        with torch.cuda.device(x1c.device):
+            N.check(N.lib().mtts_cfm_pack_fwd(N.ptr(x1c), N.ptr(zc), N.ptr(tc), N.ptr(muc), B, C, T, float(sigma_min),
+                                              N.ptr(packed), N.stream_handle(x1c.device)), "mtts_cfm_pack_fwd")
+        ctx.shape = (B, C, T)
+        return packed
+
+    @staticmethod
+    def backward(ctx, d_packed):
+        if not ctx.needs_input_grad[3]:
+            return None, None, None, None, None
+        B, C, T = ctx.shape
+        dp = d_packed.detach().to(torch.float32).contiguous()
+        d_mu = torch.empty((B, C, T), dtype=torch.float32, device=dp.device)
+        with torch.cuda.device(dp.device):
+            N.check(N.lib().mtts_cfm_pack_bwd(N.ptr(dp), B, C, T, N.ptr(d_mu), N.stream_handle(dp.device)),
+                    "mtts_cfm_pack_bwd")
+        return None, None, None, d_mu, None
+
+
 def fused_losses(u_pred, mu_y, x1, z, mask, sigma_min):
     """(diff_loss, prior_loss); see _FusedLosses.  mask [B, 1, T] or [B, T]."""
     if mask.dim() == 3:
@@ -158,9 +191,10 @@ class BaseConditionalFlowMatching(nn.Module, ABC):
         if z is None:
             z = torch.randn_like(x1)
         s = self.sigma_min
-        phi_t = (1 - (1 - s) * t) * z + t * x1
-        u_pred = self.estimator.forward_tm(phi_t.transpose(1, 2), mask[:, 0], mu.transpose(1, 2),
-                                           t.reshape(b))
+        # phi_t (:139) packed with mu into the decoder's token-major input in one launch
+        packed = _CfmPack.apply(x1, z, t, mu, s)
+        phi_t = packed[..., : x1.shape[1]].transpose(1, 2)
+        u_pred = self.estimator.forward_tm_packed(packed, mask[:, 0], t.reshape(b))
         # sum((u_pred - u)^2) / (sum(mask) * n_feats) and the prior loss, fused (flow_matching.py:145-149)
         loss, prior = fused_losses(u_pred, prior_mu, x1, z, mask, s)
         return loss, prior, phi_t
