@@ -16,6 +16,8 @@
  *   mtts_layernorm_fwd / _bwd         <- BasicTransformerBlock norm1 / norm3 (transformer.py:316, 345)
  *   mtts_attention_fwd / _bwd         <- diffusers AttnProcessor2_0 scaled_dot_product_attention with
  *                                        the float 0/1 mask as an additive key bias (transformer.py:320-328)
+ *   mtts_cfm_pack_fwd / _bwd          <- phi_t (flow_matching.py:138) + pack([x, mu], "b * t") (decoder.py:288)
+ *   mtts_time_embedding               <- SinusoidalPosEmb.forward (decoder.py:8-31)
  */
 #ifndef MTTS_DECODER_H_
 #define MTTS_DECODER_H_

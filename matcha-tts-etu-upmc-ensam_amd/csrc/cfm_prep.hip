@@ -1,6 +1,6 @@
 // Decoder-input preparation of the CFM training step on gfx950 (reference: flow_matching.py:130-145 and
 // decoder.py:8-31, 288):
-//   mtts_cfm_pack_fwd : phi_t = (1 - (1 - sigma) t) z + t x1 (flow_matching.py:139) and the channel
+//   mtts_cfm_pack_fwd : phi_t = (1 - (1 - sigma) t) z + t x1 (flow_matching.py:138) and the channel
 //                       concat with mu (decoder.py:288, einops pack), written straight into the decoder's
 //                       token-major input [B, T, 2C] = [phi^T | mu^T] -- one pass instead of the scalar
 //                       ops on t, two multiplies, an add, two transposes and a concat.

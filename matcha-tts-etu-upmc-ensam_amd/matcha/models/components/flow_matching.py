@@ -66,7 +66,7 @@ class _FusedLosses(torch.autograd.Function):
 
 
 class _CfmPack(torch.autograd.Function):
-    """phi_t = (1 - (1 - sigma) t) z + t x1 (flow_matching.py:139) packed with mu into the decoder's
+    """phi_t = (1 - (1 - sigma) t) z + t x1 (flow_matching.py:138) packed with mu into the decoder's
     token-major input [B, T, 2C] (decoder.py:288) in one HIP pass (csrc/cfm_prep.hip); backward
     returns mu's gradient (x1 = y, z and t carry none, as in the reference)."""
 

@@ -1,6 +1,6 @@
 """CFM step prologue/epilogue kernels (csrc/cfm_prep.hip, csrc/losses.hip) against plain torch fp32
 restatements of the reference expressions:
-  phi_t + channel pack   flow_matching.py:139, decoder.py:288   (bit-exact: same fp32 op order)
+  phi_t + channel pack   flow_matching.py:138, decoder.py:288   (bit-exact: same fp32 op order)
   SinusoidalPosEmb       decoder.py:8-31                        (device libm sin/cos/exp: 2 ulp-ish)
   CFM + prior losses     flow_matching.py:145-149, matcha_tts.py:319-323 (fp32 reduction order differs)
 """
@@ -29,7 +29,7 @@ def test_cfm_pack_bitwise(B, C, T):
     mu.requires_grad_(True)
     s = 1e-4
     packed = _CfmPack.apply(x1, z, t, mu, s)
-    phi = (1 - (1 - s) * t) * z + t * x1  # flow_matching.py:139
+    phi = (1 - (1 - s) * t) * z + t * x1  # flow_matching.py:138
     want = torch.cat([phi, mu.detach()], dim=1).transpose(1, 2)  # decoder.py:288 (token-major)
     assert packed.shape == (B, T, 2 * C)
     assert torch.equal(packed, want)
@@ -81,7 +81,7 @@ def test_fused_losses_match_torch(B, C, T):
 
     u_ref = u_pred.detach().clone().requires_grad_(True)
     mu_ref = mu_y.detach().clone().requires_grad_(True)
-    u = x1 - (1 - s) * z  # flow_matching.py:140
+    u = x1 - (1 - s) * z  # flow_matching.py:141
     diff_w = torch.sum((u_ref.transpose(1, 2) - u) ** 2) / (torch.sum(mask) * C)  # :145-149, unmasked mse
     prior_w = torch.sum(0.5 * ((x1 - mu_ref) ** 2 + math.log(2 * math.pi)) * mask) / (torch.sum(mask) * C)
     torch.testing.assert_close(diff, diff_w, rtol=1e-5, atol=1e-6)
