@@ -10,8 +10,8 @@
 // Arithmetic follows torch's elementwise order exactly (separate fp32 roundings, no contraction:
 // __fmul_rn / __fadd_rn / __fsub_rn), so phi and the embedding equal the torch expressions bit for bit
 // up to the device libm's expf / sinf / cosf, which torch's kernels also call.
-// Layout: one workgroup per (utterance, 64-frame tile); channel-major rows are read 64 frames at a
-// time (256-byte coalesced), staged in LDS (pitch 65: conflict-free transposed reads), and written as
+// Layout: one workgroup per (utterance, 32-frame tile); channel-major rows are read 32 frames at a
+// time (128-byte coalesced), staged in LDS (pitch 33: conflict-free transposed reads), and written as
 // contiguous token-major rows.
 #include <hip/hip_runtime.h>
 
@@ -22,7 +22,7 @@
 
 namespace {
 
-constexpr int kPT = 64;  // frames per workgroup
+constexpr int kPT = 32;  // frames per workgroup (B=32 x 600 frames: 608 workgroups, 33 KB LDS each)
 constexpr int kPThreads = 256;
 constexpr int kPMaxC = 128;
 constexpr int kPPitch = kPT + 1;
