@@ -14,8 +14,8 @@ Rank 0 prints ONE JSON line: value = utterances/s over all ranks (max-over-ranks
   roofline      the dominant kernel (decoder conv_gemm_kernel): HIP events around each of its launches
                 on the launch stream during one extra eager fwd+bwd after the timed region;
   maximum_path  Mcells/s and roofline_mas (HIP events around maximum_path on the batch's own lattice);
-  cpu_baseline  (N=1) the oracle restatement of the reference step and the reference Cython MAS
-                (oracle/_ref when built) timed on this host's cores.
+  cpu_baseline  (N=1) the oracle restatement of the reference step (same B, Tx, Ty) and the C
+                restatement of the reference MAS (oracle/libmas_oracle.so) timed on this host's cores.
 """
 from __future__ import annotations
 
@@ -45,7 +45,7 @@ def decoder_train_flops(B: int, T: int) -> float:
 
 def cpu_baseline(B_cpu: int, Tx: int, Ty: int, budget_s: float) -> dict:
     """Reference CPU path timed on this host: the oracle's fp32 train step (train mode, dropout on)
-    + AdamW, and the MAS (reference Cython from oracle/_ref if built, else the C restatement)."""
+    + clip + AdamW at the bench's own batch shape, and the MAS (the pinned C restatement)."""
     import numpy as np
 
     sys.path.insert(0, str(ROOT / "tests"))
@@ -81,28 +81,17 @@ def cpu_baseline(B_cpu: int, Tx: int, Ty: int, budget_s: float) -> dict:
     out = {"value": round(B_cpu / step_s, 3), "unit": "utterances/s", "cores": threads, "kind": "port",
            "sample": f"{n} fp32 train steps (fwd+bwd+clip+AdamW, dropout on) of the oracle restatement "
                      f"(oracle/matcha_oracle.py) at B={B_cpu}, Tx={Tx}, Ty={Ty}; {threads} torch threads"}
-    # MAS on the host: reference Cython when present (oracle/_ref), else the C restatement
+    # MAS on the host: the C restatement oracle/libmas_oracle.so (pinned bit-exact to the reference
+    # Cython, tests/test_oracle_golden.py); the compiled reference itself never travels to the GPU box
     rng = np.random.default_rng(0)
     Bm = 32
     value = rng.normal(-100.0, 10.0, size=(Bm, Tx, Ty)).astype(np.float32)
     t_x = np.full(Bm, Tx, np.int32)
     t_y = np.full(Bm, Ty, np.int32)
-    kind, fn = "port", None
-    so = sorted((ROOT / "oracle" / "_ref").glob("core*.so"))
-    if so:
-        import importlib.util
+    kind = "port"
 
-        spec = importlib.util.spec_from_file_location("core", so[0])
-        core = importlib.util.module_from_spec(spec)
-        spec.loader.exec_module(core)
-        kind = "reference"
-
-        def fn():
-            p = np.zeros(value.shape, np.int32)
-            core.compute_batch_alignments(p, value.copy(), t_x, t_y)
-    else:
-        def fn():
-            OB.mas_batch(value, t_x, t_y)
+    def fn():
+        OB.mas_batch(value, t_x, t_y)
     fn()
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < 3.0:
@@ -111,8 +100,20 @@ def cpu_baseline(B_cpu: int, Tx: int, Ty: int, budget_s: float) -> dict:
     ms = (time.perf_counter() - t0) / n * 1e3
     out["mas"] = {"value": round(Bm * Tx * Ty / ms / 1e3, 1), "unit": "Mcells/s", "kind": kind,
                   "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
-                  "sample": f"{n} x compute_batch_alignments B={Bm} {Tx}x{Ty} ({ms:.3f} ms each, incl. copy)"}
+                  "sample": f"{n} x compute_batch_alignments (oracle/mas_oracle.c) B={Bm} {Tx}x{Ty} "
+                            f"({ms:.3f} ms each, incl. copy)"}
+    out["cpu_model"] = _cpu_model()
     return out
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def main():
@@ -329,7 +330,7 @@ def main():
             "synthesise": synth,
         }
         if world == 1 and not args.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(4, Tx, Ty, args.cpu_budget)
+            rec["cpu_baseline"] = cpu_baseline(B, Tx, Ty, args.cpu_budget)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -19,16 +19,22 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 INCLUDE = ROOT / "include"
-OBJ = PKG / "build" / "obj"
-LIB = PKG / "lib" / "libmtts_hip.so"
+# MTTS_BUILD_VARIANT=pk: a diagnostic build WITH packed-fp32 VALU ops (lib/libmtts_hip_pk.so, loaded
+# only through MTTS_LIB by tools/wgrad_debug.py to reproduce the fault documented in DESIGN.md §9)
+VARIANT = os.environ.get("MTTS_BUILD_VARIANT", "")
+OBJ = PKG / "build" / ("obj_" + VARIANT if VARIANT else "obj")
+LIB = PKG / "lib" / ("libmtts_hip_" + VARIANT + ".so" if VARIANT else "libmtts_hip.so")
 ARCH = "gfx950"
 
-# -packed-fp32-ops: no v_pk_{add,mul,fma}_f32.  On the MI355X box, packed-fp32 VALU ops in the bf16
-# wgrad staging produced wrong low-half results in lanes 16-31 / 48-63 whenever several workgroups
-# shared a CU (nondeterministic dW/db; bit-exact with one workgroup per CU or with the feature off;
-# tools/wgrad_debug.py, DESIGN.md "Toolchain findings").  The host pass ignores the feature (warning).
+# -packed-fp32-ops: no v_pk_{add,mul,fma}_f32 -- a performance choice: beside MFMAs a packed-fp32 VALU
+# op costs more issue cycles than two scalar ones (MI355X_MICROARCH.md), the step ran 1.7 % faster.
+# Correctness does not depend on it any more: the wgrad fault the flag once masked (v_pk_mul_f32 of
+# dY by an op_sel-swapped mask pair) is removed in the source, and the pk variant
+# below passes every op test.  The host pass ignores the feature (warning).
 COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
-          "-Wall", "-Wno-unused-function", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+          "-Wall", "-Wno-unused-function"]
+if VARIANT != "pk":
+    COMMON += ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 # Per-file extra flags.  The MAS DP must not contract value*mask + best into an FMA (bit parity with
 # the Cython, core.pyx:80 / __init__.py:45).
 EXTRA = {

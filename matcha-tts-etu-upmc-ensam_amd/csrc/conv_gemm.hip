@@ -504,10 +504,14 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
             float yv[2][4], xv[2][4];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const float ym = R.yok[c][h] ? 1.f : 0.f;
+                // the dY row validity is a SELECT, not a multiply by a 0/1 mask: built with packed-fp32
+                // VALU ops, hipcc turned that multiply into v_pk_mul_f32 over the mask pair of two rows
+                // (op_sel:[0,1] op_sel_hi:[1,0]), which returned wrong, nondeterministic products under
+                // CU co-residency (tools/gpu_r2d.sh reproduces it, variant F fixes it)
+                const bool yk = R.yok[c][h];
                 const float xm = R.xok[c][h] ? (p.a_scale ? R.xs[c][h] : 1.f) : 0.f;
-                yv[h][0] = R.y[c][h].x * ym; yv[h][1] = R.y[c][h].y * ym;
-                yv[h][2] = R.y[c][h].z * ym; yv[h][3] = R.y[c][h].w * ym;
+                yv[h][0] = yk ? R.y[c][h].x : 0.f; yv[h][1] = yk ? R.y[c][h].y : 0.f;
+                yv[h][2] = yk ? R.y[c][h].z : 0.f; yv[h][3] = yk ? R.y[c][h].w : 0.f;
                 if constexpr (!ABF16) {
                     xv[h][0] = R.x[c][h].x * xm; xv[h][1] = R.x[c][h].y * xm;
                     xv[h][2] = R.x[c][h].z * xm; xv[h][3] = R.x[c][h].w * xm;

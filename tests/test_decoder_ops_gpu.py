@@ -203,9 +203,12 @@ def test_ops_refuse_cpu_and_never_fall_back():
 # packed-fp32 miscompute in the wgrad staging (wrong low halves in lanes 16-31/48-63 under CU
 # co-residency, relative error 3e-3..1e-2); these catch that class of error.
 BIG = [(32, 600, 256, 768, 1), (32, 600, 512, 256, 3), (32, 120, 192, 768, 3)]
+# T < rows_per_step: the generic row walk (wgrad INC=false), the instantiation whose packed-fp32 build
+# faulted
+GENERIC = [(1200, 16, 256, 768, 1), (800, 24, 512, 256, 3)]
 
 
-@pytest.mark.parametrize("B,T,Cin,Cout,k", BIG)
+@pytest.mark.parametrize("B,T,Cin,Cout,k", BIG + GENERIC)
 @pytest.mark.parametrize("rows_per_step,target_blocks,depth", [(32, -1, 1), (32, 1024, 1), (64, 1024, 1), (32, 512, 2)])
 def test_wgrad_bf16_exact_and_deterministic(B, T, Cin, Cout, k, rows_per_step, target_blocks, depth):
     from matcha.models.components import _ops as O
