@@ -252,6 +252,31 @@ def main():
                  "note": "wall clock incl. host sync for the predicted lengths; random-init weights, length_scale 5"}
         model.train()
 
+    # bf16-mixed vs 32-true on the bench batch (SURVEY 7 "hard parts"): the same weights, tokens, mels and
+    # injected t / z, eval mode; the 32-true product path equals the CPU oracle at this batch (losses to
+    # 0 relative, alignment bit-exact: tests/test_headline_gpu.py::test_bench_batch_b32_vs_oracle)
+    precision_check = None
+    if args.precision == "bf16-mixed":
+        model.eval()
+        gen = torch.Generator(device=dev).manual_seed(44)
+        t_inj = torch.rand(B, 1, 1, generator=gen, device=dev)
+        z_inj = torch.randn(B, 80, Ty, generator=gen, device=dev)
+        res = {}
+        with torch.no_grad():
+            for prec in ("32-true", "bf16-mixed"):
+                with torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec == "bf16-mixed"):
+                    out = model(batch["x"], batch["x_lengths"], batch["y"], batch["y_lengths"], t=t_inj, z=z_inj)
+                res[prec] = ([float(v) for v in out[:3]], out[3].detach())
+        model.train()
+        l32, a32 = res["32-true"]
+        l16, a16 = res["bf16-mixed"]
+        precision_check = {
+            "bf16_loss_rel_err": [round(abs(a - b) / abs(b), 6) for a, b in zip(l16, l32)],
+            "losses": ["dur", "prior", "diff"],
+            "alignment_cell_agreement": round(float((a16 == a32).float().mean().item()), 6),
+            "note": "bf16-mixed vs the 32-true path (= the oracle at this batch) on the bench batch, eval mode, "
+                    "same t / z; the duration loss moves with MAS boundary flips (tests/test_headline_gpu.py)"}
+
     mas_ms = sum(a.elapsed_time(b) for a, b in mas_events) / max(len(mas_events), 1)
     cells = B * Tx * Ty
     mas_gbs = 12.0 * cells / (mas_ms * 1e-3) / 1e9
@@ -327,6 +352,7 @@ def main():
                              "achieved_tflops_step": round(flops / (step_ms * 1e-3) / 1e12, 2),
                              "peak_tflops": FP32_MFMA_TFLOPS if args.precision == "32-true" else BF16_DENSE_TFLOPS},
             "losses": [round(v, 5) for v in losses],
+            "precision_check": precision_check,
             "synthesise": synth,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -244,7 +244,9 @@ int mtts_rope_qk(const float *x, float *y, int32_t rows, int32_t T, int32_t C, i
  *   coef = min(max_norm / (||g||_2 + 1e-6), 1) (max_norm <= 0: no clipping); t = *step + 1;
  *   p *= 1 - lr*wd; m += (1-b1)(g*coef - m); v = b2 v + (1-b2)(g*coef)^2;
  *   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps);  *step = t.
- * lr and step are device scalars (graph-replay safe); the norm is reduced in a fixed order.
+ * lr (fp64) and step (fp32) are device scalars (graph-replay safe); the norm is reduced in a fixed order.
+ * betas / eps / weight decay / lr are doubles as in torch: every derived scalar (1-b1, 1-b2, lr/(1-b1^t),
+ * sqrt(1-b2^t), 1-lr*wd) is formed in double and rounded to fp32 once, then each torch op rounds once.
  * ------------------------------------------------------------------------------------------- */
 typedef struct mtts_adamw_chunk {
     const float *grad;
@@ -255,8 +257,8 @@ typedef struct mtts_adamw_chunk {
 
 size_t mtts_clip_adamw_workspace_size(int32_t nchunks);
 int mtts_clip_adamw(const mtts_adamw_chunk *chunks, int32_t nchunks, float *params, float *exp_avg,
-                    float *exp_avg_sq, const float *lr, float *step, float max_norm, float beta1, float beta2,
-                    float eps, float weight_decay, void *workspace, size_t workspace_bytes, void *hip_stream);
+                    float *exp_avg_sq, const double *lr, float *step, float max_norm, double beta1, double beta2,
+                    double eps, double weight_decay, void *workspace, size_t workspace_bytes, void *hip_stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Partial-sum reductions of the parameter gradients, batched.
@@ -303,6 +305,18 @@ int mtts_cfm_pack_fwd(const float *x1, const float *z, const float *t, const flo
 int mtts_cfm_pack_bwd(const float *d_packed, int32_t B, int32_t C, int32_t T, float *d_mu, void *hip_stream);
 /* SinusoidalPosEmb: out[b,k] = sin(scale t_b f_k), out[b,dim/2+k] = cos(...), f_k = exp(-k ln(1e4)/(dim/2-1)) */
 int mtts_time_embedding(const float *t, int32_t B, int32_t dim, float scale, float *out, void *hip_stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Token embedding (text_encoder.py:341-342 nn.Embedding, :389 `embedding(x) * sqrt(C)`), csrc/embedding.hip
+ * ------------------------------------------------------------------------------------------- */
+/* out[r,:] = weight[ids[r],:] * scale; ids int64 [rows] in [0, V) (validated by the caller: out-of-range ids
+ * are clamped, where torch raises a device assert); weight [V,C], out [rows,C] fp32. */
+int mtts_embedding_fwd(const int64_t *ids, const float *weight, int64_t rows, int32_t V, int32_t C, float scale,
+                       float *out, void *hip_stream);
+/* dweight[v,:] = sum_{r: ids[r]==v, ascending r} dout[r,:] * scale (overwrites; deterministic, unlike torch's
+ * atomic embedding backward); C <= 1024. */
+int mtts_embedding_bwd(const int64_t *ids, const float *dout, int64_t rows, int32_t V, int32_t C, float scale,
+                       float *dweight, void *hip_stream);
 
 #ifdef __cplusplus
 } /* extern "C" */

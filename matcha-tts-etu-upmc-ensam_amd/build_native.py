@@ -40,6 +40,7 @@ if VARIANT != "pk":
 EXTRA = {
     "mas.hip": ["-ffp-contract=off"],
     "cfm_prep.hip": ["-ffp-contract=off"],  # phi_t and the time embedding round like torch (no fma)
+    "losses.hip": ["-ffp-contract=off"],  # u = x1 - (1 - sigma) z and the prior term: torch's roundings
 }
 
 

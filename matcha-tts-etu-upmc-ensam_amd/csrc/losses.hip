@@ -11,6 +11,8 @@
 // channel-major [B, C, T].  One workgroup per (utterance, 64-frame tile): the token-major tile
 // (64 x C contiguous floats) is staged through LDS (row pitch C+1: conflict-free transposed reads),
 // the channel-major rows are read 64 frames at a time (256-byte coalesced).
+// u = x1 - (1 - sigma) z rounds like torch's two ops (mul, then sub: built with -ffp-contract=off, the
+// same as cfm_prep.hip's phi_t).
 // Sums: per-thread fp32 in a fixed order, then a fixed tree per workgroup, then the finalize kernel
 // sums the workgroup partials in index order -- deterministic and run-to-run identical.
 #include <hip/hip_runtime.h>
@@ -174,7 +176,7 @@ extern "C" int mtts_losses_fwd(const float *u_pred, const float *x1, const float
     dim3 grid((T + kLT - 1) / kLT, B);
     float *part = static_cast<float *>(workspace);
     hipLaunchKernelGGL(loss_partials_kernel, grid, dim3(kLThreads), 0, st, u_pred, x1, z, y, mu_y, mask, C, T,
-                       1.f - sigma_min, part);
+                       (float)(1.0 - (double)sigma_min), part);  // torch: (1 - s) is a Python double
     int rc = mtts::check_launch("loss_partials_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(kLThreads), 0, st, part, (int)(grid.x * grid.y), mask,
@@ -193,6 +195,7 @@ extern "C" int mtts_losses_bwd(const float *g_diff, const float *g_prior, const 
     if (!du_pred && !dmu_y) return MTTS_OK;
     dim3 grid((T + kLT - 1) / kLT, B);
     hipLaunchKernelGGL(loss_bwd_kernel, grid, dim3(kLThreads), 0, static_cast<hipStream_t>(hip_stream), g_diff,
-                       g_prior, fwd_out + 2, u_pred, x1, z, y, mu_y, mask, C, T, 1.f - sigma_min, du_pred, dmu_y);
+                       g_prior, fwd_out + 2, u_pred, x1, z, y, mu_y, mask, C, T, (float)(1.0 - (double)sigma_min), du_pred,
+                       dmu_y);
     return mtts::check_launch("loss_bwd_kernel");
 }

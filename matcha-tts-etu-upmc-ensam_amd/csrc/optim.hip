@@ -6,6 +6,8 @@
 //   total = ||g||_2 over all parameters,  coef = min(max_norm / (total + 1e-6), 1)
 //   g' = g * coef;  p *= 1 - lr*wd;  m = m + (1-b1)(g' - m);  v = b2 v + (1-b2) g'^2
 //   p -= lr / (1 - b1^t) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+// with torch's scalars (double on the host, rounded to fp32 once) and one rounding per torch op, so
+// the result is within 1-2 ulp of torch's AdamW (tests/test_training_gpu.py).
 // torch runs this as ~8 multi-tensor launches (norm, scale, fused Adam per dtype/device group) over
 // ~300 tensors: 0.44 ms per step at 19 M parameters.  Here the parameters and both moment buffers
 // are one flat fp32 array each (the model's parameters are views into it), the gradients are
@@ -63,30 +65,42 @@ __global__ __launch_bounds__(kThreads) void adamw_sumsq_kernel(const mtts_adamw_
 __global__ __launch_bounds__(kThreads) void adamw_update_kernel(const mtts_adamw_chunk *__restrict__ chunks, int nchunks,
                                                                 const float *__restrict__ partial, float *__restrict__ p,
                                                                 float *__restrict__ m, float *__restrict__ v,
-                                                                const float *__restrict__ lr_ptr,
+                                                                const double *__restrict__ lr_ptr,
                                                                 const float *__restrict__ t_next,
-                                                                float *__restrict__ step, float max_norm, float b1,
-                                                                float b2, float eps, float wd) {
+                                                                float *__restrict__ step, float max_norm, double b1,
+                                                                double b2, double eps_d, double wd) {
     __shared__ float red[kThreads / 64];
     // total squared norm: every block sums the same partials in the same order
     float s = 0.f;
     for (int i = threadIdx.x; i < nchunks; i += kThreads) s += partial[i];
     const float total = sqrtf(block_reduce_sum(s, red));
+    // clip_grad_norm_: coef = clamp(max_norm / (total + 1e-6), max=1), fp32 tensor arithmetic
     float coef = 1.f;
     if (max_norm > 0.f) coef = fminf(max_norm / (total + 1e-6f), 1.f);
     const float t = t_next[0];
     if (blockIdx.x == 0 && threadIdx.x == 0) step[0] = t;
-    const float lr = lr_ptr[0];
-    const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
-    const float step_size = lr / bc1, bc2s = sqrtf(bc2), decay = 1.f - lr * wd;
+    // torch's multi-tensor AdamW (torch/optim/adam.py, decoupled weight decay) derives every scalar in
+    // double precision on the host and hands it to fp32 kernels: the same here, so each constant is the
+    // float torch uses (computing 1 - b2 from a float b2 would be off by 1.3e-5 relative)
+    const double lr = lr_ptr[0];
+    const float decay = (float)(1.0 - lr * wd);
+    const float w1 = (float)(1.0 - b1), b2f = (float)b2, w2 = (float)(1.0 - b2);
+    const float neg_step = (float)(-(lr / (1.0 - pow(b1, (double)t))));
+    const float bc2s = (float)sqrt(1.0 - pow(b2, (double)t));
+    const float eps = (float)eps_d;
     const mtts_adamw_chunk c = chunks[blockIdx.x];
     float *pp = p + c.offset, *mm = m + c.offset, *vv = v + c.offset;
+    // one fp32 rounding per torch op: _foreach_mul_(grads, coef), _foreach_mul_(params, 1 - lr wd),
+    // _foreach_lerp_(m, g, 1 - b1) (weight < 0.5: m + w (g - m)), _foreach_mul_(v, b2),
+    // _foreach_addcmul_(v, g, g, 1 - b2), sqrt(v) / sqrt(bc2) + eps, _foreach_addcdiv_(p, m, denom, -lr / bc1)
     auto upd = [&](float g, float &pi, float &mi, float &vi) {
-        g *= coef;
-        pi *= decay;
-        mi = mi + (1.f - b1) * (g - mi);
-        vi = b2 * vi + (1.f - b2) * g * g;
-        pi = pi - step_size * mi / (sqrtf(vi) / bc2s + eps);
+        g = __fmul_rn(g, coef);
+        pi = __fmul_rn(pi, decay);
+        mi = __fadd_rn(mi, __fmul_rn(w1, __fsub_rn(g, mi)));
+        vi = __fmul_rn(vi, b2f);
+        vi = __fadd_rn(vi, __fmul_rn(__fmul_rn(w2, g), g));
+        const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vi), bc2s), eps);
+        pi = __fadd_rn(pi, __fmul_rn(neg_step, __fdiv_rn(mi, denom)));
     };
     const bool vec = (((uintptr_t)c.grad | (uintptr_t)pp) & 15) == 0;  // flat regions start 16-byte aligned
     const int n4 = vec ? c.n / 4 : 0;
@@ -112,9 +126,9 @@ extern "C" size_t mtts_clip_adamw_workspace_size(int32_t nchunks) {
 }
 
 extern "C" int mtts_clip_adamw(const mtts_adamw_chunk *chunks, int32_t nchunks, float *params, float *exp_avg,
-                               float *exp_avg_sq, const float *lr, float *step, float max_norm, float beta1,
-                               float beta2, float eps, float weight_decay, void *workspace, size_t workspace_bytes,
-                               void *hip_stream) {
+                               float *exp_avg_sq, const double *lr, float *step, float max_norm, double beta1,
+                               double beta2, double eps, double weight_decay, void *workspace,
+                               size_t workspace_bytes, void *hip_stream) {
     MTTS_CHECK_ARG(chunks && params && exp_avg && exp_avg_sq && lr && step && nchunks >= 0,
                    "clip_adamw: null pointer");
     if (nchunks == 0) return MTTS_OK;

@@ -21,11 +21,13 @@ so no loss or gradient depends on them.  For the same reason residual adds use t
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch
 import torch.nn as nn
 
+from matcha import _native as N
 from matcha.models.components import _ops as O
 from matcha.utils.model import sequence_mask
 
@@ -203,6 +205,43 @@ class Encoder(nn.Module):
         return (self.forward_tm(x.transpose(1, 2), m) * m.unsqueeze(-1)).transpose(1, 2)
 
 
+class _Embedding(torch.autograd.Function):
+    """embedding(ids) * scale (text_encoder.py:389) in one HIP launch; the weight gradient sums each
+    token's rows in index order (csrc/embedding.hip) -- deterministic, where torch's embedding backward
+    uses atomics -- so the whole train step is bit-reproducible run to run."""
+
+    @staticmethod
+    def forward(ctx, ids, weight, scale):
+        N.require_device(ids, weight)
+        ids_c = ids.reshape(-1).to(torch.int64).contiguous()
+        w = weight.detach().to(torch.float32).contiguous()
+        V, C = w.shape
+        out = torch.empty(ids_c.numel(), C, dtype=torch.float32, device=w.device)
+        with torch.cuda.device(w.device):
+            N.check(N.lib().mtts_embedding_fwd(N.ptr(ids_c), N.ptr(w), ids_c.numel(), V, C, float(scale), N.ptr(out),
+                                               N.stream_handle(w.device)), "mtts_embedding_fwd")
+        ctx.save_for_backward(ids_c)
+        ctx.shape, ctx.scale = (V, C), float(scale)
+        return out.view(*ids.shape, C)
+
+    @staticmethod
+    def backward(ctx, g):
+        (ids_c,) = ctx.saved_tensors
+        V, C = ctx.shape
+        gc = g.detach().to(torch.float32).reshape(-1, C).contiguous()
+        dw = torch.empty(V, C, dtype=torch.float32, device=gc.device)
+        with torch.cuda.device(gc.device):
+            N.check(N.lib().mtts_embedding_bwd(N.ptr(ids_c), N.ptr(gc), ids_c.numel(), V, C, ctx.scale, N.ptr(dw),
+                                               N.stream_handle(gc.device)), "mtts_embedding_bwd")
+        return None, dw, None
+
+
+N.register("mtts_embedding_fwd", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                                ctypes.c_int32, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p])
+N.register("mtts_embedding_bwd", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                                ctypes.c_int32, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p])
+
+
 class TextEncoder(nn.Module):
     def __init__(self, encoder_type, encoder_params, duration_predictor_params, n_vocab):
         super().__init__()
@@ -227,7 +266,8 @@ class TextEncoder(nn.Module):
     def forward(self, text_input, text_lengths):
         """text_encoder.py:376-402 -> (mu [B, n_feats, T], logw [B, 1, T], x_mask [B, 1, T])."""
         with O.weight_pack_scope(self):
-            emb = self.embedding(text_input) * math.sqrt(self.channel_dim)  # [B, T, C]: token-major already
+            # [B, T, C]: token-major already
+            emb = _Embedding.apply(text_input, self.embedding.weight, math.sqrt(self.channel_dim))
             m = sequence_mask(text_lengths, emb.size(1)).to(emb.dtype)
             h = self.prenet.forward_tm(emb, m) if self.prenet is not None else emb
             h = self.encoder.forward_tm(h, m)

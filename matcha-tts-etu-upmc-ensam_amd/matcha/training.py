@@ -62,13 +62,15 @@ class _AdamWChunk(ctypes.Structure):  # include/mtts_decoder.h mtts_adamw_chunk
 class _FlatClipAdamW:
     """clip_grad_norm_(max_norm) + AdamW(lr, (0.9, 0.999), eps 1e-8, wd 1e-6) -- the reference step's
     optimizer (baselightningmodule.py:59-65, train.py gradient_clip_val) -- as mtts_clip_adamw over a
-    flat parameter array.  lr is a device scalar (the cosine schedule writes it); the step count lives
+    flat parameter array.  lr is a float64 device scalar (the cosine schedule writes it); the step count lives
     on the device; the gradient table is rebuilt whenever the gradient tensors change (eager calls)
     and frozen by bind_grads() for graph capture."""
 
     CHUNK = 32768
 
     def __init__(self, params, lr: torch.Tensor, max_norm: float, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-6):
+        if lr.dtype != torch.float64:
+            raise TypeError("lr must be a float64 device scalar (torch derives AdamW's scalars in double)")
         self.params = list(params)
         dev = self.params[0].device
         offs, off = [], 0
@@ -146,7 +148,7 @@ class _FlatClipAdamW:
 N.register("mtts_clip_adamw_workspace_size", ctypes.c_size_t, [ctypes.c_int32])
 N.register("mtts_clip_adamw", ctypes.c_int,
            [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-            ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+            ctypes.c_void_p, ctypes.c_float, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
             ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p])
 
 
@@ -184,7 +186,7 @@ class Trainer:
             self.flat = None  # N>1: packed gradients for the all-reduce (sized at capture)
             for p in self.params:
                 p.grad = None
-            self.lr = torch.tensor(cfg.lr, device=self.dev)
+            self.lr = torch.tensor(cfg.lr, device=self.dev, dtype=torch.float64)  # torch keeps lr a double
             # clip + AdamW as two HIP launches (csrc/optim.hip) over one flat fp32 parameter array:
             # the parameters become views into it (names / state_dict unchanged), each region
             # 16-byte aligned; the moments are flat arrays of the same layout

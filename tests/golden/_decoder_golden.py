@@ -232,6 +232,116 @@ def model_case(out, seed=13):
                                  sum(p.numel() for p in model.decoder.parameters())], np.int64)
 
 
+def headline_case(out, seed=41, B=4, Tx=120, Ty=600):
+    """BASELINE config 3's shape (Tx=120, Ty=600) at B=4: the reference MatchaTTS.forward
+    (matcha_tts.py:247-325) in fp32 eval mode with t / z replayed from the seed
+    (flow_matching.py:130,133): losses, the MAS alignment and per-parameter gradient norms."""
+    import torch
+
+    from matcha.models.matcha_tts import MatchaTTS
+    from weights_recipe import apply_recipe
+
+    model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192)
+    apply_recipe(model, seed)
+    model.eval()
+    g = torch.Generator().manual_seed(seed + 1)
+    # SURVEY 8d: lengths U[0.7 max, max] with element 0 = max
+    x_lengths = torch.tensor([Tx] + [int(v) for v in torch.randint(int(0.7 * Tx), Tx + 1, (B - 1,), generator=g)])
+    y_lengths = torch.tensor([Ty] + [int(v) for v in torch.randint(int(0.7 * Ty), Ty + 1, (B - 1,), generator=g)])
+    x = torch.randint(1, 150, (B, Tx), generator=g) * (torch.arange(Tx)[None] < x_lengths[:, None])
+    y = torch.randn(B, 80, Ty, generator=g) * (torch.arange(Ty)[None, None] < y_lengths[:, None, None])
+    torch.manual_seed(seed + 2)
+    t_inj = torch.rand([B, 1, 1])
+    z_inj = torch.randn(B, 80, Ty)
+    torch.manual_seed(seed + 2)
+    dur, prior, diff, attn = model(x=x, x_lengths=x_lengths, y=y, y_lengths=y_lengths)
+    (dur + prior + diff).backward()
+    out["h_x"], out["h_x_lengths"], out["h_y"], out["h_y_lengths"] = x.numpy(), x_lengths.numpy(), y.numpy(), y_lengths.numpy()
+    out["h_t"], out["h_z"] = t_inj.numpy(), z_inj.numpy()
+    out["h_losses"] = np.array([dur.item(), prior.item(), diff.item()], np.float64)
+    out["h_attn_rows"] = attn_row_starts(attn.detach().numpy())
+    out["h_param_names"] = np.array([n for n, _ in model.named_parameters()])
+    out["h_grad_norms"] = np.array([p.grad.double().norm().item() if p.grad is not None else 0.0
+                                    for _, p in model.named_parameters()])
+
+
+def attn_row_starts(attn):
+    """[B, Tx, Ty] 0/1 monotone path -> int32 [B, Tx] first column of each row (-1: empty row)."""
+    B, Tx, _ = attn.shape
+    rows = np.full((B, Tx), -1, np.int32)
+    for b in range(B):
+        for x in range(Tx):
+            nz = np.flatnonzero(attn[b, x])
+            if nz.size:
+                rows[b, x] = nz[0]
+                assert np.all(attn[b, x, nz[0]:nz[-1] + 1] == 1)
+    return rows
+
+
+def synth_case(out, prefix, seed, B, Tx, x_lengths, n_timesteps, length_scale, temperature=1.0):
+    """The reference MatchaTTS.synthesise (matcha_tts.py:178-245: encoder, ceil'd durations,
+    generate_path, Euler ODE flow_matching.py:42-104) run from a seed; the Gaussian draw
+    z = randn_like(mu) * temperature (flow_matching.py:60) is replayed from the same seed."""
+    import torch
+
+    from matcha.models.matcha_tts import MatchaTTS
+    from weights_recipe import apply_recipe
+
+    model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192)
+    apply_recipe(model, seed)
+    model.eval()
+    g = torch.Generator().manual_seed(seed + 1)
+    xl = torch.tensor(x_lengths)
+    x = torch.randint(1, 150, (B, Tx), generator=g) * (torch.arange(Tx)[None] < xl[:, None])
+    # record the reference's own draw: z = randn_like(mu) (flow_matching.py:60), then * temperature
+    drawn = []
+    real_randn_like = torch.randn_like
+
+    def recording_randn_like(*a, **k):
+        drawn.append(real_randn_like(*a, **k))
+        return drawn[-1]
+
+    torch.manual_seed(seed + 2)
+    torch.randn_like = recording_randn_like
+    try:
+        res = model.synthesise(x, xl, n_timesteps, temperature=temperature, length_scale=length_scale)
+    finally:
+        torch.randn_like = real_randn_like
+    assert len(drawn) == 1
+    z = drawn[0] * temperature
+    out[prefix + "x"], out[prefix + "x_lengths"] = x.numpy(), xl.numpy()
+    out[prefix + "z"] = z.numpy()
+    out[prefix + "cfg"] = np.array([n_timesteps, length_scale, temperature], np.float64)
+    for k in ("encoder_outputs", "decoder_outputs", "mel", "mel_lengths"):
+        out[prefix + k] = res[k].numpy()
+    out[prefix + "attn"] = res["attn"].numpy().astype(np.int8)
+
+
+def main_headline():
+    install_shims()
+    sys.path.insert(0, str(HERE))
+    import torch
+
+    torch.set_num_threads(8)
+    out: dict[str, np.ndarray] = {}
+    headline_case(out)
+    np.savez_compressed(HERE / "headline_golden.npz", **out)
+    print("wrote headline_golden.npz", out["h_losses"])
+
+
+def main_synth():
+    install_shims()
+    sys.path.insert(0, str(HERE))
+    import torch
+
+    torch.set_num_threads(8)
+    out: dict[str, np.ndarray] = {}
+    synth_case(out, "a_", 23, 2, 11, [11, 8], 4, 1.0)
+    synth_case(out, "b_", 29, 3, 17, [17, 12, 5], 6, 2.0, temperature=0.667)
+    np.savez_compressed(HERE / "synth_golden.npz", **out)
+    print("wrote synth_golden.npz", {k: v.shape for k, v in out.items()})
+
+
 def main():
     install_shims()
     sys.path.insert(0, str(HERE))

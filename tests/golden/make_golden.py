@@ -3,7 +3,9 @@ container, where /root/reference exists; the fixtures are committed and travel t
 
     make -C oracle ref                      # compiles the reference core.pyx into oracle/_ref/
     python tests/golden/make_golden.py mas  # MAS fixtures from the compiled Cython
-    python tests/golden/make_golden.py decoder  # decoder/CFM/MatchaTTS fixtures (see _decoder.py)
+    python tests/golden/make_golden.py decoder  # decoder/CFM/MatchaTTS fixtures (see _decoder_golden.py)
+    python tests/golden/make_golden.py headline # MatchaTTS.forward at the bench shape (B=4, 120x600)
+    python tests/golden/make_golden.py synth    # MatchaTTS.synthesise with the z draw replayed
 
 MAS fixtures (mas_golden.npz) -- outputs of compute_batch_alignments (core.pyx:101-128) and of the
 reference wrapper maximum_path (__init__.py:40-55):
@@ -157,3 +159,11 @@ if __name__ == "__main__":
         import _decoder_golden  # noqa: E402
 
         _decoder_golden.main()
+    if "headline" in what or "synth" in what:
+        sys.path.insert(0, str(HERE))
+        import _decoder_golden  # noqa: E402
+
+        if "headline" in what:
+            _decoder_golden.main_headline()
+        if "synth" in what:
+            _decoder_golden.main_synth()

@@ -66,7 +66,7 @@ def test_time_embedding(B, dim, scale):
     assert torch.allclose(got[:, :4], want[:, :4], atol=1e-6)
 
 
-@pytest.mark.parametrize("B,C,T", [(2, 80, 50), (4, 80, 301)])
+@pytest.mark.parametrize("B,C,T", [(2, 80, 50), (4, 80, 301), (3, 128, 97)])
 def test_fused_losses_match_torch(B, C, T):
     from matcha.models.components.flow_matching import fused_losses
 
@@ -89,4 +89,24 @@ def test_fused_losses_match_torch(B, C, T):
     (diff + 0.5 * prior).backward()
     (diff_w + 0.5 * prior_w).backward()
     torch.testing.assert_close(u_pred.grad, u_ref.grad, rtol=1e-5, atol=1e-8)
+    torch.testing.assert_close(mu_y.grad, mu_ref.grad, rtol=1e-5, atol=1e-8)
+
+
+def test_fused_prior_loss_only():
+    """prior_loss without the CFM term (u_pred=None, MatchaTTS with a decoder computing its own loss):
+    matcha_tts.py:319-323 on the [B, T] mask."""
+    from matcha.models.components.flow_matching import fused_losses
+
+    B, C, T = 3, 80, 77
+    x1, z, t, mu_y = _inputs(B, C, T, 9)
+    lengths = torch.tensor([77, 40, 12], device=DEV)
+    mask = (torch.arange(T, device=DEV)[None] < lengths[:, None]).float().unsqueeze(1)
+    mu_y.requires_grad_(True)
+    diff, prior = fused_losses(None, mu_y, x1, z, mask, 1e-4)
+    mu_ref = mu_y.detach().clone().requires_grad_(True)
+    prior_w = torch.sum(0.5 * ((x1 - mu_ref) ** 2 + math.log(2 * math.pi)) * mask) / (torch.sum(mask) * C)
+    assert diff.item() == 0.0
+    torch.testing.assert_close(prior, prior_w, rtol=1e-5, atol=1e-6)
+    prior.backward()
+    prior_w.backward()
     torch.testing.assert_close(mu_y.grad, mu_ref.grad, rtol=1e-5, atol=1e-8)

@@ -202,3 +202,31 @@ def test_encoder_bf16_deterministic():
             mu, logw, _ = m.encoder(b["x"], b["x_lengths"])
         outs.append((mu.clone(), logw.clone()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("B,T,V,C", [(32, 120, 150, 192), (3, 17, 150, 192), (2, 5, 7, 40), (1, 300, 150, 1000)])
+def test_embedding_fwd_bitwise_bwd_deterministic(B, T, V, C):
+    """Token embedding * sqrt(C) (text_encoder.py:389): forward bitwise equal to torch's lookup and
+    multiply; weight gradient within fp32 summation-order rounding of a float64 sum, and bitwise
+    identical run to run (torch's own backward sums with atomics)."""
+    import math
+
+    from matcha.models.components.text_encoder import _Embedding
+
+    g = torch.Generator().manual_seed(B * T + V)
+    ids = torch.randint(0, V, (B, T), generator=g).to(DEV)
+    ids[0, : min(T, 40)] = 3  # one token owning many rows
+    w = torch.randn(V, C, generator=g).to(DEV).requires_grad_(True)
+    dout = torch.randn(B, T, C, generator=g).to(DEV)
+    s = math.sqrt(C)
+    out = _Embedding.apply(ids, w, s)
+    want = torch.nn.functional.embedding(ids, w.detach()) * s
+    assert torch.equal(out, want)
+    out.backward(dout)
+    g1 = w.grad.clone()
+    w.grad = None
+    _Embedding.apply(ids, w, s).backward(dout)
+    assert torch.equal(w.grad, g1)
+    ref = torch.zeros(V, C, dtype=torch.float64, device=DEV).index_add_(0, ids.reshape(-1),
+                                                                        (dout * s).reshape(-1, C).double())
+    torch.testing.assert_close(g1.double(), ref, rtol=1e-5, atol=1e-4)

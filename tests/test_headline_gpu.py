@@ -1,0 +1,147 @@
+"""The bench configuration (BASELINE config 3: Tx=120, Ty=600) pinned against the reference in both
+precisions.
+
+* headline_golden.npz: the REFERENCE MatchaTTS.forward (matcha_tts.py:247-325) at B=4, 120x600,
+  fp32, eval mode, t / z replayed from the seed (tests/golden/_decoder_golden.py headline_case).
+* B=32 (the bench batch): the product against the CPU oracle restatement (oracle/matcha_oracle.py,
+  itself pinned to the reference fixtures) on the same weights, tokens, mels, t and z.
+
+32-true: alignment bit-exact, each loss within 1e-4 relative (the north star's bar).
+bf16-mixed (what bench.py runs): MFMA operands in bf16, so the encoder's mu_x moves by ~3e-3
+relative and logw by ~1e-2.  The bounds below (BF16_LOSS_RTOL, per loss) come from the errors
+measured on the MI355X (profiles/r02/precision.md):
+  prior / diff loss: 2.2e-4 .. 4.2e-4 relative (B=4, B=32, 512x4096)  -> bound 1e-3;
+  duration loss: 3.1e-3 (B=32), 3.9e-3 (512x4096), 9.9e-2 (B=4)       -> bound 0.15.
+The duration loss is the sensitive one: it compares logw with log(durations of the MAS path), and
+the MAS is an argmax -- under the bf16 lattice perturbation near-tied DP decisions flip and move
+row boundaries by a frame (B=4: 28 of 437 rows changed duration, 0.5 % of the path cells), which
+moves log(duration) by up to log 2 for short rows.  The alignment is therefore compared cell by cell
+(BF16_ATTN_AGREE).
+"""
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from golden._decoder_golden import attn_row_starts
+from golden.weights_recipe import apply_recipe
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+GH = np.load(Path(__file__).parent / "golden" / "headline_golden.npz")
+FP32_LOSS_RTOL = 1e-4       # north star: mel / flow-matching loss within 1e-4 relative
+BF16_LOSS_RTOL = np.array([0.15, 1e-3, 1e-3])  # (dur, prior, diff), from the measurements above
+BF16_ATTN_AGREE = 0.99      # fraction of [Tx, Ty] alignment cells equal to the fp32 reference path
+
+
+def _run(model, x, xl, y, yl, t, z, precision):
+    amp = torch.autocast("cuda", dtype=torch.bfloat16, enabled=precision == "bf16-mixed")
+    with amp:
+        dur, prior, diff, attn = model(x, xl, y, yl, t=t, z=z)
+        total = dur + prior + diff
+    total.backward()
+    torch.cuda.synchronize()
+    return np.array([dur.item(), prior.item(), diff.item()]), attn.detach().cpu().numpy()
+
+
+def _product(seed):
+    from matcha.models.matcha_tts import MatchaTTS
+
+    model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(DEV)
+    apply_recipe(model, seed)
+    model.eval()
+    return model
+
+
+def _agree(attn, ref_attn, xl, yl):
+    """Fraction of valid [t_x, t_y] cells where two 0/1 alignments agree."""
+    same = total = 0
+    for b in range(attn.shape[0]):
+        a, r = attn[b, : xl[b], : yl[b]], ref_attn[b, : xl[b], : yl[b]]
+        same += int((a == r).sum())
+        total += a.size
+    return same / total
+
+
+@pytest.mark.parametrize("precision", ["32-true", "bf16-mixed"])
+def test_headline_b4_vs_reference(precision):
+    model = _product(41)
+    g = lambda k: torch.from_numpy(GH[k]).to(DEV)  # noqa: E731
+    got, attn = _run(model, g("h_x"), g("h_x_lengths"), g("h_y"), g("h_y_lengths"), g("h_t"), g("h_z"), precision)
+    want = GH["h_losses"]
+    err = np.abs(got - want) / np.abs(want)
+    rows = attn_row_starts(attn.astype(np.int8))
+    print(f"{precision}: losses {got} reference {want} rel err {err}")
+    if precision == "32-true":
+        np.testing.assert_array_equal(rows, GH["h_attn_rows"])
+        assert (err <= FP32_LOSS_RTOL).all(), err
+        gn = np.array([p.grad.double().norm().item() if p.grad is not None else 0.0 for _, p in model.named_parameters()])
+        np.testing.assert_allclose(gn, GH["h_grad_norms"], rtol=5e-3, atol=1e-6)
+    else:
+        import oracle_bind as OB
+
+        xl, yl = GH["h_x_lengths"], GH["h_y_lengths"]
+        ref_attn = OB.row_start_to_path(GH["h_attn_rows"], xl, yl, attn.shape[-1])
+        agree = _agree(attn.astype(np.int8), ref_attn, xl, yl)
+        with torch.no_grad():
+            enc32 = model.encoder(g("h_x"), g("h_x_lengths"))
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                enc16 = model.encoder(g("h_x"), g("h_x_lengths"))
+        m = enc32[2]
+        d_logw = ((enc16[1] - enc32[1]) * m).abs().max().item()
+        r_mu = ((enc16[0] - enc32[0]) * m).norm().item() / (enc32[0] * m).norm().item()
+        dur16 = attn.astype(np.int64).sum(-1)
+        dur32 = ref_attn.astype(np.int64).sum(-1)
+        print(f"bf16 alignment agreement {agree:.5f}; rows whose duration moved {(dur16 != dur32).sum()} of "
+              f"{int(xl.sum())}; max |logw16 - logw32| {d_logw:.4f}; mu_x rel err {r_mu:.2e}")
+        assert (err <= BF16_LOSS_RTOL).all(), err
+        assert agree >= BF16_ATTN_AGREE
+
+
+_B32 = {}
+
+
+def _oracle_b32():
+    """The CPU oracle's fp32 forward at the bench batch (B=32, 120x600), computed once per session."""
+    if not _B32:
+        import oracle_bind as OB
+        from matcha.training import synthetic_batch
+        from oracle import matcha_oracle as MO
+
+        def mp(value, mask):
+            return torch.from_numpy(OB.maximum_path(value.detach().float().numpy(), mask.detach().float().numpy())[0])
+
+        ref = MO.MatchaTTSOracle(150, 80, 192, maximum_path=mp)
+        apply_recipe(ref, 43)
+        ref.eval()
+        b = synthetic_batch(32, 120, 600, seed=1000, device="cpu")
+        gen = torch.Generator().manual_seed(44)
+        t = torch.rand(32, 1, 1, generator=gen)
+        z = torch.randn(32, 80, 600, generator=gen)
+        with torch.no_grad():
+            dur, prior, diff, attn = ref(b["x"], b["x_lengths"], b["y"], b["y_lengths"], t=t, z=z)
+        _B32.update(batch=b, t=t, z=z, losses=np.array([float(dur), float(prior), float(diff)]),
+                    attn=attn.numpy().astype(np.int8))
+    return _B32
+
+
+@pytest.mark.parametrize("precision", ["32-true", "bf16-mixed"])
+def test_bench_batch_b32_vs_oracle(precision):
+    o = _oracle_b32()
+    model = _product(43)
+    b = {k: v.to(DEV) for k, v in o["batch"].items()}
+    got, attn = _run(model, b["x"], b["x_lengths"], b["y"], b["y_lengths"], o["t"].to(DEV), o["z"].to(DEV), precision)
+    err = np.abs(got - o["losses"]) / np.abs(o["losses"])
+    xl, yl = o["batch"]["x_lengths"].numpy(), o["batch"]["y_lengths"].numpy()
+    agree = _agree(attn.astype(np.int8), o["attn"], xl, yl)
+    print(f"B=32 {precision}: losses {got} oracle {o['losses']} rel err {err} alignment agreement {agree:.6f}")
+    if precision == "32-true":
+        np.testing.assert_array_equal(attn.astype(np.int8), o["attn"])
+        assert (err <= FP32_LOSS_RTOL).all(), err
+    else:
+        assert (err <= BF16_LOSS_RTOL).all(), err
+        assert agree >= BF16_ATTN_AGREE
+    assert all(p.grad is None or torch.isfinite(p.grad).all() for p in model.parameters())

@@ -120,3 +120,28 @@ def test_synthesise_vs_oracle(length_scale, n_steps):
     assert rel(out["encoder_outputs"].cpu().numpy(), exp["encoder_outputs"].numpy()) < 1e-5
     assert rel(out["decoder_outputs"].cpu().numpy(), exp["decoder_outputs"].numpy()) < 1e-4
     assert rel(out["mel"].cpu().numpy(), exp["mel"].numpy()) < 1e-4
+
+
+GS = np.load(Path(__file__).parent / "golden" / "synth_golden.npz")
+
+
+@pytest.mark.parametrize("prefix,seed", [("a_", 23), ("b_", 29)])
+def test_synthesise_vs_reference(prefix, seed):
+    """MatchaTTS.synthesise against the REFERENCE's own synthesise (matcha_tts.py:178-245,
+    flow_matching.py:42-104, model.py:77-114) run from a seed, with its z = randn_like(mu) * temperature
+    replayed (synth_golden.npz, tests/golden/_decoder_golden.py synth_case): lengths and alignment
+    exact, outputs within 1e-4 relative (fp32 MFMA mode)."""
+    from matcha.models.matcha_tts import MatchaTTS
+
+    model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(DEV)
+    apply_recipe(model, seed)
+    model.eval()
+    n_steps, length_scale, temperature = GS[prefix + "cfg"]
+    g = lambda k: torch.from_numpy(GS[prefix + k]).to(DEV)  # noqa: E731
+    out = model.synthesise(g("x"), g("x_lengths"), int(n_steps), temperature=float(temperature),
+                           length_scale=float(length_scale), z=g("z"))
+    np.testing.assert_array_equal(out["mel_lengths"].cpu().numpy(), GS[prefix + "mel_lengths"])
+    np.testing.assert_array_equal(out["attn"].cpu().numpy().astype(np.int8), GS[prefix + "attn"])
+    for k in ("encoder_outputs", "decoder_outputs", "mel"):
+        assert out[k].shape == GS[prefix + k].shape, k
+        assert rel(out[k].cpu().numpy(), GS[prefix + k]) < 1e-4, k
