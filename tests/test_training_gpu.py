@@ -156,13 +156,17 @@ def test_clip_adamw_matches_torch(grad_scale):
         assert (norm.item() > 1.0) == (grad_scale > 1.0)
         for i, (a, b) in enumerate(zip(p_hip, p_ref)):
             d = (a.detach() - b.detach()).abs()
-            assert (d <= _ulp2(b.detach())).all(), (step, i, d.max().item())
+            r = d / _ulp2(b.detach())
+            j = int(r.argmax())
+            assert r.max() <= 1.0, (step, i, a.reshape(-1)[j].item(), b.reshape(-1)[j].item(), grads[step][i].reshape(-1)[j].item())
         m_ref = torch.cat([ref.state[p]["exp_avg"].reshape(-1) for p in p_ref])
         v_ref = torch.cat([ref.state[p]["exp_avg_sq"].reshape(-1) for p in p_ref])
         m_hip = torch.cat([opt.exp_avg[o:o + p.numel()] for p, o in zip(p_hip, opt.offsets)])
         v_hip = torch.cat([opt.exp_avg_sq[o:o + p.numel()] for p, o in zip(p_hip, opt.offsets)])
-        torch.testing.assert_close(m_hip, m_ref, rtol=1e-6, atol=1e-12)
-        torch.testing.assert_close(v_hip, v_ref, rtol=1e-6, atol=1e-16)
+        # the clip coefficient (a norm summed in another order) may differ by an ulp, which moves every
+        # clipped gradient -- and the moments built from it -- by an ulp of the gradient scale
+        torch.testing.assert_close(m_hip, m_ref, rtol=1e-6, atol=4 * torch.finfo(torch.float32).eps * m_ref.abs().max().item())
+        torch.testing.assert_close(v_hip, v_ref, rtol=1e-6, atol=4 * torch.finfo(torch.float32).eps * v_ref.abs().max().item())
 
 
 def _inject(m, t, z):
@@ -227,5 +231,6 @@ def test_accumulate_grad_batches_2_vs_torch(graph):
 
 
 def _ulp2(r):
-    """2 ulp of the parameter, or of the update (~lr = 1e-4) where the parameter is smaller."""
-    return 2 * torch.finfo(torch.float32).eps * r.abs().clamp_min(1e-4)
+    """2 ulp of the parameter, or -- where the parameter is smaller than the updates it has received
+    (three steps of ~lr = 1e-4 each) -- 2 ulp of that accumulated update."""
+    return 2 * torch.finfo(torch.float32).eps * r.abs().clamp_min(4e-4)
