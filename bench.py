@@ -8,7 +8,8 @@
 A step = forward (text encoder, fp32 log-prior lattice, HIP maximum_path, CFM decoder) + backward +
 grad-norm clip (1.0) + AdamW on B=32 utterances per GPU (Tx=120, Ty=600, 80 mels; BASELINE config 3),
 one process per GPU, data parallel over RCCL.  By default the whole step is one captured HIP graph
-replay (N>1: graph fwd+bwd, one RCCL all-reduce of the flat gradient buffer, graph clip+AdamW);
+replay (N>1: the graph also holds the bucketed RCCL all-reduces, forked off as backward completes
+each bucket -- matcha/dp.py -- then clip+AdamW on the averaged flat gradients);
 --no-graph runs it eagerly under DDP.  Inputs are resident in HBM before the timed region.
 Rank 0 prints ONE JSON line: value = utterances/s over all ranks (max-over-ranks wall time), plus
   roofline      the dominant kernel (decoder conv_gemm_kernel): HIP events around each of its launches
@@ -147,6 +148,12 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world == 1 and os.environ.get("MTTS_FORCE_DP") == "1":
+        # rehearsal of the data-parallel step on one GPU: a world-size-1 RCCL group, so the bucketed
+        # all-reduces run (as copies) exactly as at N>1; never used for reported numbers
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29541")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
 
     import matcha.utils.monotonic_align as MA
     from matcha.models.matcha_tts import MatchaTTS
@@ -352,13 +359,17 @@ def main():
                              "achieved_tflops_step": round(flops / (step_ms * 1e-3) / 1e12, 2),
                              "peak_tflops": FP32_MFMA_TFLOPS if args.precision == "32-true" else BF16_DENSE_TFLOPS},
             "losses": [round(v, 5) for v in losses],
+            "dp": None if trainer.reducer is None else {
+                "buckets": len(trainer.reducer.buckets), "bucket_mb": trainer.cfg.bucket_mb,
+                "flat_floats": trainer.reducer.flat.numel(), "transport": type(trainer.reducer.comm).__name__,
+                "overlapped_in_graph": bool(next(iter(trainer._graphs.values()))["overlap"]) if trainer._graphs else None},
             "precision_check": precision_check,
             "synthesise": synth,
         }
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(B, Tx, Ty, args.cpu_budget)
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

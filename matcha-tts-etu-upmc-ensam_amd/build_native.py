@@ -82,7 +82,7 @@ def build(force: bool = False, jobs: int | None = None) -> Path:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
     if force or not LIB.exists() or LIB.stat().st_mtime < max(o.stat().st_mtime for o in objs):
         tmp = LIB.with_suffix(".so.tmp")
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs), "-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -1,0 +1,245 @@
+"""Data-parallel gradient exchange of the training step: bucketed all-reduce overlapped with backward.
+
+The reference trains on one device (train.py:81-84); the north star (BASELINE.json) shards
+utterances over the GPUs of a node with the gradient all-reduce over RCCL overlapped with backward.
+DDP does that eagerly; the captured training step (matcha/training.py, graph=True) needs the
+collectives INSIDE its HIP graph, which torch's ProcessGroupNCCL cannot provide on this stack
+(tools/graph_event_probe.py: its watchdog aborts the process during capture), so:
+
+* ``GradBucketReducer`` lays every differentiated parameter's gradient out in one flat fp32 buffer,
+  in the order backward produces them (recorded in a warm-up pass), cut into ~``bucket_mb`` buckets.
+  A post-accumulate-grad hook counts each bucket's gradients; when the last one lands, the bucket is
+  packed (one ``torch.cat`` into its flat slice, after flushing the deferred weight-gradient sums
+  that produce them) and handed to the communicator on a side stream -- captured, that is a forked
+  branch of the graph, so the reduction of bucket k runs while backward computes bucket k+1.
+  Buckets are issued strictly in index order on every rank (RCCL requires one collective order).
+  The step's logged scalars ride in the last bucket: one collective for everything
+  (baselightningmodule.py:117-199 issues one sync_dist all-reduce per logged value).
+* ``RcclComm``: an RCCL communicator owned by libmtts_hip (csrc/dp_comm.cpp, include/mtts_dp.h)
+  whose ``ncclAllReduce(ncclAvg)`` may be captured.  ``TorchComm``: torch.distributed (gloo on CPU,
+  or any backend eagerly); it cannot be captured, so a graph step with it reduces the whole flat
+  buffer once after the graph (no overlap) -- the shared-GPU gloo rehearsal uses that.
+
+Gradient averaging (mean over ranks) happens in the collective (ncclAvg) or right after it
+(TorchComm: sum then divide), before clipping -- DDP's semantics.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from matcha import _native as N
+
+N.register("mtts_dp_unique_id", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t])
+N.register("mtts_dp_comm_init", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.POINTER(ctypes.c_void_p)])
+N.register("mtts_dp_allreduce_f32", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                                   ctypes.c_void_p])
+N.register("mtts_dp_comm_destroy", ctypes.c_int, [ctypes.c_void_p])
+N.register("mtts_dp_rccl_version", ctypes.c_int, [])
+
+
+class TorchComm:
+    """torch.distributed all-reduce (sum, then / world): eager only."""
+
+    capturable = False
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+
+    def all_reduce_mean_(self, t: torch.Tensor) -> None:
+        dist.all_reduce(t, group=self.group)
+        t.div_(self.world)
+
+
+class RcclComm:
+    """One RCCL communicator for this process (ranks as torch.distributed's), capturable."""
+
+    capturable = True
+
+    def __init__(self, device: torch.device):
+        self.world = dist.get_world_size()
+        self.rank = dist.get_rank()
+        uid = (ctypes.c_char * 128)()
+        if self.rank == 0:
+            N.check(N.lib().mtts_dp_unique_id(uid, 128), "mtts_dp_unique_id")
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=0)  # over the default group's store/backend
+        uid = (ctypes.c_char * 128).from_buffer_copy(box[0])
+        self._comm = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            N.check(N.lib().mtts_dp_comm_init(uid, 128, self.world, self.rank, ctypes.byref(self._comm)),
+                    "mtts_dp_comm_init")
+
+    def all_reduce_mean_(self, t: torch.Tensor) -> None:
+        N.check(N.lib().mtts_dp_allreduce_f32(self._comm, t.data_ptr(), t.numel(), 1,
+                                              torch.cuda.current_stream(t.device).cuda_stream),
+                "mtts_dp_allreduce_f32")
+
+    def close(self):
+        if self._comm:
+            N.lib().mtts_dp_comm_destroy(self._comm)
+            self._comm = ctypes.c_void_p()
+
+
+def make_comm(device: torch.device, kind: str = "auto"):
+    """'rccl' (libmtts_hip's communicator), 'torch' (torch.distributed), 'auto' = rccl on an nccl
+    (RCCL) default group, torch otherwise (gloo)."""
+    if kind == "auto":
+        kind = "rccl" if (device.type == "cuda" and dist.get_backend() == "nccl") else "torch"
+    return RcclComm(device) if kind == "rccl" else TorchComm()
+
+
+class GradBucketReducer:
+    """Flat, bucketed gradient all-reduce (see the module docstring).
+
+    params: the differentiated parameters in the order backward finishes them.  After ``finish()``
+    every parameter's ``.grad`` is a view of the reduced flat buffer (the optimizer reads these) and
+    ``scalars()`` returns the averaged logged values."""
+
+    N_SCALARS = 4
+
+    def __init__(self, params, comm, bucket_mb: float = 16.0, device=None, tail_mb: float = 4.0):
+        self.params = list(params)
+        self.comm = comm
+        self.device = device or self.params[0].device
+        self.index = {id(p): i for i, p in enumerate(self.params)}
+        # buckets are cut from the END of the arrival order: the last bucket (the first layers, whose
+        # gradients backward finishes last) is the one whose reduction cannot overlap anything, so it
+        # is kept small (tail_mb); the others are ~bucket_mb
+        limit = max(int(bucket_mb * 2 ** 20 / 4), 1)
+        tail = max(int(min(tail_mb, bucket_mb) * 2 ** 20 / 4), 1)
+        cuts, end, size = [], len(self.params), 0
+        for i in range(len(self.params) - 1, -1, -1):
+            size += self.params[i].numel()
+            if size >= (tail if not cuts else limit) and i > 0:
+                cuts.append((i, end))
+                end, size = i, 0
+        cuts.append((0, end))
+        self.buckets = [c for c in reversed(cuts) if c[1] > c[0]] or [(0, len(self.params))]  # (start, end)
+        self.bucket_of = []
+        for k, (s, e) in enumerate(self.buckets):
+            self.bucket_of += [k] * (e - s)
+        offs, off = [], 0
+        for p in self.params:
+            offs.append(off)
+            off += p.numel()
+        self.offsets = offs
+        self.n_grad = off
+        # the last bucket's slice also carries the logged scalars (one collective per step)
+        self.flat = torch.zeros(off + self.N_SCALARS, dtype=torch.float32, device=self.device)
+        self.spans = []
+        for k, (s, e) in enumerate(self.buckets):
+            lo = offs[s] if s < len(self.params) else off
+            hi = (offs[e] if e < len(self.params) else off) + (self.N_SCALARS if k == len(self.buckets) - 1 else 0)
+            self.spans.append((lo, hi))
+        self.views = [self.flat[o:o + p.numel()].view_as(p) for p, o in zip(self.params, offs)]
+        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        self.armed = False
+        self.overlap = True
+        self._pending_scalars = None
+        self._ready = [0] * len(self.buckets)
+        self._issued = 0
+        self.grad_refs = None  # the gradient tensors packed in the last armed pass
+
+    # -------------------------------------------------------------------- per step
+    def arm(self, scalars: torch.Tensor, overlap: bool) -> None:
+        """Call before the backward of the last micro-batch.  ``scalars``: the 4 logged values
+        (already the micro-batch mean).  overlap=False packs only; the caller reduces after."""
+        self.armed = True
+        capturing = self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
+        self.overlap = overlap and self.comm is not None and (self.comm.capturable or not capturing)
+        self._pending_scalars = scalars
+        self._ready = [0] * len(self.buckets)
+        self._issued = 0
+        self.grad_refs = [None] * len(self.params)
+
+    def _on_grad(self, p) -> None:
+        if not self.armed:
+            return
+        i = self.index[id(p)]
+        self.grad_refs[i] = p.grad
+        k = self.bucket_of[i]
+        self._ready[k] += 1
+        while self._issued < len(self.buckets):  # strictly in bucket order on every rank
+            k = self._issued
+            s, e = self.buckets[k]
+            if self._ready[k] < e - s:
+                break
+            self._issue(k)
+            self._issued += 1
+
+    def _issue(self, k: int) -> None:
+        from matcha.models.components import _ops as OPS
+
+        OPS.flush_deferred_grad_sums()  # the bucket's weight gradients may still be queued sums
+        s, e = self.buckets[k]
+        lo, hi = self.spans[k]
+        grads = [self.grad_refs[i].reshape(-1) for i in range(s, e)]
+        n = self.offsets[e] - lo if e < len(self.params) else self.n_grad - lo
+        if grads:
+            torch.cat(grads, out=self.flat[lo:lo + n])
+        if k == len(self.buckets) - 1:
+            self.flat[self.n_grad:].copy_(self._pending_scalars)
+        if self.overlap:
+            cur = torch.cuda.current_stream(self.device) if self.stream is not None else None
+            if cur is not None:
+                self.stream.wait_stream(cur)
+                with torch.cuda.stream(self.stream):
+                    self.comm.all_reduce_mean_(self.flat[lo:hi])
+            else:
+                self.comm.all_reduce_mean_(self.flat[lo:hi])
+
+    def finish(self) -> None:
+        """After the armed backward: every bucket issued, the current stream joined with the reductions
+        (overlap) or the whole buffer reduced now (no overlap), parameters' .grad -> flat views."""
+        if not self.armed:
+            return
+        self.armed = False
+        if self._issued != len(self.buckets):
+            missing = [i for i, g in enumerate(self.grad_refs) if g is None]
+            raise RuntimeError(f"GradBucketReducer: {len(missing)} parameters got no gradient this step "
+                               f"(first: index {missing[:3]}); the bucket layout assumes a fixed set")
+        if self.overlap:
+            if self.stream is not None:
+                torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        self.attach_views()
+
+    def reduce_now(self) -> None:
+        """No-overlap mode: one all-reduce of the packed buffer (eager, e.g. after a graph replay)."""
+        self.comm.all_reduce_mean_(self.flat)
+
+    def attach_views(self) -> None:
+        for p, v in zip(self.params, self.views):
+            p.grad = v
+
+    def scalars(self) -> torch.Tensor:
+        return self.flat[self.n_grad:]
+
+    def remove(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+class ArrivalRecorder:
+    """Records the order in which backward finishes the parameters' gradients (post-accumulate hooks)."""
+
+    def __init__(self, params):
+        self.order = []
+        self._seen = set()
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on) for p in params]
+
+    def _on(self, p):
+        if id(p) not in self._seen:
+            self._seen.add(id(p))
+            self.order.append(p)
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

@@ -438,6 +438,16 @@ def deferred_grad_sums(enabled: bool = True):
             _DEFER["keep"].clear()  # stream-ordered frees, after the flush launch
 
 
+def flush_deferred_grad_sums() -> None:
+    """Runs the queued parameter-gradient sums now (inside deferred_grad_sums(); no-op outside): the
+    data-parallel reducer calls it before packing a bucket, so the deferral still batches the sums of
+    each bucket into one launch."""
+    if not _DEFER["on"]:
+        return
+    N.check(N.lib().mtts_flush_reductions(torch.cuda.current_stream().cuda_stream), "mtts_flush_reductions")
+    _DEFER["keep"].clear()  # stream-ordered frees, after the flush launch
+
+
 def _grad_sums(backward):
     """Backward decorator: a Function with non-leaf weights sums its partials at once."""
     @functools.wraps(backward)

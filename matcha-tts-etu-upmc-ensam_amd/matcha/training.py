@@ -25,6 +25,7 @@ with element 0 = max, mels ~ N(0, 1) zeroed past the length.
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import ctypes
 import math
@@ -156,12 +157,15 @@ N.register("mtts_clip_adamw", ctypes.c_int,
 class TrainConfig:
     accumulate_grad_batches: int = 1
     gradient_clip_val: float = 1.0
-    bucket_mb: float = 25.0
+    bucket_mb: float = 25.0  # DDP buckets (eager) and the graph step's all-reduce buckets
     precision: str = "32-true"  # "32-true" (reference) or "bf16-mixed"
     graph: bool = False
     lr: float = 1e-4
     eta_min: float = 1e-6
     t_max_epochs: int = 1000
+    graph_cache: int = 4  # captured steps kept per input-shape key (LRU); bucketed padding keeps keys few
+    dp: str = "auto"  # N>1 exchange: "ddp" (eager only), "buckets" (GradBucketReducer), "auto"
+    comm: str = "auto"  # bucket reducer transport: "rccl" (capturable, libmtts_hip), "torch", "auto"
 
 
 class Trainer:
@@ -169,6 +173,9 @@ class Trainer:
     # side stream (11.25 vs 11.01 ms): the ~100 cross-stream edges cost more than the overlap returns
     side_stream_wgrad = os.environ.get("MTTS_SIDE_WGRAD", "0") == "1"
     defer_grad_sums = os.environ.get("MTTS_DEFER_GRAD_SUMS", "1") != "0"
+    # MTTS_FORCE_DP=1: run the data-parallel exchange even at world size 1 (rehearses the bucketed
+    # RCCL path on a one-GPU box; the all-reduce of one rank is a copy)
+    force_dp = os.environ.get("MTTS_FORCE_DP", "0") == "1"
 
     def __init__(self, model: MatchaTTS, cfg: TrainConfig = TrainConfig()):
         self.cfg = cfg
@@ -179,11 +186,19 @@ class Trainer:
         self.global_step = 0
         self.epoch = 0
         self.last_losses = None
+        self.dp = self.world > 1 or (self.force_dp and dist.is_available() and dist.is_initialized())
+        mode = cfg.dp if cfg.dp != "auto" else ("buckets" if cfg.graph else "ddp")
+        if cfg.graph and mode == "ddp":
+            raise ValueError("the graph step exchanges gradients with the bucket reducer (dp='buckets')")
+        self.dp_mode = mode if self.dp else None
+        self.reducer = None
+        self._recorder = None
+        self._arm = None  # (overlap,) while the reducer is to be armed in the next backward
+        self._graphs = collections.OrderedDict()
+        if self.dp and self.world > 1:  # identical initial weights on every rank (what DDP's broadcast does)
+            for p in model.state_dict().values():
+                dist.broadcast(p, 0)
         if cfg.graph:
-            if self.world > 1:  # identical initial weights on every rank (what DDP's broadcast does)
-                for p in model.state_dict().values():
-                    dist.broadcast(p, 0)
-            self.flat = None  # N>1: packed gradients for the all-reduce (sized at capture)
             for p in self.params:
                 p.grad = None
             self.lr = torch.tensor(cfg.lr, device=self.dev, dtype=torch.float64)  # torch keeps lr a double
@@ -192,11 +207,9 @@ class Trainer:
             # 16-byte aligned; the moments are flat arrays of the same layout
             self.optimizer = _FlatClipAdamW(self.params, self.lr, cfg.gradient_clip_val)
             self.scheduler = None
-            self._g_fb = self._g_opt = None
-            self._static = None
             self.wrapped = model
         else:
-            if self.world > 1:
+            if self.dp_mode == "ddp":
                 self.wrapped = torch.nn.parallel.DistributedDataParallel(
                     model, device_ids=[self.dev.index] if self.dev.type == "cuda" else None,
                     bucket_cap_mb=cfg.bucket_mb, gradient_as_bucket_view=True, broadcast_buffers=False)
@@ -221,8 +234,8 @@ class Trainer:
         side = self.cfg.graph and fresh and self.side_stream_wgrad
         # the parameter-gradient partial sums of the whole backward in one batched launch
         # (components/_ops.py deferred_grad_sums): also needs fresh gradients, and no DDP hook
-        # reading them during the backward
-        defer = fresh and self.defer_grad_sums and not side and (self.cfg.graph or self.world == 1)
+        # reading them during the backward (the bucket reducer flushes the queue per bucket)
+        defer = fresh and self.defer_grad_sums and not side and (self.cfg.graph or self.dp_mode != "ddp")
         with OPS.deferred_grad_sums(defer), OPS.side_stream_wgrad(side):
             return self._fwd_bwd_body(batches, sync_ctx)
 
@@ -236,9 +249,13 @@ class Trainer:
                     dur, prior, diff, _ = self.wrapped(x=batch["x"], x_lengths=batch["x_lengths"],
                                                        y=batch["y"], y_lengths=batch["y_lengths"])
                     total = dur + prior + diff
+                vals = torch.stack([dur.detach(), torch.as_tensor(prior).detach(), diff.detach(), total.detach()]).float()
+                logged = vals if logged is None else logged + vals
+                if i == n - 1 and self._arm is not None:
+                    # the last micro-batch's backward exchanges the accumulated gradients (and the logged
+                    # means) bucket by bucket as backward produces them
+                    self.reducer.arm(logged / n, overlap=self._arm)
                 (total / n).backward()
-            vals = torch.stack([dur.detach(), torch.as_tensor(prior).detach(), diff.detach(), total.detach()]).float()
-            logged = vals if logged is None else logged + vals
         return logged / n
 
     def _clip_and_update(self):
@@ -249,35 +266,88 @@ class Trainer:
             torch.nn.utils.clip_grad_norm_(self.params, self.cfg.gradient_clip_val, foreach=True)
         self.optimizer.step()
 
+    def _ensure_reducer(self, batches, run_step):
+        """First DP step: one pass with an arrival recorder fixes the bucket layout (backward order)."""
+        if self.reducer is not None:
+            return None
+        from matcha import dp as DP
+
+        rec = DP.ArrivalRecorder(self.params)
+        try:
+            logged = run_step()
+        finally:
+            rec.remove()
+        comm = DP.make_comm(self.dev, self.cfg.comm)
+        self.reducer = DP.GradBucketReducer(rec.order, comm, self.cfg.bucket_mb, self.dev)
+        return logged
+
     # ------------------------------------------------------------------------------------ eager
     def _eager_step(self, batches):
         n = len(batches)
-        ddp = self.world > 1
+        ddp = self.dp_mode == "ddp"
 
         def sync_ctx(i):
             return self.wrapped.no_sync() if (ddp and i < n - 1) else contextlib.nullcontext()
 
-        logged = self._fwd_bwd(batches, sync_ctx)
-        if ddp:  # the step's logged scalars in one collective (sync_dist=True)
-            dist.all_reduce(logged)
-            logged = logged / self.world
+        if self.dp_mode == "buckets" and self.reducer is None:
+            logged = self._ensure_reducer(batches, lambda: self._fwd_bwd(batches))
+            # this first step: pack what backward produced and reduce it in one call
+            for i, p in enumerate(self.reducer.params):
+                self.reducer.views[i].copy_(p.grad)
+            self.reducer.flat[self.reducer.n_grad:].copy_(logged)
+            self.reducer.reduce_now()
+            self.reducer.attach_views()
+            logged = self.reducer.scalars().clone()
+        elif self.dp_mode == "buckets":
+            self._arm = True
+            try:
+                self._fwd_bwd(batches)
+            finally:
+                self._arm = None
+            self.reducer.finish()
+            logged = self.reducer.scalars().clone()
+        else:
+            logged = self._fwd_bwd(batches, sync_ctx)
+            if ddp:  # the step's logged scalars in one collective (sync_dist=True)
+                dist.all_reduce(logged)
+                logged = logged / self.world
         self._clip_and_update()
         self.optimizer.zero_grad(set_to_none=True)
         return logged
 
     # ------------------------------------------------------------------------------------ graph
     def _graph_capture(self, batches):
-        self._static = [{k: v.clone() for k, v in b.items()} for b in batches]
+        """Captures the step for this input-shape key.  N=1: graph 1 = fwd+bwd (fresh gradients),
+        graph 2 = clip + AdamW on them.  DP with a capturable communicator: ONE graph -- fwd, bwd with
+        each bucket's RCCL all-reduce forked off as backward completes it, join, clip + AdamW on the
+        reduced flat buffer.  DP with torch.distributed: graph 1 packs the buckets, the host reduces
+        the flat buffer, graph 2 steps."""
+        e = {"static": [{k: v.clone() for k, v in b.items()} for b in batches]}
+        static = e["static"]
         # warm-up (allocator pools, lazy library loads, optimizer state) must not leave updates behind
         saved = [p.detach().clone() for p in self.params]
         saved_state = self.optimizer.state_snapshot()
         side = torch.cuda.Stream(self.dev)
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):
-            for _ in range(2):
+            for it in range(2):
                 for p in self.params:
                     p.grad = None
-                self._fwd_bwd(self._static)
+                if self.dp and self.reducer is None:
+                    self._ensure_reducer(batches, lambda: self._fwd_bwd(static))
+                    for i, p in enumerate(self.reducer.params):
+                        self.reducer.views[i].copy_(p.grad)
+                    self.reducer.reduce_now()
+                    self.reducer.attach_views()
+                elif self.dp:
+                    self._arm = True
+                    try:
+                        self._fwd_bwd(static)
+                    finally:
+                        self._arm = None
+                    self.reducer.finish()
+                else:
+                    self._fwd_bwd(static)
                 self._clip_and_update()
         torch.cuda.current_stream(self.dev).wait_stream(side)
         gparams = [p for p in self.params if p.grad is not None]  # parameters the step differentiates
@@ -286,45 +356,59 @@ class Trainer:
                 p.copy_(s_)
             self.optimizer.state_restore(saved_state)  # moments / step back to their pre-warm-up values
 
-        if self.world > 1:
-            self.flat = torch.zeros(sum(p.numel() for p in gparams), device=self.dev, dtype=torch.float32)
-        self._g_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_fb):
+        overlap = self.dp and self.reducer.comm.capturable
+        if self.dp:
+            self.reducer.attach_views()
+            self.optimizer.bind_grads()  # the table points at the flat buffer's views (fixed addresses)
+        e["g_fb"] = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(e["g_fb"]):
             for p in self.params:
                 p.grad = None  # autograd hands over each fresh gradient: no accumulate kernels
-            self._logged = self._fwd_bwd(self._static)
-            if self.world > 1:
-                torch.cat([p.grad.reshape(-1) for p in gparams], out=self.flat)
-        self._fb_grads = [p.grad for p in gparams]  # graph-pool outputs, kept alive with the graph
-        if self.world > 1:
-            off = 0
-            for p in gparams:  # the optimizer graph reads the all-reduced flat buffer
-                p.grad = self.flat[off:off + p.numel()].view_as(p)
-                off += p.numel()
-        # the optimizer graph: its gradient table points at the (fixed) graph-pool gradients
-        self.optimizer.bind_grads()
-        self._g_opt = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_opt, pool=self._g_fb.pool()):
-            self._clip_and_update()
+            if self.dp:
+                self._arm = overlap
+                try:
+                    e["logged"] = self._fwd_bwd(static)
+                finally:
+                    self._arm = None
+                self.reducer.finish()  # joins the forked all-reduces; .grad -> flat views
+                if overlap:
+                    self._clip_and_update()
+            else:
+                e["logged"] = self._fwd_bwd(static)
+        e["fb_grads"] = [p.grad for p in gparams]  # graph-pool outputs, kept alive with the graph
+        e["g_opt"] = None
+        if not overlap:
+            if not self.dp:  # the optimizer graph's table points at the (fixed) graph-pool gradients
+                self.optimizer.bind_grads()
+            e["g_opt"] = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(e["g_opt"], pool=e["g_fb"].pool()):
+                self._clip_and_update()
+        e["opt_keep"] = (self.optimizer._table, self.optimizer._ws)  # the captured kernels read these
+        e["overlap"] = overlap
+        return e
 
     def _graph_step(self, batches):
-        if self._g_fb is None or len(batches) != len(self._static) or any(
-                b[k].shape != s[k].shape for b, s in zip(batches, self._static) for k in s):
-            self._graph_capture(batches)
-        for b, s in zip(batches, self._static):
+        key = tuple(tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(b.items())) for b in batches)
+        e = self._graphs.get(key)
+        if e is None:
+            e = self._graph_capture(batches)
+            self._graphs[key] = e
+            while len(self._graphs) > max(1, self.cfg.graph_cache):
+                self._graphs.popitem(last=False)  # least recently used shape
+        else:
+            self._graphs.move_to_end(key)
+        for b, s in zip(batches, e["static"]):
             for k, v in s.items():
                 if b[k] is not v:
                     v.copy_(b[k], non_blocking=True)
-        self._g_fb.replay()
-        logged = self._logged
-        if self.world > 1:
-            dist.all_reduce(self.flat)  # one RCCL all-reduce of every gradient
-            self.flat.div_(self.world)
-            logged = logged.clone()
-            dist.all_reduce(logged)
-            logged = logged / self.world
-        self._g_opt.replay()
-        return logged
+        e["g_fb"].replay()
+        if not self.dp:
+            e["g_opt"].replay()
+            return e["logged"]
+        if not e["overlap"]:  # torch.distributed transport: one eager all-reduce of the packed buffer
+            self.reducer.reduce_now()
+            e["g_opt"].replay()
+        return self.reducer.scalars()
 
     # ------------------------------------------------------------------------------------ api
     def step(self, batches: list[dict]) -> torch.Tensor:

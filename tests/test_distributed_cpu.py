@@ -45,62 +45,85 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+def _batches(rank, accumulate):
+    from matcha.training import synthetic_batch
+
+    return [synthetic_batch(4, 12, 40, seed=100 * (m + 1) + rank, device="cpu") for m in range(accumulate)]
+
+
+def _worker(rank, world, port, q, dp, accumulate, steps):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.manual_seed(rank)  # different init per rank: DDP must broadcast rank 0's weights
-    from matcha.training import TrainConfig, Trainer, synthetic_batch
+    torch.manual_seed(rank)  # different init per rank: the trainer must broadcast rank 0's weights
+    from matcha.training import TrainConfig, Trainer
 
     model = TinyTTS()
-    tr = Trainer(model, TrainConfig(precision="32-true", graph=False))
-    b = synthetic_batch(4, 12, 40, seed=100 + rank, device="cpu")
-    logged = tr.step([b])
+    # bucket_mb tiny: TinyTTS's parameters fall into two buckets
+    tr = Trainer(model, TrainConfig(precision="32-true", graph=False, dp=dp, accumulate_grad_batches=accumulate,
+                                    bucket_mb=0.001))
+    logs = []
+    for _ in range(steps):
+        logs.append(tr.step(_batches(rank, accumulate)).detach().clone().numpy())
+    nb = len(tr.reducer.buckets) if tr.reducer is not None else 0
     state = {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}  # by value, not fd-shared
-    q.put((rank, state, logged.numpy().copy()))
+    q.put((rank, state, logs, nb))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _reference_update():
-    """One process: rank 0's init, mean of the two shards' gradients, one clip + AdamW step."""
-    from matcha.training import synthetic_batch
-
+def _reference_update(accumulate, steps):
+    """One process: rank 0's init; per step the mean over ranks of each rank's accumulated gradient
+    (sum over micro-batches of grad(loss / accumulate)), clip_grad_norm_(1.0), AdamW."""
     torch.manual_seed(0)
     model = TinyTTS()
-    grads, losses = [], []
-    for r in range(2):
-        model.zero_grad(set_to_none=True)
-        b = synthetic_batch(4, 12, 40, seed=100 + r, device="cpu")
-        d, p, f, _ = model(b["x"], b["x_lengths"], b["y"], b["y_lengths"])
-        (d + p + f).backward()
-        grads.append([q.grad.clone() for q in model.parameters()])
-        losses.append(torch.stack([d, p, f, d + p + f]).detach())
-    for q, g0, g1 in zip(model.parameters(), *grads):
-        q.grad = (g0 + g1) / 2
-    torch.nn.utils.clip_grad_norm_(list(model.parameters()), 1.0)
     opt = model.configure_optimizers()["optimizer"]
-    opt.step()
-    return {k: v.detach().clone() for k, v in model.state_dict().items()}, (losses[0] + losses[1]) / 2
+    logs = []
+    for _ in range(steps):
+        grads, losses = [], []
+        for r in range(2):
+            model.zero_grad(set_to_none=True)
+            lr_ = 0
+            for b in _batches(r, accumulate):
+                d, p, f, _ = model(b["x"], b["x_lengths"], b["y"], b["y_lengths"])
+                ((d + p + f) / accumulate).backward()
+                lr_ = lr_ + torch.stack([d, p, f, d + p + f]).detach()
+            grads.append([q.grad.clone() for q in model.parameters()])
+            losses.append(lr_ / accumulate)
+        for q, g0, g1 in zip(model.parameters(), *grads):
+            q.grad = (g0 + g1) / 2
+        torch.nn.utils.clip_grad_norm_(list(model.parameters()), 1.0)
+        opt.step()
+        logs.append((losses[0] + losses[1]) / 2)
+    return {k: v.detach().clone() for k, v in model.state_dict().items()}, logs
 
 
 @pytest.mark.timeout(180)
-def test_data_parallel_two_ranks_gloo():
+@pytest.mark.parametrize("dp,accumulate,steps", [("ddp", 1, 1), ("buckets", 1, 3), ("buckets", 2, 2)])
+def test_data_parallel_two_ranks_gloo(dp, accumulate, steps):
+    """ddp: torch DDP (the eager default).  buckets: matcha.dp.GradBucketReducer -- the flat, bucketed
+    exchange the captured graph step uses (here eager over gloo): bucket layout from the recorded
+    backward order, per-bucket packing from post-accumulate hooks, the logged means riding in the last
+    bucket, .grad re-pointed at the flat buffer's views for the optimizer; step 1 records and reduces
+    in one call, later steps issue each bucket as backward completes it."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, dp, accumulate, steps)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
     for _ in range(2):
-        rank, state, logged = q.get(timeout=150)
-        res[rank] = ({k: torch.from_numpy(v) for k, v in state.items()}, torch.from_numpy(logged))
+        rank, state, logs, nb = q.get(timeout=150)
+        res[rank] = ({k: torch.from_numpy(v) for k, v in state.items()}, [torch.from_numpy(v) for v in logs], nb)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    ref_state, ref_logged = _reference_update()
+    if dp == "buckets":
+        assert res[0][2] >= 2  # several buckets actually exercised
+    ref_state, ref_logs = _reference_update(accumulate, steps)
     for k in ref_state:
         torch.testing.assert_close(res[0][0][k], res[1][0][k], rtol=0, atol=0)  # replicas identical
         torch.testing.assert_close(res[0][0][k], ref_state[k], rtol=1e-5, atol=1e-7)
-    torch.testing.assert_close(res[0][1], ref_logged, rtol=1e-5, atol=1e-7)
-    torch.testing.assert_close(res[1][1], ref_logged, rtol=1e-5, atol=1e-7)
+    for r in (0, 1):
+        for got, want in zip(res[r][1], ref_logs):
+            torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-7)
