@@ -313,8 +313,8 @@ int mtts_time_embedding(const float *t, int32_t B, int32_t dim, float scale, flo
  * are clamped, where torch raises a device assert); weight [V,C], out [rows,C] fp32. */
 int mtts_embedding_fwd(const int64_t *ids, const float *weight, int64_t rows, int32_t V, int32_t C, float scale,
                        float *out, void *hip_stream);
-/* dweight[v,:] = sum_{r: ids[r]==v, ascending r} dout[r,:] * scale (overwrites; deterministic, unlike torch's
- * atomic embedding backward); C <= 1024. */
+/* dweight[v,:] = sum over rows r with ids[r]==v of dout[r,:] * scale in a fixed order (overwrites; deterministic,
+ * unlike torch's atomic embedding backward). */
 int mtts_embedding_bwd(const int64_t *ids, const float *dout, int64_t rows, int32_t V, int32_t C, float scale,
                        float *dweight, void *hip_stream);
 
