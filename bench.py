@@ -223,10 +223,12 @@ def main():
     from matcha.models.components import _ops as OPS
 
     for rep in range(2):
-        OPS.LAUNCH_LOG = []
+        OPS.LAUNCH_LOG, OPS.WGRAD_LOG, OPS.ATTN_LOG = [], [], []
         trainer._fwd_bwd([batch])
         torch.cuda.synchronize()
     gemm_log, OPS.LAUNCH_LOG = OPS.LAUNCH_LOG, None
+    wgrad_log, OPS.WGRAD_LOG = OPS.WGRAD_LOG, None
+    attn_log, OPS.ATTN_LOG = OPS.ATTN_LOG, None
     model.zero_grad(set_to_none=False)
     gemm_ms = [r[0].elapsed_time(r[1]) for r in gemm_log]
     gemm_flops = sum(r[2] for r in gemm_log)
@@ -325,6 +327,35 @@ def main():
         gemm_roofline = {"bound": "mfma", "achieved": round(gemm_tflops, 1), "peak": gemm_peak,
                          "unit": "TFLOP/s", "frac": round(gemm_tflops / gemm_peak, 4), **common}
 
+    def roofline_of(log, kernel, note):
+        """Roofline line of a launch log: bound from the arithmetic intensity vs the ridge point."""
+        if not log:
+            return None
+        ms = [r[0].elapsed_time(r[1]) for r in log]
+        t = sum(ms) * 1e-3
+        fl, by = sum(r[2] for r in log), sum(r[4] for r in log)
+        tf, gb = fl / t / 1e12, by / t / 1e9
+        ai = fl / max(by, 1)
+        line = {"kernel": kernel, "launches_per_step": len(log), "avg_launch_us": round(sum(ms) / len(ms) * 1e3, 2),
+                "algorithmic_flops_per_launch": round(fl / len(log)), "algorithmic_bytes_per_launch": round(by / len(log)),
+                "arithmetic_intensity_flop_per_byte": round(ai, 1), "ridge_flop_per_byte": round(ridge, 1),
+                "mfma_tflops": round(tf, 1), "hbm_gbs": round(gb, 1), "traffic": None, "note": note}
+        if ai < ridge:
+            return {"bound": "hbm", "achieved": round(gb, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(gb / HBM_PEAK_GBS, 4), **line}
+        return {"bound": "mfma", "achieved": round(tf, 1), "peak": gemm_peak, "unit": "TFLOP/s",
+                "frac": round(tf / gemm_peak, 4), **line}
+
+    roofline_wgrad = roofline_of(
+        wgrad_log, "conv_wgrad_kernel + wgrad slab reduce (weight-gradient GEMMs, decoder + encoder)",
+        "HIP events around each mtts_conv_wgrad call (one eager fwd+bwd of the bench batch); 2*M*N*K FLOP; "
+        "bytes = dY + unique A rows + dW; each call includes its fp32 partial-slab reduce (this eager pass does "
+        "not defer the sums)")
+    roofline_attn = roofline_of(
+        attn_log, "attn_fwd_kernel / attn_bwd_dq_kernel + attn_bwd_dkv_kernel (decoder + encoder attention)",
+        "HIP events around each mtts_attention_fwd / _bwd call; FLOP = 4 B H T^2 D fwd, 8 B H T^2 D bwd "
+        "(standard flash-attention accounting, recomputation not counted)")
+
     if rank == 0:
         rec = {
             "metric": "training utterances/sec (whole node) + maximum_path Mcells/sec, LJSpeech batch=32",
@@ -350,6 +381,8 @@ def main():
                              "fused_note": "what the step runs: log-prior lattice from mu_x / y + DP + durations "
                                            "+ frame rows (mtts_prior_maximum_path)"},
             "roofline": gemm_roofline,
+            "roofline_wgrad": roofline_wgrad,
+            "roofline_attn": roofline_attn,
             "roofline_mas": {"kernel": "mas_dp_kernel + mas_expand_kernel (maximum_path)", "bound": "hbm",
                              "achieved": round(mas_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(mas_gbs / HBM_PEAK_GBS, 4), "traffic": None,

@@ -83,6 +83,8 @@ typedef struct mtts_conv_gemm_args {
                                         precision only, LDS-DMA schedules) */
 #define MTTS_GEMM_F_C_BF16 0x4       /* C (not C_pre) is written as bf16 (ldc in elements) */
 #define MTTS_GEMM_F_FAST_ACT 0x8     /* GELU / GELU' with a 5e-7 (fp32-evaluated) erf approximation (bf16-mixed) */
+#define MTTS_GEMM_F_PRE_BF16 0x10    /* C_pre is written and aux read as bf16 (bf16-mixed: the saved pre-activation,
+                                        half the bytes; ldc / ldaux in elements, % 4 == 0 for the vector epilogue) */
 
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
 /* Same, with an explicit schedule: 0..17 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;

@@ -806,6 +806,8 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     MTTS_CHECK_ARG((p.act != MTTS_ACT_DGELU && p.act != MTTS_ACT_DRELU) || p.aux,
                    "conv_gemm: MTTS_ACT_DGELU / MTTS_ACT_DRELU need aux");
     MTTS_CHECK_ARG(p.dropout_p <= 0.f || (p.seed && p.dropout_p < 1.f), "conv_gemm: dropout needs a seed pointer");
+    MTTS_CHECK_ARG(!(p.flags & MTTS_GEMM_F_PRE_BF16) || precision == MTTS_PREC_BF16,
+                   "conv_gemm: a bf16 pre-activation needs bf16 precision");
     const bool glds_id = cfg >= MTTS_GEMM_GLDS && cfg < MTTS_GEMM_GLDS + mtts::conv_gemm_glds_num_cfgs();
     MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || cfg == MTTS_GEMM_PANEL || glds_id, "conv_gemm: bad tile config");
     MTTS_CHECK_ARG(splits >= 0, "conv_gemm: bad split count");
@@ -815,6 +817,8 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     const bool bf16 = precision == MTTS_PREC_BF16;
     if (cfg == MTTS_GEMM_PANEL) {
         if (!bf16) return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: panel schedule is bf16 only");
+        if (p.flags & (MTTS_GEMM_F_PRE_BF16 | MTTS_GEMM_F_C_BF16))
+            return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: panel schedule writes fp32 only");
         if (mtts::conv_gemm_panel_launch(p, st) == 0) return mtts::check_launch("conv_gemm_panel_kernel");
         return mtts::fail(MTTS_ERR_SHAPE, "conv_gemm: panel schedule does not fit");
     }

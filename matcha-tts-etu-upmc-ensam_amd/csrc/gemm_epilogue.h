@@ -62,8 +62,17 @@ __device__ __forceinline__ void gemm_epilogue(const mtts_conv_gemm_args &p, f32x
                 if (crows[v] < 0) continue;
                 const size_t crow = (size_t)crows[v];
                 float val = acc[i][j][v] + bn;
-                if (p.C_pre) p.C_pre[crow * p.ldc + n] = val;
-                if (p.act) val = epi_act(p.act, val, p.aux + crow * p.ldaux + n, p.flags & MTTS_GEMM_F_FAST_ACT);
+                const bool pre16 = p.flags & MTTS_GEMM_F_PRE_BF16;
+                if (p.C_pre) {
+                    if (pre16) reinterpret_cast<__bf16 *>(p.C_pre)[crow * p.ldc + n] = (__bf16)val;
+                    else p.C_pre[crow * p.ldc + n] = val;
+                }
+                if (p.act) {
+                    float a = 0.f;
+                    if (p.aux) a = pre16 ? (float)reinterpret_cast<const __bf16 *>(p.aux)[crow * p.ldaux + n]
+                                         : p.aux[crow * p.ldaux + n];
+                    val = epi_act(p.act, val, &a, p.flags & MTTS_GEMM_F_FAST_ACT);
+                }
                 if (p.dropout_p > 0.f)
                     val = dropout_keep(s0, s1, (uint32_t)crow, (uint32_t)n, p.dropout_p)
                               ? val * (1.0f / (1.0f - p.dropout_p))
@@ -82,12 +91,31 @@ __device__ __forceinline__ void gemm_epilogue(const mtts_conv_gemm_args &p, f32x
 // Everything after the bias for 4 consecutive columns n..n+3 of output row crow (float4 I/O).
 __device__ __forceinline__ void epilogue_row4(const mtts_conv_gemm_args &p, int crow, int n, float (&e)[4],
                                               uint32_t s0, uint32_t s1, float keep_scale) {
+    typedef float f32x2_ __attribute__((ext_vector_type(2)));
+    typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
     const size_t off = (size_t)crow * p.ldc + n;
-    if (p.C_pre) *reinterpret_cast<float4 *>(p.C_pre + off) = make_float4(e[0], e[1], e[2], e[3]);
+    const bool pre16 = p.flags & MTTS_GEMM_F_PRE_BF16;
+    if (p.C_pre) {
+        if (pre16) {
+            const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_){e[0], e[1]}, bf16x2_));
+            const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_){e[2], e[3]}, bf16x2_));
+            *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(p.C_pre) + off) = make_uint2(lo, hi);
+        } else {
+            *reinterpret_cast<float4 *>(p.C_pre + off) = make_float4(e[0], e[1], e[2], e[3]);
+        }
+    }
     if (p.act) {
         float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (p.act == MTTS_ACT_DGELU || p.act == MTTS_ACT_DRELU)
-            a = *reinterpret_cast<const float4 *>(p.aux + (size_t)crow * p.ldaux + n);
+        if (p.act == MTTS_ACT_DGELU || p.act == MTTS_ACT_DRELU) {
+            const size_t ao = (size_t)crow * p.ldaux + n;
+            if (pre16) {  // bf16 -> fp32 is exact: the bits move to the high half
+                const uint2 h = *reinterpret_cast<const uint2 *>(reinterpret_cast<const uint16_t *>(p.aux) + ao);
+                a = make_float4(__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xffff0000u),
+                                __uint_as_float(h.y << 16), __uint_as_float(h.y & 0xffff0000u));
+            } else {
+                a = *reinterpret_cast<const float4 *>(p.aux + ao);
+            }
+        }
         const float av[4] = {a.x, a.y, a.z, a.w};
         const bool fast = p.flags & MTTS_GEMM_F_FAST_ACT;
 #pragma unroll
@@ -108,8 +136,6 @@ __device__ __forceinline__ void epilogue_row4(const mtts_conv_gemm_args &p, int 
         for (int q = 0; q < 4; ++q) e[q] *= cs;
     }
     if (p.flags & MTTS_GEMM_F_C_BF16) {
-        typedef float f32x2_ __attribute__((ext_vector_type(2)));
-        typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
         const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_){e[0], e[1]}, bf16x2_));
         const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_){e[2], e[3]}, bf16x2_));
         *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(p.C) + off) = make_uint2(lo, hi);
@@ -151,6 +177,7 @@ __device__ __forceinline__ void gemm_store_partial(const mtts_conv_gemm_args &p,
 // other use of `stage` (a workgroup barrier after its last LDS read).
 __host__ __device__ inline bool gemm_epilogue_vec_ok(const mtts_conv_gemm_args &p) {
     auto al = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
+    // (a bf16 C / C_pre / aux row chunk of 4 elements is 8 bytes: 16-byte bases and ld % 4 keep it aligned)
     return p.N % 4 == 0 && p.ldc % 4 == 0 && al(p.C) && al(p.C_pre) && al(p.bias) && (!p.residual || (p.ldr % 4 == 0 && al(p.residual))) &&
            (!p.aux || (p.ldaux % 4 == 0 && al(p.aux)));
 }

@@ -52,6 +52,7 @@ GEMM_F_BINARY_SCALE = 0x1  # include/mtts_decoder.h MTTS_GEMM_F_BINARY_SCALE
 GEMM_F_A_BF16 = 0x2  # MTTS_GEMM_F_A_BF16: A operand stored bf16 (bf16-mixed activations)
 GEMM_F_C_BF16 = 0x4  # MTTS_GEMM_F_C_BF16: output stored bf16
 GEMM_F_FAST_ACT = 0x8  # MTTS_GEMM_F_FAST_ACT: 1.5e-7-accurate erf in GELU epilogues (bf16-mixed only)
+GEMM_F_PRE_BF16 = 0x10  # MTTS_GEMM_F_PRE_BF16: C_pre written / aux read as bf16
 _FAST_ACT = os.environ.get("MTTS_EXACT_GELU") != "1"
 GEMM_GLDS = 32  # MTTS_GEMM_GLDS: first LDS-DMA schedule id
 
@@ -318,6 +319,18 @@ def packed(spec: PackSpec, prec: int) -> tuple[torch.Tensor, int]:
 # launch stream.  Algorithmic bytes: the unique input rows once (nb*Ti*cin*4), the packed weights,
 # the output, and the residual / aux / pre-activation tensors the epilogue touches.
 LAUNCH_LOG: list | None = None
+# The same for the weight-gradient GEMMs (mtts_conv_wgrad: partial slabs, and their reduction when it
+# runs inside the call) and the attention kernels (mtts_attention_fwd / _bwd): lists of
+# (start_event, end_event, algorithmic_flops, precision, algorithmic_bytes, kind).
+WGRAD_LOG: list | None = None
+ATTN_LOG: list | None = None
+
+
+def _events(dev):
+    st = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    return st, e0, e1
 
 
 def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_stride=1, out_off=0, *, prec,
@@ -343,7 +356,10 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     args.flags = ((GEMM_F_BINARY_SCALE if (binary_scale and a_scale is not None) else 0)
                   | (GEMM_F_A_BF16 if A.dtype == torch.bfloat16 else 0)
                   | (GEMM_F_C_BF16 if C.dtype == torch.bfloat16 else 0)
-                  | (GEMM_F_FAST_ACT if (prec == PREC_BF16 and _FAST_ACT) else 0))
+                  | (GEMM_F_FAST_ACT if (prec == PREC_BF16 and _FAST_ACT) else 0)
+                  | (GEMM_F_PRE_BF16 if any(t is not None and t.dtype == torch.bfloat16 for t in (C_pre, aux)) else 0))
+    if C_pre is not None and aux is not None and C_pre.dtype != aux.dtype:
+        raise ValueError("C_pre and aux must share a dtype")
     log = LAUNCH_LOG
     if log is not None:
         st = torch.cuda.current_stream(C.device)
@@ -358,7 +374,7 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
         e1.record(st)
         M_ = nb * To
         nbytes = nb * Ti * cin * A.element_size() + N_ * Kp * Wp.element_size() + M_ * N_ * C.element_size()
-        nbytes += sum(M_ * N_ * 4 for t in (residual, aux, C_pre) if t is not None)
+        nbytes += sum(M_ * N_ * t.element_size() for t in (residual, aux, C_pre) if t is not None)
         log.append((e0, e1, 2.0 * M_ * N_ * args.K, prec, nbytes,
                     dict(M=M_, N=N_, K=args.K, cin=cin, ntaps=len(offs), in_stride=in_stride, res=residual is not None,
                          act=act, pre=C_pre is not None, drop=dropout_p > 0, cs=c_scale is not None,
@@ -496,9 +512,18 @@ def _wgrad_launch(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, of
     lib = N.lib()
     ws = torch.empty(int(lib.mtts_conv_wgrad_workspace_size(ctypes.byref(args))), dtype=torch.uint8, device=dY.device)
     _keep_partials(ws)
+    log = WGRAD_LOG
+    if log is not None:
+        st, e0, e1 = _events(dY.device)
     rc = lib.mtts_conv_wgrad_tile(ctypes.byref(args), prec, rows_per_step, target_blocks, depth, dw.data_ptr(), strides[0],
                                   strides[1], strides[2], N.ptr(db), 0, ws.data_ptr(), ws.numel(), _stream(dY))
     N.check(rc, "mtts_conv_wgrad")
+    if log is not None:
+        e1.record(st)
+        M_ = nb * To
+        # dY rows read once, the unique A rows once, dW (and db) written once
+        nbytes = M_ * N_ * dY.element_size() + nb * Ti * cin * A.element_size() + N_ * args.K * 4
+        log.append((e0, e1, 2.0 * M_ * N_ * args.K, prec, nbytes, "wgrad"))
 
 
 def _check(*ts):
@@ -721,10 +746,12 @@ class _FeedForwardTM(torch.autograd.Function):
         W2p, K2p = packed(spec_linear((w2,)), prec)
         ctx.w2t = packed(spec_linear((w2,), dgrad=True), prec) if any(ctx.needs_input_grad) else None
         ctx.w1t = packed(spec_linear((w1,), dgrad=True), prec) if ctx.needs_input_grad[0] else None
-        z = torch.empty(M, H, device=x.device, dtype=torch.float32)
         # bf16-mixed: the GELU output is only ever the next GEMM's (and its wgrad's) bf16 MFMA operand,
-        # so it is stored as bf16 -- half the bytes written here and read twice later
+        # so it is stored as bf16 -- half the bytes written here and read twice later; the saved
+        # pre-activation (read once, by GELU' in the backward) too, as autocast would keep it
         h16 = prec == PREC_BF16 and os.environ.get("MTTS_FF_FP32_HIDDEN") != "1"
+        z16 = prec == PREC_BF16 and os.environ.get("MTTS_FF_FP32_PRE") != "1"
+        z = torch.empty(M, H, device=x.device, dtype=torch.bfloat16 if z16 else torch.float32)
         h = torch.empty(M, H, device=x.device, dtype=torch.bfloat16 if h16 else torch.float32)
         seed = _new_seed(x.device) if dropout_p > 0 else None
         _gemm(x2, M, M, 1, 1, [0], K, W1p, K1p, H, h, M, prec=prec, bias=_f32c(b1), act=ACT_GELU, C_pre=z,
@@ -997,7 +1024,15 @@ class _AttentionTM(torch.autograd.Function):
         lse = torch.empty(B, heads, T, device=qkv.device, dtype=torch.float32)
         seed = _new_seed(qkv.device) if dropout_p > 0 else None
         a = _AttentionTM._args(qkv, bias, o, lse, heads, dropout_p, seed)
+        log = ATTN_LOG
+        if log is not None:
+            st, e0, e1 = _events(qkv.device)
         N.check(N.lib().mtts_attention_fwd(ctypes.byref(a), prec, _stream(qkv)), "mtts_attention_fwd")
+        if log is not None:
+            e1.record(st)
+            D = C3 // 3 // heads
+            # two T x T x D products per head; q, k, v read, o and the row statistic written
+            log.append((e0, e1, 4.0 * B * heads * T * T * D, prec, 4 * B * T * C3 // 3 * 4 + B * heads * T * 4, "fwd"))
         ctx.save_for_backward(qkv, bias, o, lse)
         ctx.heads, ctx.prec, ctx.drop = heads, prec, (dropout_p, seed)
         return o
@@ -1017,8 +1052,18 @@ class _AttentionTM(torch.autograd.Function):
         lib = N.lib()
         ws = torch.empty(int(lib.mtts_attention_bwd_workspace_size(B, T, ctx.heads)), dtype=torch.uint8,
                          device=qkv.device)
+        log = ATTN_LOG
+        if log is not None:
+            st, e0, e1 = _events(qkv.device)
         N.check(lib.mtts_attention_bwd(ctypes.byref(a), ctypes.byref(g), ctx.prec, ws.data_ptr(), ws.numel(),
                                        _stream(qkv)), "mtts_attention_bwd")
+        if log is not None:
+            e1.record(st)
+            D = C // ctx.heads
+            # four T x T x D products per head (dV, dP, dQ, dK; the recomputed S not counted); q, k, v, o,
+            # dO, the row statistic read, dq, dk, dv written
+            log.append((e0, e1, 8.0 * B * ctx.heads * T * T * D, ctx.prec,
+                        8 * B * T * C * 4 + B * ctx.heads * T * 4, "bwd"))
         return dqkv, None, None, None
 
 
