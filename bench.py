@@ -107,6 +107,23 @@ def cpu_baseline(B_cpu: int, Tx: int, Ty: int, budget_s: float) -> dict:
     return out
 
 
+def mas_chain_bound(Tx: int, Ty: int, mas_ms: float, clock_ghz: float = 2.1) -> dict:
+    """The DP is a Ty-long dependency chain per utterance (one wave each, utterances in parallel on
+    their own CUs): per column a lane updates its K = ceil(Tx / 64) rows (about 9 dependent VALU
+    instructions per row -- score, compare, select, add, band test, backpointer shift/or) plus one
+    DPP neighbour exchange, each waiting ~8 cycles for its predecessor at one wave per SIMD.  The
+    estimate is that chain's length; measured / estimate near 1 means the kernel runs at its chain
+    bound, not at HBM speed (which the 12 B/cell roofline would ask for)."""
+    K = 1
+    while 64 * K < Tx:
+        K *= 2
+    cyc_per_col = (9 * K + 2) * 8
+    est_ms = Ty * cyc_per_col / (clock_ghz * 1e9) * 1e3
+    return {"columns": Ty, "rows_per_lane": K, "model_cycles_per_column": cyc_per_col,
+            "estimate_ms": round(est_ms, 4), "measured_ns_per_column": round(mas_ms * 1e6 / Ty, 1),
+            "measured_over_estimate": round(mas_ms / est_ms, 2), "clock_ghz_assumed": clock_ghz}
+
+
 def _cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -387,6 +404,7 @@ def main():
                              "achieved": round(mas_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(mas_gbs / HBM_PEAK_GBS, 4), "traffic": None,
                              "algorithmic_bytes_per_launch": 12 * cells,
+                             "chain_bound": mas_chain_bound(Tx, Ty, mas_ms),
                              "note": "12 B/cell (value+mask read, path write); chain-bound: one wave per utterance"},
             "decoder_mfma": {"train_flops_per_step": flops,
                              "achieved_tflops_step": round(flops / (step_ms * 1e-3) / 1e12, 2),

@@ -13,9 +13,9 @@
  *
  * Reference interfaces replaced (paths relative to the reference repository root):
  *   mtts_maximum_path_f32          <- matcha/utils/monotonic_align/__init__.py:40-55  maximum_path(value, mask)
- *   mtts_prior_maximum_path        <- matcha/models/matcha_tts.py:461-478 (log-prior lattice + maximum_path +
+ *   mtts_prior_maximum_path        <- matcha/models/matcha_tts.py:276-288 (log-prior lattice + maximum_path +
  *                                     the duration target), fused
- *   mtts_expand_rows_fwd / _bwd    <- matcha/models/matcha_tts.py:504-505  mu_y = attn^T @ mu_x
+ *   mtts_expand_rows_fwd / _bwd    <- matcha/models/matcha_tts.py:314-315  mu_y = attn^T @ mu_x
  *   mtts_compute_batch_alignments  <- matcha/utils/monotonic_align/core.pyx:101-128   compute_batch_alignments(...)
  *                                     (bound as maximum_path_c, __init__.py:4-8)
  *   mtts_losses_fwd / _bwd         <- flow_matching.py:145-149 (CFM loss) + matcha_tts.py:319-323 (prior loss)
@@ -38,7 +38,7 @@ extern "C" {
 typedef enum mtts_status {
     MTTS_OK = 0,
     MTTS_ERR_INVALID_ARG = -1, /* null pointer, negative size, bad flag */
-    MTTS_ERR_SHAPE = -2,       /* shape outside what the kernels support (e.g. Tx > 512) */
+    MTTS_ERR_SHAPE = -2,       /* shape outside what the kernels support (e.g. Tx > 1024) */
     MTTS_ERR_WORKSPACE = -3,   /* workspace too small */
     MTTS_ERR_HIP = -4,         /* a HIP runtime call failed (launch, attribute) */
     MTTS_ERR_UNSUPPORTED = -5  /* feature not built into this library */
@@ -57,7 +57,7 @@ const char *mtts_last_error(void);
 #define MTTS_MAS_NO_DENSE_PATH 0x2   /* only row_start_out/lengths_out: do not write `path`    */
 
 /* Maximum text length (Tx) the kernels accept. */
-#define MTTS_MAS_MAX_TX 512
+#define MTTS_MAS_MAX_TX 1024
 
 /* Bytes of device workspace mtts_maximum_path_f32 / mtts_compute_batch_alignments need. */
 size_t mtts_maximum_path_workspace_size(int32_t B, int32_t Tx, int32_t Ty);
@@ -96,8 +96,8 @@ int mtts_compute_batch_alignments(int32_t *paths, float *values, const int32_t *
                                   void *hip_stream);
 
 /*
- * Fused alignment of the training forward (matcha_tts.py:461-478):
- *   lattice[b,i,j] = (log N(y[b,:,j]; mu_x[b,:,i], I)) * x_mask[b,i] * y_mask[b,j]   (matcha_tts.py:467-472,
+ * Fused alignment of the training forward (matcha_tts.py:276-288):
+ *   lattice[b,i,j] = (log N(y[b,:,j]; mu_x[b,:,i], I)) * x_mask[b,i] * y_mask[b,j]   (matcha_tts.py:277-282,
  *                    maximum_path's value*mask) with the masks from x_lengths / y_lengths (int64 [B]),
  *   then the DP and backtrack of mtts_maximum_path_f32 on it (t_x = x_lengths, t_y = y_lengths).
  *   mu_x : float32 [B, C, Tx], y : float32 [B, C, Ty] (channel-major, C-contiguous, device memory).
@@ -115,7 +115,7 @@ int mtts_prior_maximum_path(const float *mu_x, const float *y, const int64_t *x_
                             void *workspace, size_t workspace_bytes, void *hip_stream);
 
 /*
- * mu_y = attn^T @ mu_x for a hard alignment (matcha_tts.py:504-505) as a gather, and its backward:
+ * mu_y = attn^T @ mu_x for a hard alignment (matcha_tts.py:314-315) as a gather, and its backward:
  *   fwd: dst[b,c,j] = src[b,c,col_row[b,j]] (0 where col_row < 0); src [B,C,Tx], dst [B,C,Ty] float32.
  *   bwd: dx[b,c,i] = sum over the frames j of row i (row_start / lengths of mtts_maximum_path_f32) of
  *        dy[b,c,j]: 16 strided partial sums (j = start + l + 16k, ascending k) combined by a fixed

@@ -333,7 +333,7 @@ __global__ __launch_bounds__(256) void mas_expand_kernel(const int32_t *__restri
 }
 
 // ------------------------------------------------------------------------------------------------
-// Fused producer: the log-prior lattice of matcha_tts.py:467-472 (MatchaTTS.forward) computed
+// Fused producer: the log-prior lattice of matcha_tts.py:277-282 (MatchaTTS.forward) computed
 // straight from mu_x [B,C,Tx] and y [B,C,Ty] (channel-major, as the encoder / data loader hold them)
 // and multiplied by the attention mask x_mask[i] * y_mask[j] (maximum_path's value*mask,
 // __init__.py:45), written once to HBM for the DP:
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(256) void log_prior_kernel(const float *__restrict_
     }
 }
 
-// Alignment consumers from the row starts (matcha_tts.py:477-478, 504-505): durations
+// Alignment consumers from the row starts (matcha_tts.py:287-288, 504-505): durations
 // dur[b,x] = sum_y attn[b,x,y] (the run length of row x) and col_row[b,y] = the text row of frame y
 // (-1 past t_y), which turns mu_y = attn^T mu_x into a gather.  One block per utterance.
 __global__ __launch_bounds__(256) void mas_runs_kernel(const int32_t *__restrict__ row_start,
@@ -530,7 +530,7 @@ struct WsLayout {
 
 WsLayout ws_layout(int B, int Tx, int Ty) {
     WsLayout w{};
-    w.K = Tx <= 64 ? 1 : Tx <= 128 ? 2 : Tx <= 256 ? 4 : 8;
+    w.K = Tx <= 64 ? 1 : Tx <= 128 ? 2 : Tx <= 256 ? 4 : Tx <= 512 ? 8 : 16;
     w.Txp = kWave * w.K;
     w.nch = (Ty + 31) / 32;
     w.lds_bits = (size_t)w.Txp * w.nch * 4 <= (size_t)kLdsBitsLimit;
@@ -597,14 +597,15 @@ int launch_dp(MasArgs a, int B, const WsLayout &w, bool vec, bool dp_out, hipStr
         case 1: return launch_dp_kc<1, 32>(a, B, vec, w.lds_bits, dp_out, shmem, st);
         case 2: return launch_dp_kc<2, 16>(a, B, vec, w.lds_bits, dp_out, shmem, st);
         case 4: return launch_dp_kc<4, 8>(a, B, vec, w.lds_bits, dp_out, shmem, st);
-        default: return launch_dp_kc<8, 4>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+        case 8: return launch_dp_kc<8, 4>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+        default: return launch_dp_kc<16, 2>(a, B, vec, w.lds_bits, dp_out, shmem, st);
     }
 }
 
 int check_shape(int B, int Tx, int Ty) {
     if (B < 0 || Tx < 1 || Ty < 1) return mtts::fail(MTTS_ERR_INVALID_ARG, "maximum_path: bad shape");
     if (Tx > MTTS_MAS_MAX_TX)
-        return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: Tx > MTTS_MAS_MAX_TX (512) is not supported");
+        return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: Tx > MTTS_MAS_MAX_TX (1024) is not supported");
     if ((int64_t)Tx * Ty * 4 >= (int64_t)1 << 31)
         return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: one utterance's lattice exceeds 2 GiB");
     return MTTS_OK;

@@ -1,6 +1,6 @@
 """Matcha-TTS model (drop-in for matcha/models/matcha_tts.py).
 
-Reference: MatchaTTS :219-325 (simple-params init :294-366, synthesise :368-435, forward :437-515).
+Reference: MatchaTTS matcha_tts.py:29-325 (config init :74-102, simple-params init :104-176, synthesise :178-245, forward :247-325).
 The train-step forward keeps the reference's order and arithmetic; the monotonic alignment runs on
 the GPU (matcha.utils.monotonic_align.maximum_path -> csrc/mas.hip) instead of the reference's
 device->host->device Cython round trip, so the step never synchronises with the host.  The log-prior
@@ -34,13 +34,13 @@ class MatchaTTS(BaseLightningClass):
         self.prior_loss = prior_loss
         self.use_precomputed_durations = use_precomputed_durations
         self.scheduler_config = scheduler
-        if encoder is not None and decoder is not None and cfm is not None:  # :264-292
+        if encoder is not None and decoder is not None and cfm is not None:  # :74-102
             self.n_feats = n_feats
             self.encoder = TextEncoder(encoder.encoder_type, encoder.encoder_params,
                                        encoder.duration_predictor_params, n_vocab)
             self.decoder = CFM(in_channels=2 * encoder.encoder_params.n_feats,
                                out_channel=encoder.encoder_params.n_feats, cfm_params=cfm, decoder_params=decoder)
-        else:  # :294-366
+        else:  # :104-176
             if out_channels is None or hidden_channels is None:
                 raise ValueError("give either (encoder, decoder, cfm) configs or (out_channels, hidden_channels)")
             self.n_feats = out_channels
@@ -79,7 +79,7 @@ class MatchaTTS(BaseLightningClass):
                 "mel_lengths": y_lengths, "rtf": rtf}
 
     def log_prior(self, mu_x, y):
-        """matcha_tts.py:467-472 in fp32: -1/2 sum y^2 + sum mu*y - 1/2 sum mu^2 - n/2 log(2 pi)."""
+        """matcha_tts.py:277-282 in fp32: -1/2 sum y^2 + sum mu*y - 1/2 sum mu^2 - n/2 log(2 pi)."""
         with torch.autocast(device_type=mu_x.device.type, enabled=False):
             mu_x = mu_x.float()
             y = y.float()
@@ -91,7 +91,7 @@ class MatchaTTS(BaseLightningClass):
             return y_square - y_mu_double + mu_square + const
 
     def forward(self, x, x_lengths, y, y_lengths, out_size=None, cond=None, durations=None, *, t=None, z=None):
-        """Returns (dur_loss, prior_loss, diff_loss, attn) -- matcha_tts.py:437-515.  ``t``/``z``
+        """Returns (dur_loss, prior_loss, diff_loss, attn) -- matcha_tts.py:247-325.  ``t``/``z``
         (keyword-only) inject the CFM randomness for parity tests."""
         # the text encoder runs on the same HIP GEMM/attention kernels as the decoder and follows the
         # caller's precision (bf16 MFMA operands inside a bf16 autocast region)
@@ -104,7 +104,7 @@ class MatchaTTS(BaseLightningClass):
             attn = generate_path(durations.squeeze(1), attn_mask.squeeze(1))
             dur = torch.sum(attn, -1)
         else:
-            # :461-478 fused on the GPU: lattice (log_prior) * attn_mask -> maximum_path -> sum(attn, -1),
+            # :276-288 fused on the GPU: lattice (log_prior) * attn_mask -> maximum_path -> sum(attn, -1),
             # with the attention mask taken from the lengths (never materialised)
             with torch.no_grad():
                 attn, dur, col_row, row_start, lens = monotonic_align.prior_maximum_path(mu_x, y, x_lengths,
@@ -112,7 +112,7 @@ class MatchaTTS(BaseLightningClass):
             runs = (col_row, row_start, lens)
         logw_ = torch.log(1e-8 + dur.unsqueeze(1)) * x_mask
         dur_loss = duration_loss(logw, logw_, x_lengths)
-        if out_size is not None:  # :480-502 (host-side random crop, as the reference)
+        if out_size is not None:  # :290-312 (host-side random crop, as the reference)
             max_offset = (y_lengths - out_size).clamp(0)
             offset_ranges = list(zip([0] * max_offset.shape[0], max_offset.cpu().numpy()))
             out_offset = torch.LongTensor([random.choice(range(s, e)) if e > s else 0
@@ -133,7 +133,7 @@ class MatchaTTS(BaseLightningClass):
             mu_y = monotonic_align.expand_rows(mu_x, *runs)
         else:
             mu_y = torch.matmul(attn.squeeze(1).transpose(1, 2), mu_x.transpose(1, 2)).transpose(1, 2)
-        # CFM loss (:506) and prior loss (:508-511) in one fused HIP pass (components/flow_matching.py)
+        # CFM loss (:317) and prior loss (:319-323) in one fused HIP pass (components/flow_matching.py)
         diff_loss, prior_loss, _ = self.decoder.compute_loss_and_prior(y, y_mask, mu_y,
                                                                        mu_y if self.prior_loss else None, t=t, z=z)
         if not self.prior_loss:

@@ -16,6 +16,15 @@ import torch
 from matcha import _native as N
 
 
+def _check_tx(Tx: int) -> None:
+    """The DP keeps one utterance's text rows in one wave (16 rows per lane at most): t_x <= 1024.
+    The reference Cython (core.pyx:14-96) has no cap; LJSpeech tops out near 190 tokens and
+    BASELINE config 5 uses 512, so the limit is a documented shape error, not a silent truncation."""
+    if Tx > N.MTTS_MAS_MAX_TX:
+        raise ValueError(f"maximum_path: text length {Tx} exceeds the GPU kernel's limit of "
+                         f"{N.MTTS_MAS_MAX_TX} rows (MTTS_MAS_MAX_TX, include/mtts.h)")
+
+
 def _workspace(B: int, Tx: int, Ty: int, device) -> torch.Tensor:
     nbytes = int(N.lib().mtts_maximum_path_workspace_size(B, Tx, Ty))
     return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
@@ -44,6 +53,7 @@ def maximum_path(value: torch.Tensor, mask: torch.Tensor, *, return_row_start: b
     value = value.contiguous()
     mask = mask.contiguous()
     B, Tx, Ty = value.shape
+    _check_tx(Tx)
     dev = value.device
     path = torch.empty((B, Tx, Ty), dtype=torch.float32, device=dev)
     row_start = torch.empty((B, Tx), dtype=torch.int32, device=dev) if return_row_start else None
@@ -74,6 +84,7 @@ def maximum_path_c(paths: torch.Tensor, values: torch.Tensor, t_xs: torch.Tensor
     if not (paths.is_contiguous() and values.is_contiguous()):
         raise ValueError("maximum_path_c mutates its arguments in place: they must be C-contiguous")
     B, Tx, Ty = values.shape
+    _check_tx(Tx)
     t_xs = t_xs.to(torch.int32).contiguous()
     t_ys = t_ys.to(torch.int32).contiguous()
     dev = values.device
@@ -91,7 +102,7 @@ compute_batch_alignments = maximum_path_c
 
 def prior_maximum_path(mu_x: torch.Tensor, y: torch.Tensor, x_lengths: torch.Tensor, y_lengths: torch.Tensor, *,
                        return_lattice: bool = False):
-    """The training forward's alignment step fused (matcha_tts.py:461-478, MatchaTTS.forward):
+    """The training forward's alignment step fused (matcha_tts.py:276-288, MatchaTTS.forward):
     log-prior lattice from mu_x [B,C,Tx] and y [B,C,Ty] (fp32), masked by the length masks, Viterbi
     max path, and the duration target -- one lattice write to HBM instead of two bmm's, their
     elementwise tail, the [B,Tx,Ty] attention mask and a reduction over the dense path
@@ -109,6 +120,7 @@ def prior_maximum_path(mu_x: torch.Tensor, y: torch.Tensor, x_lengths: torch.Ten
     xl = x_lengths.detach().to(torch.int64).contiguous()
     yl = y_lengths.detach().to(torch.int64).contiguous()
     B, C, Tx = mu_x.shape
+    _check_tx(Tx)
     Ty = y.shape[2]
     dev = mu_x.device
     attn = torch.empty((B, Tx, Ty), dtype=torch.float32, device=dev)
@@ -129,7 +141,7 @@ def prior_maximum_path(mu_x: torch.Tensor, y: torch.Tensor, x_lengths: torch.Ten
 
 
 class _ExpandRows(torch.autograd.Function):
-    """mu_y = attn^T @ mu_x for a hard alignment (matcha_tts.py:504-505) as a gather of mu_x columns;
+    """mu_y = attn^T @ mu_x for a hard alignment (matcha_tts.py:314-315) as a gather of mu_x columns;
     backward sums each text row's run of frames (deterministic segment sums, no atomics)."""
 
     @staticmethod

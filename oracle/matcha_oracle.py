@@ -8,7 +8,7 @@ training forward:
                  additive bias, erf GELU)
   CFM loss       /root/reference/matcha/models/components/flow_matching.py:106-151
   text encoder   /root/reference/matcha/models/components/text_encoder.py:17-402
-  model forward  /root/reference/matcha/models/matcha_tts.py:437-515 (simple-params init :294-366)
+  model forward  /root/reference/matcha/models/matcha_tts.py:247-325 (simple-params init :294-366)
   utilities      /root/reference/matcha/utils/model.py:13-135
 Parameter names equal the reference's, so a state_dict moves between reference, oracle and product.
 Dropout layers sit where the reference has them (decoder 0.05, encoder 0.1) and are active only in
@@ -356,7 +356,7 @@ class EncoderO(nn.Module):  # text_encoder.py:256-322
         return x * m
 
 
-class TextEncoderO(nn.Module):  # text_encoder.py:325-402 (simple-params config, matcha_tts.py:313-334)
+class TextEncoderO(nn.Module):  # text_encoder.py:325-402 (simple-params config, matcha_tts.py:104-176)
     def __init__(self, n_vocab, n_feats=80, c=192, cf=768, heads=2, layers=6, k=3, dp_filter=256):
         super().__init__()
         self.c = c
@@ -387,7 +387,7 @@ def fix_len_compatibility(length, num_downsamplings_in_unet=2):  # model.py:37-5
 
 
 class MatchaTTSOracle(nn.Module):
-    """MatchaTTS(n_vocab, out_channels=80, hidden_channels=192) forward (matcha_tts.py:437-515)."""
+    """MatchaTTS(n_vocab, out_channels=80, hidden_channels=192) forward (matcha_tts.py:247-325)."""
 
     def __init__(self, n_vocab=150, out_channels=80, hidden_channels=192, maximum_path=None):
         super().__init__()
@@ -422,7 +422,7 @@ class MatchaTTSOracle(nn.Module):
         mu_x, logw, x_mask = self.encoder(x, x_lengths)
         y_mask = sequence_mask(y_lengths, y.shape[-1]).unsqueeze(1).to(x_mask)
         attn_mask = x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)
-        with torch.no_grad():  # matcha_tts.py:466-475
+        with torch.no_grad():  # matcha_tts.py:276-285
             const = -0.5 * math.log(2 * math.pi) * self.n_feats
             factor = -0.5 * torch.ones(mu_x.shape, dtype=mu_x.dtype)
             y_square = torch.matmul(factor.transpose(1, 2), y ** 2)

@@ -1,7 +1,7 @@
 """CPU restatement of the log-prior lattice and the alignment consumers -- TEST INFRASTRUCTURE ONLY.
 
 Only tests/ may import this module (the product never does).  It restates, in numpy fp32:
-  * the lattice producer of MatchaTTS.forward, reference matcha/models/matcha_tts.py:467-472
+  * the lattice producer of MatchaTTS.forward, reference matcha/models/matcha_tts.py:277-282
         const = -0.5 * log(2 pi) * n_feats
         factor = -0.5 * ones(mu_x.shape)
         y_square = factor^T @ y**2 ;  y_mu_double = (2 * factor * mu_x)^T @ y
@@ -13,8 +13,8 @@ Only tests/ may import this module (the product never does).  It restates, in nu
     matmuls sum in an implementation-defined (blocked) order; against them the lattice agrees to
     fp32 rounding, and the alignments agree exactly unless a DP decision is a near-tie.
   * maximum_path's value * mask (monotonic_align/__init__.py:45) with mask = x_mask[i] * y_mask[j]
-    (matcha_tts.py:461).
-  * the consumers of the hard alignment, matcha_tts.py:477-478 and 504-505:
+    (matcha_tts.py:276).
+  * the consumers of the hard alignment, matcha_tts.py:287-288 and 504-505:
         durations  sum_y attn[b, x, y]          (logw_ = log(1e-8 + durations) * x_mask)
         mu_y       attn^T @ mu_x               (a gather of mu_x columns on a one-hot attn)
 """
@@ -51,7 +51,7 @@ def log_prior_lattice(mu_x: np.ndarray, y: np.ndarray, x_lengths, y_lengths) -> 
 
 
 def durations(path: np.ndarray) -> np.ndarray:
-    """sum_y attn[b, x, y] as float32 [B, Tx] (matcha_tts.py:477)."""
+    """sum_y attn[b, x, y] as float32 [B, Tx] (matcha_tts.py:287)."""
     return np.asarray(path, np.float32).sum(-1, dtype=np.float32)
 
 
@@ -64,5 +64,5 @@ def col_row(path: np.ndarray) -> np.ndarray:
 
 
 def expand_rows(mu_x: np.ndarray, path: np.ndarray) -> np.ndarray:
-    """attn^T @ mu_x as the reference computes it (matcha_tts.py:504-505): [B,C,Ty], float64 sums."""
+    """attn^T @ mu_x as the reference computes it (matcha_tts.py:314-315): [B,C,Ty], float64 sums."""
     return np.einsum("bxy,bcx->bcy", np.asarray(path, np.float64), np.asarray(mu_x, np.float64))

@@ -108,9 +108,10 @@ def _rand_case(rng, B, Tx, Ty, ties=False):
 
 @pytest.mark.parametrize("Tx,Ty", [(1, 1), (2, 3), (63, 64), (64, 64), (65, 130), (127, 129),
                                    (128, 128), (129, 301), (200, 203), (255, 600), (256, 257),
-                                   (257, 700), (300, 999), (511, 1001), (512, 512), (77, 33 * 32 + 5)])
+                                   (257, 700), (300, 999), (511, 1001), (512, 512), (77, 33 * 32 + 5),
+                                   (513, 600), (700, 1501), (1024, 1024), (1000, 2100)])
 def test_random_vs_oracle(Tx, Ty):
-    """Every K specialisation (rows/lane 1,2,4,8), odd Ty (scalar loads), LDS- and HBM-resident
+    """Every K specialisation (rows/lane 1,2,4,8,16), odd Ty (scalar loads), LDS- and HBM-resident
     backpointers, square lattices (forced diagonal), and ties."""
     rng = np.random.default_rng(Tx * 10007 + Ty)
     for ties in (False, True):
@@ -188,7 +189,7 @@ def test_no_host_sync_and_stream_ordering():
                                        (2, 16, 1, 5), (3, 80, 300, 301)])
 def test_prior_maximum_path_vs_oracle(B, C, Tx, Ty):
     """mtts_prior_maximum_path: the masked lattice is bit-identical to the numpy restatement of
-    matcha_tts.py:467-472 (oracle/prior_oracle.py), the path bit-identical to the CPU oracle's
+    matcha_tts.py:277-282 (oracle/prior_oracle.py), the path bit-identical to the CPU oracle's
     maximum_path on that lattice, durations == path.sum(-1), col_row == the path's row per frame."""
     from matcha.utils.monotonic_align import prior_maximum_path
     from oracle import prior_oracle as PO
@@ -212,7 +213,7 @@ def test_prior_maximum_path_vs_oracle(B, C, Tx, Ty):
 
 
 def test_prior_lattice_matches_torch_formula():
-    """Against the reference's own formula (matcha_tts.py:467-472 in float64): fp32 rounding only."""
+    """Against the reference's own formula (matcha_tts.py:277-282 in float64): fp32 rounding only."""
     from matcha.utils.monotonic_align import prior_maximum_path
 
     g = torch.Generator().manual_seed(5)
@@ -253,3 +254,15 @@ def test_expand_rows_matches_bmm_and_its_gradient():
     gref = torch.matmul(gy.double(), attn.double().transpose(1, 2))
     err = (a.grad.double() - gref).abs().max().item() / gref.abs().max().item()
     assert err < 1e-6, err
+
+
+def test_text_length_limit_is_a_clear_error():
+    """Beyond MTTS_MAS_MAX_TX (1024 rows; the reference Cython has no cap) the wrapper refuses with a
+    ValueError naming the limit instead of a native shape error."""
+    import torch
+
+    from matcha.utils.monotonic_align import maximum_path
+
+    v = torch.zeros(1, 1025, 1100, device="cuda")
+    with pytest.raises(ValueError, match="1024"):
+        maximum_path(v, torch.ones_like(v))
