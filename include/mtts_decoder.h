@@ -119,7 +119,9 @@ typedef struct mtts_conv_wgrad_args {
     int32_t off[MTTS_CONV_MAX_TAPS];
     int32_t cin;
     int32_t N, K;
-    int32_t flags; /* MTTS_GEMM_F_A_BF16: A holds bf16 (lda in elements; bf16 precision only) */
+    int32_t flags; /* MTTS_GEMM_F_A_BF16: A holds bf16 (lda in elements; bf16 precision only);
+                      MTTS_GEMM_F_BINARY_SCALE: a_scale holds only 0 / 1 (lets the bf16 LDS-DMA schedule
+                      drop masked rows by address selection) */
 } mtts_conv_wgrad_args;
 
 size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *args);
@@ -127,7 +129,8 @@ int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precision, float *
                     int64_t sj, float *db, int32_t accumulate, void *workspace, size_t workspace_bytes,
                     void *hip_stream);
 /* Same, with an explicit schedule: rows_per_step 32 (or 64, bf16), target_blocks 64..1024 for the
- * row split, depth 1 (or 2, bf16) row steps in flight (-1 = defaults).  For tuning;
+ * row split, depth 1 (or 2, bf16) row steps in flight (-1 = defaults); depth 3 with rows_per_step -1 (bf16,
+ * fp32 operands) = the LDS-DMA schedule (csrc/wgrad_glds.hip; where it does not apply, the default).  For tuning;
  * mtts_conv_wgrad_workspace_size covers every schedule. */
 int mtts_conv_wgrad_tile(const mtts_conv_wgrad_args *args, int32_t precision, int32_t rows_per_step,
                          int32_t target_blocks, int32_t depth, float *dw, int64_t sn, int64_t sc, int64_t sj,

@@ -113,6 +113,14 @@ int conv_gemm_glds_launch(int id, const mtts_conv_gemm_args &p, int M, int split
 size_t conv_gemm_glds_splitk_bytes(const mtts_conv_gemm_args &p, int splits);
 }  // namespace mtts
 
+struct mtts_conv_wgrad_args;
+namespace mtts {
+// wgrad_glds.hip: LDS-DMA weight-gradient schedule (fp32 operands, bf16 MFMA)
+bool wgrad_glds_applies(const mtts_conv_wgrad_args &p, int rows_per_split);
+int wgrad_glds_launch(const mtts_conv_wgrad_args &p, int splits, int rows_per_split, float *part, float *part_db,
+                      hipStream_t st);
+}  // namespace mtts
+
 struct mtts_reduce_job;
 namespace mtts {
 // reduce.hip: runs the partial-sum jobs now, or queues them while deferral is on

@@ -508,7 +508,8 @@ def _wgrad_launch(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, of
     for i, o in enumerate(offs):
         args.off[i] = o
     args.N, args.K = N_, len(offs) * cin
-    args.flags = GEMM_F_A_BF16 if A.dtype == torch.bfloat16 else 0
+    # every row scale the model passes is a 0/1 sequence mask (as in _gemm)
+    args.flags = (GEMM_F_A_BF16 if A.dtype == torch.bfloat16 else 0) | (GEMM_F_BINARY_SCALE if a_scale is not None else 0)
     lib = N.lib()
     ws = torch.empty(int(lib.mtts_conv_wgrad_workspace_size(ctypes.byref(args))), dtype=torch.uint8, device=dY.device)
     _keep_partials(ws)

@@ -209,7 +209,8 @@ GENERIC = [(1200, 16, 256, 768, 1), (800, 24, 512, 256, 3)]
 
 
 @pytest.mark.parametrize("B,T,Cin,Cout,k", BIG + GENERIC)
-@pytest.mark.parametrize("rows_per_step,target_blocks,depth", [(32, -1, 1), (32, 1024, 1), (64, 1024, 1), (32, 512, 2)])
+@pytest.mark.parametrize("rows_per_step,target_blocks,depth", [(-1, -1, -1), (-1, -1, 3), (32, -1, 1), (32, 1024, 1),
+                                                               (64, 1024, 1), (32, 512, 2)])
 def test_wgrad_bf16_exact_and_deterministic(B, T, Cin, Cout, k, rows_per_step, target_blocks, depth):
     from matcha.models.components import _ops as O
 
@@ -233,6 +234,41 @@ def test_wgrad_bf16_exact_and_deterministic(B, T, Cin, Cout, k, rows_per_step, t
     assert (db.double() - refb).abs().max().item() <= 1e-5 * refb.abs().max().item()
     for dw2, db2 in outs[1:]:
         assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout,k,stride", [(8, 300, 256, 256, 3, 1), (8, 301, 256, 256, 3, 2), (6, 77, 192, 768, 5, 1),
+                                                  (4, 64, 512, 160, 1, 1), (32, 40, 96, 200, 3, 1)])
+def test_wgrad_lds_dma_masked_strided(B, T, Cin, Cout, k, stride):
+    """The LDS-DMA wgrad schedule (csrc/wgrad_glds.hip, opt-in MTTS_WGRAD_GLDS=1) with a 0/1 row mask, ragged lengths,
+    stride 2, 1..5 taps and N / K not multiples of the 128 tile: against float64 on bf16-exact operands
+    (1e-5 of the output scale), bitwise repeatable, and equal in value to the register-staged kernel."""
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator(device="cpu").manual_seed(B * T + Cin + k + stride)
+    x = torch.randn(B, T, Cin, generator=g).bfloat16().float().to(DEV)
+    lengths = torch.randint(T // 3, T + 1, (B,), generator=g)
+    lengths[0] = T
+    m = (torch.arange(T)[None] < lengths[:, None]).float().to(DEV)
+    pad = k // 2
+    To = (T + 2 * pad - k) // stride + 1
+    dy = torch.randn(B, To, Cout, generator=g).bfloat16().float().to(DEV)
+    xm = (x * m.unsqueeze(-1)).double()
+    ref = torch.nn.grad.conv1d_weight(xm.transpose(1, 2), (Cout, Cin, k), dy.double().transpose(1, 2), stride=stride,
+                                      padding=pad)
+    refb = dy.double().sum((0, 1))
+    outs = []
+    for sched in [(-1, -1, 3)] * 2 + [(32, -1, 1)]:  # depth 3: the LDS-DMA schedule
+        dw = torch.full((Cout, Cin, k), float("nan"), device=DEV)
+        db = torch.full((Cout,), float("nan"), device=DEV)
+        O._wgrad(dy, To, 1, 0, x, T, To, B, stride, [j - pad for j in range(k)], Cin, Cout, dw, (Cin * k, k, 1),
+                 prec=O.PREC_BF16, a_scale=m, db=db, rows_per_step=sched[0], target_blocks=sched[1], depth=sched[2])
+        outs.append((dw, db))
+    torch.cuda.synchronize()
+    dw, db = outs[0]
+    assert (dw.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+    assert (db.double() - refb).abs().max().item() <= 1e-5 * refb.abs().max().item()
+    assert torch.equal(dw, outs[1][0]) and torch.equal(db, outs[1][1])
+    torch.testing.assert_close(dw, outs[2][0], rtol=1e-5, atol=1e-5 * ref.abs().max().item())
 
 
 @pytest.mark.parametrize("B,T,Cin,Cout,k", BIG)
@@ -326,7 +362,11 @@ def test_bf16_operand_storage_bitwise(B, T, Cin, Cout, k, cfg):
         O._wgrad(dy, T, 1, 0, xa, T, T, B, 1, offs, Cin, Cout, dw, (Cin * k, k, 1), prec=O.PREC_BF16, a_scale=m, db=db)
         outs.append((dw, db))
     torch.cuda.synchronize()
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    # fp32 A runs the LDS-DMA wgrad, bf16 A the register-staged one: the same bf16 products, summed over
+    # other row splits (128-row rounds) and the bias column sums in another fixed order -- equal to fp32
+    # reordering (~1e-6 of the scale for sums of up to 19200 terms)
+    for a, b in zip(outs[0], outs[1]):
+        assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item()
 
 
 def test_reduce_partials_jobs():
