@@ -121,8 +121,10 @@ typedef struct mtts_conv_wgrad_args {
     int32_t N, K;
     int32_t flags; /* MTTS_GEMM_F_A_BF16: A holds bf16 (lda in elements; bf16 precision only);
                       MTTS_GEMM_F_BINARY_SCALE: a_scale holds only 0 / 1 (lets the bf16 LDS-DMA schedule
-                      drop masked rows by address selection) */
+                      drop masked rows by address selection); MTTS_WGRAD_F_DY_BF16: dY holds bf16 (ldy in
+                      elements, rows 8-byte aligned; bf16 precision, default schedule) */
 } mtts_conv_wgrad_args;
+#define MTTS_WGRAD_F_DY_BF16 0x20
 
 size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *args);
 int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precision, float *dw, int64_t sn, int64_t sc,
@@ -167,7 +169,9 @@ int mtts_act_dropout_bwd(const float *dy, const float *y, float *dx, int32_t row
 /* LayerNorm over the last dim of x [M, C]; mean/rstd [M] saved.  C % 4 == 0, C <= 1024.  Optional
  * fused tail applied to the normalized output: act MTTS_ACT_RELU, then dropout(p) with the
  * counter-based mask keyed (seed, row, channel) -- the text encoder's LN -> ReLU -> Dropout
- * (text_encoder.py:48-55) and LN -> Dropout (:81-95).  act = MTTS_ACT_NONE, p = 0: plain LayerNorm. */
+ * (text_encoder.py:48-55) and LN -> Dropout (:81-95).  act = MTTS_ACT_NONE, p = 0: plain LayerNorm.
+ * act | MTTS_NORM_F_Y_BF16: y is written as bf16 (a GEMM operand in bf16-mixed mode, half the bytes). */
+#define MTTS_NORM_F_Y_BF16 0x100
 int mtts_layernorm_fwd(const float *x, const float *w, const float *b, float *y, float *mean, float *rstd,
                        int32_t M, int32_t C, float eps, int32_t act, float dropout_p, const uint32_t *seed,
                        void *hip_stream);
@@ -178,6 +182,11 @@ int mtts_layernorm_bwd(const float *dy, const float *x, const float *w, const fl
                        const float *rstd, float *dx, float *dw, float *db, int32_t M, int32_t C, int32_t act,
                        float dropout_p, const uint32_t *seed, void *workspace, size_t workspace_bytes,
                        void *hip_stream);
+/* Plain LayerNorm backward plus a residual branch's gradient: dx = LN'(dy) + dres (a pre-LN transformer
+ * sub-block, transformer.py:316-358, where x feeds both the norm and the residual add). */
+int mtts_layernorm_bwd_res(const float *dy, const float *x, const float *w, const float *b, const float *mean,
+                           const float *rstd, const float *dres, float *dx, float *dw, float *db, int32_t M,
+                           int32_t C, void *workspace, size_t workspace_bytes, void *hip_stream);
 
 /*
  * Batched weight packing (csrc/pack.hip): each job is one affine gather of an fp32 torch weight into

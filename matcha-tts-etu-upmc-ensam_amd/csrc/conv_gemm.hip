@@ -362,11 +362,15 @@ struct WgradGeom {
 // wrap per step) and 32-bit element offsets; the launcher picks the generic path otherwise.
 // ABF16: A holds bf16 (MTTS_GEMM_F_A_BF16, bf16 precision only): 8-byte row chunks instead of 16, no
 // conversion on the way to LDS (the masked-row zeroing is a select).
-template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false>
+// YBF16: dY holds bf16 (MTTS_WGRAD_F_DY_BF16): 8-byte row chunks, staged as is (the bias column sums
+// convert exactly).
+template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_args p, int rows_per_split,
                                                                float *__restrict__ part, float *__restrict__ part_db) {
     static_assert(!ABF16 || BF16, "bf16 A needs the bf16 path");
+    static_assert(!YBF16 || BF16, "bf16 dY needs the bf16 path");
     const uint16_t *A16 = reinterpret_cast<const uint16_t *>(p.A);
+    const uint16_t *Y16 = reinterpret_cast<const uint16_t *>(p.dY);
     using Gm = WgradGeom<BF16, KB>;
     using ST = typename Gm::ST;
     constexpr int T = Gm::T, LDR = Gm::LDR, LDW = Gm::LDW, IMG = Gm::kImg, CH = Gm::CH;
@@ -437,6 +441,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
     struct Regs {
         float4 y[CH][2], x[CH][2];
         uint2 x16[CH][2];  // ABF16: the 4 bf16 of the chunk
+        uint2 y16[CH][2];  // YBF16
         float xs[CH][2];
         bool yok[CH][2], xok[CH][2];
     };
@@ -455,7 +460,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const bool mv = 2 * c_rp[c] + h < rows_left;
-                    R.y[c][h] = *reinterpret_cast<const float4 *>(p.dY + (uint32_t)((mv ? s_y[c][h] : 0) + y_col));
+                    if constexpr (YBF16)
+                        R.y16[c][h] = *reinterpret_cast<const uint2 *>(Y16 + (uint32_t)((mv ? s_y[c][h] : 0) + y_col));
+                    else
+                        R.y[c][h] = *reinterpret_cast<const float4 *>(p.dY + (uint32_t)((mv ? s_y[c][h] : 0) + y_col));
                     R.yok[c][h] = mv;
                     const bool xok = mv && (unsigned)s_i[c][h] < (unsigned)p.Ti;
                     const int xr = xok ? s_x[c][h] : 0;
@@ -484,7 +492,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
                 divmod_fast(mv ? m : 0, p.To, inv_to, b, u);
                 const bool yok = mv && c_nok[c];
                 const size_t yrow = yok ? (size_t)b * p.To_full + (size_t)u * p.out_stride + p.out_off : 0;
-                R.y[c][h] = *reinterpret_cast<const float4 *>(p.dY + yrow * p.ldy + (yok ? n0 + c_cc[c] : 0));
+                if constexpr (YBF16)
+                    R.y16[c][h] = *reinterpret_cast<const uint2 *>(Y16 + yrow * p.ldy + (yok ? n0 + c_cc[c] : 0));
+                else
+                    R.y[c][h] = *reinterpret_cast<const float4 *>(p.dY + yrow * p.ldy + (yok ? n0 + c_cc[c] : 0));
                 R.yok[c][h] = yok;
                 const int irow = u * p.in_stride + c_toff[c];
                 const bool xok = mv && c_kok[c] && irow >= 0 && irow < p.Ti;
@@ -510,8 +521,16 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
                 // CU co-residency (tools/gpu_r2d.sh reproduces it, variant F fixes it)
                 const bool yk = R.yok[c][h];
                 const float xm = R.xok[c][h] ? (p.a_scale ? R.xs[c][h] : 1.f) : 0.f;
-                yv[h][0] = yk ? R.y[c][h].x : 0.f; yv[h][1] = yk ? R.y[c][h].y : 0.f;
-                yv[h][2] = yk ? R.y[c][h].z : 0.f; yv[h][3] = yk ? R.y[c][h].w : 0.f;
+                float4 yf;
+                if constexpr (YBF16) {  // bf16 -> fp32 is exact: the bits move to the high half
+                    const uint2 q = R.y16[c][h];
+                    yf = make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                                     __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
+                } else {
+                    yf = R.y[c][h];
+                }
+                yv[h][0] = yk ? yf.x : 0.f; yv[h][1] = yk ? yf.y : 0.f;
+                yv[h][2] = yk ? yf.z : 0.f; yv[h][3] = yk ? yf.w : 0.f;
                 if constexpr (!ABF16) {
                     xv[h][0] = R.x[c][h].x * xm; xv[h][1] = R.x[c][h].y * xm;
                     xv[h][2] = R.x[c][h].z * xm; xv[h][3] = R.x[c][h].w * xm;
@@ -828,9 +847,11 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
         if (!bf16 || !mtts::conv_gemm_glds_applies(p))
             return mtts::fail(MTTS_ERR_UNSUPPORTED,
                               "conv_gemm: a bf16 A needs bf16 precision, cin >= 64, cin / lda % 8 == 0, 0/1 a_scale");
-        if (cfg < 0) {
+        if (cfg < 0) {  // 64 x 64 three-stage tiles unless the one-round 64 x 256 schedule applies (K >= 768,
+            // 128..256 tiles); tools/preln_shapes.py: the FFN dgrad from a bf16 d(pre-activation), 19200 x
+            // 256 x 1024, 24.8 us on 64 x 64 vs 33.5 on 64 x 256 two-stage
             cfg = pick_cfg(p, M, bf16);
-            if (cfg < MTTS_GEMM_GLDS) cfg = MTTS_GEMM_GLDS + 9;
+            if (cfg < MTTS_GEMM_GLDS) cfg = MTTS_GEMM_GLDS + 12;
         } else if (cfg < MTTS_GEMM_GLDS) {
             return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: a bf16 A needs an LDS-DMA schedule");
         }
@@ -941,20 +962,20 @@ extern "C" size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *arg
     return mtts::align_up((size_t)splits * args->N * args->K * 4, 256) + (size_t)splits * args->N * 4 + 256;
 }
 
-template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false>
+template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false>
 static int wgrad_launch_k(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
                           hipStream_t st) {
     using Gm = WgradGeom<BF16, KB>;
     static bool attr_set = false;
     if (Gm::kLds > 64 * 1024 && !attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)Gm::kLds) != hipSuccess)
             return mtts::fail(MTTS_ERR_HIP, "conv_wgrad: LDS attribute");
         attr_set = true;
     }
     dim3 grid((unsigned)(((p.N + 127) / 128) * ((p.K + 127) / 128) * splits));
-    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16>), grid, dim3(kThreads), Gm::kLds, st, p, rps,
-                       part, part_db);
+    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16>), grid, dim3(kThreads), Gm::kLds, st, p,
+                       rps, part, part_db);
     return mtts::check_launch("conv_wgrad_kernel");
 }
 
@@ -971,9 +992,16 @@ template <bool BF16, int KB, int DEPTH>
 static int wgrad_launch(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
                         hipStream_t st) {
     if constexpr (BF16 && KB == 32 && DEPTH == 1) {
-        if (p.flags & MTTS_GEMM_F_A_BF16)
-            return wgrad_inc_ok(p, KB) ? wgrad_launch_k<true, 32, 1, true, true>(p, splits, rps, part, part_db, st)
-                                       : wgrad_launch_k<true, 32, 1, false, true>(p, splits, rps, part, part_db, st);
+        const bool a16 = p.flags & MTTS_GEMM_F_A_BF16, y16 = p.flags & MTTS_WGRAD_F_DY_BF16, inc = wgrad_inc_ok(p, KB);
+        if (a16 && y16)
+            return inc ? wgrad_launch_k<true, 32, 1, true, true, true>(p, splits, rps, part, part_db, st)
+                       : wgrad_launch_k<true, 32, 1, false, true, true>(p, splits, rps, part, part_db, st);
+        if (y16)
+            return inc ? wgrad_launch_k<true, 32, 1, true, false, true>(p, splits, rps, part, part_db, st)
+                       : wgrad_launch_k<true, 32, 1, false, false, true>(p, splits, rps, part, part_db, st);
+        if (a16)
+            return inc ? wgrad_launch_k<true, 32, 1, true, true>(p, splits, rps, part, part_db, st)
+                       : wgrad_launch_k<true, 32, 1, false, true>(p, splits, rps, part, part_db, st);
     }
     return wgrad_inc_ok(p, KB) ? wgrad_launch_k<BF16, KB, DEPTH, true>(p, splits, rps, part, part_db, st)
                                : wgrad_launch_k<BF16, KB, DEPTH, false>(p, splits, rps, part, part_db, st);
@@ -1006,9 +1034,9 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
     }
     if (rows_per_step < 0) rows_per_step = 32;
     if (depth < 0) depth = 1;
-    if (p.flags & MTTS_GEMM_F_A_BF16) {
+    if (p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_WGRAD_F_DY_BF16)) {
         MTTS_CHECK_ARG(bf16 && rows_per_step == 32 && depth == 1 && p.lda % 4 == 0 && (uintptr_t)p.A % 8 == 0,
-                       "conv_wgrad: a bf16 A needs bf16 precision, the default schedule and 8-byte aligned rows");
+                       "conv_wgrad: a bf16 A or dY needs bf16 precision, the default schedule and 8-byte aligned rows");
     }
     MTTS_CHECK_ARG(rows_per_step == 32 || (rows_per_step == 64 && bf16), "conv_wgrad: rows_per_step 32 (or 64 bf16)");
     MTTS_CHECK_ARG(depth == 1 || (depth == 2 && bf16), "conv_wgrad: depth 1 (or 2 bf16)");

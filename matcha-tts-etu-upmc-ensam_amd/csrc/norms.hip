@@ -377,6 +377,7 @@ int submit_param_sums(const float *pa, float *outa, const float *pb, float *outb
 
 // ------------------------------------------------------------------------------ LayerNorm
 // one wave per row; lane handles float4 chunks lane*4 + 256*i
+template <bool Y16>  // Y16: y written as bf16 (MTTS_NORM_F_Y_BF16)
 __global__ __launch_bounds__(kThreads) void layernorm_fwd_kernel(const float *__restrict__ x, const float *__restrict__ w,
                                                                  const float *__restrict__ bia, float *__restrict__ y,
                                                                  float *__restrict__ mean_out, float *__restrict__ rstd_out,
@@ -431,7 +432,15 @@ __global__ __launch_bounds__(kThreads) void layernorm_fwd_kernel(const float *__
                     if (p > 0.f) o[j] = mtts::dropout_keep(sd0, sd1, (uint32_t)row, (uint32_t)(c + j), p) ? o[j] * inv_keep : 0.f;
                 }
             }
-            *reinterpret_cast<float4 *>(yr + c) = make_float4(o[0], o[1], o[2], o[3]);
+            if constexpr (Y16) {
+                typedef float f2 __attribute__((ext_vector_type(2)));
+                typedef __bf16 h2 __attribute__((ext_vector_type(2)));
+                const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){o[0], o[1]}, h2));
+                const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){o[2], o[3]}, h2));
+                *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(y) + (size_t)row * C + c) = make_uint2(lo, hi);
+            } else {
+                *reinterpret_cast<float4 *>(yr + c) = make_float4(o[0], o[1], o[2], o[3]);
+            }
         }
     }
 }
@@ -450,7 +459,7 @@ __global__ __launch_bounds__(kThreads) void layernorm_bwd_kernel(const float *__
                                                                  const float *__restrict__ rstd_in, float *__restrict__ dx,
                                                                  float *__restrict__ pw, float *__restrict__ pb, int M,
                                                                  int C, int act, float p, const uint32_t *__restrict__ seed,
-                                                                 int rows_per_block) {
+                                                                 int rows_per_block, const float *__restrict__ dres) {
     __shared__ float4 red[2][kThreads / 64][256];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float4 aw[4], ab[4];
@@ -515,6 +524,10 @@ __global__ __launch_bounds__(kThreads) void layernorm_bwd_kernel(const float *__
                 o.y = rstd * (g[i].y - m1 - xh[i].y * m2);
                 o.z = rstd * (g[i].z - m1 - xh[i].z * m2);
                 o.w = rstd * (g[i].w - m1 - xh[i].w * m2);
+                if (dres) {  // + the residual branch's gradient (pre-LN block: x feeds the LN and the residual)
+                    const float4 r = *reinterpret_cast<const float4 *>(dres + (size_t)row * C + c);
+                    o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+                }
                 *reinterpret_cast<float4 *>(dx + (size_t)row * C + c) = o;
             }
         }
@@ -604,14 +617,20 @@ extern "C" int mtts_layernorm_fwd(const float *x, const float *w, const float *b
                                   float *rstd, int32_t M, int32_t C, float eps, int32_t act, float dropout_p,
                                   const uint32_t *seed, void *hip_stream) {
     MTTS_CHECK_ARG(x && w && b && y && mean && rstd, "layernorm_fwd: null pointer");
+    const bool y16 = act & MTTS_NORM_F_Y_BF16;
+    act &= ~MTTS_NORM_F_Y_BF16;
     MTTS_CHECK_ARG(act == MTTS_ACT_NONE || act == MTTS_ACT_RELU, "layernorm_fwd: act must be NONE or RELU");
     MTTS_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed), "layernorm_fwd: bad dropout");
     MTTS_CHECK_ARG(M >= 0 && C >= 4 && C % 4 == 0 && C <= 1024, "layernorm_fwd: need C % 4 == 0, C <= 1024");
     MTTS_CHECK_ARG(aligned16(x) && aligned16(y) && aligned16(w) && aligned16(b), "layernorm_fwd: 16-byte alignment");
     if (M == 0) return MTTS_OK;
     const int rows_per_block = kThreads / 64;
-    hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((M + rows_per_block - 1) / rows_per_block), dim3(kThreads), 0,
-                       static_cast<hipStream_t>(hip_stream), x, w, b, y, mean, rstd, M, C, eps, act, dropout_p, seed);
+    if (y16)
+        hipLaunchKernelGGL(layernorm_fwd_kernel<true>, dim3((M + rows_per_block - 1) / rows_per_block), dim3(kThreads), 0,
+                           static_cast<hipStream_t>(hip_stream), x, w, b, y, mean, rstd, M, C, eps, act, dropout_p, seed);
+    else
+        hipLaunchKernelGGL(layernorm_fwd_kernel<false>, dim3((M + rows_per_block - 1) / rows_per_block), dim3(kThreads), 0,
+                           static_cast<hipStream_t>(hip_stream), x, w, b, y, mean, rstd, M, C, eps, act, dropout_p, seed);
     return mtts::check_launch("layernorm_fwd_kernel");
 }
 
@@ -621,11 +640,12 @@ extern "C" size_t mtts_layernorm_bwd_workspace_size(int32_t M, int32_t C) {
     return (size_t)2 * ((M + rpb - 1) / rpb) * C * sizeof(float);
 }
 
-extern "C" int mtts_layernorm_bwd(const float *dy, const float *x, const float *w, const float *b, const float *mean,
-                                  const float *rstd, float *dx, float *dw, float *db, int32_t M, int32_t C,
-                                  int32_t act, float dropout_p, const uint32_t *seed, void *workspace,
-                                  size_t workspace_bytes, void *hip_stream) {
+static int layernorm_bwd_impl(const float *dy, const float *x, const float *w, const float *b, const float *mean,
+                              const float *rstd, const float *dres, float *dx, float *dw, float *db, int32_t M,
+                              int32_t C, int32_t act, float dropout_p, const uint32_t *seed, void *workspace,
+                              size_t workspace_bytes, void *hip_stream) {
     MTTS_CHECK_ARG(dy && x && w && mean && rstd && dx, "layernorm_bwd: null pointer");
+    MTTS_CHECK_ARG(!dres || aligned16(dres), "layernorm_bwd: dres must be 16-byte aligned");
     MTTS_CHECK_ARG(act == MTTS_ACT_NONE || (act == MTTS_ACT_RELU && b), "layernorm_bwd: act RELU needs b");
     MTTS_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed), "layernorm_bwd: bad dropout");
     MTTS_CHECK_ARG(M >= 0 && C >= 4 && C % 4 == 0 && C <= 1024, "layernorm_bwd: need C % 4 == 0, C <= 1024");
@@ -639,8 +659,24 @@ extern "C" int mtts_layernorm_bwd(const float *dy, const float *x, const float *
     float *pw = static_cast<float *>(workspace);
     float *pb = pw + (size_t)nblk * C;
     hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(nblk), dim3(kThreads), 0, st, dy, x, w, b, mean, rstd, dx, pw, pb, M,
-                       C, act, dropout_p, seed, rpb);
+                       C, act, dropout_p, seed, rpb, dres);
     int rc = mtts::check_launch("layernorm_bwd_kernel");
     if (rc) return rc;
     return submit_param_sums(pw, dw, pb, db, nblk, C, st);
+}
+
+extern "C" int mtts_layernorm_bwd(const float *dy, const float *x, const float *w, const float *b, const float *mean,
+                                  const float *rstd, float *dx, float *dw, float *db, int32_t M, int32_t C,
+                                  int32_t act, float dropout_p, const uint32_t *seed, void *workspace,
+                                  size_t workspace_bytes, void *hip_stream) {
+    return layernorm_bwd_impl(dy, x, w, b, mean, rstd, nullptr, dx, dw, db, M, C, act, dropout_p, seed, workspace,
+                              workspace_bytes, hip_stream);
+}
+
+extern "C" int mtts_layernorm_bwd_res(const float *dy, const float *x, const float *w, const float *b,
+                                      const float *mean, const float *rstd, const float *dres, float *dx, float *dw,
+                                      float *db, int32_t M, int32_t C, void *workspace, size_t workspace_bytes,
+                                      void *hip_stream) {
+    return layernorm_bwd_impl(dy, x, w, b, mean, rstd, dres, dx, dw, db, M, C, MTTS_ACT_NONE, 0.f, nullptr, workspace,
+                              workspace_bytes, hip_stream);
 }

@@ -283,7 +283,7 @@ namespace mtts {
 // inside int32, a NULL or 0/1 a_scale (MTTS_GEMM_F_BINARY_SCALE), and the mask rows of every split fit
 // the workgroup's staging buffer.
 bool wgrad_glds_applies(const mtts_conv_wgrad_args &p, int rows_per_split) {
-    if (p.flags & MTTS_GEMM_F_A_BF16) return false;
+    if (p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_WGRAD_F_DY_BF16)) return false;
     if (p.To < kR || p.out_stride < 1 || p.in_stride < 1 || p.ntaps < 1) return false;
     if (p.a_scale && !(p.flags & MTTS_GEMM_F_BINARY_SCALE)) return false;
     const int64_t ymax = ((int64_t)p.nb + 2) * p.To_full * p.ldy;

@@ -53,6 +53,7 @@ GEMM_F_A_BF16 = 0x2  # MTTS_GEMM_F_A_BF16: A operand stored bf16 (bf16-mixed act
 GEMM_F_C_BF16 = 0x4  # MTTS_GEMM_F_C_BF16: output stored bf16
 GEMM_F_FAST_ACT = 0x8  # MTTS_GEMM_F_FAST_ACT: 1.5e-7-accurate erf in GELU epilogues (bf16-mixed only)
 GEMM_F_PRE_BF16 = 0x10  # MTTS_GEMM_F_PRE_BF16: C_pre written / aux read as bf16
+WGRAD_F_DY_BF16 = 0x20  # MTTS_WGRAD_F_DY_BF16: the weight gradient's dY holds bf16
 _FAST_ACT = os.environ.get("MTTS_EXACT_GELU") != "1"
 GEMM_GLDS = 32  # MTTS_GEMM_GLDS: first LDS-DMA schedule id
 
@@ -509,7 +510,8 @@ def _wgrad_launch(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, of
         args.off[i] = o
     args.N, args.K = N_, len(offs) * cin
     # every row scale the model passes is a 0/1 sequence mask (as in _gemm)
-    args.flags = (GEMM_F_A_BF16 if A.dtype == torch.bfloat16 else 0) | (GEMM_F_BINARY_SCALE if a_scale is not None else 0)
+    args.flags = ((GEMM_F_A_BF16 if A.dtype == torch.bfloat16 else 0) | (GEMM_F_BINARY_SCALE if a_scale is not None else 0)
+                  | (WGRAD_F_DY_BF16 if dY.dtype == torch.bfloat16 else 0))
     lib = N.lib()
     ws = torch.empty(int(lib.mtts_conv_wgrad_workspace_size(ctypes.byref(args))), dtype=torch.uint8, device=dY.device)
     _keep_partials(ws)
@@ -1024,16 +1026,7 @@ class _AttentionTM(torch.autograd.Function):
         o = torch.empty(B, T, C3 // 3, device=qkv.device, dtype=torch.float32)
         lse = torch.empty(B, heads, T, device=qkv.device, dtype=torch.float32)
         seed = _new_seed(qkv.device) if dropout_p > 0 else None
-        a = _AttentionTM._args(qkv, bias, o, lse, heads, dropout_p, seed)
-        log = ATTN_LOG
-        if log is not None:
-            st, e0, e1 = _events(qkv.device)
-        N.check(N.lib().mtts_attention_fwd(ctypes.byref(a), prec, _stream(qkv)), "mtts_attention_fwd")
-        if log is not None:
-            e1.record(st)
-            D = C3 // 3 // heads
-            # two T x T x D products per head; q, k, v read, o and the row statistic written
-            log.append((e0, e1, 4.0 * B * heads * T * T * D, prec, 4 * B * T * C3 // 3 * 4 + B * heads * T * 4, "fwd"))
+        _attn_fwd(qkv, bias, o, lse, heads, prec, dropout_p, seed)
         ctx.save_for_backward(qkv, bias, o, lse)
         ctx.heads, ctx.prec, ctx.drop = heads, prec, (dropout_p, seed)
         return o
@@ -1041,31 +1034,47 @@ class _AttentionTM(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         qkv, bias, o, lse = ctx.saved_tensors
-        do = _f32c(do)
-        B, T, C3 = qkv.shape
-        C = C3 // 3
-        dqkv = torch.empty_like(qkv)
-        a = _AttentionTM._args(qkv, bias, o, lse, ctx.heads, *ctx.drop)
-        g = AttnGrads()
-        g.dout, g.lddo = do.data_ptr(), C
-        base, es = dqkv.data_ptr(), dqkv.element_size()
-        g.dq, g.dk, g.dv, g.ldd = base, base + C * es, base + 2 * C * es, C3
-        lib = N.lib()
-        ws = torch.empty(int(lib.mtts_attention_bwd_workspace_size(B, T, ctx.heads)), dtype=torch.uint8,
-                         device=qkv.device)
-        log = ATTN_LOG
-        if log is not None:
-            st, e0, e1 = _events(qkv.device)
-        N.check(lib.mtts_attention_bwd(ctypes.byref(a), ctypes.byref(g), ctx.prec, ws.data_ptr(), ws.numel(),
-                                       _stream(qkv)), "mtts_attention_bwd")
-        if log is not None:
-            e1.record(st)
-            D = C // ctx.heads
-            # four T x T x D products per head (dV, dP, dQ, dK; the recomputed S not counted); q, k, v, o,
-            # dO, the row statistic read, dq, dk, dv written
-            log.append((e0, e1, 8.0 * B * ctx.heads * T * T * D, ctx.prec,
-                        8 * B * T * C * 4 + B * ctx.heads * T * 4, "bwd"))
-        return dqkv, None, None, None
+        return _attn_bwd(_f32c(do), qkv, bias, o, lse, ctx.heads, ctx.prec, *ctx.drop), None, None, None
+
+
+def _attn_fwd(qkv, bias, o, lse, heads, prec, dropout_p=0.0, seed=None):
+    B, T, C3 = qkv.shape
+    a = _AttentionTM._args(qkv, bias, o, lse, heads, dropout_p, seed)
+    log = ATTN_LOG
+    if log is not None:
+        st, e0, e1 = _events(qkv.device)
+    N.check(N.lib().mtts_attention_fwd(ctypes.byref(a), prec, _stream(qkv)), "mtts_attention_fwd")
+    if log is not None:
+        e1.record(st)
+        D = C3 // 3 // heads
+        # two T x T x D products per head; q, k, v read, o and the row statistic written
+        log.append((e0, e1, 4.0 * B * heads * T * T * D, prec, 4 * B * T * C3 // 3 * 4 + B * heads * T * 4, "fwd"))
+
+
+def _attn_bwd(do, qkv, bias, o, lse, heads, prec, dropout_p=0.0, seed=None):
+    """-> d(q|k|v) [B, T, 3C] from dO [B, T, C]."""
+    B, T, C3 = qkv.shape
+    C = C3 // 3
+    dqkv = torch.empty_like(qkv)
+    a = _AttentionTM._args(qkv, bias, o, lse, heads, dropout_p, seed)
+    g = AttnGrads()
+    g.dout, g.lddo = do.data_ptr(), C
+    base, es = dqkv.data_ptr(), dqkv.element_size()
+    g.dq, g.dk, g.dv, g.ldd = base, base + C * es, base + 2 * C * es, C3
+    lib = N.lib()
+    ws = torch.empty(int(lib.mtts_attention_bwd_workspace_size(B, T, heads)), dtype=torch.uint8, device=qkv.device)
+    log = ATTN_LOG
+    if log is not None:
+        st, e0, e1 = _events(qkv.device)
+    N.check(lib.mtts_attention_bwd(ctypes.byref(a), ctypes.byref(g), prec, ws.data_ptr(), ws.numel(),
+                                   _stream(qkv)), "mtts_attention_bwd")
+    if log is not None:
+        e1.record(st)
+        D = C // heads
+        # four T x T x D products per head (dV, dP, dQ, dK; the recomputed S not counted); q, k, v, o,
+        # dO, the row statistic read, dq, dk, dv written
+        log.append((e0, e1, 8.0 * B * heads * T * T * D, prec, 8 * B * T * C * 4 + B * heads * T * 4, "bwd"))
+    return dqkv
 
 
 def attention_tm(qkv, key_bias, heads: int, dropout_p: float = 0.0):
@@ -1074,6 +1083,186 @@ def attention_tm(qkv, key_bias, heads: int, dropout_p: float = 0.0):
     0/1 mask is ADDED to the scores (diffusers AttnProcessor2_0 + prepare_attention_mask),
     so padded keys are down-weighted, not removed.  Returns o [B, T, C] token-major."""
     return _AttentionTM.apply(qkv, key_bias, heads, float(dropout_p))
+
+
+# ------------------------------------------------------------------------------------------ pre-LN sub-blocks
+# BasicTransformerBlock (transformer.py:297-370) is two pre-LN residual sub-blocks:
+#     h + Dropout(to_out(SDPA(LN1(h) Wq, LN1(h) Wk, LN1(h) Wv)))      and      h + FF(LN3(h)).
+# Each runs as ONE autograd Function, so tensors only a GEMM reads can be stored as bf16 in bf16-mixed
+# mode (as autocast would hold them) without autograd casting gradients to their dtype: the attention
+# block's LayerNorm output (the q|k|v projection's A operand) and the FFN's d(pre-activation) (the dgrad
+# GEMM's A, the weight gradient's dY).  The backward adds the residual branch's gradient inside the
+# LayerNorm backward (mtts_layernorm_bwd_res) instead of an autograd accumulate kernel per sub-block.
+N.register("mtts_layernorm_bwd_res", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P])
+NORM_F_Y_BF16 = 0x100  # include/mtts_decoder.h MTTS_NORM_F_Y_BF16
+_PRELN_N16 = os.environ.get("MTTS_PRELN_N16", "1") != "0"  # attention block's LN output as bf16 (A/B switch)
+
+
+def _ln_fwd(h2, w, b, eps, y16):
+    M, C = h2.shape
+    n = torch.empty(M, C, device=h2.device, dtype=torch.bfloat16 if y16 else torch.float32)
+    mean = torch.empty(M, device=h2.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    N.check(N.lib().mtts_layernorm_fwd(h2.data_ptr(), w.data_ptr(), b.data_ptr(), n.data_ptr(), mean.data_ptr(),
+                                       rstd.data_ptr(), M, C, float(eps),
+                                       ACT_NONE | (NORM_F_Y_BF16 if n.dtype == torch.bfloat16 else 0), 0.0, None,
+                                       _stream(h2)), "mtts_layernorm_fwd")
+    return n, mean, rstd
+
+
+def _ln_bwd_res(dn, h2, w, b, mean, rstd, dres):
+    M, C = h2.shape
+    dh = torch.empty_like(h2)
+    dw = torch.empty(C, device=h2.device, dtype=torch.float32)
+    db = torch.empty_like(dw)
+    lib = N.lib()
+    ws = torch.empty(max(int(lib.mtts_layernorm_bwd_workspace_size(M, C)), 1), dtype=torch.uint8, device=h2.device)
+    _keep_partials(ws)
+    N.check(lib.mtts_layernorm_bwd_res(dn.data_ptr(), h2.data_ptr(), w.data_ptr(), b.data_ptr(), mean.data_ptr(),
+                                       rstd.data_ptr(), dres.data_ptr(), dh.data_ptr(), dw.data_ptr(), db.data_ptr(),
+                                       M, C, ws.data_ptr(), ws.numel(), _stream(h2)), "mtts_layernorm_bwd_res")
+    return dh, dw, db
+
+
+class _PreLNAttentionTM(torch.autograd.Function):
+    """h + Dropout(to_out(attention(LN1(h) W_qkv))) -- diffusers Attention (AttnProcessor2_0) behind
+    BasicTransformerBlock.norm1 (transformer.py:316-331); the float key mask is an additive bias."""
+
+    @staticmethod
+    def forward(ctx, h, ln_w, ln_b, eps, key_bias, heads, dropout_p, w_out, b_out, wq, wk, wv):
+        _check(h, ln_w, key_bias, w_out, wq)
+        prec = gemm_precision()
+        shp = h.shape
+        h2 = _f32c(h).reshape(-1, shp[-1])
+        M, C = h2.shape
+        B, T = shp[0], shp[1]
+        lnw, lnb = _f32c(ln_w), _f32c(ln_b)
+        n, mean, rstd = _ln_fwd(h2, lnw, lnb, eps, prec == PREC_BF16 and _PRELN_N16)
+        Wqkv, Kq = packed(spec_linear((wq, wk, wv)), prec)
+        Wo, Ko = packed(spec_linear((w_out,)), prec)
+        ctx.wqkv_t = packed(spec_linear((wq, wk, wv), dgrad=True), prec)
+        ctx.wo_t = packed(spec_linear((w_out,), dgrad=True), prec)
+        C3 = 3 * wq.shape[0]
+        qkv = torch.empty(B, T, C3, device=h.device, dtype=torch.float32)
+        _gemm(n, M, M, 1, 1, [0], C, Wqkv, Kq, C3, qkv.view(M, C3), M, prec=prec)
+        bias = _f32c(key_bias)
+        o = torch.empty(B, T, C3 // 3, device=h.device, dtype=torch.float32)
+        lse = torch.empty(B, heads, T, device=h.device, dtype=torch.float32)
+        _attn_fwd(qkv, bias, o, lse, heads, prec)
+        y = torch.empty(M, C, device=h.device, dtype=torch.float32)
+        seed = _new_seed(h.device) if dropout_p > 0 else None
+        _gemm(o.view(M, C3 // 3), M, M, 1, 1, [0], C3 // 3, Wo, Ko, C, y, M, prec=prec, bias=_f32c(b_out),
+              residual=h2, dropout_p=dropout_p, seed=seed)
+        ctx.save_for_backward(h2, lnw, lnb, mean, rstd, n, qkv, bias, o, lse)
+        ctx.leaf = _leaves(ln_w, ln_b, w_out, b_out, wq, wk, wv)
+        ctx.cfg = (prec, shp, heads, float(dropout_p), seed, [w.shape for w in (wq, wk, wv)], b_out is not None)
+        return y.reshape(shp)
+
+    @staticmethod
+    @_grad_sums
+    def backward(ctx, dy):
+        h2, lnw, lnb, mean, rstd, n, qkv, bias, o, lse = ctx.saved_tensors
+        prec, shp, heads, p, seed, qshapes, has_bout = ctx.cfg
+        M, C = h2.shape
+        B, T, C3 = qkv.shape
+        Ci = C3 // 3
+        dev = h2.device
+        dres = _f32c(dy).reshape(M, C)  # the residual branch's gradient
+        g = dres
+        if p > 0:  # through to_out's dropout: regenerate the forward's mask
+            g = torch.empty_like(dres)
+            N.check(N.lib().mtts_dropout_apply(dres.data_ptr(), g.data_ptr(), M, C, C, float(p), seed.data_ptr(),
+                                               _stream(g)), "mtts_dropout_apply")
+        # to_out: weight + bias gradient, dgrad -> dO
+        dwo = torch.empty(C, Ci, device=dev, dtype=torch.float32)
+        dbo = torch.empty(C, device=dev, dtype=torch.float32) if has_bout else None
+        _wgrad(g, M, 1, 0, o.view(M, Ci), M, M, 1, 1, [0], Ci, C, dwo, (Ci, 1, 0), prec=prec, db=dbo)
+        Wot, Kot = ctx.wo_t
+        do = torch.empty(B, T, Ci, device=dev, dtype=torch.float32)
+        _gemm(g, M, M, 1, 1, [0], C, Wot, Kot, Ci, do.view(M, Ci), M, prec=prec)
+        # attention backward -> d(q|k|v)
+        dqkv = _attn_bwd(do, qkv, bias, o, lse, heads, prec)
+        # stacked q|k|v projection: weight gradients (A = the bf16 / fp32 LayerNorm output), dgrad -> dn
+        dq2 = dqkv.view(M, C3)
+        dwqkv = torch.empty(C3, C, device=dev, dtype=torch.float32)
+        _wgrad(dq2, M, 1, 0, n, M, M, 1, 1, [0], C, C3, dwqkv, (C, 1, 0), prec=prec)
+        Wqt, Kqt = ctx.wqkv_t
+        dn = torch.empty(M, C, device=dev, dtype=torch.float32)
+        _gemm(dq2, M, M, 1, 1, [0], C3, Wqt, Kqt, C, dn, M, prec=prec)
+        dh, dlnw, dlnb = _ln_bwd_res(dn, h2, lnw, lnb, mean, rstd, dres)
+        dwq, dwk, dwv = (d.view(s_) for d, s_ in zip(dwqkv.split([s_[0] for s_ in qshapes], dim=0), qshapes))
+        return dh.reshape(shp), dlnw, dlnb, None, None, None, None, dwo, dbo, dwq, dwk, dwv
+
+
+class _PreLNFeedForwardTM(torch.autograd.Function):
+    """h + Linear2(Dropout(GELU(Linear1(LN3(h))))) -- BasicTransformerBlock.norm3 + FeedForward
+    (transformer.py:345-358, :105-188); GELU / dropout / residual in the GEMM epilogues, GELU' folded
+    into the second GEMM's dgrad epilogue."""
+
+    @staticmethod
+    def forward(ctx, h, ln_w, ln_b, eps, w1, b1, w2, b2, dropout_p):
+        _check(h, ln_w, w1, w2)
+        prec = gemm_precision()
+        shp = h.shape
+        h2 = _f32c(h).reshape(-1, shp[-1])
+        M, C = h2.shape
+        H = w1.shape[0]
+        lnw, lnb = _f32c(ln_w), _f32c(ln_b)
+        # fp32 LayerNorm output here: the GELU-epilogue GEMM and the weight gradient run faster on the
+        # register-staged schedules (fp32 A) than on the LDS-DMA ones (bf16 A) -- tools/preln_shapes.py
+        n, mean, rstd = _ln_fwd(h2, lnw, lnb, eps, False)
+        W1p, K1p = packed(spec_linear((w1,)), prec)
+        W2p, K2p = packed(spec_linear((w2,)), prec)
+        ctx.w2t = packed(spec_linear((w2,), dgrad=True), prec)
+        ctx.w1t = packed(spec_linear((w1,), dgrad=True), prec)
+        b16 = prec == PREC_BF16
+        z = torch.empty(M, H, device=h.device, dtype=torch.bfloat16 if b16 else torch.float32)  # pre-activation
+        hid = torch.empty(M, H, device=h.device, dtype=torch.bfloat16 if b16 else torch.float32)
+        seed = _new_seed(h.device) if dropout_p > 0 else None
+        _gemm(n, M, M, 1, 1, [0], C, W1p, K1p, H, hid, M, prec=prec, bias=_f32c(b1), act=ACT_GELU, C_pre=z,
+              dropout_p=dropout_p, seed=seed)
+        y = torch.empty(M, C, device=h.device, dtype=torch.float32)
+        _gemm(hid, M, M, 1, 1, [0], H, W2p, K2p, C, y, M, prec=prec, bias=_f32c(b2), residual=h2)
+        ctx.save_for_backward(h2, lnw, lnb, mean, rstd, n, z, hid)
+        ctx.leaf = _leaves(ln_w, ln_b, w1, b1, w2, b2)
+        ctx.cfg = (prec, shp, float(dropout_p), seed, w1.shape, w2.shape, b1 is not None, b2 is not None)
+        return y.reshape(shp)
+
+    @staticmethod
+    @_grad_sums
+    def backward(ctx, dy):
+        h2, lnw, lnb, mean, rstd, n, z, hid = ctx.saved_tensors
+        prec, shp, p, seed, w1s, w2s, has_b1, has_b2 = ctx.cfg
+        M, C = h2.shape
+        H = w1s[0]
+        dev = h2.device
+        dy2 = _f32c(dy).reshape(M, C)  # also the residual branch's gradient
+        dw2 = torch.empty(w2s, device=dev, dtype=torch.float32)
+        db2 = torch.empty(C, device=dev, dtype=torch.float32) if has_b2 else None
+        _wgrad(dy2, M, 1, 0, hid, M, M, 1, 1, [0], H, C, dw2, (H, 1, 0), prec=prec, db=db2)
+        W2t, K2p = ctx.w2t
+        # d(pre-activation): bf16 in bf16-mixed -- only the next dgrad GEMM and dW1 read it
+        dz = torch.empty(M, H, device=dev, dtype=torch.bfloat16 if prec == PREC_BF16 else torch.float32)
+        _gemm(dy2, M, M, 1, 1, [0], C, W2t, K2p, H, dz, M, prec=prec, act=ACT_DGELU, aux=z, dropout_p=p, seed=seed)
+        dw1 = torch.empty(w1s, device=dev, dtype=torch.float32)
+        db1 = torch.empty(H, device=dev, dtype=torch.float32) if has_b1 else None
+        _wgrad(dz, M, 1, 0, n, M, M, 1, 1, [0], C, H, dw1, (C, 1, 0), prec=prec, db=db1)
+        W1t, K1p = ctx.w1t
+        dn = torch.empty(M, C, device=dev, dtype=torch.float32)
+        _gemm(dz, M, M, 1, 1, [0], H, W1t, K1p, C, dn, M, prec=prec)
+        dh, dlnw, dlnb = _ln_bwd_res(dn, h2, lnw, lnb, mean, rstd, dy2)
+        return dh.reshape(shp), dlnw, dlnb, None, dw1, db1, dw2, db2, None
+
+
+def preln_attention_tm(h, ln_w, ln_b, eps, key_bias, heads, wq, wk, wv, w_out, b_out, dropout_p: float = 0.0):
+    """h + Dropout(to_out(SDPA(q, k, v, key bias))), q|k|v = LN(h) [Wq; Wk; Wv]^T (no bias), token-major."""
+    return _PreLNAttentionTM.apply(h, ln_w, ln_b, float(eps), key_bias, int(heads), float(dropout_p), w_out, b_out,
+                                   wq, wk, wv)
+
+
+def preln_ff_tm(h, ln_w, ln_b, eps, w1, b1, w2, b2, dropout_p: float = 0.0):
+    """h + W2 Dropout(GELU(W1 LN(h) + b1)) + b2, token-major."""
+    return _PreLNFeedForwardTM.apply(h, ln_w, ln_b, float(eps), w1, b1, w2, b2, float(dropout_p))
 
 
 class _RopeTM(torch.autograd.Function):

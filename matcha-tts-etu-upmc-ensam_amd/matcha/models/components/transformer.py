@@ -11,12 +11,16 @@ Token-major forward (``forward_tm``): the q/k/v projections run as ONE GEMM agai
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
 import torch.nn as nn
 
 from matcha.models.components import _ops as O
+
+# MTTS_PRELN_FUSED=0: BasicTransformerBlock.forward_tm runs op by op (A/B measurements)
+_PRELN_FUSED = os.environ.get("MTTS_PRELN_FUSED", "1") != "0"
 
 
 class GELU(nn.Module):
@@ -106,11 +110,22 @@ class BasicTransformerBlock(nn.Module):
         self.ff = FeedForward(dim, dropout=dropout, activation_fn=activation_fn, final_dropout=final_dropout)
 
     def forward_tm(self, h, key_bias):
-        """h [B, T, C]; key_bias [B, T] (the reference's float mask)."""
-        n = O.layer_norm_tm(h, self.norm1.weight, self.norm1.bias, self.norm1.eps)
-        h = self.attn1.forward_tm(n, key_bias, residual=h)
-        n = O.layer_norm_tm(h, self.norm3.weight, self.norm3.bias, self.norm3.eps)
-        return self.ff.forward_tm(n, residual=h)
+        """h [B, T, C]; key_bias [B, T] (the reference's float mask).  Each pre-LN residual sub-block is
+        one fused op (components/_ops.py preln_attention_tm / preln_ff_tm)."""
+        a, ff = self.attn1, self.ff
+        if not _PRELN_FUSED:  # op-by-op composition (A/B measurements)
+            n = O.layer_norm_tm(h, self.norm1.weight, self.norm1.bias, self.norm1.eps)
+            h = a.forward_tm(n, key_bias, residual=h)
+            n = O.layer_norm_tm(h, self.norm3.weight, self.norm3.bias, self.norm3.eps)
+            return ff.forward_tm(n, residual=h)
+        h = O.preln_attention_tm(h, self.norm1.weight, self.norm1.bias, self.norm1.eps, key_bias, a.heads,
+                                 a.to_q.weight, a.to_k.weight, a.to_v.weight, a.to_out[0].weight, a.to_out[0].bias,
+                                 dropout_p=a.to_out[1].p if self.training else 0.0)
+        if len(ff.net) > 3:
+            raise NotImplementedError("final_dropout is not used by the Matcha decoder")
+        return O.preln_ff_tm(h, self.norm3.weight, self.norm3.bias, self.norm3.eps, ff.net[0].proj.weight,
+                             ff.net[0].proj.bias, ff.net[2].weight, ff.net[2].bias,
+                             dropout_p=ff.net[1].p if self.training else 0.0)
 
     def forward(self, hidden_states, attention_mask=None, encoder_hidden_states=None,
                 encoder_attention_mask=None, timestep=None, cross_attention_kwargs=None, class_labels=None):

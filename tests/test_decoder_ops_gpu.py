@@ -409,3 +409,84 @@ def test_reduce_partials_jobs():
     for p, o, e, _ in cases:
         torch.testing.assert_close(o, e, rtol=1e-5, atol=1e-4)
     assert O is not None
+
+
+def _preln_inputs(B, T, C, heads, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    r = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).to(DEV).requires_grad_(True)
+    h = r(B, T, C)
+    ln_w, ln_b = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV).requires_grad_(True), r(C, sc=0.1)
+    wq, wk, wv = (r(C, C, sc=C ** -0.5) for _ in range(3))
+    wo, bo = r(C, C, sc=C ** -0.5), r(C, sc=0.1)
+    w1, b1 = r(4 * C, C, sc=C ** -0.5), r(4 * C, sc=0.1)
+    w2, b2 = r(C, 4 * C, sc=(4 * C) ** -0.5), r(C, sc=0.1)
+    key_bias = torch.zeros(B, T, device=DEV)
+    for b in range(B):
+        key_bias[b, : T - 7 * b] = 1  # the reference's float 0/1 mask, added to the scores
+    return h, ln_w, ln_b, wq, wk, wv, wo, bo, w1, b1, w2, b2, key_bias
+
+
+def _preln_ref(h, ln_w, ln_b, wq, wk, wv, wo, bo, w1, b1, w2, b2, key_bias, heads):
+    """BasicTransformerBlock (transformer.py:297-370) in plain torch fp32."""
+    B, T, C = h.shape
+    n = F.layer_norm(h, (C,), ln_w, ln_b, 1e-5)
+    sp = lambda t: t.view(B, T, heads, C // heads).transpose(1, 2)
+    o = F.scaled_dot_product_attention(sp(n @ wq.T), sp(n @ wk.T), sp(n @ wv.T), attn_mask=key_bias[:, None, None, :])
+    h = h + F.linear(o.transpose(1, 2).reshape(B, T, C), wo, bo)
+    n = F.layer_norm(h, (C,), ln_w, ln_b, 1e-5)
+    return h + F.linear(F.gelu(F.linear(n, w1, b1)), w2, b2)
+
+
+def _preln_fused(h, ln_w, ln_b, wq, wk, wv, wo, bo, w1, b1, w2, b2, key_bias, heads):
+    from matcha.models.components import _ops as O
+
+    h = O.preln_attention_tm(h, ln_w, ln_b, 1e-5, key_bias, heads, wq, wk, wv, wo, bo)
+    return O.preln_ff_tm(h, ln_w, ln_b, 1e-5, w1, b1, w2, b2)
+
+
+def _preln_unfused(h, ln_w, ln_b, wq, wk, wv, wo, bo, w1, b1, w2, b2, key_bias, heads):
+    from matcha.models.components import _ops as O
+
+    n = O.layer_norm_tm(h, ln_w, ln_b, 1e-5)
+    qkv = O.linear_tm(n, (wq, wk, wv), None)
+    h = O.linear_tm(O.attention_tm(qkv, key_bias, heads), wo, bo, residual=h)
+    n = O.layer_norm_tm(h, ln_w, ln_b, 1e-5)
+    return O.ff_tm(n, w1, b1, w2, b2, residual=h)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("B,T,C,heads", [(2, 150, 256, 4), (3, 37, 64, 2)])
+def test_preln_blocks_vs_torch(prec, B, T, C, heads):
+    """The fused pre-LN sub-blocks (LN output bf16 in bf16-mixed, residual gradient added in the LN
+    backward) against plain torch fp32."""
+    *ins, kb = _preln_inputs(B, T, C, heads)
+    _run(lambda *a: _preln_fused(*a, kb, heads), lambda *a: _preln_ref(*a, kb, heads), ins, prec)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_preln_blocks_match_unfused_ops(prec):
+    """Fusing changes where values live, not the arithmetic: bitwise equal to the op-by-op composition in
+    fp32 mode; in bf16-mixed mode the forward agrees to accumulation order (a bf16 A operand runs on the
+    LDS-DMA schedule, fp32 on the register-staged one: same products, another fp32 summation order) and
+    the gradients to bf16 rounding (the first FFN bias gradient now sums the bf16 d(pre-activation), as
+    autocast's would)."""
+    B, T, C, heads = 2, 150, 256, 4
+    *ins, kb = _preln_inputs(B, T, C, heads)
+    outs = []
+    for fn in (_preln_fused, _preln_unfused):
+        xs = [t.detach().clone().requires_grad_(True) for t in ins]
+        with _ctx(prec):
+            y = fn(*xs, kb, heads)
+        torch.manual_seed(1)
+        y.backward(torch.randn_like(y))
+        outs.append((y.detach(), [x.grad for x in xs]))
+    (y0, g0), (y1, g1) = outs
+    if prec == "fp32":
+        assert torch.equal(y0, y1)
+    else:
+        assert rel(y0, y1) < 1e-5, rel(y0, y1)
+    for i, (a, b) in enumerate(zip(g0, g1)):
+        if prec == "fp32":
+            assert torch.equal(a, b), i
+        else:
+            assert rel(a, b) < 1e-2, (i, rel(a, b))
