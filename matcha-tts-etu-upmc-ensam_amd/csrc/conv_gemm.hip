@@ -784,8 +784,22 @@ static int pick_cfg(const mtts_conv_gemm_args &p, int M, bool bf16) {
     if (!(sched_mask & 2) && mtts::conv_gemm_glds_applies(p) && p.K >= 768) {
         const int t = glds_tiles(p, M);
         if ((t >= 128 && t <= 256) || (t < 128 && p.K >= 1536 && p.N % 4 == 0)) return MTTS_GEMM_GLDS + 10;
+        // scalar-addressed LDS-DMA loop (whole-tap K steps): 64 x 64 two-stage tiles beat the register
+        // schedules on the 19200-row convs (tools/gemm_tall_sweep.py, profiles/r02/gemm_lean: 29.0 vs 29.7,
+        // 44.9 vs 48.5, 34.6 vs 38.3 us)
+        if (!(sched_mask & 8) && t > 256 && mtts::conv_gemm_glds_lean(p)) return MTTS_GEMM_GLDS + 13;
     }
+    if (!(sched_mask & 8) && p.K < 768 && p.N >= 512 && mtts::conv_gemm_glds_applies(p) && mtts::conv_gemm_glds_lean(p))
+        return MTTS_GEMM_GLDS + 9;  // the q|k|v projection, the encoder's 192 -> 768 conv: 35.1 vs 37.2 us
     return p.K >= 384 ? 12 : 7;
+}
+
+// bf16 A (LDS-DMA only): 64 x 256 two-stage tiles when they fill the chip, 64 x 64 three-stage below
+// (profiles/r02/gemm_lean: 19.0 vs 21.0 us on the 19200 x 256 x 768 conv, 23.4 vs 32.7 on the q|k|v
+// projection; 13.2 vs 13.4 on the 9600-row conv, 16.5 vs 25.5 on the encoder's 3840 x 192 x 2304)
+static int pick_cfg_a16(const mtts_conv_gemm_args &p, int M) {
+    if (p.act == MTTS_ACT_GELU || p.act == MTTS_ACT_DGELU) return MTTS_GEMM_GLDS + 12;
+    return glds_tiles(p, M) >= 256 ? MTTS_GEMM_GLDS + 9 : MTTS_GEMM_GLDS + 12;
 }
 
 // Split-K (LDS-DMA schedules, heuristic pick only): grids below half the chip with >= 24 K steps
@@ -847,11 +861,8 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
         if (!bf16 || !mtts::conv_gemm_glds_applies(p))
             return mtts::fail(MTTS_ERR_UNSUPPORTED,
                               "conv_gemm: a bf16 A needs bf16 precision, cin >= 64, cin / lda % 8 == 0, 0/1 a_scale");
-        if (cfg < 0) {  // 64 x 64 three-stage tiles unless the one-round 64 x 256 schedule applies (K >= 768,
-            // 128..256 tiles); tools/preln_shapes.py: the FFN dgrad from a bf16 d(pre-activation), 19200 x
-            // 256 x 1024, 24.8 us on 64 x 64 vs 33.5 on 64 x 256 two-stage
-            cfg = pick_cfg(p, M, bf16);
-            if (cfg < MTTS_GEMM_GLDS) cfg = MTTS_GEMM_GLDS + 12;
+        if (cfg < 0) {
+            cfg = pick_cfg_a16(p, M);
         } else if (cfg < MTTS_GEMM_GLDS) {
             return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: a bf16 A needs an LDS-DMA schedule");
         }

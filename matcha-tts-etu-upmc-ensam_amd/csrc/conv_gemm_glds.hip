@@ -23,6 +23,7 @@
 
 #include <cstdint>
 #include <type_traits>
+#include <utility>
 
 #include "gemm_epilogue.h"
 #include "mtts_common.h"
@@ -62,6 +63,36 @@ __device__ __forceinline__ void glds16(const void *src, void *lds_base) {
         : "memory");
 }
 
+// One buffer_load_dwordx4 ... lds: 16 bytes per lane from rsrc + voff + soff into LDS at lds_base + 16*lane.
+// A lane whose voff lies past the descriptor's num_records reads zeros (the masked / out-of-range rows:
+// MTTS_GLDS_OOB); the per-step advance lives in the scalar soff, so the K loop issues its loads with no
+// vector address arithmetic.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t MTTS_GLDS_OOB = 0x80000000u;
+
+__device__ __forceinline__ u32x4 make_rsrc(const void *base, uint32_t bytes) {
+    const uint64_t a = (uint64_t)(uintptr_t)base;
+    u32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    r.y = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    r.z = __builtin_amdgcn_readfirstlane(bytes);
+    r.w = 0x00020000u;
+    return r;
+}
+
+__device__ __forceinline__ void bload16(uint32_t voff, u32x4 rsrc, uint32_t soff, uint32_t lds) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+        : "memory");
+}
+
 // s_waitcnt vmcnt(N) (expcnt / lgkmcnt left at their maxima; gfx9 encoding: vmcnt[3:0] | [15:14])
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -82,7 +113,11 @@ struct GldsGeom {
 
 // ABF16: A is bf16 in HBM (MTTS_GEMM_F_A_BF16): 128-byte rows, the same image and swizzle as W, and
 // the fragment read needs no conversion.
-template <int WM, int WN, int TM, int TN, int STAGES, bool ABF16>
+// LEAN (cin % 64 == 0, so every K step lies inside one tap and K % 64 == 0; 32-bit byte offsets): the
+// operands are read through buffer descriptors, the K step advance is a scalar offset and only a tap
+// change touches per-lane state -- the register-addressed loop spent ~12 vector instructions per DMA
+// on pointer and tap bookkeeping (~26 VALU per MFMA on the 19200 x 256 x 768 conv, SQ counters).
+template <int WM, int WN, int TM, int TN, int STAGES, bool ABF16, bool LEAN>
 __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_gemm_args p, int ksteps, float *part) {
     using G = GldsGeom<WM, WN, TM, TN, STAGES, ABF16>;
     constexpr int ES = ABF16 ? 2 : 4;        // bytes per A element
@@ -107,6 +142,20 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
         if constexpr (decltype(S)::value == 0) return sW0;
         else if constexpr (decltype(S)::value == 1) return sW1;
         else return sW2;
+    };
+    // LDS byte addresses of the stage buffers, cast from the __shared__ objects themselves (a constant:
+    // no generic-pointer null check)
+    typedef __attribute__((address_space(3))) unsigned char lds_u8;
+    auto lds_addr = [](const lds_u8 *q) { return (uint32_t)(uintptr_t)q; };
+    auto abuf_l = [&](auto S) -> uint32_t {
+        if constexpr (decltype(S)::value == 0) return lds_addr((const lds_u8 *)sA0);
+        else if constexpr (decltype(S)::value == 1) return lds_addr((const lds_u8 *)sA1);
+        else return lds_addr((const lds_u8 *)sA2);
+    };
+    auto wbuf_l = [&](auto S) -> uint32_t {
+        if constexpr (decltype(S)::value == 0) return lds_addr((const lds_u8 *)sW0);
+        else if constexpr (decltype(S)::value == 1) return lds_addr((const lds_u8 *)sW1);
+        else return lds_addr((const lds_u8 *)sW2);
     };
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -178,9 +227,64 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
         w_ptr[i] = static_cast<const uint16_t *>(p.W) + (size_t)(w_nok[i] ? n0 + n : 0) * p.Kp + w_k[i];
     }
 
+    // ---- LEAN state: per chunk the tap-0 element index of its row and the byte offset of the current
+    // tap (MTTS_GLDS_OOB when that tap's row is absent or masked); scalar tap / channel-block counters
+    const int tapstride = offstep * p.lda;
+    int l_row[LEAN ? GA : 1];
+    uint32_t l_vo[LEAN ? GA : 1], l_vw[LEAN ? GW : 1];
+    int l_tap = 0, l_chs = 0;
+    uint32_t l_soa = 0, l_sow = 0;
+    u32x4 l_rsa, l_rsw;
+    if constexpr (LEAN) {
+        const int k0 = kstep0 * kBK;
+        l_tap = __builtin_amdgcn_readfirstlane(k0 / p.cin);
+        const int ch0 = k0 - l_tap * p.cin;
+        l_chs = __builtin_amdgcn_readfirstlane((p.cin - ch0) / kBK);
+        l_soa = __builtin_amdgcn_readfirstlane((uint32_t)(ch0 * ES));
+        l_sow = __builtin_amdgcn_readfirstlane((uint32_t)(k0 * 2));
+        l_rsa = make_rsrc(p.A, (uint32_t)((long long)p.nb * p.Ti * p.lda * ES));
+        l_rsw = make_rsrc(p.W, (uint32_t)((long long)p.N * p.Kp * 2));
+#pragma unroll
+        for (int i = 0; i < GA; ++i) {
+            const int r = RPI * (i * NW + wave) + lane / CPR;
+            const int lc = (lane % CPR) ^ (ABF16 ? ((r >> 1) & 7) : (r & 15));
+            int b = 0, u = 0;
+            mtts::divmod_fast(m0 + r < M ? m0 + r : 0, p.To, inv_to, b, u);
+            l_row[i] = (b * p.Ti + u * p.in_stride + off0) * p.lda + lc * EPC;
+            l_vo[i] = ((a_ok[i] >> min(l_tap, 31)) & 1u) ? (uint32_t)((l_row[i] + l_tap * tapstride) * ES) : MTTS_GLDS_OOB;
+        }
+#pragma unroll
+        for (int i = 0; i < GW; ++i) {
+            const int n = 8 * (i * NW + wave) + (lane >> 3);
+            const int lc = (lane & 7) ^ ((n >> 1) & 7);
+            l_vw[i] = w_nok[i] ? (uint32_t)(((n0 + n) * p.Kp + lc * 8) * 2) : MTTS_GLDS_OOB;
+        }
+    }
+
     auto issue = [&](auto S) {
         unsigned char *abase = abuf(S);
         unsigned char *wbase = wbuf(S);
+        if constexpr (LEAN) {
+            const uint32_t la = abuf_l(S), lw = wbuf_l(S);
+#pragma unroll
+            for (int i = 0; i < GA; ++i)
+                bload16(l_vo[i], l_rsa, l_soa, __builtin_amdgcn_readfirstlane(la + (i * NW + wave) * 1024));
+#pragma unroll
+            for (int i = 0; i < GW; ++i)
+                bload16(l_vw[i], l_rsw, l_sow, __builtin_amdgcn_readfirstlane(lw + (i * NW + wave) * 1024));
+            l_sow += kBK * 2;
+            l_soa += kBK * ES;
+            if (--l_chs == 0) {  // next tap (wave-uniform branch; nothing in flight depends on registers)
+                ++l_tap;
+                l_chs = p.cin / kBK;
+                l_soa = 0;
+#pragma unroll
+                for (int i = 0; i < GA; ++i)
+                    l_vo[i] = ((a_ok[i] >> min(l_tap, 31)) & 1u) ? (uint32_t)((l_row[i] + l_tap * tapstride) * ES)
+                                                                 : MTTS_GLDS_OOB;
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < GA; ++i) {
             const bool ok = (a_ok[i] >> min(a_j[i], 31)) & 1u;  // a_j >= ntaps (past K): bit is 0
@@ -312,32 +416,51 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(mtts_conv_gemm_arg
 
 struct GldsCfg {
     int wm, wn, tm, tn, stages;
+    bool f32a, bf16a;  // which A storages have an instantiation (LDS <= 160 KiB, registers)
 };
 constexpr GldsCfg kGlds[] = {
-    {1, 4, 2, 2, 2},  // 32: 64 x 256, 256 thr, 2 stages (96 KiB)
-    {1, 4, 2, 2, 3},  // 33: 64 x 256, 3 stages (144 KiB)
-    {2, 2, 2, 2, 2},  // 34: 128 x 128, 2 stages (96 KiB)
-    {2, 2, 2, 2, 3},  // 35: 128 x 128, 3 stages (144 KiB)
-    {1, 4, 1, 2, 2},  // 36: 32 x 256, 2 stages (80 KiB)
-    {1, 4, 1, 2, 3},  // 37: 32 x 256, 3 stages (120 KiB)
-    {2, 2, 1, 2, 2},  // 38: 64 x 128, 2 stages (64 KiB)
-    {2, 2, 1, 2, 3},  // 39: 64 x 128, 3 stages (96 KiB)
-    {1, 4, 1, 1, 3},  // 40: 32 x 128, 3 stages (72 KiB)
-    {2, 4, 1, 2, 2},  // 41: 64 x 256, 512 thr (waves 32 x 64), 2 stages (96 KiB)
-    {2, 4, 1, 2, 3},  // 42: 64 x 256, 512 thr, 3 stages (144 KiB)
-    {1, 2, 2, 2, 3},  // 43: 64 x 128, 128 thr (waves 64 x 64), 3 stages (96 KiB)
-    {2, 2, 1, 1, 3},  // 44: 64 x 64, 3 stages (72 KiB)
-    {2, 2, 1, 1, 2},  // 45: 64 x 64, 2 stages (48 KiB)
-    {2, 4, 2, 2, 2},  // 46: 128 x 256, 512 thr (waves 64 x 64), 2 stages (128 KiB)
-    {4, 2, 1, 2, 2},  // 47: 128 x 128, 512 thr (waves 32 x 64), 2 stages (96 KiB)
+    {1, 4, 2, 2, 2, true, false},   // 32: 64 x 256, 256 thr, 2 stages (96 KiB)
+    {1, 4, 2, 2, 3, false, false},  // 33: 64 x 256, 3 stages (144 KiB; fp32 A spills: 7x slower)
+    {2, 2, 2, 2, 2, true, false},   // 34: 128 x 128, 2 stages (96 KiB)
+    {2, 2, 2, 2, 3, false, false},  // 35: 128 x 128, 3 stages (144 KiB; fp32 A spills: 7x slower)
+    {1, 4, 1, 2, 2, true, false},   // 36: 32 x 256, 2 stages (80 KiB)
+    {1, 4, 1, 2, 3, true, false},   // 37: 32 x 256, 3 stages (120 KiB)
+    {2, 2, 1, 2, 2, true, false},   // 38: 64 x 128, 2 stages (64 KiB)
+    {2, 2, 1, 2, 3, true, false},   // 39: 64 x 128, 3 stages (96 KiB)
+    {1, 4, 1, 1, 3, true, false},   // 40: 32 x 128, 3 stages (72 KiB)
+    {2, 4, 1, 2, 2, true, true},    // 41: 64 x 256, 512 thr (waves 32 x 64), 2 stages (96 KiB)
+    {2, 4, 1, 2, 3, true, true},    // 42: 64 x 256, 512 thr, 3 stages (144 KiB)
+    {1, 2, 2, 2, 3, true, false},   // 43: 64 x 128, 128 thr (waves 64 x 64), 3 stages (96 KiB)
+    {2, 2, 1, 1, 3, true, true},    // 44: 64 x 64, 3 stages (72 KiB)
+    {2, 2, 1, 1, 2, true, false},   // 45: 64 x 64, 2 stages (48 KiB)
+    {2, 4, 2, 2, 2, true, true},    // 46: 128 x 256, 512 thr (waves 64 x 64), 2 stages (128 KiB)
+    {4, 2, 1, 2, 2, true, false},   // 47: 128 x 128, 512 thr (waves 32 x 64), 2 stages (96 KiB)
 };
 constexpr int kNumGlds = sizeof(kGlds) / sizeof(kGlds[0]);
+
+}  // namespace
+
+namespace mtts {
+// The LEAN loop needs whole-tap K steps and 32-bit byte offsets with room for MTTS_GLDS_OOB.
+bool conv_gemm_glds_lean(const mtts_conv_gemm_args &p) {
+    static const bool off = [] {
+        const char *e = getenv("MTTS_GLDS_LEAN");
+        return e && e[0] == '0';
+    }();
+    const int es = (p.flags & MTTS_GEMM_F_A_BF16) ? 2 : 4;
+    return !off && p.cin % kBK == 0 && (long long)p.nb * p.Ti * p.lda * es < (1ll << 31) &&
+           (long long)p.N * p.Kp * 2 < (1ll << 31);
+}
+}  // namespace mtts
+
+namespace {
 
 template <int C, bool ABF16>
 int launch_glds_t(const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
     constexpr GldsCfg c = kGlds[C];
     using G = GldsGeom<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16>;
-    auto kern = conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16>;
+    auto kern = mtts::conv_gemm_glds_lean(p) ? conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16, true>
+                                : conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16, false>;
     const int nk = (p.K + kBK - 1) / kBK;
     const int ksteps = (nk + splits - 1) / splits;
     const int S = splits > 1 ? (nk + ksteps - 1) / ksteps : 1;  // every split non-empty
@@ -351,15 +474,23 @@ int launch_glds_t(const mtts_conv_gemm_args &p, int M, int splits, float *part, 
     return mtts::check_launch("splitk_epilogue_kernel");
 }
 
-// bf16-A instantiations exist for the schedules the heuristic picks (64 x 256 two / three stages,
-// 64 x 64, 128 x 256); any other id with a bf16 A runs the 64 x 256 two-stage one
+// A schedule without an instantiation for the operand's storage runs the 64 x 256 two-stage one (41)
 template <int C>
 int launch_glds(const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
     if (p.flags & MTTS_GEMM_F_A_BF16) {
-        if constexpr (C == 9 || C == 10 || C == 12 || C == 14) return launch_glds_t<C, true>(p, M, splits, part, st);
+        if constexpr (kGlds[C].bf16a) return launch_glds_t<C, true>(p, M, splits, part, st);
         else return launch_glds_t<9, true>(p, M, splits, part, st);
     }
-    return launch_glds_t<C, false>(p, M, splits, part, st);
+    if constexpr (kGlds[C].f32a) return launch_glds_t<C, false>(p, M, splits, part, st);
+    else return launch_glds_t<9, false>(p, M, splits, part, st);
+}
+
+template <int... I>
+int launch_glds_id(int id, const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st,
+                   std::integer_sequence<int, I...>) {
+    int rc = MTTS_ERR_INVALID_ARG;
+    ((id == I ? (rc = launch_glds<I>(p, M, splits, part, st), true) : false) || ...);
+    return rc;
 }
 
 }  // namespace
@@ -388,24 +519,7 @@ size_t conv_gemm_glds_splitk_bytes(const mtts_conv_gemm_args &p, int splits) {
 }
 
 int conv_gemm_glds_launch(int id, const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
-    switch (id) {
-        case 0: return launch_glds<0>(p, M, splits, part, st);
-        case 1: return launch_glds<1>(p, M, splits, part, st);
-        case 2: return launch_glds<2>(p, M, splits, part, st);
-        case 3: return launch_glds<3>(p, M, splits, part, st);
-        case 4: return launch_glds<4>(p, M, splits, part, st);
-        case 5: return launch_glds<5>(p, M, splits, part, st);
-        case 6: return launch_glds<6>(p, M, splits, part, st);
-        case 7: return launch_glds<7>(p, M, splits, part, st);
-        case 8: return launch_glds<8>(p, M, splits, part, st);
-        case 9: return launch_glds<9>(p, M, splits, part, st);
-        case 10: return launch_glds<10>(p, M, splits, part, st);
-        case 11: return launch_glds<11>(p, M, splits, part, st);
-        case 12: return launch_glds<12>(p, M, splits, part, st);
-        case 13: return launch_glds<13>(p, M, splits, part, st);
-        case 14: return launch_glds<14>(p, M, splits, part, st);
-        default: return launch_glds<15>(p, M, splits, part, st);
-    }
+    return launch_glds_id(id, p, M, splits, part, st, std::make_integer_sequence<int, kNumGlds>{});
 }
 
 }  // namespace mtts

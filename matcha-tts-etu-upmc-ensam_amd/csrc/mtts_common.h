@@ -108,6 +108,7 @@ int conv_gemm_panel_launch(const mtts_conv_gemm_args &p, hipStream_t st);
 // conv_gemm_glds.hip: bf16 LDS-DMA schedules (ids MTTS_GEMM_GLDS + 0 .. num - 1)
 int conv_gemm_glds_num_cfgs();
 bool conv_gemm_glds_applies(const mtts_conv_gemm_args &p);
+bool conv_gemm_glds_lean(const mtts_conv_gemm_args &p);  // whole-tap K steps: scalar-addressed loop
 // splits > 1: split-K into `part` (conv_gemm_glds_splitk_bytes of workspace) + a combine/epilogue pass
 int conv_gemm_glds_launch(int id, const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st);
 size_t conv_gemm_glds_splitk_bytes(const mtts_conv_gemm_args &p, int splits);

@@ -15,6 +15,7 @@ SHAPES = {  # B, T, Cin, Cout, k
 name = sys.argv[1] if len(sys.argv) > 1 else "conv3_full_256"
 cfg = int(sys.argv[2]) if len(sys.argv) > 2 else -1
 iters = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+a16 = len(sys.argv) > 4 and sys.argv[4] == "bf16"  # A stored as bf16
 B, T, Cin, Cout, k = SHAPES[name]
 dev = torch.device("cuda")
 x = torch.randn(B, T, Cin, device=dev)
@@ -23,12 +24,14 @@ w = torch.randn(Cout, Cin, k, device=dev) / math.sqrt(Cin * k)
 Wp, Kp = O.pack_weight(w.permute(0, 2, 1).reshape(Cout, k * Cin), O.PREC_BF16)
 y = torch.empty(B, T, Cout, device=dev)
 offs = [j - k // 2 for j in range(k)]
+x32 = x
+x = x.to(torch.bfloat16) if a16 else x
 f = lambda: O._gemm(x, T, T, B, 1, offs, Cin, Wp, Kp, Cout, y, T, prec=O.PREC_BF16, a_scale=m, tile_cfg=cfg,
                   binary_scale=True)
 for _ in range(iters):
     f()
 torch.cuda.synchronize()
-ref = torch.nn.functional.conv1d(x.transpose(1, 2), w, padding=k // 2).transpose(1, 2)
+ref = torch.nn.functional.conv1d(x32.transpose(1, 2), w, padding=k // 2).transpose(1, 2)
 err = ((y - ref).norm() / ref.norm()).item()
 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 a.record()

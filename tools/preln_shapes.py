@@ -31,7 +31,7 @@ def t_ev(fn, iters=20):
 
 P = O.PREC_BF16
 seed = torch.tensor([12345, 678], dtype=torch.int32, device=dev)
-ONLY = sys.argv[1].split(",") if len(sys.argv) > 1 else None
+ONLY = sys.argv[1].split(",") if len(sys.argv) > 1 and __name__ == "__main__" else None
 
 
 def gemm_case(name, M, K, N, a16, c16=False, act=O.ACT_NONE, pre=False, aux=False, res=False, bias=True):
@@ -86,18 +86,19 @@ def wgrad_case(name, M, K, N, a16, y16):
                       "default_us": res[(-1, -1, -1)], "best": list(best), "best_us": res[best]}), flush=True)
 
 
-for M in (19200, 9600):
-    for a16 in (False, True):
-        if not ONLY or "gemm" in ONLY:
-            gemm_case("qkv", M, 256, 768, a16, bias=False)
-            gemm_case("ff1_gelu", M, 256, 1024, a16, c16=True, act=O.ACT_GELU, pre=True)
-            gemm_case("ff_dgrad_dz_dn", M, 1024, 256, a16, bias=False)
-        if not ONLY or "wgrad" in ONLY:
-            wgrad_case("dW_qkv", M, 256, 768, a16, False)
-            for y16 in (False, True):
-                wgrad_case("dW1", M, 256, 1024, a16, y16)
-    if not ONLY or "gemm" in ONLY:
-        for c16 in (False, True):  # dgelu producing dz fp32 / bf16
-            A = None
-            gemm_case("ff2_dgrad_dgelu_C" + ("16" if c16 else "32"), M, 256, 1024, False, c16=c16, act=O.ACT_DGELU,
-                      aux=True, bias=False)
+if __name__ == "__main__":
+  for M in (19200, 9600):
+      for a16 in (False, True):
+          if not ONLY or "gemm" in ONLY:
+              gemm_case("qkv", M, 256, 768, a16, bias=False)
+              gemm_case("ff1_gelu", M, 256, 1024, a16, c16=True, act=O.ACT_GELU, pre=True)
+              gemm_case("ff_dgrad_dz_dn", M, 1024, 256, a16, bias=False)
+          if not ONLY or "wgrad" in ONLY:
+              wgrad_case("dW_qkv", M, 256, 768, a16, False)
+              for y16 in (False, True):
+                  wgrad_case("dW1", M, 256, 1024, a16, y16)
+      if not ONLY or "gemm" in ONLY:
+          for c16 in (False, True):  # dgelu producing dz fp32 / bf16
+              A = None
+              gemm_case("ff2_dgrad_dgelu_C" + ("16" if c16 else "32"), M, 256, 1024, False, c16=c16, act=O.ACT_DGELU,
+                        aux=True, bias=False)
