@@ -152,6 +152,18 @@ int mtts_gn_mish_bwd(const float *dy, const float *h, const float *gamma, const 
                      const float *mean, const float *rstd, float *dh, float *dgamma, float *dbeta, float *dadd,
                      int32_t B, int32_t T, int32_t C, int32_t G, void *workspace, size_t workspace_bytes,
                      void *hip_stream);
+/* The same with the activation storage chosen by flags (bf16-mixed mode: the conv output h and the
+ * Block1D output y are only GEMM operands and GroupNorm inputs, stored as autocast holds them):
+ * forward MTTS_NORM_F_X_BF16 (h bf16) | MTTS_NORM_F_Y_BF16 (y bf16); backward MTTS_NORM_F_X_BF16 |
+ * MTTS_NORM_F_Y_BF16 (h and dh bf16) [| MTTS_NORM_F_DY_BF16 (dy bf16)], or 0.  Statistics and sums in
+ * fp32; bf16 values are widened exactly and the outputs rounded once. */
+int mtts_gn_mish_fwd_ex(const void *h, const float *gamma, const float *beta, const float *mask, const float *add,
+                        void *y, float *mean, float *rstd, int32_t B, int32_t T, int32_t C, int32_t G, float eps,
+                        int32_t flags, void *hip_stream);
+int mtts_gn_mish_bwd_ex(const void *dy, const void *h, const float *gamma, const float *beta, const float *mask,
+                        const float *mean, const float *rstd, void *dh, float *dgamma, float *dbeta, float *dadd,
+                        int32_t B, int32_t T, int32_t C, int32_t G, int32_t flags, void *workspace,
+                        size_t workspace_bytes, void *hip_stream);
 
 /*
  * Counter-based dropout (train mode, nn.Dropout semantics: keep with prob 1-p, scale 1/(1-p)).
@@ -172,6 +184,8 @@ int mtts_act_dropout_bwd(const float *dy, const float *y, float *dx, int32_t row
  * (text_encoder.py:48-55) and LN -> Dropout (:81-95).  act = MTTS_ACT_NONE, p = 0: plain LayerNorm.
  * act | MTTS_NORM_F_Y_BF16: y is written as bf16 (a GEMM operand in bf16-mixed mode, half the bytes). */
 #define MTTS_NORM_F_Y_BF16 0x100
+#define MTTS_NORM_F_X_BF16 0x200  /* GroupNorm: the input h (forward and backward) holds bf16           */
+#define MTTS_NORM_F_DY_BF16 0x400 /* GroupNorm backward: dy holds bf16 (with X_BF16 | Y_BF16)            */
 int mtts_layernorm_fwd(const float *x, const float *w, const float *b, float *y, float *mean, float *rstd,
                        int32_t M, int32_t C, float eps, int32_t act, float dropout_p, const uint32_t *seed,
                        void *hip_stream);

@@ -62,15 +62,43 @@ __device__ __forceinline__ float block_sum(float v, float *red) {
     return s;
 }
 
+// 4 consecutive elements of an fp32 or bf16 tensor (bf16 -> fp32 is exact), and the store back (one
+// rounding to bf16, v_cvt_pk_bf16_f32)
+template <typename T>
+__device__ __forceinline__ float4 ld4(const T *p) {
+    if constexpr (sizeof(T) == 4) {
+        return *reinterpret_cast<const float4 *>(p);
+    } else {
+        const uint2 q = *reinterpret_cast<const uint2 *>(p);
+        return make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                           __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void st4(T *p, float4 v) {
+    if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<float4 *>(p) = v;
+    } else {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        typedef __bf16 h2 __attribute__((ext_vector_type(2)));
+        const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){v.x, v.y}, h2));
+        const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){v.z, v.w}, h2));
+        *reinterpret_cast<uint2 *>(p) = make_uint2(lo, hi);
+    }
+}
+
 // GroupNorm kernels: one 16-wave workgroup per (batch, group), so the three streaming passes over
 // the group's T x C/G values keep enough loads in flight (256 workgroups fill the 256 CUs)
 constexpr int kGnThreads = 1024;
 
 // thread layout inside a group: cg/4 float4 columns, kThreads/(cg/4) token rows per pass
-__global__ __launch_bounds__(kGnThreads) void gn_mish_fwd_kernel(const float *__restrict__ h, const float *__restrict__ gamma,
+// TH / TY: storage of h / y (float, or uint16_t = bf16 bits: MTTS_NORM_F_X_BF16 / _Y_BF16)
+template <typename TH, typename TY>
+__global__ __launch_bounds__(kGnThreads) void gn_mish_fwd_kernel(const TH *__restrict__ h, const float *__restrict__ gamma,
                                                                const float *__restrict__ beta,
                                                                const float *__restrict__ mask,
-                                                               const float *__restrict__ add, float *__restrict__ y,
+                                                               const float *__restrict__ add, TY *__restrict__ y,
                                                                float *__restrict__ mean_out,
                                                                float *__restrict__ rstd_out, int T, int C, int G,
                                                                float eps) {
@@ -83,20 +111,20 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_fwd_kernel(const float *__
     const int col = tid % cols, r0 = tid / cols;
     const bool active = r0 < rows_per_pass;
     const int c0 = g * cg + col * 4;
-    const float *hb = h + (size_t)b * T * C + c0;
+    const TH *hb = h + (size_t)b * T * C + c0;
     const float n = (float)T * cg;
 
     float s = 0.f;
     if (active)
         for (int t = r0; t < T; t += rows_per_pass) {
-            const float4 v = *reinterpret_cast<const float4 *>(hb + (size_t)t * C);
+            const float4 v = ld4(hb + (size_t)t * C);
             s += (v.x + v.y) + (v.z + v.w);
         }
     const float mean = block_sum<kGnThreads>(s, red) / n;
     float q = 0.f;
     if (active)
         for (int t = r0; t < T; t += rows_per_pass) {
-            const float4 v = *reinterpret_cast<const float4 *>(hb + (size_t)t * C);
+            const float4 v = ld4(hb + (size_t)t * C);
             const float a = v.x - mean, bq = v.y - mean, cq = v.z - mean, d = v.w - mean;
             q += (a * a + bq * bq) + (cq * cq + d * d);
         }
@@ -111,27 +139,27 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_fwd_kernel(const float *__
     const float4 be = *reinterpret_cast<const float4 *>(beta + c0);
     float4 ad = make_float4(0.f, 0.f, 0.f, 0.f);
     if (add) ad = *reinterpret_cast<const float4 *>(add + (size_t)b * C + c0);
-    float *yb = y + (size_t)b * T * C + c0;
+    TY *yb = y + (size_t)b * T * C + c0;
     for (int t = r0; t < T; t += rows_per_pass) {
-        const float4 v = *reinterpret_cast<const float4 *>(hb + (size_t)t * C);
+        const float4 v = ld4(hb + (size_t)t * C);
         const float m = mask ? mask[(size_t)b * T + t] : 1.f;
         float4 o;
         o.x = mish_f((v.x - mean) * rstd * ga.x + be.x) * m + ad.x;
         o.y = mish_f((v.y - mean) * rstd * ga.y + be.y) * m + ad.y;
         o.z = mish_f((v.z - mean) * rstd * ga.z + be.z) * m + ad.z;
         o.w = mish_f((v.w - mean) * rstd * ga.w + be.w) * m + ad.w;
-        *reinterpret_cast<float4 *>(yb + (size_t)t * C) = o;
+        st4(yb + (size_t)t * C, o);
     }
 }
 
 // Register-resident variants (T <= P * rows_per_pass): the group's values are loaded ONCE into
 // registers -- one HBM read + one write per element instead of three / four streaming passes -- with
 // the same per-thread summation order as the streaming kernels.
-template <int P>
-__global__ __launch_bounds__(kGnThreads) void gn_mish_fwd_reg_kernel(const float *__restrict__ h, const float *__restrict__ gamma,
+template <int P, typename TH, typename TY>
+__global__ __launch_bounds__(kGnThreads) void gn_mish_fwd_reg_kernel(const TH *__restrict__ h, const float *__restrict__ gamma,
                                                                    const float *__restrict__ beta,
                                                                    const float *__restrict__ mask,
-                                                                   const float *__restrict__ add, float *__restrict__ y,
+                                                                   const float *__restrict__ add, TY *__restrict__ y,
                                                                    float *__restrict__ mean_out,
                                                                    float *__restrict__ rstd_out, int T, int C, int G,
                                                                    float eps) {
@@ -141,14 +169,14 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_fwd_reg_kernel(const float
     const int tid = threadIdx.x, col = tid % cols, r0 = tid / cols;
     const bool active = r0 < rpp;
     const int c0 = g * cg + col * 4;
-    const float *hb = h + (size_t)b * T * C + c0;
+    const TH *hb = h + (size_t)b * T * C + c0;
     const float n = (float)T * cg;
     float4 v[P];
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < P; ++k) {
         const int t = r0 + k * rpp;
-        v[k] = (active && t < T) ? *reinterpret_cast<const float4 *>(hb + (size_t)t * C) : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[k] = (active && t < T) ? ld4(hb + (size_t)t * C) : make_float4(0.f, 0.f, 0.f, 0.f);
         s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
     }
     const float mean = block_sum<kGnThreads>(s, red) / n;
@@ -170,7 +198,7 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_fwd_reg_kernel(const float
     const float4 be = *reinterpret_cast<const float4 *>(beta + c0);
     float4 ad = make_float4(0.f, 0.f, 0.f, 0.f);
     if (add) ad = *reinterpret_cast<const float4 *>(add + (size_t)b * C + c0);
-    float *yb = y + (size_t)b * T * C + c0;
+    TY *yb = y + (size_t)b * T * C + c0;
 #pragma unroll
     for (int k = 0; k < P; ++k) {
         const int t = r0 + k * rpp;
@@ -181,15 +209,16 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_fwd_reg_kernel(const float
         o.y = mish_f((v[k].y - mean) * rstd * ga.y + be.y) * m + ad.y;
         o.z = mish_f((v[k].z - mean) * rstd * ga.z + be.z) * m + ad.z;
         o.w = mish_f((v[k].w - mean) * rstd * ga.w + be.w) * m + ad.w;
-        *reinterpret_cast<float4 *>(yb + (size_t)t * C) = o;
+        st4(yb + (size_t)t * C, o);
     }
 }
 
-template <int P>
+// TD / TH / TO: storage of dy / h / dh (float or bf16 bits)
+template <int P, typename TD, typename TH, typename TO>
 __global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_reg_kernel(
-    const float *__restrict__ dy, const float *__restrict__ h, const float *__restrict__ gamma,
+    const TD *__restrict__ dy, const TH *__restrict__ h, const float *__restrict__ gamma,
     const float *__restrict__ beta, const float *__restrict__ mask, const float *__restrict__ mean_in,
-    const float *__restrict__ rstd_in, float *__restrict__ dh, float *__restrict__ pg, float *__restrict__ pb,
+    const float *__restrict__ rstd_in, TO *__restrict__ dh, float *__restrict__ pg, float *__restrict__ pb,
     float *__restrict__ dadd, int T, int C, int G) {
     __shared__ float red[kGnThreads / 64];
     __shared__ float4 chred[3][kGnThreads];
@@ -201,16 +230,16 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_reg_kernel(
     const float mean = mean_in[b * G + g], rstd = rstd_in[b * G + g];
     const float4 ga = *reinterpret_cast<const float4 *>(gamma + c0);
     const float4 be = *reinterpret_cast<const float4 *>(beta + c0);
-    const float *hb = h + (size_t)b * T * C + c0;
-    const float *db_ = dy + (size_t)b * T * C + c0;
+    const TH *hb = h + (size_t)b * T * C + c0;
+    const TD *db_ = dy + (size_t)b * T * C + c0;
     const float n = (float)T * cg;
     float4 v[P], gu[P];
 #pragma unroll
     for (int k = 0; k < P; ++k) {
         const int t = r0 + k * rpp;
         const bool ok = active && t < T;
-        v[k] = ok ? *reinterpret_cast<const float4 *>(hb + (size_t)t * C) : make_float4(0.f, 0.f, 0.f, 0.f);
-        gu[k] = ok ? *reinterpret_cast<const float4 *>(db_ + (size_t)t * C) : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[k] = ok ? ld4(hb + (size_t)t * C) : make_float4(0.f, 0.f, 0.f, 0.f);
+        gu[k] = ok ? ld4(db_ + (size_t)t * C) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     float s1 = 0.f, s2 = 0.f;
     float4 ag = make_float4(0, 0, 0, 0), ab = make_float4(0, 0, 0, 0), ad = make_float4(0, 0, 0, 0);
@@ -255,7 +284,7 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_reg_kernel(
         if (dadd) *reinterpret_cast<float4 *>(dadd + (size_t)b * C + cc) = sd;
     }
     if (!active) return;
-    float *dhb = dh + (size_t)b * T * C + c0;
+    TO *dhb = dh + (size_t)b * T * C + c0;
 #pragma unroll
     for (int k = 0; k < P; ++k) {
         const int t = r0 + k * rpp;
@@ -265,17 +294,18 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_reg_kernel(
         o.y = rstd * (gu[k].y * ga.y - m1 - (v[k].y - mean) * rstd * m2);
         o.z = rstd * (gu[k].z * ga.z - m1 - (v[k].z - mean) * rstd * m2);
         o.w = rstd * (gu[k].w * ga.w - m1 - (v[k].w - mean) * rstd * m2);
-        *reinterpret_cast<float4 *>(dhb + (size_t)t * C) = o;
+        st4(dhb + (size_t)t * C, o);
     }
 }
 
 // Backward.  Per element: u = xhat*gamma + beta, g_u = dy * mask * mish'(u), dxhat = g_u * gamma.
 // dh = rstd * (dxhat - mean(dxhat) - xhat * mean(dxhat * xhat)) over the (b, g) group.
 // Partial outputs per (b, c): pg[b,c] = sum_t g_u*xhat, pb[b,c] = sum_t g_u, dadd[b,c] = sum_t dy.
+template <typename TD, typename TH, typename TO>
 __global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_kernel(
-    const float *__restrict__ dy, const float *__restrict__ h, const float *__restrict__ gamma,
+    const TD *__restrict__ dy, const TH *__restrict__ h, const float *__restrict__ gamma,
     const float *__restrict__ beta, const float *__restrict__ mask, const float *__restrict__ mean_in,
-    const float *__restrict__ rstd_in, float *__restrict__ dh, float *__restrict__ pg, float *__restrict__ pb,
+    const float *__restrict__ rstd_in, TO *__restrict__ dh, float *__restrict__ pg, float *__restrict__ pb,
     float *__restrict__ dadd, int T, int C, int G) {
     __shared__ float red[kGnThreads / 64];
     __shared__ float4 chred[3][kGnThreads];
@@ -290,16 +320,16 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_kernel(
     const float mean = mean_in[b * G + g], rstd = rstd_in[b * G + g];
     const float4 ga = *reinterpret_cast<const float4 *>(gamma + c0);
     const float4 be = *reinterpret_cast<const float4 *>(beta + c0);
-    const float *hb = h + (size_t)b * T * C + c0;
-    const float *db_ = dy + (size_t)b * T * C + c0;
+    const TH *hb = h + (size_t)b * T * C + c0;
+    const TD *db_ = dy + (size_t)b * T * C + c0;
     const float n = (float)T * cg;
 
     float s1 = 0.f, s2 = 0.f;
     float4 ag = make_float4(0, 0, 0, 0), ab = make_float4(0, 0, 0, 0), ad = make_float4(0, 0, 0, 0);
     if (active)
         for (int t = r0; t < T; t += rows_per_pass) {
-            const float4 v = *reinterpret_cast<const float4 *>(hb + (size_t)t * C);
-            const float4 d = *reinterpret_cast<const float4 *>(db_ + (size_t)t * C);
+            const float4 v = ld4(hb + (size_t)t * C);
+            const float4 d = ld4(db_ + (size_t)t * C);
             const float m = mask ? mask[(size_t)b * T + t] : 1.f;
             float xh, gu;
 #define MTTS_GN_BWD_ACC(X, D, GA, BE, AG, AB, AD)          \
@@ -337,10 +367,10 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_kernel(
         if (dadd) *reinterpret_cast<float4 *>(dadd + (size_t)b * C + cc) = sd;
     }
     if (!active) return;
-    float *dhb = dh + (size_t)b * T * C + c0;
+    TO *dhb = dh + (size_t)b * T * C + c0;
     for (int t = r0; t < T; t += rows_per_pass) {
-        const float4 v = *reinterpret_cast<const float4 *>(hb + (size_t)t * C);
-        const float4 d = *reinterpret_cast<const float4 *>(db_ + (size_t)t * C);
+        const float4 v = ld4(hb + (size_t)t * C);
+        const float4 d = ld4(db_ + (size_t)t * C);
         const float m = mask ? mask[(size_t)b * T + t] : 1.f;
         float4 o;
         float xh, gu;
@@ -353,7 +383,7 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_kernel(
         MTTS_GN_BWD_OUT(v.z, d.z, ga.z, be.z, o.z)
         MTTS_GN_BWD_OUT(v.w, d.w, ga.w, be.w, o.w)
 #undef MTTS_GN_BWD_OUT
-        *reinterpret_cast<float4 *>(dhb + (size_t)t * C) = o;
+        st4(dhb + (size_t)t * C, o);
     }
 }
 
@@ -557,60 +587,113 @@ bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 
 }  // namespace
 
-extern "C" int mtts_gn_mish_fwd(const float *h, const float *gamma, const float *beta, const float *mask,
-                                const float *add, float *y, float *mean, float *rstd, int32_t B, int32_t T,
-                                int32_t C, int32_t G, float eps, void *hip_stream) {
+template <typename TH, typename TY>
+static void gn_fwd_launch(const void *h, const float *gamma, const float *beta, const float *mask, const float *add,
+                          void *y, float *mean, float *rstd, int B, int T, int C, int G, float eps, hipStream_t st) {
+    const TH *hh = static_cast<const TH *>(h);
+    TY *yy = static_cast<TY *>(y);
+    const int passes = (T + kGnThreads / (C / G / 4) - 1) / (kGnThreads / (C / G / 4));
+    if (passes <= 4)
+        hipLaunchKernelGGL((gn_mish_fwd_reg_kernel<4, TH, TY>), dim3(G, B), dim3(kGnThreads), 0, st, hh, gamma, beta,
+                           mask, add, yy, mean, rstd, T, C, G, eps);
+    else if (passes <= 8)
+        hipLaunchKernelGGL((gn_mish_fwd_reg_kernel<8, TH, TY>), dim3(G, B), dim3(kGnThreads), 0, st, hh, gamma, beta,
+                           mask, add, yy, mean, rstd, T, C, G, eps);
+    else
+        hipLaunchKernelGGL((gn_mish_fwd_kernel<TH, TY>), dim3(G, B), dim3(kGnThreads), 0, st, hh, gamma, beta, mask, add,
+                           yy, mean, rstd, T, C, G, eps);
+}
+
+extern "C" int mtts_gn_mish_fwd_ex(const void *h, const float *gamma, const float *beta, const float *mask,
+                                   const float *add, void *y, float *mean, float *rstd, int32_t B, int32_t T,
+                                   int32_t C, int32_t G, float eps, int32_t flags, void *hip_stream) {
     MTTS_CHECK_ARG(h && gamma && beta && y && mean && rstd, "gn_mish_fwd: null pointer");
     MTTS_CHECK_ARG(B >= 0 && T >= 1 && G >= 1 && C % G == 0 && (C / G) % 4 == 0 && C / G <= 4 * kGnThreads,
                    "gn_mish_fwd: need C % G == 0 and (C/G) % 4 == 0");
+    MTTS_CHECK_ARG(!(flags & ~(MTTS_NORM_F_X_BF16 | MTTS_NORM_F_Y_BF16)), "gn_mish_fwd: unknown flag");
     MTTS_CHECK_ARG(aligned16(h) && aligned16(y) && aligned16(gamma) && aligned16(beta) && (!add || aligned16(add)),
                    "gn_mish_fwd: tensors must be 16-byte aligned");
     if (B == 0) return MTTS_OK;
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
-    const int passes = (T + kGnThreads / (C / G / 4) - 1) / (kGnThreads / (C / G / 4));
-    if (passes <= 4)
-        hipLaunchKernelGGL(gn_mish_fwd_reg_kernel<4>, dim3(G, B), dim3(kGnThreads), 0, st, h, gamma, beta, mask, add, y,
-                           mean, rstd, T, C, G, eps);
-    else if (passes <= 8)
-        hipLaunchKernelGGL(gn_mish_fwd_reg_kernel<8>, dim3(G, B), dim3(kGnThreads), 0, st, h, gamma, beta, mask, add, y,
-                           mean, rstd, T, C, G, eps);
-    else
-        hipLaunchKernelGGL(gn_mish_fwd_kernel, dim3(G, B), dim3(kGnThreads), 0, st, h, gamma, beta, mask, add, y, mean,
-                           rstd, T, C, G, eps);
+    const bool x16 = flags & MTTS_NORM_F_X_BF16, y16 = flags & MTTS_NORM_F_Y_BF16;
+    if (x16 && y16) gn_fwd_launch<uint16_t, uint16_t>(h, gamma, beta, mask, add, y, mean, rstd, B, T, C, G, eps, st);
+    else if (x16) gn_fwd_launch<uint16_t, float>(h, gamma, beta, mask, add, y, mean, rstd, B, T, C, G, eps, st);
+    else if (y16) gn_fwd_launch<float, uint16_t>(h, gamma, beta, mask, add, y, mean, rstd, B, T, C, G, eps, st);
+    else gn_fwd_launch<float, float>(h, gamma, beta, mask, add, y, mean, rstd, B, T, C, G, eps, st);
     return mtts::check_launch("gn_mish_fwd_kernel");
+}
+
+extern "C" int mtts_gn_mish_fwd(const float *h, const float *gamma, const float *beta, const float *mask,
+                                const float *add, float *y, float *mean, float *rstd, int32_t B, int32_t T,
+                                int32_t C, int32_t G, float eps, void *hip_stream) {
+    return mtts_gn_mish_fwd_ex(h, gamma, beta, mask, add, y, mean, rstd, B, T, C, G, eps, 0, hip_stream);
 }
 
 extern "C" size_t mtts_gn_mish_bwd_workspace_size(int32_t B, int32_t C) {
     return (size_t)2 * (B > 0 ? B : 0) * (C > 0 ? C : 0) * sizeof(float);
 }
 
-extern "C" int mtts_gn_mish_bwd(const float *dy, const float *h, const float *gamma, const float *beta,
-                                const float *mask, const float *mean, const float *rstd, float *dh, float *dgamma,
-                                float *dbeta, float *dadd, int32_t B, int32_t T, int32_t C, int32_t G,
-                                void *workspace, size_t workspace_bytes, void *hip_stream) {
+template <typename TD, typename TH, typename TO>
+static void gn_bwd_launch(const void *dy, const void *h, const float *gamma, const float *beta, const float *mask,
+                          const float *mean, const float *rstd, void *dh, float *pg, float *pb, float *dadd, int B,
+                          int T, int C, int G, hipStream_t st) {
+    const TD *d = static_cast<const TD *>(dy);
+    const TH *hh = static_cast<const TH *>(h);
+    TO *o = static_cast<TO *>(dh);
+    const int passes = (T + kGnThreads / (C / G / 4) - 1) / (kGnThreads / (C / G / 4));
+    if (passes <= 4)
+        hipLaunchKernelGGL((gn_mish_bwd_reg_kernel<4, TD, TH, TO>), dim3(G, B), dim3(kGnThreads), 0, st, d, hh, gamma,
+                           beta, mask, mean, rstd, o, pg, pb, dadd, T, C, G);
+    else if (passes <= 6)  // (8 spills at 1024 threads)
+        hipLaunchKernelGGL((gn_mish_bwd_reg_kernel<6, TD, TH, TO>), dim3(G, B), dim3(kGnThreads), 0, st, d, hh, gamma,
+                           beta, mask, mean, rstd, o, pg, pb, dadd, T, C, G);
+    else
+        hipLaunchKernelGGL((gn_mish_bwd_kernel<TD, TH, TO>), dim3(G, B), dim3(kGnThreads), 0, st, d, hh, gamma, beta,
+                           mask, mean, rstd, o, pg, pb, dadd, T, C, G);
+}
+
+extern "C" int mtts_gn_mish_bwd_ex(const void *dy, const void *h, const float *gamma, const float *beta,
+                                   const float *mask, const float *mean, const float *rstd, void *dh, float *dgamma,
+                                   float *dbeta, float *dadd, int32_t B, int32_t T, int32_t C, int32_t G,
+                                   int32_t flags, void *workspace, size_t workspace_bytes, void *hip_stream) {
     MTTS_CHECK_ARG(dy && h && gamma && beta && mean && rstd && dh, "gn_mish_bwd: null pointer");
     MTTS_CHECK_ARG(B >= 0 && T >= 1 && G >= 1 && C % G == 0 && (C / G) % 4 == 0, "gn_mish_bwd: bad shape");
     MTTS_CHECK_ARG(aligned16(dy) && aligned16(h) && aligned16(dh) && (!dadd || aligned16(dadd)),
                    "gn_mish_bwd: tensors must be 16-byte aligned");
+    const int known = MTTS_NORM_F_X_BF16 | MTTS_NORM_F_Y_BF16 | MTTS_NORM_F_DY_BF16;
+    MTTS_CHECK_ARG(!(flags & ~known), "gn_mish_bwd: unknown flag");
     if (B == 0) return MTTS_OK;
     if (!workspace || workspace_bytes < mtts_gn_mish_bwd_workspace_size(B, C))
         return mtts::fail(MTTS_ERR_WORKSPACE, "gn_mish_bwd: workspace too small");
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
     float *pg = static_cast<float *>(workspace);
     float *pb = pg + (size_t)B * C;
-    const int passes = (T + kGnThreads / (C / G / 4) - 1) / (kGnThreads / (C / G / 4));
-    if (passes <= 4)
-        hipLaunchKernelGGL(gn_mish_bwd_reg_kernel<4>, dim3(G, B), dim3(kGnThreads), 0, st, dy, h, gamma, beta, mask, mean,
-                           rstd, dh, pg, pb, dadd, T, C, G);
-    else if (passes <= 6)  // (8 spills at 1024 threads)
-        hipLaunchKernelGGL(gn_mish_bwd_reg_kernel<6>, dim3(G, B), dim3(kGnThreads), 0, st, dy, h, gamma, beta, mask, mean,
-                           rstd, dh, pg, pb, dadd, T, C, G);
-    else
-        hipLaunchKernelGGL(gn_mish_bwd_kernel, dim3(G, B), dim3(kGnThreads), 0, st, dy, h, gamma, beta, mask, mean, rstd,
-                           dh, pg, pb, dadd, T, C, G);
+    // the storage combinations the decoder runs: all fp32 (32-true); bf16 h and dh with fp32 or bf16 dy
+    switch (flags) {
+        case 0:
+            gn_bwd_launch<float, float, float>(dy, h, gamma, beta, mask, mean, rstd, dh, pg, pb, dadd, B, T, C, G, st);
+            break;
+        case MTTS_NORM_F_X_BF16 | MTTS_NORM_F_Y_BF16:
+            gn_bwd_launch<float, uint16_t, uint16_t>(dy, h, gamma, beta, mask, mean, rstd, dh, pg, pb, dadd, B, T, C, G, st);
+            break;
+        case MTTS_NORM_F_X_BF16 | MTTS_NORM_F_Y_BF16 | MTTS_NORM_F_DY_BF16:
+            gn_bwd_launch<uint16_t, uint16_t, uint16_t>(dy, h, gamma, beta, mask, mean, rstd, dh, pg, pb, dadd, B, T, C,
+                                                        G, st);
+            break;
+        default:
+            return mtts::fail(MTTS_ERR_UNSUPPORTED, "gn_mish_bwd: unsupported storage combination");
+    }
     int rc = mtts::check_launch("gn_mish_bwd_kernel");
     if (rc) return rc;
     return submit_param_sums(pg, dgamma, pb, dbeta, B, C, st);
+}
+
+extern "C" int mtts_gn_mish_bwd(const float *dy, const float *h, const float *gamma, const float *beta,
+                                const float *mask, const float *mean, const float *rstd, float *dh, float *dgamma,
+                                float *dbeta, float *dadd, int32_t B, int32_t T, int32_t C, int32_t G,
+                                void *workspace, size_t workspace_bytes, void *hip_stream) {
+    return mtts_gn_mish_bwd_ex(dy, h, gamma, beta, mask, mean, rstd, dh, dgamma, dbeta, dadd, B, T, C, G, 0, workspace,
+                               workspace_bytes, hip_stream);
 }
 
 extern "C" int mtts_layernorm_fwd(const float *x, const float *w, const float *b, float *y, float *mean,

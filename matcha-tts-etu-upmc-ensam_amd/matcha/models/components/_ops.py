@@ -114,6 +114,10 @@ N.register("mtts_gn_mish_fwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I
 N.register("mtts_gn_mish_bwd_workspace_size", _SZ, [_I, _I])
 N.register("mtts_gn_mish_bwd", ctypes.c_int,
            [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _SZ, _P])
+N.register("mtts_gn_mish_fwd_ex", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _P])
+N.register("mtts_gn_mish_bwd_ex", ctypes.c_int,
+           [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P])
+NORM_F_X_BF16, NORM_F_DY_BF16 = 0x200, 0x400  # include/mtts_decoder.h
 N.register("mtts_layernorm_fwd", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I, _I, _F, _I, _F, _P, _P])
 N.register("mtts_layernorm_bwd_workspace_size", _SZ, [_I, _I])
 N.register("mtts_layernorm_bwd", ctypes.c_int,
@@ -150,6 +154,19 @@ def _f32c(t: torch.Tensor | None) -> torch.Tensor | None:
     if t.dtype != torch.float32:
         t = t.float()
     return t.contiguous()
+
+
+def _actc(t: torch.Tensor | None, prec: int) -> torch.Tensor | None:
+    """An activation as the kernels take it: bf16 stays bf16 in bf16-mixed mode (a GEMM A operand /
+    GroupNorm input stored as autocast would hold it), anything else becomes contiguous fp32."""
+    if t is not None and t.dtype == torch.bfloat16 and prec == PREC_BF16:
+        return t.contiguous()
+    return _f32c(t)
+
+
+def _bf16_operand_ok(c: int) -> bool:
+    """A bf16 A operand needs the LDS-DMA schedules: >= 64 channels, rows of whole 16-byte chunks."""
+    return c >= 64 and c % 8 == 0
 
 
 _SEED_SCOPE: contextvars.ContextVar = contextvars.ContextVar("mtts_seed_scope", default=None)
@@ -539,13 +556,15 @@ class _ConvTM(torch.autograd.Function):
     (nn.Conv1d on x*mask, token-major; act None or ReLU; residual only without act/dropout)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, mask, out_scale, stride, padding, act, dropout_p, residual):
+    def forward(ctx, x, weight, bias, mask, out_scale, stride, padding, act, dropout_p, residual, out_bf16):
         _check(x, weight, mask, residual)
         assert residual is None or (act == ACT_NONE and dropout_p == 0.0)
         prec = gemm_precision()
-        x = _f32c(x)
+        x = _actc(x, prec)
         B, Ti, Cin = x.shape
         Cout, _, k = weight.shape
+        if x.dtype == torch.bfloat16 and not _bf16_operand_ok(Cin):
+            x = x.float()
         To = (Ti + 2 * padding - k) // stride + 1
         Wp, Kp = packed(spec_conv_fwd(weight), prec)
         # the backward's dgrad operands come from the same packing pass (weight_pack_scope)
@@ -554,7 +573,10 @@ class _ConvTM(torch.autograd.Function):
             ctx.wd = [packed(spec_conv_dgrad(weight), prec)] if stride == 1 else \
                 [packed(spec_conv_dgrad(weight, (ph + padding) % stride, stride), prec)
                  if len(range((ph + padding) % stride, k, stride)) else None for ph in range(stride)]
-        y = torch.empty(B, To, Cout, device=x.device, dtype=torch.float32)
+        # bf16 output (bf16-mixed, out_bf16): GroupNorm input / next GEMM operand; its gradient then comes
+        # back as bf16 too, and is the dgrad GEMM's bf16 A operand
+        y16 = out_bf16 and prec == PREC_BF16 and _bf16_operand_ok(Cout) and act == ACT_NONE and dropout_p == 0.0
+        y = torch.empty(B, To, Cout, device=x.device, dtype=torch.bfloat16 if y16 else torch.float32)
         mask = _f32c(mask)
         out_scale = _f32c(out_scale)
         bias_c = _f32c(bias)
@@ -572,7 +594,10 @@ class _ConvTM(torch.autograd.Function):
     def backward(ctx, dy):
         x, weight, mask, out_scale, y = ctx.saved_tensors
         stride, pad, prec, has_bias, act, p, seed, has_res = ctx.cfg
-        dy = _f32c(dy)
+        dy = _actc(dy, prec)
+        if dy.dtype == torch.bfloat16 and (out_scale is not None or act != ACT_NONE or p > 0
+                                           or not _bf16_operand_ok(dy.shape[-1])):
+            dy = dy.float()
         if out_scale is not None:
             dy = dy * out_scale.unsqueeze(-1)
         dres = dy if has_res else None
@@ -587,7 +612,7 @@ class _ConvTM(torch.autograd.Function):
         To = dy.shape[1]
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x)
+            dx = torch.empty_like(x)  # in x's storage: a bf16 x (a GroupNorm output) gets a bf16 gradient
             if stride == 1:
                 Wd, Kp = ctx.wd[0]
                 _gemm(dy, To, Ti, B, 1, [pad - j for j in range(k)], Cout, Wd, Kp, Cin, dx, Ti, prec=prec,
@@ -608,7 +633,7 @@ class _ConvTM(torch.autograd.Function):
             db = torch.empty(Cout, device=x.device, dtype=torch.float32) if has_bias else None
             _wgrad(dy, To, 1, 0, x, Ti, To, B, stride, [j - pad for j in range(k)], Cin, Cout, dw,
                    (Cin * k, k, 1), prec=prec, a_scale=mask, db=db)
-        return dx, dw, db, None, None, None, None, None, None, dres
+        return dx, dw, db, None, None, None, None, None, None, dres, None
 
 
 class _ConvTransposeTM(torch.autograd.Function):
@@ -878,18 +903,24 @@ def conv_ffn_tm(x, w1, b1, w2, b2, mask, residual=None, p_in: float = 0.0, p_out
 
 # ------------------------------------------------------------------------------------------ norms
 class _GroupNormMishTM(torch.autograd.Function):
+    """mish(GN(h)) * mask + add; in bf16-mixed mode h may be bf16 (a conv GEMM's bf16 output) and y is
+    written as bf16 when asked (it only feeds the next conv's GEMM); dh comes back in h's storage."""
+
     @staticmethod
-    def forward(ctx, h, gamma, beta, mask, add, groups, eps):
+    def forward(ctx, h, gamma, beta, mask, add, groups, eps, out_bf16):
         _check(h, gamma, mask, add)
-        h = _f32c(h)
+        prec = gemm_precision()
+        h = _actc(h, prec)
         B, T, C = h.shape
-        y = torch.empty_like(h)
+        y16 = out_bf16 and prec == PREC_BF16
+        y = torch.empty(B, T, C, device=h.device, dtype=torch.bfloat16 if y16 else torch.float32)
         mean = torch.empty(B, groups, device=h.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
         gamma_c, beta_c, mask_c, add_c = _f32c(gamma), _f32c(beta), _f32c(mask), _f32c(add)
-        N.check(N.lib().mtts_gn_mish_fwd(h.data_ptr(), gamma_c.data_ptr(), beta_c.data_ptr(), N.ptr(mask_c),
-                                         N.ptr(add_c), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), B, T, C,
-                                         groups, float(eps), _stream(h)), "mtts_gn_mish_fwd")
+        flags = (NORM_F_X_BF16 if h.dtype == torch.bfloat16 else 0) | (NORM_F_Y_BF16 if y16 else 0)
+        N.check(N.lib().mtts_gn_mish_fwd_ex(h.data_ptr(), gamma_c.data_ptr(), beta_c.data_ptr(), N.ptr(mask_c),
+                                            N.ptr(add_c), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), B, T, C,
+                                            groups, float(eps), flags, _stream(h)), "mtts_gn_mish_fwd")
         ctx.save_for_backward(h, gamma_c, beta_c, mask_c, mean, rstd)
         ctx.leaf = _leaves(gamma, beta)
         ctx.cfg = (groups, add is not None)
@@ -900,20 +931,22 @@ class _GroupNormMishTM(torch.autograd.Function):
     def backward(ctx, dy):
         h, gamma, beta, mask, mean, rstd = ctx.saved_tensors
         groups, has_add = ctx.cfg
-        dy = _f32c(dy)
+        h16 = h.dtype == torch.bfloat16
+        dy = dy.contiguous() if (h16 and dy.dtype == torch.bfloat16) else _f32c(dy)
         B, T, C = h.shape
         dh = torch.empty_like(h)
         dg = torch.empty(C, device=h.device, dtype=torch.float32)
         dbt = torch.empty_like(dg)
         dadd = torch.empty(B, C, device=h.device, dtype=torch.float32) if has_add else None
+        flags = (NORM_F_X_BF16 | NORM_F_Y_BF16 if h16 else 0) | (NORM_F_DY_BF16 if dy.dtype == torch.bfloat16 else 0)
         lib = N.lib()
         ws = torch.empty(int(lib.mtts_gn_mish_bwd_workspace_size(B, C)), dtype=torch.uint8, device=h.device)
         _keep_partials(ws)
-        N.check(lib.mtts_gn_mish_bwd(dy.data_ptr(), h.data_ptr(), gamma.data_ptr(), beta.data_ptr(), N.ptr(mask),
-                                     mean.data_ptr(), rstd.data_ptr(), dh.data_ptr(), dg.data_ptr(), dbt.data_ptr(),
-                                     N.ptr(dadd), B, T, C, groups, ws.data_ptr(), ws.numel(), _stream(h)),
+        N.check(lib.mtts_gn_mish_bwd_ex(dy.data_ptr(), h.data_ptr(), gamma.data_ptr(), beta.data_ptr(), N.ptr(mask),
+                                        mean.data_ptr(), rstd.data_ptr(), dh.data_ptr(), dg.data_ptr(), dbt.data_ptr(),
+                                        N.ptr(dadd), B, T, C, groups, flags, ws.data_ptr(), ws.numel(), _stream(h)),
                 "mtts_gn_mish_bwd")
-        return dh, dg, dbt, None, dadd, None, None
+        return dh, dg, dbt, None, dadd, None, None, None
 
 
 class _LayerNormTM(torch.autograd.Function):
@@ -961,14 +994,14 @@ class _LayerNormTM(torch.autograd.Function):
 
 # ------------------------------------------------------------------------------------------ public ops
 def conv_tm(x, weight, bias, mask=None, stride: int = 1, padding: int | None = None, out_scale=None,
-            relu: bool = False, dropout_p: float = 0.0, residual=None):
+            relu: bool = False, dropout_p: float = 0.0, residual=None, out_bf16: bool = False):
     """y = (residual + dropout(relu(Conv1d(x * mask)))) * out_scale, token-major.  x [B,T,Cin], weight
     [Cout,Cin,k] (nn.Conv1d layout, k <= 8), mask/out_scale [B,T] or None.
     decoder.py:59,65,78,85,95,192,239,248,251,369-371; text_encoder.py:48-57, 81-96."""
     if padding is None:
         padding = weight.shape[-1] // 2
     return _ConvTM.apply(x, weight, bias, mask, out_scale, stride, padding, ACT_RELU if relu else ACT_NONE,
-                         float(dropout_p), residual)
+                         float(dropout_p), residual, bool(out_bf16))
 
 
 def conv_transpose_tm(x, weight, bias, mask=None):
@@ -976,10 +1009,11 @@ def conv_transpose_tm(x, weight, bias, mask=None):
     return _ConvTransposeTM.apply(x, weight, bias, mask)
 
 
-def group_norm_mish_tm(h, gamma, beta, groups: int, mask=None, add=None, eps: float = 1e-5):
+def group_norm_mish_tm(h, gamma, beta, groups: int, mask=None, add=None, eps: float = 1e-5, out_bf16: bool = False):
     """mish(GroupNorm(h)) * mask (+ add[b, c]): Block1D tail (decoder.py:58-66) with Resnet1D's
-    time-embedding add (decoder.py:82-83) fused; statistics over the full padded length."""
-    return _GroupNormMishTM.apply(h, gamma, beta, mask, add, groups, eps)
+    time-embedding add (decoder.py:82-83) fused; statistics over the full padded length.  out_bf16: in
+    bf16-mixed mode, store the result as bf16 (when its only consumer is a conv GEMM)."""
+    return _GroupNormMishTM.apply(h, gamma, beta, mask, add, groups, eps, bool(out_bf16))
 
 
 def layer_norm_tm(h, weight, bias, eps: float = 1e-5, relu: bool = False, dropout_p: float = 0.0):

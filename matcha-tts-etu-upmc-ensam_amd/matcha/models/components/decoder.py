@@ -67,10 +67,12 @@ class Block1D(nn.Module):
             nn.Mish(),
         )
 
-    def forward_tm(self, x, mask, add=None):
+    def forward_tm(self, x, mask, add=None, out_bf16=False):
+        """bf16-mixed: the conv output (read only by the GroupNorm) is stored as bf16, and so is the
+        result when out_bf16 (its only consumer is the next conv's GEMM) -- as autocast would hold them."""
         conv, gn = self.block[0], self.block[1]
-        h = O.conv_tm(x, conv.weight, conv.bias, mask, padding=conv.padding[0])
-        return O.group_norm_mish_tm(h, gn.weight, gn.bias, gn.num_groups, mask, add, gn.eps)
+        h = O.conv_tm(x, conv.weight, conv.bias, mask, padding=conv.padding[0], out_bf16=True)
+        return O.group_norm_mish_tm(h, gn.weight, gn.bias, gn.num_groups, mask, add, gn.eps, out_bf16=out_bf16)
 
     def forward(self, x, mask):  # channel-major API of the reference
         return self.forward_tm(x.transpose(1, 2), mask[:, 0]).transpose(1, 2)
@@ -91,8 +93,8 @@ class Resnet1D(nn.Module):
         if tproj is None:
             with torch.autocast("cuda", enabled=False):  # [B, C] time projection, fp32
                 tproj = self.mlp(time_emb.float())
-        h = self.block1.forward_tm(x, mask, add=tproj)
-        h = self.block2.forward_tm(h, mask)
+        h = self.block1.forward_tm(x, mask, add=tproj, out_bf16=True)
+        h = self.block2.forward_tm(h, mask)  # fp32: the residual of res_conv's epilogue
         # res_conv(x*m) + h with the add in the GEMM epilogue ((acc + bias) + h, torch's order)
         return O.conv_tm(x, self.res_conv.weight, self.res_conv.bias, mask, padding=0, residual=h)
 
@@ -263,9 +265,10 @@ class Decoder(nn.Module):
                 m = F.interpolate(m.unsqueeze(1), size=new, mode="nearest")[:, 0]
             else:
                 m = m[:, :new].contiguous()
-        h = _conv_tm(self.final_conv, h, m)
+        fc = self.final_conv
+        h = O.conv_tm(h, fc.weight, fc.bias, m, stride=fc.stride[0], padding=fc.padding[0], out_bf16=True)
         h = O.group_norm_mish_tm(h, self.final_norm.weight, self.final_norm.bias, self.final_norm.num_groups,
-                                 None, None, self.final_norm.eps)  # no mask after the final Mish (:366-368)
+                                 None, None, self.final_norm.eps, out_bf16=True)  # no mask after the Mish (:366-368)
         return O.conv_tm(h, self.final_proj.weight, self.final_proj.bias, m, padding=0, out_scale=mask)
 
     def forward(self, x, mask, mu, t, cond=None):

@@ -490,3 +490,66 @@ def test_preln_blocks_match_unfused_ops(prec):
             assert torch.equal(a, b), i
         else:
             assert rel(a, b) < 1e-2, (i, rel(a, b))
+
+
+@pytest.mark.parametrize("B,T,C,G,dy16", [(4, 600, 256, 8, False), (3, 300, 256, 8, True), (2, 2000, 256, 8, True)])
+def test_group_norm_mish_bf16_storage(B, T, C, G, dy16):
+    """bf16-stored GroupNorm input / output / gradient (MTTS_NORM_F_X/Y/DY_BF16): the same fp32 arithmetic
+    on the exactly widened values, outputs rounded once -- equal to the fp32-storage kernel's result
+    rounded to bf16 (the register-resident and the streaming kernels)."""
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator(device="cpu").manual_seed(B * T + G)
+    h = (torch.randn(B, T, C, generator=g) * 2 + 0.5).bfloat16().to(DEV)
+    gamma = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    m = _mask(B, T, [T - 9 * i for i in range(B)])
+    add = torch.randn(B, C, generator=g).to(DEV)
+    # dy16: a bf16 output, whose incoming gradient autograd hands over as bf16 (the Block1D feeding a
+    # conv); else an fp32 output from a bf16 input with an fp32 gradient (the block feeding the residual)
+    dy = torch.randn(B, T, C, generator=g).to(DEV)
+    if dy16:
+        dy = dy.bfloat16().float()
+    outs = []
+    for x, o16 in ((h.float(), False), (h, dy16)):
+        xx = x.clone().requires_grad_(True)
+        with _ctx("bf16"):
+            y = O.group_norm_mish_tm(xx, gamma, beta, G, m, add, out_bf16=o16)
+        y.backward(dy.to(y.dtype))
+        outs.append((y.detach(), xx.grad))
+    (y32, g32), (y16, g16) = outs
+    assert y16.dtype == (torch.bfloat16 if dy16 else torch.float32) and g16.dtype == torch.bfloat16
+    torch.testing.assert_close(y16.float(), y32.to(y16.dtype).float(), rtol=0, atol=0)
+    torch.testing.assert_close(g16.float(), g32.bfloat16().float(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_conv_bf16_storage_chain(stride):
+    """conv (bf16 out) -> GroupNorm+Mish (bf16 out) -> conv: the bf16-mixed storage path against the same
+    ops with fp32 storage (bf16 rounding of the stored activations and gradients only)."""
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator(device="cpu").manual_seed(11 + stride)
+    B, T, C = 4, 300, 256
+    x = torch.randn(B, T, C, generator=g).to(DEV)
+    w1 = (torch.randn(C, C, 3, generator=g) / math.sqrt(3 * C)).to(DEV)
+    w2 = (torch.randn(C, C, 3, generator=g) / math.sqrt(3 * C)).to(DEV)
+    b1, b2 = torch.randn(C, generator=g).to(DEV), torch.randn(C, generator=g).to(DEV)
+    gam, bet = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV), (0.1 * torch.randn(C, generator=g)).to(DEV)
+    m = _mask(B, T, [T - 13 * i for i in range(B)])
+    res = []
+    for bf in (False, True):
+        ins = [t.clone().requires_grad_(True) for t in (x, w1, w2, b1, b2, gam, bet)]
+        xx, ww1, ww2, bb1, bb2, gg, be = ins
+        with _ctx("bf16"):
+            h = O.conv_tm(xx, ww1, bb1, m, out_bf16=bf)
+            a = O.group_norm_mish_tm(h, gg, be, 8, m, out_bf16=bf)
+            y = O.conv_tm(a, ww2, bb2, m, stride=stride)
+        assert (h.dtype == torch.bfloat16) == bf and (a.dtype == torch.bfloat16) == bf and y.dtype == torch.float32
+        torch.manual_seed(3)
+        y.backward(torch.randn_like(y))
+        res.append((y.detach(), [t.grad for t in ins]))
+    (y0, g0), (y1, g1) = res
+    assert rel(y1, y0) < 1e-2, rel(y1, y0)
+    for i, (a, b) in enumerate(zip(g1, g0)):
+        assert rel(a, b) < 2e-2, (i, rel(a, b))
