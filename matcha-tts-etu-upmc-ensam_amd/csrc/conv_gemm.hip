@@ -364,11 +364,16 @@ struct WgradGeom {
 // conversion on the way to LDS (the masked-row zeroing is a select).
 // YBF16: dY holds bf16 (MTTS_WGRAD_F_DY_BF16): 8-byte row chunks, staged as is (the bias column sums
 // convert exactly).
-template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false>
+// LIN (with INC): stride 1, Ti == To == To_full, no output offset -- the dY row of token row m is m and
+// its tap-j A row m + off_j, so the per-step address advance is one uniform offset (rb * ld) and only
+// the tap validity needs the row's position u in its sequence (~12 instead of ~22 vector instructions
+// per staged row; the bias column sums only in the k-tile-0 blocks, behind a block-uniform branch).
+template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false, bool LIN = false>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_args p, int rows_per_split,
                                                                float *__restrict__ part, float *__restrict__ part_db) {
     static_assert(!ABF16 || BF16, "bf16 A needs the bf16 path");
     static_assert(!YBF16 || BF16, "bf16 dY needs the bf16 path");
+    static_assert(!LIN || INC, "the linear row walk is a special case of the incremental one");
     const uint16_t *A16 = reinterpret_cast<const uint16_t *>(p.A);
     const uint16_t *Y16 = reinterpret_cast<const uint16_t *>(p.dY);
     using Gm = WgradGeom<BF16, KB>;
@@ -435,6 +440,19 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
             }
     }
     const int y_col = min(n0 + c_cc[0], p.N - 4);  // per-chunk y column (chunks differ only in row pair)
+    // LIN: per staged row, the lane-constant parts of its dY / A element offsets and mask index
+    int l_y[LIN ? CH : 1][2], l_x[LIN ? CH : 1][2], l_m[LIN ? CH : 1][2];
+    if constexpr (LIN) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int rr = 2 * c_rp[c] + h;
+                l_y[c][h] = rr * p.ldy + y_col;
+                l_m[c][h] = rr + c_toff[c];
+                l_x[c][h] = l_m[c][h] * p.lda + c_ch[c];
+            }
+    }
 
     // One staged step, loaded unconditionally from clamped addresses; validity, the row mask and the
     // bias column sums are applied at store time so the loads stay in flight through the compute.
@@ -453,6 +471,29 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
         for (int i = 0; i < 4; ++i) colsum[c][i] = 0.f;
 
     auto load = [&](Regs &R, int rb) {
+        if constexpr (LIN) {
+            const int rows_left = r_end - rb;
+            const int yb = rb * p.ldy, xb = rb * p.lda;  // uniform
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const bool mv = 2 * c_rp[c] + h < rows_left;
+                    const uint32_t ye = (uint32_t)(mv ? yb + l_y[c][h] : y_col);
+                    if constexpr (YBF16) R.y16[c][h] = *reinterpret_cast<const uint2 *>(Y16 + ye);
+                    else R.y[c][h] = *reinterpret_cast<const float4 *>(p.dY + ye);
+                    R.yok[c][h] = mv;
+                    const bool xok = mv && (unsigned)(s_u[c][h] + c_toff[c]) < (unsigned)p.Ti;
+                    const uint32_t xe = (uint32_t)(xok ? xb + l_x[c][h] : c_ch[c]);
+                    if constexpr (ABF16) R.x16[c][h] = *reinterpret_cast<const uint2 *>(A16 + xe);
+                    else R.x[c][h] = *reinterpret_cast<const float4 *>(p.A + xe);
+                    R.xs[c][h] = *(p.a_scale ? p.a_scale + (uint32_t)(xok ? rb + l_m[c][h] : 0) : p.A);
+                    R.xok[c][h] = xok;
+                    const int u = s_u[c][h] + KB;
+                    s_u[c][h] = u >= p.To ? u - p.To : u;
+                }
+            return;
+        }
         if constexpr (INC) {
             const int rows_left = r_end - rb;
 #pragma unroll
@@ -536,9 +577,12 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
                     xv[h][2] = R.x[c][h].z * xm; xv[h][3] = R.x[c][h].w * xm;
                 }
             }
-            // unconditional (only k-tile-0 blocks store it): a select per element costs more than the add
+            // INC / generic: unconditional (only k-tile-0 blocks store it; a select per element costs more
+            // than the add); LIN: behind the block-uniform branch
+            if (!LIN || do_db) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) colsum[c][i] += yv[0][i] + yv[1][i];
+                for (int i = 0; i < 4; ++i) colsum[c][i] += yv[0][i] + yv[1][i];
+            }
             const int r2 = 2 * c_rp[c];
             if constexpr (BF16) {
                 auto pk = [](float a, float b) { return pack_bf16x2(a, b); };
@@ -973,21 +1017,27 @@ extern "C" size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *arg
     return mtts::align_up((size_t)splits * args->N * args->K * 4, 256) + (size_t)splits * args->N * 4 + 256;
 }
 
-template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false>
+template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false, bool LIN = false>
 static int wgrad_launch_k(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
                           hipStream_t st) {
     using Gm = WgradGeom<BF16, KB>;
     static bool attr_set = false;
     if (Gm::kLds > 64 * 1024 && !attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)Gm::kLds) != hipSuccess)
             return mtts::fail(MTTS_ERR_HIP, "conv_wgrad: LDS attribute");
         attr_set = true;
     }
     dim3 grid((unsigned)(((p.N + 127) / 128) * ((p.K + 127) / 128) * splits));
-    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16>), grid, dim3(kThreads), Gm::kLds, st, p,
-                       rps, part, part_db);
+    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN>), grid, dim3(kThreads), Gm::kLds,
+                       st, p, rps, part, part_db);
     return mtts::check_launch("conv_wgrad_kernel");
+}
+
+// The linear row walk (LIN): every row's dY / A rows follow from the token row index alone.
+static bool wgrad_lin_ok(const mtts_conv_wgrad_args &p) {
+    static const bool off = [] { const char *e = getenv("MTTS_WGRAD_LIN"); return e && e[0] == '0'; }();
+    return !off && p.in_stride == 1 && p.out_stride == 1 && p.out_off == 0 && p.To_full == p.To && p.Ti == p.To;
 }
 
 // The incremental row walk needs one wrap per step (To >= KB) and element offsets that stay inside
@@ -1004,6 +1054,11 @@ static int wgrad_launch(const mtts_conv_wgrad_args &p, int splits, int rps, floa
                         hipStream_t st) {
     if constexpr (BF16 && KB == 32 && DEPTH == 1) {
         const bool a16 = p.flags & MTTS_GEMM_F_A_BF16, y16 = p.flags & MTTS_WGRAD_F_DY_BF16, inc = wgrad_inc_ok(p, KB);
+        // the linear walk measured faster only with a bf16 A and an fp32 dY (19200-row conv: 44.4 vs 48.0 us;
+        // fp32 / fp32 42.7 vs 42.9, bf16 dY 48.1 vs 42.9: tools/wgrad_store_ab.py) -- the staging's VALU is
+        // not what bounds the other storages
+        if (inc && a16 && !y16 && wgrad_lin_ok(p))
+            return wgrad_launch_k<true, 32, 1, true, true, false, true>(p, splits, rps, part, part_db, st);
         if (a16 && y16)
             return inc ? wgrad_launch_k<true, 32, 1, true, true, true>(p, splits, rps, part, part_db, st)
                        : wgrad_launch_k<true, 32, 1, false, true, true>(p, splits, rps, part, part_db, st);

@@ -215,16 +215,17 @@ class Decoder(nn.Module):
 
     def _time_projections(self, temb):
         """Every ResnetBlock's mlp(temb) = Linear(Mish(temb)) (decoder.py:80-81) as ONE GEMM: the Mish of
-        the shared time embedding is computed once and the blocks' Linear weights are stacked along N
-        (their gradients come back as separate views), instead of 6 x (mish, addmm) forward and
-        6 x (mish', 2 mm, bias sum, accumulate) backward launches.  fp32, like the per-block path."""
+        the shared time embedding is computed once and the blocks' Linear weights are stacked along N,
+        instead of 6 x (mish, addmm) forward and 6 x (mish', 2 mm, bias sum, accumulate) backward
+        launches.  fp32, like the per-block path.  B rows only (32 x 1024 -> 1536): a plain library GEMM
+        -- the implicit-conv kernel's 32-row tiles gave it 12 workgroups (82 us for its dgrad)."""
         resnets = ([r for r, *_ in self.Downsampling_Blocks] + [r for r, _ in self.Mid_Blocks]
                    + [r for r, *_ in self.Upsampling_Blocks])
         lins = [r.mlp[1] for r in resnets]
         with torch.autocast("cuda", enabled=False):
             act = F.mish(temb.float())
             bias = torch.cat([lin.bias for lin in lins])
-            tp = O.linear_tm(act, tuple(lin.weight for lin in lins), bias)
+            tp = F.linear(act, torch.cat([lin.weight for lin in lins]), bias)
         return dict(zip(map(id, resnets), tp.split([lin.out_features for lin in lins], dim=-1)))
 
     def _forward_tm(self, x, mask, mu, t, packed=None):

@@ -553,3 +553,38 @@ def test_conv_bf16_storage_chain(stride):
     assert rel(y1, y0) < 1e-2, rel(y1, y0)
     for i, (a, b) in enumerate(zip(g1, g0)):
         assert rel(a, b) < 2e-2, (i, rel(a, b))
+
+
+@pytest.mark.parametrize("a16,y16", [(False, False), (True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("B,T,Cin,Cout,k", [(8, 300, 256, 256, 3), (5, 77, 192, 768, 5), (32, 40, 256, 128, 1)])
+def test_wgrad_linear_walk_storage(a16, y16, B, T, Cin, Cout, k):
+    """The register wgrad's linear row walk (stride 1, equal lengths: every product conv / linear) with
+    each operand storage, a ragged 0/1 row mask and the bias sums: against float64 (1e-5 of the scale)
+    and bitwise repeatable; with and without the bias gradient (the raw-bf16 dY staging)."""
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator(device="cpu").manual_seed(B * T + Cin + k + 2 * a16 + y16)
+    x = torch.randn(B, T, Cin, generator=g).bfloat16().float().to(DEV)
+    lengths = torch.randint(T // 3, T + 1, (B,), generator=g)
+    lengths[0] = T
+    m = (torch.arange(T)[None] < lengths[:, None]).float().to(DEV)
+    pad = k // 2
+    dy = torch.randn(B, T, Cout, generator=g).bfloat16().float().to(DEV)
+    ref = torch.nn.grad.conv1d_weight((x * m.unsqueeze(-1)).double().transpose(1, 2), (Cout, Cin, k),
+                                      dy.double().transpose(1, 2), padding=pad)
+    refb = dy.double().sum((0, 1))
+    xa = x.bfloat16() if a16 else x
+    dya = dy.bfloat16() if y16 else dy
+    outs = []
+    for with_db in (True, True, False):
+        dw = torch.full((Cout, Cin, k), float("nan"), device=DEV)
+        db = torch.full((Cout,), float("nan"), device=DEV) if with_db else None
+        O._wgrad(dya, T, 1, 0, xa, T, T, B, 1, [j - pad for j in range(k)], Cin, Cout, dw, (Cin * k, k, 1),
+                 prec=O.PREC_BF16, a_scale=m, db=db)
+        outs.append((dw, db))
+    torch.cuda.synchronize()
+    dw, db = outs[0]
+    assert (dw.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+    assert (db.double() - refb).abs().max().item() <= 1e-5 * refb.abs().max().item()
+    assert torch.equal(dw, outs[1][0]) and torch.equal(db, outs[1][1])
+    assert torch.equal(dw, outs[2][0])  # the bias-free path stages the same values
