@@ -55,6 +55,7 @@ GEMM_F_FAST_ACT = 0x8  # MTTS_GEMM_F_FAST_ACT: 1.5e-7-accurate erf in GELU epilo
 GEMM_F_PRE_BF16 = 0x10  # MTTS_GEMM_F_PRE_BF16: C_pre written / aux read as bf16
 WGRAD_F_DY_BF16 = 0x20  # MTTS_WGRAD_F_DY_BF16: the weight gradient's dY holds bf16
 _FAST_ACT = os.environ.get("MTTS_EXACT_GELU") != "1"
+
 GEMM_GLDS = 32  # MTTS_GEMM_GLDS: first LDS-DMA schedule id
 
 
@@ -358,6 +359,14 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     (matcha.utils.model.sequence_mask: 0/1 by construction, as the reference's x * mask), so
     ``binary_scale`` defaults to True: the bf16 LDS-DMA schedule then reads masked rows as zeros
     instead of multiplying.  Pass False for a general row scale."""
+    # host-side shape checks before any launch (the kernel trusts W's rows / the output's extent)
+    if Wp.dim() != 2 or Wp.shape[0] < N_ or Wp.shape[1] != Kp or Kp < len(offs) * cin:
+        raise ValueError(f"packed weight {tuple(Wp.shape)} does not cover N={N_}, Kp={Kp}, K={len(offs) * cin}")
+    if C.shape[-1] < N_ or C.numel() < nb * To_full * C.shape[-1] or A.shape[-1] < cin:
+        raise ValueError(f"GEMM operands too small: A {tuple(A.shape)}, C {tuple(C.shape)}, N={N_}")
+    for t, w_ in ((residual, N_), (aux, N_), (C_pre, N_)):
+        if t is not None and (t.shape[-1] < w_ or t.numel() < nb * To_full * t.shape[-1]):
+            raise ValueError(f"epilogue operand {tuple(t.shape)} too small for N={N_}")
     args = ConvGemmArgs()
     args.A, args.a_scale, args.lda, args.Ti, args.To, args.nb = A.data_ptr(), N.ptr(a_scale), A.shape[-1], Ti, To, nb
     args.in_stride, args.ntaps, args.cin = in_stride, len(offs), cin
@@ -1242,8 +1251,9 @@ class _PreLNFeedForwardTM(torch.autograd.Function):
         M, C = h2.shape
         H = w1.shape[0]
         lnw, lnb = _f32c(ln_w), _f32c(ln_b)
-        # fp32 LayerNorm output here: the GELU-epilogue GEMM and the weight gradient run faster on the
-        # register-staged schedules (fp32 A) than on the LDS-DMA ones (bf16 A) -- tools/preln_shapes.py
+        # fp32 LayerNorm output here: with it bf16 the GELU GEMM runs the 64 x 256 LDS-DMA tiles, faster
+        # in isolation (53.3 vs 61.0 us at 19200 x 1024 x 256, tools/ff_epilogue_cost.py) but the step
+        # measured slower (9.22 vs 8.92 ms); the register-staged schedule hides the GELU epilogue
         n, mean, rstd = _ln_fwd(h2, lnw, lnb, eps, False)
         W1p, K1p = packed(spec_linear((w1,)), prec)
         W2p, K2p = packed(spec_linear((w2,)), prec)

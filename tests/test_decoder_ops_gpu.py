@@ -588,3 +588,4 @@ def test_wgrad_linear_walk_storage(a16, y16, B, T, Cin, Cout, k):
     assert (db.double() - refb).abs().max().item() <= 1e-5 * refb.abs().max().item()
     assert torch.equal(dw, outs[1][0]) and torch.equal(db, outs[1][1])
     assert torch.equal(dw, outs[2][0])  # the bias-free path stages the same values
+
