@@ -997,9 +997,14 @@ static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks,
     const int M = p.nb * p.To;
     const int tiles = ((p.N + 127) / 128) * ((p.K + 127) / 128);
     static const int min_blocks = [] { const char *e = getenv("MTTS_WGRAD_MINBLK"); return e ? atoi(e) : 256; }();
+    // bf16-stored operands: ~3 blocks per CU (each step's loads are half the bytes, so more blocks -- more
+    // steps in flight per CU -- pay for the extra slab traffic: 19200-row conv 49.8 -> 38.4 us with both
+    // operands bf16, 42.8 -> 36.6 with bf16 dY; fp32 operands are neutral: tools/wgrad_store_ab.py)
+    static const int min_blocks16 = [] { const char *e = getenv("MTTS_WGRAD_MINBLK16"); return e ? atoi(e) : 768; }();
     static const int split_rows = [] { const char *e = getenv("MTTS_WGRAD_ROWS"); return e && atoi(e) > 0 ? atoi(e) : 768; }();
+    const int mb = (p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_WGRAD_F_DY_BF16)) ? min_blocks16 : min_blocks;
     int s = target_blocks > 0 ? (target_blocks + tiles - 1) / tiles
-                              : max((min_blocks + tiles - 1) / tiles, (M + split_rows / 2) / split_rows);
+                              : max((mb + tiles - 1) / tiles, (M + split_rows / 2) / split_rows);
     s = max(1, min(s, (M + 4 * kb - 1) / (4 * kb)));  // at least 4 steps per split
     int rps = (M + s - 1) / s;
     rps = (rps + kb - 1) / kb * kb;
@@ -1052,22 +1057,22 @@ static bool wgrad_inc_ok(const mtts_conv_wgrad_args &p, int kb) {
 template <bool BF16, int KB, int DEPTH>
 static int wgrad_launch(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
                         hipStream_t st) {
-    if constexpr (BF16 && KB == 32 && DEPTH == 1) {
+    if constexpr (BF16 && (KB == 32 || KB == 64) && DEPTH == 1) {
         const bool a16 = p.flags & MTTS_GEMM_F_A_BF16, y16 = p.flags & MTTS_WGRAD_F_DY_BF16, inc = wgrad_inc_ok(p, KB);
         // the linear walk measured faster only with a bf16 A and an fp32 dY (19200-row conv: 44.4 vs 48.0 us;
         // fp32 / fp32 42.7 vs 42.9, bf16 dY 48.1 vs 42.9: tools/wgrad_store_ab.py) -- the staging's VALU is
         // not what bounds the other storages
-        if (inc && a16 && !y16 && wgrad_lin_ok(p))
+        if (KB == 32 && inc && a16 && !y16 && wgrad_lin_ok(p))
             return wgrad_launch_k<true, 32, 1, true, true, false, true>(p, splits, rps, part, part_db, st);
         if (a16 && y16)
-            return inc ? wgrad_launch_k<true, 32, 1, true, true, true>(p, splits, rps, part, part_db, st)
-                       : wgrad_launch_k<true, 32, 1, false, true, true>(p, splits, rps, part, part_db, st);
+            return inc ? wgrad_launch_k<true, KB, 1, true, true, true>(p, splits, rps, part, part_db, st)
+                       : wgrad_launch_k<true, KB, 1, false, true, true>(p, splits, rps, part, part_db, st);
         if (y16)
-            return inc ? wgrad_launch_k<true, 32, 1, true, false, true>(p, splits, rps, part, part_db, st)
-                       : wgrad_launch_k<true, 32, 1, false, false, true>(p, splits, rps, part, part_db, st);
+            return inc ? wgrad_launch_k<true, KB, 1, true, false, true>(p, splits, rps, part, part_db, st)
+                       : wgrad_launch_k<true, KB, 1, false, false, true>(p, splits, rps, part, part_db, st);
         if (a16)
-            return inc ? wgrad_launch_k<true, 32, 1, true, true>(p, splits, rps, part, part_db, st)
-                       : wgrad_launch_k<true, 32, 1, false, true>(p, splits, rps, part, part_db, st);
+            return inc ? wgrad_launch_k<true, KB, 1, true, true>(p, splits, rps, part, part_db, st)
+                       : wgrad_launch_k<true, KB, 1, false, true>(p, splits, rps, part, part_db, st);
     }
     return wgrad_inc_ok(p, KB) ? wgrad_launch_k<BF16, KB, DEPTH, true>(p, splits, rps, part, part_db, st)
                                : wgrad_launch_k<BF16, KB, DEPTH, false>(p, splits, rps, part, part_db, st);
@@ -1101,8 +1106,8 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
     if (rows_per_step < 0) rows_per_step = 32;
     if (depth < 0) depth = 1;
     if (p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_WGRAD_F_DY_BF16)) {
-        MTTS_CHECK_ARG(bf16 && rows_per_step == 32 && depth == 1 && p.lda % 4 == 0 && (uintptr_t)p.A % 8 == 0,
-                       "conv_wgrad: a bf16 A or dY needs bf16 precision, the default schedule and 8-byte aligned rows");
+        MTTS_CHECK_ARG(bf16 && depth == 1 && p.lda % 4 == 0 && (uintptr_t)p.A % 8 == 0,
+                       "conv_wgrad: a bf16 A or dY needs bf16 precision, one step in flight and 8-byte aligned rows");
     }
     MTTS_CHECK_ARG(rows_per_step == 32 || (rows_per_step == 64 && bf16), "conv_wgrad: rows_per_step 32 (or 64 bf16)");
     MTTS_CHECK_ARG(depth == 1 || (depth == 2 && bf16), "conv_wgrad: depth 1 (or 2 bf16)");

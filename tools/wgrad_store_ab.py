@@ -17,11 +17,14 @@ m = (torch.rand(B, T, device=dev) > 0.1).float()
 pad = k // 2
 dw = torch.empty(Cout, Cin, k, device=dev)
 db = torch.empty(Cout, device=dev)
+KB = int(sys.argv[2]) if len(sys.argv) > 2 else -1  # rows per step (-1: default 32)
+TB = int(sys.argv[3]) if len(sys.argv) > 3 else -1  # target blocks
 for a16, y16 in ((False, False), (True, False), (False, True), (True, True)):
     x = x32.bfloat16() if a16 else x32
     dy = dy32.bfloat16() if y16 else dy32
     run = lambda: O._wgrad(dy, T, 1, 0, x, T, T, B, 1, [j - pad for j in range(k)], Cin, Cout, dw, (Cin * k, k, 1),
-                           prec=O.PREC_BF16, a_scale=m, db=db)
+                           prec=O.PREC_BF16, a_scale=m, db=db, rows_per_step=KB, target_blocks=TB,
+                           depth=1 if KB > 0 else -1)
     us = t_ev(run)
-    print("ok", name, "A16" if a16 else "A32", "Y16" if y16 else "Y32", f"{us:.1f}us",
+    print("ok", name, f"kb={KB} tb={TB}", "A16" if a16 else "A32", "Y16" if y16 else "Y32", f"{us:.1f}us",
           f"{2 * B * T * Cin * k * Cout / us / 1e6:.0f}TF", flush=True)
