@@ -18,9 +18,19 @@ import torch
 from torch.nn.utils.rnn import pad_sequence
 
 
-def collate(batch):
+def _round_up(n: int, q: int) -> int:
+    return -(-n // q) * q
+
+
+def collate(batch, x_quantum: int = 1, y_quantum: int = 1):
     """ljspeech_datamodule.py:84-109: items {"x": int64 [Tx_i], "y": [n_mels, Ty_i], "x_lengths",
-    "y_lengths"} -> padded batch dict (padding value 0)."""
+    "y_lengths"} -> padded batch dict (padding value 0).
+
+    x_quantum / y_quantum > 1 pad Tx_max / Ty_max further, up to a multiple of the quantum, so that
+    batches fall into a few padded shapes and the graph-mode Trainer replays a cached step graph
+    instead of capturing one per batch (its LRU cache, TrainConfig.graph_cache).  1 (default) is the
+    reference's padding to the batch maximum; a larger padded T only adds masked frames, but the
+    decoder's GroupNorm statistics run over the padded length (decoder.py:58-66), as with bucketing."""
     x = [item["x"] for item in batch]
     x_lengths = torch.tensor([int(item["x_lengths"]) for item in batch])
     y_lengths = torch.tensor([int(item["y_lengths"]) for item in batch])
@@ -28,6 +38,11 @@ def collate(batch):
     # time-major views for pad_sequence, back to [B, n_mels, T] (the reference's transposes, :104-105)
     y_padded = pad_sequence([item["y"].transpose(0, 1) for item in batch], batch_first=True,
                             padding_value=0).transpose(1, 2)
+    tx, ty = _round_up(x_padded.shape[1], x_quantum), _round_up(y_padded.shape[2], y_quantum)
+    if tx != x_padded.shape[1]:
+        x_padded = torch.nn.functional.pad(x_padded, (0, tx - x_padded.shape[1]))
+    if ty != y_padded.shape[2]:
+        y_padded = torch.nn.functional.pad(y_padded, (0, ty - y_padded.shape[2]))
     return {"x": x_padded, "x_lengths": x_lengths, "y": y_padded, "y_lengths": y_lengths}
 
 

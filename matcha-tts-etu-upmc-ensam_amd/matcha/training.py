@@ -163,7 +163,9 @@ class TrainConfig:
     lr: float = 1e-4
     eta_min: float = 1e-6
     t_max_epochs: int = 1000
-    graph_cache: int = 4  # captured steps kept per input-shape key (LRU); bucketed padding keeps keys few
+    # captured steps kept per input-shape key (LRU); collate(x_quantum=16, y_quantum=64) on bucketed batches
+    # keeps real data to ~20 padded shapes (tests/test_data_path.py) -- size the cache to cover them
+    graph_cache: int = 4
     dp: str = "auto"  # N>1 exchange: "ddp" (eager only), "buckets" (GradBucketReducer), "auto"
     comm: str = "auto"  # bucket reducer transport: "rccl" (capturable, libmtts_hip), "torch", "auto"
 

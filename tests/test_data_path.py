@@ -108,6 +108,30 @@ def test_bucketing_cuts_padding():
     assert pad_ratio(32) < 1.1 < 1.5 < pad_ratio(0)
 
 
+def test_quantized_padding_bounds_graph_shapes():
+    """collate(x_quantum, y_quantum) on bucketed LJSpeech-like lengths: the padded shapes fall into a few
+    classes (the graph-mode Trainer caches one captured step per shape), the extra padding is zeros and
+    the padded fraction stays small.  (TrainConfig.graph_cache should cover the classes: each captured
+    step keeps its own memory pool, a few GB at B=32 -- 288 GB of HBM holds dozens.)"""
+    from matcha.data_management.ljspeech_datamodule import LengthBucketBatchSampler, collate
+
+    g = torch.Generator().manual_seed(7)
+    Ty = torch.randint(150, 900, (4096,), generator=g)
+    Tx = (Ty // 5).clamp_min(8)
+    shapes, real, padded = set(), 0, 0
+    for b in LengthBucketBatchSampler(Ty, 32, 1, 0, bucket_batches=32, seed=2):
+        items = [{"x": torch.ones(int(Tx[i]), dtype=torch.int64), "y": torch.ones(4, int(Ty[i])),
+                  "x_lengths": Tx[i], "y_lengths": Ty[i]} for i in b]
+        out = collate(items, x_quantum=16, y_quantum=64)
+        assert out["x"].shape[1] % 16 == 0 and out["y"].shape[2] % 64 == 0
+        assert out["x"].sum() == Tx[b].sum() and out["y"].sum() == 4 * Ty[b].sum()  # the extra padding is 0
+        shapes.add((out["x"].shape[1], out["y"].shape[2]))
+        real += int(Ty[b].sum())
+        padded += out["y"].shape[2] * len(b)
+    assert len(shapes) <= 24  # vs ~128 distinct (Tx, Ty) maxima without the quantum
+    assert padded / real < 1.2
+
+
 @pytest.mark.gpu
 def test_mel_hip_matches_golden_and_oracle():
     from matcha.utils.audio_process import MelSpectrogram
