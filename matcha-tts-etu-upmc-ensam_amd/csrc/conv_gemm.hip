@@ -833,8 +833,10 @@ static int pick_cfg(const mtts_conv_gemm_args &p, int M, bool bf16) {
         // 44.9 vs 48.5, 34.6 vs 38.3 us)
         if (!(sched_mask & 8) && t > 256 && mtts::conv_gemm_glds_lean(p)) return MTTS_GEMM_GLDS + 13;
     }
-    if (!(sched_mask & 8) && p.K < 768 && p.N >= 512 && mtts::conv_gemm_glds_applies(p) && mtts::conv_gemm_glds_lean(p))
-        return MTTS_GEMM_GLDS + 9;  // the q|k|v projection, the encoder's 192 -> 768 conv: 35.1 vs 37.2 us
+    if (!(sched_mask & 8) && p.K < 768 && p.N >= 512 && glds_tiles(p, M) >= 256 && mtts::conv_gemm_glds_applies(p) &&
+        mtts::conv_gemm_glds_lean(p))
+        return MTTS_GEMM_GLDS + 9;  // the decoder's q|k|v projection: 35.1 vs 37.2 us (one workgroup per CU:
+                                    // not below one round of tiles -- the text encoder's 3840-row GEMMs)
     return p.K >= 384 ? 12 : 7;
 }
 
