@@ -241,7 +241,10 @@ typedef struct mtts_attn_args {
     float scale;
     float dropout_p;      /* dropout on the probabilities (text encoder, text_encoder.py:222); 0 = off */
     const uint32_t *seed; /* device pointer (2 words), keyed (seed, (b*H+h)*T + q, key) */
+    int32_t flags;        /* MTTS_ATTN_F_IO_BF16: q/k/v/o and the gradients' dout/dq/dk/dv hold bf16
+                             (bf16 precision; strides in elements); lse / Drow stay fp32 */
 } mtts_attn_args;
+#define MTTS_ATTN_F_IO_BF16 0x1
 
 typedef struct mtts_attn_grads {
     const float *dout; /* dL/do, row stride lddo */

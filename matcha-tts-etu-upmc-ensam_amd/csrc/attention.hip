@@ -110,6 +110,24 @@ __device__ __forceinline__ bf16x8 frag8(const float *e) {
 
 __device__ __forceinline__ int crow(int v, int lh) { return (v & 3) + 8 * (v >> 2) + 4 * lh; }
 
+// q / k / v / o / dO / dq / dk / dv storage (TI): fp32, or bf16 bits (uint16_t, MTTS_ATTN_F_IO_BF16 in
+// bf16-mixed mode: the MFMA operands are bf16 anyway, so the producers' GEMMs write half the bytes)
+template <typename TI>
+__device__ __forceinline__ float4 ld4f(const TI *p) {
+    if constexpr (sizeof(TI) == 4) {
+        return *reinterpret_cast<const float4 *>(p);
+    } else {
+        const uint2 q = *reinterpret_cast<const uint2 *>(p);
+        return make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                           __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
+    }
+}
+template <typename TI>
+__device__ __forceinline__ void st4f(TI *p, float4 v) {
+    if constexpr (sizeof(TI) == 4) *reinterpret_cast<float4 *>(p) = v;
+    else *reinterpret_cast<uint2 *>(p) = make_uint2(pack2(v.x, v.y), pack2(v.z, v.w));
+}
+
 // The 16 C-layout rows a lane holds are 4 runs of 4: per-row LDS constants (key bias, lse, D) are
 // read as 4 float4 (ds_read_b128) instead of 16 scalars.
 __device__ __forceinline__ void crow_load16(const float *base, int lh, float (&out)[16]) {
@@ -143,13 +161,14 @@ template <int D>
 struct RowFrag<true, D> {
     bf16x8 f[D / 16];
     // mul: a prescale folded into the operand before its bf16 rounding (the softmax scale * log2 e)
-    __device__ void load(const float *row, bool ok, int lh, int dh, float mul = 1.f) {
+    template <typename TI>
+    __device__ void load(const TI *row, bool ok, int lh, int dh, float mul = 1.f) {
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) {
             float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
             const int c = 16 * ks + 8 * lh;
-            if (ok && c < dh) a = *reinterpret_cast<const float4 *>(row + c);
-            if (ok && c + 4 < dh) b = *reinterpret_cast<const float4 *>(row + c + 4);
+            if (ok && c < dh) a = ld4f(row + c);
+            if (ok && c + 4 < dh) b = ld4f(row + c + 4);
             const float e[8] = {a.x * mul, a.y * mul, a.z * mul, a.w * mul,
                                 b.x * mul, b.y * mul, b.z * mul, b.w * mul};
             f[ks] = frag8(e);
@@ -224,7 +243,8 @@ struct TileLoader {
     // through the compute phase.  Rows past T are NOT zeroed: they hold finite data (row 0 of the
     // batch) and every kernel gives them probability 0 (key bias -inf / query lse +inf), so they add
     // exact zeros to every product.
-    __device__ void load(const float *base, int ld, int b, int T, int r0, int tid, int dh) {
+    template <typename TI>
+    __device__ void load(const TI *base, int ld, int b, int T, int r0, int tid, int dh) {
         narrow = dh < D;
 #pragma unroll
         for (int i = 0; i < Gm::F4; ++i) {
@@ -232,7 +252,7 @@ struct TileLoader {
             stage_rc<BF16, D>(tid + kThreads * i, r, c);
             const bool ok = r0 + r < T && c < dh;
             const size_t off = ok ? ((size_t)b * T + r0 + r) * ld + c : (size_t)b * T * ld;
-            v[i] = *reinterpret_cast<const float4 *>(base + off);
+            v[i] = ld4f(base + off);
         }
     }
     __device__ void store(typename Gm::T *rowt, typename Gm::T *trt, int tid, int dh) const {
@@ -339,8 +359,11 @@ __device__ __forceinline__ void tile_loop(int ntiles, Load &&load, Store &&store
 
 // ------------------------------------------------------------------------------------------------
 // forward: grid (ceil(T/128), H, B); lane = query
-template <bool BF16, int D>
+template <bool BF16, int D, typename TI = float>
 __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_fwd_kernel(mtts_attn_args p) {
+    const TI *Qp = reinterpret_cast<const TI *>(p.q), *Kp = reinterpret_cast<const TI *>(p.k),
+             *Vp = reinterpret_cast<const TI *>(p.v);
+    TI *Op = reinterpret_cast<TI *>(p.o);
     using Gm = G<BF16, D>;
     using ST = typename Gm::T;
     constexpr int NB = nbuf(fwd_stage<BF16, D>());
@@ -355,13 +378,13 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_fwd_
     const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
     const int q = blockIdx.x * kRowsPerBlock + wave * 32 + lr;
     const bool q_ok = q < T;
-    const float *Kb = p.k + h * dh, *Vb = p.v + h * dh;
+    const TI *Kb = Kp + h * dh, *Vb = Vp + h * dh;
     const float c0 = key_bias_c0(p, b);
 
     // bf16: q carries scale * log2 e (scores come out of the MFMA in the log2 domain)
     const float sl2 = p.scale * kLog2e;
     RowFrag<BF16, D> qf;
-    qf.load(p.q + h * dh + ((size_t)b * T + (q_ok ? q : 0)) * p.ldq, q_ok, lh, dh, BF16 ? sl2 : 1.f);
+    qf.load(Qp + h * dh + ((size_t)b * T + (q_ok ? q : 0)) * p.ldq, q_ok, lh, dh, BF16 ? sl2 : 1.f);
 
     f32x16 acc[Gm::NT];
 #pragma unroll
@@ -447,23 +470,27 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_fwd_
 
     if (q_ok) {
         const float inv = 1.f / l;
-        float *orow = p.o + ((size_t)b * T + q) * p.ldo + h * dh;
+        TI *orow = Op + ((size_t)b * T + q) * p.ldo + h * dh;
 #pragma unroll
         for (int t = 0; t < Gm::NT; ++t)
 #pragma unroll
             for (int g = 0; g < 4; ++g)
                 if (t * 32 + 8 * g + 4 * lh < dh)
-                *reinterpret_cast<float4 *>(orow + t * 32 + 8 * g + 4 * lh) =
-                    make_float4(acc[t][4 * g] * inv, acc[t][4 * g + 1] * inv, acc[t][4 * g + 2] * inv,
-                                acc[t][4 * g + 3] * inv);
+                    st4f(orow + t * 32 + 8 * g + 4 * lh,
+                         make_float4(acc[t][4 * g] * inv, acc[t][4 * g + 1] * inv, acc[t][4 * g + 2] * inv,
+                                     acc[t][4 * g + 3] * inv));
         if (lh == 0) p.lse[((size_t)b * p.H + h) * T + q] = m + log2f(l);
     }
 }
 
 // ------------------------------------------------------------------------------------------------
 // backward, dQ: grid (ceil(T/128), H, B); lane = query.  Also writes Drow = rowsum(dO * O) for dKV.
-template <bool BF16, int D>
+template <bool BF16, int D, typename TI = float>
 __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(mtts_attn_args p, mtts_attn_grads g, float *Drow) {
+    const TI *Qp = reinterpret_cast<const TI *>(p.q), *Kp = reinterpret_cast<const TI *>(p.k),
+             *Vp = reinterpret_cast<const TI *>(p.v), *Op = reinterpret_cast<const TI *>(p.o),
+             *Gp = reinterpret_cast<const TI *>(g.dout);
+    TI *DQp = reinterpret_cast<TI *>(g.dq);
     using Gm = G<BF16, D>;
     using ST = typename Gm::T;
     constexpr int NB = nbuf(dq_stage<BF16, D>());
@@ -480,22 +507,22 @@ __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(
     const int q = blockIdx.x * kRowsPerBlock + wave * 32 + lr;
     const bool q_ok = q < T;
     const size_t qrow = (size_t)b * T + (q_ok ? q : 0);
-    const float *Kb = p.k + h * dh, *Vb = p.v + h * dh;
+    const TI *Kb = Kp + h * dh, *Vb = Vp + h * dh;
 
     const float sl2 = p.scale * kLog2e, c0 = key_bias_c0(p, b);
     RowFrag<BF16, D> qf, gf;
-    qf.load(p.q + h * dh + qrow * p.ldq, q_ok, lh, dh, BF16 ? sl2 : 1.f);  // as the forward's
-    gf.load(g.dout + h * dh + qrow * g.lddo, q_ok, lh, dh);
+    qf.load(Qp + h * dh + qrow * p.ldq, q_ok, lh, dh, BF16 ? sl2 : 1.f);  // as the forward's
+    gf.load(Gp + h * dh + qrow * g.lddo, q_ok, lh, dh);
     // Drow[q] = sum_d dO[q,d] * O[q,d]: each half-wave lane sums D/2 dims
     float dsum = 0.f;
     if (q_ok) {
-        const float *orow = p.o + qrow * p.ldo + h * dh + (D / 2) * lh;
-        const float *grow = g.dout + qrow * g.lddo + h * dh + (D / 2) * lh;
+        const TI *orow = Op + qrow * p.ldo + h * dh + (D / 2) * lh;
+        const TI *grow = Gp + qrow * g.lddo + h * dh + (D / 2) * lh;
 #pragma unroll
         for (int i = 0; i < D / 2; i += 4) {
             if ((D / 2) * lh + i >= dh) break;
-            const float4 a = *reinterpret_cast<const float4 *>(orow + i);
-            const float4 c = *reinterpret_cast<const float4 *>(grow + i);
+            const float4 a = ld4f(orow + i);
+            const float4 c = ld4f(grow + i);
             dsum += a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
         }
     }
@@ -578,24 +605,27 @@ __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(
     tile_loop<NB>((T + kTile - 1) / kTile, load, store, compute);
 
     if (q_ok) {
-        float *drow = g.dq + ((size_t)b * T + q) * g.ldd + h * dh;
+        TI *drow = DQp + ((size_t)b * T + q) * g.ldd + h * dh;
         const float sc = p.scale;
 #pragma unroll
         for (int t = 0; t < Gm::NT; ++t)
 #pragma unroll
             for (int gi = 0; gi < 4; ++gi)
                 if (t * 32 + 8 * gi + 4 * lh < dh)
-                *reinterpret_cast<float4 *>(drow + t * 32 + 8 * gi + 4 * lh) =
-                    make_float4(acc[t][4 * gi] * sc, acc[t][4 * gi + 1] * sc, acc[t][4 * gi + 2] * sc,
-                                acc[t][4 * gi + 3] * sc);
+                    st4f(drow + t * 32 + 8 * gi + 4 * lh,
+                         make_float4(acc[t][4 * gi] * sc, acc[t][4 * gi + 1] * sc, acc[t][4 * gi + 2] * sc,
+                                     acc[t][4 * gi + 3] * sc));
     }
 }
 
 // ------------------------------------------------------------------------------------------------
 // backward, dK/dV: grid (ceil(T/128), H, B); lane = key.  C layout: rows = queries, col = key.
-template <bool BF16, int D>
+template <bool BF16, int D, typename TI = float>
 __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_dkv_kernel(mtts_attn_args p, mtts_attn_grads g,
                                                                 const float *Drow) {
+    const TI *Qp = reinterpret_cast<const TI *>(p.q), *Kp = reinterpret_cast<const TI *>(p.k),
+             *Vp = reinterpret_cast<const TI *>(p.v), *Gp = reinterpret_cast<const TI *>(g.dout);
+    TI *DKp = reinterpret_cast<TI *>(g.dk), *DVp = reinterpret_cast<TI *>(g.dv);
     using Gm = G<BF16, D>;
     using ST = typename Gm::T;
     constexpr int NB = nbuf(dkv_stage<BF16, D>());
@@ -616,10 +646,10 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
 
     const float sl2 = p.scale * kLog2e, c0 = key_bias_c0(p, b);
     RowFrag<BF16, D> kf, vf;
-    kf.load(p.k + h * dh + krow * p.ldq, k_ok, lh, dh, BF16 ? sl2 : 1.f);  // bf16: S in the log2 domain
-    vf.load(p.v + h * dh + krow * p.ldq, k_ok, lh, dh);
+    kf.load(Kp + h * dh + krow * p.ldq, k_ok, lh, dh, BF16 ? sl2 : 1.f);  // bf16: S in the log2 domain
+    vf.load(Vp + h * dh + krow * p.ldq, k_ok, lh, dh);
     const float bias2 = (k_ok && p.key_bias) ? (p.key_bias[krow] - c0) * kLog2e : 0.f;
-    const float *Qb = p.q + h * dh, *Gb = g.dout + h * dh;
+    const TI *Qb = Qp + h * dh, *Gb = Gp + h * dh;
     const size_t sbase = ((size_t)b * p.H + h) * T;
 
     f32x16 dk[Gm::NT], dv[Gm::NT];
@@ -702,8 +732,8 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
     tile_loop<NB>((T + kTile - 1) / kTile, load, store, compute);
 
     if (k_ok) {
-        float *dkr = g.dk + krow * g.ldd + h * dh;
-        float *dvr = g.dv + krow * g.ldd + h * dh;
+        TI *dkr = DKp + krow * g.ldd + h * dh;
+        TI *dvr = DVp + krow * g.ldd + h * dh;
         const float sc = p.scale;
 #pragma unroll
         for (int t = 0; t < Gm::NT; ++t)
@@ -711,10 +741,9 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
             for (int gi = 0; gi < 4; ++gi) {
                 const int c = t * 32 + 8 * gi + 4 * lh;
                 if (c >= dh) continue;
-                *reinterpret_cast<float4 *>(dkr + c) = make_float4(dk[t][4 * gi] * sc, dk[t][4 * gi + 1] * sc,
-                                                                   dk[t][4 * gi + 2] * sc, dk[t][4 * gi + 3] * sc);
-                *reinterpret_cast<float4 *>(dvr + c) =
-                    make_float4(dv[t][4 * gi], dv[t][4 * gi + 1], dv[t][4 * gi + 2], dv[t][4 * gi + 3]);
+                st4f(dkr + c, make_float4(dk[t][4 * gi] * sc, dk[t][4 * gi + 1] * sc, dk[t][4 * gi + 2] * sc,
+                                          dk[t][4 * gi + 3] * sc));
+                st4f(dvr + c, make_float4(dv[t][4 * gi], dv[t][4 * gi + 1], dv[t][4 * gi + 2], dv[t][4 * gi + 3]));
             }
     }
 }
@@ -743,29 +772,38 @@ int check_args(const mtts_attn_args *p, int precision) {
     MTTS_CHECK_ARG(p->scale > 0.f, "attention: scale must be positive");
     MTTS_CHECK_ARG(p->dropout_p >= 0.f && p->dropout_p < 1.f && (p->dropout_p == 0.f || p->seed),
                    "attention: dropout_p in [0, 1) with a seed");
+    MTTS_CHECK_ARG(!(p->flags & ~MTTS_ATTN_F_IO_BF16), "attention: unknown flag");
+    MTTS_CHECK_ARG(!(p->flags & MTTS_ATTN_F_IO_BF16) || precision == MTTS_PREC_BF16,
+                   "attention: bf16 storage needs bf16 precision");
     return MTTS_OK;
 }
 
-template <bool BF16, int D>
+template <bool BF16, int D, typename TI = float>
 int fwd_launch(const mtts_attn_args &p, hipStream_t st) {
+    if constexpr (BF16 && sizeof(TI) == 4) {
+        if (p.flags & MTTS_ATTN_F_IO_BF16) return fwd_launch<true, D, uint16_t>(p, st);
+    }
     constexpr size_t lds = lds_bytes(fwd_stage<BF16, D>());
     static_assert(lds <= kLdsMax, "attention fwd LDS");
-    if (!set_lds(attn_fwd_kernel<BF16, D>, lds)) return mtts::fail(MTTS_ERR_HIP, "attention: LDS attribute");
+    if (!set_lds(attn_fwd_kernel<BF16, D, TI>, lds)) return mtts::fail(MTTS_ERR_HIP, "attention: LDS attribute");
     dim3 grid((p.T + kRowsPerBlock - 1) / kRowsPerBlock, p.H, p.B);
-    hipLaunchKernelGGL((attn_fwd_kernel<BF16, D>), grid, dim3(kThreads), lds, st, p);
+    hipLaunchKernelGGL((attn_fwd_kernel<BF16, D, TI>), grid, dim3(kThreads), lds, st, p);
     return mtts::check_launch("attn_fwd_kernel");
 }
 
-template <bool BF16, int D>
+template <bool BF16, int D, typename TI = float>
 int bwd_launch(const mtts_attn_args &p, const mtts_attn_grads &g, float *Drow, hipStream_t st) {
+    if constexpr (BF16 && sizeof(TI) == 4) {
+        if (p.flags & MTTS_ATTN_F_IO_BF16) return bwd_launch<true, D, uint16_t>(p, g, Drow, st);
+    }
     constexpr size_t lq = lds_bytes(dq_stage<BF16, D>()), lkv = lds_bytes(dkv_stage<BF16, D>());
     static_assert(lq <= kLdsMax && lkv <= kLdsMax, "attention bwd LDS");
-    if (!set_lds(attn_bwd_dq_kernel<BF16, D>, lq) || !set_lds(attn_bwd_dkv_kernel<BF16, D>, lkv))
+    if (!set_lds(attn_bwd_dq_kernel<BF16, D, TI>, lq) || !set_lds(attn_bwd_dkv_kernel<BF16, D, TI>, lkv))
         return mtts::fail(MTTS_ERR_HIP, "attention_bwd: LDS attribute");
     dim3 grid((p.T + kRowsPerBlock - 1) / kRowsPerBlock, p.H, p.B);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<BF16, D>), grid, dim3(kThreads), lq, st, p, g, Drow);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<BF16, D, TI>), grid, dim3(kThreads), lq, st, p, g, Drow);
     if (int rc = mtts::check_launch("attn_bwd_dq_kernel")) return rc;
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<BF16, D>), grid, dim3(kThreads), lkv, st, p, g, (const float *)Drow);
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<BF16, D, TI>), grid, dim3(kThreads), lkv, st, p, g, (const float *)Drow);
     return mtts::check_launch("attn_bwd_dkv_kernel");
 }
 

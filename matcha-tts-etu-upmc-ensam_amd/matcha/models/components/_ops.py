@@ -86,7 +86,8 @@ class AttnArgs(ctypes.Structure):
                 ("key_bias", ctypes.c_void_p), ("o", ctypes.c_void_p), ("ldo", ctypes.c_int32),
                 ("lse", ctypes.c_void_p), ("B", ctypes.c_int32), ("T", ctypes.c_int32), ("H", ctypes.c_int32),
                 ("D", ctypes.c_int32), ("scale", ctypes.c_float), ("dropout_p", ctypes.c_float),
-                ("seed", ctypes.c_void_p)]
+                ("seed", ctypes.c_void_p), ("flags", ctypes.c_int32)]
+ATTN_F_IO_BF16 = 0x1  # include/mtts_decoder.h MTTS_ATTN_F_IO_BF16
 
 
 class AttnGrads(ctypes.Structure):
@@ -1057,6 +1058,10 @@ class _AttentionTM(torch.autograd.Function):
         a.B, a.T, a.H, a.D = B, T, heads, C // heads
         a.scale = 1.0 / math.sqrt(C // heads)
         a.dropout_p, a.seed = float(dropout_p), N.ptr(seed)
+        if qkv.dtype == torch.bfloat16:  # bf16 q|k|v (and o, dO, dq|dk|dv): MTTS_ATTN_F_IO_BF16
+            if o.dtype != torch.bfloat16:
+                raise ValueError("attention: bf16 q|k|v needs a bf16 output")
+            a.flags = ATTN_F_IO_BF16
         return a
 
     @staticmethod
@@ -1095,9 +1100,11 @@ def _attn_fwd(qkv, bias, o, lse, heads, prec, dropout_p=0.0, seed=None):
 
 
 def _attn_bwd(do, qkv, bias, o, lse, heads, prec, dropout_p=0.0, seed=None):
-    """-> d(q|k|v) [B, T, 3C] from dO [B, T, C]."""
+    """-> d(q|k|v) [B, T, 3C] from dO [B, T, C] (in qkv's storage)."""
     B, T, C3 = qkv.shape
     C = C3 // 3
+    if do.dtype != qkv.dtype:
+        raise ValueError("attention backward: dO must be stored like q|k|v")
     dqkv = torch.empty_like(qkv)
     a = _AttentionTM._args(qkv, bias, o, lse, heads, dropout_p, seed)
     g = AttnGrads()
@@ -1139,6 +1146,7 @@ def attention_tm(qkv, key_bias, heads: int, dropout_p: float = 0.0):
 N.register("mtts_layernorm_bwd_res", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _SZ, _P])
 NORM_F_Y_BF16 = 0x100  # include/mtts_decoder.h MTTS_NORM_F_Y_BF16
 _PRELN_N16 = os.environ.get("MTTS_PRELN_N16", "1") != "0"  # attention block's LN output as bf16 (A/B switch)
+_ATTN_IO16 = os.environ.get("MTTS_ATTN_IO16", "1") != "0"  # bf16 q|k|v / o / dO / dq|dk|dv (A/B switch)
 
 
 def _ln_fwd(h2, w, b, eps, y16):
@@ -1186,10 +1194,13 @@ class _PreLNAttentionTM(torch.autograd.Function):
         ctx.wqkv_t = packed(spec_linear((wq, wk, wv), dgrad=True), prec)
         ctx.wo_t = packed(spec_linear((w_out,), dgrad=True), prec)
         C3 = 3 * wq.shape[0]
-        qkv = torch.empty(B, T, C3, device=h.device, dtype=torch.float32)
+        # bf16-mixed: q|k|v and o are only MFMA operands (attention, to_out) -- stored bf16
+        io16 = prec == PREC_BF16 and _ATTN_IO16 and _bf16_operand_ok(C3 // 3)
+        adt = torch.bfloat16 if io16 else torch.float32
+        qkv = torch.empty(B, T, C3, device=h.device, dtype=adt)
         _gemm(n, M, M, 1, 1, [0], C, Wqkv, Kq, C3, qkv.view(M, C3), M, prec=prec)
         bias = _f32c(key_bias)
-        o = torch.empty(B, T, C3 // 3, device=h.device, dtype=torch.float32)
+        o = torch.empty(B, T, C3 // 3, device=h.device, dtype=adt)
         lse = torch.empty(B, heads, T, device=h.device, dtype=torch.float32)
         _attn_fwd(qkv, bias, o, lse, heads, prec)
         y = torch.empty(M, C, device=h.device, dtype=torch.float32)
@@ -1221,7 +1232,7 @@ class _PreLNAttentionTM(torch.autograd.Function):
         dbo = torch.empty(C, device=dev, dtype=torch.float32) if has_bout else None
         _wgrad(g, M, 1, 0, o.view(M, Ci), M, M, 1, 1, [0], Ci, C, dwo, (Ci, 1, 0), prec=prec, db=dbo)
         Wot, Kot = ctx.wo_t
-        do = torch.empty(B, T, Ci, device=dev, dtype=torch.float32)
+        do = torch.empty(B, T, Ci, device=dev, dtype=qkv.dtype)  # stored like q|k|v
         _gemm(g, M, M, 1, 1, [0], C, Wot, Kot, Ci, do.view(M, Ci), M, prec=prec)
         # attention backward -> d(q|k|v)
         dqkv = _attn_bwd(do, qkv, bias, o, lse, heads, prec)

@@ -96,3 +96,34 @@ def test_attention_rejects_unsupported_head_dim():
     a.B, a.T, a.H, a.D, a.scale = 1, 4, 1, 128, 1.0
     rc = N.lib().mtts_attention_fwd(ctypes.byref(a), O.PREC_FP32, O._stream(buf))
     assert rc == -1 and b"head dim" in N.lib().mtts_last_error()
+
+
+@pytest.mark.parametrize("B,T,H,D", [(4, 600, 4, 64), (3, 77, 2, 32)])
+def test_attention_bf16_storage(B, T, H, D):
+    """MTTS_ATTN_F_IO_BF16: bf16 q|k|v / o / dO / dq|dk|dv.  On bf16-representable inputs the forward is
+    the fp32-storage kernel's output rounded once (same MFMA operands); the backward agrees to bf16
+    rounding (the dO . O row sums read the rounded O)."""
+    from matcha.models.components import _ops as O
+
+    rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()
+
+    g = torch.Generator(device="cpu").manual_seed(B * T + H)
+    C = H * D
+    qkv = torch.randn(B, T, 3 * C, generator=g).bfloat16().float().to(DEV)
+    kb = torch.zeros(B, T, device=DEV)
+    for b in range(B):
+        kb[b, : T - 5 * b] = 1
+    do = torch.randn(B, T, C, generator=g).bfloat16().float().to(DEV)
+    res = []
+    for dt in (torch.float32, torch.bfloat16):
+        x = qkv.to(dt)
+        o = torch.empty(B, T, C, device=DEV, dtype=dt)
+        lse = torch.empty(B, H, T, device=DEV)
+        O._attn_fwd(x, kb, o, lse, H, O.PREC_BF16)
+        dqkv = O._attn_bwd(do.to(dt), x, kb, o, lse, H, O.PREC_BF16)
+        res.append((o, lse, dqkv))
+    torch.cuda.synchronize()
+    (o32, l32, d32), (o16, l16, d16) = res
+    assert torch.equal(o16, o32.bfloat16())
+    assert torch.equal(l16, l32)
+    assert rel(d16.float(), d32) < 1e-2, rel(d16.float(), d32)

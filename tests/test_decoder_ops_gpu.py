@@ -466,10 +466,10 @@ def test_preln_blocks_vs_torch(prec, B, T, C, heads):
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 def test_preln_blocks_match_unfused_ops(prec):
     """Fusing changes where values live, not the arithmetic: bitwise equal to the op-by-op composition in
-    fp32 mode; in bf16-mixed mode the forward agrees to accumulation order (a bf16 A operand runs on the
-    LDS-DMA schedule, fp32 on the register-staged one: same products, another fp32 summation order) and
-    the gradients to bf16 rounding (the first FFN bias gradient now sums the bf16 d(pre-activation), as
-    autocast's would)."""
+    fp32 mode.  In bf16-mixed mode the fused block also STORES q|k|v, o, dO and dq|dk|dv as bf16 (the
+    op-by-op path keeps them fp32 and rounds them to bf16 MFMA operands inside the kernels): the q
+    prescale then rounds twice and o is rounded once more before the output projection, so forward and
+    gradients agree to bf16 rounding (~1e-3)."""
     B, T, C, heads = 2, 150, 256, 4
     *ins, kb = _preln_inputs(B, T, C, heads)
     outs = []
@@ -484,7 +484,7 @@ def test_preln_blocks_match_unfused_ops(prec):
     if prec == "fp32":
         assert torch.equal(y0, y1)
     else:
-        assert rel(y0, y1) < 1e-5, rel(y0, y1)
+        assert rel(y0, y1) < 5e-3, rel(y0, y1)
     for i, (a, b) in enumerate(zip(g0, g1)):
         if prec == "fp32":
             assert torch.equal(a, b), i

@@ -8,7 +8,9 @@ if [ -n "$TESTS" ]; then
 fi
 for i in 1 2; do
   for L in ab cur; do
-    if [ $L = ab ]; then export MTTS_LIB=$R/matcha-tts-etu-upmc-ensam_amd/lib/ab/libmtts_hip.so; else unset MTTS_LIB; fi
+    # AB_ENV: settings the baseline leg needs (e.g. switching off a feature the older build lacks)
+    if [ $L = ab ]; then export MTTS_LIB=$R/matcha-tts-etu-upmc-ensam_amd/lib/ab/libmtts_hip.so; for kv in $AB_ENV; do export $kv; done
+    else unset MTTS_LIB; for kv in $AB_ENV; do unset ${kv%%=*}; done; fi
     timeout -k 10 300 python bench.py --no-cpu-baseline --no-synth --steps 40 > $O/b_${L}_$i.json 2> $O/b_${L}_$i.err || { tail -5 $O/b_${L}_$i.err; exit 1; }
     python -c "import json;d=json.loads(open('$O/b_${L}_$i.json').read().strip().splitlines()[-1]);print('$L', d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'])"
   done
