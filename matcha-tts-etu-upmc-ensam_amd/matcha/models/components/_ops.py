@@ -846,6 +846,9 @@ class _ConvFFNTM(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, mask, residual, p_in, p_out):
         _check(x, w1, w2, mask, residual)
         prec = gemm_precision()
+        # the encoder's residual IS the FFN input: the backward adds the residual gradient in the input
+        # dgrad's epilogue (one tensor, no autograd accumulate kernel)
+        ctx.res_is_x = residual is x
         x = _f32c(x)
         B, T, Cin = x.shape
         F_, _, k = w1.shape
@@ -901,7 +904,12 @@ class _ConvFFNTM(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             W1d, K1d = ctx.w1d
             dx = torch.empty_like(x)
-            _gemm(dz1, T, T, B, 1, doffs, F_, W1d, K1d, Cin, dx, T, prec=prec, c_scale=m)
+            fuse = ctx.res_is_x and dres is not None
+            # (dgrad + g) * m = dgrad * m + g: g = dy * m already vanishes on the masked rows
+            _gemm(dz1, T, T, B, 1, doffs, F_, W1d, K1d, Cin, dx, T, prec=prec, c_scale=m,
+                  residual=g if fuse else None)
+            if fuse:
+                dres = None
         return dx, dw1, db1, dw2, db2, None, dres, None, None
 
 

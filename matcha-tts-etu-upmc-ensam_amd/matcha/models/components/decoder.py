@@ -226,7 +226,12 @@ class Decoder(nn.Module):
             act = F.mish(temb.float())
             bias = torch.cat([lin.bias for lin in lins])
             tp = F.linear(act, torch.cat([lin.weight for lin in lins]), bias)
-        return dict(zip(map(id, resnets), tp.split([lin.out_features for lin in lins], dim=-1)))
+            if len({lin.out_features for lin in lins}) == 1:  # [B, n*C] -> n contiguous [B, C] (one copy)
+                n = len(lins)
+                parts = tp.view(tp.shape[0], n, -1).transpose(0, 1).contiguous().unbind(0)
+            else:
+                parts = [t.contiguous() for t in tp.split([lin.out_features for lin in lins], dim=-1)]
+        return dict(zip(map(id, resnets), parts))
 
     def _forward_tm(self, x, mask, mu, t, packed=None):
         with torch.autocast("cuda", enabled=False):  # [B, 1024] time MLP: tiny, kept fp32
