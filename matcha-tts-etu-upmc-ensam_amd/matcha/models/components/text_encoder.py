@@ -131,11 +131,15 @@ class MultiHeadAttention(nn.Module):
             self.key_conv.bias.data.copy_(self.query_conv.bias.data)
         nn.init.xavier_uniform_(self.value_conv.weight)
 
-    def attend_tm(self, x, m, key_bias):
-        """softmax-attention output [B, T, C] of (x * m) before output_conv (text_encoder.py:188-230)."""
+    def qkv_bias(self):
+        return torch.cat([self.query_conv.bias, self.key_conv.bias, self.value_conv.bias])
+
+    def attend_tm(self, x, m, key_bias, qkv_bias=None):
+        """softmax-attention output [B, T, C] of (x * m) before output_conv (text_encoder.py:188-230).
+        qkv_bias: the stacked q|k|v bias when the caller built every layer's at once."""
         T = x.shape[1]
         qkv = O.linear_tm(x, (self.query_conv.weight, self.key_conv.weight, self.value_conv.weight),
-                          torch.cat([self.query_conv.bias, self.key_conv.bias, self.value_conv.bias]), in_scale=m)
+                          self.qkv_bias() if qkv_bias is None else qkv_bias, in_scale=m)
         cos, sin = self.query_rope.tables(T, x.device)  # query_rope and key_rope are the same rotation
         qkv = O.rope_tm(qkv, cos, sin, self.num_heads, self.query_rope.feature_dim)
         p = self.dropout_rate if self.training else 0.0
@@ -192,8 +196,12 @@ class Encoder(nn.Module):
         apply the final x * mask through their input row scale)."""
         p = self.dropout_rate if self.training else 0.0
         key_bias = (m - 1.0) * 1e4  # masked_fill(-1e4) on padded keys
-        for attn, ln1, ffn, ln2 in zip(self.attention_layers, self.norm_layers_1, self.ffn_layers, self.norm_layers_2):
-            o = attn.attend_tm(h, m, key_bias)
+        # every layer's stacked q|k|v bias in one concatenation (one launch instead of one per layer)
+        layers = list(self.attention_layers)
+        biases = torch.cat([b for a in layers for b in (a.query_conv.bias, a.key_conv.bias, a.value_conv.bias)])
+        biases = biases.split([3 * a.query_conv.bias.numel() for a in layers])
+        for attn, ln1, ffn, ln2, qb in zip(layers, self.norm_layers_1, self.ffn_layers, self.norm_layers_2, biases):
+            o = attn.attend_tm(h, m, key_bias, qkv_bias=qb)
             x = O.linear_tm(o, attn.output_conv.weight, attn.output_conv.bias, residual=h, dropout_p=p)
             x = O.layer_norm_tm(x, ln1.weight, ln1.bias, ln1.eps)
             x = ffn.forward_tm(x, m, residual=x, extra_dropout=p)

@@ -171,8 +171,9 @@ class TrainConfig:
 
 
 class Trainer:
-    # opt-in: measured in-step on MI355X the graph step got 0.25 ms SLOWER with weight gradients on a
-    # side stream (11.25 vs 11.01 ms): the ~100 cross-stream edges cost more than the overlap returns
+    # opt-in: measured in-step on MI355X the graph step got SLOWER with weight gradients on a side
+    # stream (round 1: 11.25 vs 11.01 ms; round 2: 9.43 vs 8.57 ms): the ~100 cross-stream edges cost
+    # more than the overlap returns
     side_stream_wgrad = os.environ.get("MTTS_SIDE_WGRAD", "0") == "1"
     defer_grad_sums = os.environ.get("MTTS_DEFER_GRAD_SUMS", "1") != "0"
     # MTTS_FORCE_DP=1: run the data-parallel exchange even at world size 1 (rehearses the bucketed

@@ -31,7 +31,8 @@ def t_ev(fn, iters=20):
 prec_name = sys.argv[1] if len(sys.argv) > 1 else "bf16"
 prec = O.PREC_BF16 if prec_name == "bf16" else O.PREC_FP32
 scheds = [(32, -1, 1), (32, -1, 2), (64, -1, 1), (64, -1, 2), (32, 512, 1), (32, 512, 2), (64, 512, 2),
-          (32, 1024, 1), (32, 1024, 2), (32, 128, 2), (64, 256, 2)] if prec_name == "bf16" else [(32, -1, 1), (32, 512, 1)]
+          (32, 1024, 1), (32, 1024, 2), (32, 128, 2), (64, 256, 2), (32, 64, 1), (32, 128, 1),
+          (32, 192, 1)] if prec_name == "bf16" else [(32, -1, 1), (32, 512, 1)]
 shapes = [("conv3_full_256", 32, 600, 256, 256, 3), ("conv3_half_256", 32, 300, 256, 256, 3),
           ("conv3_full_512", 32, 600, 512, 256, 3), ("lin_full_256_1024", 32, 600, 256, 1024, 1),
           ("lin_full_1024_256", 32, 600, 1024, 256, 1), ("lin_full_256_768", 32, 600, 256, 768, 1),
