@@ -196,12 +196,11 @@ class Encoder(nn.Module):
         apply the final x * mask through their input row scale)."""
         p = self.dropout_rate if self.training else 0.0
         key_bias = (m - 1.0) * 1e4  # masked_fill(-1e4) on padded keys
-        # every layer's stacked q|k|v bias in one concatenation (one launch instead of one per layer)
-        layers = list(self.attention_layers)
-        biases = torch.cat([b for a in layers for b in (a.query_conv.bias, a.key_conv.bias, a.value_conv.bias)])
-        biases = biases.split([3 * a.query_conv.bias.numel() for a in layers])
-        for attn, ln1, ffn, ln2, qb in zip(layers, self.norm_layers_1, self.ffn_layers, self.norm_layers_2, biases):
-            o = attn.attend_tm(h, m, key_bias, qkv_bias=qb)
+        # (one concatenation of every layer's q|k|v bias saved 5 launches but routed the bias gradients
+        # through autograd's SplitBackward, which then reads them on the main stream -- racing the
+        # opt-in side-stream weight gradients; per layer each bias gradient is a direct view)
+        for attn, ln1, ffn, ln2 in zip(self.attention_layers, self.norm_layers_1, self.ffn_layers, self.norm_layers_2):
+            o = attn.attend_tm(h, m, key_bias)
             x = O.linear_tm(o, attn.output_conv.weight, attn.output_conv.bias, residual=h, dropout_p=p)
             x = O.layer_norm_tm(x, ln1.weight, ln1.bias, ln1.eps)
             x = ffn.forward_tm(x, m, residual=x, extra_dropout=p)

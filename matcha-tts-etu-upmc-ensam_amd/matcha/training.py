@@ -363,8 +363,14 @@ class Trainer:
         if self.dp:
             self.reducer.attach_views()
             self.optimizer.bind_grads()  # the table points at the flat buffer's views (fixed addresses)
+        # with a process group up, its watchdog thread polls the events of earlier collectives (e.g. the
+        # eager all-reduce of the torch.distributed transport) at any time; in the default "global"
+        # capture mode such a query from another thread invalidates the capture and aborts the
+        # process.  "thread_local" restricts only this thread (the autograd thread's launches still go
+        # to the capturing stream and its allocations to the graph pool)
+        mode = "thread_local" if (dist.is_available() and dist.is_initialized()) else "global"
         e["g_fb"] = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(e["g_fb"]):
+        with torch.cuda.graph(e["g_fb"], capture_error_mode=mode):
             for p in self.params:
                 p.grad = None  # autograd hands over each fresh gradient: no accumulate kernels
             if self.dp:
@@ -384,7 +390,7 @@ class Trainer:
             if not self.dp:  # the optimizer graph's table points at the (fixed) graph-pool gradients
                 self.optimizer.bind_grads()
             e["g_opt"] = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(e["g_opt"], pool=e["g_fb"].pool()):
+            with torch.cuda.graph(e["g_opt"], pool=e["g_fb"].pool(), capture_error_mode=mode):
                 self._clip_and_update()
         e["opt_keep"] = (self.optimizer._table, self.optimizer._ws)  # the captured kernels read these
         e["overlap"] = overlap

@@ -95,11 +95,15 @@ def test_side_stream_wgrad_matches_main_stream():
         assert torch.equal(g1[n], g0[n]), n
 
 
-def test_deferred_grad_sums_match_immediate():
+@pytest.mark.parametrize("side", [False, True])
+def test_deferred_grad_sums_match_immediate(side):
     """The batched, deferred parameter-gradient sums (csrc/reduce.hip) equal the per-layer ones bitwise
-    on the decoder (same fixed-order sums, one launch instead of one per layer)."""
+    on the decoder (same fixed-order sums, one launch instead of one per layer); side: batches of them
+    run on a side stream while the backward goes on (joined at the context exit)."""
     from matcha.models.components import _ops as OPS
     from matcha.training import synthetic_batch
+
+    OPS._DEFER["side_on"], OPS._DEFER["chunk"] = side, 8
 
     b = synthetic_batch(4, 20, 80, device=DEV)
     m = _model(3)
@@ -113,14 +117,19 @@ def test_deferred_grad_sums_match_immediate():
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 dur, prior, diff, _ = m(**b, t=t, z=z)
             (dur + prior + diff).backward()
-            if defer:
+            if defer and not side:
                 assert N.lib().mtts_pending_reductions() > 50  # queued, not yet run
+            if defer and side:
+                assert OPS._DEFER["side_used"]  # some batches already launched on the side stream
         torch.cuda.synchronize()
         return {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
 
     from matcha import _native as N
 
-    g0, g1 = grads(False), grads(True)
+    try:
+        g0, g1 = grads(False), grads(True)
+    finally:
+        OPS._DEFER["side_on"], OPS._DEFER["chunk"] = False, 24
     assert N.lib().mtts_pending_reductions() == 0
     assert g0.keys() == g1.keys() and len(g0) > 100
     for n in g0:
