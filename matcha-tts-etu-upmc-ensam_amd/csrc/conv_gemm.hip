@@ -994,15 +994,18 @@ extern "C" int mtts_act_dropout_bwd(const float *dy, const float *y, float *dx, 
 // Split of the token rows over blocks: about target_blocks blocks in total, whole KB-row steps.
 constexpr int kWgradMaxTarget = 1024;
 // target_blocks < 0: the sweep's rule (tools/wgrad_sweep.py) -- about 768 rows per split (long enough
-// to amortize the pipeline and the split's slab write) but never fewer than 256 blocks.
+// to amortize the pipeline and the split's slab write) but never fewer than min_blocks (below).
 static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks, int *splits, int *rows_per_split) {
     const int M = p.nb * p.To;
     const int tiles = ((p.N + 127) / 128) * ((p.K + 127) / 128);
-    static const int min_blocks = [] { const char *e = getenv("MTTS_WGRAD_MINBLK"); return e ? atoi(e) : 256; }();
-    // bf16-stored operands: ~3 blocks per CU (each step's loads are half the bytes, so more blocks -- more
-    // steps in flight per CU -- pay for the extra slab traffic: 19200-row conv 49.8 -> 38.4 us with both
-    // operands bf16, 42.8 -> 36.6 with bf16 dY; fp32 operands are neutral: tools/wgrad_store_ab.py)
-    static const int min_blocks16 = [] { const char *e = getenv("MTTS_WGRAD_MINBLK16"); return e ? atoi(e) : 768; }();
+    // More blocks keep more row steps in flight per CU (the kernel is latency-bound) but every split adds
+    // an N x K fp32 slab that the step's batched reduce reads back.  In-kernel, bf16-stored operands liked
+    // ~3 blocks per CU (19200-row conv 49.8 -> 38.4 us, tools/wgrad_store_ab.py), but the whole step --
+    // wgrad + its slab reduce -- is fastest at ~2 blocks per CU for bf16 operands and ~1.5 for fp32 ones
+    // (same-box step sweep, tools/gpu_ab3.sh: 768/256 8.585 ms, 512/256 8.505, 512/384 8.47, 512/512 8.63,
+    // 256/256 8.65; profiles/r02/wgrad_split_sweep.txt)
+    static const int min_blocks = [] { const char *e = getenv("MTTS_WGRAD_MINBLK"); return e ? atoi(e) : 384; }();
+    static const int min_blocks16 = [] { const char *e = getenv("MTTS_WGRAD_MINBLK16"); return e ? atoi(e) : 512; }();
     static const int split_rows = [] { const char *e = getenv("MTTS_WGRAD_ROWS"); return e && atoi(e) > 0 ? atoi(e) : 768; }();
     const int mb = (p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_WGRAD_F_DY_BF16)) ? min_blocks16 : min_blocks;
     int s = target_blocks > 0 ? (target_blocks + tiles - 1) / tiles

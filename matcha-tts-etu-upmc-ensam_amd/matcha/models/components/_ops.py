@@ -609,8 +609,11 @@ class _ConvTM(torch.autograd.Function):
     (nn.Conv1d on x*mask, token-major; act None or ReLU; residual only without act/dropout)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, mask, out_scale, stride, padding, act, dropout_p, residual, out_bf16):
+    def forward(ctx, x, weight, bias, mask, out_scale, stride, padding, act, dropout_p, residual, out_bf16,
+                dx_link=None, dx_link_role=None):
         _check(x, weight, mask, residual)
+        assert dx_link is None or (stride == 1 and dx_link_role in ("give", "take"))
+        ctx.link = (dx_link, dx_link_role)
         assert residual is None or (act == ACT_NONE and dropout_p == 0.0)
         prec = gemm_precision()
         x = _actc(x, prec)
@@ -664,12 +667,20 @@ class _ConvTM(torch.autograd.Function):
         Cout, _, k = weight.shape
         To = dy.shape[1]
         dx = dw = db = None
+        link, role = ctx.link
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)  # in x's storage: a bf16 x (a GroupNorm output) gets a bf16 gradient
             if stride == 1:
                 Wd, Kp = ctx.wd[0]
+                # GradLink "take": the other consumer's dx of the same x (already computed: its backward
+                # ran first) is added in this dgrad's epilogue, (acc + dx_other) * m -- the autograd sum
+                # of the two input gradients without its add kernel (m is 0/1 and dx_other = m * ...)
+                other = link.pop() if role == "take" else None
+                fuse = other is not None and other.dtype == dx.dtype == torch.float32 and other.is_contiguous()
                 _gemm(dy, To, Ti, B, 1, [pad - j for j in range(k)], Cout, Wd, Kp, Cin, dx, Ti, prec=prec,
-                      c_scale=mask)
+                      c_scale=mask, residual=other if fuse else None)
+                if other is not None and not fuse:  # bf16 x: autograd's sum, done here
+                    dx = dx + other
             else:  # stride-2 dgrad = transposed conv = one GEMM per output phase
                 for ph in range(stride):
                     j0 = (ph + pad) % stride  # taps of this phase: j0, j0+stride, ... (a slice: no
@@ -686,7 +697,10 @@ class _ConvTM(torch.autograd.Function):
             db = torch.empty(Cout, device=x.device, dtype=torch.float32) if has_bias else None
             _wgrad(dy, To, 1, 0, x, Ti, To, B, stride, [j - pad for j in range(k)], Cin, Cout, dw,
                    (Cin * k, k, 1), prec=prec, a_scale=mask, db=db)
-        return dx, dw, db, None, None, None, None, None, None, dres, None
+        if role == "give" and dx is not None:  # handed to the "take" conv of the same x (GradLink)
+            link.put(dx)
+            dx = None
+        return dx, dw, db, None, None, None, None, None, None, dres, None, None, None
 
 
 class _ConvTransposeTM(torch.autograd.Function):
@@ -1054,15 +1068,39 @@ class _LayerNormTM(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------------------------ public ops
+class GradLink:
+    """Two stride-1 convs reading the same x (Resnet1D's block1 conv and res_conv, decoder.py:83-86):
+    the one that runs LATER in the forward ("give") hands its input gradient to the earlier one
+    ("take") instead of returning it, and the taker adds it in its dgrad GEMM epilogue -- one GEMM
+    output instead of two plus autograd's add.  Autograd runs the giver's backward first because the
+    taker's output gradient depends on it (the giver's residual input is computed from the taker's
+    output).  If the giver never ran (no input gradient), the taker adds nothing."""
+
+    __slots__ = ("buf",)
+
+    def __init__(self):
+        self.buf = None
+
+    def put(self, t):
+        assert self.buf is None, "GradLink: two gradients handed over"
+        self.buf = t
+
+    def pop(self):
+        t, self.buf = self.buf, None
+        return t
+
+
 def conv_tm(x, weight, bias, mask=None, stride: int = 1, padding: int | None = None, out_scale=None,
-            relu: bool = False, dropout_p: float = 0.0, residual=None, out_bf16: bool = False):
+            relu: bool = False, dropout_p: float = 0.0, residual=None, out_bf16: bool = False,
+            dx_link: GradLink | None = None, dx_link_role: str | None = None):
     """y = (residual + dropout(relu(Conv1d(x * mask)))) * out_scale, token-major.  x [B,T,Cin], weight
-    [Cout,Cin,k] (nn.Conv1d layout, k <= 8), mask/out_scale [B,T] or None.
+    [Cout,Cin,k] (nn.Conv1d layout, k <= 8), mask/out_scale [B,T] or None.  dx_link / dx_link_role
+    ("take" / "give"): see GradLink.
     decoder.py:59,65,78,85,95,192,239,248,251,369-371; text_encoder.py:48-57, 81-96."""
     if padding is None:
         padding = weight.shape[-1] // 2
     return _ConvTM.apply(x, weight, bias, mask, out_scale, stride, padding, ACT_RELU if relu else ACT_NONE,
-                         float(dropout_p), residual, bool(out_bf16))
+                         float(dropout_p), residual, bool(out_bf16), dx_link, dx_link_role)
 
 
 def conv_transpose_tm(x, weight, bias, mask=None):

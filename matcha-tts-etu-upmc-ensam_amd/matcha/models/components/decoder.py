@@ -12,6 +12,7 @@ half-resolution mask as a prefix slice (:311-316), nearest interpolation for odd
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -20,6 +21,9 @@ import torch.nn.functional as F
 from matcha import _native as N
 from matcha.models.components import _ops as O
 from matcha.models.components.transformer import BasicTransformerBlock
+
+# MTTS_RESNET_DX_LINK=0: autograd sums Resnet1D's two input gradients (A/B switch; the sum is the same)
+_DX_LINK = os.environ.get("MTTS_RESNET_DX_LINK", "1") != "0"
 
 
 class SinusoidalPosEmb(nn.Module):
@@ -67,11 +71,13 @@ class Block1D(nn.Module):
             nn.Mish(),
         )
 
-    def forward_tm(self, x, mask, add=None, out_bf16=False):
+    def forward_tm(self, x, mask, add=None, out_bf16=False, dx_link=None):
         """bf16-mixed: the conv output (read only by the GroupNorm) is stored as bf16, and so is the
-        result when out_bf16 (its only consumer is the next conv's GEMM) -- as autocast would hold them."""
+        result when out_bf16 (its only consumer is the next conv's GEMM) -- as autocast would hold them.
+        dx_link: the conv takes the other consumer's input gradient into its dgrad (O.GradLink)."""
         conv, gn = self.block[0], self.block[1]
-        h = O.conv_tm(x, conv.weight, conv.bias, mask, padding=conv.padding[0], out_bf16=True)
+        h = O.conv_tm(x, conv.weight, conv.bias, mask, padding=conv.padding[0], out_bf16=True,
+                      dx_link=dx_link, dx_link_role="take" if dx_link is not None else None)
         return O.group_norm_mish_tm(h, gn.weight, gn.bias, gn.num_groups, mask, add, gn.eps, out_bf16=out_bf16)
 
     def forward(self, x, mask):  # channel-major API of the reference
@@ -93,10 +99,13 @@ class Resnet1D(nn.Module):
         if tproj is None:
             with torch.autocast("cuda", enabled=False):  # [B, C] time projection, fp32
                 tproj = self.mlp(time_emb.float())
-        h = self.block1.forward_tm(x, mask, add=tproj, out_bf16=True)
+        # x feeds block1's conv and res_conv: res_conv's input gradient is added in block1's dgrad epilogue
+        link = O.GradLink() if _DX_LINK and x.requires_grad and torch.is_grad_enabled() else None
+        h = self.block1.forward_tm(x, mask, add=tproj, out_bf16=True, dx_link=link)
         h = self.block2.forward_tm(h, mask)  # fp32: the residual of res_conv's epilogue
         # res_conv(x*m) + h with the add in the GEMM epilogue ((acc + bias) + h, torch's order)
-        return O.conv_tm(x, self.res_conv.weight, self.res_conv.bias, mask, padding=0, residual=h)
+        return O.conv_tm(x, self.res_conv.weight, self.res_conv.bias, mask, padding=0, residual=h,
+                         dx_link=link, dx_link_role="give" if link is not None else None)
 
     def forward(self, x, mask, time_emb):
         return self.forward_tm(x.transpose(1, 2), mask[:, 0], time_emb).transpose(1, 2)
