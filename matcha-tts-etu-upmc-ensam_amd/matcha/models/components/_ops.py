@@ -368,6 +368,12 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     for t, w_ in ((residual, N_), (aux, N_), (C_pre, N_)):
         if t is not None and (t.shape[-1] < w_ or t.numel() < nb * To_full * t.shape[-1]):
             raise ValueError(f"epilogue operand {tuple(t.shape)} too small for N={N_}")
+    # the residual may be a row-strided view (rows ldr apart, e.g. a channel slice of a concat gradient)
+    ldr = 0
+    if residual is not None:
+        ldr = residual.stride(-2) if residual.dim() >= 2 else residual.shape[-1]
+        if residual.stride(-1) != 1 or ldr < N_ or (residual.dim() == 3 and residual.stride(0) != residual.shape[1] * ldr):
+            raise ValueError(f"residual layout {tuple(residual.shape)} / {residual.stride()} not row-strided")
     args = ConvGemmArgs()
     args.A, args.a_scale, args.lda, args.Ti, args.To, args.nb = A.data_ptr(), N.ptr(a_scale), A.shape[-1], Ti, To, nb
     args.in_stride, args.ntaps, args.cin = in_stride, len(offs), cin
@@ -375,7 +381,7 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
         args.off[i] = o
     args.W, args.N, args.K, args.Kp = Wp.data_ptr(), N_, len(offs) * cin, Kp
     args.bias, args.act = N.ptr(bias), act
-    args.residual, args.ldr = N.ptr(residual), (residual.shape[-1] if residual is not None else 0)
+    args.residual, args.ldr = N.ptr(residual), ldr
     args.c_scale = N.ptr(c_scale)
     args.C, args.ldc, args.To_full, args.out_stride, args.out_off = C.data_ptr(), C.shape[-1], To_full, out_stride, out_off
     args.C_pre = N.ptr(C_pre)
@@ -612,7 +618,7 @@ class _ConvTM(torch.autograd.Function):
     def forward(ctx, x, weight, bias, mask, out_scale, stride, padding, act, dropout_p, residual, out_bf16,
                 dx_link=None, dx_link_role=None):
         _check(x, weight, mask, residual)
-        assert dx_link is None or (stride == 1 and dx_link_role in ("give", "take"))
+        assert dx_link is None or dx_link_role == "take" or (stride == 1 and dx_link_role == "give")
         ctx.link = (dx_link, dx_link_role)
         assert residual is None or (act == ACT_NONE and dropout_p == 0.0)
         prec = gemm_precision()
@@ -670,17 +676,18 @@ class _ConvTM(torch.autograd.Function):
         link, role = ctx.link
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)  # in x's storage: a bf16 x (a GroupNorm output) gets a bf16 gradient
+            # GradLink "take": the other consumer's gradient of the same x (already computed: its backward
+            # ran first) is added in this dgrad's epilogue -- the autograd sum of the two input gradients
+            # without its add kernel.  (acc + other) * m equals m * acc + other: m is 0/1 and other is
+            # either m-scaled (a conv's dgrad) or zero wherever m is (the masked decoder rows).  A row-strided
+            # fp32 view (a slice of the up path's concat gradient) is read in place.
+            other = link.pop() if role == "take" else None
+            fuse = (other is not None and other.dtype == dx.dtype == torch.float32 and other.stride(-1) == 1
+                    and other.shape == dx.shape and other.stride(0) == other.shape[1] * other.stride(1))
             if stride == 1:
                 Wd, Kp = ctx.wd[0]
-                # GradLink "take": the other consumer's dx of the same x (already computed: its backward
-                # ran first) is added in this dgrad's epilogue, (acc + dx_other) * m -- the autograd sum
-                # of the two input gradients without its add kernel (m is 0/1 and dx_other = m * ...)
-                other = link.pop() if role == "take" else None
-                fuse = other is not None and other.dtype == dx.dtype == torch.float32 and other.is_contiguous()
                 _gemm(dy, To, Ti, B, 1, [pad - j for j in range(k)], Cout, Wd, Kp, Cin, dx, Ti, prec=prec,
                       c_scale=mask, residual=other if fuse else None)
-                if other is not None and not fuse:  # bf16 x: autograd's sum, done here
-                    dx = dx + other
             else:  # stride-2 dgrad = transposed conv = one GEMM per output phase
                 for ph in range(stride):
                     j0 = (ph + pad) % stride  # taps of this phase: j0, j0+stride, ... (a slice: no
@@ -691,7 +698,9 @@ class _ConvTM(torch.autograd.Function):
                         continue
                     Wd, Kp = ctx.wd[ph]
                     _gemm(dy, To, nrows, B, 1, [(ph + pad - j) // stride for j in js], Cout, Wd, Kp, Cin, dx, Ti,
-                          stride, ph, prec=prec, c_scale=mask)
+                          stride, ph, prec=prec, c_scale=mask, residual=other if fuse else None)
+            if other is not None and not fuse:  # bf16 x or an unusual layout: autograd's sum, done here
+                dx = dx + other
         if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
             dw = torch.empty(weight.shape, device=x.device, dtype=torch.float32)
             db = torch.empty(Cout, device=x.device, dtype=torch.float32) if has_bias else None
@@ -1088,6 +1097,29 @@ class GradLink:
     def pop(self):
         t, self.buf = self.buf, None
         return t
+
+
+class _CatSkipTM(torch.autograd.Function):
+    """[h | skip] on channels (the up path's einops pack, decoder.py:341).  Backward: h's gradient is the
+    first channel slice; skip's slice goes to the skip's earlier consumer through a GradLink (that conv
+    adds it in its dgrad epilogue, reading the slice in place) instead of autograd's strided add."""
+
+    @staticmethod
+    def forward(ctx, h, skip, link):
+        ctx.c1, ctx.link = h.shape[-1], link
+        return torch.cat([h, skip], dim=-1)
+
+    @staticmethod
+    def backward(ctx, d):
+        d1, d2 = d[..., : ctx.c1], d[..., ctx.c1:]
+        if ctx.link is not None:
+            ctx.link.put(d2)
+            d2 = None
+        return d1, d2, None
+
+
+def cat_skip_tm(h, skip, link: "GradLink | None" = None):
+    return _CatSkipTM.apply(h, skip, link)
 
 
 def conv_tm(x, weight, bias, mask=None, stride: int = 1, padding: int | None = None, out_scale=None,

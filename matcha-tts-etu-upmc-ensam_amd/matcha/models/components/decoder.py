@@ -118,8 +118,9 @@ class Downsample1D(nn.Module):
         super().__init__()
         self.conv = nn.Conv1d(dim, dim, kernel_size=3, stride=2, padding=1)
 
-    def forward_tm(self, x, mask):
-        return O.conv_tm(x, self.conv.weight, self.conv.bias, mask, stride=2, padding=1)
+    def forward_tm(self, x, mask, dx_link=None):
+        return O.conv_tm(x, self.conv.weight, self.conv.bias, mask, stride=2, padding=1, dx_link=dx_link,
+                         dx_link_role="take" if dx_link is not None else None)
 
     def forward(self, x):
         return self.conv(x)
@@ -142,8 +143,9 @@ class Upsample1D(nn.Module):
         return self.conv(inputs)
 
 
-def _conv_tm(mod: nn.Conv1d, x, mask):
-    return O.conv_tm(x, mod.weight, mod.bias, mask, stride=mod.stride[0], padding=mod.padding[0])
+def _conv_tm(mod: nn.Conv1d, x, mask, dx_link=None):
+    return O.conv_tm(x, mod.weight, mod.bias, mask, stride=mod.stride[0], padding=mod.padding[0], dx_link=dx_link,
+                     dx_link_role="take" if dx_link is not None else None)
 
 
 class Decoder(nn.Module):
@@ -251,24 +253,28 @@ class Decoder(nn.Module):
         for resnet, tfs, down in self.Downsampling_Blocks:
             m = masks[-1]
             h = self._transformers(tfs, resnet.forward_tm(h, m, temb, tps[id(resnet)]), m)
-            skips.append(h)
+            # the skip feeds this level's down conv and (later) the up path's concat: the concat hands its
+            # slice of the gradient to the down conv's dgrad epilogue (GradLink)
+            link = O.GradLink() if _DX_LINK and h.requires_grad and torch.is_grad_enabled() else None
+            skips.append((h, link))
             if isinstance(down, Downsample1D):
-                h = down.forward_tm(h, m)
+                h = down.forward_tm(h, m, dx_link=link)
                 # prefix slice (:311-316), made contiguous once (every op of the level reads it)
                 masks.append(m[:, : (m.shape[-1] + 1) // 2].contiguous())
             else:
-                h = _conv_tm(down, h, m)
+                h = _conv_tm(down, h, m, dx_link=link)
                 masks.append(m)
         masks = masks[:-1]
         m = masks[-1]
         for resnet, tfs in self.Mid_Blocks:
             h = self._transformers(tfs, resnet.forward_tm(h, m, temb, tps[id(resnet)]), m)
-        for resnet, tfs, up in self.Upsampling_Blocks:
+        n_up = len(self.Upsampling_Blocks)
+        for i_up, (resnet, tfs, up) in enumerate(self.Upsampling_Blocks):
             m = masks.pop()
-            skip = skips.pop()
+            skip, link = skips.pop()
             if h.shape[1] != skip.shape[1]:  # odd T: nearest to the skip length (:338-339)
                 h = F.interpolate(h.transpose(1, 2), size=skip.shape[1], mode="nearest").transpose(1, 2)
-            h = torch.cat([h, skip], dim=-1)
+            h = O.cat_skip_tm(h, skip, link)  # einops pack on channels (:341)
             h = self._transformers(tfs, resnet.forward_tm(h, m, temb, tps[id(resnet)]), m)
             if isinstance(up, Upsample1D):
                 h = up.forward_tm(h, m)
@@ -276,6 +282,8 @@ class Decoder(nn.Module):
             else:
                 h = _conv_tm(up, h, m)
                 new = h.shape[1]
+            if i_up + 1 < n_up:  # the next block pops its own mask: this one is only read by the head
+                continue
             if new > m.shape[-1]:
                 m = F.interpolate(m.unsqueeze(1), size=new, mode="nearest")[:, 0]
             else:

@@ -589,3 +589,75 @@ def test_wgrad_linear_walk_storage(a16, y16, B, T, Cin, Cout, k):
     assert torch.equal(dw, outs[1][0]) and torch.equal(db, outs[1][1])
     assert torch.equal(dw, outs[2][0])  # the bias-free path stages the same values
 
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_grad_link_two_consumers(stride):
+    """GradLink: a later consumer of x hands its input gradient to an earlier conv's dgrad epilogue
+    (Resnet1D's res_conv -> block1 conv; the up path's concat slice -> the down conv).  The sum equals
+    autograd's: fp32 mode, against the same ops without the link; the concat case reads a row-strided
+    slice in place."""
+    from matcha.models.components import _ops as O
+
+    B, T, C = 3, 37, 64
+    m = _mask(B, T, [37, 20, 29])
+    x0 = torch.randn(B, T, C, device=DEV)
+    w1, b1 = torch.randn(C, C, 3, device=DEV) * 0.1, torch.randn(C, device=DEV)
+    w2, b2 = torch.randn(C, C, 1, device=DEV) * 0.1, torch.randn(C, device=DEV)
+    other = torch.randn(B, T, C, device=DEV)
+
+    def run(linked, concat):
+        x = x0.clone().requires_grad_(True)
+        link = O.GradLink() if linked else None
+        y1 = O.conv_tm(x, w1, b1, m, stride=stride, padding=1, dx_link=link, dx_link_role="take" if linked else None)
+        if concat:  # x also enters [other | x]; the first channels' gradient is dropped
+            y2 = O.cat_skip_tm(other, x, link)[..., C:] * m.unsqueeze(-1)
+        else:
+            y2 = O.conv_tm(x, w2, b2, m, padding=0, dx_link=link, dx_link_role="give" if linked else None)
+        return x, y1, y2
+
+    for concat in (False, True):
+        if stride == 2 and not concat:
+            continue  # Resnet1D's convs are stride 1; a stride-2 taker only meets the concat
+        torch.manual_seed(5)
+        g1 = torch.randn(B, (T + 2 - 3) // stride + 1, C, device=DEV)
+        g2 = torch.randn(B, T, C, device=DEV)
+        grads = []
+        for linked in (False, True):
+            x, y1, y2 = run(linked, concat)
+            ((y1 * g1).sum() + (y2 * g2).sum()).backward()
+            grads.append(x.grad.clone())
+        assert rel(grads[1], grads[0]) < 1e-6, (concat, rel(grads[1], grads[0]))
+
+
+def test_decoder_grad_links_match_autograd_sums():
+    """The decoder with its GradLinks (Resnet1D inputs, skip / concat) vs the same decoder with autograd
+    summing the input gradients (MTTS_RESNET_DX_LINK=0 path): same loss, same parameter gradients (fp32
+    mode; the fused sums differ from autograd's only in the sign of masked zeros)."""
+    from matcha.models.components import decoder as D
+
+    torch.manual_seed(11)
+    dec = D.Decoder(in_channels=160, out_channels=80, channels=(256, 256), dropout=0.0, attention_head_dim=64,
+                    n_blocks=1, num_mid_blocks=2, num_heads=2).to(DEV).eval()
+    B, T = 4, 61
+    m = _mask(B, T, [61, 40, 17, 55])
+    x, mu = torch.randn(B, T, 80, device=DEV), torch.randn(B, T, 80, device=DEV)
+    t = torch.rand(B, device=DEV)
+    res = []
+    saved = D._DX_LINK
+    try:
+        for on in (False, True):
+            D._DX_LINK = on
+            dec.zero_grad(set_to_none=True)
+            xr = x.clone().requires_grad_(True)
+            out = dec.forward_tm(xr, m, mu, t)
+            (out * torch.linspace(-1, 1, 80, device=DEV)).sum().backward()
+            res.append((out.detach(), xr.grad.clone(), [p.grad.clone() for p in dec.parameters() if p.grad is not None]))
+    finally:
+        D._DX_LINK = saved
+    (o0, gx0, gp0), (o1, gx1, gp1) = res
+    assert torch.equal(o0, o1)
+    assert rel(gx1, gx0) < 1e-6
+    assert len(gp0) == len(gp1)
+    worst = max(rel(a, b) for a, b in zip(gp1, gp0))
+    assert worst < 1e-5, worst
