@@ -772,9 +772,10 @@ class _LinearTM(torch.autograd.Function):
     several weights stacked along N (the fused q|k|v projection), each receiving its own gradient."""
 
     @staticmethod
-    def forward(ctx, x, bias, residual, dropout_p, in_scale, out_scale, *weights):
+    def forward(ctx, x, bias, residual, dropout_p, in_scale, out_scale, link, *weights):
         _check(x, residual, in_scale, out_scale, *weights)
         prec = gemm_precision()
+        ctx.link = link  # (GradLink, "take" | "give_res") or None
         shp = x.shape
         x2 = _f32c(x).reshape(-1, shp[-1])
         M, K = x2.shape
@@ -819,18 +820,29 @@ class _LinearTM(torch.autograd.Function):
             dyp = torch.zeros(M, Np, device=dy2.device, dtype=torch.float32)  # columns; W^T is packed with
             dyp[:, :Nout] = dy2  # zero columns to Np already, so dgrad is exact; dW/db keep rows < Nout
             dy2 = dyp
+        link, role = ctx.link if ctx.link is not None else (None, None)
+        if role == "give_res" and dres is not None:  # the residual's gradient goes to the taker's dgrad
+            link.put(dres)
+            dres = None
         if ctx.needs_input_grad[0]:
             Wd, Kp = ctx.wd
             dx = torch.empty(M, K, device=dy2.device, dtype=torch.float32)
-            _gemm(dy2, M, M, 1, 1, [0], Np, Wd, Kp, K, dx, M, prec=prec, c_scale=ins)
+            # "take": + the other consumer's gradient of x, (acc + other) * in_scale -- equal to autograd's
+            # sum when `other` vanishes wherever in_scale does (the caller's guarantee, see GradLink users)
+            other = link.pop() if role == "take" else None
+            fuse = other is not None and other.dtype == torch.float32 and other.is_contiguous() and other.numel() == M * K
+            _gemm(dy2, M, M, 1, 1, [0], Np, Wd, Kp, K, dx, M, prec=prec, c_scale=ins,
+                  residual=other.view(M, K) if fuse else None)
             dx = dx.reshape(*shp)
+            if other is not None and not fuse:
+                dx = dx + other
         if any(ctx.needs_input_grad[6:]) or (has_bias and ctx.needs_input_grad[1]):
             dw = torch.empty(Np, K, device=dy2.device, dtype=torch.float32)
             db = torch.empty(Np, device=dy2.device, dtype=torch.float32) if has_bias else None
             _wgrad(dy2, M, 1, 0, x2, M, M, 1, 1, [0], K, Np, dw, (K, 1, 0), prec=prec, db=db, a_scale=ins)
             dws = [d.view(w_shape) for d, w_shape in zip(dw[:Nout].split(rows, dim=0), ctx.wshapes)]
             db = db[:Nout] if db is not None else None
-        return (dx, db, dres, None, None, None, *dws)
+        return (dx, db, dres, None, None, None, None, *dws)
 
 
 class _FeedForwardTM(torch.autograd.Function):
@@ -1152,13 +1164,18 @@ def layer_norm_tm(h, weight, bias, eps: float = 1e-5, relu: bool = False, dropou
     return _LayerNormTM.apply(h, weight, bias, eps, ACT_RELU if relu else ACT_NONE, float(dropout_p))
 
 
-def linear_tm(x, weight, bias=None, residual=None, dropout_p: float = 0.0, in_scale=None, out_scale=None):
+def linear_tm(x, weight, bias=None, residual=None, dropout_p: float = 0.0, in_scale=None, out_scale=None,
+              dx_link: GradLink | None = None, dx_link_role: str | None = None):
     """(residual + dropout((x * in_scale) @ W^T + b)) * out_scale   (diffusers Linear [+ Dropout]
     [+ residual]; the text encoder's masked 1x1 convs).  `weight` may be a tuple of weights stacked along
     the output dim (one GEMM, one gradient per weight); a weight may be an nn.Conv1d weight [N, K, 1].
-    in_scale / out_scale: per-row [B, T] (or [M]) scales, e.g. the sequence mask."""
+    in_scale / out_scale: per-row [B, T] (or [M]) scales, e.g. the sequence mask.
+    dx_link / dx_link_role: "take" adds the linked gradient into dx's dgrad epilogue; "give_res" hands the
+    residual's gradient to it (GradLink)."""
     ws = tuple(weight) if isinstance(weight, (tuple, list)) else (weight,)
-    return _LinearTM.apply(x, bias, residual, float(dropout_p), in_scale, out_scale, *ws)
+    link = (dx_link, dx_link_role) if dx_link is not None else None
+    assert link is None or dx_link_role in ("take", "give_res")
+    return _LinearTM.apply(x, bias, residual, float(dropout_p), in_scale, out_scale, link, *ws)
 
 
 def ff_tm(x, w1, b1, w2, b2, residual=None, dropout_p: float = 0.0):

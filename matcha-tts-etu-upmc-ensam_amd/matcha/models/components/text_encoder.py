@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -30,6 +31,9 @@ import torch.nn as nn
 from matcha import _native as N
 from matcha.models.components import _ops as O
 from matcha.utils.model import sequence_mask
+
+# MTTS_ENCODER_DX_LINK=0: autograd sums each encoder layer's two input gradients (A/B switch)
+_ENC_LINK = os.environ.get("MTTS_ENCODER_DX_LINK", "1") != "0"
 
 
 class ConvReluNorm(nn.Module):
@@ -134,12 +138,14 @@ class MultiHeadAttention(nn.Module):
     def qkv_bias(self):
         return torch.cat([self.query_conv.bias, self.key_conv.bias, self.value_conv.bias])
 
-    def attend_tm(self, x, m, key_bias, qkv_bias=None):
+    def attend_tm(self, x, m, key_bias, qkv_bias=None, dx_link=None):
         """softmax-attention output [B, T, C] of (x * m) before output_conv (text_encoder.py:188-230).
-        qkv_bias: the stacked q|k|v bias when the caller built every layer's at once."""
+        qkv_bias: the stacked q|k|v bias when the caller built every layer's at once.  dx_link: the
+        projection's dgrad takes the linked gradient of x (O.GradLink)."""
         T = x.shape[1]
         qkv = O.linear_tm(x, (self.query_conv.weight, self.key_conv.weight, self.value_conv.weight),
-                          self.qkv_bias() if qkv_bias is None else qkv_bias, in_scale=m)
+                          self.qkv_bias() if qkv_bias is None else qkv_bias, in_scale=m, dx_link=dx_link,
+                          dx_link_role="take" if dx_link is not None else None)
         cos, sin = self.query_rope.tables(T, x.device)  # query_rope and key_rope are the same rotation
         qkv = O.rope_tm(qkv, cos, sin, self.num_heads, self.query_rope.feature_dim)
         p = self.dropout_rate if self.training else 0.0
@@ -200,8 +206,13 @@ class Encoder(nn.Module):
         # through autograd's SplitBackward, which then reads them on the main stream -- racing the
         # opt-in side-stream weight gradients; per layer each bias gradient is a direct view)
         for attn, ln1, ffn, ln2 in zip(self.attention_layers, self.norm_layers_1, self.ffn_layers, self.norm_layers_2):
-            o = attn.attend_tm(h, m, key_bias)
-            x = O.linear_tm(o, attn.output_conv.weight, attn.output_conv.bias, residual=h, dropout_p=p)
+            # h feeds the masked q|k|v projection and output_conv's residual: the residual gradient is added in
+            # the projection's dgrad epilogue ((acc + g) * m; g vanishes on masked rows: it is LN1's input
+            # gradient, and LN1's output only reaches the loss through the FFN's masked output)
+            link = O.GradLink() if _ENC_LINK and h.requires_grad and torch.is_grad_enabled() else None
+            o = attn.attend_tm(h, m, key_bias, dx_link=link)
+            x = O.linear_tm(o, attn.output_conv.weight, attn.output_conv.bias, residual=h, dropout_p=p,
+                            dx_link=link, dx_link_role="give_res" if link is not None else None)
             x = O.layer_norm_tm(x, ln1.weight, ln1.bias, ln1.eps)
             x = ffn.forward_tm(x, m, residual=x, extra_dropout=p)
             h = O.layer_norm_tm(x, ln2.weight, ln2.bias, ln2.eps)

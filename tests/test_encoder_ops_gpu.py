@@ -230,3 +230,34 @@ def test_embedding_fwd_bitwise_bwd_deterministic(B, T, V, C):
     ref = torch.zeros(V, C, dtype=torch.float64, device=DEV).index_add_(0, ids.reshape(-1),
                                                                         (dout * s).reshape(-1, C).double())
     torch.testing.assert_close(g1.double(), ref, rtol=1e-5, atol=1e-4)
+
+
+def test_encoder_grad_link_matches_autograd_sum():
+    """Each encoder layer's output_conv residual gradient is added in the masked q|k|v projection's dgrad
+    epilogue (GradLink) instead of autograd's add: same losses and gradients as with autograd summing
+    them (MTTS_ENCODER_DX_LINK=0 path), fp32 mode, ragged lengths (the masked rows are where the
+    (acc + g) * m identity needs g = 0)."""
+    from matcha.models.components import text_encoder as TE
+    from matcha.models.matcha_tts import MatchaTTS
+    from matcha.training import synthetic_batch
+
+    torch.manual_seed(3)
+    model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(DEV).eval()
+    b = synthetic_batch(5, 33, 80, device=DEV)
+    res = []
+    saved = TE._ENC_LINK
+    try:
+        for on in (False, True):
+            TE._ENC_LINK = on
+            model.zero_grad(set_to_none=True)
+            mu, logw, m = model.encoder(b["x"], b["x_lengths"])
+            ((mu * torch.linspace(-1, 1, mu.shape[1], device=DEV)[:, None]).sum() + logw.square().sum()).backward()
+            grads = [p.grad.clone() for p in model.encoder.parameters() if p.grad is not None]
+            res.append((mu.detach(), logw.detach(), grads))
+    finally:
+        TE._ENC_LINK = saved
+    (mu0, lw0, g0), (mu1, lw1, g1) = res
+    assert torch.equal(mu0, mu1) and torch.equal(lw0, lw1)
+    assert len(g0) == len(g1) and len(g0) > 0
+    worst = max(((a - c).norm() / c.norm().clamp_min(1e-30)).item() for a, c in zip(g1, g0))
+    assert worst < 1e-5, worst
