@@ -1003,7 +1003,7 @@ static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks,
     // ~3 blocks per CU (19200-row conv 49.8 -> 38.4 us, tools/wgrad_store_ab.py), but the whole step --
     // wgrad + its slab reduce -- is fastest at ~2 blocks per CU for bf16 operands and ~1.5 for fp32 ones
     // (same-box step sweep, tools/gpu_ab3.sh: 768/256 8.585 ms, 512/256 8.505, 512/384 8.47, 512/512 8.63,
-    // 256/256 8.65; profiles/r02/wgrad_split_sweep.txt)
+    // 256/256 8.65; profiles/r02/step_ab_round2b.txt)
     static const int min_blocks = [] { const char *e = getenv("MTTS_WGRAD_MINBLK"); return e ? atoi(e) : 384; }();
     static const int min_blocks16 = [] { const char *e = getenv("MTTS_WGRAD_MINBLK16"); return e ? atoi(e) : 512; }();
     static const int split_rows = [] { const char *e = getenv("MTTS_WGRAD_ROWS"); return e && atoi(e) > 0 ? atoi(e) : 768; }();
