@@ -177,6 +177,12 @@ int mtts_dropout_apply(const float *x, float *y, int32_t rows, int32_t cols, int
  * MTTS_ACT_RELU) * keep(seed, r, c) / (1-p) (p > 0).  Rows/cols index like mtts_dropout_apply. */
 int mtts_act_dropout_bwd(const float *dy, const float *y, float *dx, int32_t rows, int32_t cols, int32_t ld,
                          int32_t act, float p, const uint32_t *seed, void *hip_stream);
+/* mtts_act_dropout_bwd with the output's row scale first: dx = (dy * row_scale[r]) -> act' -> dropout
+ * (row_scale [rows] or NULL).  The text encoder FFN's backward through its masked output
+ * (text_encoder.py:253, `* x_mask`) without materialising dy * mask. */
+int mtts_act_dropout_bwd_scaled(const float *dy, const float *y, const float *row_scale, float *dx, int32_t rows,
+                                int32_t cols, int32_t ld, int32_t act, float p, const uint32_t *seed,
+                                void *hip_stream);
 
 /* LayerNorm over the last dim of x [M, C]; mean/rstd [M] saved.  C % 4 == 0, C <= 1024.  Optional
  * fused tail applied to the normalized output: act MTTS_ACT_RELU, then dropout(p) with the

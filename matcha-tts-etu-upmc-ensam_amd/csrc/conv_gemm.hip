@@ -968,12 +968,14 @@ extern "C" int mtts_dropout_apply(const float *x, float *y, int32_t rows, int32_
 // dx = dy * [y > 0] (act RELU) * keep(seed, r, c) / (1-p) (p > 0): the backward of a GEMM epilogue
 // "ReLU -> dropout" from its output y (kept and positive <=> pre-activation positive).
 __global__ void act_dropout_bwd_kernel(const float *__restrict__ dy, const float *__restrict__ y, float *__restrict__ dx,
-                                       int rows, int cols, int ld, int act, float p, const uint32_t *__restrict__ seed) {
+                                       int rows, int cols, int ld, int act, float p, const uint32_t *__restrict__ seed,
+                                       const float *__restrict__ row_scale) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (int64_t)rows * cols) return;
     const int r = (int)(idx / cols), c = (int)(idx - (int64_t)r * cols);
     const size_t o = (size_t)r * ld + c;
     float v = dy[o];
+    if (row_scale) v = v * row_scale[r];
     if (act == MTTS_ACT_RELU && !(y[o] > 0.f)) v = 0.f;
     if (p > 0.f) v = mtts::dropout_keep(seed[0], seed[1], (uint32_t)r, (uint32_t)c, p) ? v * (1.0f / (1.0f - p)) : 0.f;
     dx[o] = v;
@@ -981,13 +983,19 @@ __global__ void act_dropout_bwd_kernel(const float *__restrict__ dy, const float
 
 extern "C" int mtts_act_dropout_bwd(const float *dy, const float *y, float *dx, int32_t rows, int32_t cols, int32_t ld,
                                     int32_t act, float p, const uint32_t *seed, void *hip_stream) {
+    return mtts_act_dropout_bwd_scaled(dy, y, nullptr, dx, rows, cols, ld, act, p, seed, hip_stream);
+}
+
+extern "C" int mtts_act_dropout_bwd_scaled(const float *dy, const float *y, const float *row_scale, float *dx,
+                                           int32_t rows, int32_t cols, int32_t ld, int32_t act, float p,
+                                           const uint32_t *seed, void *hip_stream) {
     MTTS_CHECK_ARG(dy && dx && rows >= 0 && cols >= 0 && ld >= cols && p >= 0.f && p < 1.f && (p == 0.f || seed),
                    "act_dropout_bwd: bad args");
     MTTS_CHECK_ARG(act == MTTS_ACT_NONE || (act == MTTS_ACT_RELU && y), "act_dropout_bwd: act NONE, or RELU with y");
     const int64_t n = (int64_t)rows * cols;
     if (n == 0) return MTTS_OK;
     hipLaunchKernelGGL(act_dropout_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       static_cast<hipStream_t>(hip_stream), dy, y, dx, rows, cols, ld, act, p, seed);
+                       static_cast<hipStream_t>(hip_stream), dy, y, dx, rows, cols, ld, act, p, seed, row_scale);
     return mtts::check_launch("act_dropout_bwd_kernel");
 }
 

@@ -126,6 +126,7 @@ N.register("mtts_layernorm_bwd", ctypes.c_int,
            [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _SZ, _P])
 N.register("mtts_dropout_apply", ctypes.c_int, [_P, _P, _I, _I, _I, _F, _P, _P])
 N.register("mtts_act_dropout_bwd", ctypes.c_int, [_P, _P, _P, _I, _I, _I, _I, _F, _P, _P])
+N.register("mtts_act_dropout_bwd_scaled", ctypes.c_int, [_P, _P, _P, _P, _I, _I, _I, _I, _F, _P, _P])
 N.register("mtts_rope_qk", ctypes.c_int, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P])
 N.register("mtts_pack_weights", ctypes.c_int, [ctypes.POINTER(PackJob), _I, _I, _P])
 N.register("mtts_attention_fwd", ctypes.c_int, [ctypes.POINTER(AttnArgs), _I, _P])
@@ -961,13 +962,24 @@ class _ConvFFNTM(torch.autograd.Function):
         pad = k // 2
         offs = [j - pad for j in range(k)]
         doffs = [pad - j for j in range(k)]
-        g = _f32c(dy) * m.unsqueeze(-1)
-        dres = g if has_res else None
-        dz2 = g
-        if p_out > 0:
+        fuse = ctx.res_is_x and has_res and ctx.needs_input_grad[0]
+        if fuse and p_out > 0:
+            # the masked output's gradient g = dy * m is only read by the dropout backward (which applies
+            # the row mask itself) and as the residual of the input dgrad, where (acc + dy) * m equals
+            # (acc + dy * m) * m for a 0/1 mask: dy is used as is, g never materialised
+            g = _f32c(dy)
             dz2 = torch.empty_like(g)
-            N.check(N.lib().mtts_act_dropout_bwd(g.data_ptr(), None, dz2.data_ptr(), B * T, Cout, Cout, ACT_NONE,
-                                                 float(p_out), s2.data_ptr(), _stream(g)), "mtts_act_dropout_bwd")
+            N.check(N.lib().mtts_act_dropout_bwd_scaled(g.data_ptr(), None, m.data_ptr(), dz2.data_ptr(), B * T, Cout,
+                                                        Cout, ACT_NONE, float(p_out), s2.data_ptr(), _stream(g)),
+                    "mtts_act_dropout_bwd_scaled")
+        else:
+            g = _f32c(dy) * m.unsqueeze(-1)
+            dz2 = g
+            if p_out > 0:
+                dz2 = torch.empty_like(g)
+                N.check(N.lib().mtts_act_dropout_bwd(g.data_ptr(), None, dz2.data_ptr(), B * T, Cout, Cout, ACT_NONE,
+                                                     float(p_out), s2.data_ptr(), _stream(g)), "mtts_act_dropout_bwd")
+        dres = g if has_res else None
         dw2 = torch.empty(w2s, device=x.device, dtype=torch.float32)
         db2 = torch.empty(Cout, device=x.device, dtype=torch.float32)
         _wgrad(dz2, T, 1, 0, h, T, T, B, 1, offs, F_, Cout, dw2, (F_ * k, k, 1), prec=prec, db=db2)
@@ -982,7 +994,6 @@ class _ConvFFNTM(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             W1d, K1d = ctx.w1d
             dx = torch.empty_like(x)
-            fuse = ctx.res_is_x and dres is not None
             # (dgrad + g) * m = dgrad * m + g: g = dy * m already vanishes on the masked rows
             _gemm(dz1, T, T, B, 1, doffs, F_, W1d, K1d, Cin, dx, T, prec=prec, c_scale=m,
                   residual=g if fuse else None)

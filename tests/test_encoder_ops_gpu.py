@@ -43,11 +43,12 @@ def _mask(B, T, seed=0):
     return (torch.arange(T)[None] < lens[:, None]).float().to(DEV)
 
 
-def test_rope_matches_reference_formula():
+@pytest.mark.parametrize("d", [96, 20])  # 96: the float4 kernel (the model's head dim); 20: the scalar one
+def test_rope_matches_reference_formula(d):
     from matcha.models.components import _ops as O
     from matcha.models.components.text_encoder import RotaryPositionalEmbeddings
 
-    B, T, H, d = 3, 37, 2, 96
+    B, T, H = 3, 37, 2
     qkv = torch.randn(B, T, 3 * H * d, device=DEV, requires_grad=True)
     rp = RotaryPositionalEmbeddings(d * 0.5)
     cos, sin = rp.tables(T, DEV)
@@ -261,3 +262,28 @@ def test_encoder_grad_link_matches_autograd_sum():
     assert len(g0) == len(g1) and len(g0) > 0
     worst = max(((a - c).norm() / c.norm().clamp_min(1e-30)).item() for a, c in zip(g1, g0))
     assert worst < 1e-5, worst
+
+
+@pytest.mark.parametrize("inverse", [0, 1])
+def test_rope_vector_and_scalar_kernels_bitwise(inverse):
+    """The float4 RoPE kernel (16-byte aligned operands) and the scalar one (an unaligned view forces it)
+    round identically -- the fp32 headline alignment is decided by ulp-level near-ties of mu_x."""
+    from matcha import _native as N
+    from matcha.models.components import _ops as O  # noqa: F401  (registers the symbols)
+    from matcha.models.components.text_encoder import RotaryPositionalEmbeddings
+
+    B, T, H, d = 4, 61, 2, 96
+    rp = RotaryPositionalEmbeddings(d * 0.5)
+    cos, sin = rp.tables(T, DEV)
+    n = B * T * 3 * H * d
+    x0 = torch.randn(n, device=DEV)
+    outs = []
+    for off in (0, 1):  # off 1: x / y not 16-byte aligned -> scalar kernel
+        x = torch.empty(n + 4, device=DEV)[off: off + n]
+        x.copy_(x0)
+        buf = torch.empty(n + 4, device=DEV)
+        y = buf[off: off + n]
+        N.check(N.lib().mtts_rope_qk(x.data_ptr(), y.data_ptr(), B * T, T, H * d, H, rp.feature_dim, cos.data_ptr(),
+                                     sin.data_ptr(), inverse, torch.cuda.current_stream().cuda_stream), "mtts_rope_qk")
+        outs.append(y.clone())
+    assert torch.equal(outs[0], outs[1])
