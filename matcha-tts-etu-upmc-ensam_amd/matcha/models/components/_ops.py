@@ -354,6 +354,28 @@ def _events(dev):
     return st, e0, e1
 
 
+def _ld(t: torch.Tensor) -> int:
+    """Row stride (elements) of a GEMM operand: contiguous, or a row-strided view (unit element stride,
+    rows ld apart, batches T * ld apart -- e.g. a channel slice of the up path's concat gradient)."""
+    if t.dim() < 2 or t.is_contiguous():
+        return t.shape[-1]
+    if t.dim() > 3 or t.stride(-1) != 1 or (t.dim() == 3 and t.stride(0) != t.shape[1] * t.stride(1)):
+        raise ValueError(f"operand layout {tuple(t.shape)} / {t.stride()} is not row-strided")
+    return t.stride(-2)
+
+
+_ROW_STRIDED = os.environ.get("MTTS_ROW_STRIDED", "1") != "0"
+
+
+def _row_strided_f32(t: torch.Tensor) -> bool:
+    if not _ROW_STRIDED:
+        return False
+    try:
+        return t.dtype == torch.float32 and t.dim() == 3 and _ld(t) >= t.shape[-1]
+    except ValueError:
+        return False
+
+
 def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_stride=1, out_off=0, *, prec,
           a_scale=None, bias=None, act=ACT_NONE, residual=None, c_scale=None, C_pre=None, aux=None,
           dropout_p=0.0, seed=None, tile_cfg=-1, binary_scale=True, splits=0):
@@ -376,7 +398,7 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
         if residual.stride(-1) != 1 or ldr < N_ or (residual.dim() == 3 and residual.stride(0) != residual.shape[1] * ldr):
             raise ValueError(f"residual layout {tuple(residual.shape)} / {residual.stride()} not row-strided")
     args = ConvGemmArgs()
-    args.A, args.a_scale, args.lda, args.Ti, args.To, args.nb = A.data_ptr(), N.ptr(a_scale), A.shape[-1], Ti, To, nb
+    args.A, args.a_scale, args.lda, args.Ti, args.To, args.nb = A.data_ptr(), N.ptr(a_scale), _ld(A), Ti, To, nb
     args.in_stride, args.ntaps, args.cin = in_stride, len(offs), cin
     for i, o in enumerate(offs):
         args.off[i] = o
@@ -580,8 +602,8 @@ def _wgrad(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin
 def _wgrad_launch(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin, N_, dw, strides, *, prec,
                   a_scale=None, db=None, rows_per_step=-1, target_blocks=-1, depth=-1):
     args = ConvWgradArgs()
-    args.dY, args.ldy, args.To_full, args.out_stride, args.out_off = dY.data_ptr(), dY.shape[-1], To_full, out_stride, out_off
-    args.A, args.a_scale, args.lda, args.Ti, args.To, args.nb = A.data_ptr(), N.ptr(a_scale), A.shape[-1], Ti, To, nb
+    args.dY, args.ldy, args.To_full, args.out_stride, args.out_off = dY.data_ptr(), _ld(dY), To_full, out_stride, out_off
+    args.A, args.a_scale, args.lda, args.Ti, args.To, args.nb = A.data_ptr(), N.ptr(a_scale), _ld(A), Ti, To, nb
     args.in_stride, args.ntaps, args.cin = in_stride, len(offs), cin
     for i, o in enumerate(offs):
         args.off[i] = o
@@ -746,7 +768,8 @@ class _ConvTransposeTM(torch.autograd.Function):
     def backward(ctx, dy):
         x, weight, mask = ctx.saved_tensors
         prec, has_bias = ctx.cfg
-        dy = _f32c(dy)
+        # the up path hands a channel slice of its concat gradient: read in place (row-strided operand)
+        dy = dy if _row_strided_f32(dy) else _f32c(dy)
         B, T, Cin = x.shape
         _, Cout, k = weight.shape
         pad, s = 1, 2
@@ -764,6 +787,9 @@ class _ConvTransposeTM(torch.autograd.Function):
             _wgrad(xm, T, 1, 0, dy, T2, T, B, s, offs, Cout, Cin, dw,
                    (weight.stride(0), weight.stride(1), weight.stride(2)), prec=prec)
         if has_bias and ctx.needs_input_grad[2]:
+            # one column reduction (25.8 us at 32 x 600 x 256).  NOT dy.sum(1).sum(0): torch picks that
+            # reduction's vectorisation from the input's address, so its rounding changed between the
+            # data-parallel and the plain graph step (tests/test_dp_gpu.py equality failed)
             db = dy.sum(dim=(0, 1))
         return dx, dw, db, None
 

@@ -661,3 +661,20 @@ def test_decoder_grad_links_match_autograd_sums():
     assert len(gp0) == len(gp1)
     worst = max(rel(a, b) for a, b in zip(gp1, gp0))
     assert worst < 1e-5, worst
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_conv_transpose_tm_row_strided_grad(prec):
+    """The transposed conv's backward reads a channel slice of a concat gradient in place (row-strided
+    dgrad / wgrad operand, decoder up path) -- same gradients as the torch reference."""
+    from matcha.models.components._ops import conv_transpose_tm
+
+    B, T, C = 3, 45, 64
+    x = torch.randn(B, T, C, device=DEV, requires_grad=True)
+    w = (torch.randn(C, C, 4, device=DEV) / math.sqrt(C * 2)).requires_grad_(True)
+    b = torch.randn(C, device=DEV, requires_grad=True)
+    m = _mask(B, T, [T, T - 7, T - 20])
+    other = torch.randn(B, 2 * T, 32, device=DEV)
+    ref = lambda x, w, b: torch.cat(  # noqa: E731
+        [F.conv_transpose1d((x * m[..., None]).transpose(1, 2), w, b, 2, 1).transpose(1, 2), other], -1)
+    _run(lambda x, w, b: torch.cat([conv_transpose_tm(x, w, b, m), other], -1), ref, [x, w, b], prec)
