@@ -368,9 +368,16 @@ struct WgradGeom {
 // its tap-j A row m + off_j, so the per-step address advance is one uniform offset (rb * ld) and only
 // the tap validity needs the row's position u in its sequence (~12 instead of ~22 vector instructions
 // per staged row; the bias column sums only in the k-tile-0 blocks, behind a block-uniform branch).
-template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false, bool LIN = false>
-__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_args p, int rows_per_split,
-                                                               float *__restrict__ part, float *__restrict__ part_db) {
+// HV = 2: two 4-wave halves per workgroup reduce the two halves of the split's row range into the same
+// 128 x 128 tile (own LDS rings, one shared barrier sequence: both halves run the same step count, rows
+// past their range masked), then add (half 0 + half 1, fixed order) before ONE slab write: the same waves
+// per CU as twice the workgroups, half the partial slabs that the step's batched reduce re-reads.
+template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false, bool LIN = false, int HV = 1>
+__global__ __launch_bounds__(kThreads * HV) void conv_wgrad_kernel(mtts_conv_wgrad_args p, int rows_per_split,
+                                                                    float *__restrict__ part, float *__restrict__ part_db) {
+    static_assert(HV == 1 || (HV == 2 && DEPTH == 1), "two halves: one step in flight");
+    static_assert(HV == 1 || (size_t)64 * kThreads * sizeof(float) <= 2 * WgradGeom<BF16, KB>::kLds,
+                  "half 1's accumulators fit the two halves' LDS");
     static_assert(!ABF16 || BF16, "bf16 A needs the bf16 path");
     static_assert(!YBF16 || BF16, "bf16 dY needs the bf16 path");
     static_assert(!LIN || INC, "the linear row walk is a special case of the incremental one");
@@ -380,10 +387,11 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
     using ST = typename Gm::ST;
     constexpr int T = Gm::T, LDR = Gm::LDR, LDW = Gm::LDW, IMG = Gm::kImg, CH = Gm::CH;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    ST *Ybuf = reinterpret_cast<ST *>(smem);  // [2][IMG] then Xs [2][IMG]
+    const int hv = HV == 2 ? (int)(threadIdx.x >> 8) : 0;  // this thread's half
+    ST *Ybuf = reinterpret_cast<ST *>(smem) + hv * 4 * IMG;  // per half: [2][IMG] then Xs [2][IMG]
     ST *Xbuf = Ybuf + 2 * IMG;
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = (int)threadIdx.x & (kThreads - 1), lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
     const int lr = lane & 31, lh = lane >> 5;
     // 1-D grid relabelled XCD-contiguous (as conv_gemm_kernel), tiles numbered n-fastest, then k, then
@@ -401,8 +409,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
         k0 = ktile * T;
     }
     const int M = p.nb * p.To;
-    const int r_begin = split * rows_per_split;
-    const int r_end = min(M, r_begin + rows_per_split);
+    // HV = 2: rows_per_split is a multiple of 2 KB; half h takes [split start + h * rows / 2, + rows / 2)
+    const int h_rows = rows_per_split / HV;
+    const int r_begin = split * rows_per_split + hv * h_rows;
+    const int r_end = min(M, r_begin + h_rows);
     const bool do_db = (ktile == 0) && part_db != nullptr;
     const float inv_to = 1.0f / (float)p.To;
 
@@ -656,7 +666,39 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
         }
     };
 
-    if (r_begin < r_end) {
+    if constexpr (HV == 2) {
+        // both halves: the same step count (block-wide barriers), rows past r_end masked by load()
+        load(R0, r_begin);
+        int buf = 0;
+        for (int s = 0; s < h_rows / KB; ++s) {
+            const int rb = r_begin + s * KB;
+            store(R0, buf);
+            mtts::lds_barrier();
+            load(R0, rb + KB);
+            compute(buf);
+            buf ^= 1;
+        }
+        // half 1's accumulators -> LDS (lane-fastest: conflict-free), half 0 adds them: acc0 + acc1
+        float *xs = reinterpret_cast<float *>(smem);
+        __syncthreads();
+        if (hv == 1) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) xs[((i * 2 + j) * 16 + v) * kThreads + tid] = acc[i][j][v];
+        }
+        __syncthreads();
+        if (hv == 0) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) acc[i][j][v] += xs[((i * 2 + j) * 16 + v) * kThreads + tid];
+        }
+    } else if (r_begin < r_end) {
         if constexpr (DEPTH == 2) {
             load(R0, r_begin);
             load(R1, r_begin + KB);
@@ -688,7 +730,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
 
     float *slab = part + (size_t)split * p.N * p.K;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2 && hv == 0; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int k = k0 + wc * 64 + j * 32 + lr;
@@ -702,17 +744,17 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(mtts_conv_wgrad_ar
     if (do_db) {
         // (row pair, column) partial sums -> LDS scratch (reusing the operand buffers), then a fixed-order
         // sum over the KB/2 row pairs (deterministic, no float atomics)
-        float *dbs = reinterpret_cast<float *>(smem);  // [KB/2][T]
+        float *dbs = reinterpret_cast<float *>(smem);  // [HV][KB/2][T]
         __syncthreads();
 #pragma unroll
         for (int c = 0; c < CH; ++c)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) dbs[c_rp[c] * T + c_cc[c] + i] = colsum[c][i];
+            for (int i = 0; i < 4; ++i) dbs[(hv * (KB / 2) + c_rp[c]) * T + c_cc[c] + i] = colsum[c][i];
         __syncthreads();
-        for (int x = tid; x < T; x += kThreads) {
+        for (int x = (int)threadIdx.x; x < T; x += kThreads * HV) {
             const int n = n0 + x;
             float sacc = 0.f;
-            for (int g = 0; g < KB / 2; ++g) sacc += dbs[g * T + x];
+            for (int g = 0; g < HV * (KB / 2); ++g) sacc += dbs[g * T + x];
             if (n < p.N) part_db[(size_t)split * p.N + n] = sacc;
         }
     }
@@ -1003,7 +1045,8 @@ extern "C" int mtts_act_dropout_bwd_scaled(const float *dy, const float *y, cons
 constexpr int kWgradMaxTarget = 1024;
 // target_blocks < 0: the sweep's rule (tools/wgrad_sweep.py) -- about 768 rows per split (long enough
 // to amortize the pipeline and the split's slab write) but never fewer than min_blocks (below).
-static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks, int *splits, int *rows_per_split) {
+static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks, int *splits, int *rows_per_split,
+                       int hv = 1) {
     const int M = p.nb * p.To;
     const int tiles = ((p.N + 127) / 128) * ((p.K + 127) / 128);
     // More blocks keep more row steps in flight per CU (the kernel is latency-bound) but every split adds
@@ -1015,7 +1058,9 @@ static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks,
     static const int min_blocks = [] { const char *e = getenv("MTTS_WGRAD_MINBLK"); return e ? atoi(e) : 384; }();
     static const int min_blocks16 = [] { const char *e = getenv("MTTS_WGRAD_MINBLK16"); return e ? atoi(e) : 512; }();
     static const int split_rows = [] { const char *e = getenv("MTTS_WGRAD_ROWS"); return e && atoi(e) > 0 ? atoi(e) : 768; }();
-    const int mb = (p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_WGRAD_F_DY_BF16)) ? min_blocks16 : min_blocks;
+    // hv = 2: two-half workgroups (twice the waves each): half the workgroups, rows in whole double steps
+    const int mb = ((p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_WGRAD_F_DY_BF16)) ? min_blocks16 : min_blocks) / hv;
+    kb *= hv;
     int s = target_blocks > 0 ? (target_blocks + tiles - 1) / tiles
                               : max((mb + tiles - 1) / tiles, (M + split_rows / 2) / split_rows);
     s = max(1, min(s, (M + 4 * kb - 1) / (4 * kb)));  // at least 4 steps per split
@@ -1035,21 +1080,39 @@ extern "C" size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *arg
     return mtts::align_up((size_t)splits * args->N * args->K * 4, 256) + (size_t)splits * args->N * 4 + 256;
 }
 
-template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false, bool LIN = false>
-static int wgrad_launch_k(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
-                          hipStream_t st) {
+template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false, bool LIN = false, int HV = 1>
+static int wgrad_launch_hv(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
+                           hipStream_t st) {
     using Gm = WgradGeom<BF16, KB>;
+    constexpr size_t lds = Gm::kLds * HV;
     static bool attr_set = false;
-    if (Gm::kLds > 64 * 1024 && !attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)Gm::kLds) != hipSuccess)
+    if (lds > 64 * 1024 && !attr_set) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN, HV>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return mtts::fail(MTTS_ERR_HIP, "conv_wgrad: LDS attribute");
         attr_set = true;
     }
     dim3 grid((unsigned)(((p.N + 127) / 128) * ((p.K + 127) / 128) * splits));
-    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN>), grid, dim3(kThreads), Gm::kLds,
+    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN, HV>), grid, dim3(kThreads * HV), lds,
                        st, p, rps, part, part_db);
     return mtts::check_launch("conv_wgrad_kernel");
+}
+
+// MTTS_WGRAD_HV=2: the two-half workgroups for the KB = 32, one-step schedules (see conv_wgrad_kernel)
+static int wgrad_hv() {
+    static const int hv = [] { const char *e = getenv("MTTS_WGRAD_HV"); return e && atoi(e) == 2 ? 2 : 1; }();
+    return hv;
+}
+
+template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false, bool LIN = false>
+static int wgrad_launch_k(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
+                          hipStream_t st) {
+    if constexpr (KB == 32 && DEPTH == 1) {
+        // (any split of whole double steps is exact with two halves; the plan makes them so when hv = 2)
+        if (wgrad_hv() == 2 && rps % (2 * KB) == 0)
+            return wgrad_launch_hv<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN, 2>(p, splits, rps, part, part_db, st);
+    }
+    return wgrad_launch_hv<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN, 1>(p, splits, rps, part, part_db, st);
 }
 
 // The linear row walk (LIN): every row's dY / A rows follow from the token row index alone.
@@ -1130,7 +1193,9 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
         return mtts::fail(MTTS_ERR_WORKSPACE, "conv_wgrad: workspace too small");
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
     int splits, rps;
-    wgrad_plan(p, rows_per_step, target_blocks, &splits, &rps);
+    // the two-half workgroups serve the register-staged KB = 32, one-step schedules
+    const int hv = (wgrad_hv() == 2 && rows_per_step == 32 && depth == 1 && !want_glds) ? 2 : 1;
+    wgrad_plan(p, rows_per_step, target_blocks, &splits, &rps, hv);
     float *part = static_cast<float *>(workspace);
     float *part_db = reinterpret_cast<float *>(static_cast<char *>(workspace) +
                                                mtts::align_up((size_t)splits * p.N * p.K * 4, 256));
