@@ -481,7 +481,10 @@ _DEFER = {"on": False, "keep": [], "side_keep": [], "side": {}, "side_used": Fal
           # captured step (8.68 -> 9.25..9.39 ms for chunks of 12/24/48 jobs, same box), like the
           # side-stream weight gradients: the default flushes once at the end
           "side_on": os.environ.get("MTTS_SIDE_REDUCE", "0") == "1",
-          "chunk": int(os.environ.get("MTTS_SIDE_REDUCE_JOBS", "24"))}
+          "chunk": int(os.environ.get("MTTS_SIDE_REDUCE_JOBS", "24")),
+          # > 0: flush on the MAIN stream once this many sums are queued (slabs re-read while still in the
+          # MALL instead of from HBM at the end of the backward)
+          "inline": int(os.environ.get("MTTS_INLINE_REDUCE_JOBS", "0"))}
 
 
 def _leaves(*ts) -> bool:
@@ -533,6 +536,12 @@ def _maybe_side_sums():
     main stream's work so far) while the backward goes on.  Their inputs (partial slabs, kept alive in
     side_keep) and outputs (fresh parameter gradients, which autograd steals without a kernel and
     nothing reads before the join) make this safe."""
+    if _DEFER["on"] and not _DEFER["side_on"] and _DEFER["inline"] > 0:
+        lib = N.lib()
+        if lib.mtts_pending_reductions() >= _DEFER["inline"]:
+            N.check(lib.mtts_flush_reductions(torch.cuda.current_stream().cuda_stream), "mtts_flush_reductions")
+            _DEFER["keep"].clear()  # stream-ordered frees, after the flush launch
+        return
     if not (_DEFER["on"] and _DEFER["side_on"]):
         return
     lib = N.lib()
