@@ -34,6 +34,8 @@ from matcha.utils.model import sequence_mask
 
 # MTTS_ENCODER_DX_LINK=0: autograd sums each encoder layer's two input gradients (A/B switch)
 _ENC_LINK = os.environ.get("MTTS_ENCODER_DX_LINK", "1") != "0"
+# MTTS_QKV_BIAS_ONE_CAT=0: one q|k|v bias concatenation per layer (A/B switch)
+_ONE_BIAS_CAT = os.environ.get("MTTS_QKV_BIAS_ONE_CAT", "1") != "0"
 
 
 class ConvReluNorm(nn.Module):
@@ -202,15 +204,22 @@ class Encoder(nn.Module):
         apply the final x * mask through their input row scale)."""
         p = self.dropout_rate if self.training else 0.0
         key_bias = (m - 1.0) * 1e4  # masked_fill(-1e4) on padded keys
-        # (one concatenation of every layer's q|k|v bias saved 5 launches but routed the bias gradients
-        # through autograd's SplitBackward, which then reads them on the main stream -- racing the
-        # opt-in side-stream weight gradients; per layer each bias gradient is a direct view)
-        for attn, ln1, ffn, ln2 in zip(self.attention_layers, self.norm_layers_1, self.ffn_layers, self.norm_layers_2):
+        # every layer's stacked q|k|v bias from ONE concatenation (one launch instead of one per layer) --
+        # except with the opt-in side-stream weight gradients: the concatenation routes the bias gradients
+        # through autograd's SplitBackward, which reads them on the main stream while the side stream
+        # still writes them; per layer each bias gradient is a direct view
+        layers = list(self.attention_layers)
+        if O._SIDE_WGRAD["on"] or not _ONE_BIAS_CAT:
+            qkv_biases = [None] * len(layers)
+        else:
+            qkv_biases = torch.cat([b for a in layers for b in (a.query_conv.bias, a.key_conv.bias, a.value_conv.bias)])
+            qkv_biases = qkv_biases.split([3 * a.query_conv.bias.numel() for a in layers])
+        for attn, ln1, ffn, ln2, qb in zip(layers, self.norm_layers_1, self.ffn_layers, self.norm_layers_2, qkv_biases):
             # h feeds the masked q|k|v projection and output_conv's residual: the residual gradient is added in
             # the projection's dgrad epilogue ((acc + g) * m; g vanishes on masked rows: it is LN1's input
             # gradient, and LN1's output only reaches the loss through the FFN's masked output)
             link = O.GradLink() if _ENC_LINK and h.requires_grad and torch.is_grad_enabled() else None
-            o = attn.attend_tm(h, m, key_bias, dx_link=link)
+            o = attn.attend_tm(h, m, key_bias, qkv_bias=qb, dx_link=link)
             x = O.linear_tm(o, attn.output_conv.weight, attn.output_conv.bias, residual=h, dropout_p=p,
                             dx_link=link, dx_link_role="give_res" if link is not None else None)
             x = O.layer_norm_tm(x, ln1.weight, ln1.bias, ln1.eps)
