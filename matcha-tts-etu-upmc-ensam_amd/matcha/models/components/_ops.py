@@ -484,7 +484,7 @@ _DEFER = {"on": False, "keep": [], "side_keep": [], "side": {}, "side_used": Fal
           "chunk": int(os.environ.get("MTTS_SIDE_REDUCE_JOBS", "24")),
           # > 0: flush on the MAIN stream once this many sums are queued (slabs re-read while still in the
           # MALL instead of from HBM at the end of the backward)
-          "inline": int(os.environ.get("MTTS_INLINE_REDUCE_JOBS", "0"))}
+          "inline": int(os.environ.get("MTTS_INLINE_REDUCE_JOBS", "8"))}
 
 
 def _leaves(*ts) -> bool:

@@ -95,15 +95,19 @@ def test_side_stream_wgrad_matches_main_stream():
         assert torch.equal(g1[n], g0[n]), n
 
 
-@pytest.mark.parametrize("side", [False, True])
+@pytest.mark.parametrize("side", [False, True, "inline"])
 def test_deferred_grad_sums_match_immediate(side):
     """The batched, deferred parameter-gradient sums (csrc/reduce.hip) equal the per-layer ones bitwise
     on the decoder (same fixed-order sums, one launch instead of one per layer); side: batches of them
-    run on a side stream while the backward goes on (joined at the context exit)."""
+    run on a side stream while the backward goes on (joined at the context exit); "inline": batches of
+    8 flushed on the main stream as they queue up (the default, MTTS_INLINE_REDUCE_JOBS)."""
     from matcha.models.components import _ops as OPS
     from matcha.training import synthetic_batch
 
-    OPS._DEFER["side_on"], OPS._DEFER["chunk"] = side, 8
+    inline = side == "inline"
+    side = side is True
+    saved_inline = OPS._DEFER["inline"]
+    OPS._DEFER["side_on"], OPS._DEFER["chunk"], OPS._DEFER["inline"] = side, 8, (8 if inline else 0)
 
     b = synthetic_batch(4, 20, 80, device=DEV)
     m = _model(3)
@@ -117,8 +121,10 @@ def test_deferred_grad_sums_match_immediate(side):
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 dur, prior, diff, _ = m(**b, t=t, z=z)
             (dur + prior + diff).backward()
-            if defer and not side:
+            if defer and not side and not inline:
                 assert N.lib().mtts_pending_reductions() > 50  # queued, not yet run
+            if defer and inline:
+                assert N.lib().mtts_pending_reductions() < 8  # flushed in batches during the backward
             if defer and side:
                 assert OPS._DEFER["side_used"]  # some batches already launched on the side stream
         torch.cuda.synchronize()
@@ -129,7 +135,7 @@ def test_deferred_grad_sums_match_immediate(side):
     try:
         g0, g1 = grads(False), grads(True)
     finally:
-        OPS._DEFER["side_on"], OPS._DEFER["chunk"] = False, 24
+        OPS._DEFER["side_on"], OPS._DEFER["chunk"], OPS._DEFER["inline"] = False, 24, saved_inline
     assert N.lib().mtts_pending_reductions() == 0
     assert g0.keys() == g1.keys() and len(g0) > 100
     for n in g0:
