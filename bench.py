@@ -134,6 +134,28 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _bucketed_batches(B, Tx, Ty, n, rank, world, dev):
+    """n length-bucketed batches for this rank: a synthetic corpus (Ty_i uniform in [Ty/4, Ty], Tx_i about
+    Ty_i * Tx / Ty), the data path's LengthBucketBatchSampler (sorted pools, batches dealt over ranks) and
+    collate with padding quanta 32 (text) / 256 (frames) -- the shapes a bucketed real-data run replays."""
+    from matcha.data_management.ljspeech_datamodule import LengthBucketBatchSampler, collate
+
+    g = torch.Generator().manual_seed(77)
+    N = B * world * 64
+    ty = (Ty * (0.25 + 0.75 * torch.rand(N, generator=g))).long().clamp(2, Ty)
+    tx = torch.minimum((ty.float() * Tx / Ty * (0.8 + 0.2 * torch.rand(N, generator=g))).long().clamp(1, Tx), ty)
+    sampler = LengthBucketBatchSampler(ty, B, num_replicas=world, rank=rank, bucket_batches=32, seed=0)
+    out = []
+    for idx in sampler:
+        items = [dict(x=torch.randint(1, 150, (int(tx[i]),), generator=g), y=torch.randn(80, int(ty[i]), generator=g),
+                      x_lengths=int(tx[i]), y_lengths=int(ty[i])) for i in idx]
+        b = collate(items, x_quantum=32, y_quantum=256)
+        out.append({k: v.to(dev) for k, v in b.items()})
+        if len(out) == n:
+            break
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,6 +169,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-synth", action="store_true", help="skip the synthesise (inference) measurement")
+    ap.add_argument("--bucketed", type=int, default=0,
+                    help="N > 0: cycle N length-bucketed batches (LengthBucketBatchSampler + collate with padding "
+                         "quanta) from a synthetic corpus with Ty in [Ty/4, Ty], Tx ~ Ty * tx/ty; --tx/--ty are "
+                         "the corpus maxima (long-form config 5); N <= the Trainer's graph cache")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -182,20 +208,26 @@ def main():
     graph = not args.no_graph
     trainer = Trainer(model, TrainConfig(precision=args.precision, graph=graph))
     B, Tx, Ty = args.batch, args.tx, args.ty
-    batch = synthetic_batch(B, Tx, Ty, seed=1000 + rank, device=dev)
+    if args.bucketed > 0:
+        batches = _bucketed_batches(B, Tx, Ty, args.bucketed, rank, world, dev)
+        batch = batches[0]
+        args.warmup = max(args.warmup, 2 * len(batches))  # every padded shape captured before timing
+    else:
+        batch = synthetic_batch(B, Tx, Ty, seed=1000 + rank, device=dev)
+        batches = [batch]
 
     mas_events: list = []
     real_mp = MA.maximum_path
 
-    for _ in range(args.warmup):
-        trainer.step([batch])
+    for i in range(args.warmup):
+        trainer.step([batches[i % len(batches)]])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        trainer.step([batch])
+    for i in range(args.steps):
+        trainer.step([batches[i % len(batches)]])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -205,6 +237,8 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
     losses = trainer.last_losses.tolist()
+    if args.bucketed > 0:  # the per-batch measurements below run on batches[0]'s padded shape
+        Tx, Ty = int(batch["x"].shape[1]), int(batch["y"].shape[2])
 
     # time maximum_path with HIP events on THIS batch's fp32 lattice (same kernels, same stream),
     # right after the timed region; the step itself runs the fused lattice + DP
@@ -391,7 +425,14 @@ def main():
                                    f"B={B}/GPU, Tx={Tx}, Ty={Ty}, 80 mels",
                        "model": "MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192)",
                        "global_batch": world * B, "seq_len": Ty, "text_len": Tx, "parallelism": f"dp{world}",
-                       "precision": args.precision, "hip_graph": graph},
+                       "precision": args.precision, "hip_graph": graph,
+                       **({"bucketed_batches": [[int(v) for v in (b["x"].shape[1], b["y"].shape[2],
+                                                                     b["x_lengths"].min(), b["y_lengths"].min())]
+                                                for b in batches],
+                           "bucketed_note": "per batch: padded Tx, padded Ty, min x_len, min y_len "
+                                            "(LengthBucketBatchSampler, collate quanta 32 / 256); corpus maxima "
+                                            f"Tx={args.tx}, Ty={args.ty}; the per-call lines below use batch 0"}
+                          if args.bucketed > 0 else {})},
             "maximum_path": {"value": round(world * cells / mas_ms / 1e3, 1), "unit": "Mcells/s (whole node)",
                              "ms_per_call": round(mas_ms, 4), "calls": len(mas_events),
                              "fused_prior_maximum_path_ms": round(fused_ms, 4),
