@@ -5,6 +5,11 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+`bench.py --gpus N` (N > 1) run without a launcher starts the N ranks itself: before any GPU call it runs
+torch.distributed.run as a child process (one rank per GPU, 127.0.0.1, a free port) and exits with the
+child's code.  Under a launcher, --gpus must equal WORLD_SIZE.  MTTS_BENCH_SHARED_GPU=1 puts every rank on
+cuda:0 over gloo (a rehearsal of the multi-rank path on a one-GPU box; never a reported number).
+
 A step = forward (text encoder, fp32 log-prior lattice, HIP maximum_path, CFM decoder) + backward +
 grad-norm clip (1.0) + AdamW on B=32 utterances per GPU (Tx=120, Ty=600, 80 mels; BASELINE config 3),
 one process per GPU, data parallel over RCCL.  By default the whole step is one captured HIP graph
@@ -156,6 +161,28 @@ def _bucketed_batches(B, Tx, Ty, n, rank, world, dev):
     return out
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawn_ranks(n: int) -> int:
+    """N ranks for `bench.py --gpus N` without a launcher: torch.distributed.run as a CHILD process (this
+    process has made no GPU call and never execs), each rank re-entering this script with WORLD_SIZE set."""
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver (RCCL)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve()), *sys.argv[1:]]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -175,7 +202,13 @@ def main():
                          "the corpus maxima (long-form config 5); N <= the Trainer's graph cache")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -206,7 +239,7 @@ def main():
     model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(dev)
     model.train()
     graph = not args.no_graph
-    trainer = Trainer(model, TrainConfig(precision=args.precision, graph=graph))
+    trainer = Trainer(model, TrainConfig(precision=args.precision, graph=graph, graph_cache=max(4, args.bucketed)))
     B, Tx, Ty = args.batch, args.tx, args.ty
     if args.bucketed > 0:
         batches = _bucketed_batches(B, Tx, Ty, args.bucketed, rank, world, dev)
@@ -452,8 +485,12 @@ def main():
                              "peak_tflops": FP32_MFMA_TFLOPS if args.precision == "32-true" else BF16_DENSE_TFLOPS},
             "losses": [round(v, 5) for v in losses],
             "dp": None if trainer.reducer is None else {
+                "ranks": int(trainer.reducer.comm.ranks), "transport": type(trainer.reducer.comm).__name__,
+                "backend": trainer.reducer.comm.backend,
+                "rccl_version": getattr(trainer.reducer.comm, "version", None),
+                "shared_gpu": os.environ.get("MTTS_BENCH_SHARED_GPU") == "1",
                 "buckets": len(trainer.reducer.buckets), "bucket_mb": trainer.cfg.bucket_mb,
-                "flat_floats": trainer.reducer.flat.numel(), "transport": type(trainer.reducer.comm).__name__,
+                "flat_floats": trainer.reducer.flat.numel(),
                 "overlapped_in_graph": bool(next(iter(trainer._graphs.values()))["overlap"]) if trainer._graphs else None},
             "precision_check": precision_check,
             "synthesise": synth,

@@ -39,7 +39,6 @@ extern "C" {
 #define MTTS_ACT_DRELU 4 /* zero where aux[row, n] <= 0 -- backward through a ReLU (aux: its output) */
 
 #define MTTS_CONV_MAX_TAPS 8
-#define MTTS_GEMM_PANEL 64 /* mtts_conv_gemm_tile schedule id of the panel kernel */
 #define MTTS_GEMM_GLDS 32  /* schedule ids 32.. : bf16 LDS-DMA kernels (csrc/conv_gemm_glds.hip)   */
 
 /*
@@ -88,8 +87,8 @@ typedef struct mtts_conv_gemm_args {
 
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
 /* Same, with an explicit schedule: 0..17 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;
- * 8..17 bf16-only: 64-wide K steps, two K steps in flight), MTTS_GEMM_PANEL = the bf16 A-resident panel schedule
- * (csrc/conv_gemm_panel.hip), -1 = heuristic.
+ * 8..17 bf16-only: 64-wide K steps, two K steps in flight), MTTS_GEMM_GLDS + i = the bf16 LDS-DMA schedules
+ * (csrc/conv_gemm_glds.hip), -1 = heuristic.
  * For tuning and tests; mtts_conv_gemm picks the configuration itself. */
 int mtts_conv_gemm_tile(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg, void *hip_stream);
 /* With a caller-owned workspace: lets the bf16 LDS-DMA schedules split K over several workgroups
@@ -131,8 +130,7 @@ int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precision, float *
                     int64_t sj, float *db, int32_t accumulate, void *workspace, size_t workspace_bytes,
                     void *hip_stream);
 /* Same, with an explicit schedule: rows_per_step 32 (or 64, bf16), target_blocks 64..1024 for the
- * row split, depth 1 (or 2, bf16) row steps in flight (-1 = defaults); depth 3 with rows_per_step -1 (bf16,
- * fp32 operands) = the LDS-DMA schedule (csrc/wgrad_glds.hip; where it does not apply, the default).  For tuning;
+ * row split, depth 1 (or 2, bf16) row steps in flight (-1 = defaults).  For tuning;
  * mtts_conv_wgrad_workspace_size covers every schedule. */
 int mtts_conv_wgrad_tile(const mtts_conv_wgrad_args *args, int32_t precision, int32_t rows_per_step,
                          int32_t target_blocks, int32_t depth, float *dw, int64_t sn, int64_t sc, int64_t sj,
@@ -346,8 +344,8 @@ int mtts_time_embedding(const float *t, int32_t B, int32_t dim, float scale, flo
 /* ---------------------------------------------------------------------------------------------
  * Token embedding (text_encoder.py:341-342 nn.Embedding, :389 `embedding(x) * sqrt(C)`), csrc/embedding.hip
  * ------------------------------------------------------------------------------------------- */
-/* out[r,:] = weight[ids[r],:] * scale; ids int64 [rows] in [0, V) (validated by the caller: out-of-range ids
- * are clamped, where torch raises a device assert); weight [V,C], out [rows,C] fp32. */
+/* out[r,:] = weight[ids[r],:] * scale; ids int64 [rows] in [0, V); weight [V,C], out [rows,C] fp32.  An
+ * out-of-range id (torch: a device assert) writes a NaN row, so the step's losses turn NaN. */
 int mtts_embedding_fwd(const int64_t *ids, const float *weight, int64_t rows, int32_t V, int32_t C, float scale,
                        float *out, void *hip_stream);
 /* dweight[v,:] = sum over rows r with ids[r]==v of dout[r,:] * scale in a fixed order (overwrites; deterministic,

@@ -27,6 +27,8 @@ int mtts_dp_unique_id(void *id_out, size_t bytes);
 int mtts_dp_comm_init(const void *id, size_t bytes, int32_t nranks, int32_t rank, void **comm_out);
 /* in-place all-reduce of count fp32 values: sum, or the mean over ranks when average != 0 */
 int mtts_dp_allreduce_f32(void *comm, float *buf, int64_t count, int32_t average, void *hip_stream);
+/* the communicator's own view: ranks it spans (ncclCommCount) and this process's rank in it */
+int mtts_dp_comm_query(void *comm, int32_t *nranks_out, int32_t *rank_out);
 int mtts_dp_comm_destroy(void *comm);
 /* the loaded RCCL's version code, -1 if RCCL cannot be loaded */
 int mtts_dp_rccl_version(void);

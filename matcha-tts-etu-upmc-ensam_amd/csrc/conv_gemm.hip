@@ -930,19 +930,12 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     MTTS_CHECK_ARG(!(p.flags & MTTS_GEMM_F_PRE_BF16) || precision == MTTS_PREC_BF16,
                    "conv_gemm: a bf16 pre-activation needs bf16 precision");
     const bool glds_id = cfg >= MTTS_GEMM_GLDS && cfg < MTTS_GEMM_GLDS + mtts::conv_gemm_glds_num_cfgs();
-    MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || cfg == MTTS_GEMM_PANEL || glds_id, "conv_gemm: bad tile config");
+    MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || glds_id, "conv_gemm: bad tile config");
     MTTS_CHECK_ARG(splits >= 0, "conv_gemm: bad split count");
     const int M = p.nb * p.To;
     if (M == 0) return MTTS_OK;
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
     const bool bf16 = precision == MTTS_PREC_BF16;
-    if (cfg == MTTS_GEMM_PANEL) {
-        if (!bf16) return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: panel schedule is bf16 only");
-        if (p.flags & (MTTS_GEMM_F_PRE_BF16 | MTTS_GEMM_F_C_BF16))
-            return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: panel schedule writes fp32 only");
-        if (mtts::conv_gemm_panel_launch(p, st) == 0) return mtts::check_launch("conv_gemm_panel_kernel");
-        return mtts::fail(MTTS_ERR_SHAPE, "conv_gemm: panel schedule does not fit");
-    }
     if (glds_id && (!bf16 || !mtts::conv_gemm_glds_applies(p)))
         return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: LDS-DMA schedule needs bf16, cin >= 64 and a 0/1 a_scale");
     if (p.flags & MTTS_GEMM_F_A_BF16) {  // bf16 A operands exist only in the LDS-DMA kernels
@@ -1168,17 +1161,6 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
     MTTS_CHECK_ARG(p.ldy % 4 == 0 && (uintptr_t)p.dY % 16 == 0, "conv_wgrad: dY rows must be 16-byte aligned");
     MTTS_CHECK_ARG(precision == MTTS_PREC_BF16 || precision == MTTS_PREC_FP32, "conv_wgrad: bad precision");
     const bool bf16 = precision == MTTS_PREC_BF16;
-    // MTTS_WGRAD_GLDS=1: the LDS-DMA schedule (wgrad_glds.hip) for the default bf16 calls.  Opt-in: measured
-    // 10-60 % SLOWER than the register-staged kernel on every step shape (profiles/r02/wgrad_glds/): both
-    // are bound by the ~25-40 GB/s per CU at which the MALL-resident fp32 operands reach a CU, and the
-    // 136 KiB ring allows one workgroup per CU (300-workgroup grids need two rounds)
-    static const bool glds_on = [] { const char *e = getenv("MTTS_WGRAD_GLDS"); return e && atoi(e) != 0; }();
-    // depth 3 asks for it explicitly (its ring keeps three 32-row steps in flight)
-    const bool want_glds = bf16 && ((glds_on && rows_per_step < 0 && depth < 0) || (depth == 3 && rows_per_step < 0));
-    if (depth == 3) {
-        MTTS_CHECK_ARG(bf16 && rows_per_step < 0, "conv_wgrad: depth 3 (LDS-DMA) needs bf16 and the default rows");
-        depth = -1;
-    }
     if (rows_per_step < 0) rows_per_step = 32;
     if (depth < 0) depth = 1;
     if (p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_WGRAD_F_DY_BF16)) {
@@ -1194,7 +1176,7 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
     int splits, rps;
     // the two-half workgroups serve the register-staged KB = 32, one-step schedules
-    const int hv = (wgrad_hv() == 2 && rows_per_step == 32 && depth == 1 && !want_glds) ? 2 : 1;
+    const int hv = (wgrad_hv() == 2 && rows_per_step == 32 && depth == 1) ? 2 : 1;
     wgrad_plan(p, rows_per_step, target_blocks, &splits, &rps, hv);
     float *part = static_cast<float *>(workspace);
     float *part_db = reinterpret_cast<float *>(static_cast<char *>(workspace) +
@@ -1207,15 +1189,7 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
         splits = 1;
     } else {
         float *pdb = db ? part_db : nullptr;
-        // the LDS-DMA kernel runs 4-step (128-row) rounds: splits of whole rounds (fewer, never more splits)
-        const int rps4 = (rps + 127) / 128 * 128, splits4 = (M + rps4 - 1) / rps4;
-        const bool glds = want_glds && mtts::wgrad_glds_applies(p, rps4);  // else: the register kernel
-        if (glds) {
-            rps = rps4;
-            splits = splits4;
-        }
-        rc = glds ? mtts::wgrad_glds_launch(p, splits, rps, part, pdb, st)
-             : !bf16 ? wgrad_launch<false, 32, 1>(p, splits, rps, part, pdb, st)
+        rc = !bf16 ? wgrad_launch<false, 32, 1>(p, splits, rps, part, pdb, st)
              : rows_per_step == 64 ? (depth == 2 ? wgrad_launch<true, 64, 2>(p, splits, rps, part, pdb, st)
                                                  : wgrad_launch<true, 64, 1>(p, splits, rps, part, pdb, st))
                                    : (depth == 2 ? wgrad_launch<true, 32, 2>(p, splits, rps, part, pdb, st)

@@ -32,6 +32,8 @@ struct Rccl {
     decltype(&ncclAllReduce) all_reduce = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
     decltype(&ncclGetVersion) get_version = nullptr;
+    decltype(&ncclCommCount) comm_count = nullptr;
+    decltype(&ncclCommUserRank) comm_user_rank = nullptr;
 };
 
 std::mutex g_mu;
@@ -55,7 +57,10 @@ const Rccl *rccl() {
     r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(h, "ncclAllReduce"));
     r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
     r.get_version = reinterpret_cast<decltype(r.get_version)>(dlsym(h, "ncclGetVersion"));
-    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce || !r.error_string) {
+    r.comm_count = reinterpret_cast<decltype(r.comm_count)>(dlsym(h, "ncclCommCount"));
+    r.comm_user_rank = reinterpret_cast<decltype(r.comm_user_rank)>(dlsym(h, "ncclCommUserRank"));
+    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_reduce || !r.error_string ||
+        !r.comm_count || !r.comm_user_rank) {
         mtts::set_error("dp_comm: librccl lacks an entry point");
         return nullptr;
     }
@@ -103,6 +108,20 @@ extern "C" int mtts_dp_allreduce_f32(void *comm, float *buf, int64_t count, int3
     const ncclResult_t rc = r->all_reduce(buf, buf, (size_t)count, ncclFloat32, average ? ncclAvg : ncclSum,
                                           static_cast<ncclComm_t>(comm), static_cast<hipStream_t>(hip_stream));
     if (rc != ncclSuccess) return rccl_fail(r, rc, "ncclAllReduce");
+    return MTTS_OK;
+}
+
+extern "C" int mtts_dp_comm_query(void *comm, int32_t *nranks_out, int32_t *rank_out) {
+    MTTS_CHECK_ARG(comm && nranks_out && rank_out, "dp_comm_query: bad args");
+    const Rccl *r = rccl();
+    if (!r) return MTTS_ERR_HIP;
+    int n = 0, me = 0;
+    ncclResult_t rc = r->comm_count(static_cast<ncclComm_t>(comm), &n);
+    if (rc != ncclSuccess) return rccl_fail(r, rc, "ncclCommCount");
+    rc = r->comm_user_rank(static_cast<ncclComm_t>(comm), &me);
+    if (rc != ncclSuccess) return rccl_fail(r, rc, "ncclCommUserRank");
+    *nranks_out = n;
+    *rank_out = me;
     return MTTS_OK;
 }
 

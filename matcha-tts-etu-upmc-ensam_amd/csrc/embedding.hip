@@ -24,10 +24,16 @@ __global__ __launch_bounds__(kEThreads) void embedding_fwd_kernel(const int64_t 
                                                                    int V, float scale, float *__restrict__ out) {
     const int64_t r = blockIdx.x;
     if (r >= rows) return;
-    int64_t v = ids[r];
-    v = v < 0 ? 0 : (v >= V ? V - 1 : v);  // ids are validated on the host; clamp keeps reads in bounds
-    const float *src = w + v * C;
+    const int64_t v = ids[r];
     float *dst = out + r * C;
+    if (v < 0 || v >= V) {
+        // nn.Embedding raises a device-side assert on an out-of-range id; a stream-ordered kernel cannot
+        // raise, so the row is poisoned with NaN instead: the losses turn NaN at once, never silently
+        // training on a clamped entry (collate() validates ids on the host as well)
+        for (int c = threadIdx.x; c < C; c += blockDim.x) dst[c] = __builtin_nanf("");
+        return;
+    }
+    const float *src = w + v * C;
     for (int c = threadIdx.x; c < C; c += blockDim.x) dst[c] = src[c] * scale;
 }
 

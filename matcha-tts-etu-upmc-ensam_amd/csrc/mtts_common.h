@@ -105,8 +105,6 @@ __device__ __forceinline__ float epi_act(int act, float v, const float *aux, boo
 
 struct mtts_conv_gemm_args;
 namespace mtts {
-// conv_gemm_panel.hip: A-resident bf16 schedule; returns 0 if launched, 1 if it does not apply.
-int conv_gemm_panel_launch(const mtts_conv_gemm_args &p, hipStream_t st);
 // conv_gemm_glds.hip: bf16 LDS-DMA schedules (ids MTTS_GEMM_GLDS + 0 .. num - 1)
 int conv_gemm_glds_num_cfgs();
 bool conv_gemm_glds_applies(const mtts_conv_gemm_args &p);
@@ -118,10 +116,6 @@ size_t conv_gemm_glds_splitk_bytes(const mtts_conv_gemm_args &p, int splits);
 
 struct mtts_conv_wgrad_args;
 namespace mtts {
-// wgrad_glds.hip: LDS-DMA weight-gradient schedule (fp32 operands, bf16 MFMA)
-bool wgrad_glds_applies(const mtts_conv_wgrad_args &p, int rows_per_split);
-int wgrad_glds_launch(const mtts_conv_wgrad_args &p, int splits, int rows_per_split, float *part, float *part_db,
-                      hipStream_t st);
 }  // namespace mtts
 
 struct mtts_reduce_job;

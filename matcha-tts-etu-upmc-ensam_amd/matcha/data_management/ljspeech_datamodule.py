@@ -22,7 +22,7 @@ def _round_up(n: int, q: int) -> int:
     return -(-n // q) * q
 
 
-def collate(batch, x_quantum: int = 1, y_quantum: int = 1):
+def collate(batch, x_quantum: int = 1, y_quantum: int = 1, n_vocab: int | None = None):
     """ljspeech_datamodule.py:84-109: items {"x": int64 [Tx_i], "y": [n_mels, Ty_i], "x_lengths",
     "y_lengths"} -> padded batch dict (padding value 0).
 
@@ -30,8 +30,15 @@ def collate(batch, x_quantum: int = 1, y_quantum: int = 1):
     batches fall into a few padded shapes and the graph-mode Trainer replays a cached step graph
     instead of capturing one per batch (its LRU cache, TrainConfig.graph_cache).  1 (default) is the
     reference's padding to the batch maximum; a larger padded T only adds masked frames, but the
-    decoder's GroupNorm statistics run over the padded length (decoder.py:58-66), as with bucketing."""
+    decoder's GroupNorm statistics run over the padded length (decoder.py:58-66), as with bucketing.
+
+    n_vocab: when given, token ids outside [0, n_vocab) raise ValueError here, on the host (the
+    reference's nn.Embedding would hit a device assert; the HIP embedding poisons such rows with NaN)."""
     x = [item["x"] for item in batch]
+    if n_vocab is not None:
+        for i, xi in enumerate(x):
+            if xi.numel() and (int(xi.min()) < 0 or int(xi.max()) >= n_vocab):
+                raise ValueError(f"collate: item {i} has token ids outside [0, {n_vocab})")
     x_lengths = torch.tensor([int(item["x_lengths"]) for item in batch])
     y_lengths = torch.tensor([int(item["y_lengths"]) for item in batch])
     x_padded = pad_sequence(x, batch_first=True, padding_value=0)

@@ -37,6 +37,8 @@ N.register("mtts_dp_comm_init", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t,
                                                ctypes.POINTER(ctypes.c_void_p)])
 N.register("mtts_dp_allreduce_f32", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                                    ctypes.c_void_p])
+N.register("mtts_dp_comm_query", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
+                                                ctypes.POINTER(ctypes.c_int32)])
 N.register("mtts_dp_comm_destroy", ctypes.c_int, [ctypes.c_void_p])
 N.register("mtts_dp_rccl_version", ctypes.c_int, [])
 
@@ -49,6 +51,8 @@ class TorchComm:
     def __init__(self, group=None):
         self.group = group
         self.world = dist.get_world_size(group)
+        self.ranks = self.world  # the ranks the collective spans
+        self.backend = dist.get_backend(group)
 
     def all_reduce_mean_(self, t: torch.Tensor) -> None:
         dist.all_reduce(t, group=self.group)
@@ -73,6 +77,14 @@ class RcclComm:
         with torch.cuda.device(device):
             N.check(N.lib().mtts_dp_comm_init(uid, 128, self.world, self.rank, ctypes.byref(self._comm)),
                     "mtts_dp_comm_init")
+        n, me = ctypes.c_int32(), ctypes.c_int32()
+        N.check(N.lib().mtts_dp_comm_query(self._comm, ctypes.byref(n), ctypes.byref(me)), "mtts_dp_comm_query")
+        if (n.value, me.value) != (self.world, self.rank):
+            raise RuntimeError(f"RCCL communicator spans {n.value} ranks as rank {me.value}; torch.distributed "
+                               f"has {self.world} / {self.rank}")
+        self.ranks = n.value  # as RCCL itself reports it (ncclCommCount)
+        self.version = int(N.lib().mtts_dp_rccl_version())
+        self.backend = "rccl"
 
     def all_reduce_mean_(self, t: torch.Tensor) -> None:
         N.check(N.lib().mtts_dp_allreduce_f32(self._comm, t.data_ptr(), t.numel(), 1,
@@ -201,7 +213,17 @@ class GradBucketReducer:
             return
         self.armed = False
         if self._issued != len(self.buckets):
+            # a parameter got no gradient on this rank.  Its peers issue every bucket, so the remaining
+            # ones are issued here too (missing gradients as zeros) before raising: the ranks stay in
+            # one collective sequence instead of blocking forever in unmatched all-reduces
             missing = [i for i, g in enumerate(self.grad_refs) if g is None]
+            for i in missing:
+                self.grad_refs[i] = torch.zeros_like(self.params[i])
+            while self._issued < len(self.buckets):
+                self._issue(self._issued)
+                self._issued += 1
+            if self.overlap and self.stream is not None:
+                torch.cuda.current_stream(self.device).wait_stream(self.stream)
             raise RuntimeError(f"GradBucketReducer: {len(missing)} parameters got no gradient this step "
                                f"(first: index {missing[:3]}); the bucket layout assumes a fixed set")
         if self.overlap:
@@ -218,6 +240,8 @@ class GradBucketReducer:
             p.grad = v
 
     def scalars(self) -> torch.Tensor:
+        """A VIEW of the averaged logged values in the flat buffer: the next step overwrites it (callers
+        that keep it clone it -- Trainer does)."""
         return self.flat[self.n_grad:]
 
     def remove(self) -> None:

@@ -1,27 +1,38 @@
 """Train-step driver: the semantics of the reference's Lightning loop (train.py:81-102,
 baselightningmodule.py:115-162) on one process per GPU.
 
-  - fp32 master weights, AdamW(1e-4, (0.9, 0.999), wd 1e-6) + per-epoch cosine (configure_optimizers)
+  - fp32 master weights, AdamW(1e-4, (0.9, 0.999), eps 1e-8, wd 1e-6) + per-epoch cosine
+    (configure_optimizers)
   - gradient clipping by global norm 1.0 (gradient_clip_val=1.0)
   - gradient accumulation (accumulate_grad_batches; the reference uses 2 x 16 = 32 per step)
   - the step's 4 logged losses reduced in ONE collective (the reference issues one sync_dist
     all-reduce per self.log call)
 
 Two execution modes:
-  graph=True (default on GPU): the whole step is captured once into a HIP graph and replayed -- about
-    a thousand kernel launches per step become one graph launch.  Gradients are NOT pre-allocated:
-    param.grad is None when backward starts, so autograd hands each parameter its freshly computed
-    gradient tensor (no per-parameter accumulate kernel).  N=1: clip + AdamW read those tensors inside
-    the same graph.  N>1: one batched copy packs them into a flat fp32 buffer, data parallelism is a
-    single RCCL all-reduce of that buffer over xGMI, and a second graph runs clip + AdamW on views of
-    it.  Dropout masks
-    (torch's and the HIP epilogues') are drawn from device-side RNG state, so every replay draws new
-    masks.  Inputs are copied into static buffers before each replay.
-  graph=False (eager): torch DDP over RCCL (bucketed all-reduce overlapped with backward, no_sync
-    for non-final accumulation micro-batches).
+  graph=True (default on GPU): the whole step is captured once per input shape into a HIP graph and
+    replayed (shape-keyed LRU cache, TrainConfig.graph_cache) -- about a thousand kernel launches per
+    step become one graph launch.  Gradients are NOT pre-allocated: param.grad is None when backward
+    starts, so autograd hands each parameter its freshly computed gradient tensor (no per-parameter
+    accumulate kernel).  N=1: clip + AdamW (csrc/optim.hip, over one flat parameter array) run in a
+    second graph on those tensors.  N>1 (matcha/dp.py): post-accumulate-grad hooks pack the gradients
+    bucket by bucket into a flat fp32 buffer and fork each bucket's RCCL all-reduce (libmtts_hip's own
+    communicator, capturable) onto a side stream while backward continues; the join, clip and AdamW on
+    views of the reduced buffer are in the SAME graph.  With torch.distributed as the transport (gloo,
+    the shared-GPU rehearsal) the graph only packs, the host reduces the flat buffer, and a second
+    graph steps.  Dropout masks (torch's and the HIP epilogues') come from device-side RNG state, so
+    every replay draws new masks.  Inputs are copied into static buffers before each replay.
+  graph=False (eager): torch DDP over RCCL (bucketed all-reduce overlapped with backward, no_sync for
+    non-final accumulation micro-batches), or the same bucket reducer (dp="buckets").
+
+N>1 graph step: every rank must replay a graph with the same collective sequence, and capturing runs
+warm-up steps that communicate, so the ranks agree on each step's padded shapes first (one small host
+all-reduce over a gloo group, MAX of the padded Tx / Ty; each rank zero-pads to it -- only masked frames
+are added, as collate's quanta do) and therefore capture, replay and evict together.  The bucket layout
+is rank 0's recorded backward order, broadcast once.
 
 Synthetic LJSpeech-shaped batches: token ids ~ U{1..149}, lengths ~ U[0.7 max, max]
-with element 0 = max, mels ~ N(0, 1) zeroed past the length.
+with element 0 = max, mels ~ N(0, 1) zeroed past the length.  A batch dict may carry "t" [B, 1, 1] and
+"z" [B, n_feats, Ty]: the CFM randomness injected for parity tests (MatchaTTS.forward's keywords).
 """
 from __future__ import annotations
 
@@ -164,10 +175,14 @@ class TrainConfig:
     eta_min: float = 1e-6
     t_max_epochs: int = 1000
     # captured steps kept per input-shape key (LRU); collate(x_quantum=16, y_quantum=64) on bucketed batches
-    # keeps real data to ~20 padded shapes (tests/test_data_path.py) -- size the cache to cover them
+    # keeps real data to ~20 padded shapes (tests/test_data_path.py) -- size the cache to cover them.  Each
+    # cached graph keeps its own memory pool holding the whole step's activations and gradients (~2-3 GB at
+    # B=32 x 600 frames bf16-mixed, ~6 GB at B=8 x 4096): 20 shapes fit the MI355X's 288 GB many times
     graph_cache: int = 4
     dp: str = "auto"  # N>1 exchange: "ddp" (eager only), "buckets" (GradBucketReducer), "auto"
     comm: str = "auto"  # bucket reducer transport: "rccl" (capturable, libmtts_hip), "torch", "auto"
+    # N>1 graph step: ranks agree on the padded shapes before every step (see the module docstring)
+    agree_shapes: bool = True
 
 
 class Trainer:
@@ -198,6 +213,10 @@ class Trainer:
         self._recorder = None
         self._arm = None  # (overlap,) while the reducer is to be armed in the next backward
         self._graphs = collections.OrderedDict()
+        # a gloo group for the host-side agreements (padded shapes, bucket layout): never syncs the GPU
+        self._host_group = None
+        if self.dp and self.world > 1:
+            self._host_group = dist.group.WORLD if dist.get_backend() == "gloo" else dist.new_group(backend="gloo")
         if self.dp and self.world > 1:  # identical initial weights on every rank (what DDP's broadcast does)
             for p in model.state_dict().values():
                 dist.broadcast(p, 0)
@@ -234,7 +253,9 @@ class Trainer:
         # side_stream_wgrad): safe when autograd steals every fresh gradient (graph step, one
         # micro-batch, gradients set to None first); joined before this returns
         fresh = n == 1 and self.dev.type == "cuda" and all(p.grad is None for p in self.params)
-        side = self.cfg.graph and fresh and self.side_stream_wgrad
+        # (never with the DP reducer: it packs gradients on the main stream while the side stream may
+        # still be writing them)
+        side = self.cfg.graph and fresh and self.side_stream_wgrad and not self.dp
         # the parameter-gradient partial sums of the whole backward in one batched launch
         # (components/_ops.py deferred_grad_sums): also needs fresh gradients, and no DDP hook
         # reading them during the backward (the bucket reducer flushes the queue per bucket)
@@ -248,9 +269,10 @@ class Trainer:
         for i, batch in enumerate(batches):
             ctx = sync_ctx(i) if sync_ctx else contextlib.nullcontext()
             with ctx:
+                inject = {k: batch[k] for k in ("t", "z") if k in batch}  # parity tests' CFM randomness
                 with self._autocast():
                     dur, prior, diff, _ = self.wrapped(x=batch["x"], x_lengths=batch["x_lengths"],
-                                                       y=batch["y"], y_lengths=batch["y_lengths"])
+                                                       y=batch["y"], y_lengths=batch["y_lengths"], **inject)
                     total = dur + prior + diff
                 vals = torch.stack([dur.detach(), torch.as_tensor(prior).detach(), diff.detach(), total.detach()]).float()
                 logged = vals if logged is None else logged + vals
@@ -280,8 +302,16 @@ class Trainer:
             logged = run_step()
         finally:
             rec.remove()
+        order = rec.order
+        if self.world > 1:  # one bucket layout on every rank: rank 0's recorded backward order
+            index = {id(p): i for i, p in enumerate(self.params)}
+            box = [[index[id(p)] for p in order]]
+            dist.broadcast_object_list(box, src=0, group=self._host_group)
+            if sorted(box[0]) != sorted(index[id(p)] for p in order):
+                raise RuntimeError("data parallel: the ranks differentiate different parameter sets")
+            order = [self.params[i] for i in box[0]]
         comm = DP.make_comm(self.dev, self.cfg.comm)
-        self.reducer = DP.GradBucketReducer(rec.order, comm, self.cfg.bucket_mb, self.dev)
+        self.reducer = DP.GradBucketReducer(order, comm, self.cfg.bucket_mb, self.dev)
         return logged
 
     # ------------------------------------------------------------------------------------ eager
@@ -396,7 +426,30 @@ class Trainer:
         e["overlap"] = overlap
         return e
 
+    def _agree_shapes(self, batches):
+        """N>1 graph step: MAX over ranks of each micro-batch's padded Tx / Ty (and one batch size), then
+        zero padding up to it, so every rank looks up -- and captures, replays, evicts -- the same key."""
+        if not (self.cfg.agree_shapes and self.dp and self.world > 1 and self.cfg.graph):
+            return batches
+        dims = torch.tensor([[b["x"].shape[1], b["y"].shape[2], b["x"].shape[0], -b["x"].shape[0]] for b in batches],
+                            dtype=torch.int64)
+        dist.all_reduce(dims, op=dist.ReduceOp.MAX, group=self._host_group)
+        out = []
+        for b, (tx, ty, bmax, nbmin) in zip(batches, dims.tolist()):
+            if bmax != -nbmin:
+                raise ValueError(f"data parallel graph step: per-rank batch sizes differ ({-nbmin}..{bmax})")
+            b = dict(b)
+            if b["x"].shape[1] < tx:
+                b["x"] = torch.nn.functional.pad(b["x"], (0, tx - b["x"].shape[1]))
+            if b["y"].shape[2] < ty:
+                b["y"] = torch.nn.functional.pad(b["y"], (0, ty - b["y"].shape[2]))
+                if "z" in b:
+                    b["z"] = torch.nn.functional.pad(b["z"], (0, ty - b["z"].shape[2]))
+            out.append(b)
+        return out
+
     def _graph_step(self, batches):
+        batches = self._agree_shapes(batches)
         key = tuple(tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(b.items())) for b in batches)
         e = self._graphs.get(key)
         if e is None:
@@ -417,7 +470,7 @@ class Trainer:
         if not e["overlap"]:  # torch.distributed transport: one eager all-reduce of the packed buffer
             self.reducer.reduce_now()
             e["g_opt"].replay()
-        return self.reducer.scalars()
+        return self.reducer.scalars().clone()  # the flat buffer is overwritten by the next replay
 
     # ------------------------------------------------------------------------------------ api
     def step(self, batches: list[dict]) -> torch.Tensor:

@@ -238,10 +238,10 @@ def test_wgrad_bf16_exact_and_deterministic(B, T, Cin, Cout, k, rows_per_step, t
 
 @pytest.mark.parametrize("B,T,Cin,Cout,k,stride", [(8, 300, 256, 256, 3, 1), (8, 301, 256, 256, 3, 2), (6, 77, 192, 768, 5, 1),
                                                   (4, 64, 512, 160, 1, 1), (32, 40, 96, 200, 3, 1)])
-def test_wgrad_lds_dma_masked_strided(B, T, Cin, Cout, k, stride):
-    """The LDS-DMA wgrad schedule (csrc/wgrad_glds.hip, opt-in MTTS_WGRAD_GLDS=1) with a 0/1 row mask, ragged lengths,
-    stride 2, 1..5 taps and N / K not multiples of the 128 tile: against float64 on bf16-exact operands
-    (1e-5 of the output scale), bitwise repeatable, and equal in value to the register-staged kernel."""
+def test_wgrad_masked_strided(B, T, Cin, Cout, k, stride):
+    """The default bf16 wgrad schedule with a 0/1 row mask, ragged lengths, stride 2, 1..5 taps and N / K not
+    multiples of the 128 tile: against float64 on bf16-exact operands (1e-5 of the output scale), bitwise
+    repeatable, and equal in value to the explicit 32-row one-step schedule."""
     from matcha.models.components import _ops as O
 
     g = torch.Generator(device="cpu").manual_seed(B * T + Cin + k + stride)
@@ -257,7 +257,7 @@ def test_wgrad_lds_dma_masked_strided(B, T, Cin, Cout, k, stride):
                                       padding=pad)
     refb = dy.double().sum((0, 1))
     outs = []
-    for sched in [(-1, -1, 3)] * 2 + [(32, -1, 1)]:  # depth 3: the LDS-DMA schedule
+    for sched in [(-1, -1, -1)] * 2 + [(32, -1, 1)]:
         dw = torch.full((Cout, Cin, k), float("nan"), device=DEV)
         db = torch.full((Cout,), float("nan"), device=DEV)
         O._wgrad(dy, To, 1, 0, x, T, To, B, stride, [j - pad for j in range(k)], Cin, Cout, dw, (Cin * k, k, 1),

@@ -127,3 +127,52 @@ def test_data_parallel_two_ranks_gloo(dp, accumulate, steps):
     for r in (0, 1):
         for got, want in zip(res[r][1], ref_logs):
             torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-7)
+
+
+def _agree_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from matcha.training import TrainConfig, Trainer, synthetic_batch
+
+    torch.manual_seed(0)
+    tr = Trainer(TinyTTS(), TrainConfig(precision="32-true", graph=True, accumulate_grad_batches=2))
+    # rank r: micro-batch shapes (Tx, Ty) differ per rank and per micro-batch
+    shapes = {0: [(12, 40), (9, 48)], 1: [(10, 44), (11, 32)]}[rank]
+    batches = [synthetic_batch(4, tx, ty, seed=rank * 10 + i, device="cpu") for i, (tx, ty) in enumerate(shapes)]
+    for b in batches:
+        b["z"] = torch.randn(4, 80, b["y"].shape[2])
+    out = tr._agree_shapes(batches)
+    got = [(tuple(b["x"].shape), tuple(b["y"].shape), tuple(b["z"].shape)) for b in out]
+    same = all(torch.equal(o["x"][:, :b["x"].shape[1]], b["x"]) and torch.equal(o["y"][..., :b["y"].shape[2]], b["y"])
+               and int(o["x"][:, b["x"].shape[1]:].abs().sum()) == 0 and float(o["y"][..., b["y"].shape[2]:].abs().sum()) == 0
+               and torch.equal(o["x_lengths"], b["x_lengths"]) for o, b in zip(out, batches))
+    # different batch sizes across ranks are refused (they could never share a captured graph)
+    bad = [synthetic_batch(4 + rank, 8, 16, seed=1, device="cpu")] * 2
+    try:
+        tr._agree_shapes(bad)
+        refused = False
+    except ValueError:
+        refused = True
+    q.put((rank, got, same, refused))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_graph_step_shape_agreement_two_ranks_gloo():
+    """Trainer._agree_shapes (the N>1 graph step): every rank pads each micro-batch to the MAX padded
+    Tx / Ty over ranks with zeros (lengths unchanged), so all ranks look up, capture and replay one key."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (g, s, f)) for r, g, s, f in (q.get(timeout=100) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = [((4, 12), (4, 80, 44), (4, 80, 44)), ((4, 11), (4, 80, 48), (4, 80, 48))]
+    for r in (0, 1):
+        assert res[r][0] == want, res[r][0]
+        assert res[r][1] and res[r][2]

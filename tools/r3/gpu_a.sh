@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 3, first GPU pass: the whole -m gpu suite (incl. the 2-rank real-model DP test), the N=1 bench,
+# and `bench.py --gpus 2` self-spawning two ranks on the shared GPU (gloo).
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/${TAG:-r3a}; mkdir -p $O; cd $R
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?
+tail -3 $O/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err; rc=$?
+echo "bench rc=$rc"; cut -c1-300 $O/bench.json; [ $rc -ne 0 ] && { tail -20 $O/bench.err; exit $rc; }
+MTTS_BENCH_SHARED_GPU=1 timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 3 --batch 8 --no-synth > $O/bench_shared2.json 2> $O/bench_shared2.err; rc=$?
+echo "shared2 rc=$rc"; python -c "import json;d=json.loads(open('$O/bench_shared2.json').read().strip().splitlines()[-1]);print(d['n_gpus'],d['dp'],d['value'])" || tail -30 $O/bench_shared2.err
+exit $rc
