@@ -24,6 +24,9 @@ from matcha.models.components.transformer import BasicTransformerBlock
 
 # MTTS_RESNET_DX_LINK=0: autograd sums Resnet1D's two input gradients (A/B switch; the sum is the same)
 _DX_LINK = os.environ.get("MTTS_RESNET_DX_LINK", "1") != "0"
+# MTTS_RESNET_BF16_STORE=0: bf16-mixed keeps the ResNet blocks' conv outputs / GroupNorm outputs in fp32
+# (precision-budget switch, tools/r3/precision_budget.py)
+_RESNET16 = os.environ.get("MTTS_RESNET_BF16_STORE", "1") != "0"
 
 
 class SinusoidalPosEmb(nn.Module):
@@ -76,9 +79,10 @@ class Block1D(nn.Module):
         result when out_bf16 (its only consumer is the next conv's GEMM) -- as autocast would hold them.
         dx_link: the conv takes the other consumer's input gradient into its dgrad (O.GradLink)."""
         conv, gn = self.block[0], self.block[1]
-        h = O.conv_tm(x, conv.weight, conv.bias, mask, padding=conv.padding[0], out_bf16=True,
+        h = O.conv_tm(x, conv.weight, conv.bias, mask, padding=conv.padding[0], out_bf16=_RESNET16,
                       dx_link=dx_link, dx_link_role="take" if dx_link is not None else None)
-        return O.group_norm_mish_tm(h, gn.weight, gn.bias, gn.num_groups, mask, add, gn.eps, out_bf16=out_bf16)
+        return O.group_norm_mish_tm(h, gn.weight, gn.bias, gn.num_groups, mask, add, gn.eps,
+                                    out_bf16=out_bf16 and _RESNET16)
 
     def forward(self, x, mask):  # channel-major API of the reference
         return self.forward_tm(x.transpose(1, 2), mask[:, 0]).transpose(1, 2)
@@ -289,9 +293,9 @@ class Decoder(nn.Module):
             else:
                 m = m[:, :new].contiguous()
         fc = self.final_conv
-        h = O.conv_tm(h, fc.weight, fc.bias, m, stride=fc.stride[0], padding=fc.padding[0], out_bf16=True)
+        h = O.conv_tm(h, fc.weight, fc.bias, m, stride=fc.stride[0], padding=fc.padding[0], out_bf16=_RESNET16)
         h = O.group_norm_mish_tm(h, self.final_norm.weight, self.final_norm.bias, self.final_norm.num_groups,
-                                 None, None, self.final_norm.eps, out_bf16=True)  # no mask after the Mish (:366-368)
+                                 None, None, self.final_norm.eps, out_bf16=_RESNET16)  # no mask after the Mish (:366-368)
         return O.conv_tm(h, self.final_proj.weight, self.final_proj.bias, m, padding=0, out_scale=mask)
 
     def forward(self, x, mask, mu, t, cond=None):

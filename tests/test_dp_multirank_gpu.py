@@ -73,8 +73,9 @@ def _worker(rank, world, port, precision, q):
         logs = [tr.step([b]).cpu() for _ in range(STEPS)]
         torch.cuda.synchronize()
         key = next(iter(tr._graphs))
-        q.put((rank, {n: p.detach().cpu() for n, p in m.named_parameters()}, torch.stack(logs),
-               tr.reducer.comm.ranks, len(tr.reducer.buckets), key))
+        # by value (numpy), not fd-shared tensors: this process may be gone when the parent unpickles
+        q.put((rank, {n: p.detach().cpu().numpy().copy() for n, p in m.named_parameters()}, torch.stack(logs).numpy(),
+               tr.reducer.comm.ranks, len(tr.reducer.buckets), repr(key)))
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -93,7 +94,8 @@ def test_two_ranks_real_model_graph_step_equals_mean_gradient(precision):
     try:
         for _ in range(2):
             rank, params, logs, ranks, nbuckets, key = q.get(timeout=240)
-            res[rank] = (params, logs, ranks, nbuckets, key)
+            res[rank] = ({n: torch.from_numpy(v) for n, v in params.items()}, torch.from_numpy(logs), ranks, nbuckets,
+                         key)
     finally:
         for p in procs:
             p.join(timeout=60)
