@@ -161,6 +161,73 @@ def _bucketed_batches(B, Tx, Ty, n, rank, world, dev):
     return out
 
 
+# kernel families of the step, by the kernel's own name in a rocprofv3 trace
+FAMILIES = {
+    "gemm": ("conv_gemm_kernel", "conv_gemm_glds_kernel", "splitk_epilogue_kernel"),
+    "wgrad": ("conv_wgrad_kernel", "reduce_partials_kernel"),
+    "attn": ("attn_fwd_kernel", "attn_bwd_dq_kernel", "attn_bwd_dkv_kernel"),
+}
+
+
+def _kname(full: str) -> str:
+    import re
+
+    m = re.search(r"::(\w+?)(<|\()", full) or re.search(r"(\w+)", full)
+    return m.group(1) if m else full[:40]
+
+
+def graph_replay_profile(args) -> dict:
+    """Per-kernel durations INSIDE the graph-replayed step: this script re-run as a child under
+    `rocprofv3 --kernel-trace` (warm-up + 4 timed steps, no other measurement), the trace cut at the step
+    boundary (one replay = the fwd/bwd graph + the optimizer graph, ending in adamw_update_kernel), summed
+    per kernel family over the last complete step.  The parent has made its own measurements already; the
+    child runs after them."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+
+    rp = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if Path("/opt/rocm/bin/rocprofv3").exists() else None)
+    if rp is None:
+        return {"error": "rocprofv3 not found"}
+    d = tempfile.mkdtemp(prefix="mtts_prof_", dir="/tmp")
+    cmd = [rp, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable,
+           str(Path(__file__).resolve()), "--profile-child", "--steps", "4", "--warmup", "2", "--batch", str(args.batch),
+           "--tx", str(args.tx), "--ty", str(args.ty), "--precision", args.precision]
+    try:
+        r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), capture_output=True, text=True,
+                           timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"error": "rocprofv3 child timed out"}
+    traces = sorted(Path(d).rglob("*kernel_trace.csv"))
+    if r.returncode != 0 or not traces:
+        return {"error": f"rocprofv3 child rc={r.returncode}: {r.stderr[-300:]}"}
+    rows = sorted(csv.DictReader(open(traces[0])), key=lambda x: int(x["Start_Timestamp"]))
+    ends = [i for i, x in enumerate(rows) if "adamw_update_kernel" in x["Kernel_Name"]]
+    if len(ends) < 2:
+        return {"error": "no complete step in the trace"}
+    seg = rows[ends[-2] + 1: ends[-1] + 1]
+    fam = {k: {"launches": 0, "us": 0.0} for k in FAMILIES}
+    per_kernel = {}
+    busy, t_end = 0.0, int(seg[0]["Start_Timestamp"])
+    for x in seg:
+        st_, en_ = int(x["Start_Timestamp"]), int(x["End_Timestamp"])
+        busy += (en_ - max(st_, t_end)) / 1e3 if en_ > t_end else 0.0
+        t_end = max(t_end, en_)
+        k = _kname(x["Kernel_Name"])
+        per_kernel[k] = per_kernel.get(k, 0.0) + (en_ - st_) / 1e3
+        for f, names in FAMILIES.items():
+            if k in names:
+                fam[f]["us"] += (en_ - st_) / 1e3
+                if k not in ("splitk_epilogue_kernel", "reduce_partials_kernel"):
+                    fam[f]["launches"] += 1
+    span = (int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])) / 1e3
+    top = sorted(per_kernel.items(), key=lambda kv: -kv[1])[:12]
+    shutil.rmtree(d, ignore_errors=True)
+    return {"families": fam, "kernels_per_step": len(seg), "step_span_us": round(span, 1),
+            "step_busy_us": round(busy, 1), "top_kernels_us": {k: round(v, 1) for k, v in top}}
+
+
 def _free_port() -> int:
     import socket
 
@@ -196,6 +263,11 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-synth", action="store_true", help="skip the synthesise (inference) measurement")
+    ap.add_argument("--profile-child", action="store_true", help=argparse.SUPPRESS)  # graph_replay_profile's child
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the same-run 32-true line and the reference step shape (B=16 x accumulate 2)")
+    ap.add_argument("--no-graph-profile", action="store_true",
+                    help="skip the rocprofv3 graph-replay leg (roofline from the eager HIP-event pass only)")
     ap.add_argument("--bucketed", type=int, default=0,
                     help="N > 0: cycle N length-bucketed batches (LengthBucketBatchSampler + collate with padding "
                          "quanta) from a synthetic corpus with Ty in [Ty/4, Ty], Tx ~ Ty * tx/ty; --tx/--ty are "
@@ -269,6 +341,8 @@ def main():
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
+    if args.profile_child:  # under rocprofv3 (graph_replay_profile): the trace is all that is wanted
+        return
     losses = trainer.last_losses.tolist()
     if args.bucketed > 0:  # the per-batch measurements below run on batches[0]'s padded shape
         Tx, Ty = int(batch["x"].shape[1]), int(batch["y"].shape[2])
@@ -314,11 +388,6 @@ def main():
     wgrad_log, OPS.WGRAD_LOG = OPS.WGRAD_LOG, None
     attn_log, OPS.ATTN_LOG = OPS.ATTN_LOG, None
     model.zero_grad(set_to_none=False)
-    gemm_ms = [r[0].elapsed_time(r[1]) for r in gemm_log]
-    gemm_flops = sum(r[2] for r in gemm_log)
-    gemm_bytes = sum(r[4] for r in gemm_log)
-    gemm_avg_us = sum(gemm_ms) / max(len(gemm_ms), 1) * 1e3
-    gemm_tflops = gemm_flops / (sum(gemm_ms) * 1e-3) / 1e12 if gemm_ms else 0.0
 
     # inference: MatchaTTS.synthesise on the same text batch, 10 Euler steps, the ODE
     # replayed as one HIP graph; length_scale 5 gives LJSpeech-like ~5 frames per token
@@ -345,100 +414,135 @@ def main():
                  "note": "wall clock incl. host sync for the predicted lengths; random-init weights, length_scale 5"}
         model.train()
 
-    # bf16-mixed vs 32-true on the bench batch (SURVEY 7 "hard parts"): the same weights, tokens, mels and
-    # injected t / z, eval mode; the 32-true product path equals the CPU oracle at this batch (losses to
-    # 0 relative, alignment bit-exact: tests/test_headline_gpu.py::test_bench_batch_b32_vs_oracle)
+    # bf16-mixed vs 32-true with the parity tests' weights and batch (tests/test_headline_gpu.py::
+    # test_bench_batch_b32_vs_oracle: recipe weights 43, synthetic batch seed 1000 -- the bench batch --, t / z
+    # from a CPU generator seeded 44; the 32-true path equals the CPU oracle there, losses to 0 relative)
     precision_check = None
-    if args.precision == "bf16-mixed":
-        model.eval()
-        gen = torch.Generator(device=dev).manual_seed(44)
-        t_inj = torch.rand(B, 1, 1, generator=gen, device=dev)
-        z_inj = torch.randn(B, 80, Ty, generator=gen, device=dev)
+    if args.precision == "bf16-mixed" and not args.bucketed and (B, Tx, Ty) == (32, 120, 600):
+        sys.path.insert(0, str(ROOT / "tests"))
+        from golden.weights_recipe import apply_recipe
+
+        pm = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(dev)
+        apply_recipe(pm, 43)
+        pm.eval()
+        pb = synthetic_batch(32, 120, 600, seed=1000, device=dev)
+        gen = torch.Generator().manual_seed(44)
+        t_inj = torch.rand(32, 1, 1, generator=gen).to(dev)
+        z_inj = torch.randn(32, 80, 600, generator=gen).to(dev)
         res = {}
         with torch.no_grad():
             for prec in ("32-true", "bf16-mixed"):
                 with torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec == "bf16-mixed"):
-                    out = model(batch["x"], batch["x_lengths"], batch["y"], batch["y_lengths"], t=t_inj, z=z_inj)
+                    out = pm(pb["x"], pb["x_lengths"], pb["y"], pb["y_lengths"], t=t_inj, z=z_inj)
                 res[prec] = ([float(v) for v in out[:3]], out[3].detach())
-        model.train()
+        del pm
         l32, a32 = res["32-true"]
         l16, a16 = res["bf16-mixed"]
         precision_check = {
-            "bf16_loss_rel_err": [round(abs(a - b) / abs(b), 6) for a, b in zip(l16, l32)],
+            "bf16_loss_rel_err": [round(abs(a - b) / abs(b), 7) for a, b in zip(l16, l32)],
             "losses": ["dur", "prior", "diff"],
             "alignment_cell_agreement": round(float((a16 == a32).float().mean().item()), 6),
-            "note": "bf16-mixed vs the 32-true path (= the oracle at this batch) on the bench batch, eval mode, "
-                    "same t / z; the duration loss moves with MAS boundary flips (tests/test_headline_gpu.py)"}
+            "weight_split": OPS._W_SPLIT,
+            "note": "bf16-mixed vs 32-true (= the oracle at this batch) with the parity tests' recipe weights and "
+                    "batch, eval mode, same t / z; bf16 activations x split bf16 weight planes (MTTS_W_SPLIT)"}
+
+    # same-run extra lines (N=1): the reference precision (32-true: exact fp32 MFMA) on the bench workload,
+    # and the reference's own step shape -- 2 micro-batches of 16 with gradient accumulation
+    # (train.py:63,85,88: batch_size 16, accumulate_grad_batches 2) -- in the bench precision
+    extra = None
+    if world == 1 and not args.no_extra and not args.bucketed and graph:
+        extra = {}
+        for name, prec, micro, acc in (("32-true", "32-true", B, 1), ("reference_step_16x2", args.precision, B // 2, 2)):
+            torch.manual_seed(1234)
+            m2 = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(dev).train()
+            tr2 = Trainer(m2, TrainConfig(precision=prec, graph=True, accumulate_grad_batches=acc))
+            bs2 = [synthetic_batch(micro, Tx, Ty, seed=2000 + i, device=dev) for i in range(acc)]
+            for _ in range(3):
+                tr2.step(bs2)
+            n2 = max(5, args.steps // 2)
+            torch.cuda.synchronize()
+            t0x = time.perf_counter()
+            for _ in range(n2):
+                tr2.step(bs2)
+            torch.cuda.synchronize()
+            ms2 = (time.perf_counter() - t0x) / n2 * 1e3
+            extra[name] = {"ms_per_step": round(ms2, 3), "utterances_per_s": round(micro * acc / ms2 * 1e3, 2),
+                           "steps": n2, "precision": prec, "micro_batch": micro, "accumulate_grad_batches": acc,
+                           "losses": [round(v, 5) for v in tr2.last_losses.tolist()]}
+            del tr2, m2
+        torch.cuda.empty_cache()
 
     mas_ms = sum(a.elapsed_time(b) for a, b in mas_events) / max(len(mas_events), 1)
     cells = B * Tx * Ty
     mas_gbs = 12.0 * cells / (mas_ms * 1e-3) / 1e9
     step_ms = elapsed / args.steps * 1e3
     flops = decoder_train_flops(B, Ty)
-    # roofline.traffic: PMC-measured HBM bytes per conv_gemm launch on THIS workload (tools/pmc_traffic.sh
-    # -> profiles/<round>/conv_gemm_traffic.json); PMC passes serialize kernels, so not collected here
-    traffic, traffic_src = None, None
-    if (B, Tx, Ty, args.precision) == (32, 120, 600, "bf16-mixed"):
-        found = sorted(ROOT.glob("profiles/r*/conv_gemm_traffic.json"))
-        if found:
-            traffic = json.loads(found[-1].read_text())["traffic_bytes_per_launch"]
-            traffic_src = str(found[-1].relative_to(ROOT))
     gemm_peak = FP32_MFMA_TFLOPS if args.precision == "32-true" else BF16_DENSE_TFLOPS
-
-    # roofline model of the dominant kernel: attainable = min(MFMA peak, AI x HBM peak).  At this
-    # workload's arithmetic intensity (algorithmic FLOPs / algorithmic bytes) the GEMMs sit below the
-    # ridge point (peak / 8 TB/s), so the binding roof is HBM; the MFMA fraction is reported beside it
-    gemm_time_s = sum(gemm_ms) * 1e-3
-    ai = gemm_flops / max(gemm_bytes, 1)
     ridge = gemm_peak * 1e12 / (HBM_PEAK_GBS * 1e9)
-    gemm_gbs = gemm_bytes / gemm_time_s / 1e9 if gemm_ms else 0.0
-    common = {"kernel": "conv_gemm_kernel (decoder + encoder implicit-GEMM conv/linear, fwd + dgrad)",
-              "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC, FETCH_SIZE x2 + WRITE_SIZE)",
-              "traffic_source": traffic_src,
-              "algorithmic_bytes_per_launch": round(gemm_bytes / max(len(gemm_log), 1)),
-              "algorithmic_flops_per_launch": round(gemm_flops / max(len(gemm_log), 1)),
-              "arithmetic_intensity_flop_per_byte": round(ai, 1), "ridge_flop_per_byte": round(ridge, 1),
-              "launches_per_step": len(gemm_log), "avg_launch_us": round(gemm_avg_us, 2),
-              "algorithmic_flops_per_step": gemm_flops,
-              "mfma_tflops": round(gemm_tflops, 1), "mfma_frac": round(gemm_tflops / gemm_peak, 4),
-              "note": "achieved over sum of launch durations (HIP events on the launch stream, one eager "
-                      "fwd+bwd of the bench batch); bytes = A read once + W + C written (+ aux/residual/"
-                      "pre-activation streams) per launch"}
-    if ai < ridge:
-        gemm_roofline = {"bound": "hbm", "achieved": round(gemm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(gemm_gbs / HBM_PEAK_GBS, 4), **common}
-    else:
-        gemm_roofline = {"bound": "mfma", "achieved": round(gemm_tflops, 1), "peak": gemm_peak,
-                         "unit": "TFLOP/s", "frac": round(gemm_tflops / gemm_peak, 4), **common}
+    # the kernels' durations inside the graph replay that was benchmarked (rocprofv3 child, N=1 only);
+    # the eager HIP-event pass above stays as the secondary figure
+    gprof = None
+    if world == 1 and not args.no_graph_profile and graph:
+        gprof = graph_replay_profile(args)
 
-    def roofline_of(log, kernel, note):
-        """Roofline line of a launch log: bound from the arithmetic intensity vs the ridge point."""
+    def traffic_of(name):
+        """PMC HBM bytes per launch of this family on THIS workload (tools/r3/pmc_families.sh ->
+        profiles/<round>/<name>_traffic.json: FETCH_SIZE x2 + WRITE_SIZE, separate passes); PMC passes
+        serialise kernels, so they are not collected inside the bench."""
+        if (B, Tx, Ty, args.precision) != (32, 120, 600, "bf16-mixed") or args.bucketed:
+            return None, None
+        found = sorted(ROOT.glob(f"profiles/r*/{name}_traffic.json"))
+        if not found:
+            return None, None
+        return json.loads(found[-1].read_text())["traffic_bytes_per_launch"], str(found[-1].relative_to(ROOT))
+
+    def roofline_of(log, fam, kernel, note):
+        """Roofline line of one kernel family: algorithmic FLOPs / bytes per step from the eager launch log
+        (the same launches the graph replays), time from the graph-replay profile when it ran (else the
+        eager HIP events); bound from the arithmetic intensity vs the ridge point."""
         if not log:
             return None
         ms = [r[0].elapsed_time(r[1]) for r in log]
-        t = sum(ms) * 1e-3
+        t_eager = sum(ms) * 1e-3
         fl, by = sum(r[2] for r in log), sum(r[4] for r in log)
+        g = (gprof or {}).get("families", {}).get(fam) if gprof and "families" in gprof else None
+        src = "graph" if g and g["us"] > 0 else "eager"
+        t = g["us"] * 1e-6 if src == "graph" else t_eager
+        n = len(log)
         tf, gb = fl / t / 1e12, by / t / 1e9
         ai = fl / max(by, 1)
-        line = {"kernel": kernel, "launches_per_step": len(log), "avg_launch_us": round(sum(ms) / len(ms) * 1e3, 2),
-                "algorithmic_flops_per_launch": round(fl / len(log)), "algorithmic_bytes_per_launch": round(by / len(log)),
+        traffic, tsrc = traffic_of(fam)
+        line = {"kernel": kernel, "timing": src, "launches_per_step": n,
+                "graph_launches_per_step": g["launches"] if g else None,
+                "avg_launch_us": round(t / n * 1e6, 2),
+                "algorithmic_flops_per_launch": round(fl / n), "algorithmic_bytes_per_launch": round(by / n),
                 "arithmetic_intensity_flop_per_byte": round(ai, 1), "ridge_flop_per_byte": round(ridge, 1),
-                "mfma_tflops": round(tf, 1), "hbm_gbs": round(gb, 1), "traffic": None, "note": note}
+                "mfma_tflops": round(tf, 1), "mfma_frac": round(tf / gemm_peak, 4), "hbm_gbs": round(gb, 1),
+                "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_source": tsrc,
+                "eager_events": {"avg_launch_us": round(t_eager / n * 1e6, 2), "hbm_gbs": round(by / t_eager / 1e9, 1),
+                                 "frac": round(by / t_eager / 1e9 / HBM_PEAK_GBS, 4)},
+                "note": note}
         if ai < ridge:
             return {"bound": "hbm", "achieved": round(gb, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(gb / HBM_PEAK_GBS, 4), **line}
         return {"bound": "mfma", "achieved": round(tf, 1), "peak": gemm_peak, "unit": "TFLOP/s",
                 "frac": round(tf / gemm_peak, 4), **line}
 
+    gemm_roofline = roofline_of(
+        gemm_log, "gemm", "conv_gemm_kernel + conv_gemm_glds_kernel (+ splitk_epilogue_kernel): decoder + encoder "
+        "implicit-GEMM conv / linear, forward and dgrad",
+        "time = the family's kernel time in one graph-replayed step (rocprofv3 trace of this command's child) / "
+        "launches; bytes = A rows read once + packed W (both planes when split) + C written (+ aux / residual / "
+        "pre-activation streams) per launch; FLOP = 2 M N K")
     roofline_wgrad = roofline_of(
-        wgrad_log, "conv_wgrad_kernel + wgrad slab reduce (weight-gradient GEMMs, decoder + encoder)",
-        "HIP events around each mtts_conv_wgrad call (one eager fwd+bwd of the bench batch); 2*M*N*K FLOP; "
-        "bytes = dY + unique A rows + dW; each call includes its fp32 partial-slab reduce (this eager pass does "
-        "not defer the sums)")
+        wgrad_log, "wgrad", "conv_wgrad_kernel + reduce_partials_kernel (weight-gradient GEMMs and the step's batched "
+        "fixed-order partial sums, which also hold the LayerNorm / GroupNorm gamma / beta partials)",
+        "2 M N K FLOP; bytes = dY + unique A rows + dW; graph time includes the whole batched reduce")
     roofline_attn = roofline_of(
-        attn_log, "attn_fwd_kernel / attn_bwd_dq_kernel + attn_bwd_dkv_kernel (decoder + encoder attention)",
-        "HIP events around each mtts_attention_fwd / _bwd call; FLOP = 4 B H T^2 D fwd, 8 B H T^2 D bwd "
-        "(standard flash-attention accounting, recomputation not counted)")
+        attn_log, "attn", "attn_fwd_kernel / attn_bwd_dq_kernel + attn_bwd_dkv_kernel (decoder + encoder attention)",
+        "FLOP = 4 B H T^2 D fwd, 8 B H T^2 D bwd (standard flash-attention accounting, recomputation not counted); "
+        "bytes = q, k, v, o (+ dO, dq, dk, dv) once")
 
     if rank == 0:
         rec = {
@@ -459,6 +563,7 @@ def main():
                        "model": "MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192)",
                        "global_batch": world * B, "seq_len": Ty, "text_len": Tx, "parallelism": f"dp{world}",
                        "precision": args.precision, "hip_graph": graph,
+                       "weight_planes": 2 if (OPS._W_SPLIT and args.precision == "bf16-mixed") else 1,
                        **({"bucketed_batches": [[int(v) for v in (b["x"].shape[1], b["y"].shape[2],
                                                                      b["x_lengths"].min(), b["y_lengths"].min())]
                                                 for b in batches],
@@ -474,6 +579,8 @@ def main():
             "roofline": gemm_roofline,
             "roofline_wgrad": roofline_wgrad,
             "roofline_attn": roofline_attn,
+            "graph_replay_profile": gprof,
+            "extra_configs": extra,
             "roofline_mas": {"kernel": "mas_dp_kernel + mas_expand_kernel (maximum_path)", "bound": "hbm",
                              "achieved": round(mas_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(mas_gbs / HBM_PEAK_GBS, 4), "traffic": None,

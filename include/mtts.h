@@ -20,6 +20,10 @@
  *                                     (bound as maximum_path_c, __init__.py:4-8)
  *   mtts_losses_fwd / _bwd         <- flow_matching.py:145-149 (CFM loss) + matcha_tts.py:319-323 (prior loss)
  *   mtts_mel_log_fwd               <- matcha/utils/audio_process.py:62-72  MelSpectrogram.__call__ (after the STFT)
+ *   mtts_sequence_mask_f32         <- matcha/utils/model.py:13-34 sequence_mask(...).to(float) (matcha_tts.py:259,
+ *                                     text_encoder.py:398) and text_encoder.py:300-303 masked_fill(-1e4) as a key bias
+ *   mtts_duration_loss_fwd / _bwd  <- matcha_tts.py:287-288 + utils/model.py:117-135 duration_loss
+ *   mtts_loss_sum                  <- baselightningmodule.py:121-128 (dur + prior + diff, the logged values)
  * Decoder / CFM operators (matcha/models/components/{decoder,transformer,flow_matching}.py) are
  * declared in mtts_decoder.h.
  */
@@ -158,6 +162,24 @@ int mtts_losses_fwd(const float *u_pred, const float *x1, const float *z, const 
 int mtts_losses_bwd(const float *g_diff, const float *g_prior, const float *fwd_out, const float *u_pred, const float *x1, const float *z,
                     const float *y, const float *mu_y, const float *y_mask, int32_t B, int32_t C, int32_t T,
                     float sigma_min, float *du_pred, float *dmu_y, void *hip_stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Step glue: sequence masks, the duration loss, the loss sum (csrc/losses.hip)
+ * ------------------------------------------------------------------------------------------- */
+/* mask[b, t] = t < lengths[b] ? 1 : 0 (fp32 [B, T]); key_bias[b, t] = (mask - 1) * 1e4 when non-NULL
+ * (either output may be NULL, not both).  lengths int64 [B]. */
+int mtts_sequence_mask_f32(const int64_t *lengths, int32_t B, int32_t T, float *mask, float *key_bias,
+                           void *hip_stream);
+/* logw_ = log(1e-8 + dur) * x_mask (x_mask from lengths);  out[0] = sum((logw - logw_)^2) / sum(lengths),
+ * out[1] = sum(lengths) as fp32.  logw, dur fp32 [B, T] (dur: the MAS durations); fixed-order sum.
+ * Backward: dlogw = (g / out[1]) * (2 (logw - logw_)). */
+int mtts_duration_loss_fwd(const float *logw, const float *dur, const int64_t *lengths, int32_t B, int32_t T,
+                           float *out, void *hip_stream);
+int mtts_duration_loss_bwd(const float *g, const float *fwd_out, const float *logw, const float *dur,
+                           const int64_t *lengths, int32_t B, int32_t T, float *dlogw, void *hip_stream);
+/* total = (dur + prior) + diff; logged (optional, 4 floats) = [dur, prior, diff, total].  prior may be NULL (0). */
+int mtts_loss_sum(const float *dur, const float *prior, const float *diff, float *total, float *logged,
+                  void *hip_stream);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -18,6 +18,9 @@
  *                                        the float 0/1 mask as an additive key bias (transformer.py:320-328)
  *   mtts_cfm_pack_fwd / _bwd          <- phi_t (flow_matching.py:138) + pack([x, mu], "b * t") (decoder.py:288)
  *   mtts_time_embedding               <- SinusoidalPosEmb.forward (decoder.py:8-31)
+ *   mtts_rows_linear_fwd / _bwd       <- TimeStepEmbeddingNet (decoder.py:33-49: Linear -> SiLU -> Linear) and
+ *                                        every Resnet1D.mlp (decoder.py:71-72, 80-81: Mish -> Linear) on the B
+ *                                        time-embedding rows, forward and backward
  */
 #ifndef MTTS_DECODER_H_
 #define MTTS_DECODER_H_
@@ -84,6 +87,11 @@ typedef struct mtts_conv_gemm_args {
 #define MTTS_GEMM_F_FAST_ACT 0x8     /* GELU / GELU' with a 5e-7 (fp32-evaluated) erf approximation (bf16-mixed) */
 #define MTTS_GEMM_F_PRE_BF16 0x10    /* C_pre is written and aux read as bf16 (bf16-mixed: the saved pre-activation,
                                         half the bytes; ldc / ldaux in elements, % 4 == 0 for the vector epilogue) */
+#define MTTS_GEMM_F_W_SPLIT 0x40     /* bf16 precision: W holds TWO bf16 planes, hi = bf16(w) at W and lo =
+                                        bf16(w - hi) at W + N*Kp (elements); every product is A*hi + A*lo (two
+                                        MFMAs), i.e. the weights enter with ~16 significant bits instead of 8:
+                                        the fp32 weights' rounding -- a STATIC perturbation of the model, the
+                                        dominant bf16-mixed loss error -- drops out (mtts_pack_job.lo_off packs it) */
 
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
 /* Same, with an explicit schedule: 0..17 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;
@@ -222,6 +230,8 @@ typedef struct mtts_pack_job {
     int32_t rows, C, ntaps, Kp, ld;
     int64_t sr, sc, sj;
     int32_t j0, js;
+    int64_t lo_off; /* bf16 only: > 0 also writes lo = bf16(w - bf16(w)) at dst + lo_off (elements): the
+                       second plane of an MTTS_GEMM_F_W_SPLIT operand; 0 = hi plane only */
 } mtts_pack_job;
 
 int mtts_pack_weights(const mtts_pack_job *jobs, int32_t njobs, int32_t precision, void *hip_stream);
@@ -352,6 +362,28 @@ int mtts_embedding_fwd(const int64_t *ids, const float *weight, int64_t rows, in
  * unlike torch's atomic embedding backward). */
 int mtts_embedding_bwd(const int64_t *ids, const float *dout, int64_t rows, int32_t V, int32_t C, float scale,
                        float *dweight, void *hip_stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Rows linear: skinny fp32 Linear layers on B rows (the decoder's time MLP, csrc/time_mlp.hip)
+ * ------------------------------------------------------------------------------------------- */
+#define MTTS_ROWS_MAX_MATS 8
+#define MTTS_ROWS_ACT_NONE 0
+#define MTTS_ROWS_ACT_SILU 1 /* x / (1 + exp(-x)) */
+#define MTTS_ROWS_ACT_MISH 2 /* x tanh(softplus(x)) */
+/* For each of nmat (<= 8) matrices W_i [N_i, K] (fp32, 16-byte aligned rows) sharing the input x [B, K]:
+ *   out_i[b, n] = sum_k x[b, k] W_i[n, k] + bias_i[n]   (bias table or its entries may be NULL)
+ *   out_act_i = act(out_i)                              (out_act table or entries may be NULL)
+ * K % 4 == 0.  Fixed-order sums (deterministic). */
+int mtts_rows_linear_fwd(const float *x, int32_t B, int32_t K, int32_t nmat, const float *const *W,
+                         const float *const *bias, const int32_t *N, float *const *out, float *const *out_act,
+                         int32_t act, void *hip_stream);
+/* Backward of out_i = a W_i^T + bias_i with a = act(pre) the layer's input rows [B, K]:
+ *   dx[b, k]   = (sum_i sum_n dy_i[b, n] W_i[n, k]) * act'(pre[b, k])   (dx may be NULL)
+ *   dW_i[n, k] = sum_b dy_i[b, n] a[b, k] ; db_i[n] = sum_b dy_i[b, n]    (dW NULL: neither; db table may be NULL)
+ * All outputs are overwritten.  act NONE: pre unused (dx is the plain input gradient). */
+int mtts_rows_linear_bwd(const float *a, const float *pre, int32_t act, int32_t B, int32_t K, int32_t nmat,
+                         const float *const *W, const int32_t *N, const float *const *dy, float *dx,
+                         float *const *dW, float *const *db, void *hip_stream);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -91,7 +91,9 @@ struct Stage<false> {
 // Block = WM x WN waves; each wave owns TM x TN MFMA tiles of 32x32 -> block tile
 // BM = 32*WM*TM rows x BN = 32*WN*TN cols, K step KB (32, or 64 for bf16: each step is one global
 // round trip, so a longer step halves the exposed latency per MFMA).
-template <bool BF16, int WM, int WN, int TM, int TN, int KB = kBK, int DEPTH = 1>
+// WS (bf16 only, MTTS_GEMM_F_W_SPLIT): W carries a second bf16 plane (the rounding residual of the fp32
+// weights) at W + N*Kp; it is staged beside the first and every fragment pair issues two MFMAs.
+template <bool BF16, int WM, int WN, int TM, int TN, int KB = kBK, int DEPTH = 1, bool WS = false>
 __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_args p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN;
@@ -100,10 +102,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
     constexpr int CB = (BN * KC + NT - 1) / NT;  // B chunks per thread per K step
     static_assert(BM * KC % NT == 0 || NT % (BM * KC) == 0, "tile/threads mismatch");
     static_assert(BF16 || KB == kBK, "fp32 path uses 32-wide K steps");
+    static_assert(!WS || BF16, "the split weight planes are bf16");
     using ST = typename Stage<BF16>::T;
     constexpr int LDK = KB + Stage<BF16>::PAD;
+    constexpr int BPL = (BN + 1) * LDK;   // one W plane image
     __shared__ ST As[2][(BM + 1) * LDK];  // + one dummy row: staging target of threads without an A chunk
-    __shared__ ST Bs[2][(BN + 1) * LDK];
+    __shared__ ST Bs[2][(WS ? 2 : 1) * BPL];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -171,6 +175,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
         bool aok[CA];
         float4 bf[CB][2];
         uint4 bh[CB];
+        uint4 bl[WS ? CB : 1];  // WS: the lo plane's chunk
         bool bok[CB];
     };
     Regs R0, R1;  // two steps in flight for DEPTH == 2
@@ -202,6 +207,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
             const size_t off = ok ? (size_t)n * p.Kp + k : 0;
             if constexpr (BF16) {
                 R.bh[c] = *reinterpret_cast<const uint4 *>(static_cast<const uint16_t *>(p.W) + off);
+                if constexpr (WS)
+                    R.bl[c] = *reinterpret_cast<const uint4 *>(static_cast<const uint16_t *>(p.W) + (size_t)p.N * p.Kp + off);
             } else {
                 const float4 *src = reinterpret_cast<const float4 *>(static_cast<const float *>(p.W) + off);
                 R.bf[c][0] = src[0];
@@ -235,6 +242,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
             ST *dst = &Bs[buf][b_row[c] * LDK + b_kc[c]];
             if constexpr (BF16) {
                 *reinterpret_cast<uint4 *>(dst) = R.bok[c] ? R.bh[c] : make_uint4(0, 0, 0, 0);
+                if constexpr (WS) *reinterpret_cast<uint4 *>(dst + BPL) = R.bok[c] ? R.bl[c] : make_uint4(0, 0, 0, 0);
             } else {
                 const float m = R.bok[c] ? 1.f : 0.f;
                 const float e[8] = {R.bf[c][0].x * m, R.bf[c][0].y * m, R.bf[c][0].z * m, R.bf[c][0].w * m,
@@ -272,6 +280,17 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                if constexpr (WS) {
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        bfr[j] = *reinterpret_cast<const bf16x8 *>(
+                            &Bs[buf][BPL + (wc * 32 * TN + j * 32 + lr) * LDK + ks * 16 + 8 * lh]);
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                }
             }
         } else {
 #pragma unroll
@@ -804,13 +823,20 @@ constexpr TileCfg kCfgs[] = {
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
-template <bool BF16, int C>
+template <bool BF16, int C, bool WS = false>
 static void launch_cfg(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
     constexpr TileCfg c = kCfgs[C];
     constexpr int BM = 32 * c.wm * c.tm, BN = 32 * c.wn * c.tn;
     dim3 grid((unsigned)(((M + BM - 1) / BM) * ((p.N + BN - 1) / BN)));
-    hipLaunchKernelGGL((conv_gemm_kernel<BF16, c.wm, c.wn, c.tm, c.tn, (BF16 ? c.kb : kBK), (BF16 ? c.depth : 1)>), grid,
-                       dim3(64 * c.wm * c.wn), 0, st, p);
+    hipLaunchKernelGGL((conv_gemm_kernel<BF16, c.wm, c.wn, c.tm, c.tn, (BF16 ? c.kb : kBK), (BF16 ? c.depth : 1), WS>),
+                       grid, dim3(64 * c.wm * c.wn), 0, st, p);
+}
+
+// Split-weight (MTTS_GEMM_F_W_SPLIT) register schedules: the two the heuristic picks, 7 (32-wide K steps)
+// and 12 (64-wide, two in flight); every other id runs the one with its K step width
+static void launch_ws(int id, const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    if (kCfgs[id].kb == 64) launch_cfg<true, 12, true>(p, M, st);
+    else launch_cfg<true, 7, true>(p, M, st);
 }
 
 template <bool BF16>
@@ -929,6 +955,8 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     MTTS_CHECK_ARG(p.dropout_p <= 0.f || (p.seed && p.dropout_p < 1.f), "conv_gemm: dropout needs a seed pointer");
     MTTS_CHECK_ARG(!(p.flags & MTTS_GEMM_F_PRE_BF16) || precision == MTTS_PREC_BF16,
                    "conv_gemm: a bf16 pre-activation needs bf16 precision");
+    MTTS_CHECK_ARG(!(p.flags & MTTS_GEMM_F_W_SPLIT) || precision == MTTS_PREC_BF16,
+                   "conv_gemm: split weight planes need bf16 precision");
     const bool glds_id = cfg >= MTTS_GEMM_GLDS && cfg < MTTS_GEMM_GLDS + mtts::conv_gemm_glds_num_cfgs();
     MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || glds_id, "conv_gemm: bad tile config");
     MTTS_CHECK_ARG(splits >= 0, "conv_gemm: bad split count");
@@ -954,7 +982,8 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
         if (pl.ws > 0 && (!ws || ws_bytes < pl.ws || (uintptr_t)ws % 16)) s = 1;  // no workspace: unsplit
         return mtts::conv_gemm_glds_launch(pl.cfg - MTTS_GEMM_GLDS, p, M, s, static_cast<float *>(ws), st);
     }
-    if (bf16) launch_by_id<true>(pl.cfg, p, M, st);
+    if (bf16 && (p.flags & MTTS_GEMM_F_W_SPLIT)) launch_ws(pl.cfg, p, M, st);
+    else if (bf16) launch_by_id<true>(pl.cfg, p, M, st);
     else launch_by_id<false>(pl.cfg, p, M, st);
     return mtts::check_launch("conv_gemm_kernel");
 }

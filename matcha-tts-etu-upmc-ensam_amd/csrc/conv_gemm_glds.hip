@@ -100,12 +100,12 @@ __device__ __forceinline__ void wait_vmcnt() {
     __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-template <int WM, int WN, int TM, int TN, int STAGES, bool ABF16 = false>
+template <int WM, int WN, int TM, int TN, int STAGES, bool ABF16 = false, bool WS = false>
 struct GldsGeom {
     static constexpr int NT = 64 * WM * WN;
     static constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN;
     static constexpr int A_BYTES = BM * kBK * (ABF16 ? 2 : 4);  // fp32 rows of 256 B / bf16 rows of 128 B
-    static constexpr int W_BYTES = BN * kBK * 2;  // bf16 rows of 128 B
+    static constexpr int W_BYTES = (WS ? 2 : 1) * BN * kBK * 2;  // bf16 rows of 128 B (WS: hi rows, then lo rows)
     static constexpr int GA = A_BYTES / (NT * 16);  // DMA instructions per thread per K step
     static constexpr int GW = W_BYTES / (NT * 16);
     static_assert(A_BYTES % (NT * 16) == 0 && W_BYTES % (NT * 16) == 0, "tile / threads mismatch");
@@ -117,9 +117,11 @@ struct GldsGeom {
 // operands are read through buffer descriptors, the K step advance is a scalar offset and only a tap
 // change touches per-lane state -- the register-addressed loop spent ~12 vector instructions per DMA
 // on pointer and tap bookkeeping (~26 VALU per MFMA on the 19200 x 256 x 768 conv, SQ counters).
-template <int WM, int WN, int TM, int TN, int STAGES, bool ABF16, bool LEAN>
+// WS (MTTS_GEMM_F_W_SPLIT): the W image holds BN hi rows then BN lo rows (the lo plane starts N*Kp
+// elements after W); each fragment pair issues A*hi and A*lo.
+template <int WM, int WN, int TM, int TN, int STAGES, bool ABF16, bool LEAN, bool WS = false>
 __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_gemm_args p, int ksteps, float *part) {
-    using G = GldsGeom<WM, WN, TM, TN, STAGES, ABF16>;
+    using G = GldsGeom<WM, WN, TM, TN, STAGES, ABF16, WS>;
     constexpr int ES = ABF16 ? 2 : 4;        // bytes per A element
     constexpr int RPI = ABF16 ? 8 : 4;       // A rows per 1 KiB DMA instruction
     constexpr int CPR = ABF16 ? 8 : 16;      // 16-byte chunks per A row of one K step
@@ -218,13 +220,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
     const uint16_t *w_ptr[GW];
     int w_k[GW];
     bool w_nok[GW];
+    const size_t w_plane = (size_t)p.N * p.Kp;  // WS: elements from the hi plane to the lo plane
 #pragma unroll
     for (int i = 0; i < GW; ++i) {
-        const int n = 8 * (i * NW + wave) + (lane >> 3);
-        const int lc = (lane & 7) ^ ((n >> 1) & 7);
+        const int ni = 8 * (i * NW + wave) + (lane >> 3);  // row of the W image
+        const int pl = (WS && ni >= BN) ? 1 : 0;
+        const int n = ni - pl * BN;
+        const int lc = (lane & 7) ^ ((ni >> 1) & 7);  // BN % 16 == 0: the lo rows swizzle like the hi rows
         w_nok[i] = n0 + n < p.N;
         w_k[i] = kstep0 * kBK + lc * 8;
-        w_ptr[i] = static_cast<const uint16_t *>(p.W) + (size_t)(w_nok[i] ? n0 + n : 0) * p.Kp + w_k[i];
+        w_ptr[i] = static_cast<const uint16_t *>(p.W) + pl * w_plane + (size_t)(w_nok[i] ? n0 + n : 0) * p.Kp + w_k[i];
     }
 
     // ---- LEAN state: per chunk the tap-0 element index of its row and the byte offset of the current
@@ -243,7 +248,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
         l_soa = __builtin_amdgcn_readfirstlane((uint32_t)(ch0 * ES));
         l_sow = __builtin_amdgcn_readfirstlane((uint32_t)(k0 * 2));
         l_rsa = make_rsrc(p.A, (uint32_t)((long long)p.nb * p.Ti * p.lda * ES));
-        l_rsw = make_rsrc(p.W, (uint32_t)((long long)p.N * p.Kp * 2));
+        l_rsw = make_rsrc(p.W, (uint32_t)((WS ? 2ll : 1ll) * p.N * p.Kp * 2));
 #pragma unroll
         for (int i = 0; i < GA; ++i) {
             const int r = RPI * (i * NW + wave) + lane / CPR;
@@ -255,9 +260,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
         }
 #pragma unroll
         for (int i = 0; i < GW; ++i) {
-            const int n = 8 * (i * NW + wave) + (lane >> 3);
-            const int lc = (lane & 7) ^ ((n >> 1) & 7);
-            l_vw[i] = w_nok[i] ? (uint32_t)(((n0 + n) * p.Kp + lc * 8) * 2) : MTTS_GLDS_OOB;
+            const int ni = 8 * (i * NW + wave) + (lane >> 3);
+            const int pl = (WS && ni >= BN) ? 1 : 0;
+            const int n = ni - pl * BN;
+            const int lc = (lane & 7) ^ ((ni >> 1) & 7);
+            l_vw[i] = w_nok[i] ? (uint32_t)((pl * w_plane + (size_t)(n0 + n) * p.Kp + lc * 8) * 2) : MTTS_GLDS_OOB;
         }
     }
 
@@ -348,6 +355,19 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            if constexpr (WS) {
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = BN + wc * 32 * TN + j * 32 + lr;
+                    const int c = 2 * ks + lh;
+                    bfr[j] = *reinterpret_cast<const bf16x8 *>(wbase + n * 128 + ((c ^ ((n >> 1) & 7)) << 4));
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
         }
     };
 
@@ -455,12 +475,13 @@ bool conv_gemm_glds_lean(const mtts_conv_gemm_args &p) {
 
 namespace {
 
-template <int C, bool ABF16>
+template <int C, bool ABF16, bool WS = false>
 int launch_glds_t(const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
     constexpr GldsCfg c = kGlds[C];
-    using G = GldsGeom<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16>;
-    auto kern = mtts::conv_gemm_glds_lean(p) ? conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16, true>
-                                : conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16, false>;
+    using G = GldsGeom<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16, WS>;
+    static_assert(!WS || 2 * c.stages * (G::A_BYTES + G::W_BYTES) / 2 <= 160 * 1024, "split-weight stages fit LDS");
+    auto kern = mtts::conv_gemm_glds_lean(p) ? conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16, true, WS>
+                                : conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16, false, WS>;
     const int nk = (p.K + kBK - 1) / kBK;
     const int ksteps = (nk + splits - 1) / splits;
     const int S = splits > 1 ? (nk + ksteps - 1) / ksteps : 1;  // every split non-empty
@@ -474,9 +495,22 @@ int launch_glds_t(const mtts_conv_gemm_args &p, int M, int splits, float *part, 
     return mtts::check_launch("splitk_epilogue_kernel");
 }
 
+// Split-weight operands (MTTS_GEMM_F_W_SPLIT) run three instantiations: 64 x 64 three-stage (44) or
+// two-stage (45), and 64 x 256 two-stage (41, 144 KiB with bf16 A, 160 KiB with fp32 A) for the wide tiles
+template <int C>
+int launch_glds_ws(const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
+    constexpr int W = kGlds[C].wn * kGlds[C].tn * 32 >= 128 ? 9 : (kGlds[C].stages == 2 ? 13 : 12);
+    if (p.flags & MTTS_GEMM_F_A_BF16) {
+        if constexpr (kGlds[W].bf16a) return launch_glds_t<W, true, true>(p, M, splits, part, st);
+        else return launch_glds_t<9, true, true>(p, M, splits, part, st);
+    }
+    return launch_glds_t<W, false, true>(p, M, splits, part, st);
+}
+
 // A schedule without an instantiation for the operand's storage runs the 64 x 256 two-stage one (41)
 template <int C>
 int launch_glds(const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
+    if (p.flags & MTTS_GEMM_F_W_SPLIT) return launch_glds_ws<C>(p, M, splits, part, st);
     if (p.flags & MTTS_GEMM_F_A_BF16) {
         if constexpr (kGlds[C].bf16a) return launch_glds_t<C, true>(p, M, splits, part, st);
         else return launch_glds_t<9, true>(p, M, splits, part, st);

@@ -199,3 +199,132 @@ extern "C" int mtts_losses_bwd(const float *g_diff, const float *g_prior, const 
                        dmu_y);
     return mtts::check_launch("loss_bwd_kernel");
 }
+
+// ------------------------------------------------------------------------------------------------
+// Step glue (matcha_tts.py:259-288, model.py:13-34 / 117-135, text_encoder.py:398 / 300-303):
+//   sequence masks from the lengths (0/1 fp32, and the text encoder's -1e4 key bias), the duration loss
+//     logw_ = log(1e-8 + dur) * x_mask ;  dur_loss = sum((logw - logw_)^2) / sum(x_lengths)
+//   with its backward, and the step's loss sum + logged vector.  Each used to be a chain of 3..10 tiny
+//   torch launches (arange / lt / cast, add / log / mul / sub / pow / sum / sum / div, add / add / stack).
+// Roundings follow torch's op sequence (-ffp-contract=off): (1e-8f + dur), logf, * mask, -, d * d;
+// the sums run in a fixed order (deterministic; torch's tree order differs by an ulp).
+namespace {
+
+constexpr int kGThreads = 1024;
+
+__global__ __launch_bounds__(256) void sequence_mask_kernel(const int64_t *__restrict__ lengths, int B, int T,
+                                                            float *__restrict__ mask, float *__restrict__ key_bias) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)B * T) return;
+    const int b = (int)(i / T), t = (int)(i - (int64_t)b * T);
+    const float m = (int64_t)t < lengths[b] ? 1.f : 0.f;
+    if (mask) mask[i] = m;
+    if (key_bias) key_bias[i] = (m - 1.0f) * 1e4f;
+}
+
+__device__ __forceinline__ float big_block_sum(float v, float *red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float s = 0.f;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < kGThreads / 64; ++i) s += red[i];
+    }
+    return s;
+}
+
+__device__ __forceinline__ float dur_diff(const float *logw, const float *dur, const int64_t *lengths, int T, int64_t i) {
+    const int b = (int)(i / T), t = (int)(i - (int64_t)b * T);
+    const float m = (int64_t)t < lengths[b] ? 1.f : 0.f;
+    const float target = logf(1e-8f + dur[i]) * m;
+    return logw[i] - target;
+}
+
+// one workgroup: B*T is the text side (a few thousand entries)
+__global__ __launch_bounds__(kGThreads) void duration_loss_fwd_kernel(const float *__restrict__ logw,
+                                                                      const float *__restrict__ dur,
+                                                                      const int64_t *__restrict__ lengths, int B, int T,
+                                                                      float *__restrict__ out) {
+    __shared__ float red[kGThreads / 64];
+    float acc = 0.f;
+    for (int64_t i = threadIdx.x; i < (int64_t)B * T; i += kGThreads) {
+        const float d = dur_diff(logw, dur, lengths, T, i);
+        acc += d * d;
+    }
+    const float s = big_block_sum(acc, red);
+    if (threadIdx.x == 0) {
+        int64_t l = 0;
+        for (int b = 0; b < B; ++b) l += lengths[b];
+        const float L = (float)l;  // torch: float32 / int64 -> float32
+        out[0] = s / L;
+        out[1] = L;
+    }
+}
+
+__global__ __launch_bounds__(256) void duration_loss_bwd_kernel(const float *__restrict__ g,
+                                                                const float *__restrict__ fwd_out,
+                                                                const float *__restrict__ logw,
+                                                                const float *__restrict__ dur,
+                                                                const int64_t *__restrict__ lengths, int B, int T,
+                                                                float *__restrict__ dlogw) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)B * T) return;
+    const float gl = g[0] / fwd_out[1];  // DivBackward: grad / sum(lengths)
+    const float d = dur_diff(logw, dur, lengths, T, i);
+    dlogw[i] = gl * (2.0f * d);  // PowBackward (exponent 2): grad * (2 * d)
+}
+
+// total = (dur + prior) + diff (torch's left-to-right adds); logged = [dur, prior, diff, total]
+__global__ void loss_sum_kernel(const float *__restrict__ dur, const float *__restrict__ prior,
+                                const float *__restrict__ diff, float *__restrict__ total, float *__restrict__ logged) {
+    if (threadIdx.x != 0) return;
+    const float d = dur[0], p = prior ? prior[0] : 0.f, f = diff[0];
+    const float t = (d + p) + f;
+    total[0] = t;
+    if (logged) {
+        logged[0] = d;
+        logged[1] = p;
+        logged[2] = f;
+        logged[3] = t;
+    }
+}
+
+}  // namespace
+
+extern "C" int mtts_sequence_mask_f32(const int64_t *lengths, int32_t B, int32_t T, float *mask, float *key_bias,
+                                      void *hip_stream) {
+    MTTS_CHECK_ARG(lengths && B >= 0 && T >= 0 && (mask || key_bias), "sequence_mask_f32: bad args");
+    const int64_t n = (int64_t)B * T;
+    if (n == 0) return MTTS_OK;
+    hipLaunchKernelGGL(sequence_mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(hip_stream), lengths, B, T, mask, key_bias);
+    return mtts::check_launch("sequence_mask_kernel");
+}
+
+extern "C" int mtts_duration_loss_fwd(const float *logw, const float *dur, const int64_t *lengths, int32_t B, int32_t T,
+                                      float *out, void *hip_stream) {
+    MTTS_CHECK_ARG(logw && dur && lengths && out && B >= 1 && T >= 1, "duration_loss_fwd: bad args");
+    hipLaunchKernelGGL(duration_loss_fwd_kernel, dim3(1), dim3(kGThreads), 0, static_cast<hipStream_t>(hip_stream),
+                       logw, dur, lengths, B, T, out);
+    return mtts::check_launch("duration_loss_fwd_kernel");
+}
+
+extern "C" int mtts_duration_loss_bwd(const float *g, const float *fwd_out, const float *logw, const float *dur,
+                                      const int64_t *lengths, int32_t B, int32_t T, float *dlogw, void *hip_stream) {
+    MTTS_CHECK_ARG(g && fwd_out && logw && dur && lengths && dlogw && B >= 1 && T >= 1, "duration_loss_bwd: bad args");
+    const int64_t n = (int64_t)B * T;
+    hipLaunchKernelGGL(duration_loss_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(hip_stream), g, fwd_out, logw, dur, lengths, B, T, dlogw);
+    return mtts::check_launch("duration_loss_bwd_kernel");
+}
+
+extern "C" int mtts_loss_sum(const float *dur, const float *prior, const float *diff, float *total, float *logged,
+                             void *hip_stream) {
+    MTTS_CHECK_ARG(dur && diff && total, "loss_sum: bad args");
+    hipLaunchKernelGGL(loss_sum_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(hip_stream), dur, prior, diff,
+                       total, logged);
+    return mtts::check_launch("loss_sum_kernel");
+}

@@ -6,7 +6,8 @@
 // phase GEMMs each need their own gather of them.  One job = one affine gather
 //     dst[r*ld + j*C + c] = src[r*sr + c*sc + (j0 + j*js)*sj],   zero for k' in [C*ntaps, Kp),
 // and a launch runs up to kJobsPerLaunch jobs (blockIdx.y = job), each thread producing 8
-// consecutive k' (one 16-byte bf16 store, or two float4).
+// consecutive k' (one 16-byte bf16 store, or two float4).  bf16 jobs with lo_off > 0 also write the
+// rounding residual bf16(w - bf16(w)) as a second plane (MTTS_GEMM_F_W_SPLIT operands).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -44,13 +45,18 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(JobBatch jb) {
             }
         }
         if constexpr (BF16) {
-            uint32_t w[4];
+            uint32_t w[4], l[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                w[i] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)e[2 * i]) |
-                       ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)e[2 * i + 1]) << 16);
-            *reinterpret_cast<uint4 *>(static_cast<uint16_t *>(j.dst) + (size_t)r * j.ld + k0) =
-                make_uint4(w[0], w[1], w[2], w[3]);
+            for (int i = 0; i < 4; ++i) {
+                const __bf16 h0 = (__bf16)e[2 * i], h1 = (__bf16)e[2 * i + 1];
+                w[i] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+                // split plane: the rounding residual, exact in fp32 (e - hi has <= 16 significant bits)
+                const __bf16 l0 = (__bf16)(e[2 * i] - (float)h0), l1 = (__bf16)(e[2 * i + 1] - (float)h1);
+                l[i] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+            }
+            uint16_t *d = static_cast<uint16_t *>(j.dst) + (size_t)r * j.ld + k0;
+            *reinterpret_cast<uint4 *>(d) = make_uint4(w[0], w[1], w[2], w[3]);
+            if (j.lo_off > 0) *reinterpret_cast<uint4 *>(d + j.lo_off) = make_uint4(l[0], l[1], l[2], l[3]);
         } else {
             float4 *d = reinterpret_cast<float4 *>(static_cast<float *>(j.dst) + (size_t)r * j.ld + k0);
             d[0] = make_float4(e[0], e[1], e[2], e[3]);
@@ -72,6 +78,8 @@ extern "C" int mtts_pack_weights(const mtts_pack_job *jobs, int32_t njobs, int32
                            j.ld % 8 == 0 && j.ld >= j.Kp,
                        "pack_weights: bad job shape (Kp, ld multiples of 8, Kp >= C*ntaps, ld >= Kp)");
         MTTS_CHECK_ARG((reinterpret_cast<uintptr_t>(j.dst) & 15) == 0, "pack_weights: dst must be 16-byte aligned");
+        MTTS_CHECK_ARG(j.lo_off >= 0 && j.lo_off % 8 == 0 && (j.lo_off == 0 || precision == MTTS_PREC_BF16),
+                       "pack_weights: lo_off (the split plane) needs bf16 and a multiple of 8");
         const long g = (long)j.rows * (j.Kp / 8);
         max_groups = g > max_groups ? g : max_groups;
     }

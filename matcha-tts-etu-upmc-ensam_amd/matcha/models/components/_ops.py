@@ -54,7 +54,13 @@ GEMM_F_C_BF16 = 0x4  # MTTS_GEMM_F_C_BF16: output stored bf16
 GEMM_F_FAST_ACT = 0x8  # MTTS_GEMM_F_FAST_ACT: 1.5e-7-accurate erf in GELU epilogues (bf16-mixed only)
 GEMM_F_PRE_BF16 = 0x10  # MTTS_GEMM_F_PRE_BF16: C_pre written / aux read as bf16
 WGRAD_F_DY_BF16 = 0x20  # MTTS_WGRAD_F_DY_BF16: the weight gradient's dY holds bf16
+GEMM_F_W_SPLIT = 0x40  # MTTS_GEMM_F_W_SPLIT: W holds a hi and a lo bf16 plane (two MFMAs per product)
 _FAST_ACT = os.environ.get("MTTS_EXACT_GELU") != "1"
+# bf16-mixed forward GEMMs take their weights as two bf16 planes (hi + rounding residual): the rounding of
+# the fp32 weights is a static model perturbation and was the bf16 loss error (tools/r3/precision_budget.py:
+# prior 2.9e-4 / diff 2.1e-4 from weight rounding alone, activations 3.8e-5 / 2.1e-5).  MTTS_W_SPLIT=0: one plane
+_W_SPLIT = os.environ.get("MTTS_W_SPLIT", "1") != "0"
+PACK_BF16_SPLIT = 2  # pack-cache kind: the bf16 hi + lo planes of a forward operand
 
 GEMM_GLDS = 32  # MTTS_GEMM_GLDS: first LDS-DMA schedule id
 
@@ -98,7 +104,8 @@ class AttnGrads(ctypes.Structure):
 class PackJob(ctypes.Structure):
     _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("rows", ctypes.c_int32), ("C", ctypes.c_int32),
                 ("ntaps", ctypes.c_int32), ("Kp", ctypes.c_int32), ("ld", ctypes.c_int32), ("sr", ctypes.c_int64),
-                ("sc", ctypes.c_int64), ("sj", ctypes.c_int64), ("j0", ctypes.c_int32), ("js", ctypes.c_int32)]
+                ("sc", ctypes.c_int64), ("sj", ctypes.c_int64), ("j0", ctypes.c_int32), ("js", ctypes.c_int32),
+                ("lo_off", ctypes.c_int64)]
 
 
 _P, _I, _F, _SZ, _U = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint32
@@ -267,9 +274,11 @@ def spec_convT_dgrad(w):
 
 
 def _run_pack(specs, prec):
+    """prec: PREC_FP32, PREC_BF16, or PACK_BF16_SPLIT ([2 * rows, Kp]: the hi plane, then the lo plane)."""
     dev = specs[0].jobs[0][0].device
-    dt = torch.bfloat16 if prec == PREC_BF16 else torch.float32
-    outs = [torch.empty(sp.rows, sp.Kp, device=dev, dtype=dt) for sp in specs]
+    split = prec == PACK_BF16_SPLIT
+    dt = torch.bfloat16 if prec in (PREC_BF16, PACK_BF16_SPLIT) else torch.float32
+    outs = [torch.empty((2 if split else 1) * sp.rows, sp.Kp, device=dev, dtype=dt) for sp in specs]
     njobs = sum(len(sp.jobs) for sp in specs)
     arr = (PackJob * njobs)()
     i = 0
@@ -283,10 +292,19 @@ def _run_pack(specs, prec):
             j.src, j.dst = src.data_ptr(), out.data_ptr() + (r0 * sp.Kp + c0) * es
             j.rows, j.C, j.ntaps, j.Kp, j.ld = rows, C, nt, kpj, sp.Kp
             j.sr, j.sc, j.sj, j.j0, j.js = sr, sc, sj, j0, js
+            j.lo_off = sp.rows * sp.Kp if split else 0
             i += 1
-    N.check(N.lib().mtts_pack_weights(arr, njobs, prec, torch.cuda.current_stream(dev).cuda_stream),
-            "mtts_pack_weights")
+    N.check(N.lib().mtts_pack_weights(arr, njobs, PREC_BF16 if split else prec,
+                                      torch.cuda.current_stream(dev).cuda_stream), "mtts_pack_weights")
+    if split:
+        for o in outs:
+            o._mtts_w_split = True  # _gemm sets MTTS_GEMM_F_W_SPLIT for it
     return outs
+
+
+def _pack_kind(spec: PackSpec, prec: int) -> int:
+    """bf16 forward operands: the split planes (unless MTTS_W_SPLIT=0); everything else as prec."""
+    return PACK_BF16_SPLIT if (prec == PREC_BF16 and _W_SPLIT and not spec.dgrad) else prec
 
 
 _PACK_SCOPE: contextvars.ContextVar = contextvars.ContextVar("mtts_pack_scope", default=None)
@@ -300,11 +318,13 @@ def weight_pack_scope(owner: torch.nn.Module):
     prec = gemm_precision()
     plan = owner.__dict__.setdefault("_mtts_pack_plan", {})
     grad = torch.is_grad_enabled()
-    specs = [sp for key, sp in plan.items() if key[0] == prec and (grad or not sp.dgrad)]
+    kinds = (prec, PACK_BF16_SPLIT) if prec == PREC_BF16 else (prec,)
     cache = {}
-    if specs:
-        for sp, t in zip(specs, _run_pack(specs, prec)):
-            cache[(prec,) + sp.key] = t
+    for kind in kinds:
+        specs = [sp for key, sp in plan.items() if key[0] == kind and (grad or not sp.dgrad)]
+        if specs:
+            for sp, t in zip(specs, _run_pack(specs, kind)):
+                cache[(kind,) + sp.key] = t
     tok = _PACK_SCOPE.set((plan, cache, prec))
     nseed = owner.__dict__.get("_mtts_seed_count", 0)
     dev = next(owner.parameters()).device
@@ -323,16 +343,17 @@ def weight_pack_scope(owner: torch.nn.Module):
 def packed(spec: PackSpec, prec: int) -> tuple[torch.Tensor, int]:
     """(operand, Kp) for `spec`, from the active weight_pack_scope when there is one."""
     act = _PACK_SCOPE.get()
+    kind = _pack_kind(spec, prec)
     if act is not None and act[2] == prec:
         plan, cache, _ = act
-        key = (prec,) + spec.key
+        key = (kind,) + spec.key
         t = cache.get(key)
         if t is None:
-            t = _run_pack([spec], prec)[0]
+            t = _run_pack([spec], kind)[0]
             cache[key] = t
             plan[key] = spec
         return t, spec.Kp
-    return _run_pack([spec], prec)[0], spec.Kp
+    return _run_pack([spec], kind)[0], spec.Kp
 
 
 # Per-launch timing for bench.py's roofline leg: when set to a list, every mtts_conv_gemm launch appends
@@ -386,6 +407,9 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     # host-side shape checks before any launch (the kernel trusts W's rows / the output's extent)
     if Wp.dim() != 2 or Wp.shape[0] < N_ or Wp.shape[1] != Kp or Kp < len(offs) * cin:
         raise ValueError(f"packed weight {tuple(Wp.shape)} does not cover N={N_}, Kp={Kp}, K={len(offs) * cin}")
+    w_split = getattr(Wp, "_mtts_w_split", False) and prec == PREC_BF16
+    if w_split and Wp.shape[0] != 2 * N_:
+        raise ValueError(f"split weight planes {tuple(Wp.shape)}: the lo plane must start at row N={N_}")
     if C.shape[-1] < N_ or C.numel() < nb * To_full * C.shape[-1] or A.shape[-1] < cin:
         raise ValueError(f"GEMM operands too small: A {tuple(A.shape)}, C {tuple(C.shape)}, N={N_}")
     for t, w_ in ((residual, N_), (aux, N_), (C_pre, N_)):
@@ -414,7 +438,8 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
                   | (GEMM_F_A_BF16 if A.dtype == torch.bfloat16 else 0)
                   | (GEMM_F_C_BF16 if C.dtype == torch.bfloat16 else 0)
                   | (GEMM_F_FAST_ACT if (prec == PREC_BF16 and _FAST_ACT) else 0)
-                  | (GEMM_F_PRE_BF16 if any(t is not None and t.dtype == torch.bfloat16 for t in (C_pre, aux)) else 0))
+                  | (GEMM_F_PRE_BF16 if any(t is not None and t.dtype == torch.bfloat16 for t in (C_pre, aux)) else 0)
+                  | (GEMM_F_W_SPLIT if w_split else 0))
     if C_pre is not None and aux is not None and C_pre.dtype != aux.dtype:
         raise ValueError("C_pre and aux must share a dtype")
     log = LAUNCH_LOG
@@ -430,7 +455,8 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     if log is not None:
         e1.record(st)
         M_ = nb * To
-        nbytes = nb * Ti * cin * A.element_size() + N_ * Kp * Wp.element_size() + M_ * N_ * C.element_size()
+        nbytes = (nb * Ti * cin * A.element_size() + (2 if w_split else 1) * N_ * Kp * Wp.element_size()
+                  + M_ * N_ * C.element_size())
         nbytes += sum(M_ * N_ * t.element_size() for t in (residual, aux, C_pre) if t is not None)
         log.append((e0, e1, 2.0 * M_ * N_ * args.K, prec, nbytes,
                     dict(M=M_, N=N_, K=args.K, cin=cin, ntaps=len(offs), in_stride=in_stride, res=residual is not None,
@@ -1534,3 +1560,164 @@ def rope_tm(qkv, cos, sin, heads: int, rope_dims: int):
     """Rotary embedding of the q and k blocks of a fused [B, T, 3C] projection (first rope_dims dims of
     each head, rotate-half form; cos/sin [T, rope_dims/2]); v passes through."""
     return _RopeTM.apply(qkv, cos, sin, heads, rope_dims)
+
+
+# ------------------------------------------------------------------------------------------ step glue
+N.register("mtts_sequence_mask_f32", ctypes.c_int, [_P, _I, _I, _P, _P, _P])
+N.register("mtts_duration_loss_fwd", ctypes.c_int, [_P, _P, _P, _I, _I, _P, _P])
+N.register("mtts_duration_loss_bwd", ctypes.c_int, [_P, _P, _P, _P, _P, _I, _I, _P, _P])
+N.register("mtts_loss_sum", ctypes.c_int, [_P, _P, _P, _P, _P, _P])
+
+
+def _lengths64(lengths: torch.Tensor) -> torch.Tensor:
+    return lengths if (lengths.dtype == torch.int64 and lengths.is_contiguous()) else lengths.to(torch.int64).contiguous()
+
+
+def sequence_mask_f32(lengths: torch.Tensor, T: int, key_bias: bool = False):
+    """fp32 0/1 mask [B, T] of utils/model.py:13-34 sequence_mask(lengths, T).float() in one launch; with
+    key_bias=True also (mask - 1) * 1e4 (the text encoder's masked_fill(-1e4) as an additive key bias):
+    returns (mask, bias)."""
+    N.require_device(lengths)
+    ln = _lengths64(lengths)
+    B = ln.numel()
+    m = torch.empty(B, T, dtype=torch.float32, device=ln.device)
+    kb = torch.empty(B, T, dtype=torch.float32, device=ln.device) if key_bias else None
+    N.check(N.lib().mtts_sequence_mask_f32(ln.data_ptr(), B, T, m.data_ptr(), N.ptr(kb), _stream(ln)),
+            "mtts_sequence_mask_f32")
+    return (m, kb) if key_bias else m
+
+
+class _DurationLoss(torch.autograd.Function):
+    """sum((logw - log(1e-8 + dur) * x_mask)^2) / sum(x_lengths) -- matcha_tts.py:287-288 + utils/model.py:117-135
+    in one launch forward and one backward (csrc/losses.hip); dur (the MAS durations) has no gradient."""
+
+    @staticmethod
+    def forward(ctx, logw, dur, lengths):
+        N.require_device(logw, dur, lengths)
+        B, T = dur.shape[0], dur.shape[-1]
+        lw, d, ln = _f32c(logw).reshape(B, T), _f32c(dur).reshape(B, T), _lengths64(lengths)
+        out = torch.empty(2, dtype=torch.float32, device=lw.device)
+        N.check(N.lib().mtts_duration_loss_fwd(lw.data_ptr(), d.data_ptr(), ln.data_ptr(), B, T, out.data_ptr(),
+                                               _stream(lw)), "mtts_duration_loss_fwd")
+        ctx.save_for_backward(lw, d, ln, out)
+        ctx.shape = logw.shape
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        lw, d, ln, out = ctx.saved_tensors
+        B, T = d.shape
+        g = _f32c(g)
+        dlogw = torch.empty_like(lw)
+        N.check(N.lib().mtts_duration_loss_bwd(g.data_ptr(), out.data_ptr(), lw.data_ptr(), d.data_ptr(), ln.data_ptr(),
+                                               B, T, dlogw.data_ptr(), _stream(lw)), "mtts_duration_loss_bwd")
+        return dlogw.view(ctx.shape), None, None
+
+
+def duration_loss_fused(logw: torch.Tensor, dur: torch.Tensor, lengths: torch.Tensor) -> torch.Tensor:
+    """logw [B, 1, T] (the duration predictor's output), dur [B, T] -> the duration loss (0-dim fp32)."""
+    return _DurationLoss.apply(logw, dur, lengths)
+
+
+class _LossSum(torch.autograd.Function):
+    """total = (dur + prior) + diff and the logged vector [dur, prior, diff, total] in one launch
+    (baselightningmodule.py:121-128); the gradient of total reaches each loss unchanged."""
+
+    @staticmethod
+    def forward(ctx, dur, prior, diff):
+        N.require_device(dur, diff)
+        dur, diff = _f32c(dur), _f32c(diff)
+        prior = _f32c(prior) if torch.is_tensor(prior) else None
+        total = torch.empty((), dtype=torch.float32, device=dur.device)
+        logged = torch.empty(4, dtype=torch.float32, device=dur.device)
+        N.check(N.lib().mtts_loss_sum(dur.data_ptr(), N.ptr(prior), diff.data_ptr(), total.data_ptr(), logged.data_ptr(),
+                                      _stream(dur)), "mtts_loss_sum")
+        ctx.has_prior = prior is not None
+        ctx.mark_non_differentiable(logged)
+        return total, logged
+
+    @staticmethod
+    def backward(ctx, g, _g_logged):
+        return g, (g if ctx.has_prior else None), g
+
+
+def loss_sum(dur, prior, diff):
+    """(total, logged): total = dur + prior + diff (prior may be the int 0 of prior_loss=False)."""
+    return _LossSum.apply(dur, prior if torch.is_tensor(prior) else None, diff)
+
+
+# ------------------------------------------------------------------------------------------ time MLP
+N.register("mtts_rows_linear_fwd", ctypes.c_int, [_P, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P])
+N.register("mtts_rows_linear_bwd", ctypes.c_int, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P])
+ROWS_ACT_NONE, ROWS_ACT_SILU, ROWS_ACT_MISH = 0, 1, 2  # include/mtts_decoder.h MTTS_ROWS_ACT_*
+
+
+def _ptrs(ts):
+    return (ctypes.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
+
+
+def _rows_fwd(x, ws, bs, outs, acts, act):
+    B, K = x.shape
+    ns = (ctypes.c_int32 * len(ws))(*[w.shape[0] for w in ws])
+    N.check(N.lib().mtts_rows_linear_fwd(x.data_ptr(), B, K, len(ws), _ptrs(ws), _ptrs(bs), ns, _ptrs(outs),
+                                         None if acts is None else _ptrs(acts), act, _stream(x)), "mtts_rows_linear_fwd")
+
+
+def _rows_bwd(a, pre, act, ws, dys, dx, dws, dbs):
+    B, K = a.shape
+    ns = (ctypes.c_int32 * len(ws))(*[w.shape[0] for w in ws])
+    N.check(N.lib().mtts_rows_linear_bwd(a.data_ptr(), N.ptr(pre), act, B, K, len(ws), _ptrs(ws), ns, _ptrs(dys),
+                                         N.ptr(dx), _ptrs(dws), _ptrs(dbs), _stream(a)), "mtts_rows_linear_bwd")
+
+
+class _TimeMLP(torch.autograd.Function):
+    """e [B, in] -> (temb, tp_0 .. tp_{n-1}): TimeStepEmbeddingNet (decoder.py:33-49, Linear -> SiLU ->
+    Linear) and every Resnet1D.mlp (decoder.py:71-72, 80-81, Mish -> Linear) on the shared temb, in fp32,
+    3 launches forward and 5 backward (csrc/time_mlp.hip).  The projections are one matrix table: no
+    weight concatenation, each tp_i is written contiguous."""
+
+    @staticmethod
+    def forward(ctx, e, w1, b1, w2, b2, n_proj, *wb):
+        N.require_device(e, w1)
+        ws = [_f32c(w) for w in wb[:n_proj]]
+        bs = [_f32c(b) for b in wb[n_proj:]]
+        e, w1, b1, w2, b2 = _f32c(e), _f32c(w1), _f32c(b1), _f32c(w2), _f32c(b2)
+        B, D = e.shape[0], w1.shape[0]
+        new = functools.partial(torch.empty, dtype=torch.float32, device=e.device)
+        h1, a1, temb, a2 = new(B, D), new(B, D), new(B, D), new(B, D)
+        _rows_fwd(e, [w1], [b1], [h1], [a1], ROWS_ACT_SILU)
+        _rows_fwd(a1, [w2], [b2], [temb], [a2], ROWS_ACT_MISH)
+        tps = [new(B, w.shape[0]) for w in ws]
+        _rows_fwd(a2, ws, bs, tps, None, ROWS_ACT_NONE)
+        ctx.save_for_backward(e, h1, a1, temb, a2, w1, w2, *ws)
+        ctx.n = n_proj
+        ctx.e_grad = ctx.needs_input_grad[0]
+        ctx.set_materialize_grads(False)
+        return (temb, *tps)
+
+    @staticmethod
+    def backward(ctx, g_temb, *g_tps):
+        e, h1, a1, temb, a2, w1, w2, *ws = ctx.saved_tensors
+        B, D = temb.shape
+        new = functools.partial(torch.empty, dtype=torch.float32, device=e.device)
+        dys = [_f32c(g) if g is not None else torch.zeros(B, w.shape[0], device=e.device) for g, w in zip(g_tps, ws)]
+        d_temb = new(B, D)
+        dws = [torch.empty_like(w) for w in ws]
+        dbs = [new(w.shape[0]) for w in ws]
+        _rows_bwd(a2, temb, ROWS_ACT_MISH, ws, dys, d_temb, dws, dbs)
+        if g_temb is not None:  # temb used directly as well (never, on the decoder's path)
+            d_temb = d_temb + _f32c(g_temb)
+        dh1, dw2, db2 = new(B, D), torch.empty_like(w2), new(D)
+        _rows_bwd(a1, h1, ROWS_ACT_SILU, [w2], [d_temb], dh1, [dw2], [db2])
+        de = new(*e.shape) if ctx.e_grad else None
+        dw1, db1 = torch.empty_like(w1), new(D)
+        _rows_bwd(e, None, ROWS_ACT_NONE, [w1], [dh1], de, [dw1], [db1])
+        return (de, dw1, db1, dw2, db2, None, *dws, *dbs)
+
+
+def time_mlp(e, linear_1, linear_2, proj_linears):
+    """(temb, [tp_i]) = (time_mlp(e), [lin_i(mish(temb))]) for nn.Linear modules; see _TimeMLP."""
+    ws = [lin.weight for lin in proj_linears]
+    bs = [lin.bias for lin in proj_linears]
+    out = _TimeMLP.apply(e, linear_1.weight, linear_1.bias, linear_2.weight, linear_2.bias, len(ws), *ws, *bs)
+    return out[0], list(out[1:])

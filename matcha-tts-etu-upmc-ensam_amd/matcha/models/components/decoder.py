@@ -27,6 +27,7 @@ _DX_LINK = os.environ.get("MTTS_RESNET_DX_LINK", "1") != "0"
 # MTTS_RESNET_BF16_STORE=0: bf16-mixed keeps the ResNet blocks' conv outputs / GroupNorm outputs in fp32
 # (precision-budget switch, tools/r3/precision_budget.py)
 _RESNET16 = os.environ.get("MTTS_RESNET_BF16_STORE", "1") != "0"
+N_ROWS_MAX_MATS = 8  # include/mtts_decoder.h MTTS_ROWS_MAX_MATS
 
 
 class SinusoidalPosEmb(nn.Module):
@@ -228,30 +229,21 @@ class Decoder(nn.Module):
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec_bf16), O.weight_pack_scope(self):
                 return self._forward_tm(None, mask.float(), None, t.float(), packed=h)
 
-    def _time_projections(self, temb):
-        """Every ResnetBlock's mlp(temb) = Linear(Mish(temb)) (decoder.py:80-81) as ONE GEMM: the Mish of
-        the shared time embedding is computed once and the blocks' Linear weights are stacked along N,
-        instead of 6 x (mish, addmm) forward and 6 x (mish', 2 mm, bias sum, accumulate) backward
-        launches.  fp32, like the per-block path.  B rows only (32 x 1024 -> 1536): a plain library GEMM
-        -- the implicit-conv kernel's 32-row tiles gave it 12 workgroups (82 us for its dgrad)."""
+    def _time_path(self, t):
+        """temb = time_mlp(SinusoidalPosEmb(t)) (decoder.py:33-49, :285-286) and every Resnet1D's
+        mlp(temb) = Linear(Mish(temb)) (:80-81), fp32 as the reference keeps it, in 1 + 3 HIP launches
+        (csrc/cfm_prep.hip, csrc/time_mlp.hip); backward 5.  Returns (temb, {id(resnet): tp})."""
         resnets = ([r for r, *_ in self.Downsampling_Blocks] + [r for r, _ in self.Mid_Blocks]
                    + [r for r, *_ in self.Upsampling_Blocks])
-        lins = [r.mlp[1] for r in resnets]
         with torch.autocast("cuda", enabled=False):
-            act = F.mish(temb.float())
-            bias = torch.cat([lin.bias for lin in lins])
-            tp = F.linear(act, torch.cat([lin.weight for lin in lins]), bias)
-            if len({lin.out_features for lin in lins}) == 1:  # [B, n*C] -> n contiguous [B, C] (one copy)
-                n = len(lins)
-                parts = tp.view(tp.shape[0], n, -1).transpose(0, 1).contiguous().unbind(0)
-            else:
-                parts = [t.contiguous() for t in tp.split([lin.out_features for lin in lins], dim=-1)]
-        return dict(zip(map(id, resnets), parts))
+            e = self.time_embeddings(t)
+            if len(resnets) > N_ROWS_MAX_MATS:
+                raise ValueError(f"the fused time path takes up to {N_ROWS_MAX_MATS} Resnet1D blocks")
+            temb, tps = O.time_mlp(e, self.time_mlp.linear_1, self.time_mlp.linear_2, [r.mlp[1] for r in resnets])
+        return temb, dict(zip(map(id, resnets), tps))
 
     def _forward_tm(self, x, mask, mu, t, packed=None):
-        with torch.autocast("cuda", enabled=False):  # [B, 1024] time MLP: tiny, kept fp32
-            temb = self.time_mlp(self.time_embeddings(t))
-        tps = self._time_projections(temb)
+        temb, tps = self._time_path(t)  # [B, 1024] time MLP + every block's projection, fp32
         h = torch.cat([x, mu], dim=-1) if packed is None else packed  # einops pack "b * t" on channels (:288)
         skips, masks = [], [mask]
         for resnet, tfs, down in self.Downsampling_Blocks:

@@ -30,7 +30,6 @@ import torch.nn as nn
 
 from matcha import _native as N
 from matcha.models.components import _ops as O
-from matcha.utils.model import sequence_mask
 
 # MTTS_ENCODER_DX_LINK=0: autograd sums each encoder layer's two input gradients (A/B switch)
 _ENC_LINK = os.environ.get("MTTS_ENCODER_DX_LINK", "1") != "0"
@@ -199,11 +198,13 @@ class Encoder(nn.Module):
              for _ in range(num_layers)])
         self.norm_layers_2 = nn.ModuleList([nn.LayerNorm(hidden_channels) for _ in range(num_layers)])
 
-    def forward_tm(self, h, m):
+    def forward_tm(self, h, m, key_bias=None):
         """text_encoder.py:296-322, token-major; returns the UNMASKED last LayerNorm output (callers
-        apply the final x * mask through their input row scale)."""
+        apply the final x * mask through their input row scale).  key_bias: (m - 1) * 1e4 if the caller
+        has it (O.sequence_mask_f32 makes both in one launch)."""
         p = self.dropout_rate if self.training else 0.0
-        key_bias = (m - 1.0) * 1e4  # masked_fill(-1e4) on padded keys
+        if key_bias is None:
+            key_bias = (m - 1.0) * 1e4  # masked_fill(-1e4) on padded keys
         # every layer's stacked q|k|v bias from ONE concatenation (one launch instead of one per layer) --
         # except with the opt-in side-stream weight gradients: the concatenation routes the bias gradients
         # through autograd's SplitBackward, which reads them on the main stream while the side stream
@@ -295,9 +296,10 @@ class TextEncoder(nn.Module):
         with O.weight_pack_scope(self):
             # [B, T, C]: token-major already
             emb = _Embedding.apply(text_input, self.embedding.weight, math.sqrt(self.channel_dim))
-            m = sequence_mask(text_lengths, emb.size(1)).to(emb.dtype)
+            # sequence_mask(...).to(float) and the attention's -1e4 key bias in one launch
+            m, key_bias = O.sequence_mask_f32(text_lengths, emb.size(1), key_bias=True)
             h = self.prenet.forward_tm(emb, m) if self.prenet is not None else emb
-            h = self.encoder.forward_tm(h, m)
+            h = self.encoder.forward_tm(h, m, key_bias)
             mu = O.linear_tm(h, self.mean_projection.weight, self.mean_projection.bias, in_scale=m, out_scale=m)
             logw = self.duration_predictor.forward_tm(h.detach(), m)
         return mu.transpose(1, 2), logw.transpose(1, 2), m.unsqueeze(1)

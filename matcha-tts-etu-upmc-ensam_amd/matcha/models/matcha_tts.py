@@ -18,9 +18,10 @@ import torch
 
 import matcha.utils.monotonic_align as monotonic_align
 from matcha.models.baselightningmodule import BaseLightningClass
+from matcha.models.components import _ops as O
 from matcha.models.components.flow_matching import ConditionalFlowMatching as CFM
 from matcha.models.components.text_encoder import TextEncoder
-from matcha.utils.model import denormalize, duration_loss, fix_len_compatibility, generate_path, sequence_mask
+from matcha.utils.model import denormalize, fix_len_compatibility, generate_path, sequence_mask
 
 
 class MatchaTTS(BaseLightningClass):
@@ -97,7 +98,7 @@ class MatchaTTS(BaseLightningClass):
         # caller's precision (bf16 MFMA operands inside a bf16 autocast region)
         mu_x, logw, x_mask = self.encoder(x, x_lengths)
         y_max_length = y.shape[-1]
-        y_mask = sequence_mask(y_lengths, y_max_length).unsqueeze(1).to(x_mask)
+        y_mask = O.sequence_mask_f32(y_lengths, y_max_length).unsqueeze(1)  # sequence_mask(...).to(x_mask), one launch
         runs = None
         if self.use_precomputed_durations:
             attn_mask = x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)
@@ -110,8 +111,9 @@ class MatchaTTS(BaseLightningClass):
                 attn, dur, col_row, row_start, lens = monotonic_align.prior_maximum_path(mu_x, y, x_lengths,
                                                                                           y_lengths)
             runs = (col_row, row_start, lens)
-        logw_ = torch.log(1e-8 + dur.unsqueeze(1)) * x_mask
-        dur_loss = duration_loss(logw, logw_, x_lengths)
+        # logw_ = log(1e-8 + dur) * x_mask ; duration_loss(logw, logw_, x_lengths)  (:287-288, model.py:117-135)
+        # as one HIP launch each way
+        dur_loss = O.duration_loss_fused(logw, dur, x_lengths)
         if out_size is not None:  # :290-312 (host-side random crop, as the reference)
             max_offset = (y_lengths - out_size).clamp(0)
             offset_ranges = list(zip([0] * max_offset.shape[0], max_offset.cpu().numpy()))

@@ -273,15 +273,15 @@ class Trainer:
                 with self._autocast():
                     dur, prior, diff, _ = self.wrapped(x=batch["x"], x_lengths=batch["x_lengths"],
                                                        y=batch["y"], y_lengths=batch["y_lengths"], **inject)
-                    total = dur + prior + diff
-                vals = torch.stack([dur.detach(), torch.as_tensor(prior).detach(), diff.detach(), total.detach()]).float()
+                # total = dur + prior + diff and the logged [dur, prior, diff, total] in one launch
+                total, vals = OPS.loss_sum(dur, prior, diff)
                 logged = vals if logged is None else logged + vals
                 if i == n - 1 and self._arm is not None:
                     # the last micro-batch's backward exchanges the accumulated gradients (and the logged
                     # means) bucket by bucket as backward produces them
                     self.reducer.arm(logged / n, overlap=self._arm)
-                (total / n).backward()
-        return logged / n
+                (total / n if n > 1 else total).backward()
+        return logged / n if n > 1 else logged
 
     def _clip_and_update(self):
         if isinstance(self.optimizer, _FlatClipAdamW):  # graph mode: clipping is inside the fused step

@@ -1,0 +1,99 @@
+"""The train step's glue in HIP (csrc/losses.hip) against the torch expressions it replaces:
+sequence masks (utils/model.py:13-34, text_encoder.py:300-303), the duration loss with its backward
+(matcha_tts.py:287-288, utils/model.py:117-135), the loss sum + logged vector (baselightningmodule.py:121-128)."""
+from __future__ import annotations
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+@pytest.mark.parametrize("B,T", [(1, 1), (3, 17), (32, 120), (8, 4096)])
+def test_sequence_mask_f32_and_key_bias(B, T):
+    from matcha.models.components import _ops as O
+    from matcha.utils.model import sequence_mask
+
+    g = torch.Generator().manual_seed(B + T)
+    lengths = torch.randint(0, T + 1, (B,), generator=g).to(DEV)
+    lengths[0] = T
+    m, kb = O.sequence_mask_f32(lengths, T, key_bias=True)
+    want = sequence_mask(lengths, T).float()
+    assert torch.equal(m, want)
+    assert torch.equal(kb, (want - 1.0) * 1e4)
+    assert torch.equal(O.sequence_mask_f32(lengths.int(), T), want)
+
+
+@pytest.mark.parametrize("B,T", [(4, 24), (32, 120), (8, 512)])
+def test_duration_loss_matches_torch(B, T):
+    from matcha.models.components import _ops as O
+    from matcha.utils.model import sequence_mask
+
+    g = torch.Generator().manual_seed(B * T)
+    lengths = torch.randint(1, T + 1, (B,), generator=g)
+    lengths[0] = T
+    x_mask = sequence_mask(lengths, T).float().unsqueeze(1).to(DEV)
+    dur = (torch.randint(0, 12, (B, T), generator=g).float().to(DEV)) * x_mask[:, 0]  # zero durations included
+    logw0 = torch.randn(B, 1, T, generator=g).to(DEV) * x_mask
+    lengths = lengths.to(DEV)
+
+    logw = logw0.clone().requires_grad_(True)
+    loss = O.duration_loss_fused(logw, dur, lengths)
+    loss.backward()
+    ref_w = logw0.clone().requires_grad_(True)
+    logw_ = torch.log(1e-8 + dur.unsqueeze(1)) * x_mask
+    ref = torch.sum((ref_w - logw_) ** 2) / torch.sum(lengths)
+    ref.backward()
+    torch.testing.assert_close(loss, ref, rtol=2e-6, atol=0)  # fixed-order vs torch's tree sum
+    torch.testing.assert_close(logw.grad, ref_w.grad, rtol=1e-6, atol=1e-9)
+
+
+def test_loss_sum_and_gradients():
+    from matcha.models.components import _ops as O
+
+    vals = [torch.tensor(v, device=DEV, requires_grad=True) for v in (0.75, 2.5, 4.125)]
+    total, logged = O.loss_sum(*vals)
+    assert float(total) == (0.75 + 2.5) + 4.125
+    assert logged.tolist() == [0.75, 2.5, 4.125, 7.375] and not logged.requires_grad
+    (3.0 * total).backward()
+    assert [float(v.grad) for v in vals] == [3.0, 3.0, 3.0]
+    d, f = (torch.tensor(v, device=DEV, requires_grad=True) for v in (1.0, 2.0))
+    total, logged = O.loss_sum(d, 0, f)  # prior_loss=False: the int 0 of the reference
+    total.backward()
+    assert logged.tolist() == [1.0, 0.0, 2.0, 3.0] and float(d.grad) == float(f.grad) == 1.0
+
+
+@pytest.mark.parametrize("B", [1, 5, 32])
+def test_time_mlp_matches_torch(B):
+    """decoder.py:33-49 (Linear -> SiLU -> Linear) + each Resnet1D.mlp (Mish -> Linear) on the shared temb:
+    the fused HIP path (csrc/time_mlp.hip) against the torch modules, forward and every weight / bias
+    gradient, fp32."""
+    import torch.nn.functional as F
+
+    from matcha.models.components import _ops as O
+    from matcha.models.components.decoder import TimeStepEmbeddingNet
+
+    torch.manual_seed(B)
+    mlp = TimeStepEmbeddingNet(160, 1024).to(DEV)
+    projs = [torch.nn.Linear(1024, 256).to(DEV) for _ in range(6)]
+    e = torch.randn(B, 160, device=DEV) * 3
+    temb, tps = O.time_mlp(e, mlp.linear_1, mlp.linear_2, projs)
+    w = [torch.randn(B, 256, device=DEV) for _ in projs]
+    sum((tp * wi).sum() for tp, wi in zip(tps, w)).backward()
+    got = [p.grad.clone() for p in list(mlp.parameters()) + [q for lin in projs for q in lin.parameters()]]
+    for p in list(mlp.parameters()) + [q for lin in projs for q in lin.parameters()]:
+        p.grad = None
+    ref_temb = mlp(e)
+    ref_tps = [lin(F.mish(ref_temb)) for lin in projs]
+    sum((tp * wi).sum() for tp, wi in zip(ref_tps, w)).backward()
+    want = [p.grad for p in list(mlp.parameters()) + [q for lin in projs for q in lin.parameters()]]
+    torch.testing.assert_close(temb, ref_temb, rtol=2e-5, atol=2e-6)
+    for a, b in zip(tps, ref_tps):
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-6)
+        assert a.is_contiguous()
+    for a, b in zip(got, want):
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-5 * b.abs().max().item())
+    # deterministic: a second pass is bitwise identical
+    temb2, tps2 = O.time_mlp(e, mlp.linear_1, mlp.linear_2, projs)
+    assert torch.equal(temb, temb2) and all(torch.equal(a, b) for a, b in zip(tps, tps2))

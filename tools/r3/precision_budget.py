@@ -98,6 +98,23 @@ def child(name: str) -> None:
         out["dec32"] = rel(run(True)[0])
         MA.prior_maximum_path = real_pmp
         del model.decoder.compute_loss_and_prior
+        # weight rounding vs activation rounding: the GEMM weights (conv / linear, not the embedding lookup)
+        # rounded to bf16 in both runs
+        if name == "default":
+            saved_w = {}
+            with torch.no_grad():
+                for n_, p_ in model.named_parameters():
+                    if p_.dim() >= 2 and "embedding" not in n_:
+                        saved_w[n_] = p_.detach().clone()
+                        p_.copy_(p_.bfloat16().float())
+            lr32, _ = run(False)
+            lr16, _ = run(True)
+            with torch.no_grad():
+                for n_, p_ in model.named_parameters():
+                    if n_ in saved_w:
+                        p_.copy_(saved_w[n_])
+            out["wround_fp32_vs_fp32"] = rel(lr32)  # the effect of rounding the weights alone
+            out["wround_bf16_vs_wround_fp32"] = [abs(x - y) / abs(y) for x, y in zip(lr16, lr32)]  # activations alone
         print(json.dumps(out), flush=True)
 
 
