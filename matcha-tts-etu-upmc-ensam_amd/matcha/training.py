@@ -273,8 +273,14 @@ class Trainer:
                 with self._autocast():
                     dur, prior, diff, _ = self.wrapped(x=batch["x"], x_lengths=batch["x_lengths"],
                                                        y=batch["y"], y_lengths=batch["y_lengths"], **inject)
-                # total = dur + prior + diff and the logged [dur, prior, diff, total] in one launch
-                total, vals = OPS.loss_sum(dur, prior, diff)
+                # total = dur + prior + diff and the logged [dur, prior, diff, total] in one launch (device
+                # tensors; the CPU data-parallel tests drive this loop with a CPU stand-in model)
+                if dur.device.type == "cuda":
+                    total, vals = OPS.loss_sum(dur, prior, diff)
+                else:
+                    total = dur + prior + diff
+                    vals = torch.stack([dur.detach(), torch.as_tensor(prior).detach(), diff.detach(),
+                                        total.detach()]).float()
                 logged = vals if logged is None else logged + vals
                 if i == n - 1 and self._arm is not None:
                     # the last micro-batch's backward exchanges the accumulated gradients (and the logged
