@@ -430,21 +430,33 @@ def main():
         t_inj = torch.rand(32, 1, 1, generator=gen).to(dev)
         z_inj = torch.randn(32, 80, 600, generator=gen).to(dev)
         res = {}
+        modes = (("32-true", "32-true", False, False), ("one_plane", "bf16-mixed", False, False),
+                 ("split_weights", "bf16-mixed", True, False), ("parity_policy", "bf16-mixed", True, True))
         with torch.no_grad():
-            for prec in ("32-true", "bf16-mixed"):
+            for name, prec, split, enc32 in modes:
+                old = OPS.set_weight_split(split)
+                pm.encoder_fp32 = enc32
                 with torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec == "bf16-mixed"):
                     out = pm(pb["x"], pb["x_lengths"], pb["y"], pb["y_lengths"], t=t_inj, z=z_inj)
-                res[prec] = ([float(v) for v in out[:3]], out[3].detach())
+                OPS.set_weight_split(old)
+                res[name] = ([float(v) for v in out[:3]], out[3].detach())
         del pm
         l32, a32 = res["32-true"]
-        l16, a16 = res["bf16-mixed"]
+
+        def errs(name):
+            l16, a16 = res[name]
+            return {"loss_rel_err": [round(abs(a - b) / abs(b), 7) for a, b in zip(l16, l32)],
+                    "alignment_cell_agreement": round(float((a16 == a32).float().mean().item()), 6)}
+
         precision_check = {
-            "bf16_loss_rel_err": [round(abs(a - b) / abs(b), 7) for a, b in zip(l16, l32)],
-            "losses": ["dur", "prior", "diff"],
-            "alignment_cell_agreement": round(float((a16 == a32).float().mean().item()), 6),
-            "weight_split": OPS._W_SPLIT,
+            "bf16_loss_rel_err": errs("split_weights" if OPS._W_SPLIT else "one_plane")["loss_rel_err"],
+            "run_mode": "split_weights" if OPS._W_SPLIT else "one_plane",
+            "modes": {k: errs(k) for k in ("one_plane", "split_weights", "parity_policy")},
+            "losses": ["dur", "prior", "diff"], "bar": "prior / diff within 1e-4 relative (north star)",
             "note": "bf16-mixed vs 32-true (= the oracle at this batch) with the parity tests' recipe weights and "
-                    "batch, eval mode, same t / z; bf16 activations x split bf16 weight planes (MTTS_W_SPLIT)"}
+                    "batch, eval mode, same t / z.  one_plane: bf16 weights (the fp32 weights' rounding is the "
+                    "error); split_weights: hi + rounding-residual bf16 planes (MTTS_W_SPLIT=1); parity_policy: "
+                    "split weights + the text encoder in exact fp32 (MatchaTTS.encoder_fp32)"}
 
     # same-run extra lines (N=1): the reference precision (32-true: exact fp32 MFMA) on the bench workload,
     # and the reference's own step shape -- 2 micro-batches of 16 with gradient accumulation
@@ -452,9 +464,16 @@ def main():
     extra = None
     if world == 1 and not args.no_extra and not args.bucketed and graph:
         extra = {}
-        for name, prec, micro, acc in (("32-true", "32-true", B, 1), ("reference_step_16x2", args.precision, B // 2, 2)):
+        lines = [("32-true", "32-true", B, 1, False), ("reference_step_16x2", args.precision, B // 2, 2, OPS._W_SPLIT)]
+        if args.precision == "bf16-mixed":
+            lines.append(("bf16_split_weights" if not OPS._W_SPLIT else "bf16_one_plane", args.precision, B, 1,
+                          not OPS._W_SPLIT))
+            lines.append(("bf16_parity_policy", args.precision, B, 1, True))
+        for name, prec, micro, acc, split in lines:
+            old_split = OPS.set_weight_split(split)
             torch.manual_seed(1234)
             m2 = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(dev).train()
+            m2.encoder_fp32 = name == "bf16_parity_policy"
             tr2 = Trainer(m2, TrainConfig(precision=prec, graph=True, accumulate_grad_batches=acc))
             bs2 = [synthetic_batch(micro, Tx, Ty, seed=2000 + i, device=dev) for i in range(acc)]
             for _ in range(3):
@@ -468,8 +487,10 @@ def main():
             ms2 = (time.perf_counter() - t0x) / n2 * 1e3
             extra[name] = {"ms_per_step": round(ms2, 3), "utterances_per_s": round(micro * acc / ms2 * 1e3, 2),
                            "steps": n2, "precision": prec, "micro_batch": micro, "accumulate_grad_batches": acc,
+                           "weight_planes": 2 if (split and prec == "bf16-mixed") else 1,
                            "losses": [round(v, 5) for v in tr2.last_losses.tolist()]}
             del tr2, m2
+            OPS.set_weight_split(old_split)
         torch.cuda.empty_cache()
 
     mas_ms = sum(a.elapsed_time(b) for a, b in mas_events) / max(len(mas_events), 1)

@@ -334,6 +334,12 @@ typedef struct mtts_reduce_job {
 } mtts_reduce_job;
 
 int mtts_reduce_partials(const mtts_reduce_job *jobs, int32_t njobs, void *hip_stream);
+/* out[c] (+)= sum_r x[r * ld + c] for c < n (a bias gradient): one partials launch over 128-row chunks
+ * (workspace: mtts_colsum_workspace_size bytes, kept alive by the caller until the sums ran) + one
+ * reduce job, queued when deferral is on.  Fixed order (deterministic). */
+size_t mtts_colsum_workspace_size(int64_t rows, int32_t n);
+int mtts_colsum(const float *x, int64_t rows, int32_t n, int32_t ld, float *out, int32_t accumulate, float *workspace,
+                size_t workspace_bytes, void *hip_stream);
 void mtts_defer_reductions(int32_t on);
 int32_t mtts_pending_reductions(void);
 int mtts_flush_reductions(void *hip_stream);
@@ -370,20 +376,27 @@ int mtts_embedding_bwd(const int64_t *ids, const float *dout, int64_t rows, int3
 #define MTTS_ROWS_ACT_NONE 0
 #define MTTS_ROWS_ACT_SILU 1 /* x / (1 + exp(-x)) */
 #define MTTS_ROWS_ACT_MISH 2 /* x tanh(softplus(x)) */
-/* For each of nmat (<= 8) matrices W_i [N_i, K] (fp32, 16-byte aligned rows) sharing the input x [B, K]:
+/* For each of nmat (<= 8) matrices W_i [N_i, K] (fp32, 16-byte aligned rows; stacked: N_i % 64 == 0)
+ * sharing the input x [B, K]:
  *   out_i[b, n] = sum_k x[b, k] W_i[n, k] + bias_i[n]   (bias table or its entries may be NULL)
  *   out_act_i = act(out_i)                              (out_act table or entries may be NULL)
- * K % 4 == 0.  Fixed-order sums (deterministic). */
+ * K % 4 == 0.  Exact fp32 MFMA; the reduction is split over workgroups (256 indices each) and summed in a
+ * fixed order by the last workgroup of each output tile: deterministic.  workspace: at least
+ * mtts_rows_linear_workspace_size(B, K, nmat, N) bytes, 256-byte aligned, its first (counter) region
+ * ZEROED once by the caller before first use -- the kernels leave it zeroed (graph replays reuse it);
+ * one workspace serves the forward and backward calls of the same (B, K, nmat, N) on one stream. */
+size_t mtts_rows_linear_workspace_size(int32_t B, int32_t K, int32_t nmat, const int32_t *N);
 int mtts_rows_linear_fwd(const float *x, int32_t B, int32_t K, int32_t nmat, const float *const *W,
                          const float *const *bias, const int32_t *N, float *const *out, float *const *out_act,
-                         int32_t act, void *hip_stream);
+                         int32_t act, void *workspace, size_t workspace_bytes, void *hip_stream);
 /* Backward of out_i = a W_i^T + bias_i with a = act(pre) the layer's input rows [B, K]:
- *   dx[b, k]   = (sum_i sum_n dy_i[b, n] W_i[n, k]) * act'(pre[b, k])   (dx may be NULL)
+ *   dx[b, k]   = (sum_i sum_n dy_i[b, n] W_i[n, k]) * act'(pre[b, k])   (dx may be NULL; N_i % 4 == 0)
  *   dW_i[n, k] = sum_b dy_i[b, n] a[b, k] ; db_i[n] = sum_b dy_i[b, n]    (dW NULL: neither; db table may be NULL)
- * All outputs are overwritten.  act NONE: pre unused (dx is the plain input gradient). */
+ * All outputs are overwritten.  act NONE: pre unused (dx is the plain input gradient).  Workspace as above. */
 int mtts_rows_linear_bwd(const float *a, const float *pre, int32_t act, int32_t B, int32_t K, int32_t nmat,
                          const float *const *W, const int32_t *N, const float *const *dy, float *dx,
-                         float *const *dW, float *const *db, void *hip_stream);
+                         float *const *dW, float *const *db, void *workspace, size_t workspace_bytes,
+                         void *hip_stream);
 
 #ifdef __cplusplus
 } /* extern "C" */

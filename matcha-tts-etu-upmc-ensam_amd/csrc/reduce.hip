@@ -11,6 +11,9 @@
 // is bitwise reproducible.  Long, narrow jobs (the norm partials: ~500 slabs of 256 columns) use 16
 // groups x 16 slices per block; wide ones (weight gradients) 64 groups x 4 slices.
 //
+// mtts_colsum: column sums of a tall matrix as per-128-row-chunk partials (one launch) + one such job (the
+// transposed conv's bias gradient, decoder.py:112), fixed order like the rest.
+//
 // Deferral (mtts_defer_reductions) queues the jobs of a whole backward pass and mtts_flush_reductions
 // runs them in one batched launch; the queue is process-wide because autograd calls the backward
 // entry points from its own thread.
@@ -141,6 +144,26 @@ int check_jobs(const mtts_reduce_job *jobs, int njobs) {
     return MTTS_OK;
 }
 
+constexpr int kColChunk = 128;
+
+__global__ __launch_bounds__(256) void colsum_partials_kernel(const float *__restrict__ x, int64_t rows, int n, int ld,
+                                                              float *__restrict__ part) {
+    const int c = blockIdx.y * 256 + threadIdx.x;
+    if (c >= n) return;
+    const int64_t r0 = (int64_t)blockIdx.x * kColChunk;
+    const int64_t r1 = r0 + kColChunk < rows ? r0 + kColChunk : rows;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // four chains, added in a fixed order
+    int64_t r = r0;
+    for (; r + 3 < r1; r += 4) {
+        a0 += x[r * ld + c];
+        a1 += x[(r + 1) * ld + c];
+        a2 += x[(r + 2) * ld + c];
+        a3 += x[(r + 3) * ld + c];
+    }
+    for (; r < r1; ++r) a0 += x[r * ld + c];
+    part[(size_t)blockIdx.x * n + c] = (a0 + a1) + (a2 + a3);
+}
+
 std::mutex g_mu;
 bool g_defer = false;
 std::vector<mtts_reduce_job> g_queue;
@@ -185,6 +208,31 @@ int mtts_flush_reductions(void *hip_stream) {
         q.swap(g_queue);
     }
     return launch_jobs(q.data(), (int)q.size(), static_cast<hipStream_t>(hip_stream));
+}
+
+int mtts_colsum(const float *x, int64_t rows, int32_t n, int32_t ld, float *out, int32_t accumulate, float *workspace,
+                size_t workspace_bytes, void *hip_stream) {
+    MTTS_CHECK_ARG(x && out && rows >= 1 && n >= 1 && ld >= n, "colsum: bad args");
+    const int64_t chunks = (rows + kColChunk - 1) / kColChunk;
+    MTTS_CHECK_ARG(chunks <= INT32_MAX, "colsum: too many rows");
+    if (!workspace || workspace_bytes < (size_t)chunks * n * sizeof(float))
+        return mtts::fail(MTTS_ERR_WORKSPACE, "colsum: workspace too small");
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+    hipLaunchKernelGGL(colsum_partials_kernel, dim3((unsigned)chunks, (n + 255) / 256), dim3(256), 0, st, x, rows, n, ld,
+                       workspace);
+    if (int rc = mtts::check_launch("colsum_partials_kernel")) return rc;
+    mtts_reduce_job j = {};
+    j.part = workspace;
+    j.out = out;
+    j.stride = n;
+    j.n = n;
+    j.splits = (int32_t)chunks;
+    j.accumulate = accumulate;
+    return mtts::submit_reductions(&j, 1, st);
+}
+
+size_t mtts_colsum_workspace_size(int64_t rows, int32_t n) {
+    return rows < 1 || n < 1 ? 0 : (size_t)((rows + kColChunk - 1) / kColChunk) * n * sizeof(float);
 }
 
 void mtts_discard_reductions(void) {

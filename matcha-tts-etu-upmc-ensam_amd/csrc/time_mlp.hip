@@ -23,7 +23,6 @@
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-constexpr int kMaxWaves = 16;
 constexpr int kChunk = 64;  // reduction indices per wave and pass: 32 MFMAs of 32x32x2
 
 enum Mode { kFwd = 0, kDgrad = 1, kWgrad = 2 };
@@ -64,19 +63,36 @@ __device__ __forceinline__ float act_grad(int act, float v) {
     return 1.f;
 }
 
-// Grid: tiles of C (rows = tm tiles of 32, cols as the mode defines), one workgroup each, nw waves.
-// Operand fragments of v_mfma_f32_32x32x2_f32: lane l holds A(row l%32, slot l/32) and B(slot l/32,
-// col l%32).  Pass index j covers reduction indices r0 + 4j .. r0 + 4j + 3: slot s of MFMA 2j + e takes
-// index r0 + 4j + 2s + e (any fixed bijection works: both operands use the same one).
+// One workgroup = one 32 x 32 tile of C and one 256-wide range of the reduction (4 waves x 64); the
+// reduction is split over KS workgroups per tile so that a launch spreads over ~200 CUs.  Operand fragments
+// of v_mfma_f32_32x32x2_f32: lane l holds A(row l%32, slot l/32) and B(slot l/32, col l%32); within a
+// wave's 64 indices, slot s of MFMA j takes index 32 s + j (one fixed bijection for both operands).
+// Operands contiguous along the reduction (x / W rows in the forward, dy rows in dgrad) are staged through
+// LDS with coalesced float4 loads (a 32 x 64 block per wave); the others are read straight into the
+// fragment (lanes run along their contiguous dimension).  The 4 wave partials are added in wave order;
+// with KS > 1 the workgroup stores its partial tile and the LAST of the tile's KS workgroups to arrive
+// (a per-tile ticket counter, agent-scope release / acquire) adds the KS partials in index order and runs
+// the epilogue -- a fixed summation order whatever the arrival order, and the counter is reset for the next
+// launch (graph replays reuse it).
+constexpr int kWaves = 4;
+constexpr int kRange = kWaves * kChunk;  // reduction indices per workgroup
+constexpr int kLd = 65;                  // staged row pitch (floats): conflict-free column reads
+
+struct Ws {
+    float *part;        // [tiles][KS][32 * 32]
+    unsigned *counter;  // [tiles], zero between launches
+    int ks;
+};
+
 template <int MODE>
-__global__ __launch_bounds__(64 * kMaxWaves) void rows_gemm_kernel(MatTable T, const float *__restrict__ x, int B,
-                                                                   int K, int act, const float *__restrict__ pre,
-                                                                   float *__restrict__ dx, int col_tiles) {
-    __shared__ float part[kMaxWaves][16][64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+__global__ __launch_bounds__(64 * kWaves) void rows_gemm_kernel(MatTable T, const float *__restrict__ x, int B, int K,
+                                                                int act, const float *__restrict__ pre,
+                                                                float *__restrict__ dx, int col_tiles, Ws ws) {
+    extern __shared__ float lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lr = lane & 31, s = lane >> 5;
-    // tile -> (row block, column block, matrix)
-    const int rt = blockIdx.x / col_tiles, ct = blockIdx.x - rt * col_tiles;
+    const int tile = blockIdx.x / ws.ks, ksi = blockIdx.x - tile * ws.ks;
+    const int rt = tile / col_tiles, ct = tile - rt * col_tiles;
     int mat = 0, m0 = rt * 32, c0 = ct * 32, R = 0;
     if constexpr (MODE == kFwd) {  // rows b, cols n of matrix mat (stacked column tiles), reduce over K
         while (mat + 1 < T.nmat && c0 >= T.n_off[mat + 1]) ++mat;
@@ -85,60 +101,94 @@ __global__ __launch_bounds__(64 * kMaxWaves) void rows_gemm_kernel(MatTable T, c
     } else if constexpr (MODE == kDgrad) {  // rows b, cols k, reduce over the stacked n
         R = T.n_off[T.nmat];
     } else {  // rows n of matrix mat (stacked row tiles), cols k, reduce over b
-        m0 = rt * 32;
         while (mat + 1 < T.nmat && m0 >= T.n_off[mat + 1]) ++mat;
         m0 -= T.n_off[mat];
         R = B;
     }
+    const int r0 = ksi * kRange + wave * kChunk;  // this wave's 64 indices
+    float *sA = lds + wave * 2 * 32 * kLd, *sB = sA + 32 * kLd;
+    // stage a 32 x 64 block (rows row0.., indices r0..r0+63) of a row-major matrix, zero outside
+    auto stage = [&](const float *base, int ld, int nrows, int r_end, float *dst) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = q * 64 + lane, row = e >> 4, c4 = (e & 15) * 4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (row < nrows && r0 + c4 < r_end) v = *reinterpret_cast<const float4 *>(base + (size_t)row * ld + r0 + c4);
+            dst[row * kLd + c4] = v.x;
+            dst[row * kLd + c4 + 1] = v.y;
+            dst[row * kLd + c4 + 2] = v.z;
+            dst[row * kLd + c4 + 3] = v.w;
+        }
+    };
+    float a[32], b[32];
+    if constexpr (MODE == kFwd) {
+        stage(x + (size_t)m0 * K, K, min(32, B - m0), R, sA);
+        stage(T.W[mat] + (size_t)c0 * K, K, min(32, T.N[mat] - c0), R, sB);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            a[j] = sA[lr * kLd + 32 * s + j];
+            b[j] = sB[lr * kLd + 32 * s + j];
+        }
+    } else if constexpr (MODE == kDgrad) {
+        int dm = 0;  // the wave's matrix (stacked N_i are multiples of 64: a wave never straddles two)
+        while (dm + 1 < T.nmat && r0 >= T.n_off[dm + 1]) ++dm;
+        const int base = T.n_off[dm], Nm = T.N[dm];
+        stage(T.dy[dm] + (size_t)m0 * Nm - base, Nm, min(32, B - m0), min(R, base + Nm), sA);
+        __syncthreads();
+        const int k = c0 + lr;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const int r = r0 + 32 * s + j;
+            a[j] = sA[lr * kLd + 32 * s + j];
+            b[j] = r < R && k < K ? T.W[dm][(size_t)(r - base) * K + k] : 0.f;
+        }
+    } else {
+        const int n = m0 + lr, k = c0 + lr, Nm = T.N[mat];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const int r = r0 + 32 * s + j;
+            a[j] = r < R && n < Nm ? T.dy[mat][(size_t)r * Nm + n] : 0.f;
+            b[j] = r < R && k < K ? x[(size_t)r * K + k] : 0.f;
+        }
+    }
     f32x16 acc;
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[v] = 0.f;
-    for (int r0 = wave * kChunk; r0 < R; r0 += nw * kChunk) {
-        float a[32], b[32];  // this pass: 16 index pairs x (A, B)
-        // dgrad: the pass's matrix (every N_i is a multiple of kChunk: a pass never straddles two)
-        int dm = 0;
-        if constexpr (MODE == kDgrad) {
-            while (dm + 1 < T.nmat && r0 >= T.n_off[dm + 1]) ++dm;
-        }
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int r = r0 + 4 * j + 2 * s + e;
-                const bool ok = r < R;
-                float av = 0.f, bv = 0.f;
-                if constexpr (MODE == kFwd) {
-                    const int row = min(m0 + lr, B - 1), n = c0 + lr;
-                    av = ok && m0 + lr < B ? x[(size_t)row * K + r] : 0.f;
-                    bv = ok && n < T.N[mat] ? T.W[mat][(size_t)n * K + r] : 0.f;
-                } else if constexpr (MODE == kDgrad) {
-                    const int rn = r - T.n_off[dm], Nm = T.N[dm];
-                    const int row = min(m0 + lr, B - 1), k = c0 + lr;
-                    av = ok && m0 + lr < B ? T.dy[dm][(size_t)row * Nm + rn] : 0.f;
-                    bv = ok && k < K ? T.W[dm][(size_t)rn * K + k] : 0.f;
-                } else {
-                    const int n = m0 + lr, k = c0 + lr, Nm = T.N[mat];
-                    av = ok && n < Nm ? T.dy[mat][(size_t)r * Nm + n] : 0.f;
-                    bv = ok && k < K ? x[(size_t)r * K + k] : 0.f;
-                }
-                a[2 * j + e] = av;
-                b[2 * j + e] = bv;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 32; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
-    }
-    // wave order sum of the partial tiles (wave 0 adds waves 1 .. nw-1 in order)
+    for (int j = 0; j < 32; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
+    // the workgroup's tile: waves 1..3 through LDS (the staging area is free after this barrier), wave order
+    const int nw = blockDim.x >> 6;
     if (nw > 1) {
+        __syncthreads();
+        float *part = lds;  // [nw][16][64]
         if (wave > 0) {
 #pragma unroll
-            for (int v = 0; v < 16; ++v) part[wave][v][lane] = acc[v];
+            for (int v = 0; v < 16; ++v) part[(wave * 16 + v) * 64 + lane] = acc[v];
         }
         __syncthreads();
         if (wave > 0) return;
         for (int w = 1; w < nw; ++w)
 #pragma unroll
-            for (int v = 0; v < 16; ++v) acc[v] += part[w][v][lane];
+            for (int v = 0; v < 16; ++v) acc[v] += part[(w * 16 + v) * 64 + lane];
+    }
+    if (ws.ks > 1) {  // split reduction: the last workgroup of the tile to arrive sums the partials in order
+        float *mine = ws.part + ((size_t)tile * ws.ks + ksi) * 1024;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) mine[v * 64 + lane] = acc[v];
+        __threadfence();  // release: the partial is visible device-wide before the ticket
+        unsigned ticket = 0;
+        if (lane == 0) ticket = atomicAdd(ws.counter + tile, 1u);
+        ticket = __shfl(ticket, 0);
+        if (ticket != (unsigned)ws.ks - 1) return;
+        __threadfence();  // acquire: the other workgroups' partials
+        const float *all = ws.part + (size_t)tile * ws.ks * 1024;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[v] = __builtin_nontemporal_load(all + v * 64 + lane);
+        for (int q = 1; q < ws.ks; ++q)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) acc[v] += __builtin_nontemporal_load(all + (size_t)q * 1024 + v * 64 + lane);
+        if (lane == 0) atomicExch(ws.counter + tile, 0u);  // ready for the next launch
     }
     // C(row, col) of acc[v]: row = (v & 3) + 8 (v >> 2) + 4 s, col = lr
 #pragma unroll
@@ -164,7 +214,7 @@ __global__ __launch_bounds__(64 * kMaxWaves) void rows_gemm_kernel(MatTable T, c
         if (ct == 0 && T.out2[mat] && lane < 32 && m0 + lane < T.N[mat]) {
             const int n = m0 + lane, Nm = T.N[mat];
             float sacc = 0.f;
-            for (int b = 0; b < B; ++b) sacc += T.dy[mat][(size_t)b * Nm + n];
+            for (int b2 = 0; b2 < B; ++b2) sacc += T.dy[mat][(size_t)b2 * Nm + n];
             T.out2[mat][n] = sacc;
         }
     }
@@ -183,23 +233,65 @@ int fill_table(MatTable &T, int nmat, const int32_t *N) {
     return MTTS_OK;
 }
 
-int waves_for(int R) {
-    const int w = (R + kChunk - 1) / kChunk;
-    return w < 1 ? 1 : (w > kMaxWaves ? kMaxWaves : w);
+// launch geometry of one rows GEMM: KS workgroups per tile, waves per workgroup, dynamic LDS bytes
+struct Geo {
+    int ks, waves;
+    size_t lds;
+};
+Geo geometry(int R, bool staged) {
+    Geo g;
+    g.ks = (R + kRange - 1) / kRange;
+    g.waves = R >= kRange ? kWaves : (R + kChunk - 1) / kChunk;
+    const size_t stage = staged ? (size_t)g.waves * 2 * 32 * kLd * sizeof(float) : 0;
+    const size_t red = g.waves > 1 ? (size_t)g.waves * 16 * 64 * sizeof(float) : 0;
+    g.lds = stage > red ? stage : red;
+    return g;
+}
+
+int check_ws(const Geo &g, int tiles, void *ws, size_t ws_bytes, Ws &w) {
+    w.ks = g.ks;
+    w.part = nullptr;
+    w.counter = nullptr;
+    if (g.ks == 1) return MTTS_OK;
+    const size_t need = mtts::align_up((size_t)tiles * sizeof(unsigned), 256) + (size_t)tiles * g.ks * 1024 * sizeof(float);
+    if (!ws || ws_bytes < need || (uintptr_t)ws % 256)
+        return mtts::fail(MTTS_ERR_WORKSPACE, "rows_linear: workspace too small (mtts_rows_linear_workspace_size)");
+    w.counter = static_cast<unsigned *>(ws);
+    w.part = reinterpret_cast<float *>(static_cast<char *>(ws) + mtts::align_up((size_t)tiles * sizeof(unsigned), 256));
+    return MTTS_OK;
 }
 
 }  // namespace
 
+extern "C" size_t mtts_rows_linear_workspace_size(int32_t B, int32_t K, int32_t nmat, const int32_t *N) {
+    if (B < 1 || K < 1 || nmat < 1 || nmat > MTTS_ROWS_MAX_MATS || !N) return 0;
+    size_t nt = 0;  // 32-column tiles of the stacked outputs
+    for (int i = 0; i < nmat; ++i) nt += (size_t)(N[i] + 31) / 32;
+    const size_t rt = (size_t)(B + 31) / 32, kt = (size_t)(K + 31) / 32;
+    auto ks = [](size_t r) { return (r + kRange - 1) / kRange; };
+    // (tiles, splits) of the forward, dgrad and wgrad launches
+    const size_t t[3] = {rt * nt, rt * kt, nt * kt}, k[3] = {ks(K), ks(nt * 32), ks(B)};
+    size_t tiles = 0, parts = 0;
+    for (int m = 0; m < 3; ++m) {
+        if (k[m] < 2) continue;
+        tiles = t[m] > tiles ? t[m] : tiles;
+        parts = t[m] * k[m] > parts ? t[m] * k[m] : parts;
+    }
+    return mtts::align_up(tiles * sizeof(unsigned), 256) + parts * 1024 * sizeof(float);
+}
+
 extern "C" int mtts_rows_linear_fwd(const float *x, int32_t B, int32_t K, int32_t nmat, const float *const *W,
                                     const float *const *bias, const int32_t *N, float *const *out,
-                                    float *const *out_act, int32_t act, void *hip_stream) {
-    MTTS_CHECK_ARG(x && W && out && B >= 1 && K >= 1, "rows_linear_fwd: bad args");
+                                    float *const *out_act, int32_t act, void *workspace, size_t workspace_bytes,
+                                    void *hip_stream) {
+    MTTS_CHECK_ARG(x && W && out && B >= 1 && K >= 4 && K % 4 == 0 && (uintptr_t)x % 16 == 0,
+                   "rows_linear_fwd: bad args (K % 4 == 0, 16-byte aligned rows)");
     MTTS_CHECK_ARG(act >= MTTS_ROWS_ACT_NONE && act <= MTTS_ROWS_ACT_MISH, "rows_linear_fwd: bad act");
     MatTable T{};
     if (int rc = fill_table(T, nmat, N)) return rc;
     int col_tiles = 0;
     for (int i = 0; i < nmat; ++i) {
-        MTTS_CHECK_ARG(W[i] && out[i], "rows_linear_fwd: null matrix / output");
+        MTTS_CHECK_ARG(W[i] && out[i] && (uintptr_t)W[i] % 16 == 0, "rows_linear_fwd: null / unaligned matrix");
         MTTS_CHECK_ARG(nmat == 1 || N[i] % 32 == 0, "rows_linear_fwd: stacked matrices need N_i % 32 == 0");
         T.W[i] = W[i];
         T.bias[i] = bias ? bias[i] : nullptr;
@@ -208,15 +300,19 @@ extern "C" int mtts_rows_linear_fwd(const float *x, int32_t B, int32_t K, int32_
         col_tiles += (N[i] + 31) / 32;
     }
     if (nmat == 1) T.n_off[1] = col_tiles * 32;  // one matrix: every column tile is its own
-    const int rt = (B + 31) / 32;
-    hipLaunchKernelGGL(rows_gemm_kernel<kFwd>, dim3(rt * col_tiles), dim3(64 * waves_for(K)), 0,
-                       static_cast<hipStream_t>(hip_stream), T, x, B, K, act, nullptr, nullptr, col_tiles);
+    const int tiles = ((B + 31) / 32) * col_tiles;
+    const Geo g = geometry(K, true);
+    Ws w;
+    if (int rc = check_ws(g, tiles, workspace, workspace_bytes, w)) return rc;
+    hipLaunchKernelGGL(rows_gemm_kernel<kFwd>, dim3(tiles * g.ks), dim3(64 * g.waves), g.lds,
+                       static_cast<hipStream_t>(hip_stream), T, x, B, K, act, nullptr, nullptr, col_tiles, w);
     return mtts::check_launch("rows_gemm_kernel<fwd>");
 }
 
 extern "C" int mtts_rows_linear_bwd(const float *a, const float *pre, int32_t act, int32_t B, int32_t K, int32_t nmat,
                                     const float *const *W, const int32_t *N, const float *const *dy, float *dx,
-                                    float *const *dW, float *const *db, void *hip_stream) {
+                                    float *const *dW, float *const *db, void *workspace, size_t workspace_bytes,
+                                    void *hip_stream) {
     MTTS_CHECK_ARG(W && dy && B >= 1 && K >= 1, "rows_linear_bwd: bad args");
     MTTS_CHECK_ARG(act >= MTTS_ROWS_ACT_NONE && act <= MTTS_ROWS_ACT_MISH && (act == MTTS_ROWS_ACT_NONE || pre),
                    "rows_linear_bwd: act' needs the pre-activation");
@@ -226,7 +322,8 @@ extern "C" int mtts_rows_linear_bwd(const float *a, const float *pre, int32_t ac
     if (int rc = fill_table(T, nmat, N)) return rc;
     int row_tiles = 0;
     for (int i = 0; i < nmat; ++i) {
-        MTTS_CHECK_ARG(W[i] && dy[i], "rows_linear_bwd: null matrix");
+        MTTS_CHECK_ARG(W[i] && dy[i] && (!dx || (N[i] % 4 == 0 && (uintptr_t)dy[i] % 16 == 0)),
+                       "rows_linear_bwd: null matrix (dx: N_i % 4 == 0, 16-byte aligned dy rows)");
         T.W[i] = W[i];
         T.dy[i] = dy[i];
         T.out[i] = dW ? dW[i] : nullptr;
@@ -237,14 +334,21 @@ extern "C" int mtts_rows_linear_bwd(const float *a, const float *pre, int32_t ac
     if (nmat == 1) T.n_off[1] = N[0];
     const int kt = (K + 31) / 32;
     if (dx) {
-        hipLaunchKernelGGL(rows_gemm_kernel<kDgrad>, dim3(((B + 31) / 32) * kt), dim3(64 * waves_for(T.n_off[nmat])), 0,
-                           st, T, nullptr, B, K, act, pre, dx, kt);
+        const int tiles = ((B + 31) / 32) * kt;
+        const Geo g = geometry(T.n_off[nmat], true);
+        Ws w;
+        if (int rc = check_ws(g, tiles, workspace, workspace_bytes, w)) return rc;
+        hipLaunchKernelGGL(rows_gemm_kernel<kDgrad>, dim3(tiles * g.ks), dim3(64 * g.waves), g.lds, st, T, nullptr, B,
+                           K, act, pre, dx, kt, w);
         if (int rc = mtts::check_launch("rows_gemm_kernel<dgrad>")) return rc;
     }
     if (dW) {
         if (nmat == 1) T.n_off[1] = row_tiles * 32;
-        hipLaunchKernelGGL(rows_gemm_kernel<kWgrad>, dim3(row_tiles * kt), dim3(64 * waves_for(B)), 0, st, T, a, B, K,
-                           act, nullptr, nullptr, kt);
+        const Geo g = geometry(B, false);
+        Ws w;
+        if (int rc = check_ws(g, row_tiles * kt, workspace, workspace_bytes, w)) return rc;
+        hipLaunchKernelGGL(rows_gemm_kernel<kWgrad>, dim3(row_tiles * kt * g.ks), dim3(64 * g.waves), g.lds, st, T, a,
+                           B, K, act, nullptr, nullptr, kt, w);
         if (int rc = mtts::check_launch("rows_gemm_kernel<wgrad>")) return rc;
     }
     return MTTS_OK;

@@ -56,10 +56,21 @@ GEMM_F_PRE_BF16 = 0x10  # MTTS_GEMM_F_PRE_BF16: C_pre written / aux read as bf16
 WGRAD_F_DY_BF16 = 0x20  # MTTS_WGRAD_F_DY_BF16: the weight gradient's dY holds bf16
 GEMM_F_W_SPLIT = 0x40  # MTTS_GEMM_F_W_SPLIT: W holds a hi and a lo bf16 plane (two MFMAs per product)
 _FAST_ACT = os.environ.get("MTTS_EXACT_GELU") != "1"
-# bf16-mixed forward GEMMs take their weights as two bf16 planes (hi + rounding residual): the rounding of
-# the fp32 weights is a static model perturbation and was the bf16 loss error (tools/r3/precision_budget.py:
-# prior 2.9e-4 / diff 2.1e-4 from weight rounding alone, activations 3.8e-5 / 2.1e-5).  MTTS_W_SPLIT=0: one plane
-_W_SPLIT = os.environ.get("MTTS_W_SPLIT", "1") != "0"
+# Weight planes of the bf16-mixed forward GEMMs.  Split (two bf16 planes, hi + rounding residual): the
+# rounding of the fp32 weights is a static model perturbation and is the bf16 loss error
+# (tools/r3/precision_budget.py: prior 2.9e-4 / diff 2.1e-4 from weight rounding alone, activations
+# 3.8e-5 / 2.1e-5 at B=32) -- with split planes bf16-mixed meets the 1e-4 loss bar at the bench batch, at
+# ~+50 % forward-GEMM time (bench.py reports both lines).  Default one plane (the throughput mode);
+# MTTS_W_SPLIT=1 or set_weight_split(True) selects the split planes.
+_W_SPLIT = os.environ.get("MTTS_W_SPLIT", "0") == "1"
+
+
+def set_weight_split(on: bool) -> bool:
+    """Selects one (False) or two (True) bf16 weight planes for the bf16-mixed forward GEMMs from the next
+    forward on; returns the previous setting.  (Captured graphs keep the packing they were captured with.)"""
+    global _W_SPLIT
+    old, _W_SPLIT = _W_SPLIT, bool(on)
+    return old
 PACK_BF16_SPLIT = 2  # pack-cache kind: the bf16 hi + lo planes of a forward operand
 
 GEMM_GLDS = 32  # MTTS_GEMM_GLDS: first LDS-DMA schedule id
@@ -144,6 +155,8 @@ N.register("mtts_defer_reductions", None, [_I])
 N.register("mtts_pending_reductions", _I, [])
 N.register("mtts_flush_reductions", ctypes.c_int, [_P])
 N.register("mtts_discard_reductions", None, [])
+N.register("mtts_colsum_workspace_size", _SZ, [_I64, _I])
+N.register("mtts_colsum", ctypes.c_int, [_P, _I64, _I, _I, _P, _I, _P, _SZ, _P])
 
 
 # ------------------------------------------------------------------------------------------ helpers
@@ -303,7 +316,7 @@ def _run_pack(specs, prec):
 
 
 def _pack_kind(spec: PackSpec, prec: int) -> int:
-    """bf16 forward operands: the split planes (unless MTTS_W_SPLIT=0); everything else as prec."""
+    """bf16 forward operands: the split planes when selected (set_weight_split); everything else as prec."""
     return PACK_BF16_SPLIT if (prec == PREC_BF16 and _W_SPLIT and not spec.dgrad) else prec
 
 
@@ -321,7 +334,8 @@ def weight_pack_scope(owner: torch.nn.Module):
     kinds = (prec, PACK_BF16_SPLIT) if prec == PREC_BF16 else (prec,)
     cache = {}
     for kind in kinds:
-        specs = [sp for key, sp in plan.items() if key[0] == kind and (grad or not sp.dgrad)]
+        specs = [sp for key, sp in plan.items()
+                 if key[0] == kind and (grad or not sp.dgrad) and _pack_kind(sp, prec) == kind]
         if specs:
             for sp, t in zip(specs, _run_pack(specs, kind)):
                 cache[(kind,) + sp.key] = t
@@ -822,10 +836,15 @@ class _ConvTransposeTM(torch.autograd.Function):
             _wgrad(xm, T, 1, 0, dy, T2, T, B, s, offs, Cout, Cin, dw,
                    (weight.stride(0), weight.stride(1), weight.stride(2)), prec=prec)
         if has_bias and ctx.needs_input_grad[2]:
-            # one column reduction (25.8 us at 32 x 600 x 256).  NOT dy.sum(1).sum(0): torch picks that
-            # reduction's vectorisation from the input's address, so its rounding changed between the
-            # data-parallel and the plain graph step (tests/test_dp_gpu.py equality failed)
-            db = dy.sum(dim=(0, 1))
+            # column sums of dy (rows may be strided: a slice of the concat gradient) in a fixed order:
+            # 128-row partials + a job in the step's batched gradient sums (torch's reduction: 26 us)
+            db = torch.empty(Cout, device=dy.device, dtype=torch.float32)
+            rows = B * T2
+            ws = torch.empty(int(N.lib().mtts_colsum_workspace_size(rows, Cout)) // 4, device=dy.device,
+                             dtype=torch.float32)
+            _keep_partials(ws, dy)
+            N.check(N.lib().mtts_colsum(dy.data_ptr(), rows, Cout, _ld(dy), db.data_ptr(), 0, ws.data_ptr(),
+                                        ws.numel() * 4, _stream(dy)), "mtts_colsum")
         return dx, dw, db, None
 
 
@@ -1647,8 +1666,9 @@ def loss_sum(dur, prior, diff):
 
 
 # ------------------------------------------------------------------------------------------ time MLP
-N.register("mtts_rows_linear_fwd", ctypes.c_int, [_P, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P])
-N.register("mtts_rows_linear_bwd", ctypes.c_int, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P])
+N.register("mtts_rows_linear_workspace_size", _SZ, [_I, _I, _I, _P])
+N.register("mtts_rows_linear_fwd", ctypes.c_int, [_P, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P, _SZ, _P])
+N.register("mtts_rows_linear_bwd", ctypes.c_int, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _SZ, _P])
 ROWS_ACT_NONE, ROWS_ACT_SILU, ROWS_ACT_MISH = 0, 1, 2  # include/mtts_decoder.h MTTS_ROWS_ACT_*
 
 
@@ -1656,18 +1676,40 @@ def _ptrs(ts):
     return (ctypes.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
 
 
+# per (device, B, K, N...) workspaces of the rows GEMMs: the counter region is zeroed once here and left
+# zeroed by the kernels, so a captured graph replays with the same buffers (never freed: a few hundred KB)
+_ROWS_WS: dict = {}
+
+
+def _rows_ws(dev, B, K, ns):
+    key = (dev, B, K, tuple(ns))
+    t = _ROWS_WS.get(key)
+    if t is None:
+        arr = (ctypes.c_int32 * len(ns))(*ns)
+        nb = int(N.lib().mtts_rows_linear_workspace_size(B, K, len(ns), arr))
+        t = torch.zeros(max(nb, 256) // 4 + 64, dtype=torch.float32, device=dev)
+        _ROWS_WS[key] = t
+    return t
+
+
 def _rows_fwd(x, ws, bs, outs, acts, act):
     B, K = x.shape
-    ns = (ctypes.c_int32 * len(ws))(*[w.shape[0] for w in ws])
+    nl = [w.shape[0] for w in ws]
+    wsb = _rows_ws(x.device, B, K, nl)
+    ns = (ctypes.c_int32 * len(ws))(*nl)
     N.check(N.lib().mtts_rows_linear_fwd(x.data_ptr(), B, K, len(ws), _ptrs(ws), _ptrs(bs), ns, _ptrs(outs),
-                                         None if acts is None else _ptrs(acts), act, _stream(x)), "mtts_rows_linear_fwd")
+                                         None if acts is None else _ptrs(acts), act, wsb.data_ptr(),
+                                         wsb.numel() * 4, _stream(x)), "mtts_rows_linear_fwd")
 
 
 def _rows_bwd(a, pre, act, ws, dys, dx, dws, dbs):
     B, K = a.shape
-    ns = (ctypes.c_int32 * len(ws))(*[w.shape[0] for w in ws])
+    nl = [w.shape[0] for w in ws]
+    wsb = _rows_ws(a.device, B, K, nl)
+    ns = (ctypes.c_int32 * len(ws))(*nl)
     N.check(N.lib().mtts_rows_linear_bwd(a.data_ptr(), N.ptr(pre), act, B, K, len(ws), _ptrs(ws), ns, _ptrs(dys),
-                                         N.ptr(dx), _ptrs(dws), _ptrs(dbs), _stream(a)), "mtts_rows_linear_bwd")
+                                         N.ptr(dx), _ptrs(dws), _ptrs(dbs), wsb.data_ptr(), wsb.numel() * 4,
+                                         _stream(a)), "mtts_rows_linear_bwd")
 
 
 class _TimeMLP(torch.autograd.Function):

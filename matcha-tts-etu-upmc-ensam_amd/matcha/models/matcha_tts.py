@@ -24,7 +24,17 @@ from matcha.models.components.text_encoder import TextEncoder
 from matcha.utils.model import denormalize, fix_len_compatibility, generate_path, sequence_mask
 
 
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
 class MatchaTTS(BaseLightningClass):
+    encoder_fp32 = False  # bf16-mixed: run the text encoder in exact fp32 (the parity policy, see forward)
+
     def __init__(self, n_vocab, n_feats=None, encoder=None, decoder=None, cfm=None, data_statistics=None,
                  out_size=None, optimizer=None, scheduler=None, prior_loss=True, use_precomputed_durations=False,
                  out_channels=None, hidden_channels=None):
@@ -95,8 +105,11 @@ class MatchaTTS(BaseLightningClass):
         """Returns (dur_loss, prior_loss, diff_loss, attn) -- matcha_tts.py:247-325.  ``t``/``z``
         (keyword-only) inject the CFM randomness for parity tests."""
         # the text encoder runs on the same HIP GEMM/attention kernels as the decoder and follows the
-        # caller's precision (bf16 MFMA operands inside a bf16 autocast region)
-        mu_x, logw, x_mask = self.encoder(x, x_lengths)
+        # caller's precision (bf16 MFMA operands inside a bf16 autocast region) unless encoder_fp32 is set:
+        # then it runs exact fp32 MFMA inside bf16-mixed (its activations' bf16 rounding is what is left of
+        # the bf16 prior-loss error once the weights enter as split planes -- tools/r3/precision_budget.py)
+        with torch.autocast(device_type=x.device.type, enabled=False) if self.encoder_fp32 else _nullctx():
+            mu_x, logw, x_mask = self.encoder(x, x_lengths)
         y_max_length = y.shape[-1]
         y_mask = O.sequence_mask_f32(y_lengths, y_max_length).unsqueeze(1)  # sequence_mask(...).to(x_mask), one launch
         runs = None

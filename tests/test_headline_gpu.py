@@ -7,11 +7,13 @@ precisions.
   itself pinned to the reference fixtures) on the same weights, tokens, mels, t and z.
 
 32-true: alignment bit-exact, each loss within 1e-4 relative (the north star's bar).
-bf16-mixed (what bench.py runs): MFMA operands in bf16, so the encoder's mu_x moves by ~3e-3
-relative and logw by ~1e-2.  The bounds below (BF16_LOSS_RTOL, per loss) come from the errors
-measured on the MI355X (profiles/r02/precision.md):
-  prior / diff loss: 2.2e-4 .. 4.2e-4 relative (B=4, B=32, 512x4096)  -> bound 1e-3;
-  duration loss: 3.1e-3 (B=32), 3.9e-3 (512x4096), 9.9e-2 (B=4)       -> bound 0.15.
+bf16-parity (bf16-mixed with split bf16 weight planes, MTTS_GEMM_F_W_SPLIT, and the text encoder in exact
+fp32, MatchaTTS.encoder_fp32): prior / diff loss within the same 1e-4 bar (BAR_RTOL) -- the error budget
+(tools/r3/precision_budget.py, profiles/r03/precision/) traced the bf16 loss error to the static rounding
+of the fp32 weights (split planes remove it) and, at 512 x 4096, the encoder's activation rounding.
+bf16-mixed one plane (bench.py's throughput line): measured 2.3e-4 .. 3.3e-4 (prior / diff at B=32,
+512x4096) -> bound 5e-4, documented as missing the bar.  Duration loss in every bf16 mode: MAS boundary
+flips -- 3e-3 (B=32), 9.9e-2 (B=4) with one plane -> bound 0.15.
 The duration loss is the sensitive one: it compares logw with log(durations of the MAS path), and
 the MAS is an argmax -- under the bf16 lattice perturbation near-tied DP decisions flip and move
 row boundaries by a frame (B=4: 28 of 437 rows changed duration, 0.5 % of the path cells), which
@@ -33,16 +35,34 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 GH = np.load(Path(__file__).parent / "golden" / "headline_golden.npz")
 FP32_LOSS_RTOL = 1e-4       # north star: mel / flow-matching loss within 1e-4 relative
-BF16_LOSS_RTOL = np.array([0.15, 1e-3, 1e-3])  # (dur, prior, diff), from the measurements above
+BAR_RTOL = np.array([0.15, 1e-4, 1e-4])        # bf16-parity: (dur, prior, diff) -- prior / diff at the bar
+BF16_LOSS_RTOL = np.array([0.15, 5e-4, 5e-4])  # bf16-mixed, one weight plane: measured, misses the bar
 BF16_ATTN_AGREE = 0.99      # fraction of [Tx, Ty] alignment cells equal to the fp32 reference path
 
 
+def run_precision(model, precision, fn):
+    """fn() under `precision`: 32-true, bf16-mixed (one weight plane) or bf16-parity (split weight planes +
+    the encoder in fp32)."""
+    from matcha.models.components import _ops as O
+
+    parity = precision == "bf16-parity"
+    old = O.set_weight_split(parity)
+    model.encoder_fp32 = parity
+    try:
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=precision != "32-true"):
+            return fn()
+    finally:
+        O.set_weight_split(old)
+        model.encoder_fp32 = False
+
+
 def _run(model, x, xl, y, yl, t, z, precision):
-    amp = torch.autocast("cuda", dtype=torch.bfloat16, enabled=precision == "bf16-mixed")
-    with amp:
+    def fn():
         dur, prior, diff, attn = model(x, xl, y, yl, t=t, z=z)
-        total = dur + prior + diff
-    total.backward()
+        (dur + prior + diff).backward()
+        return dur, prior, diff, attn
+
+    dur, prior, diff, attn = run_precision(model, precision, fn)
     torch.cuda.synchronize()
     return np.array([dur.item(), prior.item(), diff.item()]), attn.detach().cpu().numpy()
 
@@ -66,7 +86,7 @@ def _agree(attn, ref_attn, xl, yl):
     return same / total
 
 
-@pytest.mark.parametrize("precision", ["32-true", "bf16-mixed"])
+@pytest.mark.parametrize("precision", ["32-true", "bf16-mixed", "bf16-parity"])
 def test_headline_b4_vs_reference(precision):
     model = _product(41)
     g = lambda k: torch.from_numpy(GH[k]).to(DEV)  # noqa: E731
@@ -97,7 +117,7 @@ def test_headline_b4_vs_reference(precision):
         dur32 = ref_attn.astype(np.int64).sum(-1)
         print(f"bf16 alignment agreement {agree:.5f}; rows whose duration moved {(dur16 != dur32).sum()} of "
               f"{int(xl.sum())}; max |logw16 - logw32| {d_logw:.4f}; mu_x rel err {r_mu:.2e}")
-        assert (err <= BF16_LOSS_RTOL).all(), err
+        assert (err <= (BAR_RTOL if precision == "bf16-parity" else BF16_LOSS_RTOL)).all(), err
         assert agree >= BF16_ATTN_AGREE
 
 
@@ -128,7 +148,7 @@ def _oracle_b32():
     return _B32
 
 
-@pytest.mark.parametrize("precision", ["32-true", "bf16-mixed"])
+@pytest.mark.parametrize("precision", ["32-true", "bf16-mixed", "bf16-parity"])
 def test_bench_batch_b32_vs_oracle(precision):
     o = _oracle_b32()
     model = _product(43)
@@ -142,6 +162,6 @@ def test_bench_batch_b32_vs_oracle(precision):
         np.testing.assert_array_equal(attn.astype(np.int8), o["attn"])
         assert (err <= FP32_LOSS_RTOL).all(), err
     else:
-        assert (err <= BF16_LOSS_RTOL).all(), err
+        assert (err <= (BAR_RTOL if precision == "bf16-parity" else BF16_LOSS_RTOL)).all(), err
         assert agree >= BF16_ATTN_AGREE
     assert all(p.grad is None or torch.isfinite(p.grad).all() for p in model.parameters())

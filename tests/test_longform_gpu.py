@@ -99,7 +99,7 @@ def test_cfm_decoder_t4096_vs_oracle():
         assert abs(a - b) <= 2e-3 * abs(b) + 1e-6, (n, a, b)
 
 
-@pytest.mark.parametrize("precision", ["32-true", "bf16-mixed"])
+@pytest.mark.parametrize("precision", ["32-true", "bf16-mixed", "bf16-parity"])
 def test_train_forward_512x4096_bucketed(precision):
     """MatchaTTS.forward at T_text=512, T_mel=4096 with bucketed lengths (every utterance of the
     batch within a few percent of the bucket length, as LengthBucketBatchSampler yields): fp32 --
@@ -109,7 +109,7 @@ def test_train_forward_512x4096_bucketed(precision):
     from matcha.models.matcha_tts import MatchaTTS
     from oracle import matcha_oracle as MO
 
-    from test_headline_gpu import BF16_ATTN_AGREE, BF16_LOSS_RTOL, _agree
+    from test_headline_gpu import BAR_RTOL, BF16_ATTN_AGREE, BF16_LOSS_RTOL, _agree, run_precision
 
     B, Tx, Ty = 2, 512, 4096
     xl = torch.tensor([512, 497])
@@ -132,10 +132,13 @@ def test_train_forward_512x4096_bucketed(precision):
     apply_recipe(model, 62)
     model.eval()
     d = lambda v: v.to(DEV)  # noqa: E731
-    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=precision == "bf16-mixed"):
-        dur, prior, diff, attn = model(d(x), d(xl), d(y), d(yl), t=d(t), z=d(z))
-        total = dur + prior + diff
-    total.backward()
+
+    def fn():
+        out = model(d(x), d(xl), d(y), d(yl), t=d(t), z=d(z))
+        (out[0] + out[1] + out[2]).backward()
+        return out
+
+    dur, prior, diff, attn = run_precision(model, precision, fn)
     torch.cuda.synchronize()
     got = np.array([dur.item(), prior.item(), diff.item()])
     exp = np.array([float(v) for v in want[:3]])
@@ -146,6 +149,6 @@ def test_train_forward_512x4096_bucketed(precision):
         np.testing.assert_array_equal(attn.cpu().numpy(), want[3].numpy())
         assert (err <= 1e-4).all(), err
     else:
-        assert (err <= BF16_LOSS_RTOL).all(), err
+        assert (err <= (BAR_RTOL if precision == "bf16-parity" else BF16_LOSS_RTOL)).all(), err
         assert agree >= BF16_ATTN_AGREE
     assert all(p.grad is None or torch.isfinite(p.grad).all() for p in model.parameters())

@@ -97,3 +97,29 @@ def test_time_mlp_matches_torch(B):
     # deterministic: a second pass is bitwise identical
     temb2, tps2 = O.time_mlp(e, mlp.linear_1, mlp.linear_2, projs)
     assert torch.equal(temb, temb2) and all(torch.equal(a, b) for a, b in zip(tps, tps2))
+
+
+@pytest.mark.parametrize("rows,n,ld", [(19200, 256, 256), (9600, 256, 512), (77, 5, 8), (1, 256, 256)])
+def test_colsum_fixed_order(rows, n, ld):
+    """mtts_colsum (the transposed conv's bias gradient): column sums of a row-strided matrix, 128-row
+    partials + a fixed-order reduce: within fp32 rounding of the float64 sum, bitwise repeatable."""
+    import ctypes
+
+    from matcha import _native as N
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator().manual_seed(rows + n)
+    x = torch.randn(rows, ld, generator=g).to(DEV)
+    lib = N.lib()
+    outs = []
+    for _ in range(2):
+        ws = torch.empty(int(lib.mtts_colsum_workspace_size(rows, n)) // 4, device=DEV)
+        out = torch.full((n,), float("nan"), device=DEV)
+        N.check(lib.mtts_colsum(x.data_ptr(), rows, n, ld, out.data_ptr(), 0, ws.data_ptr(), ws.numel() * 4,
+                                O._stream(x)), "mtts_colsum")
+        outs.append(out)
+    torch.cuda.synchronize()
+    ref = x[:, :n].double().sum(0)
+    assert (outs[0].double() - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
+    assert torch.equal(outs[0], outs[1])
+    assert ctypes  # (ctypes-bound entry point)

@@ -16,6 +16,15 @@ DEV = torch.device("cuda:0")
 TOL = 3e-5
 
 
+@pytest.fixture(autouse=True)
+def _split_planes():
+    from matcha.models.components import _ops as O
+
+    old = O.set_weight_split(True)
+    yield
+    O.set_weight_split(old)
+
+
 def _bf16_exact(*shape, seed):
     g = torch.Generator().manual_seed(seed)
     return torch.randn(*shape, generator=g).bfloat16().float().to(DEV)

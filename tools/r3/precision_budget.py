@@ -24,6 +24,8 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[2]
 CONFIGS = {
     "default": {},
+    "split": {"MTTS_W_SPLIT": "1"},
+    "split_encfp32": {"MTTS_W_SPLIT": "1", "MTTS_BUDGET_ENC_FP32": "1"},
     "preln_fp32": {"MTTS_PRELN_N16": "0"},
     "attn_io_fp32": {"MTTS_ATTN_IO16": "0"},
     "ffn_fp32": {"MTTS_FF_FP32_HIDDEN": "1", "MTTS_FF_FP32_PRE": "1"},
@@ -45,6 +47,7 @@ def child(name: str) -> None:
 
     dev = torch.device("cuda:0")
     model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(dev)
+    model.encoder_fp32 = os.environ.get("MTTS_BUDGET_ENC_FP32") == "1"
     apply_recipe(model, 43)
     model.eval()
     real_pmp, real_enc = MA.prior_maximum_path, model.encoder.forward
