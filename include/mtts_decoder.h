@@ -376,7 +376,7 @@ int mtts_embedding_bwd(const int64_t *ids, const float *dout, int64_t rows, int3
 #define MTTS_ROWS_ACT_NONE 0
 #define MTTS_ROWS_ACT_SILU 1 /* x / (1 + exp(-x)) */
 #define MTTS_ROWS_ACT_MISH 2 /* x tanh(softplus(x)) */
-/* For each of nmat (<= 8) matrices W_i [N_i, K] (fp32, 16-byte aligned rows; stacked: N_i % 64 == 0)
+/* For each of nmat (<= 8) matrices W_i [N_i, K] (fp32, 16-byte aligned rows)
  * sharing the input x [B, K]:
  *   out_i[b, n] = sum_k x[b, k] W_i[n, k] + bias_i[n]   (bias table or its entries may be NULL)
  *   out_act_i = act(out_i)                              (out_act table or entries may be NULL)

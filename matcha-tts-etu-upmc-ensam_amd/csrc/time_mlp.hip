@@ -34,7 +34,9 @@ struct MatTable {
     float *out2[MTTS_ROWS_MAX_MATS];      // fwd: act(out_i) (optional); wgrad: db_i (optional)
     const float *dy[MTTS_ROWS_MAX_MATS];  // dgrad / wgrad: dy_i [B, N_i]
     int N[MTTS_ROWS_MAX_MATS];
-    int n_off[MTTS_ROWS_MAX_MATS + 1];    // prefix sums of N (dgrad: the stacked reduction index)
+    int n_off[MTTS_ROWS_MAX_MATS + 1];    // prefix sums of N_i rounded up to 32 (the stacked 32-wide tiles)
+    int r_off[MTTS_ROWS_MAX_MATS + 1];    // prefix sums of N_i rounded up to 64 (dgrad's reduction index:
+                                          // a wave's 64 indices never straddle two matrices)
     int nmat;
 };
 
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(64 * kWaves) void rows_gemm_kernel(MatTable T, cons
         c0 -= T.n_off[mat];
         R = K;
     } else if constexpr (MODE == kDgrad) {  // rows b, cols k, reduce over the stacked n
-        R = T.n_off[T.nmat];
+        R = T.r_off[T.nmat];
     } else {  // rows n of matrix mat (stacked row tiles), cols k, reduce over b
         while (mat + 1 < T.nmat && m0 >= T.n_off[mat + 1]) ++mat;
         m0 -= T.n_off[mat];
@@ -131,9 +133,9 @@ __global__ __launch_bounds__(64 * kWaves) void rows_gemm_kernel(MatTable T, cons
             b[j] = sB[lr * kLd + 32 * s + j];
         }
     } else if constexpr (MODE == kDgrad) {
-        int dm = 0;  // the wave's matrix (stacked N_i are multiples of 64: a wave never straddles two)
-        while (dm + 1 < T.nmat && r0 >= T.n_off[dm + 1]) ++dm;
-        const int base = T.n_off[dm], Nm = T.N[dm];
+        int dm = 0;  // the wave's matrix (r_off: a wave's 64 indices never straddle two)
+        while (dm + 1 < T.nmat && r0 >= T.r_off[dm + 1]) ++dm;
+        const int base = T.r_off[dm], Nm = T.N[dm];
         stage(T.dy[dm] + (size_t)m0 * Nm - base, Nm, min(32, B - m0), min(R, base + Nm), sA);
         __syncthreads();
         const int k = c0 + lr;
@@ -141,7 +143,7 @@ __global__ __launch_bounds__(64 * kWaves) void rows_gemm_kernel(MatTable T, cons
         for (int j = 0; j < 32; ++j) {
             const int r = r0 + 32 * s + j;
             a[j] = sA[lr * kLd + 32 * s + j];
-            b[j] = r < R && k < K ? T.W[dm][(size_t)(r - base) * K + k] : 0.f;
+            b[j] = r - base < Nm && k < K ? T.W[dm][(size_t)(r - base) * K + k] : 0.f;
         }
     } else {
         const int n = m0 + lr, k = c0 + lr, Nm = T.N[mat];
@@ -223,12 +225,12 @@ __global__ __launch_bounds__(64 * kWaves) void rows_gemm_kernel(MatTable T, cons
 int fill_table(MatTable &T, int nmat, const int32_t *N) {
     MTTS_CHECK_ARG(nmat >= 1 && nmat <= MTTS_ROWS_MAX_MATS && N, "rows_linear: 1..8 matrices");
     T.nmat = nmat;
-    T.n_off[0] = 0;
+    T.n_off[0] = T.r_off[0] = 0;
     for (int i = 0; i < nmat; ++i) {
-        MTTS_CHECK_ARG(N[i] >= 1 && (nmat == 1 || N[i] % kChunk == 0),
-                       "rows_linear: stacked matrices need N_i % 64 == 0");
+        MTTS_CHECK_ARG(N[i] >= 1, "rows_linear: N_i >= 1");
         T.N[i] = N[i];
-        T.n_off[i + 1] = T.n_off[i] + (nmat == 1 ? N[i] : N[i]);
+        T.n_off[i + 1] = T.n_off[i] + (N[i] + 31) / 32 * 32;
+        T.r_off[i + 1] = T.r_off[i] + (N[i] + kChunk - 1) / kChunk * kChunk;
     }
     return MTTS_OK;
 }
@@ -265,12 +267,15 @@ int check_ws(const Geo &g, int tiles, void *ws, size_t ws_bytes, Ws &w) {
 
 extern "C" size_t mtts_rows_linear_workspace_size(int32_t B, int32_t K, int32_t nmat, const int32_t *N) {
     if (B < 1 || K < 1 || nmat < 1 || nmat > MTTS_ROWS_MAX_MATS || !N) return 0;
-    size_t nt = 0;  // 32-column tiles of the stacked outputs
-    for (int i = 0; i < nmat; ++i) nt += (size_t)(N[i] + 31) / 32;
+    size_t nt = 0, nr = 0;  // 32-column tiles of the stacked outputs; dgrad's padded reduction length
+    for (int i = 0; i < nmat; ++i) {
+        nt += (size_t)(N[i] + 31) / 32;
+        nr += (size_t)(N[i] + kChunk - 1) / kChunk * kChunk;
+    }
     const size_t rt = (size_t)(B + 31) / 32, kt = (size_t)(K + 31) / 32;
     auto ks = [](size_t r) { return (r + kRange - 1) / kRange; };
     // (tiles, splits) of the forward, dgrad and wgrad launches
-    const size_t t[3] = {rt * nt, rt * kt, nt * kt}, k[3] = {ks(K), ks(nt * 32), ks(B)};
+    const size_t t[3] = {rt * nt, rt * kt, nt * kt}, k[3] = {ks(K), ks(nr), ks(B)};
     size_t tiles = 0, parts = 0;
     for (int m = 0; m < 3; ++m) {
         if (k[m] < 2) continue;
@@ -292,14 +297,12 @@ extern "C" int mtts_rows_linear_fwd(const float *x, int32_t B, int32_t K, int32_
     int col_tiles = 0;
     for (int i = 0; i < nmat; ++i) {
         MTTS_CHECK_ARG(W[i] && out[i] && (uintptr_t)W[i] % 16 == 0, "rows_linear_fwd: null / unaligned matrix");
-        MTTS_CHECK_ARG(nmat == 1 || N[i] % 32 == 0, "rows_linear_fwd: stacked matrices need N_i % 32 == 0");
         T.W[i] = W[i];
         T.bias[i] = bias ? bias[i] : nullptr;
         T.out[i] = out[i];
         T.out2[i] = out_act ? out_act[i] : nullptr;
         col_tiles += (N[i] + 31) / 32;
     }
-    if (nmat == 1) T.n_off[1] = col_tiles * 32;  // one matrix: every column tile is its own
     const int tiles = ((B + 31) / 32) * col_tiles;
     const Geo g = geometry(K, true);
     Ws w;
@@ -331,11 +334,10 @@ extern "C" int mtts_rows_linear_bwd(const float *a, const float *pre, int32_t ac
         MTTS_CHECK_ARG(!dW || dW[i], "rows_linear_bwd: null dW");
         row_tiles += (N[i] + 31) / 32;
     }
-    if (nmat == 1) T.n_off[1] = N[0];
     const int kt = (K + 31) / 32;
     if (dx) {
         const int tiles = ((B + 31) / 32) * kt;
-        const Geo g = geometry(T.n_off[nmat], true);
+        const Geo g = geometry(T.r_off[nmat], true);
         Ws w;
         if (int rc = check_ws(g, tiles, workspace, workspace_bytes, w)) return rc;
         hipLaunchKernelGGL(rows_gemm_kernel<kDgrad>, dim3(tiles * g.ks), dim3(64 * g.waves), g.lds, st, T, nullptr, B,
@@ -343,7 +345,6 @@ extern "C" int mtts_rows_linear_bwd(const float *a, const float *pre, int32_t ac
         if (int rc = mtts::check_launch("rows_gemm_kernel<dgrad>")) return rc;
     }
     if (dW) {
-        if (nmat == 1) T.n_off[1] = row_tiles * 32;
         const Geo g = geometry(B, false);
         Ws w;
         if (int rc = check_ws(g, row_tiles * kt, workspace, workspace_bytes, w)) return rc;

@@ -145,3 +145,44 @@ def test_synthesise_vs_reference(prefix, seed):
     for k in ("encoder_outputs", "decoder_outputs", "mel"):
         assert out[k].shape == GS[prefix + k].shape, k
         assert rel(out[k].cpu().numpy(), GS[prefix + k]) < 1e-4, k
+
+
+def test_matcha_gradients_elementwise_vs_oracle():
+    """Every parameter gradient of the full MatchaTTS train-step loss (dur + prior + diff, 32-true), element
+    by element, against the CPU oracle restatement on the same recipe weights, batch and CFM randomness
+    (the fixtures pin gradient norms; this pins the entries)."""
+    import oracle_bind as OB
+    from matcha.models.matcha_tts import MatchaTTS
+    from matcha.training import synthetic_batch
+    from oracle import matcha_oracle as MO
+
+    def mp(value, mask):
+        return torch.from_numpy(OB.maximum_path(value.detach().float().numpy(), mask.detach().float().numpy())[0])
+
+    B, Tx, Ty = 4, 24, 96
+    b = synthetic_batch(B, Tx, Ty, seed=91, device="cpu")
+    gen = torch.Generator().manual_seed(92)
+    t, z = torch.rand(B, 1, 1, generator=gen), torch.randn(B, 80, Ty, generator=gen)
+    ref = MO.MatchaTTSOracle(150, 80, 192, maximum_path=mp)
+    apply_recipe(ref, 93)
+    ref.eval()
+    out = ref(b["x"], b["x_lengths"], b["y"], b["y_lengths"], t=t, z=z)
+    (out[0] + out[1] + out[2]).backward()
+    want = {n: p.grad for n, p in ref.named_parameters() if p.grad is not None}
+
+    model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(DEV)
+    apply_recipe(model, 93)
+    model.eval()
+    d = lambda v: v.to(DEV)  # noqa: E731
+    got_out = model(d(b["x"]), d(b["x_lengths"]), d(b["y"]), d(b["y_lengths"]), t=d(t), z=d(z))
+    np.testing.assert_array_equal(got_out[3].cpu().numpy(), out[3].numpy())  # the same alignment
+    (got_out[0] + got_out[1] + got_out[2]).backward()
+    got = {n: p.grad.cpu() for n, p in model.named_parameters() if p.grad is not None}
+    assert set(got) == set(want)
+    worst = 0.0
+    for n, g in want.items():
+        scale = g.abs().max().item()
+        err = (got[n] - g).abs().max().item()
+        worst = max(worst, err / max(scale, 1e-30))
+        assert err <= 2e-4 * scale + 1e-8, (n, err, scale)
+    print(f"worst element-wise gradient error / tensor max: {worst:.2e} over {len(want)} tensors")

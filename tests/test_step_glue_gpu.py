@@ -64,8 +64,8 @@ def test_loss_sum_and_gradients():
     assert logged.tolist() == [1.0, 0.0, 2.0, 3.0] and float(d.grad) == float(f.grad) == 1.0
 
 
-@pytest.mark.parametrize("B", [1, 5, 32])
-def test_time_mlp_matches_torch(B):
+@pytest.mark.parametrize("B,width,dim", [(1, 256, 1024), (5, 256, 1024), (32, 256, 1024), (3, 32, 128), (7, 96, 200)])
+def test_time_mlp_matches_torch(B, width, dim):
     """decoder.py:33-49 (Linear -> SiLU -> Linear) + each Resnet1D.mlp (Mish -> Linear) on the shared temb:
     the fused HIP path (csrc/time_mlp.hip) against the torch modules, forward and every weight / bias
     gradient, fp32."""
@@ -75,11 +75,11 @@ def test_time_mlp_matches_torch(B):
     from matcha.models.components.decoder import TimeStepEmbeddingNet
 
     torch.manual_seed(B)
-    mlp = TimeStepEmbeddingNet(160, 1024).to(DEV)
-    projs = [torch.nn.Linear(1024, 256).to(DEV) for _ in range(6)]
+    mlp = TimeStepEmbeddingNet(160, dim).to(DEV)
+    projs = [torch.nn.Linear(dim, width).to(DEV) for _ in range(6)]
     e = torch.randn(B, 160, device=DEV) * 3
     temb, tps = O.time_mlp(e, mlp.linear_1, mlp.linear_2, projs)
-    w = [torch.randn(B, 256, device=DEV) for _ in projs]
+    w = [torch.randn(B, width, device=DEV) for _ in projs]
     sum((tp * wi).sum() for tp, wi in zip(tps, w)).backward()
     got = [p.grad.clone() for p in list(mlp.parameters()) + [q for lin in projs for q in lin.parameters()]]
     for p in list(mlp.parameters()) + [q for lin in projs for q in lin.parameters()]:

@@ -227,7 +227,10 @@ def test_accumulate_grad_batches_2_vs_torch(graph):
         opt.step()
         opt.zero_grad(set_to_none=True)
         torch.cuda.synchronize()
-        torch.testing.assert_close(logged[3], (tot[0] + tot[1]) / 2, rtol=1e-6 if step else 0.0, atol=0.0)
+        # after the first step graph mode's parameters are ulps apart (HIP clip + AdamW), which moves the
+        # losses by a few ulp of their own; eager mode stays bitwise
+        rtol = 0.0 if step == 0 else (5e-6 if graph else 1e-6)
+        torch.testing.assert_close(logged[3], (tot[0] + tot[1]) / 2, rtol=rtol, atol=0.0)
         if step not in (0, 2):
             continue
         worst = []
