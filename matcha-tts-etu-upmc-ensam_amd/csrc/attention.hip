@@ -748,6 +748,419 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Short sequences (T <= 128: the text encoder, T ~ 120 x 2 heads of 96).  The kernels above give a
+// (b, h) pair one block of 128 rows, so the encoder's 64 pairs fill a quarter of the chip and each block
+// walks its two 64-row tiles in series.  Here a block owns 32 rows and its four waves split the OTHER
+// axis -- wave w takes the 32 keys (fwd, dQ) or queries (dKV) of sub-tile w -- with both tiles staged
+// at once; the waves' partial results are merged through LDS in wave order (deterministic).  4x the
+// blocks, a quarter of the serial chain per block.  fp32 reads its transposed operands from the row
+// tiles (no transposed copies), which keeps two tiles of two operands inside the LDS.
+constexpr int kShortT = 2 * kTile;
+constexpr int kShortRows = 32;
+constexpr int kWaves = kThreads / 64;
+
+template <bool BF16, int D>
+struct Short {
+    using Gm = G<BF16, D>;
+    static constexpr size_t tile = ((size_t)Gm::RE * sizeof(typename Gm::T) + 15) / 16 * 16;
+    static constexpr size_t stage = 4 * tile + 2 * (2 * kTile * sizeof(float)) + 16;  // 2 tiles x 2 operands + 2 row arrays
+    static constexpr size_t acc_set = (size_t)kWaves * Gm::NT * 16 * 64 * sizeof(float);  // one wave-partial accumulator set
+    static constexpr size_t xoff(int nacc) { return stage > nacc * acc_set ? stage : nacc * acc_set; }
+    static constexpr size_t lds(int nacc) { return xoff(nacc) + 2 * kWaves * 32 * sizeof(float) + 64; }
+};
+
+// mma_perm on a ROW tile: bf16 images are read transposed by the same call; fp32 indexes the row tile
+// by (key, d) instead of a transposed copy's (d, key)
+template <bool BF16, int D>
+__device__ __forceinline__ void mma_perm_r(f32x16 &acc, const typename G<BF16, D>::T *tile, int d, int sub, int lh,
+                                           const float (&s)[16]) {
+    if constexpr (BF16) {
+        mma_perm<BF16, D>(acc, tile, d, sub, lh, s);
+    } else {
+        constexpr int LD = G<BF16, D>::LDR;
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(tile[(sub * 32 + crow(v, lh)) * LD + d], s[v], acc, 0, 0, 0);
+    }
+}
+
+// both 64-row tiles of two operands (rows 0..127 of one head) into LDS; rows past T hold finite data
+// that every kernel weights by zero (as TileLoader)
+template <bool BF16, int D, typename TI>
+__device__ __forceinline__ void stage_pair(const TI *A, const TI *Bm, int lda, int ldb, int b, int T, int tid, int dh,
+                                           typename G<BF16, D>::T *As, typename G<BF16, D>::T *Bs) {
+    using Gm = G<BF16, D>;
+    TileLoader<BF16, D> la0, lb0, la1, lb1;
+    la0.load(A, lda, b, T, 0, tid, dh);
+    lb0.load(Bm, ldb, b, T, 0, tid, dh);
+    const bool two = T > kTile;
+    if (two) {
+        la1.load(A, lda, b, T, kTile, tid, dh);
+        lb1.load(Bm, ldb, b, T, kTile, tid, dh);
+    }
+    la0.store(As, nullptr, tid, dh);
+    lb0.store(Bs, nullptr, tid, dh);
+    if (two) {
+        la1.store(As + Gm::RE, nullptr, tid, dh);
+        lb1.store(Bs + Gm::RE, nullptr, tid, dh);
+    }
+}
+
+// The wave-partial accumulators of this wave into the merge area: [wave][t][v][lane] (lane-contiguous)
+template <int NT>
+__device__ __forceinline__ void put_partial(float *area, const f32x16 (&acc)[NT], int wave, int lane) {
+    float *mine = area + (size_t)wave * NT * 16 * 64;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) mine[(t * 16 + v) * 64 + lane] = acc[t][v];
+}
+// sum over waves (fixed order, weights wgt[w]) of the C-layout values 4g..4g+3 of tile t
+template <int NT>
+__device__ __forceinline__ float4 sum_partials(const float *area, int t, int g, int lane, const float (&wgt)[kWaves]) {
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        const float *pw = area + (size_t)w * NT * 16 * 64 + (t * 16 + 4 * g) * 64 + lane;
+        o.x += wgt[w] * pw[0];
+        o.y += wgt[w] * pw[64];
+        o.z += wgt[w] * pw[128];
+        o.w += wgt[w] * pw[192];
+    }
+    return o;
+}
+
+// forward: grid (ceil(T/32), H, B); lane = query, wave = key sub-tile
+template <bool BF16, int D, typename TI = float>
+__global__ __launch_bounds__(kThreads) void attn_fwd_short_kernel(mtts_attn_args p) {
+    const TI *Qp = reinterpret_cast<const TI *>(p.q), *Kp = reinterpret_cast<const TI *>(p.k),
+             *Vp = reinterpret_cast<const TI *>(p.v);
+    TI *Op = reinterpret_cast<TI *>(p.o);
+    using Gm = G<BF16, D>;
+    using ST = typename Gm::T;
+    using S = Short<BF16, D>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char *sp = smem;
+    ST *Ks = carve<ST>(sp, 2 * Gm::RE);
+    ST *Vs = carve<ST>(sp, 2 * Gm::RE);
+    float *bias_s = carve<float>(sp, 2 * kTile);
+    int *flag_s = carve<int>(sp, 2);
+    float *area = reinterpret_cast<float *>(smem);  // merge area: aliases the stage after the compute
+    float *ms = reinterpret_cast<float *>(smem + S::xoff(1)), *ls = ms + kWaves * 32;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;
+    const int q = blockIdx.x * kShortRows + lr;
+    const bool q_ok = q < T;
+    const int buf = wave >> 1, sub = wave & 1;
+    const float c0 = key_bias_c0(p, b), sl2 = p.scale * kLog2e;
+
+    RowFrag<BF16, D> qf;
+    qf.load(Qp + h * dh + ((size_t)b * T + (q_ok ? q : 0)) * p.ldq, q_ok, lh, dh, BF16 ? sl2 : 1.f);
+    const float br0 = stage_bias(p, b, tid & (kTile - 1), c0), br1 = stage_bias(p, b, kTile + (tid & (kTile - 1)), c0);
+    stage_pair<BF16, D>(Kp + h * dh, Vp + h * dh, p.ldq, p.ldq, b, T, tid, dh, Ks, Vs);
+    store_bias(bias_s, flag_s, 0, br0, tid);
+    store_bias(bias_s, flag_s, 1, br1, tid);
+    mtts::lds_barrier();
+
+    f32x16 acc[Gm::NT];
+#pragma unroll
+    for (int t = 0; t < Gm::NT; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    if (wave * 32 < T) {  // wave-uniform: the sub-tile holds at least one key (so m is finite)
+        const ST *K_ = Ks + buf * Gm::RE, *V_ = Vs + buf * Gm::RE;
+        f32x16 sacc;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) sacc[v] = 0.f;
+        mma_rows<BF16, D>(sacc, K_, sub * 32 + lr, lh, qf);
+        float s[16], bv[16], mx = -INFINITY;
+        const bool tb = flag_s[buf];
+        if (tb) crow_load16(bias_s + buf * kTile + sub * 32, lh, bv);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            s[v] = BF16 ? sacc[v] : sacc[v] * sl2;
+            if (tb) s[v] += bv[v];
+            mx = fmaxf(mx, s[v]);
+        }
+        m = half_max(mx);
+        float rs = 0.f;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            s[v] = fast_exp2(s[v] - m);
+            rs += s[v];
+        }
+        l = half_sum(rs);
+        if (p.dropout_p > 0.f) {
+            const uint32_t s0 = p.seed[0], s1 = p.seed[1];
+            const uint32_t prow = (uint32_t)(((size_t)b * p.H + h) * T + q);
+            const float inv_keep = 1.f / (1.f - p.dropout_p);
+#pragma unroll
+            for (int v = 0; v < 16; ++v)
+                s[v] = mtts::dropout_keep(s0, s1, prow, (uint32_t)(wave * 32 + crow(v, lh)), p.dropout_p)
+                           ? s[v] * inv_keep
+                           : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < Gm::NT; ++t) mma_perm_r<BF16, D>(acc[t], V_, t * 32 + lr, sub, lh, s);
+    }
+    mtts::lds_barrier();  // the staged tiles are dead: the merge area may overwrite them
+    if (lh == 0) {
+        ms[wave * 32 + lr] = m;
+        ls[wave * 32 + lr] = l;
+    }
+    put_partial<Gm::NT>(area, acc, wave, lane);
+    mtts::lds_barrier();
+    float M = -INFINITY, L = 0.f, wgt[kWaves];
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) M = fmaxf(M, ms[w * 32 + lr]);
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        const float mw = ms[w * 32 + lr];
+        wgt[w] = mw == -INFINITY ? 0.f : fast_exp2(mw - M);
+        L += wgt[w] * ls[w * 32 + lr];
+    }
+    if (q_ok) {
+        const float inv = 1.f / L;
+        TI *orow = Op + ((size_t)b * T + q) * p.ldo + h * dh;
+#pragma unroll
+        for (int t = 0; t < Gm::NT; ++t) {
+            const int c = t * 32 + 8 * wave + 4 * lh;  // wave w writes the C-layout group g = w
+            if (c >= dh) continue;
+            const float4 o = sum_partials<Gm::NT>(area, t, wave, lane, wgt);
+            st4f(orow + c, make_float4(o.x * inv, o.y * inv, o.z * inv, o.w * inv));
+        }
+        if (wave == 0 && lh == 0) p.lse[((size_t)b * p.H + h) * T + q] = M + log2f(L);
+    }
+}
+
+// backward dQ: grid (ceil(T/32), H, B); lane = query, wave = key sub-tile.  Writes Drow as well.
+template <bool BF16, int D, typename TI = float>
+__global__ __launch_bounds__(kThreads) void attn_bwd_dq_short_kernel(mtts_attn_args p, mtts_attn_grads g, float *Drow) {
+    const TI *Qp = reinterpret_cast<const TI *>(p.q), *Kp = reinterpret_cast<const TI *>(p.k),
+             *Vp = reinterpret_cast<const TI *>(p.v), *Op = reinterpret_cast<const TI *>(p.o),
+             *Gp = reinterpret_cast<const TI *>(g.dout);
+    TI *DQp = reinterpret_cast<TI *>(g.dq);
+    using Gm = G<BF16, D>;
+    using ST = typename Gm::T;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char *sp = smem;
+    ST *Ks = carve<ST>(sp, 2 * Gm::RE);
+    ST *Vs = carve<ST>(sp, 2 * Gm::RE);
+    float *bias_s = carve<float>(sp, 2 * kTile);
+    int *flag_s = carve<int>(sp, 2);
+    float *area = reinterpret_cast<float *>(smem);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;
+    const int q = blockIdx.x * kShortRows + lr;
+    const bool q_ok = q < T;
+    const size_t qrow = (size_t)b * T + (q_ok ? q : 0);
+    const int buf = wave >> 1, sub = wave & 1;
+    const float sl2 = p.scale * kLog2e, c0 = key_bias_c0(p, b);
+
+    RowFrag<BF16, D> qf, gf;
+    qf.load(Qp + h * dh + qrow * p.ldq, q_ok, lh, dh, BF16 ? sl2 : 1.f);
+    gf.load(Gp + h * dh + qrow * g.lddo, q_ok, lh, dh);
+    float dsum = 0.f;  // rowsum(dO * O), as the long dQ kernel (every wave: the same query per lane)
+    if (q_ok) {
+        const TI *orow = Op + qrow * p.ldo + h * dh + (D / 2) * lh;
+        const TI *grow = Gp + qrow * g.lddo + h * dh + (D / 2) * lh;
+#pragma unroll
+        for (int i = 0; i < D / 2; i += 4) {
+            if ((D / 2) * lh + i >= dh) break;
+            const float4 a = ld4f(orow + i);
+            const float4 c = ld4f(grow + i);
+            dsum += a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
+        }
+    }
+    dsum = half_sum(dsum);
+    const size_t srow = ((size_t)b * p.H + h) * T + (q_ok ? q : 0);
+    const float lse2 = q_ok ? p.lse[srow] : 0.f;
+    if (q_ok && wave == 0 && lh == 0) Drow[srow] = dsum;
+
+    const float br0 = stage_bias(p, b, tid & (kTile - 1), c0), br1 = stage_bias(p, b, kTile + (tid & (kTile - 1)), c0);
+    stage_pair<BF16, D>(Kp + h * dh, Vp + h * dh, p.ldq, p.ldq, b, T, tid, dh, Ks, Vs);
+    store_bias(bias_s, flag_s, 0, br0, tid);
+    store_bias(bias_s, flag_s, 1, br1, tid);
+    mtts::lds_barrier();
+
+    f32x16 acc[Gm::NT];
+#pragma unroll
+    for (int t = 0; t < Gm::NT; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
+    if (wave * 32 < T) {
+        const bool drop = p.dropout_p > 0.f, fold = BF16 && !drop;
+        const ST *K_ = Ks + buf * Gm::RE, *V_ = Vs + buf * Gm::RE;
+        f32x16 sacc, pacc;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            sacc[v] = BF16 ? -lse2 : 0.f;
+            pacc[v] = fold ? -dsum : 0.f;
+        }
+        mma_rows<BF16, D>(sacc, K_, sub * 32 + lr, lh, qf);  // S^T
+        mma_rows<BF16, D>(pacc, V_, sub * 32 + lr, lh, gf);  // dP^T
+        float ds[16], bv[16];
+        const bool tb = flag_s[buf];
+        if (tb) crow_load16(bias_s + buf * kTile + sub * 32, lh, bv);
+        const uint32_t s0 = drop ? p.seed[0] : 0u, s1 = drop ? p.seed[1] : 0u;
+        const float inv_keep = 1.f / (1.f - p.dropout_p);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            float x = BF16 ? sacc[v] : sacc[v] * sl2 - lse2;
+            if (tb) x += bv[v];
+            const float pr = fast_exp2(x);
+            if (fold) {
+                ds[v] = pr * pacc[v];
+            } else {
+                float dp = pacc[v];
+                if (drop)
+                    dp = mtts::dropout_keep(s0, s1, (uint32_t)srow, (uint32_t)(wave * 32 + crow(v, lh)), p.dropout_p)
+                             ? dp * inv_keep
+                             : 0.f;
+                ds[v] = pr * (dp - dsum);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < Gm::NT; ++t) mma_perm_r<BF16, D>(acc[t], K_, t * 32 + lr, sub, lh, ds);  // dQ^T += K^T dS^T
+    }
+    mtts::lds_barrier();
+    put_partial<Gm::NT>(area, acc, wave, lane);
+    mtts::lds_barrier();
+    if (q_ok) {
+        const float one[kWaves] = {1.f, 1.f, 1.f, 1.f};
+        TI *drow = DQp + ((size_t)b * T + q) * g.ldd + h * dh;
+        const float sc = p.scale;
+#pragma unroll
+        for (int t = 0; t < Gm::NT; ++t) {
+            const int c = t * 32 + 8 * wave + 4 * lh;
+            if (c >= dh) continue;
+            const float4 o = sum_partials<Gm::NT>(area, t, wave, lane, one);
+            st4f(drow + c, make_float4(o.x * sc, o.y * sc, o.z * sc, o.w * sc));
+        }
+    }
+}
+
+// backward dK/dV: grid (ceil(T/32), H, B); lane = key, wave = query sub-tile
+template <bool BF16, int D, typename TI = float>
+__global__ __launch_bounds__(kThreads) void attn_bwd_dkv_short_kernel(mtts_attn_args p, mtts_attn_grads g,
+                                                                      const float *Drow) {
+    const TI *Qp = reinterpret_cast<const TI *>(p.q), *Kp = reinterpret_cast<const TI *>(p.k),
+             *Vp = reinterpret_cast<const TI *>(p.v), *Gp = reinterpret_cast<const TI *>(g.dout);
+    TI *DKp = reinterpret_cast<TI *>(g.dk), *DVp = reinterpret_cast<TI *>(g.dv);
+    using Gm = G<BF16, D>;
+    using ST = typename Gm::T;
+    using S = Short<BF16, D>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char *sp = smem;
+    ST *Qs = carve<ST>(sp, 2 * Gm::RE);
+    ST *Gs = carve<ST>(sp, 2 * Gm::RE);
+    float *lse_s = carve<float>(sp, 2 * kTile);  // +inf past T
+    float *d_s = carve<float>(sp, 2 * kTile);
+    float *area_k = reinterpret_cast<float *>(smem), *area_v = reinterpret_cast<float *>(smem + S::acc_set);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;
+    const int key = blockIdx.x * kShortRows + lr;
+    const bool k_ok = key < T;
+    const size_t krow = (size_t)b * T + (k_ok ? key : 0);
+    const int buf = wave >> 1, sub = wave & 1;
+    const float sl2 = p.scale * kLog2e, c0 = key_bias_c0(p, b);
+
+    RowFrag<BF16, D> kf, vf;
+    kf.load(Kp + h * dh + krow * p.ldq, k_ok, lh, dh, BF16 ? sl2 : 1.f);
+    vf.load(Vp + h * dh + krow * p.ldq, k_ok, lh, dh);
+    const float bias2 = (k_ok && p.key_bias) ? (p.key_bias[krow] - c0) * kLog2e : 0.f;
+    const size_t sbase = ((size_t)b * p.H + h) * T;
+    float lse_r = 0.f, d_r = 0.f;
+    if (tid < kShortT) {
+        const float l_raw = p.lse[sbase + min(tid, T - 1)], d_raw = Drow[sbase + min(tid, T - 1)];
+        lse_r = tid < T ? l_raw : INFINITY;
+        d_r = tid < T ? d_raw : 0.f;
+    }
+    stage_pair<BF16, D>(Qp + h * dh, Gp + h * dh, p.ldq, g.lddo, b, T, tid, dh, Qs, Gs);
+    if (tid < kShortT) {
+        lse_s[tid] = lse_r;
+        d_s[tid] = d_r;
+    }
+    mtts::lds_barrier();
+
+    f32x16 dk[Gm::NT], dv[Gm::NT];
+#pragma unroll
+    for (int t = 0; t < Gm::NT; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) dk[t][v] = dv[t][v] = 0.f;
+    if (wave * 32 < T) {
+        const bool drop = p.dropout_p > 0.f, fold = BF16 && !drop;
+        const ST *Q_ = Qs + buf * Gm::RE, *G_ = Gs + buf * Gm::RE;
+        float lv[16], dv16[16];
+        crow_load16(lse_s + wave * 32, lh, lv);
+        crow_load16(d_s + wave * 32, lh, dv16);
+        f32x16 sacc, pacc;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            sacc[v] = BF16 ? bias2 - lv[v] : 0.f;
+            pacc[v] = fold ? -dv16[v] : 0.f;
+        }
+        mma_rows<BF16, D>(sacc, Q_, sub * 32 + lr, lh, kf);  // S (rows q, col = this key)
+        mma_rows<BF16, D>(pacc, G_, sub * 32 + lr, lh, vf);  // dP
+        const uint32_t s0 = drop ? p.seed[0] : 0u, s1 = drop ? p.seed[1] : 0u;
+        const float inv_keep = 1.f / (1.f - p.dropout_p);
+        float pr[16], ds[16];
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const float pv = fast_exp2(BF16 ? sacc[v] : sacc[v] * sl2 + bias2 - lv[v]);
+            pr[v] = pv;
+            if (fold) {
+                ds[v] = pv * pacc[v];
+            } else {
+                float dp = pacc[v];
+                if (drop) {
+                    const bool keep = mtts::dropout_keep(s0, s1, (uint32_t)(sbase + wave * 32 + crow(v, lh)),
+                                                         (uint32_t)key, p.dropout_p);
+                    pr[v] = keep ? pv * inv_keep : 0.f;
+                    dp = keep ? dp * inv_keep : 0.f;
+                }
+                ds[v] = pv * (dp - dv16[v]);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < Gm::NT; ++t) {
+            mma_perm_r<BF16, D>(dv[t], G_, t * 32 + lr, sub, lh, pr);  // dV^T += dO^T P
+            mma_perm_r<BF16, D>(dk[t], Q_, t * 32 + lr, sub, lh, ds);  // dK^T += Q^T dS
+        }
+    }
+    mtts::lds_barrier();
+    put_partial<Gm::NT>(area_k, dk, wave, lane);
+    put_partial<Gm::NT>(area_v, dv, wave, lane);
+    mtts::lds_barrier();
+    if (k_ok) {
+        const float one[kWaves] = {1.f, 1.f, 1.f, 1.f};
+        TI *dkr = DKp + krow * g.ldd + h * dh;
+        TI *dvr = DVp + krow * g.ldd + h * dh;
+        const float sc = p.scale;
+#pragma unroll
+        for (int t = 0; t < Gm::NT; ++t) {
+            const int c = t * 32 + 8 * wave + 4 * lh;
+            if (c >= dh) continue;
+            const float4 a = sum_partials<Gm::NT>(area_k, t, wave, lane, one);
+            const float4 e = sum_partials<Gm::NT>(area_v, t, wave, lane, one);
+            st4f(dkr + c, make_float4(a.x * sc, a.y * sc, a.z * sc, a.w * sc));
+            st4f(dvr + c, e);
+        }
+    }
+}
+
+// the short path is the default for T <= 128; MTTS_ATTN_SHORT=0 sends every shape down the long one
+bool use_short(int T) {
+    if (T > kShortT) return false;
+    const char *e = getenv("MTTS_ATTN_SHORT");
+    return !(e && e[0] == '0');
+}
+
 constexpr size_t lds_bytes(size_t stage) { return nbuf(stage) * (stage + 64); }  // + carve alignment slack
 
 template <typename K>
@@ -783,6 +1196,14 @@ int fwd_launch(const mtts_attn_args &p, hipStream_t st) {
     if constexpr (BF16 && sizeof(TI) == 4) {
         if (p.flags & MTTS_ATTN_F_IO_BF16) return fwd_launch<true, D, uint16_t>(p, st);
     }
+    if (use_short(p.T)) {
+        constexpr size_t ls = Short<BF16, D>::lds(1);
+        static_assert(ls <= kLdsMax, "attention short fwd LDS");
+        if (!set_lds(attn_fwd_short_kernel<BF16, D, TI>, ls)) return mtts::fail(MTTS_ERR_HIP, "attention: LDS attribute");
+        dim3 grid((p.T + kShortRows - 1) / kShortRows, p.H, p.B);
+        hipLaunchKernelGGL((attn_fwd_short_kernel<BF16, D, TI>), grid, dim3(kThreads), ls, st, p);
+        return mtts::check_launch("attn_fwd_short_kernel");
+    }
     constexpr size_t lds = lds_bytes(fwd_stage<BF16, D>());
     static_assert(lds <= kLdsMax, "attention fwd LDS");
     if (!set_lds(attn_fwd_kernel<BF16, D, TI>, lds)) return mtts::fail(MTTS_ERR_HIP, "attention: LDS attribute");
@@ -795,6 +1216,18 @@ template <bool BF16, int D, typename TI = float>
 int bwd_launch(const mtts_attn_args &p, const mtts_attn_grads &g, float *Drow, hipStream_t st) {
     if constexpr (BF16 && sizeof(TI) == 4) {
         if (p.flags & MTTS_ATTN_F_IO_BF16) return bwd_launch<true, D, uint16_t>(p, g, Drow, st);
+    }
+    if (use_short(p.T)) {
+        constexpr size_t sq = Short<BF16, D>::lds(1), skv = Short<BF16, D>::lds(2);
+        static_assert(sq <= kLdsMax && skv <= kLdsMax, "attention short bwd LDS");
+        if (!set_lds(attn_bwd_dq_short_kernel<BF16, D, TI>, sq) || !set_lds(attn_bwd_dkv_short_kernel<BF16, D, TI>, skv))
+            return mtts::fail(MTTS_ERR_HIP, "attention_bwd: LDS attribute");
+        dim3 grid((p.T + kShortRows - 1) / kShortRows, p.H, p.B);
+        hipLaunchKernelGGL((attn_bwd_dq_short_kernel<BF16, D, TI>), grid, dim3(kThreads), sq, st, p, g, Drow);
+        if (int rc = mtts::check_launch("attn_bwd_dq_short_kernel")) return rc;
+        hipLaunchKernelGGL((attn_bwd_dkv_short_kernel<BF16, D, TI>), grid, dim3(kThreads), skv, st, p, g,
+                           (const float *)Drow);
+        return mtts::check_launch("attn_bwd_dkv_short_kernel");
     }
     constexpr size_t lq = lds_bytes(dq_stage<BF16, D>()), lkv = lds_bytes(dkv_stage<BF16, D>());
     static_assert(lq <= kLdsMax && lkv <= kLdsMax, "attention bwd LDS");

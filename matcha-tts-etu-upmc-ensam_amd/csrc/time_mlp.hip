@@ -16,6 +16,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "mtts_common.h"
 #include "mtts_decoder.h"
@@ -84,6 +85,7 @@ struct Ws {
     float *part;        // [tiles][KS][32 * 32]
     unsigned *counter;  // [tiles], zero between launches
     int ks;
+    int passes;         // kRange-wide passes per workgroup (the waves accumulate across them)
 };
 
 template <int MODE>
@@ -107,10 +109,9 @@ __global__ __launch_bounds__(64 * kWaves) void rows_gemm_kernel(MatTable T, cons
         m0 -= T.n_off[mat];
         R = B;
     }
-    const int r0 = ksi * kRange + wave * kChunk;  // this wave's 64 indices
     float *sA = lds + wave * 2 * 32 * kLd, *sB = sA + 32 * kLd;
     // stage a 32 x 64 block (rows row0.., indices r0..r0+63) of a row-major matrix, zero outside
-    auto stage = [&](const float *base, int ld, int nrows, int r_end, float *dst) {
+    auto stage = [&](const float *base, int ld, int nrows, int r0, int r_end, float *dst) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const int e = q * 64 + lane, row = e >> 4, c4 = (e & 15) * 4;
@@ -122,43 +123,47 @@ __global__ __launch_bounds__(64 * kWaves) void rows_gemm_kernel(MatTable T, cons
             dst[row * kLd + c4 + 3] = v.w;
         }
     };
-    float a[32], b[32];
-    if constexpr (MODE == kFwd) {
-        stage(x + (size_t)m0 * K, K, min(32, B - m0), R, sA);
-        stage(T.W[mat] + (size_t)c0 * K, K, min(32, T.N[mat] - c0), R, sB);
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            a[j] = sA[lr * kLd + 32 * s + j];
-            b[j] = sB[lr * kLd + 32 * s + j];
-        }
-    } else if constexpr (MODE == kDgrad) {
-        int dm = 0;  // the wave's matrix (r_off: a wave's 64 indices never straddle two)
-        while (dm + 1 < T.nmat && r0 >= T.r_off[dm + 1]) ++dm;
-        const int base = T.r_off[dm], Nm = T.N[dm];
-        stage(T.dy[dm] + (size_t)m0 * Nm - base, Nm, min(32, B - m0), min(R, base + Nm), sA);
-        __syncthreads();
-        const int k = c0 + lr;
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            const int r = r0 + 32 * s + j;
-            a[j] = sA[lr * kLd + 32 * s + j];
-            b[j] = r - base < Nm && k < K ? T.W[dm][(size_t)(r - base) * K + k] : 0.f;
-        }
-    } else {
-        const int n = m0 + lr, k = c0 + lr, Nm = T.N[mat];
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            const int r = r0 + 32 * s + j;
-            a[j] = r < R && n < Nm ? T.dy[mat][(size_t)r * Nm + n] : 0.f;
-            b[j] = r < R && k < K ? x[(size_t)r * K + k] : 0.f;
-        }
-    }
     f32x16 acc;
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+    for (int pass = 0; pass < ws.passes; ++pass) {
+        const int r0 = (ksi * ws.passes + pass) * kRange + wave * kChunk;  // this wave's 64 indices
+        if (pass > 0) __syncthreads();  // every wave has read the previous pass's staged blocks
+        float a[32], b[32];
+        if constexpr (MODE == kFwd) {
+            stage(x + (size_t)m0 * K, K, min(32, B - m0), r0, R, sA);
+            stage(T.W[mat] + (size_t)c0 * K, K, min(32, T.N[mat] - c0), r0, R, sB);
+            __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 32; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
+            for (int j = 0; j < 32; ++j) {
+                a[j] = sA[lr * kLd + 32 * s + j];
+                b[j] = sB[lr * kLd + 32 * s + j];
+            }
+        } else if constexpr (MODE == kDgrad) {
+            int dm = 0;  // the wave's matrix (r_off: a wave's 64 indices never straddle two)
+            while (dm + 1 < T.nmat && r0 >= T.r_off[dm + 1]) ++dm;
+            const int base = T.r_off[dm], Nm = T.N[dm];
+            stage(T.dy[dm] + (size_t)m0 * Nm - base, Nm, min(32, B - m0), r0, min(R, base + Nm), sA);
+            __syncthreads();
+            const int k = c0 + lr;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                const int r = r0 + 32 * s + j;
+                a[j] = sA[lr * kLd + 32 * s + j];
+                b[j] = r - base < Nm && k < K ? T.W[dm][(size_t)(r - base) * K + k] : 0.f;
+            }
+        } else {
+            const int n = m0 + lr, k = c0 + lr, Nm = T.N[mat];
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                const int r = r0 + 32 * s + j;
+                a[j] = r < R && n < Nm ? T.dy[mat][(size_t)r * Nm + n] : 0.f;
+                b[j] = r < R && k < K ? x[(size_t)r * K + k] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 32; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
+    }
     // the workgroup's tile: waves 1..3 through LDS (the staging area is free after this barrier), wave order
     const int nw = blockDim.x >> 6;
     if (nw > 1) {
@@ -237,12 +242,20 @@ int fill_table(MatTable &T, int nmat, const int32_t *N) {
 
 // launch geometry of one rows GEMM: KS workgroups per tile, waves per workgroup, dynamic LDS bytes
 struct Geo {
-    int ks, waves;
+    int ks, waves, passes;
     size_t lds;
 };
+// passes per workgroup: MTTS_ROWS_PASSES (default 1: the whole reduction split over workgroups)
+int passes_of(int R) {
+    const char *e = getenv("MTTS_ROWS_PASSES");
+    const int want = e ? atoi(e) : 1, need = (R + kRange - 1) / kRange;
+    return want < 1 ? 1 : (want > need ? need : want);
+}
+
 Geo geometry(int R, bool staged) {
     Geo g;
-    g.ks = (R + kRange - 1) / kRange;
+    g.passes = passes_of(R);
+    g.ks = (R + kRange * g.passes - 1) / (kRange * g.passes);
     g.waves = R >= kRange ? kWaves : (R + kChunk - 1) / kChunk;
     const size_t stage = staged ? (size_t)g.waves * 2 * 32 * kLd * sizeof(float) : 0;
     const size_t red = g.waves > 1 ? (size_t)g.waves * 16 * 64 * sizeof(float) : 0;
@@ -252,6 +265,7 @@ Geo geometry(int R, bool staged) {
 
 int check_ws(const Geo &g, int tiles, void *ws, size_t ws_bytes, Ws &w) {
     w.ks = g.ks;
+    w.passes = g.passes;
     w.part = nullptr;
     w.counter = nullptr;
     if (g.ks == 1) return MTTS_OK;

@@ -34,7 +34,8 @@ def _case(B, T, heads, seed, d=64):
 
 SHAPES = [(2, 64, 4, 64), (3, 77, 4, 64), (2, 600, 4, 64), (1, 1, 4, 64), (2, 130, 2, 64), (4, 300, 4, 64),
           (1, 129, 1, 64), (2, 65, 2, 32), (2, 300, 4, 32), (3, 121, 2, 96), (1, 600, 2, 96),
-          (2, 77, 2, 16), (2, 100, 1, 40)]  # head dims below the compiled 32/64/96 run zero-padded
+          (2, 77, 2, 16), (2, 100, 1, 40),  # head dims below the compiled 32/64/96 run zero-padded
+          (2, 128, 2, 96), (3, 33, 2, 96), (2, 96, 1, 64)]  # T <= 128: the short kernels' edges
 
 
 @pytest.mark.parametrize("B,T,heads,d", SHAPES)
@@ -127,3 +128,40 @@ def test_attention_bf16_storage(B, T, H, D):
     assert torch.equal(o16, o32.bfloat16())
     assert torch.equal(l16, l32)
     assert rel(d16.float(), d32) < 1e-2, rel(d16.float(), d32)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("B,T,H,D,p", [(32, 120, 2, 96, 0.0), (4, 120, 2, 96, 0.1), (3, 70, 4, 64, 0.0)])
+def test_attention_short_path_matches_long(monkeypatch, precision, B, T, H, D, p):
+    """T <= 128 runs the short kernels (a block per 32 rows, the waves split the other axis, merged in
+    wave order); MTTS_ATTN_SHORT=0 sends the same call down the long kernels.  Same math in another
+    summation order: fp32 agrees to 1e-5, bf16 to bf16 rounding of the products; each path is bitwise
+    repeatable.  With dropout both regenerate the same mask (same (row, key) hash)."""
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator(device="cpu").manual_seed(T * H + D)
+    C = H * D
+    qkv = torch.randn(B, T, 3 * C, generator=g).to(DEV)
+    kb = torch.zeros(B, T, device=DEV)
+    for b in range(B):
+        kb[b, : max(1, T - 7 * b)] = 1
+    do = torch.randn(B, T, C, generator=g).to(DEV)
+    prec = O.PREC_FP32 if precision == "fp32" else O.PREC_BF16
+    seed = torch.tensor([1234, 99], dtype=torch.int32, device=DEV) if p > 0 else None
+    outs = {}
+    for mode in ("1", "1", "0"):
+        monkeypatch.setenv("MTTS_ATTN_SHORT", mode)
+        o = torch.empty(B, T, C, device=DEV)
+        lse = torch.empty(B, H, T, device=DEV)
+        O._attn_fwd(qkv, kb, o, lse, H, prec, dropout_p=p, seed=seed)
+        d = O._attn_bwd(do, qkv, kb, o, lse, H, prec, dropout_p=p, seed=seed)
+        torch.cuda.synchronize()
+        if mode in outs:
+            a = outs[mode]
+            assert torch.equal(a[0], o) and torch.equal(a[1], lse) and torch.equal(a[2], d)
+        outs[mode] = (o, lse, d)
+    (o1, l1, d1), (o0, l0, d0) = outs["1"], outs["0"]
+    rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()
+    tol = 1e-5 if precision == "fp32" else 1e-2
+    assert rel(o1, o0) < tol and rel(d1, d0) < tol, (rel(o1, o0), rel(d1, d0))
+    torch.testing.assert_close(l1, l0, rtol=0, atol=1e-4 if precision == "fp32" else 2e-2)

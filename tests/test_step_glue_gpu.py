@@ -64,11 +64,14 @@ def test_loss_sum_and_gradients():
     assert logged.tolist() == [1.0, 0.0, 2.0, 3.0] and float(d.grad) == float(f.grad) == 1.0
 
 
+@pytest.mark.parametrize("passes", ["1", "3"])
 @pytest.mark.parametrize("B,width,dim", [(1, 256, 1024), (5, 256, 1024), (32, 256, 1024), (3, 32, 128), (7, 96, 200)])
-def test_time_mlp_matches_torch(B, width, dim):
+def test_time_mlp_matches_torch(monkeypatch, B, width, dim, passes):
     """decoder.py:33-49 (Linear -> SiLU -> Linear) + each Resnet1D.mlp (Mish -> Linear) on the shared temb:
     the fused HIP path (csrc/time_mlp.hip) against the torch modules, forward and every weight / bias
-    gradient, fp32."""
+    gradient, fp32; the reduction split over workgroups (one pass each) and over passes inside a
+    workgroup (MTTS_ROWS_PASSES)."""
+    monkeypatch.setenv("MTTS_ROWS_PASSES", passes)
     import torch.nn.functional as F
 
     from matcha.models.components import _ops as O

@@ -33,8 +33,8 @@ print(f"total {tot:.0f} us over {len(rows)} launches; {sum(x[1] for x in rows)/t
       f"{sum(x[2] for x in rows)/tot/1e3:.0f} GB/s algorithmic")
 agg = collections.defaultdict(lambda: [0.0, 0, 0.0, 0.0])
 for us, fl, nb, d in rows:
-    key = (d["M"], d["N"], d["K"], d["cin"], d["ntaps"], d["in_stride"], d["res"], d["act"], d["pre"], d["drop"], d["cs"], d["asc"])
+    key = (d["M"], d["N"], d["K"], d["cin"], d["ntaps"], d["in_stride"], d["res"], d["act"], d["pre"], d["drop"], d["cs"], d["asc"], d.get("cfg", -1))
     a = agg[key]; a[0] += us; a[1] += 1; a[2] += fl; a[3] += nb
-print("   us  n   avg   TF/s  GB/s   M      N    K   cin tap s res act pre drop cs asc")
+print("   us  n   avg   TF/s  GB/s   M      N    K   cin tap s res act pre drop cs asc cfg")
 for k, a in sorted(agg.items(), key=lambda kv: -kv[1][0]):
     print(f"{a[0]:6.0f} {a[1]:2d} {a[0]/a[1]:6.1f} {a[2]/a[0]/1e6:5.0f} {a[3]/a[0]/1e3:5.0f}  " + " ".join(str(int(x)) for x in k))
