@@ -34,6 +34,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kTile = 64;           // keys (fwd, dQ) or queries (dKV) per LDS stage
 constexpr int kRowsPerBlock = 128;  // queries (fwd, dQ) or keys (dKV) per block: 4 waves x 32
 constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr size_t kLdsMax = 160 * 1024;
 
@@ -233,48 +234,60 @@ __device__ __forceinline__ void mma_perm(f32x16 &acc, const typename G<BF16, D>:
 }
 
 // Staging of a 64-row tile of one head (rows r0.. of batch b) into LDS: row layout and/or transposed.
-// Rows >= T are zero.
-template <bool BF16, int D>
+// TI = uint16_t (bf16 storage, bf16 MFMA): the 4 bf16 of a chunk travel as raw bits into the image --
+// no unpack to fp32 and repack.
+template <bool BF16, int D, typename TI = float>
 struct TileLoader {
     using Gm = G<BF16, D>;
-    float4 v[Gm::F4];
+    static constexpr bool kRaw = BF16 && sizeof(TI) == 2;
+    float4 v[kRaw ? 1 : Gm::F4];
+    uint2 r[kRaw ? Gm::F4 : 1];
     bool narrow = false;  // runtime head dim dh < D: columns past dh are zeroed
     // unconditional loads from clamped addresses: no branch around a load, so the loads stay in flight
     // through the compute phase.  Rows past T are NOT zeroed: they hold finite data (row 0 of the
     // batch) and every kernel gives them probability 0 (key bias -inf / query lse +inf), so they add
     // exact zeros to every product.
-    template <typename TI>
     __device__ void load(const TI *base, int ld, int b, int T, int r0, int tid, int dh) {
         narrow = dh < D;
+        const TI *bb = base + (size_t)b * T * ld;  // batch b, row 0
 #pragma unroll
         for (int i = 0; i < Gm::F4; ++i) {
-            int r, c;
-            stage_rc<BF16, D>(tid + kThreads * i, r, c);
-            const bool ok = r0 + r < T && c < dh;
-            const size_t off = ok ? ((size_t)b * T + r0 + r) * ld + c : (size_t)b * T * ld;
-            v[i] = ld4f(base + off);
+            int rr, c;
+            stage_rc<BF16, D>(tid + kThreads * i, rr, c);
+            const bool ok = r0 + rr < T && c < dh;
+            const TI *src = bb + (ok ? (r0 + rr) * ld + c : 0);
+            if constexpr (kRaw) r[i] = *reinterpret_cast<const uint2 *>(src);
+            else v[i] = ld4f(src);
         }
     }
     __device__ void store(typename Gm::T *rowt, typename Gm::T *trt, int tid, int dh) const {
 #pragma unroll
         for (int i = 0; i < Gm::F4; ++i) {
-            int r, c;
-            stage_rc<BF16, D>(tid + kThreads * i, r, c);
-            float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-            if (narrow && c >= dh) e[0] = e[1] = e[2] = e[3] = 0.f;
-            if constexpr (BF16) {  // one image serves both reads: `trt` names it when `rowt` is null
+            int rr, c;
+            stage_rc<BF16, D>(tid + kThreads * i, rr, c);
+            if constexpr (kRaw) {
+                uint2 w = r[i];
+                if (narrow && c >= dh) w = make_uint2(0u, 0u);
                 typename Gm::T *img = rowt ? rowt : trt;
-                if (img)
-                    *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(img) + img_off<D>(r, c)) =
-                        make_uint2(pack2(e[0], e[1]), pack2(e[2], e[3]));
+                if (img) *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(img) + img_off<D>(rr, c)) = w;
+                continue;
             } else {
-                if (rowt) {
+                float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+                if (narrow && c >= dh) e[0] = e[1] = e[2] = e[3] = 0.f;
+                if constexpr (BF16) {  // one image serves both reads: `trt` names it when `rowt` is null
+                    typename Gm::T *img = rowt ? rowt : trt;
+                    if (img)
+                        *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(img) + img_off<D>(rr, c)) =
+                            make_uint2(pack2(e[0], e[1]), pack2(e[2], e[3]));
+                } else {
+                    if (rowt) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) rowt[r * Gm::LDR + c + j] = e[j];
-                }
-                if (trt) {
+                        for (int j = 0; j < 4; ++j) rowt[rr * Gm::LDR + c + j] = e[j];
+                    }
+                    if (trt) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) trt[(c + j) * Gm::LDT + r] = e[j];
+                        for (int j = 0; j < 4; ++j) trt[(c + j) * Gm::LDT + rr] = e[j];
+                    }
                 }
             }
         }
@@ -341,7 +354,6 @@ __device__ __forceinline__ void tile_loop(int ntiles, Load &&load, Store &&store
     mtts::lds_barrier();
     for (int it = 0; it < ntiles; ++it) {
         const int buf = NB == 2 ? (it & 1) : 0;
-        const bool more = it + 1 < ntiles;
         load((it + 1) * kTile);  // past the last tile every row is masked off (branch-free body)
         compute(buf, it * kTile);
         if constexpr (NB == 2) {
@@ -349,7 +361,7 @@ __device__ __forceinline__ void tile_loop(int ntiles, Load &&load, Store &&store
             mtts::lds_barrier();
         } else {
             mtts::lds_barrier();
-            if (more) {
+            if (it + 1 < ntiles) {
                 store(0);
                 mtts::lds_barrier();
             }
@@ -359,8 +371,13 @@ __device__ __forceinline__ void tile_loop(int ntiles, Load &&load, Store &&store
 
 // ------------------------------------------------------------------------------------------------
 // forward: grid (ceil(T/128), H, B); lane = query
-template <bool BF16, int D, typename TI = float>
-__global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_fwd_kernel(mtts_attn_args p) {
+// three workgroups per CU for the decoder's instance (bf16 storage, no dropout: 165 VGPRs): its 640
+// workgroups at B = 32, T = 600 then run in one round instead of 512 + 128
+template <bool BF16, int D, typename TI, bool DROP>
+constexpr int fwd_min_blocks() { return (BF16 && D <= 64) ? ((!DROP && sizeof(TI) == 2) ? 3 : 2) : 1; }
+
+template <bool BF16, int D, typename TI = float, bool DROP = true>
+__global__ __launch_bounds__(kThreads, (fwd_min_blocks<BF16, D, TI, DROP>())) void attn_fwd_kernel(mtts_attn_args p) {
     const TI *Qp = reinterpret_cast<const TI *>(p.q), *Kp = reinterpret_cast<const TI *>(p.k),
              *Vp = reinterpret_cast<const TI *>(p.v);
     TI *Op = reinterpret_cast<TI *>(p.o);
@@ -393,19 +410,19 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_fwd_
         for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
     float m = -INFINITY, l = 0.f;
 
-    TileLoader<BF16, D> lk, lv;
+    TileLoader<BF16, D, TI> lk, lv;
     float bias_r = 0.f;
-    auto load = [&](int k0) {
+    auto load = [&](int k0) __attribute__((always_inline)) {
         lk.load(Kb, p.ldq, b, T, k0, tid, dh);
         lv.load(Vb, p.ldq, b, T, k0, tid, dh);
         bias_r = stage_bias(p, b, k0 + (tid & (kTile - 1)), c0);
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf) __attribute__((always_inline)) {
         lk.store(Ks + buf * Gm::RE, nullptr, tid, dh);
         lv.store(nullptr, Vt + buf * (BF16 ? Gm::RE : Gm::TE), tid, dh);
         store_bias(bias_s, flag_s, buf, bias_r, tid);
     };
-    const bool drop = p.dropout_p > 0.f;
+    const bool drop = DROP && p.dropout_p > 0.f;  // DROP = false: no dropout code
     uint32_t s0 = 0, s1 = 0;
     if (drop) {
         s0 = p.seed[0];
@@ -413,15 +430,19 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_fwd_
     }
     const float inv_keep = 1.f / (1.f - p.dropout_p);
     const uint32_t prow = (uint32_t)(((size_t)b * p.H + h) * T + q);  // dropout row key of this query
-    auto body = [&](int buf, int k0, auto has_bias) {
+    auto body = [&](int buf, int k0, auto has_bias) __attribute__((always_inline)) {
         constexpr bool TB = decltype(has_bias)::value;
         const ST *K_ = Ks + buf * Gm::RE, *V_ = Vt + buf * (BF16 ? Gm::RE : Gm::TE);
         const float *bs = bias_s + buf * kTile;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
+            // bf16: the running max enters as the accumulator's start (S^T - m out of the MFMA; this also
+            // shortened the live ranges enough for three workgroups per CU); m = -inf before the first
+            // sub-tile, whose start is 0
+            const bool first = m == -INFINITY;  // wave-uniform (every lane starts there)
             f32x16 sacc;
 #pragma unroll
-            for (int v = 0; v < 16; ++v) sacc[v] = 0.f;
+            for (int v = 0; v < 16; ++v) sacc[v] = (BF16 && !first) ? -m : 0.f;
             mma_rows<BF16, D>(sacc, K_, sub * 32 + lr, lh, qf);  // S^T: rows = keys, col = this lane's query
             float s[16], bv[16], mx = -INFINITY;
             if constexpr (TB) crow_load16(bs + sub * 32, lh, bv);
@@ -432,20 +453,40 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_fwd_
                 mx = fmaxf(mx, s[v]);
             }
             mx = half_max(mx);
-            if (__any(mx > m + kDefer)) {  // m = -inf before the first sub-tile: always taken there
-                const float m_new = fmaxf(m, mx);
-                const float corr = fast_exp2(m - m_new);
-                l *= corr;
+            if constexpr (BF16) {  // s holds S - m (first: S)
+                if (first) {
+                    m = mx;
 #pragma unroll
-                for (int t = 0; t < Gm::NT; ++t)
+                    for (int v = 0; v < 16; ++v) s[v] -= mx;
+                } else if (__any(mx > kDefer)) {
+                    const float up = fmaxf(mx, 0.f), corr = fast_exp2(-up);
+                    l *= corr;
 #pragma unroll
-                    for (int v = 0; v < 16; ++v) acc[t][v] *= corr;
-                m = m_new;
+                    for (int t = 0; t < Gm::NT; ++t)
+#pragma unroll
+                        for (int v = 0; v < 16; ++v) acc[t][v] *= corr;
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) s[v] -= up;
+                    m += up;
+                }
+            } else {
+                if (__any(mx > m + kDefer)) {  // m = -inf before the first sub-tile: always taken there
+                    const float m_new = fmaxf(m, mx);
+                    const float corr = fast_exp2(m - m_new);
+                    l *= corr;
+#pragma unroll
+                    for (int t = 0; t < Gm::NT; ++t)
+#pragma unroll
+                        for (int v = 0; v < 16; ++v) acc[t][v] *= corr;
+                    m = m_new;
+                }
+#pragma unroll
+                for (int v = 0; v < 16; ++v) s[v] -= m;
             }
             float rs = 0.f;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
-                s[v] = fast_exp2(s[v] - m);
+                s[v] = fast_exp2(s[v]);
                 rs += s[v];
             }
             l += half_sum(rs);
@@ -460,7 +501,7 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_fwd_
             for (int t = 0; t < Gm::NT; ++t) mma_perm<BF16, D>(acc[t], V_, t * 32 + lr, sub, lh, s);  // O^T += V^T P^T
         }
     };
-    auto compute = [&](int buf, int k0) {  // tiles inside the valid keys skip the bias (wave-uniform)
+    auto compute = [&](int buf, int k0) __attribute__((always_inline)) {  // tiles inside the valid keys skip the bias (wave-uniform)
         if (flag_s[buf])
             body(buf, k0, std::true_type{});
         else
@@ -485,7 +526,7 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_fwd_
 
 // ------------------------------------------------------------------------------------------------
 // backward, dQ: grid (ceil(T/128), H, B); lane = query.  Also writes Drow = rowsum(dO * O) for dKV.
-template <bool BF16, int D, typename TI = float>
+template <bool BF16, int D, typename TI = float, bool DROP = true>
 __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(mtts_attn_args p, mtts_attn_grads g, float *Drow) {
     const TI *Qp = reinterpret_cast<const TI *>(p.q), *Kp = reinterpret_cast<const TI *>(p.k),
              *Vp = reinterpret_cast<const TI *>(p.v), *Op = reinterpret_cast<const TI *>(p.o),
@@ -537,19 +578,19 @@ __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(
 #pragma unroll
         for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
 
-    TileLoader<BF16, D> lk, lv;
+    TileLoader<BF16, D, TI> lk, lv;
     float bias_r = 0.f;
-    auto load = [&](int k0) {
+    auto load = [&](int k0) __attribute__((always_inline)) {
         lk.load(Kb, p.ldq, b, T, k0, tid, dh);
         lv.load(Vb, p.ldq, b, T, k0, tid, dh);
         bias_r = stage_bias(p, b, k0 + (tid & (kTile - 1)), c0);
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf) __attribute__((always_inline)) {
         lk.store(Ks + buf * Gm::RE, BF16 ? nullptr : Kt + buf * Gm::TE, tid, dh);
         lv.store(Vs + buf * Gm::RE, nullptr, tid, dh);
         store_bias(bias_s, flag_s, buf, bias_r, tid);
     };
-    const bool drop = p.dropout_p > 0.f;
+    const bool drop = DROP && p.dropout_p > 0.f;  // DROP = false: no dropout code
     uint32_t s0 = 0, s1 = 0;
     if (drop) {
         s0 = p.seed[0];
@@ -560,7 +601,7 @@ __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(
     // bf16 without dropout: the row constants start the accumulators (S^T - lse, dP^T - D), so the
     // chains end ready for exp2 and the product
     const bool fold = BF16 && !drop;
-    auto body = [&](int buf, int k0, auto has_bias) {
+    auto body = [&](int buf, int k0, auto has_bias) __attribute__((always_inline)) {
         constexpr bool TB = decltype(has_bias)::value;
         const ST *K_ = Ks + buf * Gm::RE, *V_ = Vs + buf * Gm::RE, *KT_ = BF16 ? K_ : Kt + buf * Gm::TE;
         const float *bs = bias_s + buf * kTile;
@@ -596,7 +637,7 @@ __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(
             for (int t = 0; t < Gm::NT; ++t) mma_perm<BF16, D>(acc[t], KT_, t * 32 + lr, sub, lh, ds);  // dQ^T += K^T dS^T
         }
     };
-    auto compute = [&](int buf, int k0) {
+    auto compute = [&](int buf, int k0) __attribute__((always_inline)) {
         if (flag_s[buf])
             body(buf, k0, std::true_type{});
         else
@@ -620,7 +661,7 @@ __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(
 
 // ------------------------------------------------------------------------------------------------
 // backward, dK/dV: grid (ceil(T/128), H, B); lane = key.  C layout: rows = queries, col = key.
-template <bool BF16, int D, typename TI = float>
+template <bool BF16, int D, typename TI = float, bool DROP = true>
 __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_dkv_kernel(mtts_attn_args p, mtts_attn_grads g,
                                                                 const float *Drow) {
     const TI *Qp = reinterpret_cast<const TI *>(p.q), *Kp = reinterpret_cast<const TI *>(p.k),
@@ -658,9 +699,9 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
 #pragma unroll
         for (int v = 0; v < 16; ++v) dk[t][v] = dv[t][v] = 0.f;
 
-    TileLoader<BF16, D> lq, lg;
+    TileLoader<BF16, D, TI> lq, lg;
     float lse_r = 0.f, d_r = 0.f;
-    auto load = [&](int q0) {
+    auto load = [&](int q0) __attribute__((always_inline)) {
         lq.load(Qb, p.ldq, b, T, q0, tid, dh);
         lg.load(Gb, g.lddo, b, T, q0, tid, dh);
         {
@@ -670,7 +711,7 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
             d_r = qq < T ? d_raw : 0.f;
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf) __attribute__((always_inline)) {
         lq.store(Qs + buf * Gm::RE, BF16 ? nullptr : Qt + buf * Gm::TE, tid, dh);
         lg.store(Gs + buf * Gm::RE, BF16 ? nullptr : Gt + buf * Gm::TE, tid, dh);
         if (tid < kTile) {
@@ -678,7 +719,7 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
             d_s[buf * kTile + tid] = d_r;
         }
     };
-    const bool drop = p.dropout_p > 0.f;
+    const bool drop = DROP && p.dropout_p > 0.f;  // DROP = false: no dropout code
     uint32_t s0 = 0, s1 = 0;
     if (drop) {
         s0 = p.seed[0];
@@ -686,7 +727,7 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
     }
     const float inv_keep = 1.f / (1.f - p.dropout_p);
     const bool fold = BF16 && !drop;  // row constants start the accumulators (as in the dQ kernel)
-    auto compute = [&](int buf, int q0) {
+    auto compute = [&](int buf, int q0) __attribute__((always_inline)) {
         const ST *Q_ = Qs + buf * Gm::RE, *G_ = Gs + buf * Gm::RE;
         const ST *QT_ = BF16 ? Q_ : Qt + buf * Gm::TE, *GT_ = BF16 ? G_ : Gt + buf * Gm::TE;
         const float *ls = lse_s + buf * kTile, *dd = d_s + buf * kTile;
@@ -758,7 +799,6 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
 // tiles (no transposed copies), which keeps two tiles of two operands inside the LDS.
 constexpr int kShortT = 2 * kTile;
 constexpr int kShortRows = 32;
-constexpr int kWaves = kThreads / 64;
 
 template <bool BF16, int D>
 struct Short {
@@ -791,7 +831,7 @@ template <bool BF16, int D, typename TI>
 __device__ __forceinline__ void stage_pair(const TI *A, const TI *Bm, int lda, int ldb, int b, int T, int tid, int dh,
                                            typename G<BF16, D>::T *As, typename G<BF16, D>::T *Bs) {
     using Gm = G<BF16, D>;
-    TileLoader<BF16, D> la0, lb0, la1, lb1;
+    TileLoader<BF16, D, TI> la0, lb0, la1, lb1;
     la0.load(A, lda, b, T, 0, tid, dh);
     lb0.load(Bm, ldb, b, T, 0, tid, dh);
     const bool two = T > kTile;
@@ -1206,9 +1246,12 @@ int fwd_launch(const mtts_attn_args &p, hipStream_t st) {
     }
     constexpr size_t lds = lds_bytes(fwd_stage<BF16, D>());
     static_assert(lds <= kLdsMax, "attention fwd LDS");
-    if (!set_lds(attn_fwd_kernel<BF16, D, TI>, lds)) return mtts::fail(MTTS_ERR_HIP, "attention: LDS attribute");
+    const bool drop = p.dropout_p > 0.f;  // the dropout-free instance holds fewer registers
+    if (!set_lds(attn_fwd_kernel<BF16, D, TI, true>, lds) || !set_lds(attn_fwd_kernel<BF16, D, TI, false>, lds))
+        return mtts::fail(MTTS_ERR_HIP, "attention: LDS attribute");
     dim3 grid((p.T + kRowsPerBlock - 1) / kRowsPerBlock, p.H, p.B);
-    hipLaunchKernelGGL((attn_fwd_kernel<BF16, D, TI>), grid, dim3(kThreads), lds, st, p);
+    if (drop) hipLaunchKernelGGL((attn_fwd_kernel<BF16, D, TI, true>), grid, dim3(kThreads), lds, st, p);
+    else hipLaunchKernelGGL((attn_fwd_kernel<BF16, D, TI, false>), grid, dim3(kThreads), lds, st, p);
     return mtts::check_launch("attn_fwd_kernel");
 }
 
@@ -1231,12 +1274,18 @@ int bwd_launch(const mtts_attn_args &p, const mtts_attn_grads &g, float *Drow, h
     }
     constexpr size_t lq = lds_bytes(dq_stage<BF16, D>()), lkv = lds_bytes(dkv_stage<BF16, D>());
     static_assert(lq <= kLdsMax && lkv <= kLdsMax, "attention bwd LDS");
-    if (!set_lds(attn_bwd_dq_kernel<BF16, D, TI>, lq) || !set_lds(attn_bwd_dkv_kernel<BF16, D, TI>, lkv))
+    if (!set_lds(attn_bwd_dq_kernel<BF16, D, TI, true>, lq) || !set_lds(attn_bwd_dkv_kernel<BF16, D, TI, true>, lkv) ||
+        !set_lds(attn_bwd_dq_kernel<BF16, D, TI, false>, lq) || !set_lds(attn_bwd_dkv_kernel<BF16, D, TI, false>, lkv))
         return mtts::fail(MTTS_ERR_HIP, "attention_bwd: LDS attribute");
     dim3 grid((p.T + kRowsPerBlock - 1) / kRowsPerBlock, p.H, p.B);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<BF16, D, TI>), grid, dim3(kThreads), lq, st, p, g, Drow);
+    const bool drop = p.dropout_p > 0.f;
+    if (drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<BF16, D, TI, true>), grid, dim3(kThreads), lq, st, p, g, Drow);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<BF16, D, TI, false>), grid, dim3(kThreads), lq, st, p, g, Drow);
     if (int rc = mtts::check_launch("attn_bwd_dq_kernel")) return rc;
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<BF16, D, TI>), grid, dim3(kThreads), lkv, st, p, g, (const float *)Drow);
+    if (drop)
+        hipLaunchKernelGGL((attn_bwd_dkv_kernel<BF16, D, TI, true>), grid, dim3(kThreads), lkv, st, p, g, (const float *)Drow);
+    else
+        hipLaunchKernelGGL((attn_bwd_dkv_kernel<BF16, D, TI, false>), grid, dim3(kThreads), lkv, st, p, g, (const float *)Drow);
     return mtts::check_launch("attn_bwd_dkv_kernel");
 }
 

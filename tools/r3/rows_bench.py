@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """Time MLP (csrc/time_mlp.hip) at the decoder's shapes (B=32, 160 -> 1024 -> 1024, 6 x 1024 -> 256):
-forward and backward time per call with HIP events, for MTTS_ROWS_PASSES in {1, 2, 4, 6}, run back to back
+forward + backward (8 launches) timed as a captured graph replayed back to back, for MTTS_ROWS_PASSES in {1, 2, 4, 6}, run back to back
 (clean caches) and right after a 512 MB fill that leaves the L2s dirty (as in the train step, where the
 time path's backward follows the decoder's big kernels)."""
 import os
@@ -23,27 +23,45 @@ w = [torch.randn(32, 256, device=dev) for _ in projs]
 junk = torch.empty(128 * 1024 * 1024, device=dev)
 
 
-def once(dirty):
-    s0, s1, s2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-    if dirty:
-        junk.fill_(1.0)
-    s0.record()
-    temb, tps = O.time_mlp(e, mlp.linear_1, mlp.linear_2, projs)
-    s1.record()
-    if dirty:
-        pass
-    torch.autograd.backward(tps, w)
-    s2.record()
-    torch.cuda.synchronize()
-    return s0.elapsed_time(s1) * 1e3, s1.elapsed_time(s2) * 1e3
-
-
-for passes in ("1", "2", "4", "6"):
+def graph_of(dirty, passes):
     os.environ["MTTS_ROWS_PASSES"] = passes
+    for p in list(mlp.parameters()) + [q for lin in projs for q in lin.parameters()]:
+        p.grad = None
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        for _ in range(2):  # warm-up outside the capture (workspaces, packing)
+            temb, tps = O.time_mlp(e, mlp.linear_1, mlp.linear_2, projs)
+            torch.autograd.backward(tps, w)
+    torch.cuda.current_stream().wait_stream(st)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        if dirty:
+            junk.fill_(1.0)
+        temb, tps = O.time_mlp(e, mlp.linear_1, mlp.linear_2, projs)
+        torch.autograd.backward(tps, w)
+    return g
+
+
+def replay_us(g, n=50):
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    g.replay()
+    torch.cuda.synchronize()
+    s0.record()
+    for _ in range(n):
+        g.replay()
+    s1.record()
+    torch.cuda.synchronize()
+    return s0.elapsed_time(s1) * 1e3 / n
+
+
+gf = torch.cuda.CUDAGraph()
+with torch.cuda.graph(gf):
+    junk.fill_(1.0)
+fill = replay_us(gf)
+print(f"512 MB fill alone: {fill:.1f} us", flush=True)
+for passes in ("1", "2", "4", "6"):
     for dirty in (False, True):
-        for _ in range(3):
-            once(dirty)
-        r = [once(dirty) for _ in range(20)]
-        f = sorted(x[0] for x in r)[10]
-        b = sorted(x[1] for x in r)[10]
-        print(f"passes={passes} dirty={dirty}: fwd {f:7.1f} us  bwd {b:7.1f} us (median of 20)", flush=True)
+        t = replay_us(graph_of(dirty, passes))
+        print(f"passes={passes} dirty={dirty}: time MLP fwd+bwd graph replay {t - (fill if dirty else 0):7.1f} us "
+              f"(8 launches)", flush=True)
