@@ -1,0 +1,10 @@
+#!/bin/bash
+# rows GEMM whole-reduction mode: glue tests, rows graph bench (both modes) under a kernel trace, step breakdown
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/${TAG:-r3p}; mkdir -p $O; cd $R
+timeout -k 10 200 python -u -m pytest tests/test_step_glue_gpu.py tests/test_model_gpu.py -q --maxfail 6 --timeout 100 --timeout-method thread > $O/tests.log 2>&1; rc=$?
+tail -2 $O/tests.log; [ $rc -ne 0 ] && { grep -E "^FAILED|^E  " $O/tests.log | head -40; exit $rc; }
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/rows -o run -- python3 $R/tools/r3/rows_bench.py > $O/rows.log 2>&1; echo "rows rc=$?"; grep split $O/rows.log
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu-baseline --no-synth --no-extra --no-graph-profile --steps 10 --warmup 3 > $O/prof.json 2> $O/prof.err; rc=$?
+echo "prof rc=$rc"; [ $rc -ne 0 ] && { tail -20 $O/prof.err; exit $rc; }
+T=$(find $O/prof -name "*kernel_trace.csv" | head -1); python3 $R/tools/step_breakdown.py $T > $O/step.txt; head -24 $O/step.txt; grep rows_gemm $O/step.txt
