@@ -165,8 +165,8 @@ def _bucketed_batches(B, Tx, Ty, n, rank, world, dev):
 FAMILIES = {
     "gemm": ("conv_gemm_kernel", "conv_gemm_glds_kernel", "splitk_epilogue_kernel"),
     "wgrad": ("conv_wgrad_kernel", "reduce_partials_kernel"),
-    "attn": ("attn_fwd_kernel", "attn_bwd_dq_kernel", "attn_bwd_dkv_kernel", "attn_fwd_short_kernel",
-             "attn_bwd_dq_short_kernel", "attn_bwd_dkv_short_kernel"),
+    "attn": ("attn_fwd_kernel", "attn_bwd_dq_kernel", "attn_bwd_dkv_kernel", "attn_drow_kernel",
+             "attn_bwd_merged_kernel", "attn_fwd_short_kernel", "attn_bwd_dq_short_kernel", "attn_bwd_dkv_short_kernel"),
 }
 
 
@@ -562,7 +562,7 @@ def main():
         "fixed-order partial sums, which also hold the LayerNorm / GroupNorm gamma / beta partials)",
         "2 M N K FLOP; bytes = dY + unique A rows + dW; graph time includes the whole batched reduce")
     roofline_attn = roofline_of(
-        attn_log, "attn", "attn_fwd / attn_bwd_dq + attn_bwd_dkv kernels, long (decoder) and short (encoder, T <= 128)",
+        attn_log, "attn", "attn_fwd + backward (Drow pre-pass + merged dQ / dK-dV launch) kernels, long (decoder) and short (encoder, T <= 128)",
         "FLOP = 4 B H T^2 D fwd, 8 B H T^2 D bwd (standard flash-attention accounting, recomputation not counted); "
         "bytes = q, k, v, o (+ dO, dq, dk, dv) once")
 

@@ -525,9 +525,29 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<BF16, D, TI, DROP>())) vo
 }
 
 // ------------------------------------------------------------------------------------------------
-// backward, dQ: grid (ceil(T/128), H, B); lane = query.  Also writes Drow = rowsum(dO * O) for dKV.
-template <bool BF16, int D, typename TI = float, bool DROP = true>
-__global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(mtts_attn_args p, mtts_attn_grads g, float *Drow) {
+// dsum = rowsum(dO * O) over this lane's half of the head dims, then the two halves -- one function for
+// the dQ pass and the Drow pre-pass, so both form the same value
+template <int D, typename TI>
+__device__ __forceinline__ float row_dot(const TI *orow, const TI *grow, int lh, int dh, bool ok) {
+    float dsum = 0.f;
+    if (ok) {
+        orow += (D / 2) * lh;
+        grow += (D / 2) * lh;
+#pragma unroll
+        for (int i = 0; i < D / 2; i += 4) {
+            if ((D / 2) * lh + i >= dh) break;
+            const float4 a = ld4f(orow + i);
+            const float4 c = ld4f(grow + i);
+            dsum += a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
+        }
+    }
+    return half_sum(dsum);
+}
+
+// backward, dQ: grid (ceil(T/128), H, B); lane = query.  Writes Drow = rowsum(dO * O) for dKV unless the
+// pre-pass did (Drow null).  bx: this workgroup's query block.
+template <bool BF16, int D, typename TI, bool DROP>
+__device__ __forceinline__ void bwd_dq_body(const mtts_attn_args &p, const mtts_attn_grads &g, float *Drow, int bx) {
     const TI *Qp = reinterpret_cast<const TI *>(p.q), *Kp = reinterpret_cast<const TI *>(p.k),
              *Vp = reinterpret_cast<const TI *>(p.v), *Op = reinterpret_cast<const TI *>(p.o),
              *Gp = reinterpret_cast<const TI *>(g.dout);
@@ -545,7 +565,7 @@ __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
     const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
-    const int q = blockIdx.x * kRowsPerBlock + wave * 32 + lr;
+    const int q = bx * kRowsPerBlock + wave * 32 + lr;
     const bool q_ok = q < T;
     const size_t qrow = (size_t)b * T + (q_ok ? q : 0);
     const TI *Kb = Kp + h * dh, *Vb = Vp + h * dh;
@@ -555,22 +575,10 @@ __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(
     qf.load(Qp + h * dh + qrow * p.ldq, q_ok, lh, dh, BF16 ? sl2 : 1.f);  // as the forward's
     gf.load(Gp + h * dh + qrow * g.lddo, q_ok, lh, dh);
     // Drow[q] = sum_d dO[q,d] * O[q,d]: each half-wave lane sums D/2 dims
-    float dsum = 0.f;
-    if (q_ok) {
-        const TI *orow = Op + qrow * p.ldo + h * dh + (D / 2) * lh;
-        const TI *grow = Gp + qrow * g.lddo + h * dh + (D / 2) * lh;
-#pragma unroll
-        for (int i = 0; i < D / 2; i += 4) {
-            if ((D / 2) * lh + i >= dh) break;
-            const float4 a = ld4f(orow + i);
-            const float4 c = ld4f(grow + i);
-            dsum += a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
-        }
-    }
-    dsum = half_sum(dsum);
+    const float dsum = row_dot<D>(Op + qrow * p.ldo + h * dh, Gp + qrow * g.lddo + h * dh, lh, dh, q_ok);
     const size_t srow = ((size_t)b * p.H + h) * T + (q_ok ? q : 0);
     const float lse2 = q_ok ? p.lse[srow] : 0.f;
-    if (q_ok && lh == 0) Drow[srow] = dsum;
+    if (Drow && q_ok && lh == 0) Drow[srow] = dsum;
 
     f32x16 acc[Gm::NT];
 #pragma unroll
@@ -661,9 +669,8 @@ __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(
 
 // ------------------------------------------------------------------------------------------------
 // backward, dK/dV: grid (ceil(T/128), H, B); lane = key.  C layout: rows = queries, col = key.
-template <bool BF16, int D, typename TI = float, bool DROP = true>
-__global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_dkv_kernel(mtts_attn_args p, mtts_attn_grads g,
-                                                                const float *Drow) {
+template <bool BF16, int D, typename TI, bool DROP>
+__device__ __forceinline__ void bwd_dkv_body(const mtts_attn_args &p, const mtts_attn_grads &g, const float *Drow, int bx) {
     const TI *Qp = reinterpret_cast<const TI *>(p.q), *Kp = reinterpret_cast<const TI *>(p.k),
              *Vp = reinterpret_cast<const TI *>(p.v), *Gp = reinterpret_cast<const TI *>(g.dout);
     TI *DKp = reinterpret_cast<TI *>(g.dk), *DVp = reinterpret_cast<TI *>(g.dv);
@@ -681,7 +688,7 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
     const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
-    const int key = blockIdx.x * kRowsPerBlock + wave * 32 + lr;
+    const int key = bx * kRowsPerBlock + wave * 32 + lr;
     const bool k_ok = key < T;
     const size_t krow = (size_t)b * T + (k_ok ? key : 0);
 
@@ -787,6 +794,40 @@ __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_
                 st4f(dvr + c, make_float4(dv[t][4 * gi], dv[t][4 * gi + 1], dv[t][4 * gi + 2], dv[t][4 * gi + 3]));
             }
     }
+}
+
+template <bool BF16, int D, typename TI = float, bool DROP = true>
+__global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(mtts_attn_args p, mtts_attn_grads g, float *Drow) {
+    bwd_dq_body<BF16, D, TI, DROP>(p, g, Drow, blockIdx.x);
+}
+template <bool BF16, int D, typename TI = float, bool DROP = true>
+__global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_dkv_kernel(mtts_attn_args p, mtts_attn_grads g,
+                                                                                        const float *Drow) {
+    bwd_dkv_body<BF16, D, TI, DROP>(p, g, Drow, blockIdx.x);
+}
+
+// Drow pre-pass: rowsum(dO * O) per (query, head), grid (ceil(T/128), H, B), the dQ pass's lane mapping
+// and summation (row_dot) -- so the merged backward below needs no ordering between its two halves
+template <int D, typename TI>
+__global__ __launch_bounds__(kThreads) void attn_drow_kernel(mtts_attn_args p, mtts_attn_grads g, float *Drow) {
+    const TI *Op = reinterpret_cast<const TI *>(p.o), *Gp = reinterpret_cast<const TI *>(g.dout);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;
+    const int q = blockIdx.x * kRowsPerBlock + wave * 32 + lr;
+    const bool q_ok = q < T;
+    const size_t qrow = (size_t)b * T + (q_ok ? q : 0);
+    const float dsum = row_dot<D>(Op + qrow * p.ldo + h * dh, Gp + qrow * g.lddo + h * dh, lh, dh, q_ok);
+    if (q_ok && lh == 0) Drow[((size_t)b * p.H + h) * T + q] = dsum;
+}
+
+// Merged backward: grid (2 * nq, H, B) -- the first nq workgroups run the dQ pass, the rest the dK/dV pass
+// (Drow from the pre-pass).  One launch of twice the workgroups: at T = 600 the 640 + 640 workgroups fill
+// ~2.5 rounds of the 512 slots instead of 2 + 2.
+template <bool BF16, int D, typename TI = float, bool DROP = true>
+__global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_merged_kernel(mtts_attn_args p, mtts_attn_grads g,
+                                                                                           float *Drow, int nq) {
+    if ((int)blockIdx.x < nq) bwd_dq_body<BF16, D, TI, DROP>(p, g, nullptr, blockIdx.x);
+    else bwd_dkv_body<BF16, D, TI, DROP>(p, g, Drow, blockIdx.x - nq);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1255,6 +1296,12 @@ int fwd_launch(const mtts_attn_args &p, hipStream_t st) {
     return mtts::check_launch("attn_fwd_kernel");
 }
 
+// merged backward (default) or the two-launch dQ, dK/dV sequence (MTTS_ATTN_BWD_MERGED=0)
+bool bwd_merged() {
+    const char *e = getenv("MTTS_ATTN_BWD_MERGED");
+    return !(e && e[0] == '0');
+}
+
 template <bool BF16, int D, typename TI = float>
 int bwd_launch(const mtts_attn_args &p, const mtts_attn_grads &g, float *Drow, hipStream_t st) {
     if constexpr (BF16 && sizeof(TI) == 4) {
@@ -1279,6 +1326,18 @@ int bwd_launch(const mtts_attn_args &p, const mtts_attn_grads &g, float *Drow, h
         return mtts::fail(MTTS_ERR_HIP, "attention_bwd: LDS attribute");
     dim3 grid((p.T + kRowsPerBlock - 1) / kRowsPerBlock, p.H, p.B);
     const bool drop = p.dropout_p > 0.f;
+    if (bwd_merged()) {  // Drow pre-pass, then the two passes as ONE launch
+        constexpr size_t lm = lq > lkv ? lq : lkv;
+        if (!set_lds(attn_bwd_merged_kernel<BF16, D, TI, true>, lm) || !set_lds(attn_bwd_merged_kernel<BF16, D, TI, false>, lm))
+            return mtts::fail(MTTS_ERR_HIP, "attention_bwd: LDS attribute");
+        hipLaunchKernelGGL((attn_drow_kernel<D, TI>), grid, dim3(kThreads), 0, st, p, g, Drow);
+        if (int rc = mtts::check_launch("attn_drow_kernel")) return rc;
+        const int nq = (int)grid.x;
+        dim3 grid2(2 * grid.x, grid.y, grid.z);
+        if (drop) hipLaunchKernelGGL((attn_bwd_merged_kernel<BF16, D, TI, true>), grid2, dim3(kThreads), lm, st, p, g, Drow, nq);
+        else hipLaunchKernelGGL((attn_bwd_merged_kernel<BF16, D, TI, false>), grid2, dim3(kThreads), lm, st, p, g, Drow, nq);
+        return mtts::check_launch("attn_bwd_merged_kernel");
+    }
     if (drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<BF16, D, TI, true>), grid, dim3(kThreads), lq, st, p, g, Drow);
     else hipLaunchKernelGGL((attn_bwd_dq_kernel<BF16, D, TI, false>), grid, dim3(kThreads), lq, st, p, g, Drow);
     if (int rc = mtts::check_launch("attn_bwd_dq_kernel")) return rc;

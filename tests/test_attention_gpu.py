@@ -165,3 +165,33 @@ def test_attention_short_path_matches_long(monkeypatch, precision, B, T, H, D, p
     tol = 1e-5 if precision == "fp32" else 1e-2
     assert rel(o1, o0) < tol and rel(d1, d0) < tol, (rel(o1, o0), rel(d1, d0))
     torch.testing.assert_close(l1, l0, rtol=0, atol=1e-4 if precision == "fp32" else 2e-2)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("B,T,H,D,io16", [(4, 600, 4, 64, True), (2, 300, 4, 64, False), (3, 200, 2, 96, False)])
+def test_attention_bwd_merged_equals_two_launch(monkeypatch, precision, B, T, H, D, io16):
+    """The merged backward (a Drow pre-pass + ONE launch whose first half runs the dQ pass and second half
+    the dK/dV pass) against the two-launch sequence (MTTS_ATTN_BWD_MERGED=0): bitwise equal -- the pre-pass
+    forms rowsum(dO * O) with the dQ pass's own lane mapping and summation (row_dot)."""
+    from matcha.models.components import _ops as O
+
+    if io16 and precision == "fp32":
+        pytest.skip("bf16 storage needs bf16 precision")
+    g = torch.Generator(device="cpu").manual_seed(B * T + D)
+    C = H * D
+    dt = torch.bfloat16 if io16 else torch.float32
+    qkv = torch.randn(B, T, 3 * C, generator=g).to(DEV).to(dt)
+    kb = torch.zeros(B, T, device=DEV)
+    for b in range(B):
+        kb[b, : T - 9 * b] = 1
+    do = torch.randn(B, T, C, generator=g).to(DEV).to(dt)
+    prec = O.PREC_FP32 if precision == "fp32" else O.PREC_BF16
+    o = torch.empty(B, T, C, device=DEV, dtype=dt)
+    lse = torch.empty(B, H, T, device=DEV)
+    O._attn_fwd(qkv, kb, o, lse, H, prec)
+    res = []
+    for merged in ("1", "0"):
+        monkeypatch.setenv("MTTS_ATTN_BWD_MERGED", merged)
+        res.append(O._attn_bwd(do, qkv, kb, o, lse, H, prec))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0], res[1])

@@ -2,5 +2,5 @@
 REGEX = {
     "gemm": "conv_gemm_kernel|conv_gemm_glds_kernel|splitk_epilogue_kernel",
     "wgrad": "conv_wgrad_kernel|reduce_partials_kernel",
-    "attn": "attn_fwd_kernel|attn_bwd_dq_kernel|attn_bwd_dkv_kernel|attn_fwd_short_kernel|attn_bwd_dq_short_kernel|attn_bwd_dkv_short_kernel",
+    "attn": "attn_fwd|attn_bwd|attn_drow",
 }
