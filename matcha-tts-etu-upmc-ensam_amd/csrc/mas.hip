@@ -530,7 +530,7 @@ struct WsLayout {
 
 WsLayout ws_layout(int B, int Tx, int Ty) {
     WsLayout w{};
-    w.K = Tx <= 64 ? 1 : Tx <= 128 ? 2 : Tx <= 256 ? 4 : Tx <= 512 ? 8 : 16;
+    w.K = Tx <= 64 ? 1 : Tx <= 128 ? 2 : Tx <= 256 ? 4 : Tx <= 512 ? 8 : Tx <= 1024 ? 16 : 32;
     w.Txp = kWave * w.K;
     w.nch = (Ty + 31) / 32;
     w.lds_bits = (size_t)w.Txp * w.nch * 4 <= (size_t)kLdsBitsLimit;
@@ -598,14 +598,15 @@ int launch_dp(MasArgs a, int B, const WsLayout &w, bool vec, bool dp_out, hipStr
         case 2: return launch_dp_kc<2, 16>(a, B, vec, w.lds_bits, dp_out, shmem, st);
         case 4: return launch_dp_kc<4, 8>(a, B, vec, w.lds_bits, dp_out, shmem, st);
         case 8: return launch_dp_kc<8, 4>(a, B, vec, w.lds_bits, dp_out, shmem, st);
-        default: return launch_dp_kc<16, 2>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+        case 16: return launch_dp_kc<16, 2>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+        default: return launch_dp_kc<32, 1>(a, B, vec, w.lds_bits, dp_out, shmem, st);  // Tx <= 2048
     }
 }
 
 int check_shape(int B, int Tx, int Ty) {
     if (B < 0 || Tx < 1 || Ty < 1) return mtts::fail(MTTS_ERR_INVALID_ARG, "maximum_path: bad shape");
     if (Tx > MTTS_MAS_MAX_TX)
-        return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: Tx > MTTS_MAS_MAX_TX (1024) is not supported");
+        return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: Tx > MTTS_MAS_MAX_TX (2048) is not supported");
     if ((int64_t)Tx * Ty * 4 >= (int64_t)1 << 31)
         return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: one utterance's lattice exceeds 2 GiB");
     return MTTS_OK;

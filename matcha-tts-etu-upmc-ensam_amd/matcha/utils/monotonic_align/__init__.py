@@ -17,7 +17,7 @@ from matcha import _native as N
 
 
 def _check_tx(Tx: int) -> None:
-    """The DP keeps one utterance's text rows in one wave (16 rows per lane at most): t_x <= 1024.
+    """The DP keeps one utterance's text rows in one wave (32 rows per lane at most): t_x <= 2048.
     The reference Cython (core.pyx:14-96) has no cap; LJSpeech tops out near 190 tokens and
     BASELINE config 5 uses 512, so the limit is a documented shape error, not a silent truncation."""
     if Tx > N.MTTS_MAS_MAX_TX:

@@ -60,6 +60,34 @@ with torch.cuda.graph(gf):
     junk.fill_(1.0)
 fill = replay_us(gf)
 print(f"512 MB fill alone: {fill:.1f} us", flush=True)
+def torch_graph():
+    """the same forward + backward as torch ops (fp32; hipBLASLt GEMMs + elementwise), as a captured graph"""
+    import torch.nn.functional as F
+
+    for q in list(mlp.parameters()) + [q for lin in projs for q in lin.parameters()]:
+        q.grad = None
+
+    def run():
+        temb = mlp(e)
+        a2 = F.mish(temb)
+        w_all = torch.cat([lin.weight for lin in projs])
+        b_all = torch.cat([lin.bias for lin in projs])
+        tps = F.linear(a2, w_all, b_all).split(256, dim=1)
+        torch.autograd.backward(tps, w)
+
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        for _ in range(2):
+            run()
+    torch.cuda.current_stream().wait_stream(st)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        run()
+    return g
+
+
+print(f"torch ops (hipBLASLt): time MLP fwd+bwd graph replay {replay_us(torch_graph()):7.1f} us", flush=True)
 for passes in ("1", "2", "4", "6"):
     for dirty in (False, True):
         t = replay_us(graph_of(dirty, passes))
