@@ -50,14 +50,24 @@ __global__ __launch_bounds__(kThreads) void adamw_sumsq_kernel(const mtts_adamw_
     __shared__ float red[kThreads / 64];
     if (blockIdx.x == 0 && threadIdx.x == 0) t_next[0] = step[0] + 1.f;
     const mtts_adamw_chunk c = chunks[blockIdx.x];
+    // The summation order depends on the chunk's values only, never on where its gradient lives: the
+    // data-parallel step keeps gradients in bucket views whose alignment differs from the allocator's,
+    // and both must clip with the same norm bit for bit.  Thread t sums groups of 4 (t, t + 256, ...);
+    // an unaligned or ragged group is loaded element-wise with zeros past the end.
     float s = 0.f;
     const bool vec = ((uintptr_t)c.grad & 15) == 0;
-    const int n4 = vec ? c.n / 4 : 0;
-    for (int i = threadIdx.x; i < n4; i += kThreads) {
-        const float4 g = reinterpret_cast<const float4 *>(c.grad)[i];
+    const int ng = (c.n + 3) / 4;
+    for (int i = threadIdx.x; i < ng; i += kThreads) {
+        float4 g;
+        if (vec && 4 * i + 4 <= c.n) {
+            g = reinterpret_cast<const float4 *>(c.grad)[i];
+        } else {
+            const float *q = c.grad + 4 * i;
+            const int r = c.n - 4 * i;
+            g = make_float4(q[0], r > 1 ? q[1] : 0.f, r > 2 ? q[2] : 0.f, r > 3 ? q[3] : 0.f);
+        }
         s += (g.x * g.x + g.y * g.y) + (g.z * g.z + g.w * g.w);
     }
-    for (int i = 4 * n4 + threadIdx.x; i < c.n; i += kThreads) s += c.grad[i] * c.grad[i];
     s = block_reduce_sum(s, red);
     if (threadIdx.x == 0) partial[blockIdx.x] = s;
 }

@@ -25,8 +25,17 @@ struct JobBatch {
 };
 
 template <bool BF16>
+__device__ __forceinline__ void pack_tiles(const mtts_pack_job &j, float (*tile)[65]);
+__host__ __device__ inline bool tiled_job(const mtts_pack_job &j);
+
+template <bool BF16>
 __global__ __launch_bounds__(kThreads) void pack_kernel(JobBatch jb) {
     const mtts_pack_job &j = jb.job[blockIdx.y];
+    if (tiled_job(j)) {  // job-uniform branch
+        __shared__ float tile[32][65];
+        pack_tiles<BF16>(j, tile);
+        return;
+    }
     const int groups = j.Kp / 8;
     const long total = (long)j.rows * groups;
     const int K = j.C * j.ntaps;
@@ -63,6 +72,61 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(JobBatch jb) {
             d[1] = make_float4(e[4], e[5], e[6], e[7]);
         }
     }
+}
+
+// Transposing jobs (sc > sr: a dgrad layout gathers a weight COLUMN per destination row, e.g. the linear
+// dgrad's sc = K) read one 4-byte element per 8 destination elements from lines they barely use.  Tiled
+// here: 32 destination rows x 64 c of one tap are read with the destination ROW fastest across threads
+// (src stride sr: 1 or k), transposed through LDS, and written as 16-byte row segments.  C % 8 == 0
+// (every 8-element group lies inside one tap), Kp == C * ntaps (no padding to zero), 16-byte aligned dst.
+constexpr int kTR = 32, kTC = 64;
+
+template <bool BF16>
+__device__ __forceinline__ void pack_tiles(const mtts_pack_job &j, float (*tile)[kTC + 1]) {
+    const int rt = (j.rows + kTR - 1) / kTR, ct = (j.C + kTC - 1) / kTC;
+    const long ntile = (long)rt * ct * j.ntaps;
+    const int tid = threadIdx.x;
+    for (long t = blockIdx.x; t < ntile; t += gridDim.x) {
+        const int tap = (int)(t / ((long)rt * ct)), rem = (int)(t - (long)tap * rt * ct);
+        const int r0 = (rem / ct) * kTR, c0 = (rem % ct) * kTC;
+        const float *src = j.src + (int64_t)(j.j0 + tap * j.js) * j.sj;
+        __syncthreads();  // the previous tile's LDS reads are done
+#pragma unroll
+        for (int i = 0; i < kTR * kTC / kThreads; ++i) {  // load: destination row fastest (src stride sr)
+            const int e = tid + kThreads * i, rr = e % kTR, cc = e / kTR;
+            const int r = r0 + rr, c = c0 + cc;
+            tile[rr][cc] = (r < j.rows && c < j.C) ? src[(int64_t)r * j.sr + (int64_t)c * j.sc] : 0.f;
+        }
+        __syncthreads();
+        const int rr = tid / (kTC / 8), g = tid % (kTC / 8);  // 32 rows x 8 groups of 8 = 256 threads
+        const int r = r0 + rr, c = c0 + 8 * g;
+        if (r >= j.rows || c >= j.C) continue;
+        float e[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) e[q] = tile[rr][8 * g + q];
+        const size_t off = (size_t)r * j.ld + (size_t)tap * j.C + c;
+        if constexpr (BF16) {
+            uint32_t w[4], l[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const __bf16 h0 = (__bf16)e[2 * q], h1 = (__bf16)e[2 * q + 1];
+                w[q] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+                const __bf16 l0 = (__bf16)(e[2 * q] - (float)h0), l1 = (__bf16)(e[2 * q + 1] - (float)h1);
+                l[q] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+            }
+            uint16_t *d = static_cast<uint16_t *>(j.dst) + off;
+            *reinterpret_cast<uint4 *>(d) = make_uint4(w[0], w[1], w[2], w[3]);
+            if (j.lo_off > 0) *reinterpret_cast<uint4 *>(d + j.lo_off) = make_uint4(l[0], l[1], l[2], l[3]);
+        } else {
+            float4 *d = reinterpret_cast<float4 *>(static_cast<float *>(j.dst) + off);
+            d[0] = make_float4(e[0], e[1], e[2], e[3]);
+            d[1] = make_float4(e[4], e[5], e[6], e[7]);
+        }
+    }
+}
+
+__host__ __device__ inline bool tiled_job(const mtts_pack_job &j) {
+    return j.sc > j.sr && j.C % 8 == 0 && j.Kp == j.C * j.ntaps && ((uintptr_t)j.dst & 15) == 0;
 }
 
 }  // namespace

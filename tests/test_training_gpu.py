@@ -184,6 +184,33 @@ def test_clip_adamw_matches_torch(grad_scale):
         torch.testing.assert_close(v_hip, v_ref, rtol=1e-6, atol=4 * torch.finfo(torch.float32).eps * v_ref.abs().max().item())
 
 
+def test_clip_norm_independent_of_gradient_alignment():
+    """The clipped step is bit-identical whether the gradients are allocator-aligned tensors or
+    unaligned views into one buffer (the data-parallel step's buckets): the norm's summation order
+    depends on the values only (csrc/optim.hip adamw_sumsq_kernel)."""
+    from matcha.training import _FlatClipAdamW
+
+    g = torch.Generator().manual_seed(9)
+    shapes = [(192, 80, 3), (5,), (1001,), (7, 5), (1,), (33, 3)]
+    init = [torch.randn(s, generator=g) for s in shapes]
+    grads = [torch.randn(s, generator=g) * 3.0 for s in shapes]  # norm well above 1: clipping active
+    out = []
+    for shift in (0, 1, 3):
+        ps = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+        opt = _FlatClipAdamW(ps, torch.tensor(1e-4, device=DEV, dtype=torch.float64), 1.0)
+        buf = torch.zeros(sum(x.numel() for x in grads) + 8, device=DEV)
+        off = shift
+        for p, gr in zip(ps, grads):
+            view = buf[off:off + gr.numel()].view_as(gr)
+            view.copy_(gr.to(DEV))
+            p.grad = view if shift else gr.to(DEV).clone()
+            off += gr.numel()
+        opt.step()
+        torch.cuda.synchronize()
+        out.append(opt.flat.clone())
+    assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])
+
+
 def _inject(m, t, z):
     m.decoder.compute_loss_and_prior = (lambda f: (lambda *a, **k: f(*a, **{**k, "t": t, "z": z})))(
         m.decoder.compute_loss_and_prior)
