@@ -20,15 +20,19 @@ for fam, rx in REGEX.items():
         vals = {}
         for r in csv.DictReader(open(files[0])):
             if r["Counter_Name"] == counter:
-                vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-        tot[counter] = (sum(vals.values()), len(vals))
+                d = int(r["Dispatch_Id"])
+                vals[d] = vals.get(d, 0.0) + float(r["Counter_Value"])
+        # the profiled program also runs the warm-up pass (same dispatches as each logged pass): drop it
+        ids = sorted(vals)
+        warm = len(ids) * algo.get("warmup_passes", 1) // (algo["passes"] + algo.get("warmup_passes", 1))
+        tot[counter] = (sum(vals[d] for d in ids[warm:]), len(ids) - warm)
     n = algo[fam]["launches"]
     fetch_b = 2.0 * 1024 * tot["FETCH_SIZE"][0] / n
     write_b = 1024 * tot["WRITE_SIZE"][0] / n
     algo_b = algo[fam]["algorithmic_bytes"] / n
     out = {"family": fam, "kernels_regex": rx,
            "workload": "tools/r3/pmc_families.py: two eager bf16 fwd+bwd passes of the bench batch (B=32, 120x600)",
-           "launches": n, "dispatches": tot["FETCH_SIZE"][1], "fetch_bytes_per_launch": round(fetch_b),
+           "launches": n, "dispatches": tot["FETCH_SIZE"][1], "warmup_dispatches_dropped": True, "fetch_bytes_per_launch": round(fetch_b),
            "write_bytes_per_launch": round(write_b), "traffic_bytes_per_launch": round(fetch_b + write_b),
            "algorithmic_bytes_per_launch": round(algo_b), "traffic_over_algorithmic": round((fetch_b + write_b) / algo_b, 3),
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes with --kernel-include-regex; "
