@@ -143,6 +143,12 @@ int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precision, float *
 int mtts_conv_wgrad_tile(const mtts_conv_wgrad_args *args, int32_t precision, int32_t rows_per_step,
                          int32_t target_blocks, int32_t depth, float *dw, int64_t sn, int64_t sc, int64_t sj,
                          float *db, int32_t accumulate, void *workspace, size_t workspace_bytes, void *hip_stream);
+/* Inside the reduction deferral (mtts_defer_reductions below) the weight-gradient GEMMs are queued too
+ * (unless MTTS_DEFER_WGRAD=0) and mtts_flush_reductions launches them batched -- up to 12 per launch, each
+ * with its own row split -- before their sums; a queued gradient takes a split plan with fewer, longer
+ * splits (the batch fills the chip).  mode 0: that plan for queued gradients only (default); 1: for every
+ * call (an immediate call then equals a queued one bitwise); 2: the per-launch plan for every call. */
+void mtts_wgrad_plan_mode(int32_t mode);
 
 /*
  * y[b,t,c] = mish(GN(h)[b,t,c]) * mask[b,t] + add[b,c]      (mask / add optional)

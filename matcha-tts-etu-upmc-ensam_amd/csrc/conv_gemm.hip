@@ -25,7 +25,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 
 #include <cstdint>
 
@@ -391,9 +394,32 @@ struct WgradGeom {
 // 128 x 128 tile (own LDS rings, one shared barrier sequence: both halves run the same step count, rows
 // past their range masked), then add (half 0 + half 1, fixed order) before ONE slab write: the same waves
 // per CU as twice the workgroups, half the partial slabs that the step's batched reduce re-reads.
+// Batched launch: up to kWgradBatch independent weight gradients of the same kernel instantiation in one
+// grid (the blocks of job j are [first[j], first[j+1]); each job keeps its own row split, so a job's
+// partial slabs are bitwise those of its own launch).  The backward's queued weight gradients run this
+// way (mtts::flush_wgrads) instead of one latency-bound launch per layer; a lone call is a batch of one.
+struct WgradJobK {
+    mtts_conv_wgrad_args a;
+    float *part, *part_db;  // the job's slabs [splits][N][K] and bias partials [splits][N] (or null)
+    int32_t rps;            // token rows per split
+    int32_t pad_;
+};
+constexpr int kWgradBatch = 12;  // ~1.7 KiB of kernel arguments
+struct WgradBatch {
+    WgradJobK job[kWgradBatch];
+    int32_t first[kWgradBatch + 1];
+    int32_t njobs;
+};
+
 template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false, bool LIN = false, int HV = 1>
-__global__ __launch_bounds__(kThreads * HV) void conv_wgrad_kernel(mtts_conv_wgrad_args p, int rows_per_split,
-                                                                    float *__restrict__ part, float *__restrict__ part_db) {
+__global__ __launch_bounds__(kThreads * HV) void conv_wgrad_kernel(const WgradBatch wb) {
+    int jb = 0;  // this block's job (block-uniform scan over the batch's first-block table)
+    while (jb + 1 < wb.njobs && (int)blockIdx.x >= wb.first[jb + 1]) ++jb;
+    const mtts_conv_wgrad_args &p = wb.job[jb].a;
+    const int rows_per_split = wb.job[jb].rps;
+    float *__restrict__ part = wb.job[jb].part;
+    float *__restrict__ part_db = wb.job[jb].part_db;
+    const int blk = (int)blockIdx.x - wb.first[jb], nblk = wb.first[jb + 1] - wb.first[jb];
     static_assert(HV == 1 || (HV == 2 && DEPTH == 1), "two halves: one step in flight");
     static_assert(HV == 1 || (size_t)64 * kThreads * sizeof(float) <= 2 * WgradGeom<BF16, KB>::kLds,
                   "half 1's accumulators fit the two halves' LDS");
@@ -418,7 +444,7 @@ __global__ __launch_bounds__(kThreads * HV) void conv_wgrad_kernel(mtts_conv_wgr
     int n0, k0, split, ktile;
     {
         const int ntn = (p.N + T - 1) / T, ntk = (p.K + T - 1) / T;
-        const int nwg = gridDim.x, orig = blockIdx.x;
+        const int nwg = nblk, orig = blk;  // the job's own block numbering (its launch alone: the grid's)
         const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
         const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
         split = wgid / (ntn * ntk);
@@ -1067,8 +1093,12 @@ extern "C" int mtts_act_dropout_bwd_scaled(const float *dy, const float *y, cons
 constexpr int kWgradMaxTarget = 1024;
 // target_blocks < 0: the sweep's rule (tools/wgrad_sweep.py) -- about 768 rows per split (long enough
 // to amortize the pipeline and the split's slab write) but never fewer than min_blocks (below).
+// batched: the job is queued for a batched launch (mtts::flush_wgrads) whose other jobs fill the chip
+// beside it, so it takes fewer, longer splits -- fewer N x K slabs to write and sum (step sweep with the
+// whole backward's weight gradients batched at its end, same box: min blocks 384/512 + 768 rows 7.62 ms,
+// 256/256 7.41, 128/128 + 768 rows 7.36, 128/128 + 1536 rows 7.34, 64/64 + 3072 rows 7.58).
 static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks, int *splits, int *rows_per_split,
-                       int hv = 1) {
+                       int hv = 1, bool batched = false) {
     const int M = p.nb * p.To;
     const int tiles = ((p.N + 127) / 128) * ((p.K + 127) / 128);
     // More blocks keep more row steps in flight per CU (the kernel is latency-bound) but every split adds
@@ -1080,12 +1110,17 @@ static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks,
     static const int min_blocks = [] { const char *e = getenv("MTTS_WGRAD_MINBLK"); return e ? atoi(e) : 384; }();
     static const int min_blocks16 = [] { const char *e = getenv("MTTS_WGRAD_MINBLK16"); return e ? atoi(e) : 512; }();
     static const int split_rows = [] { const char *e = getenv("MTTS_WGRAD_ROWS"); return e && atoi(e) > 0 ? atoi(e) : 768; }();
+    static const int b_min_blocks = [] { const char *e = getenv("MTTS_WGRAD_BMINBLK"); return e ? atoi(e) : 128; }();
+    static const int b_split_rows = [] { const char *e = getenv("MTTS_WGRAD_BROWS"); return e && atoi(e) > 0 ? atoi(e) : 1536; }();
     // hv = 2: two-half workgroups (twice the waves each): half the workgroups, rows in whole double steps
-    const int mb = ((p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_WGRAD_F_DY_BF16)) ? min_blocks16 : min_blocks) / hv;
+    const int mb = (batched ? b_min_blocks
+                            : (p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_WGRAD_F_DY_BF16)) ? min_blocks16 : min_blocks) / hv;
+    const int rows = batched ? b_split_rows : split_rows;
     kb *= hv;
     int s = target_blocks > 0 ? (target_blocks + tiles - 1) / tiles
-                              : max((mb + tiles - 1) / tiles, (M + split_rows / 2) / split_rows);
-    s = max(1, min(s, (M + 4 * kb - 1) / (4 * kb)));  // at least 4 steps per split
+                              : max((mb + tiles - 1) / tiles, (M + rows / 2) / rows);
+    static const int min_steps = [] { const char *e = getenv("MTTS_WGRAD_MINSTEPS"); return e && atoi(e) > 0 ? atoi(e) : 4; }();
+    s = max(1, min(s, (M + min_steps * kb - 1) / (min_steps * kb)));  // at least min_steps steps per split
     int rps = (M + s - 1) / s;
     rps = (rps + kb - 1) / kb * kb;
     *rows_per_split = max(rps, kb);
@@ -1099,12 +1134,13 @@ extern "C" size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *arg
     wgrad_plan(*args, 32, kWgradMaxTarget, &splits, &rps);
     wgrad_plan(*args, 32, -1, &s2, &r2);
     splits = max(splits, s2);
+    wgrad_plan(*args, 32, -1, &s2, &r2, 1, true);
+    splits = max(splits, s2);
     return mtts::align_up((size_t)splits * args->N * args->K * 4, 256) + (size_t)splits * args->N * 4 + 256;
 }
 
 template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false, bool LIN = false, int HV = 1>
-static int wgrad_launch_hv(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
-                           hipStream_t st) {
+static int wgrad_launch_hv(const WgradBatch &wb, hipStream_t st) {
     using Gm = WgradGeom<BF16, KB>;
     constexpr size_t lds = Gm::kLds * HV;
     static bool attr_set = false;
@@ -1114,9 +1150,8 @@ static int wgrad_launch_hv(const mtts_conv_wgrad_args &p, int splits, int rps, f
             return mtts::fail(MTTS_ERR_HIP, "conv_wgrad: LDS attribute");
         attr_set = true;
     }
-    dim3 grid((unsigned)(((p.N + 127) / 128) * ((p.K + 127) / 128) * splits));
-    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN, HV>), grid, dim3(kThreads * HV), lds,
-                       st, p, rps, part, part_db);
+    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN, HV>), dim3((unsigned)wb.first[wb.njobs]),
+                       dim3(kThreads * HV), lds, st, wb);
     return mtts::check_launch("conv_wgrad_kernel");
 }
 
@@ -1127,14 +1162,11 @@ static int wgrad_hv() {
 }
 
 template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false, bool LIN = false>
-static int wgrad_launch_k(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
-                          hipStream_t st) {
+static int wgrad_launch_k(const WgradBatch &wb, bool hv2, hipStream_t st) {
     if constexpr (KB == 32 && DEPTH == 1) {
-        // (any split of whole double steps is exact with two halves; the plan makes them so when hv = 2)
-        if (wgrad_hv() == 2 && rps % (2 * KB) == 0)
-            return wgrad_launch_hv<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN, 2>(p, splits, rps, part, part_db, st);
+        if (hv2) return wgrad_launch_hv<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN, 2>(wb, st);
     }
-    return wgrad_launch_hv<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN, 1>(p, splits, rps, part, part_db, st);
+    return wgrad_launch_hv<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN, 1>(wb, st);
 }
 
 // The linear row walk (LIN): every row's dY / A rows follow from the token row index alone.
@@ -1152,29 +1184,114 @@ static bool wgrad_inc_ok(const mtts_conv_wgrad_args &p, int kb) {
            p.in_stride >= 1;
 }
 
+// Everything the instantiation choice below depends on: jobs with equal keys run the same kernel and can
+// share one batched launch.
+struct WgradKey {
+    bool bf16, a16, y16, inc, lin, hv2;
+    int kb, depth;
+    bool operator==(const WgradKey &o) const {
+        return bf16 == o.bf16 && a16 == o.a16 && y16 == o.y16 && inc == o.inc && lin == o.lin && hv2 == o.hv2 &&
+               kb == o.kb && depth == o.depth;
+    }
+};
+
+static WgradKey wgrad_key(const mtts_conv_wgrad_args &p, bool bf16, int kb, int depth, int rps) {
+    WgradKey k;
+    k.bf16 = bf16;
+    k.kb = bf16 ? kb : 32;
+    k.depth = bf16 ? depth : 1;
+    k.a16 = (p.flags & MTTS_GEMM_F_A_BF16) != 0;
+    k.y16 = (p.flags & MTTS_WGRAD_F_DY_BF16) != 0;
+    k.inc = wgrad_inc_ok(p, k.kb);
+    k.lin = k.bf16 && k.kb == 32 && k.depth == 1 && k.inc && k.a16 && !k.y16 && wgrad_lin_ok(p);
+    // (any split of whole double steps is exact with two halves; the plan makes them so when hv = 2)
+    k.hv2 = k.kb == 32 && k.depth == 1 && wgrad_hv() == 2 && rps % (2 * k.kb) == 0;
+    return k;
+}
+
 template <bool BF16, int KB, int DEPTH>
-static int wgrad_launch(const mtts_conv_wgrad_args &p, int splits, int rps, float *part, float *part_db,
-                        hipStream_t st) {
+static int wgrad_launch(const WgradBatch &wb, const WgradKey &k, hipStream_t st) {
     if constexpr (BF16 && (KB == 32 || KB == 64) && DEPTH == 1) {
-        const bool a16 = p.flags & MTTS_GEMM_F_A_BF16, y16 = p.flags & MTTS_WGRAD_F_DY_BF16, inc = wgrad_inc_ok(p, KB);
         // the linear walk measured faster only with a bf16 A and an fp32 dY (19200-row conv: 44.4 vs 48.0 us;
         // fp32 / fp32 42.7 vs 42.9, bf16 dY 48.1 vs 42.9: tools/wgrad_store_ab.py) -- the staging's VALU is
         // not what bounds the other storages
-        if (KB == 32 && inc && a16 && !y16 && wgrad_lin_ok(p))
-            return wgrad_launch_k<true, 32, 1, true, true, false, true>(p, splits, rps, part, part_db, st);
-        if (a16 && y16)
-            return inc ? wgrad_launch_k<true, KB, 1, true, true, true>(p, splits, rps, part, part_db, st)
-                       : wgrad_launch_k<true, KB, 1, false, true, true>(p, splits, rps, part, part_db, st);
-        if (y16)
-            return inc ? wgrad_launch_k<true, KB, 1, true, false, true>(p, splits, rps, part, part_db, st)
-                       : wgrad_launch_k<true, KB, 1, false, false, true>(p, splits, rps, part, part_db, st);
-        if (a16)
-            return inc ? wgrad_launch_k<true, KB, 1, true, true>(p, splits, rps, part, part_db, st)
-                       : wgrad_launch_k<true, KB, 1, false, true>(p, splits, rps, part, part_db, st);
+        if (KB == 32 && k.lin) return wgrad_launch_k<true, 32, 1, true, true, false, true>(wb, k.hv2, st);
+        if (k.a16 && k.y16)
+            return k.inc ? wgrad_launch_k<true, KB, 1, true, true, true>(wb, k.hv2, st)
+                         : wgrad_launch_k<true, KB, 1, false, true, true>(wb, k.hv2, st);
+        if (k.y16)
+            return k.inc ? wgrad_launch_k<true, KB, 1, true, false, true>(wb, k.hv2, st)
+                         : wgrad_launch_k<true, KB, 1, false, false, true>(wb, k.hv2, st);
+        if (k.a16)
+            return k.inc ? wgrad_launch_k<true, KB, 1, true, true>(wb, k.hv2, st)
+                         : wgrad_launch_k<true, KB, 1, false, true>(wb, k.hv2, st);
     }
-    return wgrad_inc_ok(p, KB) ? wgrad_launch_k<BF16, KB, DEPTH, true>(p, splits, rps, part, part_db, st)
-                               : wgrad_launch_k<BF16, KB, DEPTH, false>(p, splits, rps, part, part_db, st);
+    return k.inc ? wgrad_launch_k<BF16, KB, DEPTH, true>(wb, k.hv2, st)
+                 : wgrad_launch_k<BF16, KB, DEPTH, false>(wb, k.hv2, st);
 }
+
+static int wgrad_launch_key(const WgradBatch &wb, const WgradKey &k, hipStream_t st) {
+    if (!k.bf16) return wgrad_launch<false, 32, 1>(wb, k, st);
+    if (k.kb == 64) return k.depth == 2 ? wgrad_launch<true, 64, 2>(wb, k, st) : wgrad_launch<true, 64, 1>(wb, k, st);
+    return k.depth == 2 ? wgrad_launch<true, 32, 2>(wb, k, st) : wgrad_launch<true, 32, 1>(wb, k, st);
+}
+
+// One planned weight gradient: the kernel-side job, its instantiation key and where its slabs go.
+struct WgradPlanned {
+    WgradJobK k;
+    WgradKey key;
+    int splits;
+    float *dw;
+    int64_t sn, sc, sj;
+    float *db;
+    int accumulate;
+};
+
+// the fixed-order sums of a planned job's slabs (reduce.hip) -> dw (and db)
+static int wgrad_reduce_jobs(const WgradPlanned &w, mtts_reduce_job jobs[2]) {
+    const mtts_conv_wgrad_args &p = w.k.a;
+    const int64_t NK = (int64_t)p.N * p.K;
+    jobs[0] = mtts_reduce_job{};
+    jobs[0].part = w.k.part;
+    jobs[0].out = w.dw;
+    jobs[0].stride = NK;
+    jobs[0].n = NK;
+    jobs[0].splits = w.splits;
+    jobs[0].accumulate = w.accumulate;
+    jobs[0].cols = p.K;
+    jobs[0].cin = p.cin;
+    jobs[0].sr = w.sn;
+    jobs[0].sc = w.sc;
+    jobs[0].sj = w.sj;
+    if (!w.db) return 1;
+    jobs[1] = mtts_reduce_job{};
+    jobs[1].part = w.k.part_db;
+    jobs[1].out = w.db;
+    jobs[1].stride = p.N;
+    jobs[1].n = p.N;
+    jobs[1].splits = w.splits;
+    jobs[1].accumulate = w.accumulate;
+    return 2;
+}
+
+static int wgrad_blocks(const WgradPlanned &w) {
+    const mtts_conv_wgrad_args &p = w.k.a;
+    return ((p.N + 127) / 128) * ((p.K + 127) / 128) * w.splits;
+}
+
+// Deferred weight gradients (between mtts_defer_reductions(1) and the next flush, MTTS_DEFER_WGRAD != 0):
+// queued here and launched batched by mtts::flush_wgrads, which mtts_flush_reductions calls first.
+std::mutex g_wq_mu;
+std::vector<WgradPlanned> g_wq;
+
+static bool defer_wgrads() {
+    static const bool on = [] { const char *e = getenv("MTTS_DEFER_WGRAD"); return !(e && e[0] == '0'); }();
+    return on && mtts::deferring();
+}
+
+// mtts_wgrad_plan_mode: 0 = the batched split plan for queued gradients, the per-launch one otherwise;
+// 1 / 2 = always the batched / per-launch plan (tests: a queued and an immediate gradient bitwise equal)
+std::atomic<int> g_wgrad_plan_mode{0};
 
 // rows_per_step: 32 or 64 (bf16 only), -1 = default; target_blocks: 64..1024, -1 = default;
 // depth: row steps in flight, 1 or 2 (bf16 only), -1 = default
@@ -1206,49 +1323,103 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
     int splits, rps;
     // the two-half workgroups serve the register-staged KB = 32, one-step schedules
     const int hv = (wgrad_hv() == 2 && rows_per_step == 32 && depth == 1) ? 2 : 1;
-    wgrad_plan(p, rows_per_step, target_blocks, &splits, &rps, hv);
-    float *part = static_cast<float *>(workspace);
-    float *part_db = reinterpret_cast<float *>(static_cast<char *>(workspace) +
-                                               mtts::align_up((size_t)splits * p.N * p.K * 4, 256));
+    const bool queue = p.nb * p.To > 0 && defer_wgrads();
+    const int pm = g_wgrad_plan_mode.load();
+    wgrad_plan(p, rows_per_step, target_blocks, &splits, &rps, hv, pm == 1 || (pm == 0 && queue));
+    WgradPlanned w;
+    w.k.a = p;
+    w.k.part = static_cast<float *>(workspace);
+    w.k.part_db = db ? reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                                 mtts::align_up((size_t)splits * p.N * p.K * 4, 256))
+                     : nullptr;
+    w.k.rps = rps;
+    w.k.pad_ = 0;
+    w.key = wgrad_key(p, bf16, rows_per_step, depth, rps);
+    w.splits = splits;
+    w.dw = dw;
+    w.sn = sn;
+    w.sc = sc;
+    w.sj = sj;
+    w.db = db;
+    w.accumulate = accumulate;
     const int M = p.nb * p.To;
     if (M == 0) {
-        if (hipMemsetAsync(part, 0, (size_t)p.N * p.K * 4, st) != hipSuccess ||
+        float *part_db = reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                                   mtts::align_up((size_t)splits * p.N * p.K * 4, 256));
+        if (hipMemsetAsync(w.k.part, 0, (size_t)p.N * p.K * 4, st) != hipSuccess ||
             hipMemsetAsync(part_db, 0, (size_t)p.N * 4, st) != hipSuccess)
             return mtts::fail(MTTS_ERR_HIP, "conv_wgrad: memset failed");
-        splits = 1;
+        w.splits = 1;
+        w.k.part_db = db ? part_db : nullptr;
+    } else if (queue) {
+        std::lock_guard<std::mutex> lk(g_wq_mu);
+        g_wq.push_back(w);
+        return MTTS_OK;
     } else {
-        float *pdb = db ? part_db : nullptr;
-        rc = !bf16 ? wgrad_launch<false, 32, 1>(p, splits, rps, part, pdb, st)
-             : rows_per_step == 64 ? (depth == 2 ? wgrad_launch<true, 64, 2>(p, splits, rps, part, pdb, st)
-                                                 : wgrad_launch<true, 64, 1>(p, splits, rps, part, pdb, st))
-                                   : (depth == 2 ? wgrad_launch<true, 32, 2>(p, splits, rps, part, pdb, st)
-                                                 : wgrad_launch<true, 32, 1>(p, splits, rps, part, pdb, st));
-        if (rc) return rc;
+        WgradBatch wb;
+        wb.job[0] = w.k;
+        wb.first[0] = 0;
+        wb.first[1] = wgrad_blocks(w);
+        wb.njobs = 1;
+        if ((rc = wgrad_launch_key(wb, w.key, st))) return rc;
     }
     // sum of the split slabs (reduce.hip: now, or queued for the step's batched launch)
-    const int64_t NK = (int64_t)p.N * p.K;
-    mtts_reduce_job jobs[2] = {};
-    jobs[0].part = part;
-    jobs[0].out = dw;
-    jobs[0].stride = NK;
-    jobs[0].n = NK;
-    jobs[0].splits = splits;
-    jobs[0].accumulate = accumulate;
-    jobs[0].cols = p.K;
-    jobs[0].cin = p.cin;
-    jobs[0].sr = sn;
-    jobs[0].sc = sc;
-    jobs[0].sj = sj;
-    if (db) {
-        jobs[1].part = part_db;
-        jobs[1].out = db;
-        jobs[1].stride = p.N;
-        jobs[1].n = p.N;
-        jobs[1].splits = splits;
-        jobs[1].accumulate = accumulate;
-    }
-    return mtts::submit_reductions(jobs, db ? 2 : 1, st);
+    mtts_reduce_job jobs[2];
+    const int nj = wgrad_reduce_jobs(w, jobs);
+    return mtts::submit_reductions(jobs, nj, st);
 }
+
+namespace mtts {
+// The queued weight gradients, batched by instantiation (queue order kept within a batch), then their
+// slab sums appended to the reduction queue (mtts_flush_reductions launches that right after).
+int flush_wgrads(hipStream_t st) {
+    std::vector<WgradPlanned> q;
+    {
+        std::lock_guard<std::mutex> lk(g_wq_mu);
+        q.swap(g_wq);
+    }
+    std::vector<char> done(q.size(), 0);
+    for (size_t i = 0; i < q.size(); ++i) {
+        if (done[i]) continue;
+        WgradBatch wb;
+        wb.njobs = 0;
+        wb.first[0] = 0;
+        for (size_t j = i; j < q.size(); ++j) {
+            if (done[j] || !(q[j].key == q[i].key)) continue;
+            done[j] = 1;
+            wb.job[wb.njobs] = q[j].k;
+            wb.first[wb.njobs + 1] = wb.first[wb.njobs] + wgrad_blocks(q[j]);
+            if (++wb.njobs == kWgradBatch) {
+                if (int rc = wgrad_launch_key(wb, q[i].key, st)) return rc;
+                wb.njobs = 0;
+            }
+        }
+        if (wb.njobs > 0)
+            if (int rc = wgrad_launch_key(wb, q[i].key, st)) return rc;
+    }
+    std::vector<mtts_reduce_job> jobs;
+    for (const WgradPlanned &w : q) {
+        mtts_reduce_job j2[2];
+        const int n = wgrad_reduce_jobs(w, j2);
+        jobs.insert(jobs.end(), j2, j2 + n);
+    }
+    return queue_reductions(jobs.data(), (int)jobs.size());
+}
+
+int pending_wgrad_sums() {
+    std::lock_guard<std::mutex> lk(g_wq_mu);
+    int n = 0;
+    for (const WgradPlanned &w : g_wq) n += w.db ? 2 : 1;
+    return n;
+}
+
+void discard_wgrads() {
+    std::lock_guard<std::mutex> lk(g_wq_mu);
+    g_wq.clear();
+}
+}  // namespace mtts
+
+extern "C" void mtts_wgrad_plan_mode(int32_t mode) { g_wgrad_plan_mode.store(mode >= 0 && mode <= 2 ? mode : 0); }
 
 extern "C" int mtts_conv_wgrad(const mtts_conv_wgrad_args *args, int32_t precision, float *dw, int64_t sn,
                                int64_t sc, int64_t sj, float *db, int32_t accumulate, void *workspace,

@@ -114,14 +114,19 @@ int conv_gemm_glds_launch(int id, const mtts_conv_gemm_args &p, int M, int split
 size_t conv_gemm_glds_splitk_bytes(const mtts_conv_gemm_args &p, int splits);
 }  // namespace mtts
 
-struct mtts_conv_wgrad_args;
-namespace mtts {
-}  // namespace mtts
-
 struct mtts_reduce_job;
 namespace mtts {
 // reduce.hip: runs the partial-sum jobs now, or queues them while deferral is on
 int submit_reductions(const mtts_reduce_job *jobs, int njobs, hipStream_t st);
+// reduce.hip: appends jobs to the deferred queue whatever the deferral state (the next flush runs them)
+int queue_reductions(const mtts_reduce_job *jobs, int njobs);
+// reduce.hip: deferral currently on (mtts_defer_reductions)
+bool deferring();
+// conv_gemm.hip: the deferred weight gradients -- launched batched (their slab sums then queued), counted
+// as the slab sums they will add, dropped
+int flush_wgrads(hipStream_t st);
+int pending_wgrad_sums();
+void discard_wgrads();
 }  // namespace mtts
 
 #define MTTS_CHECK_ARG(cond, msg)                                   \

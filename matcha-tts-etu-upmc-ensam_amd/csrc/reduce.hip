@@ -16,7 +16,8 @@
 //
 // Deferral (mtts_defer_reductions) queues the jobs of a whole backward pass and mtts_flush_reductions
 // runs them in one batched launch; the queue is process-wide because autograd calls the backward
-// entry points from its own thread.
+// entry points from its own thread.  The weight-gradient GEMMs themselves are deferred too
+// (conv_gemm.hip, MTTS_DEFER_WGRAD): a flush first launches them batched, then their slab sums.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -182,6 +183,18 @@ int submit_reductions(const mtts_reduce_job *jobs, int njobs, hipStream_t st) {
     }
     return launch_jobs(jobs, njobs, st);
 }
+
+int queue_reductions(const mtts_reduce_job *jobs, int njobs) {
+    if (int rc = check_jobs(jobs, njobs)) return rc;
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_queue.insert(g_queue.end(), jobs, jobs + njobs);
+    return MTTS_OK;
+}
+
+bool deferring() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_defer;
+}
 }  // namespace mtts
 
 extern "C" {
@@ -197,11 +210,14 @@ void mtts_defer_reductions(int32_t on) {
 }
 
 int32_t mtts_pending_reductions(void) {
+    const int w = mtts::pending_wgrad_sums();  // the queued weight gradients' slab sums, still to come
     std::lock_guard<std::mutex> lk(g_mu);
-    return (int32_t)g_queue.size();
+    return (int32_t)g_queue.size() + w;
 }
 
 int mtts_flush_reductions(void *hip_stream) {
+    // queued weight gradients first (batched launches); their slab sums join the queue
+    if (int rc = mtts::flush_wgrads(static_cast<hipStream_t>(hip_stream))) return rc;
     std::vector<mtts_reduce_job> q;
     {
         std::lock_guard<std::mutex> lk(g_mu);
@@ -236,6 +252,7 @@ size_t mtts_colsum_workspace_size(int64_t rows, int32_t n) {
 }
 
 void mtts_discard_reductions(void) {
+    mtts::discard_wgrads();
     std::lock_guard<std::mutex> lk(g_mu);
     g_queue.clear();
 }

@@ -155,6 +155,7 @@ N.register("mtts_defer_reductions", None, [_I])
 N.register("mtts_pending_reductions", _I, [])
 N.register("mtts_flush_reductions", ctypes.c_int, [_P])
 N.register("mtts_discard_reductions", None, [])
+N.register("mtts_wgrad_plan_mode", None, [_I])
 N.register("mtts_colsum_workspace_size", _SZ, [_I64, _I])
 N.register("mtts_colsum", ctypes.c_int, [_P, _I64, _I, _I, _P, _I, _P, _SZ, _P])
 
@@ -512,7 +513,10 @@ def join_side_streams():
 # Parameter-gradient sums deferred to one batched launch (csrc/reduce.hip): inside
 # deferred_grad_sums() the weight-gradient GEMMs and the norm backwards only QUEUE the fixed-order sums
 # of their partial slabs; the context exit runs the queue as one launch instead of ~120 small ones.
-# The workspaces holding the partials are kept alive until then.  Valid only while nothing reads a
+# The weight-gradient GEMMs themselves are queued too (csrc/conv_gemm.hip, MTTS_DEFER_WGRAD=0 turns it
+# off) and a flush launches them batched -- up to 12 layers per launch, each with its own row split, so
+# the results are bitwise those of per-layer launches -- before their sums.
+# The workspaces holding the partials (and the queued GEMMs' inputs) are kept alive until then.  Valid only while nothing reads a
 # parameter gradient before the exit: fresh gradients (AccumulateGrad steals them, no copy kernel) of
 # LEAF weights -- a Function whose weights are not all leaves (ctx.leaf False) sums at once.
 _DEFER = {"on": False, "keep": [], "side_keep": [], "side": {}, "side_used": False,
@@ -523,8 +527,10 @@ _DEFER = {"on": False, "keep": [], "side_keep": [], "side": {}, "side_used": Fal
           "side_on": os.environ.get("MTTS_SIDE_REDUCE", "0") == "1",
           "chunk": int(os.environ.get("MTTS_SIDE_REDUCE_JOBS", "24")),
           # > 0: flush on the MAIN stream once this many sums are queued (slabs re-read while still in the
-          # MALL instead of from HBM at the end of the backward)
-          "inline": int(os.environ.get("MTTS_INLINE_REDUCE_JOBS", "8"))}
+          # MALL instead of from HBM at the end of the backward).  0 (default since the weight-gradient GEMMs
+          # are queued too): one flush at the end -- the batched launches then hold the whole backward's
+          # weight gradients (same box: 8 -> 7.99 ms, 16 7.86, 32 7.77, 64 7.71, 128 7.70, end only 7.64)
+          "inline": int(os.environ.get("MTTS_INLINE_REDUCE_JOBS", "0"))}
 
 
 def _leaves(*ts) -> bool:
@@ -662,7 +668,9 @@ def _wgrad_launch(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, of
                   | (WGRAD_F_DY_BF16 if dY.dtype == torch.bfloat16 else 0))
     lib = N.lib()
     ws = torch.empty(int(lib.mtts_conv_wgrad_workspace_size(ctypes.byref(args))), dtype=torch.uint8, device=dY.device)
-    _keep_partials(ws)
+    # inside deferred_grad_sums() the GEMM itself may be queued (MTTS_DEFER_WGRAD, run batched at the next
+    # flush): its inputs stay alive until then, like the slabs
+    _keep_partials(ws, dY, A, a_scale)
     log = WGRAD_LOG
     if log is not None:
         st, e0, e1 = _events(dY.device)

@@ -97,10 +97,12 @@ def test_side_stream_wgrad_matches_main_stream():
 
 @pytest.mark.parametrize("side", [False, True, "inline"])
 def test_deferred_grad_sums_match_immediate(side):
-    """The batched, deferred parameter-gradient sums (csrc/reduce.hip) equal the per-layer ones bitwise
-    on the decoder (same fixed-order sums, one launch instead of one per layer); side: batches of them
-    run on a side stream while the backward goes on (joined at the context exit); "inline": batches of
-    8 flushed on the main stream as they queue up (the default, MTTS_INLINE_REDUCE_JOBS)."""
+    """The deferred weight-gradient GEMMs (launched batched, csrc/conv_gemm.hip) and parameter-gradient sums
+    (csrc/reduce.hip) equal the per-layer ones bitwise on the decoder (same row splits, same fixed-order
+    sums, a few launches instead of one or two per layer); side: batches of them run on a side stream while
+    the backward goes on (joined at the context exit); "inline": batches of 8 flushed on the main stream as
+    they queue up (MTTS_INLINE_REDUCE_JOBS; the default flushes once, at the end)."""
+    from matcha import _native as N
     from matcha.models.components import _ops as OPS
     from matcha.training import synthetic_batch
 
@@ -108,6 +110,9 @@ def test_deferred_grad_sums_match_immediate(side):
     side = side is True
     saved_inline = OPS._DEFER["inline"]
     OPS._DEFER["side_on"], OPS._DEFER["chunk"], OPS._DEFER["inline"] = side, 8, (8 if inline else 0)
+    # queued weight gradients run batched with the batched split plan: the immediate pass takes the same
+    # plan, so the comparison isolates the batching (one launch for many layers) and the deferral
+    N.lib().mtts_wgrad_plan_mode(1)
 
     b = synthetic_batch(4, 20, 80, device=DEV)
     m = _model(3)
@@ -130,12 +135,11 @@ def test_deferred_grad_sums_match_immediate(side):
         torch.cuda.synchronize()
         return {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
 
-    from matcha import _native as N
-
     try:
         g0, g1 = grads(False), grads(True)
     finally:
         OPS._DEFER["side_on"], OPS._DEFER["chunk"], OPS._DEFER["inline"] = False, 24, saved_inline
+        N.lib().mtts_wgrad_plan_mode(0)
     assert N.lib().mtts_pending_reductions() == 0
     assert g0.keys() == g1.keys() and len(g0) > 100
     for n in g0:

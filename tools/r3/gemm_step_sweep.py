@@ -1,0 +1,86 @@
+"""Schedule sweep on the train step's OWN GEMM calls: one eager bf16 fwd+bwd of the bench batch records
+every O._gemm call (operands and epilogue as the model issues them); each distinct call is then re-run
+with every LDS-DMA tile config x split-K count and every register config, graph-timed, its output
+checked against the default schedule's.  One JSON line per call class (count, default, best, top 6).
+python tools/r3/gemm_step_sweep.py [max_rows]   (max_rows: only calls with nb*To <= max_rows)"""
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent.parent
+sys.path[:0] = [str(ROOT / "matcha-tts-etu-upmc-ensam_amd"), str(ROOT), str(ROOT / "tools")]
+from preln_shapes import t_ev  # noqa: E402
+from matcha.models.components import _ops as O  # noqa: E402
+from matcha.models.matcha_tts import MatchaTTS  # noqa: E402
+from matcha.training import TrainConfig, Trainer, synthetic_batch  # noqa: E402
+
+max_rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 30
+dev = torch.device("cuda")
+torch.manual_seed(1234)
+model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(dev).train()
+tr = Trainer(model, TrainConfig(precision="bf16-mixed", graph=False))
+batch = synthetic_batch(32, 120, 600, seed=1000, device=dev)
+for _ in range(2):
+    tr._fwd_bwd([batch])
+torch.cuda.synchronize()
+
+calls = {}
+orig = O._gemm
+
+
+def spy(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, *a, **kw):
+    out = orig(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, *a, **kw)
+    if nb * To <= max_rows:
+        flags = tuple(kw.get(k) is not None for k in ("a_scale", "bias", "residual", "c_scale", "C_pre", "aux"))
+        key = (nb * To, N_, len(offs) * cin, cin, len(offs), in_stride, str(A.dtype)[6:], str(C.dtype)[6:],
+               kw.get("act", 0), kw.get("dropout_p", 0.0) > 0, flags, getattr(Wp, "_mtts_w_split", False))
+        if key in calls:
+            calls[key][0] += 1
+        else:  # private copies: the sweep re-runs the call many times
+            kw2 = dict(kw)
+            for k in ("residual", "aux", "a_scale", "bias", "c_scale"):
+                if kw2.get(k) is not None:
+                    kw2[k] = kw2[k].clone()
+            if kw2.get("C_pre") is not None:
+                kw2["C_pre"] = torch.empty_like(kw2["C_pre"])
+            calls[key] = [1, (A.clone(), Ti, To, nb, in_stride, list(offs), cin, Wp, Kp, N_, torch.empty_like(C),
+                              To_full) + tuple(a), kw2]
+    return out
+
+
+O._gemm = spy
+tr._fwd_bwd([batch])
+torch.cuda.synchronize()
+O._gemm = orig
+
+for key, (count, args, kw) in sorted(calls.items(), key=lambda kv: -kv[0][0] * kv[0][1] * kv[0][2] * kv[1][0]):
+    C = args[10]
+
+    def run(cfg, splits):
+        kw2 = dict(kw, tile_cfg=cfg, splits=splits)
+        return lambda: orig(*args, **kw2)
+
+    run(-1, 0)()
+    torch.cuda.synchronize()
+    ref = C.float().clone()
+    res = {}
+    cands = [(-1, 0)] + [(c, s) for c in range(32, 55) for s in (1, 2, 3, 4, 6, 8)] + [(c, 1) for c in range(18)]
+    for cfg, s in cands:
+        fn = run(cfg, s)
+        try:
+            fn()
+            torch.cuda.synchronize()
+        except Exception:
+            continue
+        err = ((C.float() - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+        if not err < 2e-2:
+            continue
+        res[f"{cfg}/{s}"] = round(t_ev(fn), 1)
+    best = sorted(res.items(), key=lambda kv: kv[1])[:6]
+    M, N_, K = key[0], key[1], key[2]
+    print(json.dumps({"M": M, "N": N_, "K": K, "cin": key[3], "taps": key[4], "stride": key[5], "A": key[6],
+                      "C": key[7], "act": key[8], "drop": key[9], "flags": key[10], "wsplit": key[11],
+                      "count": count, "default_us": res.get("-1/0"), "best": best,
+                      "gain_us_total": round(count * (res.get("-1/0", 0) - best[0][1]), 1)}), flush=True)
