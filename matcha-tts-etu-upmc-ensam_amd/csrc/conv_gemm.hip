@@ -1307,7 +1307,9 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
     MTTS_CHECK_ARG(p.ldy % 4 == 0 && (uintptr_t)p.dY % 16 == 0, "conv_wgrad: dY rows must be 16-byte aligned");
     MTTS_CHECK_ARG(precision == MTTS_PREC_BF16 || precision == MTTS_PREC_FP32, "conv_wgrad: bad precision");
     const bool bf16 = precision == MTTS_PREC_BF16;
-    if (rows_per_step < 0) rows_per_step = 32;
+    // MTTS_WGRAD_KB=64: 64-row steps by default in bf16 (A/B switch)
+    static const int default_kb = [] { const char *e = getenv("MTTS_WGRAD_KB"); return e && atoi(e) == 64 ? 64 : 32; }();
+    if (rows_per_step < 0) rows_per_step = bf16 ? default_kb : 32;
     if (depth < 0) depth = 1;
     if (p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_WGRAD_F_DY_BF16)) {
         MTTS_CHECK_ARG(bf16 && depth == 1 && p.lda % 4 == 0 && (uintptr_t)p.A % 8 == 0,

@@ -604,6 +604,54 @@ def _maybe_side_sums():
     _DEFER["side_used"] = True
 
 
+# MTTS_SIDE_FLUSH (default on): at the decoder -> encoder seam of the backward (flow_matching._CfmPack) the
+# decoder's queued weight gradients + sums are launched on a side stream, forked there and joined at the
+# deferral's exit, so their chip-filling batched launches overlap the text encoder's latency-bound backward
+_SIDE_FLUSH = os.environ.get("MTTS_SIDE_FLUSH", "1") != "0"
+
+
+def flush_deferred_side() -> None:
+    """Inside deferred_grad_sums() (no-op outside, or with MTTS_SIDE_FLUSH=0): everything queued so far
+    -- the weight-gradient GEMMs, batched, then the sums -- runs on a side stream forked from the current
+    one here, while the backward continues on it; the deferral's exit (or the next main-stream flush)
+    joins it.  Inputs and slabs stay alive until then (side_keep); the outputs are fresh parameter
+    gradients that nothing reads before the join."""
+    if not (_DEFER["on"] and _SIDE_FLUSH) or _DEFER["side_on"]:
+        return
+    lib = N.lib()
+    if lib.mtts_pending_reductions() == 0:
+        return
+    dev = torch.cuda.current_device()
+    side = _DEFER["side"].get(dev)
+    if side is None:
+        side = _DEFER["side"][dev] = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    N.check(lib.mtts_flush_reductions(side.cuda_stream), "mtts_flush_reductions")
+    _DEFER["side_keep"].extend(_DEFER["keep"])
+    _DEFER["keep"].clear()
+    _DEFER["side_used"] = True
+
+
+def param_grad_side_stream():
+    """Inside deferred_grad_sums() with MTTS_SIDE_FLUSH: the deferral's side stream, already ordered after
+    the current stream, for backward work whose only outputs are fresh parameter gradients (joined at the
+    deferral's exit like the side flush); None otherwise.  The caller allocates on the current stream and
+    hands every tensor the side work reads to keep_for_side()."""
+    if not (_DEFER["on"] and _SIDE_FLUSH) or _DEFER["side_on"]:
+        return None
+    dev = torch.cuda.current_device()
+    side = _DEFER["side"].get(dev)
+    if side is None:
+        side = _DEFER["side"][dev] = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    _DEFER["side_used"] = True
+    return side
+
+
+def keep_for_side(*ts) -> None:
+    _DEFER["side_keep"].extend(t for t in ts if t is not None)
+
+
 def flush_deferred_grad_sums() -> None:
     """Runs the queued parameter-gradient sums now (inside deferred_grad_sums(); no-op outside): the
     data-parallel reducer calls it before packing a bucket, so the deferral still batches the sums of
@@ -1754,14 +1802,20 @@ class _TimeMLP(torch.autograd.Function):
         d_temb = new(B, D)
         dws = [torch.empty_like(w) for w in ws]
         dbs = [new(w.shape[0]) for w in ws]
-        _rows_bwd(a2, temb, ROWS_ACT_MISH, ws, dys, d_temb, dws, dbs)
-        if g_temb is not None:  # temb used directly as well (never, on the decoder's path)
-            d_temb = d_temb + _f32c(g_temb)
         dh1, dw2, db2 = new(B, D), torch.empty_like(w2), new(D)
-        _rows_bwd(a1, h1, ROWS_ACT_SILU, [w2], [d_temb], dh1, [dw2], [db2])
         de = new(*e.shape) if ctx.e_grad else None
         dw1, db1 = torch.empty_like(w1), new(D)
-        _rows_bwd(e, None, ROWS_ACT_NONE, [w1], [dh1], de, [dw1], [db1])
+        # on the decoder's path (t carries no gradient) every output is a parameter gradient: the five
+        # launches leave the critical path for the deferral's side stream (joined before the optimizer)
+        side = param_grad_side_stream() if (not ctx.e_grad and g_temb is None) else None
+        if side is not None:
+            keep_for_side(e, h1, a1, temb, a2, w1, w2, *ws, *dys, d_temb, dh1)
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            _rows_bwd(a2, temb, ROWS_ACT_MISH, ws, dys, d_temb, dws, dbs)
+            if g_temb is not None:  # temb used directly as well (never, on the decoder's path)
+                d_temb = d_temb + _f32c(g_temb)
+            _rows_bwd(a1, h1, ROWS_ACT_SILU, [w2], [d_temb], dh1, [dw2], [db2])
+            _rows_bwd(e, None, ROWS_ACT_NONE, [w1], [dh1], de, [dw1], [db1])
         return (de, dw1, db1, dw2, db2, None, *dws, *dbs)
 
 

@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 
 from matcha import _native as N
+from matcha.models.components import _ops as O
 from matcha.models.components.decoder import Decoder
 
 
@@ -95,6 +96,8 @@ class _CfmPack(torch.autograd.Function):
         with torch.cuda.device(dp.device):
             N.check(N.lib().mtts_cfm_pack_bwd(N.ptr(dp), B, C, T, N.ptr(d_mu), N.stream_handle(dp.device)),
                     "mtts_cfm_pack_bwd")
+            # the decoder's backward is complete: its queued weight gradients overlap the encoder's backward
+            O.flush_deferred_side()
         return None, None, None, d_mu, None
 
 
