@@ -66,7 +66,14 @@ for key, (count, args, kw) in sorted(calls.items(), key=lambda kv: -kv[0][0] * k
     torch.cuda.synchronize()
     ref = C.float().clone()
     res = {}
-    cands = [(-1, 0)] + [(c, s) for c in range(32, 55) for s in (1, 2, 3, 4, 6, 8)] + [(c, 1) for c in range(18)]
+    import os
+    lo, hi = (int(v) for v in os.environ.get("SWEEP_GLDS", "32-54").split("-"))
+    spl = [int(v) for v in os.environ.get("SWEEP_SPLITS", "1,2,3,4,6,8").split(",")]
+    reg = os.environ.get("SWEEP_REG", "1") == "1"
+    min_rows = int(os.environ.get("SWEEP_MIN_ROWS", "0"))
+    if key[0] < min_rows:
+        continue
+    cands = [(-1, 0)] + [(c, s) for c in range(lo, hi + 1) for s in spl] + ([(c, 1) for c in range(18)] if reg else [])
     for cfg, s in cands:
         fn = run(cfg, s)
         try:
