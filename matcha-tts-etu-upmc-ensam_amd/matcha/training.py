@@ -260,6 +260,12 @@ class Trainer:
         # (components/_ops.py deferred_grad_sums): also needs fresh gradients, and no DDP hook
         # reading them during the backward (the bucket reducer flushes the queue per bucket)
         defer = fresh and self.defer_grad_sums and not side and (self.cfg.graph or self.dp_mode != "ddp")
+        # several micro-batches (accumulate_grad_batches): the FIRST one's gradients are fresh too -- its
+        # backward runs deferred (batched weight gradients, flushed when it ends, before the next micro-batch
+        # accumulates into them); the later ones accumulate and run per layer
+        self._defer_first = (n > 1 and self.dev.type == "cuda" and self.defer_grad_sums
+                             and all(p.grad is None for p in self.params)
+                             and (self.cfg.graph or self.dp_mode != "ddp"))
         with OPS.deferred_grad_sums(defer), OPS.side_stream_wgrad(side):
             return self._fwd_bwd_body(batches, sync_ctx)
 
@@ -268,7 +274,9 @@ class Trainer:
         logged = None
         for i, batch in enumerate(batches):
             ctx = sync_ctx(i) if sync_ctx else contextlib.nullcontext()
-            with ctx:
+            first = OPS.deferred_grad_sums(True) if (i == 0 and getattr(self, "_defer_first", False)) \
+                else contextlib.nullcontext()
+            with ctx, first:
                 inject = {k: batch[k] for k in ("t", "z") if k in batch}  # parity tests' CFM randomness
                 with self._autocast():
                     dur, prior, diff, _ = self.wrapped(x=batch["x"], x_lengths=batch["x_lengths"],

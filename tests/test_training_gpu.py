@@ -245,6 +245,18 @@ def test_accumulate_grad_batches_2_vs_torch(graph):
     _inject(m_tr, t, z)
     _inject(m_ref, t, z)
     tr = Trainer(m_tr, TrainConfig(accumulate_grad_batches=2, graph=graph))
+    # the Trainer's first micro-batch runs its weight gradients queued and batched (the batched split
+    # plan); the plain-autograd reference takes the same plan, so the gradients stay bitwise comparable
+    from matcha import _native as N
+
+    N.lib().mtts_wgrad_plan_mode(1)
+    try:
+        _accumulate2_steps(tr, m_tr, m_ref, b1, b2, graph)
+    finally:
+        N.lib().mtts_wgrad_plan_mode(0)
+
+
+def _accumulate2_steps(tr, m_tr, m_ref, b1, b2, graph):
     params = [p for p in m_ref.parameters() if p.requires_grad]
     opt = torch.optim.AdamW(params, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-6)
     for step in range(3):
