@@ -149,6 +149,10 @@ int mtts_conv_wgrad_tile(const mtts_conv_wgrad_args *args, int32_t precision, in
  * splits (the batch fills the chip).  mode 0: that plan for queued gradients only (default); 1: for every
  * call (an immediate call then equals a queued one bitwise); 2: the per-launch plan for every call. */
 void mtts_wgrad_plan_mode(int32_t mode);
+/* Caps the grid of the weight-gradient launches that follow at `blocks` workgroups, each walking several
+ * (tile, split) blocks -- bitwise the same results; 0 (default) = one workgroup per block.  The side-stream
+ * flush sets it so the batched gradients leave CUs to the latency-bound work on the main stream. */
+void mtts_wgrad_flush_cap(int32_t blocks);
 
 /*
  * y[b,t,c] = mish(GN(h)[b,t,c]) * mask[b,t] + add[b,c]      (mask / add optional)

@@ -411,15 +411,16 @@ struct WgradBatch {
     int32_t njobs;
 };
 
-template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false, bool LIN = false, int HV = 1>
-__global__ __launch_bounds__(kThreads * HV) void conv_wgrad_kernel(const WgradBatch wb) {
+// One (tile, split) block of a batch: vb is its index in the batch's block numbering.
+template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16, bool YBF16, bool LIN, int HV>
+__device__ __forceinline__ void wgrad_block(const WgradBatch &wb, const int vb) {
     int jb = 0;  // this block's job (block-uniform scan over the batch's first-block table)
-    while (jb + 1 < wb.njobs && (int)blockIdx.x >= wb.first[jb + 1]) ++jb;
+    while (jb + 1 < wb.njobs && vb >= wb.first[jb + 1]) ++jb;
     const mtts_conv_wgrad_args &p = wb.job[jb].a;
     const int rows_per_split = wb.job[jb].rps;
     float *__restrict__ part = wb.job[jb].part;
     float *__restrict__ part_db = wb.job[jb].part_db;
-    const int blk = (int)blockIdx.x - wb.first[jb], nblk = wb.first[jb + 1] - wb.first[jb];
+    const int blk = vb - wb.first[jb], nblk = wb.first[jb + 1] - wb.first[jb];
     static_assert(HV == 1 || (HV == 2 && DEPTH == 1), "two halves: one step in flight");
     static_assert(HV == 1 || (size_t)64 * kThreads * sizeof(float) <= 2 * WgradGeom<BF16, KB>::kLds,
                   "half 1's accumulators fit the two halves' LDS");
@@ -805,6 +806,18 @@ __global__ __launch_bounds__(kThreads * HV) void conv_wgrad_kernel(const WgradBa
     }
 }
 
+// The batch's blocks on gridDim.x workgroups: one each when the grid covers them (the default), else a
+// workgroup walks several (a capped grid leaves CUs to a concurrent stream: the side-stream flush, see
+// mtts_wgrad_flush_cap).  Whole-block-uniform loop; the barrier protects the LDS images between blocks.
+template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false, bool LIN = false, int HV = 1>
+__global__ __launch_bounds__(kThreads * HV) void conv_wgrad_kernel(const WgradBatch wb) {
+    const int total = wb.first[wb.njobs];
+    for (int vb = (int)blockIdx.x; vb < total; vb += (int)gridDim.x) {
+        wgrad_block<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN, HV>(wb, vb);
+        __syncthreads();
+    }
+}
+
 // The GEMM kernels compute tap offsets as off[0] + j*(off[1]-off[0]).
 bool taps_arithmetic(const int32_t *off, int ntaps) {
     for (int j = 2; j < ntaps; ++j)
@@ -1139,6 +1152,9 @@ extern "C" size_t mtts_conv_wgrad_workspace_size(const mtts_conv_wgrad_args *arg
     return mtts::align_up((size_t)splits * args->N * args->K * 4, 256) + (size_t)splits * args->N * 4 + 256;
 }
 
+// mtts_wgrad_flush_cap: > 0 caps the grid of the batched weight-gradient launches (0: one workgroup per block)
+std::atomic<int> g_wgrad_cap{0};
+
 template <bool BF16, int KB, int DEPTH, bool INC, bool ABF16 = false, bool YBF16 = false, bool LIN = false, int HV = 1>
 static int wgrad_launch_hv(const WgradBatch &wb, hipStream_t st) {
     using Gm = WgradGeom<BF16, KB>;
@@ -1150,8 +1166,9 @@ static int wgrad_launch_hv(const WgradBatch &wb, hipStream_t st) {
             return mtts::fail(MTTS_ERR_HIP, "conv_wgrad: LDS attribute");
         attr_set = true;
     }
-    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN, HV>), dim3((unsigned)wb.first[wb.njobs]),
-                       dim3(kThreads * HV), lds, st, wb);
+    const int total = wb.first[wb.njobs], cap = g_wgrad_cap.load();
+    hipLaunchKernelGGL((conv_wgrad_kernel<BF16, KB, DEPTH, INC, ABF16, YBF16, LIN, HV>),
+                       dim3((unsigned)(cap > 0 && cap < total ? cap : total)), dim3(kThreads * HV), lds, st, wb);
     return mtts::check_launch("conv_wgrad_kernel");
 }
 
@@ -1420,6 +1437,8 @@ void discard_wgrads() {
     g_wq.clear();
 }
 }  // namespace mtts
+
+extern "C" void mtts_wgrad_flush_cap(int32_t blocks) { g_wgrad_cap.store(blocks > 0 ? blocks : 0); }
 
 extern "C" void mtts_wgrad_plan_mode(int32_t mode) { g_wgrad_plan_mode.store(mode >= 0 && mode <= 2 ? mode : 0); }
 

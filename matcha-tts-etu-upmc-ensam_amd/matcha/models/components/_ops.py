@@ -156,6 +156,7 @@ N.register("mtts_pending_reductions", _I, [])
 N.register("mtts_flush_reductions", ctypes.c_int, [_P])
 N.register("mtts_discard_reductions", None, [])
 N.register("mtts_wgrad_plan_mode", None, [_I])
+N.register("mtts_wgrad_flush_cap", None, [_I])
 N.register("mtts_colsum_workspace_size", _SZ, [_I64, _I])
 N.register("mtts_colsum", ctypes.c_int, [_P, _I64, _I, _I, _P, _I, _P, _SZ, _P])
 
@@ -608,6 +609,9 @@ def _maybe_side_sums():
 # decoder's queued weight gradients + sums are launched on a side stream, forked there and joined at the
 # deferral's exit, so their chip-filling batched launches overlap the text encoder's latency-bound backward
 _SIDE_FLUSH = os.environ.get("MTTS_SIDE_FLUSH", "1") != "0"
+# MTTS_SIDE_WGRAD_CAP: workgroups the side-flushed weight-gradient batch may occupy (0 = one per block):
+# fewer leave CUs to the encoder's backward on the main stream (mtts_wgrad_flush_cap)
+_SIDE_CAP = int(os.environ.get("MTTS_SIDE_WGRAD_CAP", "0"))
 
 
 def flush_deferred_side() -> None:
@@ -626,7 +630,11 @@ def flush_deferred_side() -> None:
     if side is None:
         side = _DEFER["side"][dev] = torch.cuda.Stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
-    N.check(lib.mtts_flush_reductions(side.cuda_stream), "mtts_flush_reductions")
+    lib.mtts_wgrad_flush_cap(_SIDE_CAP)
+    try:
+        N.check(lib.mtts_flush_reductions(side.cuda_stream), "mtts_flush_reductions")
+    finally:
+        lib.mtts_wgrad_flush_cap(0)
     _DEFER["side_keep"].extend(_DEFER["keep"])
     _DEFER["keep"].clear()
     _DEFER["side_used"] = True

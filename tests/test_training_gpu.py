@@ -95,7 +95,7 @@ def test_side_stream_wgrad_matches_main_stream():
         assert torch.equal(g1[n], g0[n]), n
 
 
-@pytest.mark.parametrize("side", [False, True, "inline"])
+@pytest.mark.parametrize("side", [False, True, "inline", "cap"])
 def test_deferred_grad_sums_match_immediate(side):
     """The deferred weight-gradient GEMMs (launched batched, csrc/conv_gemm.hip) and parameter-gradient sums
     (csrc/reduce.hip) equal the per-layer ones bitwise on the decoder (same row splits, same fixed-order
@@ -107,6 +107,7 @@ def test_deferred_grad_sums_match_immediate(side):
     from matcha.training import synthetic_batch
 
     inline = side == "inline"
+    cap = side == "cap"  # batched weight-gradient launches on a capped grid (37 workgroups walk the blocks)
     side = side is True
     saved_inline = OPS._DEFER["inline"]
     OPS._DEFER["side_on"], OPS._DEFER["chunk"], OPS._DEFER["inline"] = side, 8, (8 if inline else 0)
@@ -122,6 +123,7 @@ def test_deferred_grad_sums_match_immediate(side):
 
     def grads(defer):
         m.zero_grad(set_to_none=True)
+        N.lib().mtts_wgrad_flush_cap(37 if (cap and defer) else 0)
         with OPS.deferred_grad_sums(defer):
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 dur, prior, diff, _ = m(**b, t=t, z=z)
@@ -140,6 +142,7 @@ def test_deferred_grad_sums_match_immediate(side):
     finally:
         OPS._DEFER["side_on"], OPS._DEFER["chunk"], OPS._DEFER["inline"] = False, 24, saved_inline
         N.lib().mtts_wgrad_plan_mode(0)
+        N.lib().mtts_wgrad_flush_cap(0)
     assert N.lib().mtts_pending_reductions() == 0
     assert g0.keys() == g1.keys() and len(g0) > 100
     for n in g0:
