@@ -1,0 +1,9 @@
+#!/bin/bash
+# long-form config 5 on one GPU with batched weight gradients: max-length batch and length-bucketed batches
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/${TAG:-r3wm}; mkdir -p $O; cd $R
+timeout -k 10 400 python bench.py --no-cpu-baseline --no-synth --no-extra --no-graph-profile --batch 8 --tx 512 --ty 4096 --steps 10 --warmup 3 > $O/longform_max.json 2> $O/lf1.err; rc=$?
+[ $rc -ne 0 ] && { tail -5 $O/lf1.err; exit $rc; }
+python -c "import json; d=json.load(open('$O/longform_max.json')); print('max-length', d['ms_per_step'], d['value'])"
+timeout -k 10 500 python bench.py --no-cpu-baseline --no-synth --no-extra --no-graph-profile --batch 8 --tx 512 --ty 4096 --bucketed 4 --steps 12 --warmup 8 > $O/longform_bucketed.json 2> $O/lf2.err; rc=$?
+[ $rc -ne 0 ] && { tail -5 $O/lf2.err; exit $rc; }
+python -c "import json; d=json.load(open('$O/longform_bucketed.json')); print('bucketed', d['ms_per_step'], d['value'])"
