@@ -163,7 +163,8 @@ int mtts_gn_mish_fwd(const float *h, const float *gamma, const float *beta, cons
                      float *y, float *mean, float *rstd, int32_t B, int32_t T, int32_t C, int32_t G, float eps,
                      void *hip_stream);
 size_t mtts_gn_mish_bwd_workspace_size(int32_t B, int32_t C);
-/* dh (and dgamma, dbeta [C], dadd [B,C] when non-NULL) from dy and the forward's inputs/statistics. */
+/* dh (and dgamma, dbeta [C], dadd [B,C] when non-NULL) from dy and the forward's inputs/statistics;
+ * C/G <= 256. */
 int mtts_gn_mish_bwd(const float *dy, const float *h, const float *gamma, const float *beta, const float *mask,
                      const float *mean, const float *rstd, float *dh, float *dgamma, float *dbeta, float *dadd,
                      int32_t B, int32_t T, int32_t C, int32_t G, void *workspace, size_t workspace_bytes,

@@ -152,6 +152,37 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_fwd_kernel(const TH *__res
     }
 }
 
+// Per-channel partials of the GroupNorm backward: chred[a][r * cols + c] over the block's rpp rows ->
+// pg / pb / dadd [b, c0..], in a fixed order by all threads: stage 1 sums 16-row chunks (one task per
+// array x chunk x column), stage 2 the chunks in order.  (A loop of `cols` threads over every row was a
+// serial chain of ~400 LDS reads that held its wave several microseconds behind the rest of the block.)
+constexpr int kGnChunk = 16;
+__device__ __forceinline__ void gn_column_sums(float4 (*chred)[kGnThreads], float4 (*tmp)[128], int cols, int rpp,
+                                               int tid, float *pg, float *pb, float *dadd, size_t out0) {
+    const int nch = (rpp + kGnChunk - 1) / kGnChunk;
+    for (int task = tid; task < 3 * nch * cols; task += kGnThreads) {
+        const int a = task / (nch * cols), rem = task - a * nch * cols, ch = rem / cols, c = rem - ch * cols;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int r1 = min(rpp, (ch + 1) * kGnChunk);
+        for (int r = ch * kGnChunk; r < r1; ++r) {
+            const float4 v = chred[a][r * cols + c];
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+        tmp[a][ch * cols + c] = s;
+    }
+    __syncthreads();
+    if (tid < 3 * cols) {
+        const int a = tid / cols, c = tid - a * cols;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int ch = 0; ch < nch; ++ch) {
+            const float4 v = tmp[a][ch * cols + c];
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+        float *out = a == 0 ? pg : a == 1 ? pb : dadd;
+        if (out) *reinterpret_cast<float4 *>(out + out0 + c * 4) = s;
+    }
+}
+
 // Register-resident variants (T <= P * rows_per_pass): the group's values are loaded ONCE into
 // registers -- one HBM read + one write per element instead of three / four streaming passes -- with
 // the same per-thread summation order as the streaming kernels.
@@ -222,6 +253,7 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_reg_kernel(
     float *__restrict__ dadd, int T, int C, int G) {
     __shared__ float red[kGnThreads / 64];
     __shared__ float4 chred[3][kGnThreads];
+    __shared__ float4 ctmp[3][128];
     const int g = blockIdx.x, b = blockIdx.y;
     const int cg = C / G, cols = cg / 4, rpp = kGnThreads / cols;
     const int tid = threadIdx.x, col = tid % cols, r0 = tid / cols;
@@ -270,19 +302,7 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_reg_kernel(
     chred[1][tid] = ab;
     chred[2][tid] = ad;
     __syncthreads();
-    if (tid < cols) {
-        float4 sg = make_float4(0, 0, 0, 0), sb = sg, sd = sg;
-        for (int r = 0; r < rpp; ++r) {
-            const float4 a = chred[0][r * cols + tid], bb = chred[1][r * cols + tid], dd = chred[2][r * cols + tid];
-            sg.x += a.x; sg.y += a.y; sg.z += a.z; sg.w += a.w;
-            sb.x += bb.x; sb.y += bb.y; sb.z += bb.z; sb.w += bb.w;
-            sd.x += dd.x; sd.y += dd.y; sd.z += dd.z; sd.w += dd.w;
-        }
-        const int cc = g * cg + tid * 4;
-        *reinterpret_cast<float4 *>(pg + (size_t)b * C + cc) = sg;
-        *reinterpret_cast<float4 *>(pb + (size_t)b * C + cc) = sb;
-        if (dadd) *reinterpret_cast<float4 *>(dadd + (size_t)b * C + cc) = sd;
-    }
+    gn_column_sums(chred, ctmp, cols, rpp, tid, pg, pb, dadd, (size_t)b * C + g * cg);
     if (!active) return;
     TO *dhb = dh + (size_t)b * T * C + c0;
 #pragma unroll
@@ -309,6 +329,7 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_kernel(
     float *__restrict__ dadd, int T, int C, int G) {
     __shared__ float red[kGnThreads / 64];
     __shared__ float4 chred[3][kGnThreads];
+    __shared__ float4 ctmp[3][128];
     const int g = blockIdx.x, b = blockIdx.y;
     const int cg = C / G;
     const int cols = cg / 4;
@@ -353,19 +374,7 @@ __global__ __launch_bounds__(kGnThreads) void gn_mish_bwd_kernel(
     chred[1][tid] = ab;
     chred[2][tid] = ad;
     __syncthreads();
-    if (tid < cols) {
-        float4 sg = make_float4(0, 0, 0, 0), sb = sg, sd = sg;
-        for (int r = 0; r < rows_per_pass; ++r) {
-            const float4 a = chred[0][r * cols + tid], bb = chred[1][r * cols + tid], dd = chred[2][r * cols + tid];
-            sg.x += a.x; sg.y += a.y; sg.z += a.z; sg.w += a.w;
-            sb.x += bb.x; sb.y += bb.y; sb.z += bb.z; sb.w += bb.w;
-            sd.x += dd.x; sd.y += dd.y; sd.z += dd.z; sd.w += dd.w;
-        }
-        const int cc = g * cg + tid * 4;
-        *reinterpret_cast<float4 *>(pg + (size_t)b * C + cc) = sg;
-        *reinterpret_cast<float4 *>(pb + (size_t)b * C + cc) = sb;
-        if (dadd) *reinterpret_cast<float4 *>(dadd + (size_t)b * C + cc) = sd;
-    }
+    gn_column_sums(chred, ctmp, cols, rows_per_pass, tid, pg, pb, dadd, (size_t)b * C + g * cg);
     if (!active) return;
     TO *dhb = dh + (size_t)b * T * C + c0;
     for (int t = r0; t < T; t += rows_per_pass) {
@@ -657,7 +666,8 @@ extern "C" int mtts_gn_mish_bwd_ex(const void *dy, const void *h, const float *g
                                    float *dbeta, float *dadd, int32_t B, int32_t T, int32_t C, int32_t G,
                                    int32_t flags, void *workspace, size_t workspace_bytes, void *hip_stream) {
     MTTS_CHECK_ARG(dy && h && gamma && beta && mean && rstd && dh, "gn_mish_bwd: null pointer");
-    MTTS_CHECK_ARG(B >= 0 && T >= 1 && G >= 1 && C % G == 0 && (C / G) % 4 == 0, "gn_mish_bwd: bad shape");
+    MTTS_CHECK_ARG(B >= 0 && T >= 1 && G >= 1 && C % G == 0 && (C / G) % 4 == 0 && C / G <= 256,
+                   "gn_mish_bwd: need C % G == 0, (C/G) % 4 == 0 and C/G <= 256");
     MTTS_CHECK_ARG(aligned16(dy) && aligned16(h) && aligned16(dh) && (!dadd || aligned16(dadd)),
                    "gn_mish_bwd: tensors must be 16-byte aligned");
     const int known = MTTS_NORM_F_X_BF16 | MTTS_NORM_F_Y_BF16 | MTTS_NORM_F_DY_BF16;
