@@ -288,8 +288,9 @@ def spec_convT_dgrad(w):
                     True)
 
 
-def _run_pack(specs, prec):
-    """prec: PREC_FP32, PREC_BF16, or PACK_BF16_SPLIT ([2 * rows, Kp]: the hi plane, then the lo plane)."""
+def _run_pack(specs, prec, stream=None):
+    """prec: PREC_FP32, PREC_BF16, or PACK_BF16_SPLIT ([2 * rows, Kp]: the hi plane, then the lo plane).
+    stream: launch there instead of the current stream (outputs are allocated on the current one)."""
     dev = specs[0].jobs[0][0].device
     split = prec == PACK_BF16_SPLIT
     dt = torch.bfloat16 if prec in (PREC_BF16, PACK_BF16_SPLIT) else torch.float32
@@ -309,8 +310,8 @@ def _run_pack(specs, prec):
             j.sr, j.sc, j.sj, j.j0, j.js = sr, sc, sj, j0, js
             j.lo_off = sp.rows * sp.Kp if split else 0
             i += 1
-    N.check(N.lib().mtts_pack_weights(arr, njobs, PREC_BF16 if split else prec,
-                                      torch.cuda.current_stream(dev).cuda_stream), "mtts_pack_weights")
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    N.check(N.lib().mtts_pack_weights(arr, njobs, PREC_BF16 if split else prec, st.cuda_stream), "mtts_pack_weights")
     if split:
         for o in outs:
             o._mtts_w_split = True  # _gemm sets MTTS_GEMM_F_W_SPLIT for it
@@ -332,15 +333,12 @@ def weight_pack_scope(owner: torch.nn.Module):
     from that cache.  Layouts requested for the first time are packed on demand and remembered."""
     prec = gemm_precision()
     plan = owner.__dict__.setdefault("_mtts_pack_plan", {})
-    grad = torch.is_grad_enabled()
-    kinds = (prec, PACK_BF16_SPLIT) if prec == PREC_BF16 else (prec,)
-    cache = {}
-    for kind in kinds:
-        specs = [sp for key, sp in plan.items()
-                 if key[0] == kind and (grad or not sp.dgrad) and _pack_kind(sp, prec) == kind]
-        if specs:
-            for sp, t in zip(specs, _run_pack(specs, kind)):
-                cache[(kind,) + sp.key] = t
+    pre = owner.__dict__.pop("_mtts_pack_pre", None)
+    if pre is not None and pre[0] == (prec, torch.is_grad_enabled()):
+        cache = pre[1]  # packed ahead on the side stream (prefetch_packs): wait for it
+        torch.cuda.current_stream(pre[2].device).wait_stream(pre[2])
+    else:
+        cache = _pack_plan_now(plan, prec)
     tok = _PACK_SCOPE.set((plan, cache, prec))
     nseed = owner.__dict__.get("_mtts_seed_count", 0)
     dev = next(owner.parameters()).device
@@ -354,6 +352,34 @@ def weight_pack_scope(owner: torch.nn.Module):
         _SEED_SCOPE.reset(stok)
         _PACK_SCOPE.reset(tok)
         owner.__dict__["_mtts_seed_count"] = seeds["used"]
+
+
+def _pack_plan_now(plan, prec, stream=None):
+    """Every layout in `plan` for this precision (the backward's transposed ones too when grad is
+    enabled), a few launches per kind -> {key: packed}."""
+    grad = torch.is_grad_enabled()
+    kinds = (prec, PACK_BF16_SPLIT) if prec == PREC_BF16 else (prec,)
+    cache = {}
+    for kind in kinds:
+        specs = [sp for key, sp in plan.items()
+                 if key[0] == kind and (grad or not sp.dgrad) and _pack_kind(sp, prec) == kind]
+        if specs:
+            for sp, t in zip(specs, _run_pack(specs, kind, stream)):
+                cache[(kind,) + sp.key] = t
+    return cache
+
+
+def prefetch_packs(owner: torch.nn.Module, side) -> None:
+    """Packs `owner`'s known layouts NOW on `side` (outputs allocated on the current stream), for its next
+    weight_pack_scope -- which waits for `side` and skips its own packing.  The weights must not change
+    in between (one forward)."""
+    plan = owner.__dict__.get("_mtts_pack_plan")
+    if not plan:
+        return
+    prec = gemm_precision()
+    cache = _pack_plan_now(plan, prec, side)
+    keep_for_side(*cache.values())  # alive until the side stream is joined, used or not
+    owner.__dict__["_mtts_pack_pre"] = ((prec, torch.is_grad_enabled()), cache, side)
 
 
 def packed(spec: PackSpec, prec: int) -> tuple[torch.Tensor, int]:
@@ -654,6 +680,9 @@ def param_grad_side_stream():
     side.wait_stream(torch.cuda.current_stream(dev))
     _DEFER["side_used"] = True
     return side
+
+
+side_fork = param_grad_side_stream  # the same fork, for forward work that runs ahead (prefetch)
 
 
 def keep_for_side(*ts) -> None:
@@ -1783,18 +1812,15 @@ class _TimeMLP(torch.autograd.Function):
     weight concatenation, each tp_i is written contiguous."""
 
     @staticmethod
-    def forward(ctx, e, w1, b1, w2, b2, n_proj, *wb):
+    def forward(ctx, e, w1, b1, w2, b2, n_proj, pre, *wb):
         N.require_device(e, w1)
         ws = [_f32c(w) for w in wb[:n_proj]]
         bs = [_f32c(b) for b in wb[n_proj:]]
         e, w1, b1, w2, b2 = _f32c(e), _f32c(w1), _f32c(b1), _f32c(w2), _f32c(b2)
-        B, D = e.shape[0], w1.shape[0]
-        new = functools.partial(torch.empty, dtype=torch.float32, device=e.device)
-        h1, a1, temb, a2 = new(B, D), new(B, D), new(B, D), new(B, D)
-        _rows_fwd(e, [w1], [b1], [h1], [a1], ROWS_ACT_SILU)
-        _rows_fwd(a1, [w2], [b2], [temb], [a2], ROWS_ACT_MISH)
-        tps = [new(B, w.shape[0]) for w in ws]
-        _rows_fwd(a2, ws, bs, tps, None, ROWS_ACT_NONE)
+        if pre is not None:  # launched ahead on the side stream (time_mlp_launch); the caller has joined it
+            h1, a1, temb, a2, tps = pre
+        else:
+            h1, a1, temb, a2, tps = _time_mlp_launch(e, w1, b1, w2, b2, ws, bs, _time_mlp_alloc(e, w1, b1, w2, b2, ws, bs))
         ctx.save_for_backward(e, h1, a1, temb, a2, w1, w2, *ws)
         ctx.n = n_proj
         ctx.e_grad = ctx.needs_input_grad[0]
@@ -1824,12 +1850,43 @@ class _TimeMLP(torch.autograd.Function):
                 d_temb = d_temb + _f32c(g_temb)
             _rows_bwd(a1, h1, ROWS_ACT_SILU, [w2], [d_temb], dh1, [dw2], [db2])
             _rows_bwd(e, None, ROWS_ACT_NONE, [w1], [dh1], de, [dw1], [db1])
-        return (de, dw1, db1, dw2, db2, None, *dws, *dbs)
+        return (de, dw1, db1, dw2, db2, None, None, *dws, *dbs)
 
 
-def time_mlp(e, linear_1, linear_2, proj_linears):
-    """(temb, [tp_i]) = (time_mlp(e), [lin_i(mish(temb))]) for nn.Linear modules; see _TimeMLP."""
+def _time_mlp_alloc(e, w1, b1, w2, b2, ws, bs):
+    """The forward's outputs, allocated on the current stream (a caller may then launch under another)."""
+    B, D = e.shape[0], w1.shape[0]
+    new = functools.partial(torch.empty, dtype=torch.float32, device=e.device)
+    h1, a1, temb, a2 = new(B, D), new(B, D), new(B, D), new(B, D)
+    tps = [new(B, w.shape[0]) for w in ws]
+    return h1, a1, temb, a2, tps
+
+
+def _time_mlp_launch(e, w1, b1, w2, b2, ws, bs, outs):
+    h1, a1, temb, a2, tps = outs
+    _rows_fwd(e, [w1], [b1], [h1], [a1], ROWS_ACT_SILU)
+    _rows_fwd(a1, [w2], [b2], [temb], [a2], ROWS_ACT_MISH)
+    _rows_fwd(a2, ws, bs, tps, None, ROWS_ACT_NONE)
+    return outs
+
+
+def time_mlp(e, linear_1, linear_2, proj_linears, pre=None):
+    """(temb, [tp_i]) = (time_mlp(e), [lin_i(mish(temb))]) for nn.Linear modules; see _TimeMLP.  pre: the
+    forward's tensors from time_mlp_ahead (already joined)."""
     ws = [lin.weight for lin in proj_linears]
     bs = [lin.bias for lin in proj_linears]
-    out = _TimeMLP.apply(e, linear_1.weight, linear_1.bias, linear_2.weight, linear_2.bias, len(ws), *ws, *bs)
+    out = _TimeMLP.apply(e, linear_1.weight, linear_1.bias, linear_2.weight, linear_2.bias, len(ws), pre, *ws, *bs)
     return out[0], list(out[1:])
+
+
+def time_mlp_ahead(e, linear_1, linear_2, proj_linears, side):
+    """The time MLP's forward launched on `side` now (outputs allocated on the current stream) -> the
+    `pre` tensors for time_mlp once the caller has joined `side`."""
+    w1, b1, w2, b2 = (_f32c(v) for v in (linear_1.weight, linear_1.bias, linear_2.weight, linear_2.bias))
+    ws = [_f32c(lin.weight) for lin in proj_linears]
+    bs = [_f32c(lin.bias) for lin in proj_linears]
+    outs = _time_mlp_alloc(e, w1, b1, w2, b2, ws, bs)
+    keep_for_side(e, w1, b1, w2, b2, *ws, *bs, *outs[:4], *outs[4])  # alive until the side stream is joined
+    with torch.cuda.stream(side):
+        _time_mlp_launch(e, w1, b1, w2, b2, ws, bs, outs)
+    return outs

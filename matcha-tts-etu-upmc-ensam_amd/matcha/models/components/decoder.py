@@ -229,17 +229,47 @@ class Decoder(nn.Module):
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec_bf16), O.weight_pack_scope(self):
                 return self._forward_tm(None, mask.float(), None, t.float(), packed=h)
 
+    def _resnets(self):
+        return ([r for r, *_ in self.Downsampling_Blocks] + [r for r, _ in self.Mid_Blocks]
+                + [r for r, *_ in self.Upsampling_Blocks])
+
+    def prefetch(self, t, side):
+        """Launches, on `side` (already ordered after the current stream), what this decoder's next forward
+        for CFM time t needs and nothing else produces: its weight packs and the time path (embedding +
+        time MLP forward).  Outputs are allocated on the current stream; forward waits for `side` where it
+        uses them (weight_pack_scope, _time_path) -- a Trainer step runs them beside the text encoder."""
+        O.prefetch_packs(self, side)
+        resnets = self._resnets()
+        if len(resnets) > N_ROWS_MAX_MATS:
+            return
+        with torch.autocast("cuda", enabled=False):
+            tt = t.detach().float().reshape(-1).contiguous()
+            e = torch.empty((tt.numel(), self.time_embeddings.dim), dtype=torch.float32, device=tt.device)
+            O.keep_for_side(tt, e)
+            with torch.cuda.device(tt.device):
+                N.check(N.lib().mtts_time_embedding(N.ptr(tt), tt.numel(), self.time_embeddings.dim, 1000.0, N.ptr(e),
+                                                    side.cuda_stream), "mtts_time_embedding")
+            pre = O.time_mlp_ahead(e, self.time_mlp.linear_1, self.time_mlp.linear_2, [r.mlp[1] for r in resnets], side)
+        self.__dict__["_mtts_time_pre"] = (tt.data_ptr(), tt.numel(), e, pre, side)
+
     def _time_path(self, t):
         """temb = time_mlp(SinusoidalPosEmb(t)) (decoder.py:33-49, :285-286) and every Resnet1D's
         mlp(temb) = Linear(Mish(temb)) (:80-81), fp32 as the reference keeps it, in 1 + 3 HIP launches
-        (csrc/cfm_prep.hip, csrc/time_mlp.hip); backward 5.  Returns (temb, {id(resnet): tp})."""
-        resnets = ([r for r, *_ in self.Downsampling_Blocks] + [r for r, _ in self.Mid_Blocks]
-                   + [r for r, *_ in self.Upsampling_Blocks])
+        (csrc/cfm_prep.hip, csrc/time_mlp.hip) -- or prefetched for this t (prefetch); backward 5.
+        Returns (temb, {id(resnet): tp})."""
+        resnets = self._resnets()
+        pre = self.__dict__.pop("_mtts_time_pre", None)
         with torch.autocast("cuda", enabled=False):
-            e = self.time_embeddings(t)
             if len(resnets) > N_ROWS_MAX_MATS:
                 raise ValueError(f"the fused time path takes up to {N_ROWS_MAX_MATS} Resnet1D blocks")
-            temb, tps = O.time_mlp(e, self.time_mlp.linear_1, self.time_mlp.linear_2, [r.mlp[1] for r in resnets])
+            tt = t.detach().float().reshape(-1)
+            if pre is not None and pre[0] == tt.data_ptr() and pre[1] == tt.numel():
+                torch.cuda.current_stream(tt.device).wait_stream(pre[4])
+                temb, tps = O.time_mlp(pre[2], self.time_mlp.linear_1, self.time_mlp.linear_2,
+                                       [r.mlp[1] for r in resnets], pre=pre[3])
+            else:
+                e = self.time_embeddings(t)
+                temb, tps = O.time_mlp(e, self.time_mlp.linear_1, self.time_mlp.linear_2, [r.mlp[1] for r in resnets])
         return temb, dict(zip(map(id, resnets), tps))
 
     def _forward_tm(self, x, mask, mu, t, packed=None):

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import datetime as dt
 import math
+import os
 import random
 from types import SimpleNamespace
 
@@ -22,6 +23,9 @@ from matcha.models.components import _ops as O
 from matcha.models.components.flow_matching import ConditionalFlowMatching as CFM
 from matcha.models.components.text_encoder import TextEncoder
 from matcha.utils.model import denormalize, fix_len_compatibility, generate_path, sequence_mask
+
+# MTTS_PREFETCH=0: the decoder's weight packs and time path run in place instead of ahead on the side stream
+_PREFETCH = os.environ.get("MTTS_PREFETCH", "1") != "0"
 
 
 class _nullctx:
@@ -108,6 +112,14 @@ class MatchaTTS(BaseLightningClass):
         # caller's precision (bf16 MFMA operands inside a bf16 autocast region) unless encoder_fp32 is set:
         # then it runs exact fp32 MFMA inside bf16-mixed (its activations' bf16 rounding is what is left of
         # the bf16 prior-loss error once the weights enter as split planes -- tools/r3/precision_budget.py)
+        # inside a Trainer step (the gradient deferral's side stream exists): the decoder's weight packs and
+        # time path for this step's CFM time run on the side stream beside the text encoder (t drawn here
+        # instead of in compute_loss; the same distribution)
+        side = O.side_fork() if (x.is_cuda and _PREFETCH) else None
+        if side is not None:
+            if t is None:
+                t = torch.rand([x.shape[0], 1, 1], device=x.device, dtype=torch.float32)
+            self.decoder.estimator.prefetch(t, side)
         with torch.autocast(device_type=x.device.type, enabled=False) if self.encoder_fp32 else _nullctx():
             mu_x, logw, x_mask = self.encoder(x, x_lengths)
         y_max_length = y.shape[-1]
