@@ -61,12 +61,14 @@ __global__ __launch_bounds__(kLThreads) void loss_partials_kernel(const float *_
     float d_acc = 0.f, p_acc = 0.f;
     if (u_pred) {
         const float *ub = u_pred + ((size_t)b * T + t0) * C;
+#pragma unroll 4
         for (int e = threadIdx.x; e < nt * C; e += kLThreads) {
             const int tl = e / C, c = e - tl * C;
             su[tl * kLPitch + c] = ub[e];
         }
         __syncthreads();
     }
+#pragma unroll 4
     for (int e = threadIdx.x; e < C * kLT; e += kLThreads) {
         const int c = e / kLT, tl = e - c * kLT;
         if (tl >= nt) continue;
@@ -129,7 +131,8 @@ __global__ __launch_bounds__(kLThreads) void loss_bwd_kernel(const float *__rest
     const float denom = denom_p[0];
     if (du_pred) {
         // u (channel-major) -> LDS transposed, then du_pred written token-major, coalesced
-        for (int e = threadIdx.x; e < C * kLT; e += kLThreads) {
+    #pragma unroll 4
+    for (int e = threadIdx.x; e < C * kLT; e += kLThreads) {
             const int c = e / kLT, tl = e - c * kLT;
             if (tl < nt) {
                 const size_t i = cm + (size_t)c * T + t0 + tl;
@@ -139,6 +142,7 @@ __global__ __launch_bounds__(kLThreads) void loss_bwd_kernel(const float *__rest
         __syncthreads();
         const float g = 2.f * g_diff[0] / denom;
         const size_t tb = ((size_t)b * T + t0) * C;
+#pragma unroll 4
         for (int e = threadIdx.x; e < nt * C; e += kLThreads) {
             const int tl = e / C, c = e - tl * C;
             du_pred[tb + e] = g * (u_pred[tb + e] - su[tl * kLPitch + c]);
@@ -146,7 +150,8 @@ __global__ __launch_bounds__(kLThreads) void loss_bwd_kernel(const float *__rest
     }
     if (dmu_y) {
         const float g = -g_prior[0] / denom;
-        for (int e = threadIdx.x; e < C * kLT; e += kLThreads) {
+    #pragma unroll 4
+    for (int e = threadIdx.x; e < C * kLT; e += kLThreads) {
             const int c = e / kLT, tl = e - c * kLT;
             if (tl >= nt) continue;
             const size_t i = cm + (size_t)c * T + t0 + tl;

@@ -258,9 +258,15 @@ class _Embedding(torch.autograd.Function):
         V, C = ctx.shape
         gc = g.detach().to(torch.float32).reshape(-1, C).contiguous()
         dw = torch.empty(V, C, dtype=torch.float32, device=gc.device)
+        # the weight gradient is this backward's only output: inside a Trainer step it runs on the gradient
+        # deferral's side stream, beside the final weight-gradient flush (outputs allocated here, inputs kept)
+        side = O.param_grad_side_stream()
+        if side is not None:
+            O.keep_for_side(ids_c, gc)
+        st = side.cuda_stream if side is not None else N.stream_handle(gc.device)
         with torch.cuda.device(gc.device):
             N.check(N.lib().mtts_embedding_bwd(N.ptr(ids_c), N.ptr(gc), ids_c.numel(), V, C, ctx.scale, N.ptr(dw),
-                                               N.stream_handle(gc.device)), "mtts_embedding_bwd")
+                                               st), "mtts_embedding_bwd")
         return None, dw, None
 
 
