@@ -298,3 +298,33 @@ def _ulp2(r):
     """2 ulp of the parameter, or -- where the parameter is smaller than the updates it has received
     (three steps of ~lr = 1e-4 each) -- 2 ulp of that accumulated update."""
     return 2 * torch.finfo(torch.float32).eps * r.abs().clamp_min(4e-4)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_decoder_prefetch_matches_inline(graph):
+    """The decoder's weight packs and time path launched ahead on the side stream (Decoder.prefetch, from
+    MatchaTTS.forward inside a Trainer step) give the same step as running them in place: same kernels on
+    the same inputs, so losses and every parameter after one step are bitwise equal.  t / z are passed in
+    the batch (the Trainer hands them to MatchaTTS.forward, which prefetches for that t)."""
+    import matcha.models.matcha_tts as MT
+    from matcha.training import TrainConfig, Trainer, synthetic_batch
+
+    b = synthetic_batch(4, 20, 80, device=DEV)
+    b = dict(b, t=torch.rand(4, 1, 1, device=DEV), z=torch.randn(4, 80, 80, device=DEV))
+    res = []
+    saved = MT._PREFETCH
+    try:
+        for pf in (True, False):
+            MT._PREFETCH = pf
+            m = _model(5)
+            m.eval()  # dropout off
+            tr = Trainer(m, TrainConfig(graph=graph))
+            logged = tr.step([b]).clone()
+            tr.step([b])
+            torch.cuda.synchronize()
+            res.append((logged, {n: p.detach().clone() for n, p in m.named_parameters()}))
+    finally:
+        MT._PREFETCH = saved
+    assert torch.equal(res[0][0], res[1][0]), (res[0][0], res[1][0])
+    for n in res[0][1]:
+        assert torch.equal(res[0][1][n], res[1][1][n]), n
