@@ -546,7 +546,7 @@ def join_side_streams():
 # The workspaces holding the partials (and the queued GEMMs' inputs) are kept alive until then.  Valid only while nothing reads a
 # parameter gradient before the exit: fresh gradients (AccumulateGrad steals them, no copy kernel) of
 # LEAF weights -- a Function whose weights are not all leaves (ctx.leaf False) sums at once.
-_DEFER = {"on": False, "keep": [], "side_keep": [], "side": {}, "side_used": False,
+_DEFER = {"on": False, "seam": False, "keep": [], "side_keep": [], "side": {}, "side_used": False,
           # MTTS_SIDE_REDUCE=1 (opt-in): once MTTS_SIDE_REDUCE_JOBS sums are queued, they run on a side
           # stream while the backward continues, joined at the context exit.  Measured slower in the
           # captured step (8.68 -> 9.25..9.39 ms for chunks of 12/24/48 jobs, same box), like the
@@ -577,6 +577,7 @@ def deferred_grad_sums(enabled: bool = True):
     lib = N.lib()
     lib.mtts_defer_reductions(1)
     _DEFER["on"] = True
+    _DEFER["seam"] = False
     ok = False
     try:
         yield
@@ -615,6 +616,12 @@ def _maybe_side_sums():
             N.check(lib.mtts_flush_reductions(torch.cuda.current_stream().cuda_stream), "mtts_flush_reductions")
             _DEFER["keep"].clear()  # stream-ordered frees, after the flush launch
         return
+    if _DEFER["on"] and _DEFER["seam"] and _ENC_SIDE_JOBS > 0:
+        # past the decoder/encoder seam: the encoder's own queued gradients go to the side stream in chunks
+        # (MTTS_ENC_SIDE_JOBS), behind the decoder's batch there, instead of all at the end on the main one
+        if N.lib().mtts_pending_reductions() >= _ENC_SIDE_JOBS:
+            flush_deferred_side()
+        return
     if not (_DEFER["on"] and _DEFER["side_on"]):
         return
     lib = N.lib()
@@ -638,6 +645,11 @@ _SIDE_FLUSH = os.environ.get("MTTS_SIDE_FLUSH", "1") != "0"
 # MTTS_SIDE_WGRAD_CAP: workgroups the side-flushed weight-gradient batch may occupy (0 = one per block):
 # fewer leave CUs to the encoder's backward on the main stream (mtts_wgrad_flush_cap)
 _SIDE_CAP = int(os.environ.get("MTTS_SIDE_WGRAD_CAP", "0"))
+# MTTS_ENC_SIDE_JOBS > 0: after the seam flush, side-flush again whenever this many sums are queued -- the
+# text encoder's own weight gradients then queue behind the decoder's batch on the side stream instead of
+# all running on the main one after the encoder's backward (same box: 0 -> 7.20 ms, 8 7.47, 16 7.22,
+# 24 7.12, 32 7.10, 40 7.14, 48 7.11, 64 7.11)
+_ENC_SIDE_JOBS = int(os.environ.get("MTTS_ENC_SIDE_JOBS", "32"))
 
 
 def flush_deferred_side() -> None:
@@ -664,6 +676,7 @@ def flush_deferred_side() -> None:
     _DEFER["side_keep"].extend(_DEFER["keep"])
     _DEFER["keep"].clear()
     _DEFER["side_used"] = True
+    _DEFER["seam"] = True
 
 
 def param_grad_side_stream():
