@@ -291,7 +291,10 @@ def main():
         if os.environ.get("MTTS_BENCH_SHARED_GPU") == "1":
             local = 0
             torch.cuda.set_device(local)
-            dist.init_process_group("gloo")
+            from matcha.dp import stdout_to_stderr
+
+            with stdout_to_stderr():  # gloo's connect message stays off the JSON stdout
+                dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))

@@ -25,6 +25,7 @@ Gradient averaging (mean over ranks) happens in the collective (ncclAvg) or righ
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 
 import torch
@@ -267,3 +268,21 @@ class ArrivalRecorder:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """File descriptor 1 -> 2 for the duration: gloo's rendezvous prints "Rank r is connected to n peer
+    ranks" on stdout, where bench.py's rank 0 prints exactly one JSON line."""
+    import os
+    import sys
+
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)

@@ -216,7 +216,13 @@ class Trainer:
         # a gloo group for the host-side agreements (padded shapes, bucket layout): never syncs the GPU
         self._host_group = None
         if self.dp and self.world > 1:
-            self._host_group = dist.group.WORLD if dist.get_backend() == "gloo" else dist.new_group(backend="gloo")
+            if dist.get_backend() == "gloo":
+                self._host_group = dist.group.WORLD
+            else:
+                from matcha.dp import stdout_to_stderr
+
+                with stdout_to_stderr():  # gloo's connect message stays off the bench's JSON stdout
+                    self._host_group = dist.new_group(backend="gloo")
         if self.dp and self.world > 1:  # identical initial weights on every rank (what DDP's broadcast does)
             for p in model.state_dict().values():
                 dist.broadcast(p, 0)
