@@ -541,8 +541,11 @@ def join_side_streams():
 # deferred_grad_sums() the weight-gradient GEMMs and the norm backwards only QUEUE the fixed-order sums
 # of their partial slabs; the context exit runs the queue as one launch instead of ~120 small ones.
 # The weight-gradient GEMMs themselves are queued too (csrc/conv_gemm.hip, MTTS_DEFER_WGRAD=0 turns it
-# off) and a flush launches them batched -- up to 12 layers per launch, each with its own row split, so
-# the results are bitwise those of per-layer launches -- before their sums.
+# off) and a flush launches them batched -- up to 12 layers per launch, each job keeping its own row split,
+# so a job's slabs are bitwise those of its own launch with the same plan -- before their sums.  The plan
+# itself differs by default (mtts_wgrad_plan_mode(0)): a queued job takes the batched split plan (fewer,
+# longer splits), an immediate one the per-launch plan, so the two round differently (both deterministic);
+# mtts_wgrad_plan_mode(1) gives every job the batched plan (the tests that compare them bitwise set it).
 # The workspaces holding the partials (and the queued GEMMs' inputs) are kept alive until then.  Valid only while nothing reads a
 # parameter gradient before the exit: fresh gradients (AccumulateGrad steals them, no copy kernel) of
 # LEAF weights -- a Function whose weights are not all leaves (ctx.leaf False) sums at once.
@@ -1798,7 +1801,19 @@ def _rows_ws(dev, B, K, ns):
     return t
 
 
+ROWS_MAX_MATS = 8  # include/mtts_decoder.h MTTS_ROWS_MAX_MATS: matrices per rows-linear launch
+
+
+def _chunks(n):
+    return [(i, min(i + ROWS_MAX_MATS, n)) for i in range(0, n, ROWS_MAX_MATS)]
+
+
 def _rows_fwd(x, ws, bs, outs, acts, act):
+    """out_i = x W_i^T + b_i (act_i = act(out_i)); more than ROWS_MAX_MATS matrices run as several launches."""
+    if len(ws) > ROWS_MAX_MATS:
+        for i, j in _chunks(len(ws)):
+            _rows_fwd(x, ws[i:j], bs[i:j], outs[i:j], None if acts is None else acts[i:j], act)
+        return
     B, K = x.shape
     nl = [w.shape[0] for w in ws]
     wsb = _rows_ws(x.device, B, K, nl)
@@ -1809,6 +1824,15 @@ def _rows_fwd(x, ws, bs, outs, acts, act):
 
 
 def _rows_bwd(a, pre, act, ws, dys, dx, dws, dbs):
+    """Backward of _rows_fwd.  More than ROWS_MAX_MATS matrices: one launch per chunk, and the chunks'
+    input gradients (each already times act'(pre)) summed in chunk order."""
+    if len(ws) > ROWS_MAX_MATS:
+        part = None if dx is None else torch.empty_like(dx)
+        for c, (i, j) in enumerate(_chunks(len(ws))):
+            _rows_bwd(a, pre, act, ws[i:j], dys[i:j], dx if c == 0 else part, dws[i:j], dbs[i:j])
+            if c > 0 and dx is not None:
+                dx.add_(part)
+        return
     B, K = a.shape
     nl = [w.shape[0] for w in ws]
     wsb = _rows_ws(a.device, B, K, nl)
@@ -1856,7 +1880,9 @@ class _TimeMLP(torch.autograd.Function):
         # launches leave the critical path for the deferral's side stream (joined before the optimizer)
         side = param_grad_side_stream() if (not ctx.e_grad and g_temb is None) else None
         if side is not None:
-            keep_for_side(e, h1, a1, temb, a2, w1, w2, *ws, *dys, d_temb, dh1)
+            # the outputs too: a gradient autograd drops at once (a frozen weight) must not be handed to
+            # main-stream work while the side kernels still write it
+            keep_for_side(e, h1, a1, temb, a2, w1, w2, *ws, *dys, d_temb, dh1, *dws, *dbs, dw1, db1, dw2, db2)
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             _rows_bwd(a2, temb, ROWS_ACT_MISH, ws, dys, d_temb, dws, dbs)
             if g_temb is not None:  # temb used directly as well (never, on the decoder's path)

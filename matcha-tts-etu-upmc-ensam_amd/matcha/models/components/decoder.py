@@ -27,7 +27,6 @@ _DX_LINK = os.environ.get("MTTS_RESNET_DX_LINK", "1") != "0"
 # MTTS_RESNET_BF16_STORE=0: bf16-mixed keeps the ResNet blocks' conv outputs / GroupNorm outputs in fp32
 # (precision-budget switch, tools/r3/precision_budget.py)
 _RESNET16 = os.environ.get("MTTS_RESNET_BF16_STORE", "1") != "0"
-N_ROWS_MAX_MATS = 8  # include/mtts_decoder.h MTTS_ROWS_MAX_MATS
 
 
 class SinusoidalPosEmb(nn.Module):
@@ -240,8 +239,6 @@ class Decoder(nn.Module):
         uses them (weight_pack_scope, _time_path) -- a Trainer step runs them beside the text encoder."""
         O.prefetch_packs(self, side)
         resnets = self._resnets()
-        if len(resnets) > N_ROWS_MAX_MATS:
-            return
         with torch.autocast("cuda", enabled=False):
             tt = t.detach().float().reshape(-1).contiguous()
             e = torch.empty((tt.numel(), self.time_embeddings.dim), dtype=torch.float32, device=tt.device)
@@ -254,14 +251,13 @@ class Decoder(nn.Module):
 
     def _time_path(self, t):
         """temb = time_mlp(SinusoidalPosEmb(t)) (decoder.py:33-49, :285-286) and every Resnet1D's
-        mlp(temb) = Linear(Mish(temb)) (:80-81), fp32 as the reference keeps it, in 1 + 3 HIP launches
+        mlp(temb) = Linear(Mish(temb)) (:80-81), fp32 as the reference keeps it, in 1 + 3 HIP launches (one
+        more per further 8 blocks)
         (csrc/cfm_prep.hip, csrc/time_mlp.hip) -- or prefetched for this t (prefetch); backward 5.
         Returns (temb, {id(resnet): tp})."""
         resnets = self._resnets()
         pre = self.__dict__.pop("_mtts_time_pre", None)
         with torch.autocast("cuda", enabled=False):
-            if len(resnets) > N_ROWS_MAX_MATS:
-                raise ValueError(f"the fused time path takes up to {N_ROWS_MAX_MATS} Resnet1D blocks")
             tt = t.detach().float().reshape(-1)
             if pre is not None and pre[0] == tt.data_ptr() and pre[1] == tt.numel():
                 torch.cuda.current_stream(tt.device).wait_stream(pre[4])

@@ -186,3 +186,36 @@ def test_matcha_gradients_elementwise_vs_oracle():
         worst = max(worst, err / max(scale, 1e-30))
         assert err <= 2e-4 * scale + 1e-8, (n, err, scale)
     print(f"worst element-wise gradient error / tensor max: {worst:.2e} over {len(want)} tensors")
+
+
+def test_decoder_more_than_eight_resnets_vs_oracle():
+    """channels=(32, 32, 32), num_mid_blocks=3: nine Resnet1D blocks, so the time path's stacked
+    projections run as two rows-linear launches (8 + 1 matrices) forward and backward."""
+    from matcha.models.components.decoder import Decoder
+    from oracle.matcha_oracle import DecoderOracle
+
+    kw = dict(channels=(32, 32, 32), attention_head_dim=16, num_heads=2, num_mid_blocks=3)
+    dec = Decoder(16, 8, **kw).to(DEV)
+    assert len(dec._resnets()) == 9
+    ref = DecoderOracle(16, 8, **kw)
+    apply_recipe(dec, 5)
+    apply_recipe(ref, 5)
+    dec.eval()
+    ref.eval()
+    g = torch.Generator().manual_seed(9)
+    B, T = 2, 48
+    x, mu = torch.randn(B, 8, T, generator=g), torch.randn(B, 8, T, generator=g)
+    mask = (torch.arange(T)[None, None] < torch.tensor([48, 37])[:, None, None]).float()
+    t = torch.rand(B, generator=g)
+    xd, mud = x.to(DEV).requires_grad_(True), mu.to(DEV)
+    u = dec(xd, mask.to(DEV), mud, t.to(DEV))
+    (u.square().sum()).backward()
+    xr = x.clone().requires_grad_(True)
+    ur = ref(xr, mask, mu, t)
+    (ur.square().sum()).backward()
+    assert rel(u.detach().cpu().numpy(), ur.detach().numpy()) < 1e-4
+    assert rel(xd.grad.cpu().numpy(), xr.grad.numpy()) < 1e-3
+    got = dict(dec.named_parameters())
+    for name, p in ref.named_parameters():
+        if "mlp" in name or "time_mlp" in name:  # the chunked time path's weight / bias gradients
+            assert rel(got[name].grad.cpu().numpy(), p.grad.numpy()) < 1e-3, name
