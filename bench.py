@@ -259,7 +259,10 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--tx", type=int, default=120)
     ap.add_argument("--ty", type=int, default=600)
-    ap.add_argument("--precision", default="bf16-mixed", choices=["32-true", "bf16-mixed"])
+    ap.add_argument("--precision", default="bf16-parity", choices=["32-true", "bf16-mixed", "bf16-parity"],
+                    help="bf16-parity (default): bf16-mixed with split bf16 weight planes and the text encoder's "
+                         "forward in bf16x3 -- alignment exact, losses within 1e-4 of 32-true; bf16-mixed: one "
+                         "weight plane (throughput mode, misses the loss bar); 32-true: the reference's precision")
     ap.add_argument("--no-graph", action="store_true", help="eager step (DDP) instead of the captured HIP graph")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -398,8 +401,9 @@ def main():
     synth = None
     if not args.no_synth:
         model.eval()
-        amp = torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.precision == "bf16-mixed")
-        with torch.inference_mode(), amp:
+        amp = torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.precision != "32-true")
+        pol = OPS.parity_policy(args.precision == "bf16-parity")
+        with torch.inference_mode(), amp, pol:
             xs, xls = batch["x"], batch["x_lengths"]
             for _ in range(2):
                 out = model.synthesise(xs, xls, 10, length_scale=5.0)
@@ -422,7 +426,7 @@ def main():
     # test_bench_batch_b32_vs_oracle: recipe weights 43, synthetic batch seed 1000 -- the bench batch --, t / z
     # from a CPU generator seeded 44; the 32-true path equals the CPU oracle there, losses to 0 relative)
     precision_check = None
-    if args.precision == "bf16-mixed" and not args.bucketed and (B, Tx, Ty) == (32, 120, 600):
+    if args.precision != "32-true" and not args.bucketed and (B, Tx, Ty) == (32, 120, 600):
         sys.path.insert(0, str(ROOT / "tests"))
         from golden.weights_recipe import apply_recipe
 
@@ -434,13 +438,15 @@ def main():
         t_inj = torch.rand(32, 1, 1, generator=gen).to(dev)
         z_inj = torch.randn(32, 80, 600, generator=gen).to(dev)
         res = {}
-        modes = (("32-true", "32-true", False, False), ("one_plane", "bf16-mixed", False, False),
-                 ("split_weights", "bf16-mixed", True, False), ("parity_policy", "bf16-mixed", True, True))
+        # (name, autocast, split weight planes, text encoder precision)
+        modes = (("32-true", False, False, "bf16"), ("one_plane", True, False, "bf16"),
+                 ("split_weights", True, True, "bf16"), ("parity_policy", True, True, "bf16x3"),
+                 ("parity_fp32_encoder", True, True, "fp32"))
         with torch.no_grad():
-            for name, prec, split, enc32 in modes:
+            for name, amp_on, split, enc in modes:
                 old = OPS.set_weight_split(split)
-                pm.encoder_fp32 = enc32
-                with torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec == "bf16-mixed"):
+                pm.encoder_precision = enc
+                with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp_on):
                     out = pm(pb["x"], pb["x_lengths"], pb["y"], pb["y_lengths"], t=t_inj, z=z_inj)
                 OPS.set_weight_split(old)
                 res[name] = ([float(v) for v in out[:3]], out[3].detach())
@@ -452,15 +458,19 @@ def main():
             return {"loss_rel_err": [round(abs(a - b) / abs(b), 7) for a, b in zip(l16, l32)],
                     "alignment_cell_agreement": round(float((a16 == a32).float().mean().item()), 6)}
 
+        run_mode = "parity_policy" if args.precision == "bf16-parity" else "one_plane"
         precision_check = {
-            "bf16_loss_rel_err": errs("split_weights" if OPS._W_SPLIT else "one_plane")["loss_rel_err"],
-            "run_mode": "split_weights" if OPS._W_SPLIT else "one_plane",
-            "modes": {k: errs(k) for k in ("one_plane", "split_weights", "parity_policy")},
-            "losses": ["dur", "prior", "diff"], "bar": "prior / diff within 1e-4 relative (north star)",
-            "note": "bf16-mixed vs 32-true (= the oracle at this batch) with the parity tests' recipe weights and "
+            "bf16_loss_rel_err": errs(run_mode)["loss_rel_err"],
+            "run_mode": run_mode,
+            "modes": {k: errs(k) for k in ("one_plane", "split_weights", "parity_policy", "parity_fp32_encoder")},
+            "losses": ["dur", "prior", "diff"],
+            "bar": "alignment bit-exact (agreement 1.0), mel / flow-matching loss within 1e-4 relative (north star)",
+            "note": "bf16 modes vs 32-true (= the oracle at this batch) with the parity tests' recipe weights and "
                     "batch, eval mode, same t / z.  one_plane: bf16 weights (the fp32 weights' rounding is the "
-                    "error); split_weights: hi + rounding-residual bf16 planes (MTTS_W_SPLIT=1); parity_policy: "
-                    "split weights + the text encoder in exact fp32 (MatchaTTS.encoder_fp32)"}
+                    "error); split_weights: hi + rounding-residual bf16 planes; parity_policy (bench default, "
+                    "--precision bf16-parity): split weights + the text encoder's forward in bf16x3 (split A and W "
+                    "operands, fp32 attention forward; backward bf16); parity_fp32_encoder: split weights + the "
+                    "whole text encoder in exact fp32 (round 3's policy)"}
 
     # same-run extra lines (N=1): the reference precision (32-true: exact fp32 MFMA) on the bench workload,
     # and the reference's own step shape -- 2 micro-batches of 16 with gradient accumulation
@@ -468,16 +478,16 @@ def main():
     extra = None
     if world == 1 and not args.no_extra and not args.bucketed and graph:
         extra = {}
-        lines = [("32-true", "32-true", B, 1, False), ("reference_step_16x2", args.precision, B // 2, 2, OPS._W_SPLIT)]
-        if args.precision == "bf16-mixed":
-            lines.append(("bf16_split_weights" if not OPS._W_SPLIT else "bf16_one_plane", args.precision, B, 1,
-                          not OPS._W_SPLIT))
-            lines.append(("bf16_parity_policy", args.precision, B, 1, True))
-        for name, prec, micro, acc, split in lines:
-            old_split = OPS.set_weight_split(split)
+        # (name, Trainer precision, micro-batch, accumulate, MatchaTTS.encoder_precision override)
+        lines = [("32-true", "32-true", B, 1, None), ("reference_step_16x2", args.precision, B // 2, 2, None)]
+        if args.precision != "32-true":
+            lines.append(("bf16_one_plane", "bf16-mixed", B, 1, None) if args.precision == "bf16-parity" else
+                         ("bf16_parity", "bf16-parity", B, 1, None))
+            lines.append(("bf16_parity_fp32_encoder", "bf16-parity", B, 1, "fp32"))
+        for name, prec, micro, acc, enc in lines:
             torch.manual_seed(1234)
             m2 = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(dev).train()
-            m2.encoder_fp32 = name == "bf16_parity_policy"
+            m2.encoder_precision = enc
             tr2 = Trainer(m2, TrainConfig(precision=prec, graph=True, accumulate_grad_batches=acc))
             bs2 = [synthetic_batch(micro, Tx, Ty, seed=2000 + i, device=dev) for i in range(acc)]
             for _ in range(3):
@@ -491,10 +501,10 @@ def main():
             ms2 = (time.perf_counter() - t0x) / n2 * 1e3
             extra[name] = {"ms_per_step": round(ms2, 3), "utterances_per_s": round(micro * acc / ms2 * 1e3, 2),
                            "steps": n2, "precision": prec, "micro_batch": micro, "accumulate_grad_batches": acc,
-                           "weight_planes": 2 if (split and prec == "bf16-mixed") else 1,
+                           "weight_planes": 2 if prec == "bf16-parity" else 1,
+                           "encoder": enc or ("bf16x3" if prec == "bf16-parity" else "as the precision"),
                            "losses": [round(v, 5) for v in tr2.last_losses.tolist()]}
             del tr2, m2
-            OPS.set_weight_split(old_split)
         torch.cuda.empty_cache()
 
     mas_ms = sum(a.elapsed_time(b) for a, b in mas_events) / max(len(mas_events), 1)
@@ -514,9 +524,10 @@ def main():
         """PMC HBM bytes per launch of this family on THIS workload (tools/r3/pmc_families.sh ->
         profiles/<round>/<name>_traffic.json: FETCH_SIZE x2 + WRITE_SIZE, separate passes); PMC passes
         serialise kernels, so they are not collected inside the bench."""
-        if (B, Tx, Ty, args.precision) != (32, 120, 600, "bf16-mixed") or args.bucketed:
+        if (B, Tx, Ty) != (32, 120, 600) or args.precision == "32-true" or args.bucketed:
             return None, None
-        found = sorted(ROOT.glob(f"profiles/r*/{name}_traffic.json"))
+        suffix = "_parity" if args.precision == "bf16-parity" else ""
+        found = sorted(ROOT.glob(f"profiles/r*/{name}_traffic{suffix}.json"))
         if not found:
             return None, None
         return json.loads(found[-1].read_text())["traffic_bytes_per_launch"], str(found[-1].relative_to(ROOT))
@@ -588,7 +599,9 @@ def main():
                        "model": "MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192)",
                        "global_batch": world * B, "seq_len": Ty, "text_len": Tx, "parallelism": f"dp{world}",
                        "precision": args.precision, "hip_graph": graph,
-                       "weight_planes": 2 if (OPS._W_SPLIT and args.precision == "bf16-mixed") else 1,
+                       "weight_planes": 2 if (args.precision == "bf16-parity" or
+                                              (OPS.weight_split_enabled() and args.precision == "bf16-mixed")) else 1,
+                       **({"text_encoder_forward": "bf16x3"} if args.precision == "bf16-parity" else {}),
                        **({"bucketed_batches": [[int(v) for v in (b["x"].shape[1], b["y"].shape[2],
                                                                      b["x_lengths"].min(), b["y_lengths"].min())]
                                                 for b in batches],

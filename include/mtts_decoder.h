@@ -92,6 +92,12 @@ typedef struct mtts_conv_gemm_args {
                                         MFMAs), i.e. the weights enter with ~16 significant bits instead of 8:
                                         the fp32 weights' rounding -- a STATIC perturbation of the model, the
                                         dominant bf16-mixed loss error -- drops out (mtts_pack_job.lo_off packs it) */
+#define MTTS_GEMM_F_A_SPLIT 0x80     /* with MTTS_GEMM_F_W_SPLIT and an fp32 A: A is split on the fly into
+                                        hi = bf16(a) and lo = bf16(a - hi) and every product is
+                                        A_hi*W_hi + A_hi*W_lo + A_lo*W_hi (three bf16 MFMAs, fp32 accumulate):
+                                        ~16 significant bits per operand, the bf16x3 emulation of an fp32 GEMM
+                                        (register-staged schedules; the text encoder's forward in the parity
+                                        policy) */
 
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
 /* Same, with an explicit schedule: 0..17 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;

@@ -96,7 +96,9 @@ struct Stage<false> {
 // round trip, so a longer step halves the exposed latency per MFMA).
 // WS (bf16 only, MTTS_GEMM_F_W_SPLIT): W carries a second bf16 plane (the rounding residual of the fp32
 // weights) at W + N*Kp; it is staged beside the first and every fragment pair issues two MFMAs.
-template <bool BF16, int WM, int WN, int TM, int TN, int KB = kBK, int DEPTH = 1, bool WS = false>
+// AS (with WS, MTTS_GEMM_F_A_SPLIT): the staging pass also writes A's rounding residual bf16(a - bf16(a))
+// as a second A plane, and each fragment triple issues A_hi*W_hi, A_hi*W_lo, A_lo*W_hi (bf16x3).
+template <bool BF16, int WM, int WN, int TM, int TN, int KB = kBK, int DEPTH = 1, bool WS = false, bool AS = false>
 __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_args p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN;
@@ -106,10 +108,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
     static_assert(BM * KC % NT == 0 || NT % (BM * KC) == 0, "tile/threads mismatch");
     static_assert(BF16 || KB == kBK, "fp32 path uses 32-wide K steps");
     static_assert(!WS || BF16, "the split weight planes are bf16");
+    static_assert(!AS || WS, "the split A planes go with split weights");
     using ST = typename Stage<BF16>::T;
     constexpr int LDK = KB + Stage<BF16>::PAD;
     constexpr int BPL = (BN + 1) * LDK;   // one W plane image
-    __shared__ ST As[2][(BM + 1) * LDK];  // + one dummy row: staging target of threads without an A chunk
+    constexpr int APL = (BM + 1) * LDK;   // one A plane image
+    __shared__ ST As[2][(AS ? 2 : 1) * APL];  // + one dummy row: staging target of threads without an A chunk
     __shared__ ST Bs[2][(WS ? 2 : 1) * BPL];
 
     const int tid = threadIdx.x;
@@ -235,6 +239,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
                 w.z = pack_bf16x2(e[4], e[5]);
                 w.w = pack_bf16x2(e[6], e[7]);
                 *reinterpret_cast<uint4 *>(dst) = w;
+                if constexpr (AS) {  // the residual plane: a - bf16(a), exact in fp32, rounded once to bf16
+                    const uint32_t hw[4] = {w.x, w.y, w.z, w.w};
+                    uint32_t lw[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float h0 = __uint_as_float(hw[q] << 16), h1 = __uint_as_float(hw[q] & 0xffff0000u);
+                        lw[q] = pack_bf16x2(e[2 * q] - h0, e[2 * q + 1] - h1);
+                    }
+                    *reinterpret_cast<uint4 *>(dst + APL) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+                }
             } else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) dst[i] = e[i];
@@ -284,6 +298,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
                     for (int j = 0; j < TN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
                 if constexpr (WS) {
+                    bf16x8 bhi[AS ? TN : 1];
+                    if constexpr (AS) {
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) bhi[j] = bfr[j];
+                    }
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
                         bfr[j] = *reinterpret_cast<const bf16x8 *>(
@@ -293,6 +312,17 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
 #pragma unroll
                         for (int j = 0; j < TN; ++j)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                    if constexpr (AS) {
+#pragma unroll
+                        for (int i = 0; i < TM; ++i)
+                            af[i] = *reinterpret_cast<const bf16x8 *>(
+                                &As[buf][APL + (wr * 32 * TM + i * 32 + lr) * LDK + ks * 16 + 8 * lh]);
+#pragma unroll
+                        for (int i = 0; i < TM; ++i)
+#pragma unroll
+                            for (int j = 0; j < TN; ++j)
+                                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bhi[j], acc[i][j], 0, 0, 0);
+                    }
                 }
             }
         } else {
@@ -862,20 +892,27 @@ constexpr TileCfg kCfgs[] = {
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
-template <bool BF16, int C, bool WS = false>
+template <bool BF16, int C, bool WS = false, bool AS = false>
 static void launch_cfg(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
     constexpr TileCfg c = kCfgs[C];
     constexpr int BM = 32 * c.wm * c.tm, BN = 32 * c.wn * c.tn;
     dim3 grid((unsigned)(((M + BM - 1) / BM) * ((p.N + BN - 1) / BN)));
-    hipLaunchKernelGGL((conv_gemm_kernel<BF16, c.wm, c.wn, c.tm, c.tn, (BF16 ? c.kb : kBK), (BF16 ? c.depth : 1), WS>),
+    hipLaunchKernelGGL((conv_gemm_kernel<BF16, c.wm, c.wn, c.tm, c.tn, (BF16 ? c.kb : kBK), (BF16 ? c.depth : 1), WS, AS>),
                        grid, dim3(64 * c.wm * c.wn), 0, st, p);
 }
 
 // Split-weight (MTTS_GEMM_F_W_SPLIT) register schedules: the two the heuristic picks, 7 (32-wide K steps)
-// and 12 (64-wide, two in flight); every other id runs the one with its K step width
+// and 12 (64-wide, two in flight); every other id runs the one with its K step width.  With
+// MTTS_GEMM_F_A_SPLIT the same two with the A residual plane (bf16x3).
 static void launch_ws(int id, const mtts_conv_gemm_args &p, int M, hipStream_t st) {
-    if (kCfgs[id].kb == 64) launch_cfg<true, 12, true>(p, M, st);
-    else launch_cfg<true, 7, true>(p, M, st);
+    const bool as = p.flags & MTTS_GEMM_F_A_SPLIT;
+    if (kCfgs[id].kb == 64) {
+        if (as) launch_cfg<true, 12, true, true>(p, M, st);
+        else launch_cfg<true, 12, true>(p, M, st);
+    } else {
+        if (as) launch_cfg<true, 7, true, true>(p, M, st);
+        else launch_cfg<true, 7, true>(p, M, st);
+    }
 }
 
 template <bool BF16>
@@ -996,6 +1033,9 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
                    "conv_gemm: a bf16 pre-activation needs bf16 precision");
     MTTS_CHECK_ARG(!(p.flags & MTTS_GEMM_F_W_SPLIT) || precision == MTTS_PREC_BF16,
                    "conv_gemm: split weight planes need bf16 precision");
+    MTTS_CHECK_ARG(!(p.flags & MTTS_GEMM_F_A_SPLIT) ||
+                       ((p.flags & MTTS_GEMM_F_W_SPLIT) && !(p.flags & MTTS_GEMM_F_A_BF16)),
+                   "conv_gemm: a split A needs split weight planes and an fp32 A");
     const bool glds_id = cfg >= MTTS_GEMM_GLDS && cfg < MTTS_GEMM_GLDS + mtts::conv_gemm_glds_num_cfgs();
     MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || glds_id, "conv_gemm: bad tile config");
     MTTS_CHECK_ARG(splits >= 0, "conv_gemm: bad split count");
@@ -1014,6 +1054,10 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
         } else if (cfg < MTTS_GEMM_GLDS) {
             return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: a bf16 A needs an LDS-DMA schedule");
         }
+    }
+    if (p.flags & MTTS_GEMM_F_A_SPLIT) {  // bf16x3: register-staged schedules only (the staging pass splits A)
+        if (cfg >= MTTS_GEMM_GLDS) return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: a split A needs a register schedule");
+        if (cfg < 0) cfg = p.K >= 384 ? 12 : 7;
     }
     const GemmPlan pl = plan_gemm(p, bf16, cfg, splits);
     if (pl.cfg >= MTTS_GEMM_GLDS) {

@@ -65,12 +65,58 @@ _FAST_ACT = os.environ.get("MTTS_EXACT_GELU") != "1"
 _W_SPLIT = os.environ.get("MTTS_W_SPLIT", "0") == "1"
 
 
+GEMM_F_A_SPLIT = 0x80  # MTTS_GEMM_F_A_SPLIT: with W_SPLIT, fp32 A split into hi + lo planes (bf16x3)
+# precise_forward(): inside a bf16-mixed region, the forward GEMMs take split weight planes AND split A
+# operands (A_hi W_hi + A_hi W_lo + A_lo W_hi: ~16 significant bits per operand, fp32 accumulate) and the
+# attention forward runs exact fp32 MFMA; the backward of the same ops stays bf16 one-plane.  The
+# text encoder runs this way in the parity policy (MatchaTTS.encoder_precision = "bf16x3"): its
+# activations' bf16 rounding decides the alignment's near-ties (tools/r3/precision_budget.py).
+_PRECISE: contextvars.ContextVar = contextvars.ContextVar("mtts_precise_fwd", default=False)
+
+
+@contextlib.contextmanager
+def precise_forward(on: bool = True):
+    tok = _PRECISE.set(bool(on))
+    try:
+        yield
+    finally:
+        _PRECISE.reset(tok)
+
+
 def set_weight_split(on: bool) -> bool:
     """Selects one (False) or two (True) bf16 weight planes for the bf16-mixed forward GEMMs from the next
     forward on; returns the previous setting.  (Captured graphs keep the packing they were captured with.)"""
     global _W_SPLIT
     old, _W_SPLIT = _W_SPLIT, bool(on)
     return old
+
+
+_WSPLIT_CV: contextvars.ContextVar = contextvars.ContextVar("mtts_w_split", default=None)
+# the text encoder's precision inside bf16-mixed when the model does not set its own
+# (MatchaTTS.encoder_precision): "bf16", "bf16x3" (precise_forward) or "fp32"
+_ENC_PREC: contextvars.ContextVar = contextvars.ContextVar("mtts_encoder_precision", default="bf16")
+
+
+def weight_split_enabled() -> bool:
+    v = _WSPLIT_CV.get()
+    return _W_SPLIT if v is None else v
+
+
+@contextlib.contextmanager
+def parity_policy(on: bool = True):
+    """bf16-parity inside a bf16 autocast region (the Trainer's "bf16-parity" precision): split weight
+    planes for every forward GEMM and the text encoder's forward in bf16x3 (precise_forward)."""
+    t1 = _WSPLIT_CV.set(True if on else None)
+    t2 = _ENC_PREC.set("bf16x3" if on else "bf16")
+    try:
+        yield
+    finally:
+        _ENC_PREC.reset(t2)
+        _WSPLIT_CV.reset(t1)
+
+
+def encoder_precision_default() -> str:
+    return _ENC_PREC.get()
 PACK_BF16_SPLIT = 2  # pack-cache kind: the bf16 hi + lo planes of a forward operand
 
 GEMM_GLDS = 32  # MTTS_GEMM_GLDS: first LDS-DMA schedule id
@@ -320,7 +366,7 @@ def _run_pack(specs, prec, stream=None):
 
 def _pack_kind(spec: PackSpec, prec: int) -> int:
     """bf16 forward operands: the split planes when selected (set_weight_split); everything else as prec."""
-    return PACK_BF16_SPLIT if (prec == PREC_BF16 and _W_SPLIT and not spec.dgrad) else prec
+    return PACK_BF16_SPLIT if (prec == PREC_BF16 and (weight_split_enabled() or _PRECISE.get()) and not spec.dgrad) else prec
 
 
 _PACK_SCOPE: contextvars.ContextVar = contextvars.ContextVar("mtts_pack_scope", default=None)
@@ -450,6 +496,10 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     if Wp.dim() != 2 or Wp.shape[0] < N_ or Wp.shape[1] != Kp or Kp < len(offs) * cin:
         raise ValueError(f"packed weight {tuple(Wp.shape)} does not cover N={N_}, Kp={Kp}, K={len(offs) * cin}")
     w_split = getattr(Wp, "_mtts_w_split", False) and prec == PREC_BF16
+    # bf16x3 (precise_forward): the split weights' GEMM also splits its fp32 A operand -- register schedules
+    a_split = w_split and _PRECISE.get() and A.dtype == torch.float32
+    if a_split:
+        tile_cfg, splits = (tile_cfg if 0 <= tile_cfg < GEMM_GLDS else -1), 1
     if w_split and Wp.shape[0] != 2 * N_:
         raise ValueError(f"split weight planes {tuple(Wp.shape)}: the lo plane must start at row N={N_}")
     if C.shape[-1] < N_ or C.numel() < nb * To_full * C.shape[-1] or A.shape[-1] < cin:
@@ -481,7 +531,7 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
                   | (GEMM_F_C_BF16 if C.dtype == torch.bfloat16 else 0)
                   | (GEMM_F_FAST_ACT if (prec == PREC_BF16 and _FAST_ACT) else 0)
                   | (GEMM_F_PRE_BF16 if any(t is not None and t.dtype == torch.bfloat16 for t in (C_pre, aux)) else 0)
-                  | (GEMM_F_W_SPLIT if w_split else 0))
+                  | (GEMM_F_W_SPLIT if w_split else 0) | (GEMM_F_A_SPLIT if a_split else 0))
     if C_pre is not None and aux is not None and C_pre.dtype != aux.dtype:
         raise ValueError("C_pre and aux must share a dtype")
     log = LAUNCH_LOG
@@ -1412,7 +1462,8 @@ class _AttentionTM(torch.autograd.Function):
         o = torch.empty(B, T, C3 // 3, device=qkv.device, dtype=torch.float32)
         lse = torch.empty(B, heads, T, device=qkv.device, dtype=torch.float32)
         seed = _new_seed(qkv.device) if dropout_p > 0 else None
-        _attn_fwd(qkv, bias, o, lse, heads, prec, dropout_p, seed)
+        # precise_forward: exact-fp32 MFMA forward (fp32 q|k|v here), the backward in the region's bf16
+        _attn_fwd(qkv, bias, o, lse, heads, PREC_FP32 if _PRECISE.get() else prec, dropout_p, seed)
         ctx.save_for_backward(qkv, bias, o, lse)
         ctx.heads, ctx.prec, ctx.drop = heads, prec, (dropout_p, seed)
         return o

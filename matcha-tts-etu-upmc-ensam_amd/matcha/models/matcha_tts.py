@@ -37,7 +37,19 @@ class _nullctx:
 
 
 class MatchaTTS(BaseLightningClass):
-    encoder_fp32 = False  # bf16-mixed: run the text encoder in exact fp32 (the parity policy, see forward)
+    # text encoder precision inside a bf16-mixed region (see forward): "bf16" (autocast's), "bf16x3" (forward
+    # GEMMs as split bf16 operands A_hi W_hi + A_hi W_lo + A_lo W_hi and an fp32 attention forward, backward
+    # bf16: the parity policy), "fp32" (exact fp32 MFMA forward and backward)
+    # None: the ambient default (_ops.parity_policy sets "bf16x3", otherwise "bf16")
+    encoder_precision = None
+
+    @property
+    def encoder_fp32(self) -> bool:
+        return self.encoder_precision == "fp32"
+
+    @encoder_fp32.setter
+    def encoder_fp32(self, on: bool) -> None:
+        self.encoder_precision = "fp32" if on else None
 
     def __init__(self, n_vocab, n_feats=None, encoder=None, decoder=None, cfm=None, data_statistics=None,
                  out_size=None, optimizer=None, scheduler=None, prior_loss=True, use_precomputed_durations=False,
@@ -109,9 +121,10 @@ class MatchaTTS(BaseLightningClass):
         """Returns (dur_loss, prior_loss, diff_loss, attn) -- matcha_tts.py:247-325.  ``t``/``z``
         (keyword-only) inject the CFM randomness for parity tests."""
         # the text encoder runs on the same HIP GEMM/attention kernels as the decoder and follows the
-        # caller's precision (bf16 MFMA operands inside a bf16 autocast region) unless encoder_fp32 is set:
-        # then it runs exact fp32 MFMA inside bf16-mixed (its activations' bf16 rounding is what is left of
-        # the bf16 prior-loss error once the weights enter as split planes -- tools/r3/precision_budget.py)
+        # caller's precision (bf16 MFMA operands inside a bf16 autocast region) unless encoder_precision says
+        # otherwise: "bf16x3" / "fp32" take its activations' bf16 rounding -- what is left of the bf16 prior-loss
+        # error and every alignment flip once the weights enter as split planes (tools/r3/precision_budget.py)
+        # -- out of the forward
         # inside a Trainer step (the gradient deferral's side stream exists): the decoder's weight packs and
         # time path for this step's CFM time run on the side stream beside the text encoder (t drawn here
         # instead of in compute_loss; the same distribution)
@@ -120,7 +133,14 @@ class MatchaTTS(BaseLightningClass):
             if t is None:
                 t = torch.rand([x.shape[0], 1, 1], device=x.device, dtype=torch.float32)
             self.decoder.estimator.prefetch(t, side)
-        with torch.autocast(device_type=x.device.type, enabled=False) if self.encoder_fp32 else _nullctx():
+        enc_prec = self.encoder_precision or O.encoder_precision_default()
+        if enc_prec == "fp32":
+            enc_ctx = torch.autocast(device_type=x.device.type, enabled=False)
+        elif enc_prec == "bf16x3":
+            enc_ctx = O.precise_forward()
+        else:
+            enc_ctx = _nullctx()
+        with enc_ctx:
             mu_x, logw, x_mask = self.encoder(x, x_lengths)
         y_max_length = y.shape[-1]
         y_mask = O.sequence_mask_f32(y_lengths, y_max_length).unsqueeze(1)  # sequence_mask(...).to(x_mask), one launch

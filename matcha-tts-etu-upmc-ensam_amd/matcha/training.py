@@ -169,7 +169,10 @@ class TrainConfig:
     accumulate_grad_batches: int = 1
     gradient_clip_val: float = 1.0
     bucket_mb: float = 25.0  # DDP buckets (eager) and the graph step's all-reduce buckets
-    precision: str = "32-true"  # "32-true" (reference) or "bf16-mixed"
+    # "32-true" (reference), "bf16-mixed" (autocast), or "bf16-parity": bf16-mixed with split bf16 weight
+    # planes and the text encoder's forward in bf16x3 -- alignment exact, losses within 1e-4 of 32-true
+    # (tests/test_headline_gpu.py; _ops.parity_policy)
+    precision: str = "32-true"
     graph: bool = False
     lr: float = 1e-4
     eta_min: float = 1e-6
@@ -249,8 +252,12 @@ class Trainer:
 
     # ------------------------------------------------------------------------------------ common
     def _autocast(self):
-        if self.cfg.precision == "bf16-mixed" and self.dev.type == "cuda":
-            return torch.autocast(device_type="cuda", dtype=torch.bfloat16)
+        if self.cfg.precision in ("bf16-mixed", "bf16-parity") and self.dev.type == "cuda":
+            st = contextlib.ExitStack()
+            st.enter_context(torch.autocast(device_type="cuda", dtype=torch.bfloat16))
+            if self.cfg.precision == "bf16-parity":
+                st.enter_context(OPS.parity_policy())
+            return st
         return contextlib.nullcontext()
 
     def _fwd_bwd(self, batches, sync_ctx=None):

@@ -7,18 +7,18 @@ precisions.
   itself pinned to the reference fixtures) on the same weights, tokens, mels, t and z.
 
 32-true: alignment bit-exact, each loss within 1e-4 relative (the north star's bar).
-bf16-parity (bf16-mixed with split bf16 weight planes, MTTS_GEMM_F_W_SPLIT, and the text encoder in exact
-fp32, MatchaTTS.encoder_fp32): prior / diff loss within the same 1e-4 bar (BAR_RTOL) -- the error budget
-(tools/r3/precision_budget.py, profiles/r03/precision/) traced the bf16 loss error to the static rounding
-of the fp32 weights (split planes remove it) and, at 512 x 4096, the encoder's activation rounding.
-bf16-mixed one plane (bench.py's throughput line): measured 2.3e-4 .. 3.3e-4 (prior / diff at B=32,
-512x4096) -> bound 5e-4, documented as missing the bar.  Duration loss in every bf16 mode: MAS boundary
-flips -- 3e-3 (B=32), 9.9e-2 (B=4) with one plane -> bound 0.15.
-The duration loss is the sensitive one: it compares logw with log(durations of the MAS path), and
-the MAS is an argmax -- under the bf16 lattice perturbation near-tied DP decisions flip and move
-row boundaries by a frame (B=4: 28 of 437 rows changed duration, 0.5 % of the path cells), which
-moves log(duration) by up to log 2 for short rows.  The alignment is therefore compared cell by cell
-(BF16_ATTN_AGREE).
+bf16-parity (the bench default since round 4): bf16-mixed with split bf16 weight planes
+(MTTS_GEMM_F_W_SPLIT: the fp32 weights' static rounding -- the dominant bf16 loss error, tools/r3/
+precision_budget.py -- drops out) and the text encoder's FORWARD in bf16x3 (MTTS_GEMM_F_A_SPLIT: split A
+operands as well, A_hi W_hi + A_hi W_lo + A_lo W_hi; attention forward on the fp32 MFMA), backward bf16:
+the encoder's activation rounding decided every alignment near-tie.  Bar: alignment bit-exact and every
+loss (duration included) within 1e-4 relative.  bf16-parity-fp32enc: round 3's policy (the whole encoder
+in exact fp32), same bar.
+bf16-mixed one plane (the throughput mode): measured 2.3e-4 .. 3.3e-4 (prior / diff at B=32, 512x4096)
+-> bound 5e-4, documented as missing the bar; its duration loss moves with MAS boundary flips (3e-3 at
+B=32, 9.9e-2 at B=4 -> bound 0.15) -- under a perturbed lattice near-tied DP decisions flip and move row
+boundaries by a frame, which moves log(duration) by up to log 2 for short rows, so its alignment is
+compared cell by cell (BF16_ATTN_AGREE).
 """
 from __future__ import annotations
 
@@ -35,25 +35,40 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 GH = np.load(Path(__file__).parent / "golden" / "headline_golden.npz")
 FP32_LOSS_RTOL = 1e-4       # north star: mel / flow-matching loss within 1e-4 relative
-BAR_RTOL = np.array([0.15, 1e-4, 1e-4])        # bf16-parity: (dur, prior, diff) -- prior / diff at the bar
+PARITY_RTOL = np.array([1e-4, 1e-4, 1e-4])    # bf16-parity (dur, prior, diff): every loss at the bar
 BF16_LOSS_RTOL = np.array([0.15, 5e-4, 5e-4])  # bf16-mixed, one weight plane: measured, misses the bar
-BF16_ATTN_AGREE = 0.99      # fraction of [Tx, Ty] alignment cells equal to the fp32 reference path
+BF16_ATTN_AGREE = 0.99      # one plane: fraction of [Tx, Ty] alignment cells equal to the fp32 reference path
+# precision -> (bf16 autocast, split weight planes, MatchaTTS.encoder_precision)
+MODES = {"32-true": (False, False, "bf16"), "bf16-mixed": (True, False, "bf16"),
+         "bf16-parity": (True, True, "bf16x3"), "bf16-parity-fp32enc": (True, True, "fp32")}
+PARITY_MODES = ("bf16-parity", "bf16-parity-fp32enc")
 
 
 def run_precision(model, precision, fn):
-    """fn() under `precision`: 32-true, bf16-mixed (one weight plane) or bf16-parity (split weight planes +
-    the encoder in fp32)."""
+    """fn() under `precision` (MODES): 32-true; bf16-mixed (one weight plane); bf16-parity (split weight
+    planes + the text encoder's forward in bf16x3, its attention forward in fp32 -- the bench default);
+    bf16-parity-fp32enc (split weight planes + the whole text encoder in exact fp32, round 3's policy)."""
     from matcha.models.components import _ops as O
 
-    parity = precision == "bf16-parity"
-    old = O.set_weight_split(parity)
-    model.encoder_fp32 = parity
+    amp, split, enc = MODES[precision]
+    old = O.set_weight_split(split)
+    model.encoder_precision = enc
     try:
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=precision != "32-true"):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             return fn()
     finally:
         O.set_weight_split(old)
-        model.encoder_fp32 = False
+        model.encoder_precision = "bf16"
+
+
+def check_bf16(precision, err, agree):
+    """The at-bar modes: alignment bit-exact, every loss within 1e-4; one plane: the measured bounds."""
+    if precision in PARITY_MODES:
+        assert agree == 1.0, f"{precision}: alignment not exact ({agree})"
+        assert (err <= PARITY_RTOL).all(), err
+    else:
+        assert (err <= BF16_LOSS_RTOL).all(), err
+        assert agree >= BF16_ATTN_AGREE
 
 
 def _run(model, x, xl, y, yl, t, z, precision):
@@ -86,7 +101,7 @@ def _agree(attn, ref_attn, xl, yl):
     return same / total
 
 
-@pytest.mark.parametrize("precision", ["32-true", "bf16-mixed", "bf16-parity"])
+@pytest.mark.parametrize("precision", list(MODES))
 def test_headline_b4_vs_reference(precision):
     model = _product(41)
     g = lambda k: torch.from_numpy(GH[k]).to(DEV)  # noqa: E731
@@ -117,8 +132,7 @@ def test_headline_b4_vs_reference(precision):
         dur32 = ref_attn.astype(np.int64).sum(-1)
         print(f"bf16 alignment agreement {agree:.5f}; rows whose duration moved {(dur16 != dur32).sum()} of "
               f"{int(xl.sum())}; max |logw16 - logw32| {d_logw:.4f}; mu_x rel err {r_mu:.2e}")
-        assert (err <= (BAR_RTOL if precision == "bf16-parity" else BF16_LOSS_RTOL)).all(), err
-        assert agree >= BF16_ATTN_AGREE
+        check_bf16(precision, err, agree)
 
 
 _B32 = {}
@@ -148,7 +162,7 @@ def _oracle_b32():
     return _B32
 
 
-@pytest.mark.parametrize("precision", ["32-true", "bf16-mixed", "bf16-parity"])
+@pytest.mark.parametrize("precision", list(MODES))
 def test_bench_batch_b32_vs_oracle(precision):
     o = _oracle_b32()
     model = _product(43)
@@ -162,6 +176,5 @@ def test_bench_batch_b32_vs_oracle(precision):
         np.testing.assert_array_equal(attn.astype(np.int8), o["attn"])
         assert (err <= FP32_LOSS_RTOL).all(), err
     else:
-        assert (err <= (BAR_RTOL if precision == "bf16-parity" else BF16_LOSS_RTOL)).all(), err
-        assert agree >= BF16_ATTN_AGREE
+        check_bf16(precision, err, agree)
     assert all(p.grad is None or torch.isfinite(p.grad).all() for p in model.parameters())

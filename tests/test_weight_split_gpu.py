@@ -6,6 +6,8 @@ activations and UNROUNDED fp32 weights, on each schedule family the forward uses
 (fp32 and bf16 A, 64 x 64 and 64 x 256 tiles, split-K), the register-staged GELU schedule."""
 from __future__ import annotations
 
+import contextlib
+
 import pytest
 import torch
 
@@ -83,3 +85,62 @@ def test_split_weight_packing_planes():
     assert torch.equal(hi, w.bfloat16().float())
     assert torch.equal(lo, (w - hi).bfloat16().float())
     assert ((hi + lo) - w).abs().max().item() <= 2 ** -16 * w.abs().max().item()
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout,k,cfg", [(32, 120, 192, 192, 5, -1), (4, 120, 192, 576, 1, -1),
+                                                (8, 120, 768, 192, 3, -1), (8, 120, 192, 768, 3, 7),
+                                                (8, 120, 192, 768, 3, 12), (3, 37, 256, 80, 1, -1)])
+def test_split_a_bf16x3_vs_float64(B, T, Cin, Cout, k, cfg):
+    """MTTS_GEMM_F_A_SPLIT (precise_forward): fp32 activations (NOT bf16-exact) and fp32 weights, both split
+    into hi + lo bf16 planes, A_hi W_hi + A_hi W_lo + A_lo W_hi -- an fp32 GEMM to ~2^-16 of the operands
+    (float64 reference); the one-A-plane result (bf16 activations) is far off, so the check has teeth.  The
+    text encoder's shapes (M = 32 x 120: prenet k = 5, q|k|v, FFN k = 3 both ways, mean projection) on both
+    register schedules."""
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator().manual_seed(B * Cout + k)
+    x = torch.randn(B, T, Cin, generator=g).to(DEV)
+    w = (torch.randn(Cout, Cin, k, generator=g) / (Cin * k) ** 0.5).to(DEV)
+    b = torch.randn(Cout, generator=g).to(DEV)
+    m = (torch.arange(T)[None] < torch.randint(T // 2, T + 1, (B,), generator=g)[:, None]).float().to(DEV)
+    ref = torch.nn.functional.conv1d((x * m[..., None]).double().transpose(1, 2), w.double(), b.double(),
+                                     padding=k // 2).transpose(1, 2)
+    Wp, Kp = O.packed(O.spec_conv_fwd(w), O.PREC_BF16)
+    assert Wp._mtts_w_split
+    y = torch.empty(B, T, Cout, device=DEV)
+    with O.precise_forward():
+        O._gemm(x, T, T, B, 1, [j - k // 2 for j in range(k)], Cin, Wp, Kp, Cout, y, T, prec=O.PREC_BF16,
+                a_scale=m, bias=b, tile_cfg=cfg)
+    assert _err(y, ref) < 3e-5, _err(y, ref)
+    y1 = torch.empty_like(y)  # split weights, one A plane: the activations' bf16 rounding
+    O._gemm(x, T, T, B, 1, [j - k // 2 for j in range(k)], Cin, Wp, Kp, Cout, y1, T, prec=O.PREC_BF16,
+            a_scale=m, bias=b, tile_cfg=cfg if cfg >= 0 else 12)
+    assert _err(y1, ref) > 10 * _err(y, ref)
+
+
+def test_precise_forward_encoder_backward_stays_bf16():
+    """The text encoder under precise_forward: forward GEMMs bf16x3 (their outputs within ~1e-5 of the fp32
+    encoder's), the backward unchanged from the bf16-mixed one (same gradients to bf16 accuracy)."""
+    from golden.weights_recipe import apply_recipe
+    from matcha.models.components import _ops as O
+    from matcha.models.matcha_tts import MatchaTTS
+    from matcha.training import synthetic_batch
+
+    model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(DEV)
+    apply_recipe(model, 21)
+    model.eval()
+    bt = synthetic_batch(8, 120, 600, seed=3, device=DEV)
+    outs = {}
+    for mode in ("fp32", "bf16x3", "bf16"):
+        model.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode != "fp32"), \
+                (O.precise_forward() if mode == "bf16x3" else contextlib.nullcontext()):
+            mu, logw, _ = model.encoder(bt["x"], bt["x_lengths"])
+        (mu.square().sum() + logw.square().sum()).backward()
+        outs[mode] = (mu.detach().float(), logw.detach().float(),
+                      model.encoder.encoder.ffn_layers[2].conv_net[0].weight.grad.clone())
+    r = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
+    assert r(outs["bf16x3"][0], outs["fp32"][0]) < 2e-5, r(outs["bf16x3"][0], outs["fp32"][0])
+    assert r(outs["bf16x3"][1], outs["fp32"][1]) < 2e-5
+    assert r(outs["bf16"][0], outs["fp32"][0]) > 10 * r(outs["bf16x3"][0], outs["fp32"][0])
+    assert r(outs["bf16x3"][2], outs["fp32"][2]) < 3e-2  # bf16 backward
