@@ -484,11 +484,19 @@ def main():
             lines.append(("bf16_one_plane", "bf16-mixed", B, 1, None) if args.precision == "bf16-parity" else
                          ("bf16_parity", "bf16-parity", B, 1, None))
             lines.append(("bf16_parity_fp32_encoder", "bf16-parity", B, 1, "fp32"))
+        # the data-parallel step's own cost on one GPU: a world-size-1 RCCL group, the bucketed in-graph
+        # all-reduces (copies at one rank), the per-bucket side-stream weight-gradient flushes and packing
+        lines.append(("dp_forced_n1", args.precision, B, 1, None))
         for name, prec, micro, acc, enc in lines:
+            if name == "dp_forced_n1" and not dist.is_initialized():
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ["MASTER_PORT"] = str(_free_port())
+                dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
             torch.manual_seed(1234)
             m2 = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(dev).train()
             m2.encoder_precision = enc
-            tr2 = Trainer(m2, TrainConfig(precision=prec, graph=True, accumulate_grad_batches=acc))
+            tr2 = Trainer(m2, TrainConfig(precision=prec, graph=True, accumulate_grad_batches=acc,
+                                          force_dp=name == "dp_forced_n1"))
             bs2 = [synthetic_batch(micro, Tx, Ty, seed=2000 + i, device=dev) for i in range(acc)]
             for _ in range(3):
                 tr2.step(bs2)
@@ -503,6 +511,9 @@ def main():
                            "steps": n2, "precision": prec, "micro_batch": micro, "accumulate_grad_batches": acc,
                            "weight_planes": 2 if prec == "bf16-parity" else 1,
                            "encoder": enc or ("bf16x3" if prec == "bf16-parity" else "as the precision"),
+                           **({"dp": {"ranks": int(tr2.reducer.comm.ranks), "buckets": len(tr2.reducer.buckets),
+                                      "overlapped_in_graph": bool(next(iter(tr2._graphs.values()))["overlap"])}}
+                              if tr2.reducer is not None else {}),
                            "losses": [round(v, 5) for v in tr2.last_losses.tolist()]}
             del tr2, m2
         torch.cuda.empty_cache()

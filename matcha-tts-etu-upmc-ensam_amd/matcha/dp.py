@@ -8,10 +8,12 @@ collectives INSIDE its HIP graph, which torch's ProcessGroupNCCL cannot provide 
 
 * ``GradBucketReducer`` lays every differentiated parameter's gradient out in one flat fp32 buffer,
   in the order backward produces them (recorded in a warm-up pass), cut into ~``bucket_mb`` buckets.
-  A post-accumulate-grad hook counts each bucket's gradients; when the last one lands, the bucket is
-  packed (one ``torch.cat`` into its flat slice, after flushing the deferred weight-gradient sums
-  that produce them) and handed to the communicator on a side stream -- captured, that is a forked
-  branch of the graph, so the reduction of bucket k runs while backward computes bucket k+1.
+  A post-accumulate-grad hook counts each bucket's gradients; when the last one lands, the queued
+  weight-gradient GEMMs / sums that produce them are flushed onto the deferral's side stream and the
+  bucket is packed (one ``torch.cat`` into its flat slice) and reduced on the reducer's stream after
+  both the main and the side stream -- captured, that is a forked branch of the graph, so the reduction
+  of bucket k runs while backward computes bucket k+1, and the main stream never waits for the side
+  stream's weight gradients (the N=1 step's decoder / encoder seam overlap is kept).
   Buckets are issued strictly in index order on every rank (RCCL requires one collective order).
   The step's logged scalars ride in the last bucket: one collective for everything
   (baselightningmodule.py:117-199 issues one sync_dist all-reduce per logged value).
@@ -160,12 +162,14 @@ class GradBucketReducer:
         self.grad_refs = None  # the gradient tensors packed in the last armed pass
 
     # -------------------------------------------------------------------- per step
-    def arm(self, scalars: torch.Tensor, overlap: bool) -> None:
+    def arm(self, scalars: torch.Tensor, overlap: bool, comm: bool = True) -> None:
         """Call before the backward of the last micro-batch.  ``scalars``: the 4 logged values
-        (already the micro-batch mean).  overlap=False packs only; the caller reduces after."""
+        (already the micro-batch mean).  overlap=False packs only; the caller reduces after.  comm=False
+        packs only and never communicates (a graph capture's warm-up passes: a rank may capture a new
+        shape while its peers replay, so only replays may issue collectives)."""
         self.armed = True
         capturing = self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
-        self.overlap = overlap and self.comm is not None and (self.comm.capturable or not capturing)
+        self.overlap = (comm and overlap and self.comm is not None and (self.comm.capturable or not capturing))
         self._pending_scalars = scalars
         self._ready = [0] * len(self.buckets)
         self._issued = 0
@@ -186,26 +190,43 @@ class GradBucketReducer:
             self._issue(k)
             self._issued += 1
 
-    def _issue(self, k: int) -> None:
-        from matcha.models.components import _ops as OPS
-
-        OPS.flush_deferred_grad_sums()  # the bucket's weight gradients may still be queued sums
+    def _pack(self, k: int) -> None:
         s, e = self.buckets[k]
-        lo, hi = self.spans[k]
+        lo, _ = self.spans[k]
         grads = [self.grad_refs[i].reshape(-1) for i in range(s, e)]
         n = self.offsets[e] - lo if e < len(self.params) else self.n_grad - lo
         if grads:
             torch.cat(grads, out=self.flat[lo:lo + n])
         if k == len(self.buckets) - 1:
             self.flat[self.n_grad:].copy_(self._pending_scalars)
-        if self.overlap:
-            cur = torch.cuda.current_stream(self.device) if self.stream is not None else None
-            if cur is not None:
-                self.stream.wait_stream(cur)
-                with torch.cuda.stream(self.stream):
-                    self.comm.all_reduce_mean_(self.flat[lo:hi])
-            else:
+
+    def _issue(self, k: int) -> None:
+        from matcha.models.components import _ops as OPS
+
+        lo, hi = self.spans[k]
+        if self.overlap and self.stream is not None:
+            # the bucket's weight gradients may still be queued: they run on the deferral's side stream
+            # (joined at the deferral's exit); pack + all-reduce here wait for the main and the side stream
+            side = OPS.flush_for_bucket()
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+            if side is not None:
+                self.stream.wait_stream(side)
+            with torch.cuda.stream(self.stream):
+                self._pack(k)
                 self.comm.all_reduce_mean_(self.flat[lo:hi])
+            return
+        OPS.flush_deferred_grad_sums()  # on the current stream (joins the side stream first)
+        self._pack(k)
+        if self.overlap:  # CPU (gloo): eager, in order
+            self.comm.all_reduce_mean_(self.flat[lo:hi])
+
+    def warm(self) -> None:
+        """One eager all-reduce per bucket span on every rank (all ranks call this together, when the
+        reducer is built): RCCL sets up its connections for each message size on first use, which must not
+        happen later inside one rank's graph capture while its peers replay."""
+        for lo, hi in self.spans:
+            self.comm.all_reduce_mean_(self.flat[lo:hi])
+        self.flat.zero_()
 
     def finish(self) -> None:
         """After the armed backward: every bucket issued, the current stream joined with the reductions

@@ -755,6 +755,20 @@ def keep_for_side(*ts) -> None:
     _DEFER["side_keep"].extend(t for t in ts if t is not None)
 
 
+def flush_for_bucket():
+    """Inside deferred_grad_sums(), before a data-parallel bucket is packed: every queued weight gradient
+    and sum runs now -- on the deferral's side stream when the seam flush is on (the main stream goes on
+    with the backward; the seam overlap of the N=1 step is kept), else on the main stream.  Returns the side
+    stream whose work so far the packer must wait for (None: everything is ordered on the main stream)."""
+    if not _DEFER["on"]:
+        return None
+    if _SIDE_FLUSH and not _DEFER["side_on"]:
+        flush_deferred_side()
+        return _DEFER["side"].get(torch.cuda.current_device()) if _DEFER["side_used"] else None
+    flush_deferred_grad_sums()
+    return None
+
+
 def flush_deferred_grad_sums() -> None:
     """Runs the queued parameter-gradient sums now (inside deferred_grad_sums(); no-op outside): the
     data-parallel reducer calls it before packing a bucket, so the deferral still batches the sums of

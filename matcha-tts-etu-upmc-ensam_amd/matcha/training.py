@@ -24,11 +24,14 @@ Two execution modes:
   graph=False (eager): torch DDP over RCCL (bucketed all-reduce overlapped with backward, no_sync for
     non-final accumulation micro-batches), or the same bucket reducer (dp="buckets").
 
-N>1 graph step: every rank must replay a graph with the same collective sequence, and capturing runs
-warm-up steps that communicate, so the ranks agree on each step's padded shapes first (one small host
-all-reduce over a gloo group, MAX of the padded Tx / Ty; each rank zero-pads to it -- only masked frames
-are added, as collate's quanta do) and therefore capture, replay and evict together.  The bucket layout
-is rank 0's recorded backward order, broadcast once.
+N>1 graph step: every replay issues the same collective sequence (the buckets of one fixed layout -- rank
+0's recorded backward order, broadcast once -- in bucket order), whatever shape a rank's batch has; a
+capture's warm-up passes never communicate (the reducer packs only), and the communicator's connections
+are set up once by an eager all-reduce per bucket on every rank when the reducer is built.  So each rank
+pads its batch to its own length, as the reference's DDP would, and captures new shapes on its own.
+(TrainConfig.agree_shapes=True instead pads every rank to the MAX padded Tx / Ty over ranks -- one host
+all-reduce per step -- so all ranks share one shape key; the extra padding changes the padded-length
+dependent parts of the arithmetic: GroupNorm statistics, conv bias leaking into padded frames.)
 
 Synthetic LJSpeech-shaped batches: token ids ~ U{1..149}, lengths ~ U[0.7 max, max]
 with element 0 = max, mels ~ N(0, 1) zeroed past the length.  A batch dict may carry "t" [B, 1, 1] and
@@ -184,8 +187,12 @@ class TrainConfig:
     graph_cache: int = 4
     dp: str = "auto"  # N>1 exchange: "ddp" (eager only), "buckets" (GradBucketReducer), "auto"
     comm: str = "auto"  # bucket reducer transport: "rccl" (capturable, libmtts_hip), "torch", "auto"
-    # N>1 graph step: ranks agree on the padded shapes before every step (see the module docstring)
-    agree_shapes: bool = True
+    # N>1 graph step: pad every rank's batch to the MAX padded shape over ranks (see the module docstring);
+    # off by default -- each rank keeps its own padding, as DDP in the reference's setup would
+    agree_shapes: bool = False
+    # run the data-parallel exchange even at world size 1 (a world-size-1 process group must exist): the
+    # bucketed RCCL path's cost on one GPU (bench.py extra_configs.dp_forced_n1); MTTS_FORCE_DP=1 does the same
+    force_dp: bool = False
 
 
 class Trainer:
@@ -207,7 +214,7 @@ class Trainer:
         self.global_step = 0
         self.epoch = 0
         self.last_losses = None
-        self.dp = self.world > 1 or (self.force_dp and dist.is_available() and dist.is_initialized())
+        self.dp = self.world > 1 or ((self.force_dp or cfg.force_dp) and dist.is_available() and dist.is_initialized())
         mode = cfg.dp if cfg.dp != "auto" else ("buckets" if cfg.graph else "ddp")
         if cfg.graph and mode == "ddp":
             raise ValueError("the graph step exchanges gradients with the bucket reducer (dp='buckets')")
@@ -305,8 +312,8 @@ class Trainer:
                 logged = vals if logged is None else logged + vals
                 if i == n - 1 and self._arm is not None:
                     # the last micro-batch's backward exchanges the accumulated gradients (and the logged
-                    # means) bucket by bucket as backward produces them
-                    self.reducer.arm(logged / n, overlap=self._arm)
+                    # means) bucket by bucket as backward produces them ("local": pack only, no collective)
+                    self.reducer.arm(logged / n, overlap=self._arm is True, comm=self._arm != "local")
                 (total / n if n > 1 else total).backward()
         return logged / n if n > 1 else logged
 
@@ -339,6 +346,8 @@ class Trainer:
             order = [self.params[i] for i in box[0]]
         comm = DP.make_comm(self.dev, self.cfg.comm)
         self.reducer = DP.GradBucketReducer(order, comm, self.cfg.bucket_mb, self.dev)
+        if comm.capturable:
+            self.reducer.warm()  # every rank, now: later captures run without any collective
         return logged
 
     # ------------------------------------------------------------------------------------ eager
@@ -390,6 +399,8 @@ class Trainer:
         side = torch.cuda.Stream(self.dev)
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):
+            # warm-up passes are rank-local (no collective): a rank may capture a new shape while its peers
+            # replay; only the first step of all (the reducer's construction) communicates, on every rank
             for it in range(2):
                 for p in self.params:
                     p.grad = None
@@ -397,10 +408,9 @@ class Trainer:
                     self._ensure_reducer(batches, lambda: self._fwd_bwd(static))
                     for i, p in enumerate(self.reducer.params):
                         self.reducer.views[i].copy_(p.grad)
-                    self.reducer.reduce_now()
                     self.reducer.attach_views()
                 elif self.dp:
-                    self._arm = True
+                    self._arm = "local"
                     try:
                         self._fwd_bwd(static)
                     finally:
@@ -454,8 +464,11 @@ class Trainer:
         return e
 
     def _agree_shapes(self, batches):
-        """N>1 graph step: MAX over ranks of each micro-batch's padded Tx / Ty (and one batch size), then
-        zero padding up to it, so every rank looks up -- and captures, replays, evicts -- the same key."""
+        """TrainConfig.agree_shapes (N>1 graph step, opt-in): MAX over ranks of each micro-batch's padded Tx /
+        Ty (and one batch size), then zero padding up to it, so every rank looks up the same key.  The padded
+        frames are masked, but the decoder's arithmetic depends on the padded length (GroupNorm statistics
+        over the whole padded length, conv bias leaking into padded frames -- SURVEY 0.6), so a rank's losses
+        then depend on its peers' lengths; the default keeps each rank's own padding."""
         if not (self.cfg.agree_shapes and self.dp and self.world > 1 and self.cfg.graph):
             return batches
         dims = torch.tensor([[b["x"].shape[1], b["y"].shape[2], b["x"].shape[0], -b["x"].shape[0]] for b in batches],

@@ -135,7 +135,7 @@ def _agree_worker(rank, world, port, q):
     from matcha.training import TrainConfig, Trainer, synthetic_batch
 
     torch.manual_seed(0)
-    tr = Trainer(TinyTTS(), TrainConfig(precision="32-true", graph=True, accumulate_grad_batches=2))
+    tr = Trainer(TinyTTS(), TrainConfig(precision="32-true", graph=True, accumulate_grad_batches=2, agree_shapes=True))
     # rank r: micro-batch shapes (Tx, Ty) differ per rank and per micro-batch
     shapes = {0: [(12, 40), (9, 48)], 1: [(10, 44), (11, 32)]}[rank]
     batches = [synthetic_batch(4, tx, ty, seed=rank * 10 + i, device="cpu") for i, (tx, ty) in enumerate(shapes)]
@@ -160,7 +160,7 @@ def _agree_worker(rank, world, port, q):
 
 @pytest.mark.timeout(120)
 def test_graph_step_shape_agreement_two_ranks_gloo():
-    """Trainer._agree_shapes (the N>1 graph step): every rank pads each micro-batch to the MAX padded
+    """Trainer._agree_shapes (the N>1 graph step with TrainConfig.agree_shapes): every rank pads each micro-batch to the MAX padded
     Tx / Ty over ranks with zeros (lengths unchanged), so all ranks look up, capture and replay one key."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
