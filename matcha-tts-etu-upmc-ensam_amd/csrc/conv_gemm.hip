@@ -432,8 +432,71 @@ struct WgradJobK {
     mtts_conv_wgrad_args a;
     float *part, *part_db;  // the job's slabs [splits][N][K] and bias partials [splits][N] (or null)
     int32_t rps;            // token rows per split
+    int32_t splits;
+    // in-kernel split sum (cnt != null): per-tile arrival counters (zero at rest) and where the sums go --
+    // dW[n*sn + c*sc + j*sj] for reduction column k = j*cin + c, db[n] -- (+=) when accumulate
+    int32_t *cnt;
+    float *dw, *db;
+    int64_t sn, sc, sj;
+    int32_t accumulate;
     int32_t pad_;
 };
+
+// The last block of a tile to arrive sums the tile's split slabs in split order and writes dW (and db):
+// every block's slab stores are published by an agent-scope release before its ticket (fetch_add on the
+// tile's counter); the last arriver acquires, reads every slab with plain vector loads, and re-zeroes the
+// counter.  The sum order is fixed (split 0, 1, ...) whatever the arrival order: deterministic, and no
+// separate reduce launch or its re-read of the slabs from HBM.
+__device__ __forceinline__ void wgrad_combine(const WgradJobK &J, int tile, int n0, int k0, bool ktile0) {
+    __shared__ int s_last;
+    const mtts_conv_wgrad_args &p = J.a;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab / db stores have completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(J.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == J.splits - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;  // block-uniform
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const size_t NK = (size_t)p.N * p.K;
+    const int nthr = (int)blockDim.x;
+    // 128 x 128 tile as float4 groups along k (K = ntaps * cin, cin % 8 == 0: a group is all in or out)
+    for (int g = (int)threadIdx.x; g < 128 * 32; g += nthr) {
+        const int n = n0 + (g >> 5), k = k0 + (g & 31) * 4;
+        if (n >= p.N || k >= p.K) continue;
+        const float *src = J.part + (size_t)n * p.K + k;
+        float4 a = *reinterpret_cast<const float4 *>(src);
+        for (int sp = 1; sp < J.splits; ++sp) {
+            const float4 b = *reinterpret_cast<const float4 *>(src + sp * NK);
+            a.x += b.x;
+            a.y += b.y;
+            a.z += b.z;
+            a.w += b.w;
+        }
+        const float v[4] = {a.x, a.y, a.z, a.w};
+        const int j0 = k / p.cin, c0 = k - j0 * p.cin;  // the group lies inside one tap (cin % 4 == 0)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float *o = J.dw + n * J.sn + (int64_t)(c0 + e) * J.sc + (int64_t)j0 * J.sj;
+            *o = J.accumulate ? *o + v[e] : v[e];
+        }
+    }
+    if (ktile0 && J.part_db && J.db) {
+        for (int x = (int)threadIdx.x; x < 128; x += nthr) {
+            const int n = n0 + x;
+            if (n >= p.N) continue;
+            float a = J.part_db[n];
+            for (int sp = 1; sp < J.splits; ++sp) a += J.part_db[(size_t)sp * p.N + n];
+            J.db[n] = J.accumulate ? J.db[n] + a : a;
+        }
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(J.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 constexpr int kWgradBatch = 12;  // ~1.7 KiB of kernel arguments
 struct WgradBatch {
     WgradJobK job[kWgradBatch];
@@ -833,6 +896,10 @@ __device__ __forceinline__ void wgrad_block(const WgradBatch &wb, const int vb) 
             for (int g = 0; g < HV * (KB / 2); ++g) sacc += dbs[g * T + x];
             if (n < p.N) part_db[(size_t)split * p.N + n] = sacc;
         }
+    }
+    if (wb.job[jb].cnt) {
+        const int ntn = (p.N + T - 1) / T;
+        wgrad_combine(wb.job[jb], ktile * ntn + n0 / T, n0, k0, ktile == 0);
     }
 }
 
@@ -1350,6 +1417,37 @@ static bool defer_wgrads() {
     return on && mtts::deferring();
 }
 
+// Arrival counters of the in-kernel split sums (wgrad_combine): one zeroed pool per device, handed out as a
+// ring (each launch's tiles get their own counters; the last arriver of a tile re-zeroes its counter, so a
+// range is free again once its launch has run).  MTTS_WGRAD_FUSED_SUM=0: the separate reduce launch instead.
+constexpr int kCntPool = 1 << 16;
+static int32_t *wgrad_counters(int n, hipStream_t st) {
+    static const bool off = [] { const char *e = getenv("MTTS_WGRAD_FUSED_SUM"); return e && e[0] == '0'; }();
+    if (off || n <= 0 || n > kCntPool / 16) return nullptr;
+    static std::mutex mu;
+    static int32_t *pool[64] = {};
+    static int head[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!pool[dev]) {
+        // never allocated inside a stream capture (the caller then takes the separate reduce launch)
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+        int32_t *p = nullptr;
+        if (hipMalloc(&p, kCntPool * sizeof(int32_t)) != hipSuccess) return nullptr;
+        if (hipMemset(p, 0, kCntPool * sizeof(int32_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            (void)hipFree(p);
+            return nullptr;
+        }
+        pool[dev] = p;
+    }
+    if (head[dev] + n > kCntPool) head[dev] = 0;
+    int32_t *r = pool[dev] + head[dev];
+    head[dev] += (n + 15) / 16 * 16;
+    return r;
+}
+
 // mtts_wgrad_plan_mode: 0 = the batched split plan for queued gradients, the per-launch one otherwise;
 // 1 / 2 = always the batched / per-launch plan (tests: a queued and an immediate gradient bitwise equal)
 std::atomic<int> g_wgrad_plan_mode{0};
@@ -1396,6 +1494,14 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
                                                  mtts::align_up((size_t)splits * p.N * p.K * 4, 256))
                      : nullptr;
     w.k.rps = rps;
+    w.k.splits = splits;
+    w.k.cnt = nullptr;
+    w.k.dw = dw;
+    w.k.db = db;
+    w.k.sn = sn;
+    w.k.sc = sc;
+    w.k.sj = sj;
+    w.k.accumulate = accumulate;
     w.k.pad_ = 0;
     w.key = wgrad_key(p, bf16, rows_per_step, depth, rps);
     w.splits = splits;
@@ -1414,17 +1520,21 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
             return mtts::fail(MTTS_ERR_HIP, "conv_wgrad: memset failed");
         w.splits = 1;
         w.k.part_db = db ? part_db : nullptr;
-    } else if (queue) {
-        std::lock_guard<std::mutex> lk(g_wq_mu);
-        g_wq.push_back(w);
-        return MTTS_OK;
     } else {
+        // in-kernel split sums (no reduce job) unless the counter pool is unavailable
+        w.k.cnt = wgrad_counters(((p.N + 127) / 128) * ((p.K + 127) / 128), st);
+        if (queue) {
+            std::lock_guard<std::mutex> lk(g_wq_mu);
+            g_wq.push_back(w);
+            return MTTS_OK;
+        }
         WgradBatch wb;
         wb.job[0] = w.k;
         wb.first[0] = 0;
         wb.first[1] = wgrad_blocks(w);
         wb.njobs = 1;
         if ((rc = wgrad_launch_key(wb, w.key, st))) return rc;
+        if (w.k.cnt) return MTTS_OK;
     }
     // sum of the split slabs (reduce.hip: now, or queued for the step's batched launch)
     mtts_reduce_job jobs[2];
@@ -1462,6 +1572,7 @@ int flush_wgrads(hipStream_t st) {
     }
     std::vector<mtts_reduce_job> jobs;
     for (const WgradPlanned &w : q) {
+        if (w.k.cnt) continue;  // summed in-kernel
         mtts_reduce_job j2[2];
         const int n = wgrad_reduce_jobs(w, j2);
         jobs.insert(jobs.end(), j2, j2 + n);
