@@ -164,7 +164,9 @@ def _bucketed_batches(B, Tx, Ty, n, rank, world, dev):
 # kernel families of the step, by the kernel's own name in a rocprofv3 trace
 FAMILIES = {
     "gemm": ("conv_gemm_kernel", "conv_gemm_glds_kernel", "splitk_epilogue_kernel"),
-    "wgrad": ("conv_wgrad_kernel", "reduce_partials_kernel"),
+    # weight-gradient GEMMs; their split sums run inside conv_wgrad_kernel (the last-arriving block of a tile,
+    # round 4); reduce_partials_kernel now only sums the LayerNorm / GroupNorm / bias partials -- not this family
+    "wgrad": ("conv_wgrad_kernel",),
     "attn": ("attn_fwd_kernel", "attn_bwd_dq_kernel", "attn_bwd_dkv_kernel", "attn_drow_kernel",
              "attn_bwd_merged_kernel", "attn_fwd_short_kernel", "attn_bwd_dq_short_kernel", "attn_bwd_dkv_short_kernel"),
 }
@@ -440,8 +442,8 @@ def main():
         res = {}
         # (name, autocast, split weight planes, text encoder precision)
         modes = (("32-true", False, False, "bf16"), ("one_plane", True, False, "bf16"),
-                 ("split_weights", True, True, "bf16"), ("parity_policy", True, True, "bf16x3"),
-                 ("parity_fp32_encoder", True, True, "fp32"))
+                 ("split_weights", True, True, "bf16"), ("parity_policy", True, True, "fp32fwd"),
+                 ("parity_bf16x3_encoder", True, True, "bf16x3"), ("parity_fp32_encoder", True, True, "fp32"))
         with torch.no_grad():
             for name, amp_on, split, enc in modes:
                 old = OPS.set_weight_split(split)
@@ -462,15 +464,17 @@ def main():
         precision_check = {
             "bf16_loss_rel_err": errs(run_mode)["loss_rel_err"],
             "run_mode": run_mode,
-            "modes": {k: errs(k) for k in ("one_plane", "split_weights", "parity_policy", "parity_fp32_encoder")},
+            "modes": {k: errs(k) for k in ("one_plane", "split_weights", "parity_policy", "parity_bf16x3_encoder",
+                                           "parity_fp32_encoder")},
             "losses": ["dur", "prior", "diff"],
             "bar": "alignment bit-exact (agreement 1.0), mel / flow-matching loss within 1e-4 relative (north star)",
             "note": "bf16 modes vs 32-true (= the oracle at this batch) with the parity tests' recipe weights and "
                     "batch, eval mode, same t / z.  one_plane: bf16 weights (the fp32 weights' rounding is the "
                     "error); split_weights: hi + rounding-residual bf16 planes; parity_policy (bench default, "
-                    "--precision bf16-parity): split weights + the text encoder's forward in bf16x3 (split A and W "
-                    "operands, fp32 attention forward; backward bf16); parity_fp32_encoder: split weights + the "
-                    "whole text encoder in exact fp32 (round 3's policy)"}
+                    "--precision bf16-parity): split weights + the text encoder's forward on the exact-fp32 MFMA "
+                    "(32-true's forward arithmetic; backward bf16); parity_bf16x3_encoder: the encoder forward in "
+                    "bf16x3 instead (split A and W operands, three bf16 MFMAs); parity_fp32_encoder: split weights "
+                    "+ the whole text encoder in exact fp32, backward too (round 3's policy)"}
 
     # same-run extra lines (N=1): the reference precision (32-true: exact fp32 MFMA) on the bench workload,
     # and the reference's own step shape -- 2 micro-batches of 16 with gradient accumulation
@@ -510,7 +514,7 @@ def main():
             extra[name] = {"ms_per_step": round(ms2, 3), "utterances_per_s": round(micro * acc / ms2 * 1e3, 2),
                            "steps": n2, "precision": prec, "micro_batch": micro, "accumulate_grad_batches": acc,
                            "weight_planes": 2 if prec == "bf16-parity" else 1,
-                           "encoder": enc or ("bf16x3" if prec == "bf16-parity" else "as the precision"),
+                           "encoder": enc or ("fp32fwd" if prec == "bf16-parity" else "as the precision"),
                            **({"dp": {"ranks": int(tr2.reducer.comm.ranks), "buckets": len(tr2.reducer.buckets),
                                       "overlapped_in_graph": bool(next(iter(tr2._graphs.values()))["overlap"])}}
                               if tr2.reducer is not None else {}),
@@ -559,9 +563,13 @@ def main():
         tf, gb = fl / t / 1e12, by / t / 1e9
         ai = fl / max(by, 1)
         traffic, tsrc = traffic_of(fam)
+        gl = g["launches"] if g else None
         line = {"kernel": kernel, "timing": src, "launches_per_step": n,
-                "graph_launches_per_step": g["launches"] if g else None,
+                "graph_launches_per_step": gl,
                 "avg_launch_us": round(t / n * 1e6, 2),
+                "avg_launch_unit": "per logical launch (one GEMM job of the eager log; the batched weight-gradient "
+                                   "launches of the graph hold several jobs each) -- time and bytes over the same jobs",
+                "avg_graph_launch_us": round(t / gl * 1e6, 2) if gl else None,
                 "algorithmic_flops_per_launch": round(fl / n), "algorithmic_bytes_per_launch": round(by / n),
                 "arithmetic_intensity_flop_per_byte": round(ai, 1), "ridge_flop_per_byte": round(ridge, 1),
                 "mfma_tflops": round(tf, 1), "mfma_frac": round(tf / gemm_peak, 4), "hbm_gbs": round(gb, 1),
@@ -583,9 +591,10 @@ def main():
         "launches; bytes = A rows read once + packed W (both planes when split) + C written (+ aux / residual / "
         "pre-activation streams) per launch; FLOP = 2 M N K")
     roofline_wgrad = roofline_of(
-        wgrad_log, "wgrad", "conv_wgrad_kernel + reduce_partials_kernel (weight-gradient GEMMs and the step's batched "
-        "fixed-order partial sums, which also hold the LayerNorm / GroupNorm gamma / beta partials)",
-        "2 M N K FLOP; bytes = dY + unique A rows + dW; graph time includes the whole batched reduce")
+        wgrad_log, "wgrad", "conv_wgrad_kernel (weight-gradient GEMMs, batched up to 12 jobs per launch, split slabs "
+        "summed in-kernel by each tile's last-arriving block)",
+        "2 M N K FLOP; bytes = dY + unique A rows + dW; graph time = the family's launches (their in-kernel split "
+        "sums included); the norms' gamma / beta partial sums (reduce_partials_kernel) are not in this family")
     roofline_attn = roofline_of(
         attn_log, "attn", "attn_fwd + backward (Drow pre-pass + merged dQ / dK-dV launch) kernels, long (decoder) and short (encoder, T <= 128)",
         "FLOP = 4 B H T^2 D fwd, 8 B H T^2 D bwd (standard flash-attention accounting, recomputation not counted); "
@@ -612,7 +621,7 @@ def main():
                        "precision": args.precision, "hip_graph": graph,
                        "weight_planes": 2 if (args.precision == "bf16-parity" or
                                               (OPS.weight_split_enabled() and args.precision == "bf16-mixed")) else 1,
-                       **({"text_encoder_forward": "bf16x3"} if args.precision == "bf16-parity" else {}),
+                       **({"text_encoder_forward": "exact fp32 MFMA (backward bf16)"} if args.precision == "bf16-parity" else {}),
                        **({"bucketed_batches": [[int(v) for v in (b["x"].shape[1], b["y"].shape[2],
                                                                      b["x_lengths"].min(), b["y_lengths"].min())]
                                                 for b in batches],

@@ -42,7 +42,7 @@ extern "C" {
 typedef enum mtts_status {
     MTTS_OK = 0,
     MTTS_ERR_INVALID_ARG = -1, /* null pointer, negative size, bad flag */
-    MTTS_ERR_SHAPE = -2,       /* shape outside what the kernels support (e.g. Tx > 2048) */
+    MTTS_ERR_SHAPE = -2,       /* shape outside what the kernels support (e.g. Tx > 4096) */
     MTTS_ERR_WORKSPACE = -3,   /* workspace too small */
     MTTS_ERR_HIP = -4,         /* a HIP runtime call failed (launch, attribute) */
     MTTS_ERR_UNSUPPORTED = -5  /* feature not built into this library */
@@ -61,7 +61,7 @@ const char *mtts_last_error(void);
 #define MTTS_MAS_NO_DENSE_PATH 0x2   /* only row_start_out/lengths_out: do not write `path`    */
 
 /* Maximum text length (Tx) the kernels accept. */
-#define MTTS_MAS_MAX_TX 2048 /* 32 text rows per lane of the one-wave DP */
+#define MTTS_MAS_MAX_TX 4096 /* 8 waves x 8 text rows per lane of the multi-wave DP (round 4; 2048 with MTTS_MAS_MW=0) */
 
 /* Bytes of device workspace mtts_maximum_path_f32 / mtts_compute_batch_alignments need. */
 size_t mtts_maximum_path_workspace_size(int32_t B, int32_t Tx, int32_t Ty);

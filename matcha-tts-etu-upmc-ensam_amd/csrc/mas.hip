@@ -297,6 +297,247 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
     for (int x = lane; x < Tx; x += kWave) rs_out[x] = rs[x];
 }
 
+// ------------------------------------------------------------------------------------------------
+// Multi-wave forward DP for Tx > 64 (round 4): W waves per utterance, thread t = wave*64 + lane owns the
+// KL text rows t*KL .. t*KL+KL-1.  A column's cells depend only on the previous column, so the waves
+// split the rows and run as a pipeline skewed by one 32-column chunk: in phase p wave w processes chunk
+// p - w; the x-1 neighbour of its first row is the previous wave's last row one column earlier, which
+// that wave's lane 63 wrote to an LDS edge ring (3 chunks deep) one or two phases before; a workgroup
+// barrier (LDS-only) ends every phase.  Per chunk a lane flushes one backpointer word per row (the
+// chunk IS one 32-column word).  Same arithmetic per cell as mas_dp_kernel (bit-exact with core.pyx);
+// the chain per column shrinks from K = Tx/64 rows per lane (one wave) to KL (e.g. Tx = 512: 8 -> 1)
+// at the price of one barrier per 32 columns and W - 1 fill phases.  The backtrack is mas_dp_kernel's
+// (wave 0), with the next backpointer word column prefetched while the current one is walked.
+template <int KL, int W, bool PM, bool VEC, bool LDS_BITS, bool DP_OUT>
+__global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
+    constexpr int CC = 32;       // columns per chunk (one backpointer word)
+    constexpr int C = CC / KL;   // columns per ring sub-chunk: KL * C = 32 cells per lane
+    constexpr int KB = KL * W;   // backtrack words per lane (rows per lane of wave 0's walk)
+    extern __shared__ uint32_t smem[];
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int Tx = a.Tx, Ty = a.Ty, Txp = a.Txp;
+    const size_t ubase = (size_t)b * Tx * Ty;
+    const float neg = a.neg;
+
+    int t_x, t_y;
+    if (a.t_xs) {
+        t_x = a.t_xs[b];
+        t_y = a.t_ys[b];
+    } else {  // every wave reduces the mask's first column / row itself (same sums, no hand-off)
+        const float *m = a.mask + ubase;
+        float sx = 0.f, sy = 0.f;
+        for (int x = lane; x < Tx; x += kWave) sx += m[(size_t)x * Ty];
+        for (int y = lane; y < Ty; y += kWave) sy += m[y];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            sx += __shfl_xor(sx, off);
+            sy += __shfl_xor(sy, off);
+        }
+        t_x = (int)sx;
+        t_y = (int)sy;
+    }
+    t_x = __builtin_amdgcn_readfirstlane(t_x);
+    t_y = __builtin_amdgcn_readfirstlane(t_y);
+    if (threadIdx.x == 0) {
+        a.lengths[2 * b] = t_x;
+        a.lengths[2 * b + 1] = t_y;
+    }
+
+    int32_t *rs = reinterpret_cast<int32_t *>(smem);                // [Txp] row starts
+    float *edge = reinterpret_cast<float *>(smem + Txp);            // [3][W][CC] last-row values per column
+    uint32_t *bits_l = smem + Txp + 3 * W * CC;                     // [nch][Txp] (LDS mode)
+    uint32_t *bits_g = a.bits + (size_t)b * a.nch * Txp;
+    for (int x = threadIdx.x; x < Txp; x += 64 * W) rs[x] = -1;
+
+    const bool valid = t_x >= 1 && t_y >= 1 && t_x <= t_y && t_x <= Tx && t_y <= Ty;
+    if (valid) {
+        const int x0 = (wave * 64 + lane) * KL;
+        const unsigned span = (unsigned)(t_y - t_x);
+        int roff[KL];
+#pragma unroll
+        for (int i = 0; i < KL; ++i) roff[i] = min(x0 + i, Tx - 1) * Ty;
+        const int last = Tx * Ty - 1;
+        const float *vbase = a.value + ubase;
+        const float *mbase = PM ? vbase : a.mask + ubase;
+        float dp[KL];
+        uint32_t R[KL];
+#pragma unroll
+        for (int i = 0; i < KL; ++i) {
+            dp[i] = neg;
+            R[i] = 0u;
+        }
+        constexpr int MD = PM ? 1 : 2;
+        float vbuf[2][KL][C], mbuf[MD][KL][C];
+        auto load_sub = [&](auto slot, int y0) {
+            constexpr int sl = decltype(slot)::value;
+#pragma unroll
+            for (int i = 0; i < KL; ++i) load_row_segment<C, VEC>(vbase, roff[i] + y0, last, vbuf[sl][i]);
+            if constexpr (!PM) {
+#pragma unroll
+                for (int i = 0; i < KL; ++i) load_row_segment<C, VEC>(mbase, roff[i] + y0, last, mbuf[sl][i]);
+            }
+        };
+        const int nchunks = (t_y + CC - 1) / CC;
+        const float *ein = edge + (wave > 0 ? wave - 1 : 0) * CC;  // the previous wave's ring row
+        float *eout = edge + wave * CC;
+        // one chunk: KL sub-chunks of C columns from the ring slots (P * KL + s) & 1, the next sub-chunk's
+        // loads issued before each one is processed
+        auto chunk = [&](auto parity, int c) {
+            constexpr int P = decltype(parity)::value;
+            const int r3 = c % 3, p3 = (c + 2) % 3;
+            static_for<0, KL>([&](auto sv) {
+                constexpr int s = decltype(sv)::value;
+                constexpr int sl = (P * KL + s) & 1;
+                const int y0 = c * CC + s * C;
+                load_sub(std::integral_constant<int, sl ^ 1>{}, y0 + C);
+                // the lane-0 neighbours of this sub-chunk's columns: column y needs the previous wave's last
+                // row after column y - 1 (ring slot of chunk c, or of chunk c - 1 for the chunk's first column)
+                float nbl[C];
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    const int jc = s * C + j;  // column within the chunk
+                    const int y = y0 + j;
+                    float prev;
+                    if (jc == 0) prev = edge[(p3 * W) * CC + (wave > 0 ? wave - 1 : 0) * CC + CC - 1];
+                    else prev = ein[r3 * W * CC + jc - 1];
+                    nbl[j] = wave == 0 ? (y == 0 ? 0.0f : neg) : (y == 0 ? neg : prev);
+                }
+                float eo[C];
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    const int y = y0 + j;
+                    eo[j] = neg;
+                    if (y < t_y) {
+                        float sc[KL];
+#pragma unroll
+                        for (int i = 0; i < KL; ++i) {
+                            if constexpr (PM) sc[i] = vbuf[sl][i][j];
+                            else sc[i] = vbuf[sl][i][j] * mbuf[sl][i][j];  // __init__.py:45
+                        }
+                        const float nb = dpp_wave_shr1(dp[KL - 1], nbl[j]);
+                        float ndp[KL];
+#pragma unroll
+                        for (int i = 0; i < KL; ++i) {
+                            const float fp = (i == 0) ? nb : dp[i - 1];  // core.pyx:65-66
+                            const float fs = dp[i];                      // core.pyx:70-71
+                            const int d = y - (x0 + i);
+                            const bool diag = (fp >= fs) || (d == 0);    // core.pyx:73
+                            const float best = diag ? fp : fs;
+                            const float v = best + sc[i];                // core.pyx:80
+                            ndp[i] = ((unsigned)d <= span) ? v : neg;    // band, :59-62
+                            R[i] = (R[i] << 1) | (diag ? 1u : 0u);
+                        }
+#pragma unroll
+                        for (int i = 0; i < KL; ++i) dp[i] = ndp[i];
+                        if constexpr (DP_OUT) {
+#pragma unroll
+                            for (int i = 0; i < KL; ++i)
+                                if (x0 + i < t_x) a.dp_out[ubase + (size_t)(x0 + i) * Ty + y] = ndp[i];
+                        }
+                        eo[j] = dp[KL - 1];
+                    }
+                }
+                if (lane == 63) {
+#pragma unroll
+                    for (int j = 0; j < C; ++j) eout[r3 * W * CC + s * C + j] = eo[j];
+                }
+            });
+            // the chunk's backpointer word per row (a partial last chunk left-aligned like mas_dp_kernel's)
+            const int sh = (c == nchunks - 1 && (t_y & 31)) ? 32 - (t_y & 31) : 0;
+#pragma unroll
+            for (int i = 0; i < KL; ++i) {
+                const uint32_t w = R[i] << sh;
+                if constexpr (LDS_BITS) bits_l[c * Txp + x0 + i] = w;
+                else bits_g[(size_t)c * Txp + x0 + i] = w;
+                R[i] = 0u;
+            }
+        };
+        load_sub(std::integral_constant<int, 0>{}, 0);
+        for (int i = 0; i < wave; ++i) mtts::lds_barrier();  // pipeline fill: wave w starts in phase w
+        for (int c = 0; c < nchunks; c += 2) {
+            chunk(std::integral_constant<int, 0>{}, c);
+            mtts::lds_barrier();
+            if (c + 1 < nchunks) {
+                chunk(std::integral_constant<int, 1>{}, c + 1);
+                mtts::lds_barrier();
+            }
+        }
+        for (int i = wave; i < W - 1; ++i) mtts::lds_barrier();  // drain: every wave runs nchunks + W - 1 phases
+    }
+    if constexpr (!LDS_BITS) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if constexpr (!LDS_BITS) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+
+    if (valid && wave == 0) {
+        // backtrack (mas_dp_kernel's walk): registers hold one word column slot-major, W[r] lane l = row
+        // r*64 + l; in global-bits mode the next column (c - 1) is requested while column c is walked
+        int idx = t_x - 1;
+        int y = t_y - 1;
+        int cur_c = -1;
+        uint32_t Wc[KB], Wn[LDS_BITS ? 1 : KB];
+        bool have_next = false;
+#pragma unroll
+        for (int r = 0; r < KB; ++r) Wc[r] = 0u;
+        bool done = false;
+#pragma unroll
+        for (int r = KB - 1; r >= 0; --r) {
+            while (!done && idx >= kWave * r) {
+                if (idx == 0) {
+                    if (lane == 0) rs[0] = 0;
+                    done = true;
+                    break;
+                }
+                if (idx >= y) {
+                    for (int x = lane; x <= idx; x += kWave) rs[x] = x;
+                    done = true;
+                    break;
+                }
+                const int c = y >> 5;
+                if (c != cur_c) {
+                    if constexpr (LDS_BITS) {
+#pragma unroll
+                        for (int rr = 0; rr < KB; ++rr) Wc[rr] = bits_l[c * Txp + rr * kWave + lane];
+                    } else {
+                        if (have_next && c == cur_c - 1) {
+#pragma unroll
+                            for (int rr = 0; rr < KB; ++rr) Wc[rr] = Wn[rr];
+                        } else {
+#pragma unroll
+                            for (int rr = 0; rr < KB; ++rr) Wc[rr] = bits_g[(size_t)c * Txp + rr * kWave + lane];
+                        }
+                        have_next = c > 0;
+                        const int cn = c > 0 ? c - 1 : 0;
+#pragma unroll
+                        for (int rr = 0; rr < KB; ++rr) Wn[rr] = bits_g[(size_t)cn * Txp + rr * kWave + lane];
+                    }
+                    cur_c = c;
+                }
+                const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)Wc[r], idx & (kWave - 1));
+                const int base = c << 5;
+                uint32_t m = word & (0xFFFFFFFFu << (31 - (y - base)));
+                if (idx >= base) m &= 0xFFFFFFFFu >> (idx - base);
+                int ydec;
+                if (m) {
+                    ydec = base + 31 - __builtin_ctz(m);
+                } else if (idx >= base) {
+                    ydec = idx;
+                } else {
+                    y = base - 1;
+                    continue;
+                }
+                if (lane == 0) rs[idx] = ydec;
+                idx -= 1;
+                y = ydec - 1;
+            }
+        }
+    }
+    __syncthreads();
+    int32_t *rs_out = a.row_start + (size_t)b * Tx;
+    for (int x = threadIdx.x; x < Tx; x += 64 * W) rs_out[x] = rs[x];
+}
+
 // Dense writer: path[b,x,y] = 1 iff row_start[b,x] <= y <= row_end[b,x].  One block per (b, x,
 // 1024-column slab); float4 stores when rows are 16-byte aligned.
 template <typename T, bool SET_ONLY>
@@ -526,12 +767,30 @@ struct WsLayout {
     size_t lengths, row_start, bits, total;
     int K, Txp, nch;
     bool lds_bits;
+    int W, KL;  // W > 1: the multi-wave DP (mas_dp_mw_kernel), W waves x KL rows per lane
 };
+
+// MTTS_MAS_MW=0: the one-wave DP for every Tx (A/B; Tx <= 2048 then)
+bool mw_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("MTTS_MAS_MW");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 
 WsLayout ws_layout(int B, int Tx, int Ty) {
     WsLayout w{};
+    w.W = 1;
+    w.KL = 1;
     w.K = Tx <= 64 ? 1 : Tx <= 128 ? 2 : Tx <= 256 ? 4 : Tx <= 512 ? 8 : Tx <= 1024 ? 16 : 32;
     w.Txp = kWave * w.K;
+    if (Tx > 64 && mw_enabled()) {
+        w.W = Tx <= 128 ? 2 : Tx <= 256 ? 4 : 8;
+        w.KL = Tx <= 512 ? 1 : Tx <= 1024 ? 2 : Tx <= 2048 ? 4 : 8;
+        w.K = w.W * w.KL;
+        w.Txp = kWave * w.K;
+    }
     w.nch = (Ty + 31) / 32;
     w.lds_bits = (size_t)w.Txp * w.nch * 4 <= (size_t)kLdsBitsLimit;
     size_t off = 0;
@@ -543,6 +802,37 @@ WsLayout ws_layout(int B, int Tx, int Ty) {
     if (!w.lds_bits) off = mtts::align_up(off + (size_t)B * w.nch * w.Txp * 4, 256);
     w.total = off;
     return w;
+}
+
+template <int KL, int W, bool PM>
+int launch_dp_mw(const MasArgs &a, int B, bool vec, bool lds_bits, bool dp_out, size_t shmem, hipStream_t st) {
+    dim3 grid(B), block(64 * W);
+#define MTTS_MAS_MW_LAUNCH(V, L, DO) \
+    hipLaunchKernelGGL((mas_dp_mw_kernel<KL, W, PM, V, L, DO && PM>), grid, block, shmem, st, a)
+    if (vec) {
+        if (lds_bits) {
+            if (dp_out) MTTS_MAS_MW_LAUNCH(true, true, true); else MTTS_MAS_MW_LAUNCH(true, true, false);
+        } else {
+            if (dp_out) MTTS_MAS_MW_LAUNCH(true, false, true); else MTTS_MAS_MW_LAUNCH(true, false, false);
+        }
+    } else {
+        if (lds_bits) {
+            if (dp_out) MTTS_MAS_MW_LAUNCH(false, true, true); else MTTS_MAS_MW_LAUNCH(false, true, false);
+        } else {
+            if (dp_out) MTTS_MAS_MW_LAUNCH(false, false, true); else MTTS_MAS_MW_LAUNCH(false, false, false);
+        }
+    }
+#undef MTTS_MAS_MW_LAUNCH
+    return mtts::check_launch("mas_dp_mw_kernel");
+}
+
+template <int KL, int W>
+int launch_dp_mw_pm(const MasArgs &a, int B, bool vec, bool lds_bits, bool dp_out, size_t shmem, hipStream_t st) {
+    if (!a.premasked) {
+        if (dp_out) return mtts::fail(MTTS_ERR_INVALID_ARG, "maximum_path: dp_out needs a premasked lattice");
+        return launch_dp_mw<KL, W, false>(a, B, vec, lds_bits, false, shmem, st);
+    }
+    return launch_dp_mw<KL, W, true>(a, B, vec, lds_bits, dp_out, shmem, st);
 }
 
 template <int K, int C, int D, bool PM>
@@ -592,6 +882,17 @@ int launch_dp_kc(const MasArgs &a, int B, bool vec, bool lds_bits, bool dp_out, 
 }
 
 int launch_dp(MasArgs a, int B, const WsLayout &w, bool vec, bool dp_out, hipStream_t st) {
+    if (w.W > 1) {
+        const size_t shmem = (size_t)w.Txp * 4 + (size_t)3 * w.W * 32 * 4 + (w.lds_bits ? (size_t)w.Txp * w.nch * 4 : 0);
+        if (w.W == 2) return launch_dp_mw_pm<1, 2>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+        if (w.W == 4) return launch_dp_mw_pm<1, 4>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+        switch (w.KL) {
+            case 1: return launch_dp_mw_pm<1, 8>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+            case 2: return launch_dp_mw_pm<2, 8>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+            case 4: return launch_dp_mw_pm<4, 8>(a, B, vec, w.lds_bits, dp_out, shmem, st);
+            default: return launch_dp_mw_pm<8, 8>(a, B, vec, w.lds_bits, dp_out, shmem, st);  // Tx <= 4096
+        }
+    }
     size_t shmem = (size_t)w.Txp * 4 + (w.lds_bits ? (size_t)w.Txp * w.nch * 4 : 0);
     switch (w.K) {
         case 1: return launch_dp_kc<1, 32>(a, B, vec, w.lds_bits, dp_out, shmem, st);
@@ -605,8 +906,8 @@ int launch_dp(MasArgs a, int B, const WsLayout &w, bool vec, bool dp_out, hipStr
 
 int check_shape(int B, int Tx, int Ty) {
     if (B < 0 || Tx < 1 || Ty < 1) return mtts::fail(MTTS_ERR_INVALID_ARG, "maximum_path: bad shape");
-    if (Tx > MTTS_MAS_MAX_TX)
-        return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: Tx > MTTS_MAS_MAX_TX (2048) is not supported");
+    if (Tx > MTTS_MAS_MAX_TX || (Tx > 2048 && !mw_enabled()))
+        return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: Tx > MTTS_MAS_MAX_TX (4096) is not supported");
     if ((int64_t)Tx * Ty * 4 >= (int64_t)1 << 31)
         return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: one utterance's lattice exceeds 2 GiB");
     return MTTS_OK;

@@ -18,7 +18,7 @@ LIB_PATH = Path(os.environ.get("MTTS_LIB", _PKG_ROOT / "lib" / "libmtts_hip.so")
 MTTS_OK = 0
 MTTS_MAS_VALUE_PREMASKED = 0x1
 MTTS_MAS_NO_DENSE_PATH = 0x2
-MTTS_MAS_MAX_TX = 2048
+MTTS_MAS_MAX_TX = 4096  # include/mtts.h
 
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32

@@ -75,12 +75,21 @@ _PRECISE: contextvars.ContextVar = contextvars.ContextVar("mtts_precise_fwd", de
 
 
 @contextlib.contextmanager
-def precise_forward(on: bool = True):
-    tok = _PRECISE.set(bool(on))
+def precise_forward(on: bool | str = True):
+    """on: True / "bf16x3" (split bf16 operands, three MFMAs per product) or "fp32" (the forward GEMMs on
+    the exact-fp32 MFMA with fp32 packed weights -- the 32-true arithmetic, so the forward's outputs are
+    those of 32-true; round 4: bf16x3 left one alignment near-tie of the B=4 reference fixture flipped);
+    False: off.  The backward of the same ops stays bf16 one-plane either way."""
+    tok = _PRECISE.set(("bf16x3" if on is True else on) if on else False)
     try:
         yield
     finally:
         _PRECISE.reset(tok)
+
+
+def _fwd_fp32() -> bool:
+    """precise_forward("fp32") is active: bf16-region forward GEMMs run as exact fp32."""
+    return _PRECISE.get() == "fp32"
 
 
 def set_weight_split(on: bool) -> bool:
@@ -93,7 +102,7 @@ def set_weight_split(on: bool) -> bool:
 
 _WSPLIT_CV: contextvars.ContextVar = contextvars.ContextVar("mtts_w_split", default=None)
 # the text encoder's precision inside bf16-mixed when the model does not set its own
-# (MatchaTTS.encoder_precision): "bf16", "bf16x3" (precise_forward) or "fp32"
+# (MatchaTTS.encoder_precision): "bf16", "bf16x3" / "fp32fwd" (precise_forward) or "fp32"
 _ENC_PREC: contextvars.ContextVar = contextvars.ContextVar("mtts_encoder_precision", default="bf16")
 
 
@@ -105,9 +114,10 @@ def weight_split_enabled() -> bool:
 @contextlib.contextmanager
 def parity_policy(on: bool = True):
     """bf16-parity inside a bf16 autocast region (the Trainer's "bf16-parity" precision): split weight
-    planes for every forward GEMM and the text encoder's forward in bf16x3 (precise_forward)."""
+    planes for every forward GEMM and the text encoder's forward on the exact-fp32 MFMA
+    (precise_forward("fp32"); its backward stays bf16)."""
     t1 = _WSPLIT_CV.set(True if on else None)
-    t2 = _ENC_PREC.set("bf16x3" if on else "bf16")
+    t2 = _ENC_PREC.set("fp32fwd" if on else "bf16")
     try:
         yield
     finally:
@@ -365,8 +375,14 @@ def _run_pack(specs, prec, stream=None):
 
 
 def _pack_kind(spec: PackSpec, prec: int) -> int:
-    """bf16 forward operands: the split planes when selected (set_weight_split); everything else as prec."""
-    return PACK_BF16_SPLIT if (prec == PREC_BF16 and (weight_split_enabled() or _PRECISE.get()) and not spec.dgrad) else prec
+    """bf16 forward operands: fp32 under precise_forward("fp32"), the split planes when selected
+    (set_weight_split, precise_forward("bf16x3")); everything else as prec."""
+    if prec == PREC_BF16 and not spec.dgrad:
+        if _fwd_fp32():
+            return PREC_FP32
+        if weight_split_enabled() or _PRECISE.get():
+            return PACK_BF16_SPLIT
+    return prec
 
 
 _PACK_SCOPE: contextvars.ContextVar = contextvars.ContextVar("mtts_pack_scope", default=None)
@@ -404,7 +420,7 @@ def _pack_plan_now(plan, prec, stream=None):
     """Every layout in `plan` for this precision (the backward's transposed ones too when grad is
     enabled), a few launches per kind -> {key: packed}."""
     grad = torch.is_grad_enabled()
-    kinds = (prec, PACK_BF16_SPLIT) if prec == PREC_BF16 else (prec,)
+    kinds = (prec, PACK_BF16_SPLIT, PREC_FP32) if prec == PREC_BF16 else (prec,)
     cache = {}
     for kind in kinds:
         specs = [sp for key, sp in plan.items()
@@ -495,6 +511,12 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     # host-side shape checks before any launch (the kernel trusts W's rows / the output's extent)
     if Wp.dim() != 2 or Wp.shape[0] < N_ or Wp.shape[1] != Kp or Kp < len(offs) * cin:
         raise ValueError(f"packed weight {tuple(Wp.shape)} does not cover N={N_}, Kp={Kp}, K={len(offs) * cin}")
+    if prec == PREC_BF16 and Wp.dtype == torch.float32:
+        # precise_forward("fp32"): an fp32-packed forward operand inside a bf16 region runs the exact-fp32
+        # MFMA (the 32-true kernels) on fp32 A
+        prec = PREC_FP32
+        if A.dtype != torch.float32:
+            A = A.float()
     w_split = getattr(Wp, "_mtts_w_split", False) and prec == PREC_BF16
     # bf16x3 (precise_forward): the split weights' GEMM also splits its fp32 A operand -- register schedules
     a_split = w_split and _PRECISE.get() and A.dtype == torch.float32
@@ -1943,11 +1965,17 @@ class _TimeMLP(torch.autograd.Function):
         dw1, db1 = torch.empty_like(w1), new(D)
         # on the decoder's path (t carries no gradient) every output is a parameter gradient: the five
         # launches leave the critical path for the deferral's side stream (joined before the optimizer)
-        side = param_grad_side_stream() if (not ctx.e_grad and g_temb is None) else None
+        # -- only when autograd takes EVERY output as a parameter gradient: it then steals each tensor (no
+        # kernel) and nothing reads it before the join.  The outputs are NOT kept alive here: an extra
+        # reference makes AccumulateGrad copy the gradient on the main stream while the side kernels still
+        # write it (zeros in a replayed graph, tests/test_training_gpu.py::
+        # test_graph_gradients_equal_eager_over_replays); a frozen weight (needs_input_grad False) would have
+        # its gradient dropped at once and its memory reused under the side kernels, so that case stays on
+        # the main stream
+        all_params = all(ctx.needs_input_grad[1:5]) and all(ctx.needs_input_grad[7:])
+        side = param_grad_side_stream() if (not ctx.e_grad and g_temb is None and all_params) else None
         if side is not None:
-            # the outputs too: a gradient autograd drops at once (a frozen weight) must not be handed to
-            # main-stream work while the side kernels still write it
-            keep_for_side(e, h1, a1, temb, a2, w1, w2, *ws, *dys, d_temb, dh1, *dws, *dbs, dw1, db1, dw2, db2)
+            keep_for_side(e, h1, a1, temb, a2, w1, w2, *ws, *dys, d_temb, dh1)
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             _rows_bwd(a2, temb, ROWS_ACT_MISH, ws, dys, d_temb, dws, dbs)
             if g_temb is not None:  # temb used directly as well (never, on the decoder's path)

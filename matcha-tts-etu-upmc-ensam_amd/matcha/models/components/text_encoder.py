@@ -260,7 +260,9 @@ class _Embedding(torch.autograd.Function):
         dw = torch.empty(V, C, dtype=torch.float32, device=gc.device)
         # the weight gradient is this backward's only output: inside a Trainer step it runs on the gradient
         # deferral's side stream, beside the final weight-gradient flush (outputs allocated here, inputs kept)
-        side = O.param_grad_side_stream()
+        # (only when the weight takes the gradient: a dropped output's memory could be reused under the side
+        # kernel; and the output is not kept alive -- AccumulateGrad must steal it, not copy it)
+        side = O.param_grad_side_stream() if ctx.needs_input_grad[1] else None
         if side is not None:
             O.keep_for_side(ids_c, gc)
         st = side.cuda_stream if side is not None else N.stream_handle(gc.device)

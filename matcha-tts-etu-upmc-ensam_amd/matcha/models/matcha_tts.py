@@ -37,10 +37,12 @@ class _nullctx:
 
 
 class MatchaTTS(BaseLightningClass):
-    # text encoder precision inside a bf16-mixed region (see forward): "bf16" (autocast's), "bf16x3" (forward
-    # GEMMs as split bf16 operands A_hi W_hi + A_hi W_lo + A_lo W_hi and an fp32 attention forward, backward
-    # bf16: the parity policy), "fp32" (exact fp32 MFMA forward and backward)
-    # None: the ambient default (_ops.parity_policy sets "bf16x3", otherwise "bf16")
+    # text encoder precision inside a bf16-mixed region (see forward): "bf16" (autocast's), "fp32fwd" (the
+    # forward on the exact-fp32 MFMA with fp32 weights -- 32-true's forward arithmetic --, backward bf16: the
+    # parity policy since round 4), "bf16x3" (forward GEMMs as split bf16 operands A_hi W_hi + A_hi W_lo +
+    # A_lo W_hi and an fp32 attention forward, backward bf16: ~16 significant bits, left an alignment
+    # near-tie flipped), "fp32" (exact fp32 MFMA forward and backward)
+    # None: the ambient default (_ops.parity_policy sets "fp32fwd", otherwise "bf16")
     encoder_precision = None
 
     @property
@@ -137,7 +139,9 @@ class MatchaTTS(BaseLightningClass):
         if enc_prec == "fp32":
             enc_ctx = torch.autocast(device_type=x.device.type, enabled=False)
         elif enc_prec == "bf16x3":
-            enc_ctx = O.precise_forward()
+            enc_ctx = O.precise_forward("bf16x3")
+        elif enc_prec == "fp32fwd":
+            enc_ctx = O.precise_forward("fp32")
         else:
             enc_ctx = _nullctx()
         with enc_ctx:

@@ -17,9 +17,10 @@ from matcha import _native as N
 
 
 def _check_tx(Tx: int) -> None:
-    """The DP keeps one utterance's text rows in one wave (32 rows per lane at most): t_x <= 2048.
-    The reference Cython (core.pyx:14-96) has no cap; LJSpeech tops out near 190 tokens and
-    BASELINE config 5 uses 512, so the limit is a documented shape error, not a silent truncation."""
+    """The DP keeps one utterance's text rows in one workgroup's registers (8 waves x 8 rows per lane at
+    most, csrc/mas.hip mas_dp_mw_kernel): t_x <= 4096.  The reference Cython (core.pyx:14-96) has no cap;
+    LJSpeech tops out near 190 tokens and BASELINE config 5 uses 512, so the limit is a documented shape
+    error, not a silent truncation."""
     if Tx > N.MTTS_MAS_MAX_TX:
         raise ValueError(f"maximum_path: text length {Tx} exceeds the GPU kernel's limit of "
                          f"{N.MTTS_MAS_MAX_TX} rows (MTTS_MAS_MAX_TX, include/mtts.h)")

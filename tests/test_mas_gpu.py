@@ -110,10 +110,12 @@ def _rand_case(rng, B, Tx, Ty, ties=False):
                                    (128, 128), (129, 301), (200, 203), (255, 600), (256, 257),
                                    (257, 700), (300, 999), (511, 1001), (512, 512), (77, 33 * 32 + 5),
                                    (513, 600), (700, 1501), (1024, 1024), (1000, 2100), (1025, 1100),
-                                   (1500, 2999), (2048, 2048), (2047, 4096)])
+                                   (1500, 2999), (2048, 2048), (2047, 4096), (2049, 2100), (3000, 3333),
+                                   (4095, 4095), (4096, 4200)])
 def test_random_vs_oracle(Tx, Ty):
-    """Every K specialisation (rows/lane 1,2,4,8,16,32), odd Ty (scalar loads), LDS- and HBM-resident
-    backpointers, square lattices (forced diagonal), and ties."""
+    """Every DP specialisation -- the one-wave kernel (Tx <= 64) and the multi-wave one (2 / 4 / 8 waves,
+    1 / 2 / 4 / 8 rows per lane, up to Tx = 4096) --, odd Ty (scalar loads), LDS- and HBM-resident
+    backpointers, square lattices (forced diagonal), partial last 32-column chunks, and ties."""
     rng = np.random.default_rng(Tx * 10007 + Ty)
     for ties in (False, True):
         value, t_x, t_y = _rand_case(rng, 3, Tx, max(Ty, Tx), ties)
@@ -258,12 +260,12 @@ def test_expand_rows_matches_bmm_and_its_gradient():
 
 
 def test_text_length_limit_is_a_clear_error():
-    """Beyond MTTS_MAS_MAX_TX (2048 rows; the reference Cython has no cap) the wrapper refuses with a
+    """Beyond MTTS_MAS_MAX_TX (4096 rows; the reference Cython has no cap) the wrapper refuses with a
     ValueError naming the limit instead of a native shape error."""
     import torch
 
     from matcha.utils.monotonic_align import maximum_path
 
-    v = torch.zeros(1, 2049, 2100, device="cuda")
-    with pytest.raises(ValueError, match="2048"):
+    v = torch.zeros(1, 4097, 4100, device="cuda")
+    with pytest.raises(ValueError, match="4096"):
         maximum_path(v, torch.ones_like(v))

@@ -144,3 +144,34 @@ def test_precise_forward_encoder_backward_stays_bf16():
     assert r(outs["bf16x3"][1], outs["fp32"][1]) < 2e-5
     assert r(outs["bf16"][0], outs["fp32"][0]) > 10 * r(outs["bf16x3"][0], outs["fp32"][0])
     assert r(outs["bf16x3"][2], outs["fp32"][2]) < 3e-2  # bf16 backward
+
+
+def test_precise_forward_fp32_encoder_equals_32true():
+    """The parity policy's text encoder (precise_forward("fp32") inside the bf16 region): its forward runs
+    32-true's arithmetic -- fp32 packed weights on the exact-fp32 MFMA, fp32 attention -- so mu_x and logw
+    are BITWISE those of the 32-true encoder (the alignment then follows 32-true's, which matches the
+    reference fixtures exactly); its backward stays the bf16 one (gradients within bf16 accuracy of the
+    bf16-mixed encoder's, not equal to 32-true's)."""
+    from golden.weights_recipe import apply_recipe
+    from matcha.models.components import _ops as O
+    from matcha.models.matcha_tts import MatchaTTS
+    from matcha.training import synthetic_batch
+
+    model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(DEV)
+    apply_recipe(model, 22)
+    model.eval()
+    bt = synthetic_batch(8, 120, 600, seed=5, device=DEV)
+    outs = {}
+    for mode in ("32-true", "fp32fwd", "bf16"):
+        model.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode != "32-true"), \
+                (O.precise_forward("fp32") if mode == "fp32fwd" else contextlib.nullcontext()):
+            mu, logw, _ = model.encoder(bt["x"], bt["x_lengths"])
+        (mu.square().sum() + logw.square().sum()).backward()
+        outs[mode] = (mu.detach().float(), logw.detach().float(),
+                      model.encoder.encoder.ffn_layers[2].conv_net[0].weight.grad.clone())
+    assert torch.equal(outs["fp32fwd"][0], outs["32-true"][0])
+    assert torch.equal(outs["fp32fwd"][1], outs["32-true"][1])
+    r = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
+    assert r(outs["fp32fwd"][2], outs["32-true"][2]) < 3e-2  # bf16 backward
+    assert r(outs["fp32fwd"][2], outs["bf16"][2]) < 3e-2
