@@ -164,9 +164,9 @@ def _bucketed_batches(B, Tx, Ty, n, rank, world, dev):
 # kernel families of the step, by the kernel's own name in a rocprofv3 trace
 FAMILIES = {
     "gemm": ("conv_gemm_kernel", "conv_gemm_glds_kernel", "splitk_epilogue_kernel"),
-    # weight-gradient GEMMs; their split sums run inside conv_wgrad_kernel (the last-arriving block of a tile,
-    # round 4); reduce_partials_kernel now only sums the LayerNorm / GroupNorm / bias partials -- not this family
-    "wgrad": ("conv_wgrad_kernel",),
+    # weight-gradient GEMMs + the step's batched fixed-order partial sums (reduce_partials_kernel: the split
+    # slabs, and the LayerNorm / GroupNorm / bias partials that ride in the same launches)
+    "wgrad": ("conv_wgrad_kernel", "reduce_partials_kernel"),
     "attn": ("attn_fwd_kernel", "attn_bwd_dq_kernel", "attn_bwd_dkv_kernel", "attn_drow_kernel",
              "attn_bwd_merged_kernel", "attn_fwd_short_kernel", "attn_bwd_dq_short_kernel", "attn_bwd_dkv_short_kernel"),
 }
@@ -591,10 +591,11 @@ def main():
         "launches; bytes = A rows read once + packed W (both planes when split) + C written (+ aux / residual / "
         "pre-activation streams) per launch; FLOP = 2 M N K")
     roofline_wgrad = roofline_of(
-        wgrad_log, "wgrad", "conv_wgrad_kernel (weight-gradient GEMMs, batched up to 12 jobs per launch, split slabs "
-        "summed in-kernel by each tile's last-arriving block)",
-        "2 M N K FLOP; bytes = dY + unique A rows + dW; graph time = the family's launches (their in-kernel split "
-        "sums included); the norms' gamma / beta partial sums (reduce_partials_kernel) are not in this family")
+        wgrad_log, "wgrad", "conv_wgrad_kernel + reduce_partials_kernel (weight-gradient GEMMs, batched up to 12 jobs "
+        "per launch, and the step's batched fixed-order partial sums, which also hold the LayerNorm / GroupNorm gamma / "
+        "beta partials)",
+        "2 M N K FLOP; bytes = dY + unique A rows + dW; graph time includes the whole batched reduce (the norms' "
+        "partial sums too: an upper bound on the GEMMs' own time)")
     roofline_attn = roofline_of(
         attn_log, "attn", "attn_fwd + backward (Drow pre-pass + merged dQ / dK-dV launch) kernels, long (decoder) and short (encoder, T <= 128)",
         "FLOP = 4 B H T^2 D fwd, 8 B H T^2 D bwd (standard flash-attention accounting, recomputation not counted); "

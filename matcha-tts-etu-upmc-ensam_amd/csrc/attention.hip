@@ -27,6 +27,22 @@
 #include "mtts_decoder.h"
 
 namespace {
+// XCD-aware block order (round 4): the dispatcher deals the linear block id (x fastest, then y, then z) round
+// robin over the 8 XCDs, so the query blocks of one (b, h) pair landed on 8 different L2s, each fetching that
+// pair's K / V (PMC: 1.78x the algorithmic bytes).  The id is relabelled so that consecutive (x, y, z) -- every
+// block of one pair, and for the merged backward both its dQ and dK / dV halves -- run on one XCD (the same
+// bijection as mtts::xcd_relabel of the GEMMs).
+__device__ __forceinline__ int3 xcd_blk3() {
+    const int gx = (int)gridDim.x, gy = (int)gridDim.y, nwg = gx * gy * (int)gridDim.z;
+    const int orig = (int)blockIdx.x + gx * ((int)blockIdx.y + gy * (int)blockIdx.z);
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    const int x = w % gx, t = w / gx;
+    return make_int3(x, t % gy, t / gy);
+}
+}  // namespace
+
+namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -392,8 +408,9 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<BF16, D, TI, DROP>())) vo
     int *flag_s = carve<int>(sp, NB);              // stage has a nonzero bias
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
-    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
-    const int q = blockIdx.x * kRowsPerBlock + wave * 32 + lr;
+    const int3 bk_ = xcd_blk3();
+    const int b = bk_.z, h = bk_.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
+    const int q = bk_.x * kRowsPerBlock + wave * 32 + lr;
     const bool q_ok = q < T;
     const TI *Kb = Kp + h * dh, *Vb = Vp + h * dh;
     const float c0 = key_bias_c0(p, b);
@@ -564,7 +581,8 @@ __device__ __forceinline__ void bwd_dq_body(const mtts_attn_args &p, const mtts_
     int *flag_s = carve<int>(sp, NB);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
-    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
+    const int3 bk_ = xcd_blk3();
+    const int b = bk_.z, h = bk_.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
     const int q = bx * kRowsPerBlock + wave * 32 + lr;
     const bool q_ok = q < T;
     const size_t qrow = (size_t)b * T + (q_ok ? q : 0);
@@ -687,7 +705,8 @@ __device__ __forceinline__ void bwd_dkv_body(const mtts_attn_args &p, const mtts
     float *d_s = carve<float>(sp, NB * kTile);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
-    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
+    const int3 bk_ = xcd_blk3();
+    const int b = bk_.z, h = bk_.y, T = p.T, dh = p.D;  // dh <= D: columns past dh are zero
     const int key = bx * kRowsPerBlock + wave * 32 + lr;
     const bool k_ok = key < T;
     const size_t krow = (size_t)b * T + (k_ok ? key : 0);
@@ -798,12 +817,12 @@ __device__ __forceinline__ void bwd_dkv_body(const mtts_attn_args &p, const mtts
 
 template <bool BF16, int D, typename TI = float, bool DROP = true>
 __global__ __launch_bounds__(kThreads, D <= 64 ? 2 : 1) void attn_bwd_dq_kernel(mtts_attn_args p, mtts_attn_grads g, float *Drow) {
-    bwd_dq_body<BF16, D, TI, DROP>(p, g, Drow, blockIdx.x);
+    bwd_dq_body<BF16, D, TI, DROP>(p, g, Drow, xcd_blk3().x);
 }
 template <bool BF16, int D, typename TI = float, bool DROP = true>
 __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_dkv_kernel(mtts_attn_args p, mtts_attn_grads g,
                                                                                         const float *Drow) {
-    bwd_dkv_body<BF16, D, TI, DROP>(p, g, Drow, blockIdx.x);
+    bwd_dkv_body<BF16, D, TI, DROP>(p, g, Drow, xcd_blk3().x);
 }
 
 // Drow pre-pass: rowsum(dO * O) per (query, head), grid (ceil(T/128), H, B), the dQ pass's lane mapping
@@ -812,8 +831,9 @@ template <int D, typename TI>
 __global__ __launch_bounds__(kThreads) void attn_drow_kernel(mtts_attn_args p, mtts_attn_grads g, float *Drow) {
     const TI *Op = reinterpret_cast<const TI *>(p.o), *Gp = reinterpret_cast<const TI *>(g.dout);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
-    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;
-    const int q = blockIdx.x * kRowsPerBlock + wave * 32 + lr;
+    const int3 bk_ = xcd_blk3();
+    const int b = bk_.z, h = bk_.y, T = p.T, dh = p.D;
+    const int q = bk_.x * kRowsPerBlock + wave * 32 + lr;
     const bool q_ok = q < T;
     const size_t qrow = (size_t)b * T + (q_ok ? q : 0);
     const float dsum = row_dot<D>(Op + qrow * p.ldo + h * dh, Gp + qrow * g.lddo + h * dh, lh, dh, q_ok);
@@ -826,8 +846,9 @@ __global__ __launch_bounds__(kThreads) void attn_drow_kernel(mtts_attn_args p, m
 template <bool BF16, int D, typename TI = float, bool DROP = true>
 __global__ __launch_bounds__(kThreads, (BF16 && D <= 64) ? 2 : 1) void attn_bwd_merged_kernel(mtts_attn_args p, mtts_attn_grads g,
                                                                                            float *Drow, int nq) {
-    if ((int)blockIdx.x < nq) bwd_dq_body<BF16, D, TI, DROP>(p, g, nullptr, blockIdx.x);
-    else bwd_dkv_body<BF16, D, TI, DROP>(p, g, Drow, blockIdx.x - nq);
+    const int bx = xcd_blk3().x;
+    if (bx < nq) bwd_dq_body<BF16, D, TI, DROP>(p, g, nullptr, bx);
+    else bwd_dkv_body<BF16, D, TI, DROP>(p, g, Drow, bx - nq);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -931,8 +952,9 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_short_kernel(mtts_attn_args
     float *ms = reinterpret_cast<float *>(smem + S::xoff(1)), *ls = ms + kWaves * 32;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
-    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;
-    const int q = blockIdx.x * kShortRows + lr;
+    const int3 bk_ = xcd_blk3();
+    const int b = bk_.z, h = bk_.y, T = p.T, dh = p.D;
+    const int q = bk_.x * kShortRows + lr;
     const bool q_ok = q < T;
     const int buf = wave >> 1, sub = wave & 1;
     const float c0 = key_bias_c0(p, b), sl2 = p.scale * kLog2e;
@@ -1035,8 +1057,9 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_short_kernel(mtts_attn_a
     float *area = reinterpret_cast<float *>(smem);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
-    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;
-    const int q = blockIdx.x * kShortRows + lr;
+    const int3 bk_ = xcd_blk3();
+    const int b = bk_.z, h = bk_.y, T = p.T, dh = p.D;
+    const int q = bk_.x * kShortRows + lr;
     const bool q_ok = q < T;
     const size_t qrow = (size_t)b * T + (q_ok ? q : 0);
     const int buf = wave >> 1, sub = wave & 1;
@@ -1144,8 +1167,9 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkv_short_kernel(mtts_attn_
     float *area_k = reinterpret_cast<float *>(smem), *area_v = reinterpret_cast<float *>(smem + S::acc_set);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
-    const int b = blockIdx.z, h = blockIdx.y, T = p.T, dh = p.D;
-    const int key = blockIdx.x * kShortRows + lr;
+    const int3 bk_ = xcd_blk3();
+    const int b = bk_.z, h = bk_.y, T = p.T, dh = p.D;
+    const int key = bk_.x * kShortRows + lr;
     const bool k_ok = key < T;
     const size_t krow = (size_t)b * T + (k_ok ? key : 0);
     const int buf = wave >> 1, sub = wave & 1;

@@ -98,8 +98,13 @@ struct Stage<false> {
 // weights) at W + N*Kp; it is staged beside the first and every fragment pair issues two MFMAs.
 // AS (with WS, MTTS_GEMM_F_A_SPLIT): the staging pass also writes A's rounding residual bf16(a - bf16(a))
 // as a second A plane, and each fragment triple issues A_hi*W_hi, A_hi*W_lo, A_lo*W_hi (bf16x3).
+// Split-K (part != NULL, round 4; fp32 schedules): grid = tiles x S with the S splits of a tile adjacent (one
+// XCD); split s runs K steps [s * ksteps, min(nk, (s + 1) * ksteps)) and stores its raw fp32 partial tile to
+// part[s][M][N]; mtts::splitk_combine (conv_gemm_glds.hip) then sums the splits in order and runs the
+// epilogue.  For the text encoder's long reductions on few row tiles (3840 x 192 x 2304: 240 tiles of 72
+// K steps at fp32 -- the parity policy's exact-fp32 encoder forward and 32-true).
 template <bool BF16, int WM, int WN, int TM, int TN, int KB = kBK, int DEPTH = 1, bool WS = false, bool AS = false>
-__global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_args p) {
+__global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_args p, int ksteps, float *part) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN;
     constexpr int KC = KB / 8;                    // 8-element chunks per staged row
@@ -125,17 +130,25 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
     // so block id b is relabelled to the (b % 8)-th contiguous run of tiles (bijective for any grid
     // size), and tiles are numbered N-fastest -- every column block of an A row panel runs on the same
     // XCD at about the same time and reads the panel from that XCD's L2
-    int m0, n0;
+    int m0, n0, kstep0 = 0, nk = (p.K + KB - 1) / KB;
     {
         const int nt = (p.N + BN - 1) / BN;
         const int nwg = gridDim.x, orig = blockIdx.x;
         const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-        const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+        int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+        if (part) {  // split-K: the splits of a tile are adjacent
+            const int ntiles = ((M + BM - 1) / BM) * nt;
+            const int S = nwg / ntiles;
+            const int tile = wgid / S, split = wgid - tile * S;
+            wgid = tile;
+            kstep0 = split * ksteps;
+            nk = min(ksteps, nk - kstep0);
+        }
         const int mt = wgid / nt;
         m0 = mt * BM;
         n0 = (wgid - mt * nt) * BN;
     }
-    const int nk = (p.K + KB - 1) / KB;
+    const int kbase = kstep0 * KB;  // absolute K offset of this block's first step
     const float inv_to = 1.0f / (float)p.To;
 
     Gather ga[CA];
@@ -158,8 +171,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
         if (ga[c].valid) divmod_fast(m, p.To, inv_to, b, u);
         ga[c].in_base = b * p.Ti;
         ga[c].in_u = u * p.in_stride;
-        a_j[c] = a_kc[c] / p.cin;
-        a_ch[c] = a_kc[c] - a_j[c] * p.cin;
+        a_j[c] = (kbase + a_kc[c]) / p.cin;
+        a_ch[c] = kbase + a_kc[c] - a_j[c] * p.cin;
         a_toff[c] = toff_of(a_j[c]);
     }
     int b_row[CB], b_kc[CB];
@@ -345,17 +358,17 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
     if constexpr (BF16 && DEPTH == 2) {
         // two K steps in flight: the loads of step kt+2 are issued before computing step kt, stored to
         // LDS after computing step kt+1 -- two compute phases cover each global round trip
-        load_tile(R0, 0);
+        load_tile(R0, kbase);
         store_tile(R0, 0);
-        load_tile(R1, KB);
+        load_tile(R1, kbase + KB);
         mtts::lds_barrier();
         for (int kt = 0; kt < nk; kt += 2) {
-            load_tile(R0, (kt + 2) * KB);
+            load_tile(R0, kbase + (kt + 2) * KB);
             compute(0);
             store_tile(R1, 1);
             mtts::lds_barrier();
             if (kt + 1 >= nk) break;
-            load_tile(R1, (kt + 3) * KB);
+            load_tile(R1, kbase + (kt + 3) * KB);
             compute(1);
             store_tile(R0, 0);
             mtts::lds_barrier();
@@ -363,11 +376,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
     } else {
         // branch-free body (no phi copies of in-flight registers): the step after the last one loads
         // clamped addresses with every chunk masked off and stores into the unused buffer
-        load_tile(R0, 0);
+        load_tile(R0, kbase);
         store_tile(R0, 0);
         mtts::lds_barrier();
         for (int kt = 0; kt < nk; ++kt) {
-            load_tile(R0, (kt + 1) * KB);
+            load_tile(R0, kbase + (kt + 1) * KB);
             compute(kt & 1);
             store_tile(R0, (kt + 1) & 1);
             mtts::lds_barrier();
@@ -377,6 +390,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
     // ---- epilogue ---- (the K loop ended with a barrier after every wave's last LDS access: Bs is free
     // for the 16-byte-row epilogue's per-wave 4 KiB staging images when it is large enough)
     if constexpr (sizeof(Bs) >= (size_t)WM * WN * 4096) {
+        if (part) {  // split-K partial (the launcher only splits when Bs holds the staging images)
+            mtts::gemm_store_partial<TM, TN>(p, acc, reinterpret_cast<float *>(reinterpret_cast<unsigned char *>(&Bs[0][0]) + wave * 4096),
+                                             part + (size_t)(kstep0 / ksteps) * M * p.N, m0 + wr * 32 * TM, n0 + wc * 32 * TN,
+                                             lane);
+            return;
+        }
         if (mtts::gemm_epilogue_vec_ok(p)) {
             mtts::gemm_epilogue_vec<TM, TN>(p, acc, reinterpret_cast<float *>(reinterpret_cast<unsigned char *>(&Bs[0][0]) + wave * 4096),
                                             m0 + wr * 32 * TM, n0 + wc * 32 * TN, lane);
@@ -959,13 +978,23 @@ constexpr TileCfg kCfgs[] = {
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
+namespace mtts {
+// conv_gemm_glds.hip: sum part[0..S)[M][N] in split order + the epilogue (splitk_epilogue_kernel)
+int splitk_combine(const mtts_conv_gemm_args &p, int M, const float *part, int S, hipStream_t st);
+}
+
 template <bool BF16, int C, bool WS = false, bool AS = false>
-static void launch_cfg(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+static void launch_cfg(const mtts_conv_gemm_args &p, int M, hipStream_t st, int splits = 1, float *part = nullptr) {
     constexpr TileCfg c = kCfgs[C];
     constexpr int BM = 32 * c.wm * c.tm, BN = 32 * c.wn * c.tn;
-    dim3 grid((unsigned)(((M + BM - 1) / BM) * ((p.N + BN - 1) / BN)));
-    hipLaunchKernelGGL((conv_gemm_kernel<BF16, c.wm, c.wn, c.tm, c.tn, (BF16 ? c.kb : kBK), (BF16 ? c.depth : 1), WS, AS>),
-                       grid, dim3(64 * c.wm * c.wn), 0, st, p);
+    constexpr int KBc = BF16 ? c.kb : kBK;
+    const int nk = (p.K + KBc - 1) / KBc;
+    const int ksteps = splits > 1 ? (nk + splits - 1) / splits : nk;
+    const int S = splits > 1 ? (nk + ksteps - 1) / ksteps : 1;  // every split non-empty
+    dim3 grid((unsigned)(((M + BM - 1) / BM) * ((p.N + BN - 1) / BN) * S));
+    hipLaunchKernelGGL((conv_gemm_kernel<BF16, c.wm, c.wn, c.tm, c.tn, KBc, (BF16 ? c.depth : 1), WS, AS>),
+                       grid, dim3(64 * c.wm * c.wn), 0, st, p, ksteps, S > 1 ? part : nullptr);
+    if (S > 1) mtts::splitk_combine(p, M, part, S, st);
 }
 
 // Split-weight (MTTS_GEMM_F_W_SPLIT) register schedules: the two the heuristic picks, 7 (32-wide K steps)
@@ -983,7 +1012,11 @@ static void launch_ws(int id, const mtts_conv_gemm_args &p, int M, hipStream_t s
 }
 
 template <bool BF16>
-static void launch_by_id(int id, const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+static void launch_by_id(int id, const mtts_conv_gemm_args &p, int M, hipStream_t st, int splits = 1, float *part = nullptr) {
+    if (splits > 1 && !BF16 && id == 7) {  // fp32 split-K: config 7 only (pick_splits)
+        launch_cfg<BF16, 7>(p, M, st, splits, part);
+        return;
+    }
     switch (id) {
         case 0: launch_cfg<BF16, 0>(p, M, st); break;
         case 1: launch_cfg<BF16, 1>(p, M, st); break;
@@ -1060,7 +1093,20 @@ static int pick_cfg_a16(const mtts_conv_gemm_args &p, int M) {
 }
 
 // Split-K (LDS-DMA schedules, heuristic pick only): grids below half the chip with >= 24 K steps
-static int pick_splits(const mtts_conv_gemm_args &p, int M, int cfg, int splits) {
+// fp32 register schedule 7 (32 x 128): split K when its tiles fill under one round with >= 48 K steps of 32
+// (the text encoder's FFN down-projection, 3840 x 192 x 2304: 240 tiles x 72 steps, 86-98 us unsplit in the
+// parity policy's fp32 encoder forward, profiles/r04/fused_wgrad_sum/launches); MTTS_GEMM_F32_SPLITK=0: off
+static int pick_splits_f32(const mtts_conv_gemm_args &p, int M, int cfg, int splits) {
+    static const bool off = [] { const char *e = getenv("MTTS_GEMM_F32_SPLITK"); return e && e[0] == '0'; }();
+    if (cfg != 7 || p.N % 4 || off || !mtts::gemm_epilogue_vec_ok(p)) return 1;  // the combine is float4
+    if (splits > 0) return splits;
+    const int tiles = ((M + 31) / 32) * ((p.N + 127) / 128), nk = (p.K + kBK - 1) / kBK;
+    if (tiles >= 256 || nk < 48) return 1;
+    return 4;
+}
+
+static int pick_splits(const mtts_conv_gemm_args &p, int M, int cfg, int splits, bool bf16) {
+    if (!bf16) return pick_splits_f32(p, M, cfg, splits);
     if (cfg < MTTS_GEMM_GLDS || p.N % 4) return 1;
     if (splits > 0) return splits;
     const int nk = (p.K + 63) / 64;
@@ -1076,8 +1122,15 @@ struct GemmPlan {
 static GemmPlan plan_gemm(const mtts_conv_gemm_args &p, bool bf16, int cfg, int splits) {
     const int M = p.nb * p.To;
     if (cfg < 0) cfg = pick_cfg(p, M, bf16);
-    splits = pick_splits(p, M, cfg, splits);
-    return {cfg, splits, cfg >= MTTS_GEMM_GLDS ? mtts::conv_gemm_glds_splitk_bytes(p, splits) : 0};
+    splits = pick_splits(p, M, cfg, splits, bf16);
+    size_t ws = 0;
+    if (cfg >= MTTS_GEMM_GLDS) {
+        ws = mtts::conv_gemm_glds_splitk_bytes(p, splits);
+    } else if (splits > 1) {
+        const int nk = (p.K + kBK - 1) / kBK, ksteps = (nk + splits - 1) / splits, S = (nk + ksteps - 1) / ksteps;
+        ws = S > 1 ? (size_t)S * M * p.N * sizeof(float) : 0;
+    }
+    return {cfg, splits, ws};
 }
 
 static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, int cfg, int splits, void *ws,
@@ -1134,7 +1187,11 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     }
     if (bf16 && (p.flags & MTTS_GEMM_F_W_SPLIT)) launch_ws(pl.cfg, p, M, st);
     else if (bf16) launch_by_id<true>(pl.cfg, p, M, st);
-    else launch_by_id<false>(pl.cfg, p, M, st);
+    else {
+        int s = pl.splits;
+        if (pl.ws == 0 || !ws || ws_bytes < pl.ws || (uintptr_t)ws % 16) s = 1;  // no workspace: unsplit
+        launch_by_id<false>(pl.cfg, p, M, st, s, static_cast<float *>(ws));
+    }
     return mtts::check_launch("conv_gemm_kernel");
 }
 
@@ -1419,10 +1476,14 @@ static bool defer_wgrads() {
 
 // Arrival counters of the in-kernel split sums (wgrad_combine): one zeroed pool per device, handed out as a
 // ring (each launch's tiles get their own counters; the last arriver of a tile re-zeroes its counter, so a
-// range is free again once its launch has run).  MTTS_WGRAD_FUSED_SUM=0: the separate reduce launch instead.
+// range is free again once its launch has run).  Opt-in, MTTS_WGRAD_FUSED_SUM=1: measured in the graph-replayed
+// step (round 4, profiles/r04/fused_wgrad_sum/) the weight-gradient family took 4.2 ms instead of 1.2 + 0.29 ms
+// (GEMMs + the batched reduce launches): every block's agent-scope release writes back its XCD's dirty L2
+// lines (a 64 KB slab per block, ~6.5 us per 16 KB in MI355X_MICROARCH.md's price list) before its ticket, on
+// the block's own critical path.  Default: the separate fixed-order reduce launch.
 constexpr int kCntPool = 1 << 16;
 static int32_t *wgrad_counters(int n, hipStream_t st) {
-    static const bool off = [] { const char *e = getenv("MTTS_WGRAD_FUSED_SUM"); return e && e[0] == '0'; }();
+    static const bool off = [] { const char *e = getenv("MTTS_WGRAD_FUSED_SUM"); return !(e && e[0] == '1'); }();
     if (off || n <= 0 || n > kCntPool / 16) return nullptr;
     static std::mutex mu;
     static int32_t *pool[64] = {};

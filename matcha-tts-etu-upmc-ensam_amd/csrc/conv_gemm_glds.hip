@@ -504,6 +504,12 @@ size_t conv_gemm_glds_splitk_bytes(const mtts_conv_gemm_args &p, int splits) {
     return S > 1 ? (size_t)S * p.nb * p.To * p.N * sizeof(float) : 0;
 }
 
+int splitk_combine(const mtts_conv_gemm_args &p, int M, const float *part, int S, hipStream_t st) {
+    const long long n4 = (long long)M * (p.N / 4);
+    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, p, part, S);
+    return mtts::check_launch("splitk_epilogue_kernel");
+}
+
 int conv_gemm_glds_launch(int id, const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
     return launch_glds_id(id, p, M, splits, part, st, std::make_integer_sequence<int, kNumGlds>{});
 }

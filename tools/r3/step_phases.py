@@ -18,11 +18,11 @@ def name(r):
     return m.group(1) if m else n[:30]
 
 
-marks = [("mas_dp_kernel", "last"), ("loss_partials_kernel", "last"), ("expand_rows_bwd_kernel", "first"),
+marks = [(("mas_dp_kernel", "mas_dp_mw_kernel"), "last"), ("loss_partials_kernel", "last"), ("expand_rows_bwd_kernel", "first"),
          ("embedding_bwd_kernel", "last")]
 cuts = []
 for k, how in marks:
-    hits = [i for i, r in enumerate(seg) if name(r) == k]
+    hits = [i for i, r in enumerate(seg) if name(r) in (k if isinstance(k, tuple) else (k,))]
     cuts.append((hits[-1] if how == "last" else hits[0] - 1) + 1 if hits else None)
 labels = ["encoder fwd + MAS", "decoder fwd + losses", "decoder bwd", "encoder bwd", "sums + optimizer"]
 bounds = [0] + [c for c in cuts] + [len(seg)]
