@@ -988,6 +988,10 @@ static void launch_cfg(const mtts_conv_gemm_args &p, int M, hipStream_t st, int 
     constexpr TileCfg c = kCfgs[C];
     constexpr int BM = 32 * c.wm * c.tm, BN = 32 * c.wn * c.tn;
     constexpr int KBc = BF16 ? c.kb : kBK;
+    // the split-K partial store stages through the kernel's Bs (as the vector epilogue): it must hold the waves'
+    // 4 KiB images, else the launch stays unsplit
+    constexpr size_t kBsBytes = (size_t)2 * (WS ? 2 : 1) * (BN + 1) * (KBc + Stage<BF16>::PAD) * sizeof(typename Stage<BF16>::T);
+    if (kBsBytes < (size_t)c.wm * c.wn * 4096) splits = 1;
     const int nk = (p.K + KBc - 1) / KBc;
     const int ksteps = splits > 1 ? (nk + splits - 1) / splits : nk;
     const int S = splits > 1 ? (nk + ksteps - 1) / ksteps : 1;  // every split non-empty
@@ -1013,29 +1017,26 @@ static void launch_ws(int id, const mtts_conv_gemm_args &p, int M, hipStream_t s
 
 template <bool BF16>
 static void launch_by_id(int id, const mtts_conv_gemm_args &p, int M, hipStream_t st, int splits = 1, float *part = nullptr) {
-    if (splits > 1 && !BF16 && id == 7) {  // fp32 split-K: config 7 only (pick_splits)
-        launch_cfg<BF16, 7>(p, M, st, splits, part);
-        return;
-    }
+    if (BF16) splits = 1;  // split-K on the register schedules: fp32 only
     switch (id) {
-        case 0: launch_cfg<BF16, 0>(p, M, st); break;
-        case 1: launch_cfg<BF16, 1>(p, M, st); break;
-        case 2: launch_cfg<BF16, 2>(p, M, st); break;
-        case 3: launch_cfg<BF16, 3>(p, M, st); break;
-        case 4: launch_cfg<BF16, 4>(p, M, st); break;
-        case 5: launch_cfg<BF16, 5>(p, M, st); break;
-        case 6: launch_cfg<BF16, 6>(p, M, st); break;
-        case 7: launch_cfg<BF16, 7>(p, M, st); break;
-        case 8: launch_cfg<BF16, 8>(p, M, st); break;
-        case 9: launch_cfg<BF16, 9>(p, M, st); break;
-        case 10: launch_cfg<BF16, 10>(p, M, st); break;
-        case 11: launch_cfg<BF16, 11>(p, M, st); break;
-        case 12: launch_cfg<BF16, 12>(p, M, st); break;
-        case 13: launch_cfg<BF16, 13>(p, M, st); break;
-        case 14: launch_cfg<BF16, 14>(p, M, st); break;
-        case 15: launch_cfg<BF16, 15>(p, M, st); break;
-        case 16: launch_cfg<BF16, 16>(p, M, st); break;
-        default: launch_cfg<BF16, 17>(p, M, st); break;
+        case 0: launch_cfg<BF16, 0>(p, M, st, splits, part); break;
+        case 1: launch_cfg<BF16, 1>(p, M, st, splits, part); break;
+        case 2: launch_cfg<BF16, 2>(p, M, st, splits, part); break;
+        case 3: launch_cfg<BF16, 3>(p, M, st, splits, part); break;
+        case 4: launch_cfg<BF16, 4>(p, M, st, splits, part); break;
+        case 5: launch_cfg<BF16, 5>(p, M, st, splits, part); break;
+        case 6: launch_cfg<BF16, 6>(p, M, st, splits, part); break;
+        case 7: launch_cfg<BF16, 7>(p, M, st, splits, part); break;
+        case 8: launch_cfg<BF16, 8>(p, M, st, splits, part); break;
+        case 9: launch_cfg<BF16, 9>(p, M, st, splits, part); break;
+        case 10: launch_cfg<BF16, 10>(p, M, st, splits, part); break;
+        case 11: launch_cfg<BF16, 11>(p, M, st, splits, part); break;
+        case 12: launch_cfg<BF16, 12>(p, M, st, splits, part); break;
+        case 13: launch_cfg<BF16, 13>(p, M, st, splits, part); break;
+        case 14: launch_cfg<BF16, 14>(p, M, st, splits, part); break;
+        case 15: launch_cfg<BF16, 15>(p, M, st, splits, part); break;
+        case 16: launch_cfg<BF16, 16>(p, M, st, splits, part); break;
+        default: launch_cfg<BF16, 17>(p, M, st, splits, part); break;
     }
 }
 
@@ -1057,7 +1058,10 @@ static void launch_by_id(int id, const mtts_conv_gemm_args &p, int M, hipStream_
 static int glds_tiles(const mtts_conv_gemm_args &p, int M) { return ((M + 63) / 64) * ((p.N + 255) / 256); }
 
 static int pick_cfg(const mtts_conv_gemm_args &p, int M, bool bf16) {
-    if (!bf16) return 7;
+    // fp32: 64 x 64 tiles (config 3) on the text encoder's 3840-row GEMMs -- the best register schedule on every
+    // one of its exact-fp32 forward calls (tools/r4/gemm_f32_sweep.py, profiles/r04/sweeps/f32_sweep.jsonl: 1044 ->
+    // 841 us per step with the split-K counts below); the decoder-sized fp32 GEMMs keep config 7
+    if (!bf16) return M <= 8192 ? 3 : 7;
     if (p.act == MTTS_ACT_GELU || p.act == MTTS_ACT_DGELU) return 7;
     static const int sched_mask = [] {  // MTTS_GEMM_SCHED_OFF bit mask: A/B switch for experiments
         const char *e = getenv("MTTS_GEMM_SCHED_OFF");
@@ -1092,17 +1096,40 @@ static int pick_cfg_a16(const mtts_conv_gemm_args &p, int M) {
     return glds_tiles(p, M) >= 256 ? MTTS_GEMM_GLDS + 9 : MTTS_GEMM_GLDS + 12;
 }
 
+// Split weight planes (MTTS_GEMM_F_W_SPLIT, the parity policy's decoder forward): W's bytes double, which moves
+// the best schedules (step sweep with the split planes, tools/r3/gemm_step_sweep.py SWEEP_PREC=bf16-parity ->
+// profiles/r04/sweeps/ws_sweep.jsonl: 2655 -> ~2410 us per step): GELU epilogues keep the 32 x 128 register
+// tiles; whole-tap K steps take the LDS-DMA kernels -- 64 x 64 three-stage (bf16 A) / two-stage (fp32 A) on
+// the 19200-row N <= 256 GEMMs (31.6 vs 36.0 us, 36.5 vs 56.3), 64 x 256 elsewhere (9600 x 256 x 512: 17.0 vs
+// 30.6 on the register schedule the one-plane rule picks below K = 768); other K layouts the 32-wide register
+// tiles (19200 x 256 x 480: 32.8 vs 50.6 with 64-wide steps).
+static int pick_cfg_ws(const mtts_conv_gemm_args &p, int M) {
+    if (p.act == MTTS_ACT_GELU || p.act == MTTS_ACT_DGELU) return 7;
+    if (!mtts::conv_gemm_glds_applies(p) || !mtts::conv_gemm_glds_lean(p)) return 7;
+    const bool big = M >= 16384 && p.N <= 256;
+    if (p.flags & MTTS_GEMM_F_A_BF16) return big ? MTTS_GEMM_GLDS + 12 : MTTS_GEMM_GLDS + 9;
+    return M >= 16384 ? MTTS_GEMM_GLDS + 13 : MTTS_GEMM_GLDS + 9;
+}
+
 // Split-K (LDS-DMA schedules, heuristic pick only): grids below half the chip with >= 24 K steps
 // fp32 register schedule 7 (32 x 128): split K when its tiles fill under one round with >= 48 K steps of 32
 // (the text encoder's FFN down-projection, 3840 x 192 x 2304: 240 tiles x 72 steps, 86-98 us unsplit in the
 // parity policy's fp32 encoder forward, profiles/r04/fused_wgrad_sum/launches); MTTS_GEMM_F32_SPLITK=0: off
 static int pick_splits_f32(const mtts_conv_gemm_args &p, int M, int cfg, int splits) {
     static const bool off = [] { const char *e = getenv("MTTS_GEMM_F32_SPLITK"); return e && e[0] == '0'; }();
-    if (cfg != 7 || p.N % 4 || off || !mtts::gemm_epilogue_vec_ok(p)) return 1;  // the combine is float4
-    if (splits > 0) return splits;
-    const int tiles = ((M + 31) / 32) * ((p.N + 127) / 128), nk = (p.K + kBK - 1) / kBK;
-    if (tiles >= 256 || nk < 48) return 1;
-    return 4;
+    if (p.N % 4 || off || !mtts::gemm_epilogue_vec_ok(p)) return 1;  // the combine is float4
+    if (splits > 0) return splits;  // explicit (sweeps): any register schedule
+    const int nk = (p.K + kBK - 1) / kBK;
+    if (cfg == 3) {  // 64 x 64: 4 splits from 28 K steps, 2 from 20 (sweep: 3840 x 192 x 2304 44 us at 4 vs 58 at
+                     // 1; k = 5 prenet 27.4 at 4; 3840 x 256 x 768 25.8 at 2; 576-deep ones unsplit)
+        const int tiles = ((M + 63) / 64) * ((p.N + 63) / 64);
+        if (tiles >= 256 || nk < 20) return 1;
+        return nk >= 28 ? 4 : 2;
+    }
+    if (cfg != 7) return 1;
+    const int tiles = ((M + 31) / 32) * ((p.N + 127) / 128);
+    if (tiles >= 256 || nk < 16) return 1;
+    return std::min(8, std::max(2, nk / 9));  // ~9 K steps of 32 per split
 }
 
 static int pick_splits(const mtts_conv_gemm_args &p, int M, int cfg, int splits, bool bf16) {
@@ -1165,6 +1192,9 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     const bool bf16 = precision == MTTS_PREC_BF16;
     if (glds_id && (!bf16 || !mtts::conv_gemm_glds_applies(p)))
         return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: LDS-DMA schedule needs bf16, cin >= 64 and a 0/1 a_scale");
+    static const bool ws_pick = [] { const char *e = getenv("MTTS_GEMM_WS_PICK"); return !(e && e[0] == '0'); }();
+    if (cfg < 0 && bf16 && ws_pick && (p.flags & MTTS_GEMM_F_W_SPLIT) && !(p.flags & MTTS_GEMM_F_A_SPLIT))
+        cfg = pick_cfg_ws(p, M);
     if (p.flags & MTTS_GEMM_F_A_BF16) {  // bf16 A operands exist only in the LDS-DMA kernels
         if (!bf16 || !mtts::conv_gemm_glds_applies(p))
             return mtts::fail(MTTS_ERR_UNSUPPORTED,
@@ -1482,6 +1512,8 @@ static bool defer_wgrads() {
 // lines (a 64 KB slab per block, ~6.5 us per 16 KB in MI355X_MICROARCH.md's price list) before its ticket, on
 // the block's own critical path.  Default: the separate fixed-order reduce launch.
 constexpr int kCntPool = 1 << 16;
+// (A fence-free variant -- whole-line slab stores, the last arriver polling the counter with sc1 loads -- gave
+// wrong sums and a poll that never matched (the counter line stale in the reader's L2): removed, round 4.)
 static int32_t *wgrad_counters(int n, hipStream_t st) {
     static const bool off = [] { const char *e = getenv("MTTS_WGRAD_FUSED_SUM"); return !(e && e[0] == '1'); }();
     if (off || n <= 0 || n > kCntPool / 16) return nullptr;
@@ -1582,7 +1614,7 @@ static int conv_wgrad_impl(const mtts_conv_wgrad_args *args, int32_t precision, 
         w.splits = 1;
         w.k.part_db = db ? part_db : nullptr;
     } else {
-        // in-kernel split sums (no reduce job) unless the counter pool is unavailable
+        // in-kernel split sums (no reduce job) when enabled and the counter pool is available
         w.k.cnt = wgrad_counters(((p.N + 127) / 128) * ((p.K + 127) / 128), st);
         if (queue) {
             std::lock_guard<std::mutex> lk(g_wq_mu);
