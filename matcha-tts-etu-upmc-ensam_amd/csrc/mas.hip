@@ -199,9 +199,12 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
 #pragma unroll
                     for (int i = 0; i < K; ++i) {
                         const float fp = (i == 0) ? nb : dp[i - 1];  // core.pyx:65-66
-                        const float fs = dp[i];                      // core.pyx:70-71 (dp init = neg)
                         const int d = y - (x0 + i);
-                        const bool diag = (fp >= fs) || (d == 0);    // core.pyx:73
+                        // core.pyx:70-73: diag = from_prev >= from_same or x == y.  The x == y case enters as
+                        // from_same = -inf (fp is never NaN, so fp >= -inf holds): one compare and one select on
+                        // the column chain instead of a VALU -> SALU -> VALU mask round trip (same decisions)
+                        const float fs = d == 0 ? -INFINITY : dp[i];
+                        const bool diag = fp >= fs;
                         const float best = diag ? fp : fs;
                         const float v = best + s[i];                 // core.pyx:80
                         ndp[i] = ((unsigned)d <= span) ? v : neg;    // band x_min..x_max, :59-62
@@ -399,10 +402,11 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
                 for (int j = 0; j < C; ++j) {
                     const int jc = s * C + j;  // column within the chunk
                     const int y = y0 + j;
-                    float prev;
-                    if (jc == 0) prev = edge[(p3 * W) * CC + (wave > 0 ? wave - 1 : 0) * CC + CC - 1];
-                    else prev = ein[r3 * W * CC + jc - 1];
-                    nbl[j] = wave == 0 ? (y == 0 ? 0.0f : neg) : (y == 0 ? neg : prev);
+                    // read unconditionally (wave 0 reads a valid slot and ignores it): selects, no branches
+                    const float prev = jc == 0 ? edge[(p3 * W) * CC + (wave > 0 ? wave - 1 : 0) * CC + CC - 1]
+                                               : ein[r3 * W * CC + jc - 1];
+                    const float first = wave == 0 ? 0.0f : neg;  // the column-0 predecessor of the wave's first row
+                    nbl[j] = y == 0 ? first : (wave == 0 ? neg : prev);
                 }
                 float eo[C];
 #pragma unroll
@@ -421,9 +425,9 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
 #pragma unroll
                         for (int i = 0; i < KL; ++i) {
                             const float fp = (i == 0) ? nb : dp[i - 1];  // core.pyx:65-66
-                            const float fs = dp[i];                      // core.pyx:70-71
                             const int d = y - (x0 + i);
-                            const bool diag = (fp >= fs) || (d == 0);    // core.pyx:73
+                            const float fs = d == 0 ? -INFINITY : dp[i];  // core.pyx:70-73 (see mas_dp_kernel)
+                            const bool diag = fp >= fs;
                             const float best = diag ? fp : fs;
                             const float v = best + sc[i];                // core.pyx:80
                             ndp[i] = ((unsigned)d <= span) ? v : neg;    // band, :59-62

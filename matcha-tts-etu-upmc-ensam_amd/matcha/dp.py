@@ -117,23 +117,30 @@ class GradBucketReducer:
 
     N_SCALARS = 4
 
-    def __init__(self, params, comm, bucket_mb: float = 16.0, device=None, tail_mb: float = 4.0):
+    def __init__(self, params, comm, bucket_mb: float = 16.0, device=None, tail_mb: float = 4.0, seams=()):
         self.params = list(params)
         self.comm = comm
         self.device = device or self.params[0].device
         self.index = {id(p): i for i, p in enumerate(self.params)}
         # buckets are cut from the END of the arrival order: the last bucket (the first layers, whose
         # gradients backward finishes last) is the one whose reduction cannot overlap anything, so it
-        # is kept small (tail_mb); the others are ~bucket_mb
+        # is kept small (tail_mb); the others are ~bucket_mb.  seams: parameters that start a new bucket
+        # whatever the size (the Trainer passes the text encoder's first-arriving parameter: the decoder's
+        # gradients then form their own bucket(s), issued at the decoder / encoder seam of the backward --
+        # exactly where the N=1 step flushes the decoder's queued weight gradients onto the side stream)
         limit = max(int(bucket_mb * 2 ** 20 / 4), 1)
         tail = max(int(min(tail_mb, bucket_mb) * 2 ** 20 / 4), 1)
-        cuts, end, size = [], len(self.params), 0
-        for i in range(len(self.params) - 1, -1, -1):
-            size += self.params[i].numel()
-            if size >= (tail if not cuts else limit) and i > 0:
-                cuts.append((i, end))
-                end, size = i, 0
-        cuts.append((0, end))
+        seam_idx = sorted({self.index[id(p)] for p in seams if id(p) in self.index} - {0})
+        bounds = [0] + seam_idx + [len(self.params)]
+        cuts = []
+        for seg_lo, seg_hi in reversed(list(zip(bounds[:-1], bounds[1:]))):
+            end, size = seg_hi, 0
+            for i in range(seg_hi - 1, seg_lo - 1, -1):
+                size += self.params[i].numel()
+                if size >= (tail if not cuts else limit) and i > seg_lo:
+                    cuts.append((i, end))
+                    end, size = i, 0
+            cuts.append((seg_lo, end))
         self.buckets = [c for c in reversed(cuts) if c[1] > c[0]] or [(0, len(self.params))]  # (start, end)
         self.bucket_of = []
         for k, (s, e) in enumerate(self.buckets):

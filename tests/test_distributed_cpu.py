@@ -176,3 +176,21 @@ def test_graph_step_shape_agreement_two_ranks_gloo():
     for r in (0, 1):
         assert res[r][0] == want, res[r][0]
         assert res[r][1] and res[r][2]
+
+
+def test_bucket_layout_cuts_at_seams():
+    """GradBucketReducer(seams=...): a bucket boundary at every seam parameter (the Trainer passes the text
+    encoder's first-arriving parameter, so the decoder's gradients are issued together at the decoder / encoder
+    seam of the backward), the usual size cuts inside each part, the small tail bucket last."""
+    from matcha.dp import GradBucketReducer
+
+    ps = [torch.zeros(1000, requires_grad=True) for _ in range(10)]
+    r = GradBucketReducer(ps, None, bucket_mb=1.0, device=torch.device("cpu"), tail_mb=0.005, seams=[ps[6]])
+    assert r.buckets[0][0] == 0 and r.buckets[-1][1] == 10
+    assert all(b[1] == c[0] for b, c in zip(r.buckets, r.buckets[1:]))  # contiguous
+    assert not any(s < 6 < e for s, e in r.buckets) and any(s == 6 for s, _ in r.buckets)
+    assert r.buckets[-1][1] - r.buckets[-1][0] == 2  # tail: the last 8 KB (>= 5 KB)
+    plain = GradBucketReducer(ps, None, bucket_mb=1.0, device=torch.device("cpu"), tail_mb=0.005)
+    assert any(s < 6 < e for s, e in plain.buckets)
+    r.remove()
+    plain.remove()
