@@ -449,14 +449,10 @@ int launch_glds_t(const mtts_conv_gemm_args &p, int M, int splits, float *part, 
 
 // Split-weight operands (MTTS_GEMM_F_W_SPLIT) run three instantiations: 64 x 64 three-stage (44) or
 // two-stage (45), and 64 x 256 two-stage (41, 144 KiB with bf16 A, 160 KiB with fp32 A) for the wide tiles
-// (round 4) and 128 x 128 two-stage (34: 128 KiB with fp32 A) -- W is re-streamed by half as many row tiles as
-// with 64-row tiles, which the doubled weight bytes of the split planes make worth it on the 1024-wide FFN
-// projections
+// (a 128 x 128 two-stage split-weight instance, round 4, ran 3-5x slower than the 64-row ones on the FFN
+// up-projection -- tools/r4/ff1_probe.py, profiles/r04/sweeps/ff1_probe.txt -- and was removed)
 template <int C>
 int launch_glds_ws(const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
-    if constexpr (C == 2) {  // fp32 A only (34 has no bf16-A instantiation)
-        if (!(p.flags & MTTS_GEMM_F_A_BF16)) return launch_glds_t<2, false, true>(p, M, splits, part, st);
-    }
     constexpr int W = kGlds[C].wn * kGlds[C].tn * 32 >= 128 ? 9 : (kGlds[C].stages == 2 ? 13 : 12);
     if (p.flags & MTTS_GEMM_F_A_BF16) {
         if constexpr (kGlds[W].bf16a) return launch_glds_t<W, true, true>(p, M, splits, part, st);

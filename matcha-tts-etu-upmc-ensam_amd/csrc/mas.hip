@@ -371,8 +371,13 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
             dp[i] = neg;
             R[i] = 0u;
         }
-        constexpr int MD = PM ? 1 : 2;
-        float vbuf[2][KL][C], mbuf[MD][KL][C];
+        // a 3-slot ring of sub-chunks, two in flight ahead of the one being processed: at one to eight waves
+        // per CU nothing else hides the lattice stream's latency (one slot ahead measured no faster than the
+        // one-wave kernel)
+        // (two slots with a separate mask stream: three would spill at 8 rows per lane)
+        constexpr int RING = PM ? 3 : 2;
+        constexpr int MD = PM ? 1 : RING;
+        float vbuf[RING][KL][C], mbuf[MD][KL][C];
         auto load_sub = [&](auto slot, int y0) {
             constexpr int sl = decltype(slot)::value;
 #pragma unroll
@@ -385,16 +390,16 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
         const int nchunks = (t_y + CC - 1) / CC;
         const float *ein = edge + (wave > 0 ? wave - 1 : 0) * CC;  // the previous wave's ring row
         float *eout = edge + wave * CC;
-        // one chunk: KL sub-chunks of C columns from the ring slots (P * KL + s) & 1, the next sub-chunk's
-        // loads issued before each one is processed
-        auto chunk = [&](auto parity, int c) {
-            constexpr int P = decltype(parity)::value;
+        // one chunk: KL sub-chunks of C columns from the ring slots (P * KL + s) % RING (P = c % RING), the loads
+        // of the sub-chunk RING - 1 ahead issued before each one is processed
+        auto chunk = [&](auto phase3, int c) {
+            constexpr int P = decltype(phase3)::value;
             const int r3 = c % 3, p3 = (c + 2) % 3;
             static_for<0, KL>([&](auto sv) {
                 constexpr int s = decltype(sv)::value;
-                constexpr int sl = (P * KL + s) & 1;
+                constexpr int sl = (P * KL + s) % RING;
                 const int y0 = c * CC + s * C;
-                load_sub(std::integral_constant<int, sl ^ 1>{}, y0 + C);
+                load_sub(std::integral_constant<int, (sl + RING - 1) % RING>{}, y0 + (RING - 1) * C);
                 // the lane-0 neighbours of this sub-chunk's columns: column y needs the previous wave's last
                 // row after column y - 1 (ring slot of chunk c, or of chunk c - 1 for the chunk's first column)
                 float nbl[C];
@@ -458,15 +463,19 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
                 R[i] = 0u;
             }
         };
-        load_sub(std::integral_constant<int, 0>{}, 0);
+        static_for<0, RING - 1>([&](auto sv) { load_sub(sv, decltype(sv)::value * C); });
         for (int i = 0; i < wave; ++i) mtts::lds_barrier();  // pipeline fill: wave w starts in phase w
-        for (int c = 0; c < nchunks; c += 2) {
-            chunk(std::integral_constant<int, 0>{}, c);
-            mtts::lds_barrier();
-            if (c + 1 < nchunks) {
-                chunk(std::integral_constant<int, 1>{}, c + 1);
-                mtts::lds_barrier();
-            }
+        for (int c = 0; c < nchunks; c += RING) {
+            bool go = true;
+            static_for<0, RING>([&](auto pv) {
+                constexpr int P = decltype(pv)::value;
+                if (go && c + P < nchunks) {
+                    chunk(pv, c + P);
+                    mtts::lds_barrier();
+                } else {
+                    go = false;
+                }
+            });
         }
         for (int i = wave; i < W - 1; ++i) mtts::lds_barrier();  // drain: every wave runs nchunks + W - 1 phases
     }
@@ -789,7 +798,11 @@ WsLayout ws_layout(int B, int Tx, int Ty) {
     w.KL = 1;
     w.K = Tx <= 64 ? 1 : Tx <= 128 ? 2 : Tx <= 256 ? 4 : Tx <= 512 ? 8 : Tx <= 1024 ? 16 : 32;
     w.Txp = kWave * w.K;
-    if (Tx > 64 && mw_enabled()) {
+    // the multi-wave DP where it measured faster (tools/mas_bench.py, profiles/r04/sweeps/mas_*.jsonl: 8 x 512 x 4096
+    // 0.93 vs 0.99 ms) or where the one-wave one cannot go (Tx > 2048); at Tx <= 256 the one-wave kernel is faster
+    // (120 x 600: 65 vs 72 us; 256 x 2048: 280 vs 319 us) -- the per-column dependency chain, not the rows per
+    // lane, bounds both
+    if (Tx > 256 && mw_enabled()) {
         w.W = Tx <= 128 ? 2 : Tx <= 256 ? 4 : 8;
         w.KL = Tx <= 512 ? 1 : Tx <= 1024 ? 2 : Tx <= 2048 ? 4 : 8;
         w.K = w.W * w.KL;

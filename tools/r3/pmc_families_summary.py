@@ -31,11 +31,13 @@ for fam, rx in REGEX.items():
     write_b = 1024 * tot["WRITE_SIZE"][0] / n
     algo_b = algo[fam]["algorithmic_bytes"] / n
     out = {"family": fam, "kernels_regex": rx,
-           "workload": "tools/r3/pmc_families.py: two eager bf16 fwd+bwd passes of the bench batch (B=32, 120x600)",
+           "workload": f"tools/r3/pmc_families.py: two eager {algo.get('precision', 'bf16-mixed')} fwd+bwd passes of "
+                       "the bench batch (B=32, 120x600)",
            "launches": n, "dispatches": tot["FETCH_SIZE"][1], "warmup_dispatches_dropped": True, "fetch_bytes_per_launch": round(fetch_b),
            "write_bytes_per_launch": round(write_b), "traffic_bytes_per_launch": round(fetch_b + write_b),
            "algorithmic_bytes_per_launch": round(algo_b), "traffic_over_algorithmic": round((fetch_b + write_b) / algo_b, 3),
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes with --kernel-include-regex; "
                      "KB units; FETCH_SIZE x2 on gfx950"}
-    (dst / f"{fam}_traffic.json").write_text(json.dumps(out, indent=1))
+    suffix = "_parity" if algo.get("precision") == "bf16-parity" else ""
+    (dst / f"{fam}_traffic{suffix}.json").write_text(json.dumps(out, indent=1))
     print(json.dumps(out))
