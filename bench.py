@@ -442,8 +442,9 @@ def main():
         res = {}
         # (name, autocast, split weight planes, text encoder precision)
         modes = (("32-true", False, False, "bf16"), ("one_plane", True, False, "bf16"),
-                 ("split_weights", True, True, "bf16"), ("parity_policy", True, True, "fp32fwd"),
-                 ("parity_bf16x3_encoder", True, True, "bf16x3"), ("parity_fp32_encoder", True, True, "fp32"))
+                 ("split_weights", True, True, "bf16"), ("parity_policy", True, True, OPS.encoder_precision_for_parity()),
+                 ("parity_bf16x3_encoder", True, True, "bf16x3"), ("parity_bf16x6_encoder", True, True, "bf16x6"),
+                 ("parity_fp32fwd_encoder", True, True, "fp32fwd"), ("parity_fp32_encoder", True, True, "fp32"))
         with torch.no_grad():
             for name, amp_on, split, enc in modes:
                 old = OPS.set_weight_split(split)
@@ -465,16 +466,18 @@ def main():
             "bf16_loss_rel_err": errs(run_mode)["loss_rel_err"],
             "run_mode": run_mode,
             "modes": {k: errs(k) for k in ("one_plane", "split_weights", "parity_policy", "parity_bf16x3_encoder",
-                                           "parity_fp32_encoder")},
+                                           "parity_bf16x6_encoder", "parity_fp32fwd_encoder", "parity_fp32_encoder")},
             "losses": ["dur", "prior", "diff"],
             "bar": "alignment bit-exact (agreement 1.0), mel / flow-matching loss within 1e-4 relative (north star)",
             "note": "bf16 modes vs 32-true (= the oracle at this batch) with the parity tests' recipe weights and "
                     "batch, eval mode, same t / z.  one_plane: bf16 weights (the fp32 weights' rounding is the "
                     "error); split_weights: hi + rounding-residual bf16 planes; parity_policy (bench default, "
-                    "--precision bf16-parity): split weights + the text encoder's forward on the exact-fp32 MFMA "
-                    "(32-true's forward arithmetic; backward bf16); parity_bf16x3_encoder: the encoder forward in "
-                    "bf16x3 instead (split A and W operands, three bf16 MFMAs); parity_fp32_encoder: split weights "
-                    "+ the whole text encoder in exact fp32, backward too (round 3's policy)"}
+                    "--precision bf16-parity): split weights + the text encoder's forward fp32-faithful (policy: "
+                    "see config.text_encoder_forward; backward bf16); parity_bf16x3_encoder: the encoder forward in "
+                    "bf16x3 (split A and W operands, three bf16 MFMAs); parity_bf16x6_encoder: in bf16x6 (three exact "
+                    "planes per operand, six MFMAs); parity_fp32fwd_encoder: on the exact-fp32 MFMA (32-true's "
+                    "forward arithmetic); parity_fp32_encoder: split weights + the whole text encoder in exact fp32, "
+                    "backward too (round 3's policy)"}
 
     # same-run extra lines (N=1): the reference precision (32-true: exact fp32 MFMA) on the bench workload,
     # and the reference's own step shape -- 2 micro-batches of 16 with gradient accumulation
@@ -488,6 +491,9 @@ def main():
             lines.append(("bf16_one_plane", "bf16-mixed", B, 1, None) if args.precision == "bf16-parity" else
                          ("bf16_parity", "bf16-parity", B, 1, None))
             lines.append(("bf16_parity_fp32_encoder", "bf16-parity", B, 1, "fp32"))
+            if args.precision == "bf16-parity":  # the other fp32-faithful encoder forward: bf16x6 (three planes)
+                lines.append(("bf16_parity_alt_encoder", "bf16-parity", B, 1,
+                              "fp32fwd" if OPS.encoder_precision_for_parity() == "bf16x6" else "bf16x6"))
         # the data-parallel step's own cost on one GPU: a world-size-1 RCCL group, the bucketed in-graph
         # all-reduces (copies at one rank), the per-bucket side-stream weight-gradient flushes and packing
         lines.append(("dp_forced_n1", args.precision, B, 1, None))
@@ -514,7 +520,8 @@ def main():
             extra[name] = {"ms_per_step": round(ms2, 3), "utterances_per_s": round(micro * acc / ms2 * 1e3, 2),
                            "steps": n2, "precision": prec, "micro_batch": micro, "accumulate_grad_batches": acc,
                            "weight_planes": 2 if prec == "bf16-parity" else 1,
-                           "encoder": enc or ("fp32fwd" if prec == "bf16-parity" else "as the precision"),
+                           "encoder": enc or (OPS.encoder_precision_for_parity() if prec == "bf16-parity"
+                                              else "as the precision"),
                            **({"dp": {"ranks": int(tr2.reducer.comm.ranks), "buckets": len(tr2.reducer.buckets),
                                       "overlapped_in_graph": bool(next(iter(tr2._graphs.values()))["overlap"])}}
                               if tr2.reducer is not None else {}),
@@ -622,7 +629,8 @@ def main():
                        "precision": args.precision, "hip_graph": graph,
                        "weight_planes": 2 if (args.precision == "bf16-parity" or
                                               (OPS.weight_split_enabled() and args.precision == "bf16-mixed")) else 1,
-                       **({"text_encoder_forward": "exact fp32 MFMA (backward bf16)"} if args.precision == "bf16-parity" else {}),
+                       **({"text_encoder_forward": OPS.encoder_precision_for_parity() + " (backward bf16)"}
+                          if args.precision == "bf16-parity" else {}),
                        **({"bucketed_batches": [[int(v) for v in (b["x"].shape[1], b["y"].shape[2],
                                                                      b["x_lengths"].min(), b["y_lengths"].min())]
                                                 for b in batches],

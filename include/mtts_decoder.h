@@ -99,6 +99,12 @@ typedef struct mtts_conv_gemm_args {
                                         (register-staged schedules; the text encoder's forward in the parity
                                         policy) */
 
+#define MTTS_GEMM_F_SPLIT3 0x100     /* bf16 precision, fp32 A, LDS-DMA schedules (round 4): W holds THREE bf16 planes
+                                        hi / mid / lo at W, W + N*Kp, W + 2*N*Kp (hi + mid + lo = w exactly; mtts_pack_job
+                                        with MTTS_PACK_THREE_PLANES), A is split the same way in the kernel and every
+                                        product is the six terms of combined order <= 2^-16 (bf16x6): fp32-faithful
+                                        results at bf16 MFMA rates (the parity policy's text encoder forward) */
+
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
 /* Same, with an explicit schedule: 0..17 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;
  * 8..17 bf16-only: 64-wide K steps, two K steps in flight), MTTS_GEMM_GLDS + i = the bf16 LDS-DMA schedules
@@ -248,8 +254,11 @@ typedef struct mtts_pack_job {
     int64_t sr, sc, sj;
     int32_t j0, js;
     int64_t lo_off; /* bf16 only: > 0 also writes lo = bf16(w - bf16(w)) at dst + lo_off (elements): the
-                       second plane of an MTTS_GEMM_F_W_SPLIT operand; 0 = hi plane only */
+                       second plane of an MTTS_GEMM_F_W_SPLIT operand; 0 = hi plane only.  With
+                       MTTS_PACK_THREE_PLANES or'ed in: mid = bf16(w - hi) at dst + off and lo = bf16(w - hi - mid)
+                       at dst + 2 * off (off = lo_off without the flag): an MTTS_GEMM_F_SPLIT3 operand */
 } mtts_pack_job;
+#define MTTS_PACK_THREE_PLANES (1ll << 62)
 
 int mtts_pack_weights(const mtts_pack_job *jobs, int32_t njobs, int32_t precision, void *hip_stream);
 

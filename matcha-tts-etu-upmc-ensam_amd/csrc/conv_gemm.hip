@@ -1134,6 +1134,13 @@ static int pick_splits_f32(const mtts_conv_gemm_args &p, int M, int cfg, int spl
 
 static int pick_splits(const mtts_conv_gemm_args &p, int M, int cfg, int splits, bool bf16) {
     if (!bf16) return pick_splits_f32(p, M, cfg, splits);
+    if (p.flags & MTTS_GEMM_F_SPLIT3) {  // bf16x6 on 64 x 64 LDS-DMA tiles: split K below one round of tiles
+        if (cfg < MTTS_GEMM_GLDS || p.N % 4) return 1;
+        if (splits > 0) return splits;
+        const int tiles = ((M + 63) / 64) * ((p.N + 63) / 64), nk = (p.K + 63) / 64;
+        if (tiles >= 256 || nk < 10) return 1;
+        return nk >= 24 ? 4 : 2;
+    }
     if (cfg < MTTS_GEMM_GLDS || p.N % 4) return 1;
     if (splits > 0) return splits;
     const int nk = (p.K + 63) / 64;
@@ -1192,6 +1199,14 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     const bool bf16 = precision == MTTS_PREC_BF16;
     if (glds_id && (!bf16 || !mtts::conv_gemm_glds_applies(p)))
         return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: LDS-DMA schedule needs bf16, cin >= 64 and a 0/1 a_scale");
+    if (p.flags & MTTS_GEMM_F_SPLIT3) {  // bf16x6: LDS-DMA 64 x 64 (fp32 A split in the kernel)
+        if (!bf16 || (p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_GEMM_F_W_SPLIT | MTTS_GEMM_F_A_SPLIT)))
+            return mtts::fail(MTTS_ERR_INVALID_ARG, "conv_gemm: three weight planes need bf16 precision and an fp32 A");
+        if (!mtts::conv_gemm_glds_applies(p))
+            return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: three weight planes need the LDS-DMA schedules (cin >= 64)");
+        if (cfg < 0) cfg = MTTS_GEMM_GLDS + 12;
+        if (cfg < MTTS_GEMM_GLDS) return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: three weight planes need an LDS-DMA schedule");
+    }
     static const bool ws_pick = [] { const char *e = getenv("MTTS_GEMM_WS_PICK"); return !(e && e[0] == '0'); }();
     if (cfg < 0 && bf16 && ws_pick && (p.flags & MTTS_GEMM_F_W_SPLIT) && !(p.flags & MTTS_GEMM_F_A_SPLIT))
         cfg = pick_cfg_ws(p, M);

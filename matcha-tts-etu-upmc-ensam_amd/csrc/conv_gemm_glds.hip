@@ -52,12 +52,12 @@ using mtts::u32x4;
 using mtts::wait_vmcnt;
 constexpr uint32_t MTTS_GLDS_OOB = mtts::kDmaOob;
 
-template <int WM, int WN, int TM, int TN, int STAGES, bool ABF16 = false, bool WS = false>
+template <int WM, int WN, int TM, int TN, int STAGES, bool ABF16 = false, int NPL = 1>
 struct GldsGeom {
     static constexpr int NT = 64 * WM * WN;
     static constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN;
     static constexpr int A_BYTES = BM * kBK * (ABF16 ? 2 : 4);  // fp32 rows of 256 B / bf16 rows of 128 B
-    static constexpr int W_BYTES = (WS ? 2 : 1) * BN * kBK * 2;  // bf16 rows of 128 B (WS: hi rows, then lo rows)
+    static constexpr int W_BYTES = NPL * BN * kBK * 2;  // bf16 rows of 128 B (NPL weight planes: BN rows each)
     static constexpr int GA = A_BYTES / (NT * 16);  // DMA instructions per thread per K step
     static constexpr int GW = W_BYTES / (NT * 16);
     static_assert(A_BYTES % (NT * 16) == 0 && W_BYTES % (NT * 16) == 0, "tile / threads mismatch");
@@ -71,9 +71,16 @@ struct GldsGeom {
 // on pointer and tap bookkeeping (~26 VALU per MFMA on the 19200 x 256 x 768 conv, SQ counters).
 // WS (MTTS_GEMM_F_W_SPLIT): the W image holds BN hi rows then BN lo rows (the lo plane starts N*Kp
 // elements after W); each fragment pair issues A*hi and A*lo.
-template <int WM, int WN, int TM, int TN, int STAGES, bool ABF16, bool LEAN, bool WS = false>
+// X3 (MTTS_GEMM_F_SPLIT3, fp32 A, round 4): bf16x6 -- W holds three planes hi / mid / lo (hi + mid + lo = w
+// exactly, packed by mtts_pack_weights), the fp32 A fragment is split the same way at the fragment read, and
+// every product is the six terms of combined order <= 2^-16 (hi*hi, hi*mid, mid*hi, hi*lo, lo*hi, mid*mid),
+// smallest first, into the fp32 accumulator: ~2^-24 relative per product, fp32-faithful (the parity policy's
+// text encoder forward at bf16 MFMA rates)
+template <int WM, int WN, int TM, int TN, int STAGES, bool ABF16, bool LEAN, bool WS = false, bool X3 = false>
 __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_gemm_args p, int ksteps, float *part) {
-    using G = GldsGeom<WM, WN, TM, TN, STAGES, ABF16, WS>;
+    static_assert(!X3 || (!ABF16 && !WS), "bf16x6: fp32 A, three weight planes");
+    constexpr int NPL = X3 ? 3 : (WS ? 2 : 1);
+    using G = GldsGeom<WM, WN, TM, TN, STAGES, ABF16, NPL>;
     constexpr int ES = ABF16 ? 2 : 4;        // bytes per A element
     constexpr int RPI = ABF16 ? 8 : 4;       // A rows per 1 KiB DMA instruction
     constexpr int CPR = ABF16 ? 8 : 16;      // 16-byte chunks per A row of one K step
@@ -172,11 +179,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
     const uint16_t *w_ptr[GW];
     int w_k[GW];
     bool w_nok[GW];
-    const size_t w_plane = (size_t)p.N * p.Kp;  // WS: elements from the hi plane to the lo plane
+    const size_t w_plane = (size_t)p.N * p.Kp;  // WS / X3: elements from one weight plane to the next
 #pragma unroll
     for (int i = 0; i < GW; ++i) {
         const int ni = 8 * (i * NW + wave) + (lane >> 3);  // row of the W image
-        const int pl = (WS && ni >= BN) ? 1 : 0;
+        const int pl = NPL > 1 ? ni / BN : 0;
         const int n = ni - pl * BN;
         const int lc = (lane & 7) ^ ((ni >> 1) & 7);  // BN % 16 == 0: the lo rows swizzle like the hi rows
         w_nok[i] = n0 + n < p.N;
@@ -200,7 +207,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
         l_soa = __builtin_amdgcn_readfirstlane((uint32_t)(ch0 * ES));
         l_sow = __builtin_amdgcn_readfirstlane((uint32_t)(k0 * 2));
         l_rsa = make_rsrc(p.A, (uint32_t)((long long)p.nb * p.Ti * p.lda * ES));
-        l_rsw = make_rsrc(p.W, (uint32_t)((WS ? 2ll : 1ll) * p.N * p.Kp * 2));
+        l_rsw = make_rsrc(p.W, (uint32_t)((long long)NPL * p.N * p.Kp * 2));
 #pragma unroll
         for (int i = 0; i < GA; ++i) {
             const int r = RPI * (i * NW + wave) + lane / CPR;
@@ -213,7 +220,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
 #pragma unroll
         for (int i = 0; i < GW; ++i) {
             const int ni = 8 * (i * NW + wave) + (lane >> 3);
-            const int pl = (WS && ni >= BN) ? 1 : 0;
+            const int pl = NPL > 1 ? ni / BN : 0;
             const int n = ni - pl * BN;
             const int lc = (lane & 7) ^ ((ni >> 1) & 7);
             l_vw[i] = w_nok[i] ? (uint32_t)((pl * w_plane + (size_t)(n0 + n) * p.Kp + lc * 8) * 2) : MTTS_GLDS_OOB;
@@ -277,6 +284,55 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
     auto compute = [&](auto S) {
         const unsigned char *abase = abuf(S);
         const unsigned char *wbase = wbuf(S);
+        if constexpr (X3) {
+#pragma unroll
+            for (int ks = 0; ks < kBK / 16; ++ks) {
+                bf16x8 ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int r = wr * 32 * TM + i * 32 + lr;
+                    const int c = 4 * ks + 2 * lh;
+                    const float4 x0 = *reinterpret_cast<const float4 *>(abase + r * 256 + ((c ^ (r & 15)) << 4));
+                    const float4 x1 = *reinterpret_cast<const float4 *>(abase + r * 256 + (((c + 1) ^ (r & 15)) << 4));
+                    float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+                    uint32_t wh[4], wm[4], wl[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {  // every residual is exact in fp32
+                        wh[q] = pack2(v[2 * q], v[2 * q + 1]);
+                        v[2 * q] -= __uint_as_float(wh[q] << 16);
+                        v[2 * q + 1] -= __uint_as_float(wh[q] & 0xffff0000u);
+                        wm[q] = pack2(v[2 * q], v[2 * q + 1]);
+                        v[2 * q] -= __uint_as_float(wm[q] << 16);
+                        v[2 * q + 1] -= __uint_as_float(wm[q] & 0xffff0000u);
+                        wl[q] = pack2(v[2 * q], v[2 * q + 1]);
+                    }
+                    ah[i] = __builtin_bit_cast(bf16x8, make_uint4(wh[0], wh[1], wh[2], wh[3]));
+                    am[i] = __builtin_bit_cast(bf16x8, make_uint4(wm[0], wm[1], wm[2], wm[3]));
+                    al[i] = __builtin_bit_cast(bf16x8, make_uint4(wl[0], wl[1], wl[2], wl[3]));
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = wc * 32 * TN + j * 32 + lr;
+                    const int c = 2 * ks + lh;
+                    const int sw = (c ^ ((n >> 1) & 7)) << 4;  // BN % 16 == 0: every plane swizzles alike
+                    bh[j] = *reinterpret_cast<const bf16x8 *>(wbase + n * 128 + sw);
+                    bm[j] = *reinterpret_cast<const bf16x8 *>(wbase + (n + BN) * 128 + sw);
+                    bl[j] = *reinterpret_cast<const bf16x8 *>(wbase + (n + 2 * BN) * 128 + sw);
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    }
+            }
+            return;
+        }
 #pragma unroll
         for (int ks = 0; ks < kBK / 16; ++ks) {
             bf16x8 af[TM], bfr[TN];
@@ -427,13 +483,13 @@ bool conv_gemm_glds_lean(const mtts_conv_gemm_args &p) {
 
 namespace {
 
-template <int C, bool ABF16, bool WS = false>
+template <int C, bool ABF16, bool WS = false, bool X3 = false>
 int launch_glds_t(const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
     constexpr GldsCfg c = kGlds[C];
-    using G = GldsGeom<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16, WS>;
-    static_assert(!WS || 2 * c.stages * (G::A_BYTES + G::W_BYTES) / 2 <= 160 * 1024, "split-weight stages fit LDS");
-    auto kern = mtts::conv_gemm_glds_lean(p) ? conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16, true, WS>
-                                : conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16, false, WS>;
+    using G = GldsGeom<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16, X3 ? 3 : (WS ? 2 : 1)>;
+    static_assert((!WS && !X3) || c.stages * (G::A_BYTES + G::W_BYTES) <= 160 * 1024, "split-weight stages fit LDS");
+    auto kern = mtts::conv_gemm_glds_lean(p) ? conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16, true, WS, X3>
+                                : conv_gemm_glds_kernel<c.wm, c.wn, c.tm, c.tn, c.stages, ABF16, false, WS, X3>;
     const int nk = (p.K + kBK - 1) / kBK;
     const int ksteps = (nk + splits - 1) / splits;
     const int S = splits > 1 ? (nk + ksteps - 1) / ksteps : 1;  // every split non-empty
@@ -461,9 +517,17 @@ int launch_glds_ws(const mtts_conv_gemm_args &p, int M, int splits, float *part,
     return launch_glds_t<W, false, true>(p, M, splits, part, st);
 }
 
+// bf16x6 (MTTS_GEMM_F_SPLIT3, fp32 A): 64 x 64 tiles, three stages (44: 120 KiB) or two (45)
+template <int C>
+int launch_glds_x3(const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
+    if constexpr (kGlds[C].stages >= 3) return launch_glds_t<12, false, false, true>(p, M, splits, part, st);
+    else return launch_glds_t<13, false, false, true>(p, M, splits, part, st);
+}
+
 // A schedule without an instantiation for the operand's storage runs the 64 x 256 two-stage one (41)
 template <int C>
 int launch_glds(const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
+    if (p.flags & MTTS_GEMM_F_SPLIT3) return launch_glds_x3<C>(p, M, splits, part, st);
     if (p.flags & MTTS_GEMM_F_W_SPLIT) return launch_glds_ws<C>(p, M, splits, part, st);
     if (p.flags & MTTS_GEMM_F_A_BF16) {
         if constexpr (kGlds[C].bf16a) return launch_glds_t<C, true>(p, M, splits, part, st);

@@ -7,7 +7,8 @@
 //     dst[r*ld + j*C + c] = src[r*sr + c*sc + (j0 + j*js)*sj],   zero for k' in [C*ntaps, Kp),
 // and a launch runs up to kJobsPerLaunch jobs (blockIdx.y = job), each thread producing 8
 // consecutive k' (one 16-byte bf16 store, or two float4).  bf16 jobs with lo_off > 0 also write the
-// rounding residual bf16(w - bf16(w)) as a second plane (MTTS_GEMM_F_W_SPLIT operands).
+// rounding residual bf16(w - bf16(w)) as a second plane (MTTS_GEMM_F_W_SPLIT operands), and with
+// MTTS_PACK_THREE_PLANES a third, bf16(w - hi - mid): hi + mid + lo == w exactly (MTTS_GEMM_F_SPLIT3).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -54,18 +55,25 @@ __global__ __launch_bounds__(kThreads) void pack_kernel(JobBatch jb) {
             }
         }
         if constexpr (BF16) {
-            uint32_t w[4], l[4];
+            const bool three = (j.lo_off & MTTS_PACK_THREE_PLANES) != 0;
+            const int64_t off = j.lo_off & ~MTTS_PACK_THREE_PLANES;
+            uint32_t w[4], l[4], l2[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const __bf16 h0 = (__bf16)e[2 * i], h1 = (__bf16)e[2 * i + 1];
                 w[i] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
                 // split plane: the rounding residual, exact in fp32 (e - hi has <= 16 significant bits)
-                const __bf16 l0 = (__bf16)(e[2 * i] - (float)h0), l1 = (__bf16)(e[2 * i + 1] - (float)h1);
+                const float r0 = e[2 * i] - (float)h0, r1 = e[2 * i + 1] - (float)h1;
+                const __bf16 l0 = (__bf16)r0, l1 = (__bf16)r1;
                 l[i] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+                // third plane (bf16x6): what the mid plane leaves, <= 8 significant bits -- exact in bf16
+                const __bf16 m0 = (__bf16)(r0 - (float)l0), m1 = (__bf16)(r1 - (float)l1);
+                l2[i] = (uint32_t)__builtin_bit_cast(uint16_t, m0) | ((uint32_t)__builtin_bit_cast(uint16_t, m1) << 16);
             }
             uint16_t *d = static_cast<uint16_t *>(j.dst) + (size_t)r * j.ld + k0;
             *reinterpret_cast<uint4 *>(d) = make_uint4(w[0], w[1], w[2], w[3]);
-            if (j.lo_off > 0) *reinterpret_cast<uint4 *>(d + j.lo_off) = make_uint4(l[0], l[1], l[2], l[3]);
+            if (off > 0) *reinterpret_cast<uint4 *>(d + off) = make_uint4(l[0], l[1], l[2], l[3]);
+            if (three) *reinterpret_cast<uint4 *>(d + 2 * off) = make_uint4(l2[0], l2[1], l2[2], l2[3]);
         } else {
             float4 *d = reinterpret_cast<float4 *>(static_cast<float *>(j.dst) + (size_t)r * j.ld + k0);
             d[0] = make_float4(e[0], e[1], e[2], e[3]);
@@ -144,6 +152,9 @@ extern "C" int mtts_pack_weights(const mtts_pack_job *jobs, int32_t njobs, int32
         MTTS_CHECK_ARG((reinterpret_cast<uintptr_t>(j.dst) & 15) == 0, "pack_weights: dst must be 16-byte aligned");
         MTTS_CHECK_ARG(j.lo_off >= 0 && j.lo_off % 8 == 0 && (j.lo_off == 0 || precision == MTTS_PREC_BF16),
                        "pack_weights: lo_off (the split plane) needs bf16 and a multiple of 8");
+        MTTS_CHECK_ARG(!(j.lo_off & MTTS_PACK_THREE_PLANES) ||
+                           ((j.lo_off & ~MTTS_PACK_THREE_PLANES) > 0 && !tiled_job(j)),
+                       "pack_weights: three planes need a plane offset and a non-transposing (forward) layout");
         const long g = (long)j.rows * (j.Kp / 8);
         max_groups = g > max_groups ? g : max_groups;
     }

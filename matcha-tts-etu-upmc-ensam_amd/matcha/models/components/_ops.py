@@ -76,10 +76,11 @@ _PRECISE: contextvars.ContextVar = contextvars.ContextVar("mtts_precise_fwd", de
 
 @contextlib.contextmanager
 def precise_forward(on: bool | str = True):
-    """on: True / "bf16x3" (split bf16 operands, three MFMAs per product) or "fp32" (the forward GEMMs on
-    the exact-fp32 MFMA with fp32 packed weights -- the 32-true arithmetic, so the forward's outputs are
-    those of 32-true; round 4: bf16x3 left one alignment near-tie of the B=4 reference fixture flipped);
-    False: off.  The backward of the same ops stays bf16 one-plane either way."""
+    """on: True / "bf16x3" (split bf16 operands, three MFMAs per product), "bf16x6" (three exact planes per
+    operand, six MFMAs per product: fp32-faithful, MTTS_GEMM_F_SPLIT3) or "fp32" (the forward GEMMs on the
+    exact-fp32 MFMA with fp32 packed weights -- the 32-true arithmetic, so the forward's outputs are those of
+    32-true; round 4: bf16x3 left one alignment near-tie of the B=4 reference fixture flipped); False: off.
+    The backward of the same ops stays bf16 one-plane either way."""
     tok = _PRECISE.set(("bf16x3" if on is True else on) if on else False)
     try:
         yield
@@ -111,13 +112,22 @@ def weight_split_enabled() -> bool:
     return _W_SPLIT if v is None else v
 
 
+# the parity policy's text-encoder forward: "fp32fwd" (exact-fp32 MFMA: 32-true's arithmetic) or "bf16x6"
+# (three exact bf16 planes per operand, six MFMAs: fp32-faithful at bf16 MFMA rates); MTTS_PARITY_ENCODER selects
+_PARITY_ENC = os.environ.get("MTTS_PARITY_ENCODER", "fp32fwd")
+
+
+def encoder_precision_for_parity() -> str:
+    return _PARITY_ENC
+
+
 @contextlib.contextmanager
 def parity_policy(on: bool = True):
     """bf16-parity inside a bf16 autocast region (the Trainer's "bf16-parity" precision): split weight
     planes for every forward GEMM and the text encoder's forward on the exact-fp32 MFMA
     (precise_forward("fp32"); its backward stays bf16)."""
     t1 = _WSPLIT_CV.set(True if on else None)
-    t2 = _ENC_PREC.set("fp32fwd" if on else "bf16")
+    t2 = _ENC_PREC.set(_PARITY_ENC if on else "bf16")
     try:
         yield
     finally:
@@ -128,6 +138,9 @@ def parity_policy(on: bool = True):
 def encoder_precision_default() -> str:
     return _ENC_PREC.get()
 PACK_BF16_SPLIT = 2  # pack-cache kind: the bf16 hi + lo planes of a forward operand
+PACK_BF16_SPLIT3 = 3  # pack-cache kind: hi + mid + lo bf16 planes (== w exactly) of a bf16x6 forward operand
+GEMM_F_SPLIT3 = 0x100  # MTTS_GEMM_F_SPLIT3: three weight planes, fp32 A split in the kernel (bf16x6)
+PACK_THREE_PLANES = 1 << 62  # MTTS_PACK_THREE_PLANES (mtts_pack_job.lo_off flag)
 
 GEMM_GLDS = 32  # MTTS_GEMM_GLDS: first LDS-DMA schedule id
 
@@ -345,12 +358,14 @@ def spec_convT_dgrad(w):
 
 
 def _run_pack(specs, prec, stream=None):
-    """prec: PREC_FP32, PREC_BF16, or PACK_BF16_SPLIT ([2 * rows, Kp]: the hi plane, then the lo plane).
+    """prec: PREC_FP32, PREC_BF16, PACK_BF16_SPLIT ([2 * rows, Kp]: the hi plane, then the lo plane) or
+    PACK_BF16_SPLIT3 ([3 * rows, Kp]: hi, mid, lo).
     stream: launch there instead of the current stream (outputs are allocated on the current one)."""
     dev = specs[0].jobs[0][0].device
-    split = prec == PACK_BF16_SPLIT
-    dt = torch.bfloat16 if prec in (PREC_BF16, PACK_BF16_SPLIT) else torch.float32
-    outs = [torch.empty((2 if split else 1) * sp.rows, sp.Kp, device=dev, dtype=dt) for sp in specs]
+    split3 = prec == PACK_BF16_SPLIT3
+    split = prec == PACK_BF16_SPLIT or split3
+    dt = torch.bfloat16 if prec in (PREC_BF16, PACK_BF16_SPLIT, PACK_BF16_SPLIT3) else torch.float32
+    outs = [torch.empty((3 if split3 else 2 if split else 1) * sp.rows, sp.Kp, device=dev, dtype=dt) for sp in specs]
     njobs = sum(len(sp.jobs) for sp in specs)
     arr = (PackJob * njobs)()
     i = 0
@@ -364,11 +379,14 @@ def _run_pack(specs, prec, stream=None):
             j.src, j.dst = src.data_ptr(), out.data_ptr() + (r0 * sp.Kp + c0) * es
             j.rows, j.C, j.ntaps, j.Kp, j.ld = rows, C, nt, kpj, sp.Kp
             j.sr, j.sc, j.sj, j.j0, j.js = sr, sc, sj, j0, js
-            j.lo_off = sp.rows * sp.Kp if split else 0
+            j.lo_off = (sp.rows * sp.Kp if split else 0) | (PACK_THREE_PLANES if split3 else 0)
             i += 1
     st = stream if stream is not None else torch.cuda.current_stream(dev)
     N.check(N.lib().mtts_pack_weights(arr, njobs, PREC_BF16 if split else prec, st.cuda_stream), "mtts_pack_weights")
-    if split:
+    if split3:
+        for o in outs:
+            o._mtts_w_split3 = True  # _gemm sets MTTS_GEMM_F_SPLIT3 for it
+    elif split:
         for o in outs:
             o._mtts_w_split = True  # _gemm sets MTTS_GEMM_F_W_SPLIT for it
     return outs
@@ -380,6 +398,8 @@ def _pack_kind(spec: PackSpec, prec: int) -> int:
     if prec == PREC_BF16 and not spec.dgrad:
         if _fwd_fp32():
             return PREC_FP32
+        if _PRECISE.get() == "bf16x6":
+            return PACK_BF16_SPLIT3
         if weight_split_enabled() or _PRECISE.get():
             return PACK_BF16_SPLIT
     return prec
@@ -420,7 +440,7 @@ def _pack_plan_now(plan, prec, stream=None):
     """Every layout in `plan` for this precision (the backward's transposed ones too when grad is
     enabled), a few launches per kind -> {key: packed}."""
     grad = torch.is_grad_enabled()
-    kinds = (prec, PACK_BF16_SPLIT, PREC_FP32) if prec == PREC_BF16 else (prec,)
+    kinds = (prec, PACK_BF16_SPLIT, PACK_BF16_SPLIT3, PREC_FP32) if prec == PREC_BF16 else (prec,)
     cache = {}
     for kind in kinds:
         specs = [sp for key, sp in plan.items()
@@ -518,6 +538,12 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
         if A.dtype != torch.float32:
             A = A.float()
     w_split = getattr(Wp, "_mtts_w_split", False) and prec == PREC_BF16
+    split3 = getattr(Wp, "_mtts_w_split3", False) and prec == PREC_BF16
+    if split3:
+        if Wp.shape[0] != 3 * N_:
+            raise ValueError(f"three weight planes {tuple(Wp.shape)}: the planes must start at rows N={N_}, 2N")
+        if A.dtype != torch.float32:
+            A = A.float()
     # bf16x3 (precise_forward): the split weights' GEMM also splits its fp32 A operand -- register schedules
     a_split = w_split and _PRECISE.get() and A.dtype == torch.float32
     if a_split:
@@ -553,7 +579,8 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
                   | (GEMM_F_C_BF16 if C.dtype == torch.bfloat16 else 0)
                   | (GEMM_F_FAST_ACT if (prec == PREC_BF16 and _FAST_ACT) else 0)
                   | (GEMM_F_PRE_BF16 if any(t is not None and t.dtype == torch.bfloat16 for t in (C_pre, aux)) else 0)
-                  | (GEMM_F_W_SPLIT if w_split else 0) | (GEMM_F_A_SPLIT if a_split else 0))
+                  | (GEMM_F_W_SPLIT if w_split else 0) | (GEMM_F_A_SPLIT if a_split else 0)
+                  | (GEMM_F_SPLIT3 if split3 else 0))
     if C_pre is not None and aux is not None and C_pre.dtype != aux.dtype:
         raise ValueError("C_pre and aux must share a dtype")
     log = LAUNCH_LOG
@@ -569,7 +596,7 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
     if log is not None:
         e1.record(st)
         M_ = nb * To
-        nbytes = (nb * Ti * cin * A.element_size() + (2 if w_split else 1) * N_ * Kp * Wp.element_size()
+        nbytes = (nb * Ti * cin * A.element_size() + (3 if split3 else 2 if w_split else 1) * N_ * Kp * Wp.element_size()
                   + M_ * N_ * C.element_size())
         nbytes += sum(M_ * N_ * t.element_size() for t in (residual, aux, C_pre) if t is not None)
         log.append((e0, e1, 2.0 * M_ * N_ * args.K, prec, nbytes,

@@ -142,6 +142,8 @@ class MatchaTTS(BaseLightningClass):
             enc_ctx = O.precise_forward("bf16x3")
         elif enc_prec == "fp32fwd":
             enc_ctx = O.precise_forward("fp32")
+        elif enc_prec == "bf16x6":
+            enc_ctx = O.precise_forward("bf16x6")
         else:
             enc_ctx = _nullctx()
         with enc_ctx:

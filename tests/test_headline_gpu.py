@@ -43,8 +43,8 @@ BF16_ATTN_AGREE = 0.99      # one plane: fraction of [Tx, Ty] alignment cells eq
 # precision -> (bf16 autocast, split weight planes, MatchaTTS.encoder_precision)
 MODES = {"32-true": (False, False, "bf16"), "bf16-mixed": (True, False, "bf16"),
          "bf16-parity": (True, True, "fp32fwd"), "bf16-parity-fp32enc": (True, True, "fp32"),
-         "bf16-parity-bf16x3": (True, True, "bf16x3")}
-PARITY_MODES = ("bf16-parity", "bf16-parity-fp32enc")
+         "bf16-parity-bf16x3": (True, True, "bf16x3"), "bf16-parity-bf16x6": (True, True, "bf16x6")}
+PARITY_MODES = ("bf16-parity", "bf16-parity-fp32enc", "bf16-parity-bf16x6")
 
 
 def run_precision(model, precision, fn):

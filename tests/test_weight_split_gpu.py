@@ -175,3 +175,73 @@ def test_precise_forward_fp32_encoder_equals_32true():
     r = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
     assert r(outs["fp32fwd"][2], outs["32-true"][2]) < 3e-2  # bf16 backward
     assert r(outs["fp32fwd"][2], outs["bf16"][2]) < 3e-2
+
+
+def test_pack_three_planes_exact():
+    """MTTS_PACK_THREE_PLANES: hi = bf16(w), mid = bf16(w - hi), lo = bf16(w - hi - mid) and hi + mid + lo == w
+    EXACTLY (every residual is exact in fp32 and the last one has <= 8 significant bits)."""
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator().manual_seed(5)
+    w = torch.randn(96, 40, generator=g).to(DEV)
+    t = O._run_pack([O.spec_linear((w,))], O.PACK_BF16_SPLIT3)[0]
+    assert t.shape == (3 * 96, 40) and t._mtts_w_split3
+    hi, mid, lo = t[:96].float(), t[96:192].float(), t[192:].float()
+    assert torch.equal(hi, w.bfloat16().float())
+    assert torch.equal(mid, (w - hi).bfloat16().float())
+    assert torch.equal((hi + mid) + lo, w)
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout,k,splits", [(32, 120, 192, 192, 5, 0), (4, 120, 192, 576, 1, 0),
+                                                   (8, 120, 768, 192, 3, 0), (8, 120, 768, 192, 3, 1),
+                                                   (8, 120, 192, 768, 3, 0), (3, 37, 256, 80, 1, 0),
+                                                   (32, 120, 256, 1, 1, 0)])
+def test_bf16x6_vs_float64(B, T, Cin, Cout, k, splits):
+    """MTTS_GEMM_F_SPLIT3 (precise_forward("bf16x6")): fp32 activations and weights each as three exact bf16
+    planes, the six products of combined order <= 2^-16 -- an fp32-faithful GEMM: within 2e-7 of float64 (the
+    exact-fp32 MFMA kernel itself lands ~1e-7 away), far tighter than bf16x3.  The text encoder's shapes
+    (prenet k = 5, q|k|v, FFN k = 3 both ways with and without split-K, the mean and duration projections)."""
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator().manual_seed(B * Cout + k + 7)
+    x = torch.randn(B, T, Cin, generator=g).to(DEV)
+    w = (torch.randn(Cout, Cin, k, generator=g) / (Cin * k) ** 0.5).to(DEV)
+    b = torch.randn(Cout, generator=g).to(DEV)
+    m = (torch.arange(T)[None] < torch.randint(T // 2, T + 1, (B,), generator=g)[:, None]).float().to(DEV)
+    ref = torch.nn.functional.conv1d((x * m[..., None]).double().transpose(1, 2), w.double(), b.double(),
+                                     padding=k // 2).transpose(1, 2)
+    y = torch.empty(B, T, Cout, device=DEV)
+    with O.precise_forward("bf16x6"):
+        Wp, Kp = O.packed(O.spec_conv_fwd(w), O.PREC_BF16)
+        assert Wp._mtts_w_split3
+        O._gemm(x, T, T, B, 1, [j - k // 2 for j in range(k)], Cin, Wp, Kp, Cout, y, T, prec=O.PREC_BF16,
+                a_scale=m, bias=b, splits=splits)
+    Wf, Kf = O.packed(O.spec_conv_fwd(w), O.PREC_FP32)
+    y32 = torch.empty_like(y)
+    O._gemm(x, T, T, B, 1, [j - k // 2 for j in range(k)], Cin, Wf, Kf, Cout, y32, T, prec=O.PREC_FP32,
+            a_scale=m, bias=b)
+    assert _err(y, ref) < max(2e-7, 2 * _err(y32, ref)), (_err(y, ref), _err(y32, ref))
+
+
+def test_precise_forward_bf16x6_encoder_close_to_32true():
+    """The text encoder under precise_forward("bf16x6"): mu_x / logw within fp32 rounding of the 32-true
+    encoder's (relative 1e-6, vs ~1e-5 for bf16x3), the backward bf16."""
+    from golden.weights_recipe import apply_recipe
+    from matcha.models.components import _ops as O
+    from matcha.models.matcha_tts import MatchaTTS
+    from matcha.training import synthetic_batch
+
+    model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(DEV)
+    apply_recipe(model, 23)
+    model.eval()
+    bt = synthetic_batch(8, 120, 600, seed=6, device=DEV)
+    outs = {}
+    for mode in ("32-true", "bf16x6", "bf16x3"):
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode != "32-true"), \
+                (O.precise_forward(mode) if mode != "32-true" else contextlib.nullcontext()):
+            mu, logw, _ = model.encoder(bt["x"], bt["x_lengths"])
+        outs[mode] = (mu.float(), logw.float())
+    r = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
+    assert r(outs["bf16x6"][0], outs["32-true"][0]) < 1e-6, r(outs["bf16x6"][0], outs["32-true"][0])
+    assert r(outs["bf16x6"][1], outs["32-true"][1]) < 1e-6
+    assert r(outs["bf16x3"][0], outs["32-true"][0]) > 5 * r(outs["bf16x6"][0], outs["32-true"][0])
