@@ -415,41 +415,34 @@ int submit_param_sums(const float *pa, float *outa, const float *pb, float *outb
 }
 
 // ------------------------------------------------------------------------------ LayerNorm
-// one wave per row; lane handles float4 chunks lane*4 + 256*i
-template <bool Y16>  // Y16: y written as bf16 (MTTS_NORM_F_Y_BF16)
+// Each wave normalises R consecutive rows, all their loads (and the affine weights') issued before the
+// first reduction; lane handles float4 chunks lane*4 + 256*i, NI chunks (C <= 256 * NI).  One row per
+// wave kept ~1 KB in flight per wave -- well under what a CU needs to stream at its HBM share.
+template <bool Y16, int NI, int R>  // Y16: y written as bf16 (MTTS_NORM_F_Y_BF16)
 __global__ __launch_bounds__(kThreads) void layernorm_fwd_kernel(const float *__restrict__ x, const float *__restrict__ w,
                                                                  const float *__restrict__ bia, float *__restrict__ y,
                                                                  float *__restrict__ mean_out, float *__restrict__ rstd_out,
                                                                  int M, int C, float eps, int act, float p,
                                                                  const uint32_t *__restrict__ seed) {
-    const int row = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int row0 = (blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) * R;
     const int lane = threadIdx.x & 63;
-    if (row >= M) return;
-    const float *xr = x + (size_t)row * C;
-    float4 v[4];
-    float s = 0.f;
+    if (row0 >= M) return;
+    float4 v[R][NI], ww[NI], bb[NI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int c = lane * 4 + 256 * i;
-        v[i] = c < C ? *reinterpret_cast<const float4 *>(xr + c) : make_float4(0, 0, 0, 0);
-        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-    }
-    const float mean = wave_sum(s) / C;
-    float q = 0.f;
+    for (int q = 0; q < R; ++q) {
+        const float *xr = x + (size_t)(row0 + q) * C;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int c = lane * 4 + 256 * i;
-        if (c < C) {
-            const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, d = v[i].w - mean;
-            q += (a * a + b * b) + (cc * cc + d * d);
+        for (int i = 0; i < NI; ++i) {
+            const int c = lane * 4 + 256 * i;
+            v[q][i] = row0 + q < M && c < C ? *reinterpret_cast<const float4 *>(xr + c) : make_float4(0, 0, 0, 0);
         }
     }
-    const float rstd = rsqrtf(wave_sum(q) / C + eps);
-    if (lane == 0) {
-        mean_out[row] = mean;
-        rstd_out[row] = rstd;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int c = lane * 4 + 256 * i;
+        ww[i] = c < C ? *reinterpret_cast<const float4 *>(w + c) : make_float4(0, 0, 0, 0);
+        bb[i] = c < C ? *reinterpret_cast<const float4 *>(bia + c) : make_float4(0, 0, 0, 0);
     }
-    float *yr = y + (size_t)row * C;
     uint32_t sd0 = 0, sd1 = 0;  // dropout seed words
     if (p > 0.f) {
         sd0 = seed[0];
@@ -457,41 +450,69 @@ __global__ __launch_bounds__(kThreads) void layernorm_fwd_kernel(const float *__
     }
     const float inv_keep = 1.f / (1.f - p);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int c = lane * 4 + 256 * i;
-        if (c < C) {
-            const float4 ww = *reinterpret_cast<const float4 *>(w + c);
-            const float4 bb = *reinterpret_cast<const float4 *>(bia + c);
-            float o[4] = {(v[i].x - mean) * rstd * ww.x + bb.x, (v[i].y - mean) * rstd * ww.y + bb.y,
-                          (v[i].z - mean) * rstd * ww.z + bb.z, (v[i].w - mean) * rstd * ww.w + bb.w};
-            if (act == MTTS_ACT_RELU || p > 0.f) {  // fused tail: ReLU then dropout (ConvReluNorm order)
+    for (int q = 0; q < R; ++q) {
+        const int row = row0 + q;
+        if (row >= M) break;  // wave-uniform
+        float s = 0.f;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if (act == MTTS_ACT_RELU) o[j] = fmaxf(o[j], 0.f);
-                    if (p > 0.f) o[j] = mtts::dropout_keep(sd0, sd1, (uint32_t)row, (uint32_t)(c + j), p) ? o[j] * inv_keep : 0.f;
-                }
+        for (int i = 0; i < NI; ++i) s += (v[q][i].x + v[q][i].y) + (v[q][i].z + v[q][i].w);
+        const float mean = wave_sum(s) / C;
+        float sq = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int c = lane * 4 + 256 * i;
+            if (c < C) {
+                const float a = v[q][i].x - mean, b = v[q][i].y - mean, cc = v[q][i].z - mean, d = v[q][i].w - mean;
+                sq += (a * a + b * b) + (cc * cc + d * d);
             }
-            if constexpr (Y16) {
-                typedef float f2 __attribute__((ext_vector_type(2)));
-                typedef __bf16 h2 __attribute__((ext_vector_type(2)));
-                const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){o[0], o[1]}, h2));
-                const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){o[2], o[3]}, h2));
-                *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(y) + (size_t)row * C + c) = make_uint2(lo, hi);
-            } else {
-                *reinterpret_cast<float4 *>(yr + c) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+        const float rstd = rsqrtf(wave_sum(sq) / C + eps);
+        if (lane == 0) {
+            mean_out[row] = mean;
+            rstd_out[row] = rstd;
+        }
+        float *yr = y + (size_t)row * C;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int c = lane * 4 + 256 * i;
+            if (c < C) {
+                float o[4] = {(v[q][i].x - mean) * rstd * ww[i].x + bb[i].x, (v[q][i].y - mean) * rstd * ww[i].y + bb[i].y,
+                              (v[q][i].z - mean) * rstd * ww[i].z + bb[i].z, (v[q][i].w - mean) * rstd * ww[i].w + bb[i].w};
+                if (act == MTTS_ACT_RELU || p > 0.f) {  // fused tail: ReLU then dropout (ConvReluNorm order)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (act == MTTS_ACT_RELU) o[j] = fmaxf(o[j], 0.f);
+                        if (p > 0.f) o[j] = mtts::dropout_keep(sd0, sd1, (uint32_t)row, (uint32_t)(c + j), p) ? o[j] * inv_keep : 0.f;
+                    }
+                }
+                if constexpr (Y16) {
+                    typedef float f2 __attribute__((ext_vector_type(2)));
+                    typedef __bf16 h2 __attribute__((ext_vector_type(2)));
+                    const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){o[0], o[1]}, h2));
+                    const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){o[2], o[3]}, h2));
+                    *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(y) + (size_t)row * C + c) = make_uint2(lo, hi);
+                } else {
+                    *reinterpret_cast<float4 *>(yr + c) = make_float4(o[0], o[1], o[2], o[3]);
+                }
             }
         }
     }
 }
 
-// backward: rows per block, sized for ~512 blocks (4..128 rows, a multiple of the 4 waves): the
-// encoder's 3840-row LayerNorms would otherwise run on 30 blocks
-inline int ln_rows_per_block(int M) {
-    int r = (M + 511) / 512;
-    r = (r + 3) / 4 * 4;
-    return r < 4 ? 4 : (r > 128 ? 128 : r);
+// backward: each wave takes R consecutive rows at once (all their loads issued before the first
+// reduction), the block 4 * R rows per pass, rows_per_block a multiple of that sized for ~768 blocks
+// (at most 128 rows).  One row per wave at a time left the decoder's 19200-row LayerNorms (40 rows per
+// block, 10 dependent load -> reduce -> store rounds per wave) latency-bound at 12-22 us.
+// NI: float4 chunks per lane (1: C <= 256, 4: C <= 1024).
+inline int ln_bwd_rows_in_flight(int C) { return C <= 256 ? 4 : 1; }
+inline int ln_rows_per_block(int M, int C) {
+    const int q = 4 * ln_bwd_rows_in_flight(C);  // rows per block pass
+    int r = (M + 767) / 768;
+    r = (r + q - 1) / q * q;
+    return r < q ? q : (r > 128 ? 128 : r);
 }
 
+template <int NI, int R>
 __global__ __launch_bounds__(kThreads) void layernorm_bwd_kernel(const float *__restrict__ dy, const float *__restrict__ x,
                                                                  const float *__restrict__ w, const float *__restrict__ bia,
                                                                  const float *__restrict__ mean_in,
@@ -499,15 +520,13 @@ __global__ __launch_bounds__(kThreads) void layernorm_bwd_kernel(const float *__
                                                                  float *__restrict__ pw, float *__restrict__ pb, int M,
                                                                  int C, int act, float p, const uint32_t *__restrict__ seed,
                                                                  int rows_per_block, const float *__restrict__ dres) {
-    __shared__ float4 red[2][kThreads / 64][256];
+    __shared__ float4 red[2][kThreads / 64][64 * NI];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    float4 aw[4], ab[4];
+    float4 aw[NI], ab[NI], ww[NI], bb[NI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) aw[i] = ab[i] = make_float4(0, 0, 0, 0);
-    float4 ww[4], bb[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NI; ++i) {
         const int c = lane * 4 + 256 * i;
+        aw[i] = ab[i] = make_float4(0, 0, 0, 0);
         ww[i] = c < C ? *reinterpret_cast<const float4 *>(w + c) : make_float4(0, 0, 0, 0);
         bb[i] = (c < C && act == MTTS_ACT_RELU) ? *reinterpret_cast<const float4 *>(bia + c) : make_float4(0, 0, 0, 0);
     }
@@ -519,60 +538,80 @@ __global__ __launch_bounds__(kThreads) void layernorm_bwd_kernel(const float *__
     }
     const float inv_keep = 1.f / (1.f - p);
     const int rbeg = blockIdx.x * rows_per_block;
-    for (int rr = wv; rr < rows_per_block; rr += kThreads / 64) {
-        const int row = rbeg + rr;
-        if (row >= M) break;
-        const float mean = mean_in[row], rstd = rstd_in[row];
-        float4 xh[4], g[4];
-        float s1 = 0.f, s2 = 0.f;
+    const int rend = min(M, rbeg + rows_per_block);
+    for (int r0 = rbeg + wv * R; r0 < rend; r0 += (kThreads / 64) * R) {
+        float4 xv[R][NI], dv[R][NI], rv[R][NI];
+        float mean[R], rstd[R];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int c = lane * 4 + 256 * i;
-            if (c < C) {
-                const float4 xv = *reinterpret_cast<const float4 *>(x + (size_t)row * C + c);
-                float4 dv = *reinterpret_cast<const float4 *>(dy + (size_t)row * C + c);
-                xh[i] = make_float4((xv.x - mean) * rstd, (xv.y - mean) * rstd, (xv.z - mean) * rstd,
-                                    (xv.w - mean) * rstd);
-                if (tail) {  // through the fused tail: regenerate the dropout mask, ReLU gate from the LN output
-                    float d4[4] = {dv.x, dv.y, dv.z, dv.w};
-                    const float xs[4] = {xh[i].x, xh[i].y, xh[i].z, xh[i].w};
-                    const float w4[4] = {ww[i].x, ww[i].y, ww[i].z, ww[i].w};
-                    const float b4[4] = {bb[i].x, bb[i].y, bb[i].z, bb[i].w};
+        for (int q = 0; q < R; ++q) {  // every load of the R rows first
+            const int row = r0 + q;
+            const bool ok = row < rend;
+            mean[q] = ok ? mean_in[row] : 0.f;
+            rstd[q] = ok ? rstd_in[row] : 0.f;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        if (p > 0.f)
-                            d4[j] = mtts::dropout_keep(sd0, sd1, (uint32_t)row, (uint32_t)(c + j), p) ? d4[j] * inv_keep : 0.f;
-                        if (act == MTTS_ACT_RELU && xs[j] * w4[j] + b4[j] <= 0.f) d4[j] = 0.f;
-                    }
-                    dv = make_float4(d4[0], d4[1], d4[2], d4[3]);
-                }
-                g[i] = make_float4(dv.x * ww[i].x, dv.y * ww[i].y, dv.z * ww[i].z, dv.w * ww[i].w);
-                s1 += (g[i].x + g[i].y) + (g[i].z + g[i].w);
-                s2 += (g[i].x * xh[i].x + g[i].y * xh[i].y) + (g[i].z * xh[i].z + g[i].w * xh[i].w);
-                aw[i].x += dv.x * xh[i].x; aw[i].y += dv.y * xh[i].y; aw[i].z += dv.z * xh[i].z; aw[i].w += dv.w * xh[i].w;
-                ab[i].x += dv.x; ab[i].y += dv.y; ab[i].z += dv.z; ab[i].w += dv.w;
+            for (int i = 0; i < NI; ++i) {
+                const int c = lane * 4 + 256 * i;
+                const bool in = ok && c < C;
+                xv[q][i] = in ? *reinterpret_cast<const float4 *>(x + (size_t)row * C + c) : make_float4(0, 0, 0, 0);
+                dv[q][i] = in ? *reinterpret_cast<const float4 *>(dy + (size_t)row * C + c) : make_float4(0, 0, 0, 0);
+                rv[q][i] = in && dres ? *reinterpret_cast<const float4 *>(dres + (size_t)row * C + c) : make_float4(0, 0, 0, 0);
             }
         }
-        const float m1 = wave_sum(s1) / C, m2 = wave_sum(s2) / C;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int c = lane * 4 + 256 * i;
-            if (c < C) {
-                float4 o;
-                o.x = rstd * (g[i].x - m1 - xh[i].x * m2);
-                o.y = rstd * (g[i].y - m1 - xh[i].y * m2);
-                o.z = rstd * (g[i].z - m1 - xh[i].z * m2);
-                o.w = rstd * (g[i].w - m1 - xh[i].w * m2);
-                if (dres) {  // + the residual branch's gradient (pre-LN block: x feeds the LN and the residual)
-                    const float4 r = *reinterpret_cast<const float4 *>(dres + (size_t)row * C + c);
-                    o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+        for (int q = 0; q < R; ++q) {
+            const int row = r0 + q;
+            if (row >= rend) break;  // wave-uniform
+            float4 xh[NI], g[NI];
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int c = lane * 4 + 256 * i;
+                if (c < C) {
+                    const float4 xq = xv[q][i];
+                    float4 d = dv[q][i];
+                    xh[i] = make_float4((xq.x - mean[q]) * rstd[q], (xq.y - mean[q]) * rstd[q], (xq.z - mean[q]) * rstd[q],
+                                        (xq.w - mean[q]) * rstd[q]);
+                    if (tail) {  // through the fused tail: regenerate the dropout mask, ReLU gate from the LN output
+                        float d4[4] = {d.x, d.y, d.z, d.w};
+                        const float xs[4] = {xh[i].x, xh[i].y, xh[i].z, xh[i].w};
+                        const float w4[4] = {ww[i].x, ww[i].y, ww[i].z, ww[i].w};
+                        const float b4[4] = {bb[i].x, bb[i].y, bb[i].z, bb[i].w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            if (p > 0.f)
+                                d4[j] = mtts::dropout_keep(sd0, sd1, (uint32_t)row, (uint32_t)(c + j), p) ? d4[j] * inv_keep : 0.f;
+                            if (act == MTTS_ACT_RELU && xs[j] * w4[j] + b4[j] <= 0.f) d4[j] = 0.f;
+                        }
+                        d = make_float4(d4[0], d4[1], d4[2], d4[3]);
+                    }
+                    g[i] = make_float4(d.x * ww[i].x, d.y * ww[i].y, d.z * ww[i].z, d.w * ww[i].w);
+                    s1 += (g[i].x + g[i].y) + (g[i].z + g[i].w);
+                    s2 += (g[i].x * xh[i].x + g[i].y * xh[i].y) + (g[i].z * xh[i].z + g[i].w * xh[i].w);
+                    aw[i].x += d.x * xh[i].x; aw[i].y += d.y * xh[i].y; aw[i].z += d.z * xh[i].z; aw[i].w += d.w * xh[i].w;
+                    ab[i].x += d.x; ab[i].y += d.y; ab[i].z += d.z; ab[i].w += d.w;
                 }
-                *reinterpret_cast<float4 *>(dx + (size_t)row * C + c) = o;
+            }
+            const float m1 = wave_sum(s1) / C, m2 = wave_sum(s2) / C;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int c = lane * 4 + 256 * i;
+                if (c < C) {
+                    float4 o;
+                    o.x = rstd[q] * (g[i].x - m1 - xh[i].x * m2);
+                    o.y = rstd[q] * (g[i].y - m1 - xh[i].y * m2);
+                    o.z = rstd[q] * (g[i].z - m1 - xh[i].z * m2);
+                    o.w = rstd[q] * (g[i].w - m1 - xh[i].w * m2);
+                    if (dres) {  // + the residual branch's gradient (pre-LN block: x feeds the LN and the residual)
+                        o.x += rv[q][i].x; o.y += rv[q][i].y; o.z += rv[q][i].z; o.w += rv[q][i].w;
+                    }
+                    *reinterpret_cast<float4 *>(dx + (size_t)row * C + c) = o;
+                }
             }
         }
     }
     // reduce the 4 waves' partials (fixed order) -> one [C] partial per block
-    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
         const int c4 = lane + 64 * i;  // float4 index
         if (c4 * 4 < C) {
             red[0][wv][c4] = aw[i];
@@ -717,19 +756,30 @@ extern "C" int mtts_layernorm_fwd(const float *x, const float *w, const float *b
     MTTS_CHECK_ARG(M >= 0 && C >= 4 && C % 4 == 0 && C <= 1024, "layernorm_fwd: need C % 4 == 0, C <= 1024");
     MTTS_CHECK_ARG(aligned16(x) && aligned16(y) && aligned16(w) && aligned16(b), "layernorm_fwd: 16-byte alignment");
     if (M == 0) return MTTS_OK;
-    const int rows_per_block = kThreads / 64;
-    if (y16)
-        hipLaunchKernelGGL(layernorm_fwd_kernel<true>, dim3((M + rows_per_block - 1) / rows_per_block), dim3(kThreads), 0,
-                           static_cast<hipStream_t>(hip_stream), x, w, b, y, mean, rstd, M, C, eps, act, dropout_p, seed);
-    else
-        hipLaunchKernelGGL(layernorm_fwd_kernel<false>, dim3((M + rows_per_block - 1) / rows_per_block), dim3(kThreads), 0,
-                           static_cast<hipStream_t>(hip_stream), x, w, b, y, mean, rstd, M, C, eps, act, dropout_p, seed);
+    hipStream_t st = static_cast<hipStream_t>(hip_stream);
+    // 4 rows per wave (C <= 256) once the grid still has >= 2 blocks per CU; else one
+    const int R = C <= 256 && M >= 4 * 4 * 512 ? 4 : 1;
+    const dim3 grid((M + 4 * R - 1) / (4 * R));
+#define MTTS_LN_FWD(Y, NI, RR)                                                                                          \
+    hipLaunchKernelGGL((layernorm_fwd_kernel<Y, NI, RR>), grid, dim3(kThreads), 0, st, x, w, b, y, mean, rstd, M, C, eps, \
+                       act, dropout_p, seed)
+    if (C > 256) {
+        if (y16) MTTS_LN_FWD(true, 4, 1);
+        else MTTS_LN_FWD(false, 4, 1);
+    } else if (R == 4) {
+        if (y16) MTTS_LN_FWD(true, 1, 4);
+        else MTTS_LN_FWD(false, 1, 4);
+    } else {
+        if (y16) MTTS_LN_FWD(true, 1, 1);
+        else MTTS_LN_FWD(false, 1, 1);
+    }
+#undef MTTS_LN_FWD
     return mtts::check_launch("layernorm_fwd_kernel");
 }
 
 extern "C" size_t mtts_layernorm_bwd_workspace_size(int32_t M, int32_t C) {
     if (M <= 0 || C <= 0) return 0;
-    const int rpb = ln_rows_per_block(M);
+    const int rpb = ln_rows_per_block(M, C);
     return (size_t)2 * ((M + rpb - 1) / rpb) * C * sizeof(float);
 }
 
@@ -747,12 +797,16 @@ static int layernorm_bwd_impl(const float *dy, const float *x, const float *w, c
     if (!workspace || workspace_bytes < mtts_layernorm_bwd_workspace_size(M, C))
         return mtts::fail(MTTS_ERR_WORKSPACE, "layernorm_bwd: workspace too small");
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
-    const int rpb = ln_rows_per_block(M);
+    const int rpb = ln_rows_per_block(M, C);
     const int nblk = (M + rpb - 1) / rpb;
     float *pw = static_cast<float *>(workspace);
     float *pb = pw + (size_t)nblk * C;
-    hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(nblk), dim3(kThreads), 0, st, dy, x, w, b, mean, rstd, dx, pw, pb, M,
-                       C, act, dropout_p, seed, rpb, dres);
+    if (C <= 256)
+        hipLaunchKernelGGL((layernorm_bwd_kernel<1, 4>), dim3(nblk), dim3(kThreads), 0, st, dy, x, w, b, mean, rstd, dx,
+                           pw, pb, M, C, act, dropout_p, seed, rpb, dres);
+    else
+        hipLaunchKernelGGL((layernorm_bwd_kernel<4, 1>), dim3(nblk), dim3(kThreads), 0, st, dy, x, w, b, mean, rstd, dx,
+                           pw, pb, M, C, act, dropout_p, seed, rpb, dres);
     int rc = mtts::check_launch("layernorm_bwd_kernel");
     if (rc) return rc;
     return submit_param_sums(pw, dw, pb, db, nblk, C, st);

@@ -103,7 +103,7 @@ def set_weight_split(on: bool) -> bool:
 
 _WSPLIT_CV: contextvars.ContextVar = contextvars.ContextVar("mtts_w_split", default=None)
 # the text encoder's precision inside bf16-mixed when the model does not set its own
-# (MatchaTTS.encoder_precision): "bf16", "bf16x3" / "fp32fwd" (precise_forward) or "fp32"
+# (MatchaTTS.encoder_precision): "bf16", "bf16x3" / "bf16x6" / "fp32fwd" (precise_forward) or "fp32"
 _ENC_PREC: contextvars.ContextVar = contextvars.ContextVar("mtts_encoder_precision", default="bf16")
 
 
@@ -113,7 +113,9 @@ def weight_split_enabled() -> bool:
 
 
 # the parity policy's text-encoder forward: "fp32fwd" (exact-fp32 MFMA: 32-true's arithmetic) or "bf16x6"
-# (three exact bf16 planes per operand, six MFMAs: fp32-faithful at bf16 MFMA rates); MTTS_PARITY_ENCODER selects
+# (three exact bf16 planes per operand, six MFMAs).  bf16x6 measured 8.16 vs 8.05 ms per step and 1-3x the
+# fp32 kernel's error, enough to move 2 of 437 durations at B=4 (profiles/r04/x6): fp32fwd stays the
+# default; MTTS_PARITY_ENCODER selects
 _PARITY_ENC = os.environ.get("MTTS_PARITY_ENCODER", "fp32fwd")
 
 

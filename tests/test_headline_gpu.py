@@ -44,14 +44,16 @@ BF16_ATTN_AGREE = 0.99      # one plane: fraction of [Tx, Ty] alignment cells eq
 MODES = {"32-true": (False, False, "bf16"), "bf16-mixed": (True, False, "bf16"),
          "bf16-parity": (True, True, "fp32fwd"), "bf16-parity-fp32enc": (True, True, "fp32"),
          "bf16-parity-bf16x3": (True, True, "bf16x3"), "bf16-parity-bf16x6": (True, True, "bf16x6")}
-PARITY_MODES = ("bf16-parity", "bf16-parity-fp32enc", "bf16-parity-bf16x6")
+# bf16x6 is not at the bar: measured B=4 alignment 0.99990 (2 of 437 durations moved), duration loss 4e-4
+PARITY_MODES = ("bf16-parity", "bf16-parity-fp32enc")
 
 
 def run_precision(model, precision, fn):
     """fn() under `precision` (MODES): 32-true; bf16-mixed (one weight plane); bf16-parity (split weight
     planes + the text encoder's forward in exact fp32, backward bf16 -- the bench default);
     bf16-parity-fp32enc (split weight planes + the whole text encoder in exact fp32, round 3's policy);
-    bf16-parity-bf16x3 (split weight planes + the encoder forward in bf16x3)."""
+    bf16-parity-bf16x3 / -bf16x6 (split weight planes + the encoder forward in bf16x3 / bf16x6: both
+    flip alignment cells at B=4, so they are held to the one-plane bounds)."""
     from matcha.models.components import _ops as O
 
     amp, split, enc = MODES[precision]
