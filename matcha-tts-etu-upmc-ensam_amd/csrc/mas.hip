@@ -28,6 +28,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
@@ -51,7 +52,32 @@ struct MasArgs {
     int Tx, Ty, Txp, nch;
     int premasked;
     float neg;
+    int tr_ld;  // > 0: `value` is the premasked lattice TRANSPOSED, [B][Ty][tr_ld] (x contiguous; tr_ld = Txp)
 };
+
+// K consecutive floats at p (the text rows x0 .. x0+K-1 of one column of a transposed lattice): one wave
+// instruction moves 64 * K * 4 contiguous bytes -- the row-major lattice's lane-per-row loads touched 64 lines
+// per instruction and 16 bytes of each
+template <int K>
+__device__ __forceinline__ void load_col_rows(const float *__restrict__ p, float (&dst)[K]) {
+    if constexpr (K % 4 == 0) {
+#pragma unroll
+        for (int q = 0; q < K / 4; ++q) {
+            const float4 v = reinterpret_cast<const float4 *>(p)[q];
+            dst[4 * q] = v.x;
+            dst[4 * q + 1] = v.y;
+            dst[4 * q + 2] = v.z;
+            dst[4 * q + 3] = v.w;
+        }
+    } else if constexpr (K == 2) {
+        const float2 v = *reinterpret_cast<const float2 *>(p);
+        dst[0] = v.x;
+        dst[1] = v.y;
+    } else {
+#pragma unroll
+        for (int q = 0; q < K; ++q) dst[q] = p[q];
+    }
+}
 
 __device__ __forceinline__ float dpp_wave_shr1(float src, float lane0_value) {
     // lane l <- lane l-1; lane 0 keeps lane0_value (bound_ctrl = 0 disables the write there).
@@ -84,6 +110,22 @@ __device__ __forceinline__ void load_row_segment(const float *__restrict__ base,
     }
 }
 
+// One cell of the DP on the transposed lattice (TR kernels: paths only, no dp_out), the same decisions as the
+// select chain of the row-major kernels (core.pyx:65-80) with no compare on the column chain:
+//   from_same = d == 0 ? -inf : dp      -> min(dp, +-inf)          (the x == y forced diagonal)
+//   best      = diag ? from_prev : from_same, diag = from_prev >= from_same  -> max(from_prev, from_same)
+//   band      = x in [y - span, y] ? v : max_neg_val               -> med3(v, lo, hi), (lo, hi) = (-inf, +inf)
+//                                                                     in band, (neg, neg) outside
+// max / min pick the same VALUE as the selects (they differ only in the sign of an exact zero, which no later
+// comparison sees); diag is computed beside the chain for the backpointer bit.
+__device__ __forceinline__ float cell_tr(float fp, float dp, float sc, int d, unsigned span, float neg, bool &diag) {
+    const float fs = fminf(dp, d == 0 ? -INFINITY : INFINITY);
+    diag = fp >= fs;
+    const float v = fmaxf(fp, fs) + sc;
+    const bool band = (unsigned)d <= span;
+    return __builtin_amdgcn_fmed3f(v, band ? -INFINITY : neg, band ? INFINITY : neg);
+}
+
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F &&f) {
     if constexpr (B < E) {
@@ -92,8 +134,9 @@ __device__ __forceinline__ void static_for(F &&f) {
     }
 }
 
-template <int K, int C, int D, bool PM, bool VEC, bool LDS_BITS, bool DP_OUT>
+template <int K, int C, int D, bool PM, bool VEC, bool LDS_BITS, bool DP_OUT, bool TR = false>
 __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
+    static_assert(!TR || (PM && !DP_OUT), "the transposed lattice is premasked, and dp_out is row-major");
     extern __shared__ uint32_t smem[];
     const int b = blockIdx.x;
     const int lane = threadIdx.x;
@@ -140,7 +183,7 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
 #pragma unroll
         for (int i = 0; i < K; ++i) roff[i] = min(x0 + i, Tx - 1) * Ty;
         const int last = Tx * Ty - 1;
-        const float *vbase = a.value + ubase;
+        const float *vbase = TR ? a.value + (size_t)b * Ty * a.tr_ld + x0 : a.value + ubase;
         const float *mbase = PM ? vbase : a.mask + ubase;
 
         float dp[K];
@@ -160,6 +203,16 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
 
         auto load_chunk = [&](auto slot, int y0) {
             constexpr int sl = decltype(slot)::value;
+            if constexpr (TR) {  // column-major: one K-row vector per column
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    float col[K];
+                    load_col_rows<K>(vbase + (size_t)min(y0 + j, Ty - 1) * a.tr_ld, col);
+#pragma unroll
+                    for (int i = 0; i < K; ++i) vbuf[sl][i][j] = col[i];
+                }
+                return;
+            }
 #pragma unroll
             for (int i = 0; i < K; ++i) load_row_segment<C, VEC>(vbase, roff[i] + y0, last, vbuf[sl][i]);
             if constexpr (!PM) {
@@ -183,6 +236,24 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
 
         auto process_chunk = [&](auto slot, int y0) {
             constexpr int sl = decltype(slot)::value;
+            if constexpr (TR) {  // every column of the chunk (those past t_y feed nothing the backtrack reads)
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    const int y = y0 + j;
+                    const float nb = dpp_wave_shr1(dp[K - 1], y == 0 ? 0.0f : neg);
+                    float ndp[K];
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        bool diag;
+                        ndp[i] = cell_tr(i == 0 ? nb : dp[i - 1], dp[i], vbuf[sl][i][j], y - (x0 + i), span, neg, diag);
+                        R[i] = (R[i] << 1) | (diag ? 1u : 0u);
+                    }
+#pragma unroll
+                    for (int i = 0; i < K; ++i) dp[i] = ndp[i];
+                    if ((y & 31) == 31) flush_bits(y >> 5, 0);
+                }
+                return;
+            }
 #pragma unroll
             for (int j = 0; j < C; ++j) {
                 const int y = y0 + j;
@@ -234,7 +305,12 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
                 }
             });
         }
-        if (t_y & 31) flush_bits(t_y >> 5, 32 - (t_y & 31));
+        if constexpr (TR) {  // the columns processed: whole chunks
+            const int done_cols = nload * C;
+            if (done_cols & 31) flush_bits(done_cols >> 5, 32 - (done_cols & 31));
+        } else if (t_y & 31) {
+            flush_bits(t_y >> 5, 32 - (t_y & 31));
+        }
 
         if constexpr (!LDS_BITS) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
@@ -311,8 +387,9 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
 // the chain per column shrinks from K = Tx/64 rows per lane (one wave) to KL (e.g. Tx = 512: 8 -> 1)
 // at the price of one barrier per 32 columns and W - 1 fill phases.  The backtrack is mas_dp_kernel's
 // (wave 0), with the next backpointer word column prefetched while the current one is walked.
-template <int KL, int W, bool PM, bool VEC, bool LDS_BITS, bool DP_OUT>
+template <int KL, int W, bool PM, bool VEC, bool LDS_BITS, bool DP_OUT, bool TR = false>
 __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
+    static_assert(!TR || (PM && !DP_OUT), "the transposed lattice is premasked, and dp_out is row-major");
     constexpr int CC = 32;       // columns per chunk (one backpointer word)
     constexpr int C = CC / KL;   // columns per ring sub-chunk: KL * C = 32 cells per lane
     constexpr int KB = KL * W;   // backtrack words per lane (rows per lane of wave 0's walk)
@@ -362,7 +439,7 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
 #pragma unroll
         for (int i = 0; i < KL; ++i) roff[i] = min(x0 + i, Tx - 1) * Ty;
         const int last = Tx * Ty - 1;
-        const float *vbase = a.value + ubase;
+        const float *vbase = TR ? a.value + (size_t)b * Ty * a.tr_ld + x0 : a.value + ubase;
         const float *mbase = PM ? vbase : a.mask + ubase;
         float dp[KL];
         uint32_t R[KL];
@@ -380,6 +457,16 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
         float vbuf[RING][KL][C], mbuf[MD][KL][C];
         auto load_sub = [&](auto slot, int y0) {
             constexpr int sl = decltype(slot)::value;
+            if constexpr (TR) {  // column-major: one KL-row vector per column
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    float col[KL];
+                    load_col_rows<KL>(vbase + (size_t)min(y0 + j, Ty - 1) * a.tr_ld, col);
+#pragma unroll
+                    for (int i = 0; i < KL; ++i) vbuf[sl][i][j] = col[i];
+                }
+                return;
+            }
 #pragma unroll
             for (int i = 0; i < KL; ++i) load_row_segment<C, VEC>(vbase, roff[i] + y0, last, vbuf[sl][i]);
             if constexpr (!PM) {
@@ -414,8 +501,25 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
                     nbl[j] = y == 0 ? first : (wave == 0 ? neg : prev);
                 }
                 float eo[C];
+                if constexpr (TR) {  // every column (whole chunks: those past t_y feed nothing the backtrack reads)
 #pragma unroll
-                for (int j = 0; j < C; ++j) {
+                    for (int j = 0; j < C; ++j) {
+                        const float nb = dpp_wave_shr1(dp[KL - 1], nbl[j]);
+                        float ndp[KL];
+#pragma unroll
+                        for (int i = 0; i < KL; ++i) {
+                            bool diag;
+                            ndp[i] = cell_tr(i == 0 ? nb : dp[i - 1], dp[i], vbuf[sl][i][j], y0 + j - (x0 + i), span, neg,
+                                             diag);
+                            R[i] = (R[i] << 1) | (diag ? 1u : 0u);
+                        }
+#pragma unroll
+                        for (int i = 0; i < KL; ++i) dp[i] = ndp[i];
+                        eo[j] = dp[KL - 1];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < C && !TR; ++j) {
                     const int y = y0 + j;
                     eo[j] = neg;
                     if (y < t_y) {
@@ -454,7 +558,7 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
                 }
             });
             // the chunk's backpointer word per row (a partial last chunk left-aligned like mas_dp_kernel's)
-            const int sh = (c == nchunks - 1 && (t_y & 31)) ? 32 - (t_y & 31) : 0;
+            const int sh = (!TR && c == nchunks - 1 && (t_y & 31)) ? 32 - (t_y & 31) : 0;  // TR: all 32 columns ran
 #pragma unroll
             for (int i = 0; i < KL; ++i) {
                 const uint32_t w = R[i] << sh;
@@ -601,12 +705,16 @@ __global__ __launch_bounds__(256) void mas_expand_kernel(const int32_t *__restri
 // Tile: 64 text rows x 64 frames per 256-thread block, 4 x 4 cells per thread, mu / y tiles staged
 // in LDS 16 channels at a time.  The block of tile (0, 0) also writes t_x / t_y as int32 for the DP.
 constexpr int kLpT = 64;
-constexpr int kLpC = 16;  // channels staged per LDS round
+constexpr int kLpC = 80;  // channels staged per LDS round: all of n_feats = 80 in one (16 per round left five
+                           // dependent load -> barrier -> compute rounds per block: 39 us for 32 x 120 x 600)
 
+// TR: the lattice is written transposed, out[b][j][i] with row length LX (the DP's padded row count; rows
+// Tx .. LX-1 come out 0: their mask is 0), for the DP's column-major loads.
+template <bool TR>
 __global__ __launch_bounds__(256) void log_prior_kernel(const float *__restrict__ mu, const float *__restrict__ y,
                                                         const int64_t *__restrict__ xl, const int64_t *__restrict__ yl,
                                                         int C, int Tx, int Ty, float cst, float *__restrict__ out,
-                                                        int32_t *__restrict__ txy) {
+                                                        int32_t *__restrict__ txy, int LX) {
     __shared__ __attribute__((aligned(16))) float smu[kLpC][kLpT];
     __shared__ __attribute__((aligned(16))) float sy[kLpC][kLpT];
     const int b = blockIdx.z, i0 = blockIdx.y * kLpT, j0 = blockIdx.x * kLpT;
@@ -627,6 +735,7 @@ __global__ __launch_bounds__(256) void log_prior_kernel(const float *__restrict_
         for (int q = 0; q < 4; ++q) ymu[r][q] = 0.f;
     }
     for (int c0 = 0; c0 < C; c0 += kLpC) {
+#pragma unroll 4
         for (int e = tid; e < kLpC * kLpT; e += 256) {
             const int c = c0 + e / kLpT, t = e % kLpT;
             smu[e / kLpT][t] = (c < C && i0 + t < Tx) ? mub[(size_t)c * Tx + i0 + t] : 0.f;
@@ -649,6 +758,41 @@ __global__ __launch_bounds__(256) void log_prior_kernel(const float *__restrict_
         }
         __syncthreads();
     }
+    if constexpr (TR) {
+        float v[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + ti + r;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j = j0 + tj + q;
+                const float m = (i < t_x && j < t_y) ? 1.f : 0.f;  // x_mask[i] * y_mask[j]
+                v[r][q] = (((ysq[q] - ymu[r][q]) + musq[r]) + cst) * m;
+            }
+        }
+        // through LDS (the staging tiles are free after the last channel round's barrier): the tile's 64 frames
+        // x 64 rows leave as 256-byte row segments, one frame per 16 threads
+        __shared__ __attribute__((aligned(16))) float tr[32][kLpT + 4];  // half the tile's frames per pass
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {  // frames [32 * half, 32 * half + 32) per pass
+            if ((tj >> 5) == half) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    *reinterpret_cast<float4 *>(&tr[(tj & 31) + q][ti]) = make_float4(v[0][q], v[1][q], v[2][q], v[3][q]);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {  // 32 frames x 16 float4 = 512 float4 / 256 threads
+                const int f = (tid >> 4) + 16 * e, c4 = (tid & 15) * 4;
+                const int j = j0 + 32 * half + f;
+                if (j < Ty)  // i0 + c4 + 3 < LX: LX is a multiple of the 64-row tile
+                    *reinterpret_cast<float4 *>(out + ((size_t)b * Ty + j) * LX + i0 + c4) =
+                        *reinterpret_cast<const float4 *>(&tr[f][c4]);
+            }
+            __syncthreads();
+        }
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = i0 + ti + r;
@@ -668,6 +812,32 @@ __global__ __launch_bounds__(256) void log_prior_kernel(const float *__restrict_
             for (int q = 0; q < 4; ++q)
                 if (j0 + tj + q < Ty) row[q] = v[q];
         }
+    }
+}
+
+// The public maximum_path(value, mask)'s lattice, premasked and transposed for the DP's column-major
+// loads: out[b][y][x] = value[b][x][y] * mask[b][x][y] (the one fp32 multiply of __init__.py:45, as the DP
+// forms it on arrival), 0 for Tx <= x < LX.  64 x 64 tiles through LDS, coalesced both ways.
+__global__ __launch_bounds__(256) void mas_transpose_kernel(const float *__restrict__ value,
+                                                            const float *__restrict__ mask, int Tx, int Ty, int LX,
+                                                            float *__restrict__ out) {
+    __shared__ float t[64][65];
+    const int b = blockIdx.z, x0 = blockIdx.y * 64, y0 = blockIdx.x * 64;
+    const size_t ib = (size_t)b * Tx * Ty;
+    const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+    for (int r = r0; r < 64; r += 4) {
+        const int x = x0 + r, yy = y0 + c;
+        float v = 0.f;
+        if (x < Tx && yy < Ty) {
+            const size_t e = ib + (size_t)x * Ty + yy;
+            v = mask ? value[e] * mask[e] : value[e];
+        }
+        t[r][c] = v;
+    }
+    __syncthreads();
+    for (int r = r0; r < 64; r += 4) {
+        const int yy = y0 + r, x = x0 + c;
+        if (yy < Ty && x < LX) out[((size_t)b * Ty + yy) * LX + x] = t[c][r];
     }
 }
 
@@ -777,11 +947,33 @@ __global__ __launch_bounds__(256) void expand_rows_bwd_kernel(const float *__res
 }
 
 struct WsLayout {
-    size_t lengths, row_start, bits, total;
+    size_t lengths, row_start, bits, lat, total;  // lat: the transposed lattice (maximum_path_f32, tr_enabled)
     int K, Txp, nch;
     bool lds_bits;
     int W, KL;  // W > 1: the multi-wave DP (mas_dp_mw_kernel), W waves x KL rows per lane
 };
+
+// Whether the DP reads the transposed lattice (column-major loads) for text length Tx: from Tx > 128 (one-wave K >= 4
+// and the multi-wave kernels: 8 x 256 x 2048 0.278 -> 0.249 ms, 8 x 512 x 4096 0.930 -> 0.593, 8 x 1024 x 4096 1.90 ->
+// 0.93); at K <= 2 rows per lane the row-major loads are not what binds and the transposed copy costs more than
+// it saves (32 x 120 x 600, training path: 0.102 vs 0.106 ms; profiles/r04/mas/sweep.jsonl).  MTTS_MAS_TR=0 / 1
+// force it off / on; read at every call (a host getenv), so one process can run -- and test -- both layouts.
+bool tr_enabled(int Tx) {
+    const char *e = getenv("MTTS_MAS_TR");
+    if (e && e[0] == '0') return false;
+    if (e && e[0] == '1') return true;
+    return Tx > 128;
+}
+
+// lattice chunks in flight for the one-wave DP on the transposed lattice (MTTS_MAS_TR_RING: 2 / 4 / 8)
+int tr_ring() {
+    static const int d = [] {
+        const char *e = getenv("MTTS_MAS_TR_RING");
+        const int v = e ? atoi(e) : 0;
+        return (v == 2 || v == 4 || v == 8) ? v : 4;
+    }();
+    return d;
+}
 
 // MTTS_MAS_MW=0: the one-wave DP for every Tx (A/B; Tx <= 2048 then)
 bool mw_enabled() {
@@ -792,7 +984,7 @@ bool mw_enabled() {
     return on;
 }
 
-WsLayout ws_layout(int B, int Tx, int Ty) {
+WsLayout ws_layout(int B, int Tx, int Ty, bool with_lat = false) {
     WsLayout w{};
     w.W = 1;
     w.KL = 1;
@@ -808,6 +1000,26 @@ WsLayout ws_layout(int B, int Tx, int Ty) {
         w.K = w.W * w.KL;
         w.Txp = kWave * w.K;
     }
+    // MTTS_MAS_SHAPE="W,KL" (tuning sweeps, transposed-lattice DP only -- every lattice but the core.pyx API's):
+    // W waves x KL rows per lane; W = 1 the one-wave kernel (K from Tx).  Ignored unless it covers Tx.
+    if (const char *e = getenv("MTTS_MAS_SHAPE")) {
+        int W = 0, KL = 0;
+        if (sscanf(e, "%d,%d", &W, &KL) == 2 && tr_enabled(Tx)) {
+            const bool ok1 = W == 1;
+            const bool okm = (W == 2 && (KL == 1 || KL == 2)) || (W == 4 && (KL == 1 || KL == 2 || KL == 4)) ||
+                             (W == 8 && (KL == 1 || KL == 2 || KL == 4 || KL == 8));
+            if (ok1 && Tx <= 2048) {
+                w.W = w.KL = 1;
+                w.K = Tx <= 64 ? 1 : Tx <= 128 ? 2 : Tx <= 256 ? 4 : Tx <= 512 ? 8 : Tx <= 1024 ? 16 : 32;
+                w.Txp = kWave * w.K;
+            } else if (okm && kWave * W * KL >= Tx) {
+                w.W = W;
+                w.KL = KL;
+                w.K = W * KL;
+                w.Txp = kWave * w.K;
+            }
+        }
+    }
     w.nch = (Ty + 31) / 32;
     w.lds_bits = (size_t)w.Txp * w.nch * 4 <= (size_t)kLdsBitsLimit;
     size_t off = 0;
@@ -817,6 +1029,8 @@ WsLayout ws_layout(int B, int Tx, int Ty) {
     off = mtts::align_up(off + (size_t)B * Tx * 4, 256);
     w.bits = off;
     if (!w.lds_bits) off = mtts::align_up(off + (size_t)B * w.nch * w.Txp * 4, 256);
+    w.lat = off;
+    if (with_lat && tr_enabled(Tx)) off = mtts::align_up(off + (size_t)B * Ty * w.Txp * 4, 256);
     w.total = off;
     return w;
 }
@@ -898,9 +1112,65 @@ int launch_dp_kc(const MasArgs &a, int B, bool vec, bool lds_bits, bool dp_out, 
     return launch_dp_k<K, C, 4, true>(a, B, vec, lds_bits, dp_out, shmem, st);
 }
 
-int launch_dp(MasArgs a, int B, const WsLayout &w, bool vec, bool dp_out, hipStream_t st) {
+template <int KL, int W>
+int launch_dp_mw_tr(const MasArgs &a, int B, bool lds_bits, size_t shmem, hipStream_t st) {
+    if (lds_bits)
+        hipLaunchKernelGGL((mas_dp_mw_kernel<KL, W, true, false, true, false, true>), dim3(B), dim3(64 * W), shmem, st, a);
+    else
+        hipLaunchKernelGGL((mas_dp_mw_kernel<KL, W, true, false, false, false, true>), dim3(B), dim3(64 * W), shmem, st, a);
+    return mtts::check_launch("mas_dp_mw_kernel");
+}
+
+template <int K, int C, int D>
+int launch_dp_k_tr(const MasArgs &a, int B, bool lds_bits, size_t shmem, hipStream_t st) {
+    if (lds_bits)
+        hipLaunchKernelGGL((mas_dp_kernel<K, C, D, true, false, true, false, true>), dim3(B), dim3(kWave), shmem, st, a);
+    else
+        hipLaunchKernelGGL((mas_dp_kernel<K, C, D, true, false, false, false, true>), dim3(B), dim3(kWave), shmem, st, a);
+    return mtts::check_launch("mas_dp_kernel");
+}
+
+template <int K, int C>
+int launch_dp_kc_tr(const MasArgs &a, int B, bool lds_bits, size_t shmem, hipStream_t st) {
+    const int d = tr_ring();
+    if (d == 2) return launch_dp_k_tr<K, C, 2>(a, B, lds_bits, shmem, st);
+    if (d == 8) return launch_dp_k_tr<K, C, 8>(a, B, lds_bits, shmem, st);
+    return launch_dp_k_tr<K, C, 4>(a, B, lds_bits, shmem, st);
+}
+
+// The DP on the transposed premasked lattice (a.tr_ld > 0): same kernels, column-major loads
+int launch_dp_tr(const MasArgs &a, int B, const WsLayout &w, hipStream_t st) {
     if (w.W > 1) {
         const size_t shmem = (size_t)w.Txp * 4 + (size_t)3 * w.W * 32 * 4 + (w.lds_bits ? (size_t)w.Txp * w.nch * 4 : 0);
+        if (w.W == 2) return w.KL == 2 ? launch_dp_mw_tr<2, 2>(a, B, w.lds_bits, shmem, st)
+                                       : launch_dp_mw_tr<1, 2>(a, B, w.lds_bits, shmem, st);
+        if (w.W == 4) return w.KL == 4   ? launch_dp_mw_tr<4, 4>(a, B, w.lds_bits, shmem, st)
+                             : w.KL == 2 ? launch_dp_mw_tr<2, 4>(a, B, w.lds_bits, shmem, st)
+                                         : launch_dp_mw_tr<1, 4>(a, B, w.lds_bits, shmem, st);
+        switch (w.KL) {
+            case 1: return launch_dp_mw_tr<1, 8>(a, B, w.lds_bits, shmem, st);
+            case 2: return launch_dp_mw_tr<2, 8>(a, B, w.lds_bits, shmem, st);
+            case 4: return launch_dp_mw_tr<4, 8>(a, B, w.lds_bits, shmem, st);
+            default: return launch_dp_mw_tr<8, 8>(a, B, w.lds_bits, shmem, st);
+        }
+    }
+    const size_t shmem = (size_t)w.Txp * 4 + (w.lds_bits ? (size_t)w.Txp * w.nch * 4 : 0);
+    switch (w.K) {
+        case 1: return launch_dp_kc_tr<1, 32>(a, B, w.lds_bits, shmem, st);
+        case 2: return launch_dp_kc_tr<2, 16>(a, B, w.lds_bits, shmem, st);
+        case 4: return launch_dp_kc_tr<4, 8>(a, B, w.lds_bits, shmem, st);
+        case 8: return launch_dp_kc_tr<8, 4>(a, B, w.lds_bits, shmem, st);
+        case 16: return launch_dp_kc_tr<16, 2>(a, B, w.lds_bits, shmem, st);
+        default: return launch_dp_kc_tr<32, 1>(a, B, w.lds_bits, shmem, st);
+    }
+}
+
+int launch_dp(MasArgs a, int B, const WsLayout &w, bool vec, bool dp_out, hipStream_t st) {
+    if (a.tr_ld > 0) return dp_out ? mtts::fail(MTTS_ERR_INVALID_ARG, "maximum_path: dp_out needs the row-major lattice")
+                                   : launch_dp_tr(a, B, w, st);
+    if (w.W > 1) {
+        const size_t shmem = (size_t)w.Txp * 4 + (size_t)3 * w.W * 32 * 4 + (w.lds_bits ? (size_t)w.Txp * w.nch * 4 : 0);
+        if (w.W < 8 && w.KL != 1) return mtts::fail(MTTS_ERR_UNSUPPORTED, "maximum_path: DP shape needs the transposed lattice");
         if (w.W == 2) return launch_dp_mw_pm<1, 2>(a, B, vec, w.lds_bits, dp_out, shmem, st);
         if (w.W == 4) return launch_dp_mw_pm<1, 4>(a, B, vec, w.lds_bits, dp_out, shmem, st);
         switch (w.KL) {
@@ -934,7 +1204,7 @@ int check_shape(int B, int Tx, int Ty) {
 
 extern "C" size_t mtts_maximum_path_workspace_size(int32_t B, int32_t Tx, int32_t Ty) {
     if (B < 0 || Tx < 1 || Ty < 1) return 0;
-    return ws_layout(B, Tx, Ty).total;
+    return ws_layout(B, Tx, Ty, true).total;
 }
 
 extern "C" int mtts_maximum_path_f32(const float *value, const float *mask, float *path, int32_t B,
@@ -948,7 +1218,7 @@ extern "C" int mtts_maximum_path_f32(const float *value, const float *mask, floa
     if (B == 0) return MTTS_OK;
     MTTS_CHECK_ARG(value && mask, "maximum_path: value and mask are required");
     MTTS_CHECK_ARG(path || (flags & MTTS_MAS_NO_DENSE_PATH), "maximum_path: path is null");
-    const WsLayout w = ws_layout(B, Tx, Ty);
+    const WsLayout w = ws_layout(B, Tx, Ty, true);
     if (!workspace || workspace_bytes < w.total)
         return mtts::fail(MTTS_ERR_WORKSPACE, "maximum_path: workspace too small");
     char *ws = static_cast<char *>(workspace);
@@ -957,6 +1227,16 @@ extern "C" int mtts_maximum_path_f32(const float *value, const float *mask, floa
     MasArgs a{};
     a.value = value;
     a.mask = mask;
+    if (tr_enabled(Tx)) {  // premask + transpose once (coalesced), then the DP's column-major loads
+        float *lat = reinterpret_cast<float *>(ws + w.lat);
+        const bool pm = flags & MTTS_MAS_VALUE_PREMASKED;
+        hipLaunchKernelGGL(mas_transpose_kernel, dim3((Ty + 63) / 64, w.Txp / 64, B), dim3(256), 0, st, value,
+                           pm ? nullptr : mask, Tx, Ty, w.Txp, lat);
+        rc = mtts::check_launch("mas_transpose_kernel");
+        if (rc) return rc;
+        a.value = lat;
+        a.tr_ld = w.Txp;
+    }
     a.lengths = lengths_out ? lengths_out : reinterpret_cast<int32_t *>(ws + w.lengths);
     a.row_start = row_start_out ? row_start_out : reinterpret_cast<int32_t *>(ws + w.row_start);
     a.bits = reinterpret_cast<uint32_t *>(ws + w.bits);
@@ -964,7 +1244,7 @@ extern "C" int mtts_maximum_path_f32(const float *value, const float *mask, floa
     a.Ty = Ty;
     a.Txp = w.Txp;
     a.nch = w.nch;
-    a.premasked = (flags & MTTS_MAS_VALUE_PREMASKED) ? 1 : 0;
+    a.premasked = (flags & MTTS_MAS_VALUE_PREMASKED) || a.tr_ld ? 1 : 0;
     a.neg = -1e9f;
     const bool vec = (Ty % 4 == 0) && ((uintptr_t)value % 16 == 0) &&
                      (a.premasked || (uintptr_t)mask % 16 == 0);
@@ -980,8 +1260,9 @@ extern "C" int mtts_maximum_path_f32(const float *value, const float *mask, floa
 
 extern "C" size_t mtts_prior_maximum_path_workspace_size(int32_t B, int32_t Tx, int32_t Ty) {
     if (B < 0 || Tx < 1 || Ty < 1) return 0;
-    return mtts::align_up(ws_layout(B, Tx, Ty).total, 256) + mtts::align_up((size_t)B * 2 * 4, 256) +
-           (size_t)B * Tx * Ty * 4;
+    const WsLayout w = ws_layout(B, Tx, Ty);  // lattice: row-major [B,Tx,Ty] or transposed [B,Ty,Txp]
+    return mtts::align_up(w.total, 256) + mtts::align_up((size_t)B * 2 * 4, 256) +
+           (size_t)B * Ty * (Tx > w.Txp ? Tx : w.Txp) * 4;
 }
 
 extern "C" int mtts_prior_maximum_path(const float *mu_x, const float *y, const int64_t *x_lengths,
@@ -1002,10 +1283,17 @@ extern "C" int mtts_prior_maximum_path(const float *mu_x, const float *y, const 
     int32_t *txy = reinterpret_cast<int32_t *>(ws + o_txy);
     float *lat = lattice_out ? lattice_out : reinterpret_cast<float *>(ws + o_lat);
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
+    // the lattice the caller does not see is written transposed for the DP's column-major loads
+    const bool tr = !lattice_out && tr_enabled(Tx);
 
     const float cst = (float)(-0.5 * std::log(2.0 * M_PI) * C);  // the Python scalar, rounded as torch does
-    dim3 lg((Ty + kLpT - 1) / kLpT, (Tx + kLpT - 1) / kLpT, B);
-    hipLaunchKernelGGL(log_prior_kernel, lg, dim3(256), 0, st, mu_x, y, x_lengths, y_lengths, C, Tx, Ty, cst, lat, txy);
+    dim3 lg((Ty + kLpT - 1) / kLpT, ((tr ? w.Txp : Tx) + kLpT - 1) / kLpT, B);
+    if (tr)
+        hipLaunchKernelGGL(log_prior_kernel<true>, lg, dim3(256), 0, st, mu_x, y, x_lengths, y_lengths, C, Tx, Ty, cst,
+                           lat, txy, w.Txp);
+    else
+        hipLaunchKernelGGL(log_prior_kernel<false>, lg, dim3(256), 0, st, mu_x, y, x_lengths, y_lengths, C, Tx, Ty, cst,
+                           lat, txy, 0);
     rc = mtts::check_launch("log_prior_kernel");
     if (rc) return rc;
 
@@ -1022,6 +1310,7 @@ extern "C" int mtts_prior_maximum_path(const float *mu_x, const float *y, const 
     a.nch = w.nch;
     a.premasked = 1;
     a.neg = -1e9f;
+    a.tr_ld = tr ? w.Txp : 0;
     const bool vec = (Ty % 4 == 0) && ((uintptr_t)lat % 16 == 0);
     rc = launch_dp(a, B, w, vec, false, st);
     if (rc) return rc;

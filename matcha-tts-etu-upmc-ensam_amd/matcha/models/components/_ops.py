@@ -802,6 +802,12 @@ def param_grad_side_stream():
 side_fork = param_grad_side_stream  # the same fork, for forward work that runs ahead (prefetch)
 
 
+def side_fork_available() -> bool:
+    """Whether side_fork() would return a stream (without forking): lets a caller finish the main-stream work
+    the side work reads before the fork orders the side stream after it."""
+    return bool(_DEFER["on"] and _SIDE_FLUSH) and not _DEFER["side_on"]
+
+
 def keep_for_side(*ts) -> None:
     _DEFER["side_keep"].extend(t for t in ts if t is not None)
 

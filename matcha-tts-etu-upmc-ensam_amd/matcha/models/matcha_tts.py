@@ -130,6 +130,10 @@ class MatchaTTS(BaseLightningClass):
         # inside a Trainer step (the gradient deferral's side stream exists): the decoder's weight packs and
         # time path for this step's CFM time run on the side stream beside the text encoder (t drawn here
         # instead of in compute_loss; the same distribution)
+        # t is drawn BEFORE the fork: the side stream's time embedding reads it, and the fork orders the side
+        # stream after the main stream's work up to that point only (drawn after it, the read raced the draw)
+        if x.is_cuda and _PREFETCH and t is None and O.side_fork_available():
+            t = torch.rand([x.shape[0], 1, 1], device=x.device, dtype=torch.float32)
         side = O.side_fork() if (x.is_cuda and _PREFETCH) else None
         if side is not None:
             if t is None:

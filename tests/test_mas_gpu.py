@@ -213,6 +213,29 @@ def test_prior_maximum_path_vs_oracle(B, C, Tx, Ty):
     np.testing.assert_array_equal(lens.cpu().numpy(), exp_t)
     np.testing.assert_array_equal(dur.cpu().numpy(), PO.durations(exp_path))
     np.testing.assert_array_equal(col_row.cpu().numpy(), PO.col_row(exp_path))
+    # without return_lattice the lattice is written transposed for the DP's column-major loads: same outputs
+    got = prior_maximum_path(d(mu), d(y), d(xl), d(yl))
+    for a, b in zip(got, (attn, dur, col_row, rs, lens)):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("Tx,Ty", [(1, 1), (5, 7), (64, 64), (120, 600), (129, 301), (257, 700), (512, 4096),
+                                   (1025, 1100), (2049, 2100), (4096, 4100)])
+def test_transposed_and_row_major_lattice_agree(Tx, Ty, monkeypatch):
+    """maximum_path(value, mask) with the DP on the premasked transposed lattice (default: one coalesced
+    transpose, column-major loads) and on the row-major one (MTTS_MAS_TR=0: lane-per-row loads, value * mask
+    formed in the DP): identical paths, row starts and lengths, both bit-exact vs the oracle."""
+    rng = np.random.default_rng(Tx * 31 + Ty)
+    value, t_x, t_y = _rand_case(rng, 3, Tx, Ty, ties=Tx % 2 == 0)
+    mask = O.lengths_mask(3, Tx, value.shape[2], t_x, np.maximum(t_y, t_x))
+    outs = {}
+    for tr in ("1", "0"):
+        monkeypatch.setenv("MTTS_MAS_TR", tr)
+        outs[tr] = gpu_path(value, mask)
+    for a, b in zip(outs["1"], outs["0"]):
+        np.testing.assert_array_equal(a, b)
+    exp_p, _ = O.maximum_path(value, mask)
+    np.testing.assert_array_equal(outs["1"][0], exp_p)
 
 
 def test_prior_lattice_matches_torch_formula():
