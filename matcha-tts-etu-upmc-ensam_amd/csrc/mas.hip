@@ -117,11 +117,13 @@ __device__ __forceinline__ void load_row_segment(const float *__restrict__ base,
 //   band      = x in [y - span, y] ? v : max_neg_val               -> med3(v, lo, hi), (lo, hi) = (-inf, +inf)
 //                                                                     in band, (neg, neg) outside
 // max / min pick the same VALUE as the selects (they differ only in the sign of an exact zero, which no later
-// comparison sees); diag is computed beside the chain for the backpointer bit.
+// comparison sees); diag is computed beside the chain for the backpointer bit.  min and max are written as med3
+// against an infinity (min(a, b) = med3(a, b, -inf), max(a, b) = med3(a, b, +inf)): fminf / fmaxf under IEEE
+// mode cost a canonicalising v_max_f32 x, x per operand on the chain.
 __device__ __forceinline__ float cell_tr(float fp, float dp, float sc, int d, unsigned span, float neg, bool &diag) {
-    const float fs = fminf(dp, d == 0 ? -INFINITY : INFINITY);
+    const float fs = __builtin_amdgcn_fmed3f(dp, d == 0 ? -INFINITY : INFINITY, -INFINITY);
     diag = fp >= fs;
-    const float v = fmaxf(fp, fs) + sc;
+    const float v = __builtin_amdgcn_fmed3f(fp, fs, INFINITY) + sc;
     const bool band = (unsigned)d <= span;
     return __builtin_amdgcn_fmed3f(v, band ? -INFINITY : neg, band ? INFINITY : neg);
 }
