@@ -355,7 +355,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
         }
     };
 
-    if constexpr (BF16 && DEPTH == 2) {
+    if constexpr (DEPTH == 2) {
         // two K steps in flight: the loads of step kt+2 are issued before computing step kt, stored to
         // LDS after computing step kt+1 -- two compute phases cover each global round trip
         load_tile(R0, kbase);
@@ -975,6 +975,7 @@ constexpr TileCfg kCfgs[] = {
     {1, 4, 1, 2, 64, 2},  // 15: 32 x 256, K64, two steps in flight (bf16)
     {2, 2, 1, 1, 64, 2},  // 16: 64 x 64, K64, two steps in flight (bf16)
     {1, 2, 1, 1, 64, 2},  // 17: 32 x 64 (128 threads), K64, two steps in flight (bf16)
+    {2, 2, 1, 1, 32, 2},  // 18: config 3 (64 x 64, K32) with two steps in flight (fp32; bf16 too)
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -996,7 +997,7 @@ static void launch_cfg(const mtts_conv_gemm_args &p, int M, hipStream_t st, int 
     const int ksteps = splits > 1 ? (nk + splits - 1) / splits : nk;
     const int S = splits > 1 ? (nk + ksteps - 1) / ksteps : 1;  // every split non-empty
     dim3 grid((unsigned)(((M + BM - 1) / BM) * ((p.N + BN - 1) / BN) * S));
-    hipLaunchKernelGGL((conv_gemm_kernel<BF16, c.wm, c.wn, c.tm, c.tn, KBc, (BF16 ? c.depth : 1), WS, AS>),
+    hipLaunchKernelGGL((conv_gemm_kernel<BF16, c.wm, c.wn, c.tm, c.tn, KBc, c.depth, WS, AS>),
                        grid, dim3(64 * c.wm * c.wn), 0, st, p, ksteps, S > 1 ? part : nullptr);
     if (S > 1) mtts::splitk_combine(p, M, part, S, st);
 }
@@ -1036,7 +1037,8 @@ static void launch_by_id(int id, const mtts_conv_gemm_args &p, int M, hipStream_
         case 14: launch_cfg<BF16, 14>(p, M, st, splits, part); break;
         case 15: launch_cfg<BF16, 15>(p, M, st, splits, part); break;
         case 16: launch_cfg<BF16, 16>(p, M, st, splits, part); break;
-        default: launch_cfg<BF16, 17>(p, M, st, splits, part); break;
+        case 17: launch_cfg<BF16, 17>(p, M, st, splits, part); break;
+        default: launch_cfg<BF16, 18>(p, M, st, splits, part); break;
     }
 }
 
@@ -1061,7 +1063,12 @@ static int pick_cfg(const mtts_conv_gemm_args &p, int M, bool bf16) {
     // fp32: 64 x 64 tiles (config 3) on the text encoder's 3840-row GEMMs -- the best register schedule on every
     // one of its exact-fp32 forward calls (tools/r4/gemm_f32_sweep.py, profiles/r04/sweeps/f32_sweep.jsonl: 1044 ->
     // 841 us per step with the split-K counts below); the decoder-sized fp32 GEMMs keep config 7
-    if (!bf16) return M <= 8192 ? 3 : 7;
+    // the decoder-sized fp32 GEMMs (32-true) take config 7 with two K steps in flight (config 11): same MFMAs in
+    // the same order, 32-true step 16.70 -> 16.50 ms; on the 3840-row encoder GEMMs the two-step 64 x 64 config 18
+    // measured no faster (bf16-parity 8.17 vs 8.20 ms; profiles/r04/f32_depth2/).  MTTS_GEMM_F32_DEPTH2=1 / 0:
+    // two steps in flight everywhere / nowhere
+    static const int d2 = [] { const char *e = getenv("MTTS_GEMM_F32_DEPTH2"); return e ? (e[0] == '1' ? 1 : 0) : -1; }();
+    if (!bf16) return M <= 8192 ? (d2 == 1 ? 18 : 3) : (d2 == 0 ? 7 : 11);
     if (p.act == MTTS_ACT_GELU || p.act == MTTS_ACT_DGELU) return 7;
     static const int sched_mask = [] {  // MTTS_GEMM_SCHED_OFF bit mask: A/B switch for experiments
         const char *e = getenv("MTTS_GEMM_SCHED_OFF");
@@ -1120,13 +1127,13 @@ static int pick_splits_f32(const mtts_conv_gemm_args &p, int M, int cfg, int spl
     if (p.N % 4 || off || !mtts::gemm_epilogue_vec_ok(p)) return 1;  // the combine is float4
     if (splits > 0) return splits;  // explicit (sweeps): any register schedule
     const int nk = (p.K + kBK - 1) / kBK;
-    if (cfg == 3) {  // 64 x 64: 4 splits from 28 K steps, 2 from 20 (sweep: 3840 x 192 x 2304 44 us at 4 vs 58 at
+    if (cfg == 3 || cfg == 18) {  // 64 x 64: 4 splits from 28 K steps, 2 from 20 (sweep: 3840 x 192 x 2304 44 us at 4 vs 58 at
                      // 1; k = 5 prenet 27.4 at 4; 3840 x 256 x 768 25.8 at 2; 576-deep ones unsplit)
         const int tiles = ((M + 63) / 64) * ((p.N + 63) / 64);
         if (tiles >= 256 || nk < 20) return 1;
         return nk >= 28 ? 4 : 2;
     }
-    if (cfg != 7) return 1;
+    if (cfg != 7 && cfg != 11) return 1;
     const int tiles = ((M + 31) / 32) * ((p.N + 127) / 128);
     if (tiles >= 256 || nk < 16) return 1;
     return std::min(8, std::max(2, nk / 9));  // ~9 K steps of 32 per split

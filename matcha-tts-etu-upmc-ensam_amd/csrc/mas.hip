@@ -236,8 +236,40 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
             }
         };
 
+        // Interior chunks: when every valid text row x < t_x of the chunk's columns has 1 <= y - x <= span, no cell
+        // is on the forced diagonal or outside the band, so the cell is just best-of-two + score -- the same
+        // operations as the full update on those cells (bit-identical values and decisions); rows >= t_x (padding
+        // lanes) then compute values nothing reads.  Most columns of a long utterance are interior.
+        const int hi_row = min(kWave * K, t_x) - 1;  // the last valid text row this wave owns
         auto process_chunk = [&](auto slot, int y0) {
             constexpr int sl = decltype(slot)::value;
+            if (y0 > hi_row && y0 + C - 1 <= (int)span && (TR || y0 + C <= t_y)) {  // wave-uniform
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    const int y = y0 + j;
+                    const float nb = dpp_wave_shr1(dp[K - 1], neg);  // y >= 1 here
+                    float ndp[K];
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        float sc;
+                        if constexpr (PM) sc = vbuf[sl][i][j];
+                        else sc = vbuf[sl][i][j] * mbuf[sl][i][j];  // __init__.py:45
+                        const float fp = i == 0 ? nb : dp[i - 1], fs = dp[i];
+                        const bool diag = fp >= fs;
+                        ndp[i] = (TR ? __builtin_amdgcn_fmed3f(fp, fs, INFINITY) : (diag ? fp : fs)) + sc;
+                        R[i] = (R[i] << 1) | (diag ? 1u : 0u);
+                    }
+#pragma unroll
+                    for (int i = 0; i < K; ++i) dp[i] = ndp[i];
+                    if constexpr (DP_OUT) {
+#pragma unroll
+                        for (int i = 0; i < K; ++i)
+                            if (x0 + i < t_x) a.dp_out[ubase + (size_t)(x0 + i) * Ty + y] = ndp[i];
+                    }
+                    if ((y & 31) == 31) flush_bits(y >> 5, 0);
+                }
+                return;
+            }
             if constexpr (TR) {  // every column of the chunk (those past t_y feed nothing the backtrack reads)
 #pragma unroll
                 for (int j = 0; j < C; ++j) {
@@ -503,7 +535,35 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
                     nbl[j] = y == 0 ? first : (wave == 0 ? neg : prev);
                 }
                 float eo[C];
-                if constexpr (TR) {  // every column (whole chunks: those past t_y feed nothing the backtrack reads)
+                // interior sub-chunk (see mas_dp_kernel): this wave's valid rows all strictly below the diagonal and
+                // inside the band for every column -> best-of-two + score
+                const int lo_row = wave * 64 * KL, hi_row = min(lo_row + 64 * KL, t_x) - 1;
+                const bool interior = y0 > hi_row && y0 + C - 1 - lo_row <= (int)span && (TR || y0 + C <= t_y);
+                if (interior) {
+#pragma unroll
+                    for (int j = 0; j < C; ++j) {
+                        const float nb = dpp_wave_shr1(dp[KL - 1], nbl[j]);
+                        float ndp[KL];
+#pragma unroll
+                        for (int i = 0; i < KL; ++i) {
+                            float sc;
+                            if constexpr (PM) sc = vbuf[sl][i][j];
+                            else sc = vbuf[sl][i][j] * mbuf[sl][i][j];  // __init__.py:45
+                            const float fp = i == 0 ? nb : dp[i - 1], fs = dp[i];
+                            const bool diag = fp >= fs;
+                            ndp[i] = (TR ? __builtin_amdgcn_fmed3f(fp, fs, INFINITY) : (diag ? fp : fs)) + sc;
+                            R[i] = (R[i] << 1) | (diag ? 1u : 0u);
+                        }
+#pragma unroll
+                        for (int i = 0; i < KL; ++i) dp[i] = ndp[i];
+                        if constexpr (DP_OUT) {
+#pragma unroll
+                            for (int i = 0; i < KL; ++i)
+                                if (x0 + i < t_x) a.dp_out[ubase + (size_t)(x0 + i) * Ty + y0 + j] = ndp[i];
+                        }
+                        eo[j] = dp[KL - 1];
+                    }
+                } else if constexpr (TR) {  // every column (whole chunks: those past t_y feed nothing the backtrack reads)
 #pragma unroll
                     for (int j = 0; j < C; ++j) {
                         const float nb = dpp_wave_shr1(dp[KL - 1], nbl[j]);
@@ -521,7 +581,7 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
                     }
                 }
 #pragma unroll
-                for (int j = 0; j < C && !TR; ++j) {
+                for (int j = 0; j < C && !TR && !interior; ++j) {
                     const int y = y0 + j;
                     eo[j] = neg;
                     if (y < t_y) {

@@ -248,3 +248,27 @@ def test_precise_forward_bf16x6_encoder_close_to_32true():
     print("encoder forward rel err vs 32-true (mu_x, logw):", errs)
     assert errs["bf16x6"][0] < 5e-6 and errs["bf16x6"][1] < 5e-6, errs
     assert errs["bf16x3"][0] > errs["bf16x6"][0], errs
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout,k,splits", [(32, 120, 192, 192, 5, 0), (32, 120, 768, 192, 3, 0),
+                                                   (32, 120, 768, 192, 3, 4), (32, 120, 192, 576, 1, 0),
+                                                   (3, 37, 256, 80, 1, 0), (32, 120, 192, 768, 3, 2)])
+def test_fp32_two_steps_in_flight_bitwise(B, T, Cin, Cout, k, splits):
+    """The exact-fp32 register schedules with two K steps in flight (configs 18 / 11, MTTS_GEMM_F32_DEPTH2) issue
+    the same MFMAs in the same order as configs 3 / 7: bitwise equal outputs, split-K included."""
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator().manual_seed(B * Cout + k + 11)
+    x = torch.randn(B, T, Cin, generator=g).to(DEV)
+    w = (torch.randn(Cout, Cin, k, generator=g) / (Cin * k) ** 0.5).to(DEV)
+    b = torch.randn(Cout, generator=g).to(DEV)
+    m = (torch.arange(T)[None] < torch.randint(T // 2, T + 1, (B,), generator=g)[:, None]).float().to(DEV)
+    Wf, Kf = O.packed(O.spec_conv_fwd(w), O.PREC_FP32)
+    outs = {}
+    for cfg in (3, 18, 7, 11):
+        y = torch.empty(B, T, Cout, device=DEV)
+        O._gemm(x, T, T, B, 1, [j - k // 2 for j in range(k)], Cin, Wf, Kf, Cout, y, T, prec=O.PREC_FP32,
+                a_scale=m, bias=b, tile_cfg=cfg, splits=splits)
+        outs[cfg] = y
+    assert torch.equal(outs[3], outs[18])
+    assert torch.equal(outs[7], outs[11])
