@@ -788,11 +788,12 @@ __global__ __launch_bounds__(256) void log_prior_kernel(const float *__restrict_
         txy[gridDim.z + b] = t_y;
     }
     const float *mub = mu + (size_t)b * C * Tx, *yb = y + (size_t)b * C * Ty;
-    float ymu[4][4], ysq[4], musq[4];
+    // the squared-norm terms are per row (musq) and per frame (ysq): threads 0..63 own the tile's rows, 64..127 its
+    // frames, each accumulating in channel order exactly as every thread of a row / frame used to (same values)
+    __shared__ float s_musq[kLpT], s_ysq[kLpT];
+    float ymu[4][4], ysq[4], musq[4], sq = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        ysq[r] = 0.f;
-        musq[r] = 0.f;
 #pragma unroll
         for (int q = 0; q < 4; ++q) ymu[r][q] = 0.f;
     }
@@ -805,6 +806,13 @@ __global__ __launch_bounds__(256) void log_prior_kernel(const float *__restrict_
         }
         __syncthreads();
         const int cn = min(kLpC, C - c0);
+        if (tid < 2 * kLpT) {  // wave-uniform: waves 0-1 rows, waves 2-3 frames
+            const float *col = tid < kLpT ? &smu[0][tid] : &sy[0][tid - kLpT];
+            for (int c = 0; c < cn; ++c) {
+                const float v = col[c * kLpT];
+                sq = sq + -0.5f * (v * v);
+            }
+        }
 #pragma unroll 4
         for (int c = 0; c < cn; ++c) {
             const float4 m4 = *reinterpret_cast<const float4 *>(&smu[c][ti]);
@@ -812,13 +820,19 @@ __global__ __launch_bounds__(256) void log_prior_kernel(const float *__restrict_
             const float mv[4] = {m4.x, m4.y, m4.z, m4.w}, yv[4] = {y4.x, y4.y, y4.z, y4.w};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                musq[r] = musq[r] + -0.5f * (mv[r] * mv[r]);
-                ysq[r] = ysq[r] + -0.5f * (yv[r] * yv[r]);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) ymu[r][q] = ymu[r][q] + (-mv[r]) * yv[q];
             }
         }
         __syncthreads();
+    }
+    if (tid < kLpT) s_musq[tid] = sq;
+    else if (tid < 2 * kLpT) s_ysq[tid - kLpT] = sq;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        musq[r] = s_musq[ti + r];
+        ysq[r] = s_ysq[tj + r];
     }
     if constexpr (TR) {
         float v[4][4];
