@@ -113,12 +113,13 @@ def cpu_baseline(B_cpu: int, Tx: int, Ty: int, budget_s: float) -> dict:
 
 
 def mas_chain_bound(Tx: int, Ty: int, mas_ms: float, clock_ghz: float = 2.1) -> dict:
-    """The DP is a Ty-long dependency chain per utterance (one wave each, utterances in parallel on
-    their own CUs): per column a lane updates its K = ceil(Tx / 64) rows (about 9 dependent VALU
-    instructions per row -- score, compare, select, add, band test, backpointer shift/or) plus one
-    DPP neighbour exchange, each waiting ~8 cycles for its predecessor at one wave per SIMD.  The
-    estimate is that chain's length; measured / estimate near 1 means the kernel runs at its chain
-    bound, not at HBM speed (which the 12 B/cell roofline would ask for)."""
+    """The DP is a Ty-long dependency chain per utterance (one wave each at this Tx, utterances in parallel on
+    their own CUs): per column a lane updates its K = ceil(Tx / 64) rows -- in the interior chunks (round 4:
+    every valid row strictly below the diagonal and inside the band) about 5 VALU per row (compare, select,
+    add, backpointer shift / or), at the band edges about 9 (plus the diagonal and band tests) -- plus one
+    DPP neighbour exchange, each waiting ~8 cycles for its predecessor at one wave per SIMD.  The estimate
+    uses the edge count; measured / estimate near or below 1 means the kernel runs at its chain bound, not at
+    HBM speed (which the 12 B/cell roofline would ask for)."""
     K = 1
     while 64 * K < Tx:
         K *= 2
