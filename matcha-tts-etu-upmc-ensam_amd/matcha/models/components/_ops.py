@@ -112,6 +112,10 @@ def weight_split_enabled() -> bool:
     return _W_SPLIT if v is None else v
 
 
+# MTTS_PARITY_FF1_SPLIT=0: the decoder FeedForward's GELU up-projection keeps one bf16 weight plane under the
+# parity policy (its share of the diffusion loss's weight-rounding error is ~3.5 %, tools/r3/weight_sensitivity.py)
+_FF1_SPLIT = os.environ.get("MTTS_PARITY_FF1_SPLIT", "1") != "0"
+
 # the parity policy's text-encoder forward: "fp32fwd" (exact-fp32 MFMA: 32-true's arithmetic) or "bf16x6"
 # (three exact bf16 planes per operand, six MFMAs).  bf16x6 measured 8.16 vs 8.05 ms per step and 1-3x the
 # fp32 kernel's error, enough to move 2 of 437 durations at B=4 (profiles/r04/x6): fp32fwd stays the
@@ -299,19 +303,20 @@ def pack_weight(w2d: torch.Tensor, prec: int) -> tuple[torch.Tensor, int]:
 # mtts_pack_weights jobs (include/mtts_decoder.h).  job = (src, row0, rows, col0, Kp_job, C, ntaps,
 # sr, sc, sj, j0, js): dst[row0 + r][col0 + j*C + c] = src[r*sr + c*sc + (j0 + j*js)*sj].
 class PackSpec:
-    __slots__ = ("key", "rows", "Kp", "jobs", "dgrad")
+    __slots__ = ("key", "rows", "Kp", "jobs", "dgrad", "one_plane")
 
-    def __init__(self, key, rows, Kp, jobs, dgrad):
+    def __init__(self, key, rows, Kp, jobs, dgrad, one_plane=False):
         self.key, self.rows, self.Kp, self.jobs, self.dgrad = key, rows, Kp, jobs, dgrad
+        self.one_plane = one_plane  # a forward operand kept in one bf16 plane even where the policy splits
 
 
 def _r8(n):
     return (n + 7) // 8 * 8
 
 
-def spec_linear(ws, dgrad=False):
+def spec_linear(ws, dgrad=False, one_plane=False):
     """Linear weights [N_i, K] stacked along N -> [sum N_i, Kp] (forward); dgrad: the transpose
-    [K, sum N_i] (column blocks; each N_i % 8 == 0 when stacking)."""
+    [K, sum N_i] (column blocks; each N_i % 8 == 0 when stacking).  one_plane: never the split planes."""
     ws = tuple(ws)
     K = ws[0].shape[1]  # nn.Conv1d 1x1 weights [N, K, 1] have the Linear layout
     if not dgrad:
@@ -319,7 +324,7 @@ def spec_linear(ws, dgrad=False):
         for w in ws:
             jobs.append((w, r0, w.shape[0], 0, _r8(K), K, 1, K, 1, 0, 0, 1))
             r0 += w.shape[0]
-        return PackSpec(("lin",) + tuple(id(w) for w in ws), r0, _r8(K), jobs, False)
+        return PackSpec(("lin",) + tuple(id(w) for w in ws), r0, _r8(K), jobs, False, one_plane)
     ntot = sum(w.shape[0] for w in ws)
     jobs, c0 = [], 0
     for i, w in enumerate(ws):
@@ -398,6 +403,8 @@ def _pack_kind(spec: PackSpec, prec: int) -> int:
     """bf16 forward operands: fp32 under precise_forward("fp32"), the split planes when selected
     (set_weight_split, precise_forward("bf16x3")); everything else as prec."""
     if prec == PREC_BF16 and not spec.dgrad:
+        if spec.one_plane and not _PRECISE.get():
+            return prec
         if _fwd_fp32():
             return PREC_FP32
         if _PRECISE.get() == "bf16x6":
@@ -1726,7 +1733,7 @@ class _PreLNFeedForwardTM(torch.autograd.Function):
         # in isolation (53.3 vs 61.0 us at 19200 x 1024 x 256, tools/ff_epilogue_cost.py) but the step
         # measured slower (9.22 vs 8.92 ms); the register-staged schedule hides the GELU epilogue
         n, mean, rstd = _ln_fwd(h2, lnw, lnb, eps, False)
-        W1p, K1p = packed(spec_linear((w1,)), prec)
+        W1p, K1p = packed(spec_linear((w1,), one_plane=not _FF1_SPLIT), prec)
         W2p, K2p = packed(spec_linear((w2,)), prec)
         ctx.w2t = packed(spec_linear((w2,), dgrad=True), prec)
         ctx.w1t = packed(spec_linear((w1,), dgrad=True), prec)
