@@ -112,9 +112,12 @@ def weight_split_enabled() -> bool:
     return _W_SPLIT if v is None else v
 
 
-# MTTS_PARITY_FF1_SPLIT=0: the decoder FeedForward's GELU up-projection keeps one bf16 weight plane under the
-# parity policy (its share of the diffusion loss's weight-rounding error is ~3.5 %, tools/r3/weight_sensitivity.py)
-_FF1_SPLIT = os.environ.get("MTTS_PARITY_FF1_SPLIT", "1") != "0"
+# The decoder FeedForward's GELU up-projection keeps ONE bf16 weight plane under the parity policy: its share of the
+# diffusion loss's weight-rounding error is ~3.5 % (tools/r3/weight_sensitivity.py), and its split planes cost the
+# most of any GEMM (the GELU epilogue pins it to the register schedule).  Measured (profiles/r04/ff1_one_plane/):
+# step 7.99 / 8.01 -> 7.85 / 7.86 ms; parity errors (prior, diff) B=4 vs the reference fixture 0 / 1.2e-5, B=32
+# 0 / 3.4e-7, 512 x 4096 1.9e-7 / 3.3e-5, alignment exact in all three.  MTTS_PARITY_FF1_SPLIT=1: split it too.
+_FF1_SPLIT = os.environ.get("MTTS_PARITY_FF1_SPLIT", "0") != "0"
 
 # the parity policy's text-encoder forward: "fp32fwd" (exact-fp32 MFMA: 32-true's arithmetic) or "bf16x6"
 # (three exact bf16 planes per operand, six MFMAs).  bf16x6 measured 8.16 vs 8.05 ms per step and 1-3x the
@@ -130,7 +133,8 @@ def encoder_precision_for_parity() -> str:
 @contextlib.contextmanager
 def parity_policy(on: bool = True):
     """bf16-parity inside a bf16 autocast region (the Trainer's "bf16-parity" precision): split weight
-    planes for every forward GEMM and the text encoder's forward on the exact-fp32 MFMA
+    planes for every forward GEMM but the decoder FeedForward's GELU up-projection (_FF1_SPLIT) and the text
+    encoder's forward on the exact-fp32 MFMA
     (precise_forward("fp32"); its backward stays bf16)."""
     t1 = _WSPLIT_CV.set(True if on else None)
     t2 = _ENC_PREC.set(_PARITY_ENC if on else "bf16")

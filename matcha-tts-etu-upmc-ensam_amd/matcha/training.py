@@ -179,7 +179,8 @@ class TrainConfig:
     bucket_seams: bool = True
     seam_bucket_mb: float = 64.0
     # "32-true" (reference), "bf16-mixed" (autocast), or "bf16-parity": bf16-mixed with split bf16 weight
-    # planes and the text encoder's forward on the exact-fp32 MFMA -- alignment exact, losses within 1e-4 of 32-true
+    # planes (every forward GEMM but the decoder FF's GELU up-projection) and the text encoder's forward on the
+    # exact-fp32 MFMA -- alignment exact, losses within 1e-4 of 32-true
     # (tests/test_headline_gpu.py; _ops.parity_policy)
     precision: str = "32-true"
     graph: bool = False
