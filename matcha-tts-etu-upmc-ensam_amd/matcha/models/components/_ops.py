@@ -118,6 +118,8 @@ def weight_split_enabled() -> bool:
 # step 7.99 / 8.01 -> 7.85 / 7.86 ms; parity errors (prior, diff) B=4 vs the reference fixture 0 / 1.2e-5, B=32
 # 0 / 3.4e-7, 512 x 4096 1.9e-7 / 3.3e-5, alignment exact in all three.  MTTS_PARITY_FF1_SPLIT=1: split it too.
 _FF1_SPLIT = os.environ.get("MTTS_PARITY_FF1_SPLIT", "0") != "0"
+# MTTS_PARITY_FF2_SPLIT=0: the FF down-projection in one plane too (~3 % share; A/B only)
+_FF2_SPLIT = os.environ.get("MTTS_PARITY_FF2_SPLIT", "1") != "0"
 
 # the parity policy's text-encoder forward: "fp32fwd" (exact-fp32 MFMA: 32-true's arithmetic) or "bf16x6"
 # (three exact bf16 planes per operand, six MFMAs).  bf16x6 measured 8.16 vs 8.05 ms per step and 1-3x the
@@ -1738,7 +1740,7 @@ class _PreLNFeedForwardTM(torch.autograd.Function):
         # measured slower (9.22 vs 8.92 ms); the register-staged schedule hides the GELU epilogue
         n, mean, rstd = _ln_fwd(h2, lnw, lnb, eps, False)
         W1p, K1p = packed(spec_linear((w1,), one_plane=not _FF1_SPLIT), prec)
-        W2p, K2p = packed(spec_linear((w2,)), prec)
+        W2p, K2p = packed(spec_linear((w2,), one_plane=not _FF2_SPLIT), prec)
         ctx.w2t = packed(spec_linear((w2,), dgrad=True), prec)
         ctx.w1t = packed(spec_linear((w1,), dgrad=True), prec)
         b16 = prec == PREC_BF16
