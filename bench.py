@@ -263,9 +263,10 @@ def main():
     ap.add_argument("--tx", type=int, default=120)
     ap.add_argument("--ty", type=int, default=600)
     ap.add_argument("--precision", default="bf16-parity", choices=["32-true", "bf16-mixed", "bf16-parity"],
-                    help="bf16-parity (default): bf16-mixed with split bf16 weight planes and the text encoder's "
-                         "forward in bf16x3 -- alignment exact, losses within 1e-4 of 32-true; bf16-mixed: one "
-                         "weight plane (throughput mode, misses the loss bar); 32-true: the reference's precision")
+                    help="bf16-parity (default): bf16-mixed with split bf16 weight planes (but the decoder FF "
+                         "up-projection) and the text encoder's forward on the exact-fp32 MFMA -- alignment exact, "
+                         "losses within 1e-4 of 32-true; bf16-mixed: one weight plane (throughput mode, misses the "
+                         "loss bar); 32-true: the reference's precision")
     ap.add_argument("--no-graph", action="store_true", help="eager step (DDP) instead of the captured HIP graph")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -395,6 +396,10 @@ def main():
         trainer._fwd_bwd([batch])
         torch.cuda.synchronize()
     gemm_log, OPS.LAUNCH_LOG = OPS.LAUNCH_LOG, None
+    if os.environ.get("MTTS_DUMP_GEMM_LOG"):  # per-launch shapes + eager times (tools/r5/gemm_replay.py input)
+        with open(os.environ["MTTS_DUMP_GEMM_LOG"], "w") as fh:
+            for e0, e1, fl, pr, nby, info in gemm_log:
+                fh.write(json.dumps(dict(info, us=round(e0.elapsed_time(e1) * 1e3, 2), bytes=nby)) + "\n")
     wgrad_log, OPS.WGRAD_LOG = OPS.WGRAD_LOG, None
     attn_log, OPS.ATTN_LOG = OPS.ATTN_LOG, None
     model.zero_grad(set_to_none=False)
@@ -446,15 +451,32 @@ def main():
                  ("split_weights", True, True, "bf16"), ("parity_policy", True, True, OPS.encoder_precision_for_parity()),
                  ("parity_bf16x3_encoder", True, True, "bf16x3"), ("parity_bf16x6_encoder", True, True, "bf16x6"),
                  ("parity_fp32fwd_encoder", True, True, "fp32fwd"), ("parity_fp32_encoder", True, True, "fp32"))
+        from matcha.precision import grad_errors, loss_and_grads, precision_context
+
+        trainer_modes = {"32-true": "32-true", "one_plane": "bf16-mixed", "parity_policy": "bf16-parity"}
         with torch.no_grad():
             for name, amp_on, split, enc in modes:
-                old = OPS.set_weight_split(split)
-                pm.encoder_precision = enc
-                with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp_on):
-                    out = pm(pb["x"], pb["x_lengths"], pb["y"], pb["y_lengths"], t=t_inj, z=z_inj)
-                OPS.set_weight_split(old)
+                if name in trainer_modes:  # the Trainer's own numerics (matcha.precision.precision_context)
+                    with precision_context(trainer_modes[name], pm):
+                        out = pm(pb["x"], pb["x_lengths"], pb["y"], pb["y_lengths"], t=t_inj, z=z_inj)
+                else:
+                    old = OPS.set_weight_split(split)
+                    pm.encoder_precision = enc
+                    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp_on):
+                        out = pm(pb["x"], pb["x_lengths"], pb["y"], pb["y_lengths"], t=t_inj, z=z_inj)
+                    OPS.set_weight_split(old)
+                    pm.encoder_precision = None
                 res[name] = ([float(v) for v in out[:3]], out[3].detach())
-        del pm
+        # gradients + one clip / AdamW update of the benched precision (and the one-plane mode) vs 32-true
+        # (matcha/precision.py)
+        _, g32, _ = loss_and_grads(pm, pb, "32-true", t=t_inj, z=z_inj)
+        params = {n: q.detach() for n, q in pm.named_parameters()}
+        grads_check = {}
+        for name in ("parity_policy", "one_plane"):
+            _, gm, _ = loss_and_grads(pm, pb, trainer_modes[name], t=t_inj, z=z_inj)
+            grads_check[name] = {k: (round(v, 7) if isinstance(v, float) else v)
+                                 for k, v in grad_errors(gm, g32, params).items()}
+        del pm, g32, gm
         l32, a32 = res["32-true"]
 
         def errs(name):
@@ -468,6 +490,11 @@ def main():
             "run_mode": run_mode,
             "modes": {k: errs(k) for k in ("one_plane", "split_weights", "parity_policy", "parity_bf16x3_encoder",
                                            "parity_bf16x6_encoder", "parity_fp32fwd_encoder", "parity_fp32_encoder")},
+            "grads": grads_check,
+            "grads_note": "fwd + bwd of the same batch (eval mode) in each precision: gradient vs 32-true's "
+                          "(global and per-tensor relative L2 error, the global norm's relative error) and one "
+                          "clip(1.0) + AdamW(1e-4) update from zero moments (train.py:85 32-true is the reference "
+                          "precision; the bf16 modes' backward runs in bf16)",
             "losses": ["dur", "prior", "diff"],
             "bar": "alignment bit-exact (agreement 1.0), mel / flow-matching loss within 1e-4 relative (north star)",
             "note": "bf16 modes vs 32-true (= the oracle at this batch) with the parity tests' recipe weights and "

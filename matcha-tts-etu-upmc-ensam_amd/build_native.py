@@ -2,7 +2,7 @@
 
     python build_native.py [--force] [-j N]
 
-Incremental: an object is rebuilt when its source or any header under csrc/ or ../include is newer.
+Incremental: an object is rebuilt when its source or a project header it includes (transitively) is newer.
 The .so is git-ignored but travels to the GPU box with the gpurun snapshot.
 """
 from __future__ import annotations
@@ -55,14 +55,29 @@ def sources() -> list[Path]:
     return sorted([p for p in CSRC.iterdir() if p.suffix in (".hip", ".cpp")])
 
 
-def _newest_header() -> float:
-    hs = list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h"))
-    return max((h.stat().st_mtime for h in hs), default=0.0)
+def _deps(src: Path, seen: set | None = None) -> set:
+    """The project headers `src` includes, transitively (#include "..." found in csrc/ or include/)."""
+    seen = set() if seen is None else seen
+    for line in src.read_text(errors="ignore").splitlines():
+        line = line.strip()
+        if line.startswith("#include \""):
+            name = line.split('"')[1]
+            for d in (CSRC, INCLUDE):
+                h = d / name
+                if h.exists() and h not in seen:
+                    seen.add(h)
+                    _deps(h, seen)
+                    break
+    return seen
+
+
+def _newest_header(src: Path) -> float:
+    return max((h.stat().st_mtime for h in _deps(src)), default=0.0)
 
 
 def _compile(src: Path, force: bool) -> Path:
     obj = OBJ / (src.name + ".o")
-    if not force and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _newest_header()):
+    if not force and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _newest_header(src)):
         return obj
     lang = ["-x", "hip"] if src.suffix == ".hip" else ["-x", "hip"]
     cmd = [_hipcc(), *COMMON, *EXTRA.get(src.name, []), *os.environ.get("MTTS_EXTRA_HIPCC_FLAGS", "").split(),

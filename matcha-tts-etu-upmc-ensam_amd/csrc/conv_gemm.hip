@@ -33,6 +33,7 @@
 #include <cstdint>
 
 #include "gemm_epilogue.h"
+#include "conv_gemm_pk.h"
 #include "mtts_common.h"
 #include "mtts_decoder.h"
 
@@ -1163,6 +1164,7 @@ struct GemmPlan {
 static GemmPlan plan_gemm(const mtts_conv_gemm_args &p, bool bf16, int cfg, int splits) {
     const int M = p.nb * p.To;
     if (cfg < 0) cfg = pick_cfg(p, M, bf16);
+    if (cfg >= MTTS_GEMM_PK) return {cfg, 1, mtts::conv_gemm_pk_workspace_bytes(cfg - MTTS_GEMM_PK, p, !bf16)};
     splits = pick_splits(p, M, cfg, splits, bf16);
     size_t ws = 0;
     if (cfg >= MTTS_GEMM_GLDS) {
@@ -1198,12 +1200,18 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
                        ((p.flags & MTTS_GEMM_F_W_SPLIT) && !(p.flags & MTTS_GEMM_F_A_BF16)),
                    "conv_gemm: a split A needs split weight planes and an fp32 A");
     const bool glds_id = cfg >= MTTS_GEMM_GLDS && cfg < MTTS_GEMM_GLDS + mtts::conv_gemm_glds_num_cfgs();
-    MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || glds_id, "conv_gemm: bad tile config");
+    const bool pk_id = cfg >= MTTS_GEMM_PK && cfg < MTTS_GEMM_PK + mtts::conv_gemm_pk_num_cfgs();
+    MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || glds_id || pk_id, "conv_gemm: bad tile config");
     MTTS_CHECK_ARG(splits >= 0, "conv_gemm: bad split count");
     const int M = p.nb * p.To;
     if (M == 0) return MTTS_OK;
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
     const bool bf16 = precision == MTTS_PREC_BF16;
+    if (pk_id) {  // persistent big-tile schedule, explicit id
+        if (!mtts::conv_gemm_pk_applies(cfg - MTTS_GEMM_PK, p, !bf16))
+            return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: persistent schedule needs whole-tap K steps and 16-byte rows");
+        return mtts::conv_gemm_pk_launch(cfg - MTTS_GEMM_PK, p, M, ws, ws_bytes, st, !bf16);
+    }
     if (glds_id && (!bf16 || !mtts::conv_gemm_glds_applies(p)))
         return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: LDS-DMA schedule needs bf16, cin >= 64 and a 0/1 a_scale");
     if (p.flags & MTTS_GEMM_F_SPLIT3) {  // bf16x6: LDS-DMA 64 x 64 (fp32 A split in the kernel)

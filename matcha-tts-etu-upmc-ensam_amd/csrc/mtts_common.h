@@ -59,48 +59,6 @@ __device__ __forceinline__ int tap_off(const P &p, int j) {
     return o;
 }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-
-// d/dx erf-GELU, as torch's GeluBackward (cdf + x * pdf)
-__device__ __forceinline__ float gelu_erf_grad(float x) {
-    const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-    const float pdf = expf(-0.5f * x * x) * 0.39894228040143268f;
-    return cdf + x * pdf;
-}
-
-// erf-GELU / GELU' with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7; 5.2e-7 evaluated in fp32) sharing ONE exponential
-// between erf and the normal pdf: for the bf16-mixed GEMM epilogues (MTTS_GEMM_F_FAST_ACT), where the
-// result is rounded to a bf16 operand anyway; erff (torch's erf to an ulp) made the 1024-wide FFN
-// epilogues VALU-heavy.  The fp32 parity mode keeps erff.
-__device__ __forceinline__ float erf_as_pdf(float z, float &ez2) {  // erf(z), ez2 = exp(-z^2)
-    const float a = fabsf(z);
-    const float t = __frcp_rn(1.f + 0.3275911f * a);
-    ez2 = __expf(-a * a);
-    const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
-    const float r = 1.f - poly * ez2;
-    return copysignf(r, z);
-}
-__device__ __forceinline__ float gelu_fast(float x) {
-    float e;
-    return 0.5f * x * (1.0f + erf_as_pdf(x * 0.70710678118654752f, e));
-}
-__device__ __forceinline__ float gelu_grad_fast(float x) {
-    float e;  // exp(-x^2/2)
-    const float cdf = 0.5f * (1.0f + erf_as_pdf(x * 0.70710678118654752f, e));
-    return cdf + x * e * 0.39894228040143268f;
-}
-
-// GEMM epilogue activation (include/mtts_decoder.h MTTS_ACT_*); aux is read only by the D-variants.
-__device__ __forceinline__ float epi_act(int act, float v, const float *aux, bool fast = false) {
-    switch (act) {
-        case MTTS_ACT_GELU: return fast ? gelu_fast(v) : gelu_erf(v);
-        case MTTS_ACT_DGELU: return v * (fast ? gelu_grad_fast(*aux) : gelu_erf_grad(*aux));
-        case MTTS_ACT_RELU: return fmaxf(v, 0.f);
-        case MTTS_ACT_DRELU: return *aux > 0.f ? v : 0.f;
-        default: return v;
-    }
-}
-
 }  // namespace mtts
 
 struct mtts_conv_gemm_args;

@@ -409,7 +409,9 @@ def _pack_kind(spec: PackSpec, prec: int) -> int:
     """bf16 forward operands: fp32 under precise_forward("fp32"), the split planes when selected
     (set_weight_split, precise_forward("bf16x3")); everything else as prec."""
     if prec == PREC_BF16 and not spec.dgrad:
-        if spec.one_plane and not _PRECISE.get():
+        # one_plane is the parity POLICY's choice (parity_policy()); set_weight_split(True) alone splits
+        # every forward operand, so its error numbers mean what the mode says (ADVICE r4)
+        if spec.one_plane and not _PRECISE.get() and _WSPLIT_CV.get() is not None:
             return prec
         if _fwd_fp32():
             return PREC_FP32
@@ -617,7 +619,10 @@ def _gemm(A, Ti, To, nb, in_stride, offs, cin, Wp, Kp, N_, C, To_full, out_strid
         log.append((e0, e1, 2.0 * M_ * N_ * args.K, prec, nbytes,
                     dict(M=M_, N=N_, K=args.K, cin=cin, ntaps=len(offs), in_stride=in_stride, res=residual is not None,
                          act=act, pre=C_pre is not None, drop=dropout_p > 0, cs=c_scale is not None,
-                         asc=a_scale is not None, cfg=tile_cfg)))
+                         asc=a_scale is not None, cfg=tile_cfg, nb=nb, Ti=Ti, To=To, To_full=To_full,
+                         out_stride=out_stride, out_off=out_off, offs=list(offs), lda=args.lda, ldc=args.ldc,
+                         ldr=ldr, Kp=Kp, prec=prec, flags=int(args.flags), splits=splits, ws=nws,
+                         bias=bias is not None, aux=aux is not None)))
 
 
 # Weight gradients off the critical path: inside side_stream_wgrad() every _wgrad launches on a

@@ -276,6 +276,8 @@ class Trainer:
 
     def _fwd_bwd(self, batches, sync_ctx=None):
         n = len(batches)
+        if n > 1 and self._stash_ok():
+            return self._fwd_bwd_stash(batches)
         # weight gradients on a side stream, overlapping the dgrad chain (components/_ops.py
         # side_stream_wgrad): safe when autograd steals every fresh gradient (graph step, one
         # micro-batch, gradients set to None first); joined before this returns
@@ -296,7 +298,48 @@ class Trainer:
         with OPS.deferred_grad_sums(defer), OPS.side_stream_wgrad(side):
             return self._fwd_bwd_body(batches, sync_ctx)
 
-    def _fwd_bwd_body(self, batches, sync_ctx=None):
+    def _stash_ok(self) -> bool:
+        """accumulate_grad_batches > 1 without data parallelism: every micro-batch can take the fresh-gradient
+        path (batched, deferred weight gradients and sums, side-stream seam flushes) -- its gradients are
+        stashed and summed at the end instead of accumulated per layer.  The DP reducer packs the last
+        micro-batch's gradients as backward produces them, so it keeps the accumulating path."""
+        return (self.dev.type == "cuda" and not self.dp and self.defer_grad_sums
+                and all(p.grad is None for p in self.params))
+
+    def _fwd_bwd_stash(self, batches):
+        """Micro-batch i: forward + (total / n).backward() on fresh gradients under the gradient deferral (the
+        N=1 step's fast path), its gradients stashed; the end sums them with multi-tensor adds in micro-batch
+        order, ((g_1 + g_2) + g_3) ..., the fp32 adds autograd's AccumulateGrad does -- so the result equals
+        the accumulating path's (tests/test_training_gpu.py::test_accumulate_grad_batches_2_vs_torch)."""
+        n = len(batches)
+        self._defer_first = False
+        logged = None
+        stash = []
+        for i, batch in enumerate(batches):
+            with OPS.deferred_grad_sums(True):
+                vals = self._fwd_bwd_body([batch], div=n)
+            logged = vals if logged is None else logged + vals
+            stash.append([p.grad for p in self.params])
+            for p in self.params:
+                p.grad = None
+        acc = list(stash[0])
+        for g in stash[1:]:
+            a_, b_ = [], []
+            for k, gk in enumerate(g):
+                if gk is None:
+                    continue
+                if acc[k] is None:
+                    acc[k] = gk
+                else:
+                    a_.append(acc[k])
+                    b_.append(gk)
+            if a_:
+                torch._foreach_add_(a_, b_)  # in place into micro-batch 1's (fresh, unaliased) gradients
+        for p, gk in zip(self.params, acc):
+            p.grad = gk
+        return logged / n
+
+    def _fwd_bwd_body(self, batches, sync_ctx=None, div=None):
         n = len(batches)
         logged = None
         for i, batch in enumerate(batches):
@@ -321,7 +364,8 @@ class Trainer:
                     # the last micro-batch's backward exchanges the accumulated gradients (and the logged
                     # means) bucket by bucket as backward produces them ("local": pack only, no collective)
                     self.reducer.arm(logged / n, overlap=self._arm is True, comm=self._arm != "local")
-                (total / n if n > 1 else total).backward()
+                d = div if div is not None else n
+                (total / d if d > 1 else total).backward()
         return logged / n if n > 1 else logged
 
     def _clip_and_update(self):

@@ -46,6 +46,15 @@ MODES = {"32-true": (False, False, "bf16"), "bf16-mixed": (True, False, "bf16"),
          "bf16-parity-bf16x3": (True, True, "bf16x3"), "bf16-parity-bf16x6": (True, True, "bf16x6")}
 # bf16x6 is not at the bar: measured B=4 alignment 0.99990 (2 of 437 durations moved), duration loss 4e-4
 PARITY_MODES = ("bf16-parity", "bf16-parity-fp32enc")
+# The at-bar modes' BACKWARD is bf16: their gradients pinned against the reference fixture's
+# per-tensor gradient norms (B=4) and the 32-true step's gradients / AdamW update (B=32, below).  Bounds from
+# the round-5 GPU measurement (profiles/r05/grads/), about 3x the measured value.
+GRAD_NORM_GLOBAL_RTOL = 1e-2
+GRAD_NORM_MEDIAN_RTOL = 1e-2
+GRAD_NORM_MAX_RTOL = 0.1
+B32_GRAD_GLOBAL_RTOL = 5e-2   # ||g - g32|| / ||g32||
+B32_GRAD_NORM_RTOL = 1e-2     # | ||g|| - ||g32|| | / ||g32||
+B32_UPDATE_RTOL = 0.2         # one clip + AdamW step from zero moments (~ lr * sign(g): small entries flip)
 
 
 def run_precision(model, precision, fn):
@@ -55,7 +64,11 @@ def run_precision(model, precision, fn):
     bf16-parity-bf16x3 / -bf16x6 (split weight planes + the encoder forward in bf16x3 / bf16x6: both
     flip alignment cells at B=4, so they are held to the one-plane bounds)."""
     from matcha.models.components import _ops as O
+    from matcha.precision import precision_context
 
+    if precision in ("32-true", "bf16-mixed", "bf16-parity"):  # the Trainer's own precisions, its contexts
+        with precision_context(precision, model):
+            return fn()
     amp, split, enc = MODES[precision]
     old = O.set_weight_split(split)
     model.encoder_precision = enc
@@ -64,7 +77,7 @@ def run_precision(model, precision, fn):
             return fn()
     finally:
         O.set_weight_split(old)
-        model.encoder_precision = "bf16"
+        model.encoder_precision = None
 
 
 def check_bf16(precision, err, agree):
@@ -139,6 +152,18 @@ def test_headline_b4_vs_reference(precision):
         print(f"bf16 alignment agreement {agree:.5f}; rows whose duration moved {(dur16 != dur32).sum()} of "
               f"{int(xl.sum())}; max |logw16 - logw32| {d_logw:.4f}; mu_x rel err {r_mu:.2e}")
         check_bf16(precision, err, agree)
+        # gradients of the same backward against the reference's own (fp32 CPU) per-parameter gradient norms
+        gn = np.array([p.grad.double().norm().item() if p.grad is not None else 0.0 for _, p in model.named_parameters()])
+        ref = GH["h_grad_norms"]
+        big = ref > 1e-3 * ref.max()  # tensors whose gradient is not ~0 (a relative error of ~0 is noise)
+        rel = np.abs(gn - ref)[big] / ref[big]
+        tot = abs(np.sqrt((gn ** 2).sum()) - np.sqrt((ref ** 2).sum())) / np.sqrt((ref ** 2).sum())
+        print(f"{precision}: grad norms vs reference: global {tot:.2e}, per tensor median {np.median(rel):.2e} "
+              f"max {rel.max():.2e} ({int(big.sum())} tensors)")
+        if precision in PARITY_MODES:
+            assert tot <= GRAD_NORM_GLOBAL_RTOL, tot
+            assert np.median(rel) <= GRAD_NORM_MEDIAN_RTOL, np.median(rel)
+            assert rel.max() <= GRAD_NORM_MAX_RTOL, rel.max()
 
 
 _B32 = {}
@@ -184,3 +209,26 @@ def test_bench_batch_b32_vs_oracle(precision):
     else:
         check_bf16(precision, err, agree)
     assert all(p.grad is None or torch.isfinite(p.grad).all() for p in model.parameters())
+
+
+@pytest.mark.parametrize("precision", PARITY_MODES[:1] + ("bf16-mixed",))
+def test_bench_batch_b32_grads_vs_32true(precision):
+    """The benched step's product is a parameter UPDATE: its gradients (bf16 backward) and one clip + AdamW step
+    against the 32-true step's on the bench batch (recipe weights 43, eval mode, same t / z).  32-true's own
+    gradients are pinned element-wise to the oracle (test_model_gpu.py::test_matcha_gradients_elementwise_vs_oracle)."""
+    from matcha.precision import grad_errors, loss_and_grads
+
+    o = _oracle_b32()
+    model = _product(43)
+    b = {k: v.to(DEV) for k, v in o["batch"].items()}
+    t, z = o["t"].to(DEV), o["z"].to(DEV)
+    _, g32, _ = loss_and_grads(model, b, "32-true", t=t, z=z)
+    _, g16, _ = loss_and_grads(model, b, precision, t=t, z=z)
+    params = {n: p.detach() for n, p in model.named_parameters()}
+    e = grad_errors(g16, g32, params)
+    print(f"B=32 {precision} gradients vs 32-true: {e}")
+    if precision in PARITY_MODES:
+        assert e["global_rel_err"] <= B32_GRAD_GLOBAL_RTOL, e
+        assert e["norm_rel_err"] <= B32_GRAD_NORM_RTOL, e
+        assert e["update_rel_err"] <= B32_UPDATE_RTOL, e
+    assert e["global_rel_err"] < 0.5, e  # one plane: measured, finite and in range
