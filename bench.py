@@ -276,6 +276,9 @@ def main():
                     help="skip the same-run 32-true line and the reference step shape (B=16 x accumulate 2)")
     ap.add_argument("--no-graph-profile", action="store_true",
                     help="skip the rocprofv3 graph-replay leg (roofline from the eager HIP-event pass only)")
+    ap.add_argument("--accumulate", type=int, default=1,
+                    help="N > 1: the step is N micro-batches of batch/N with gradient accumulation (the reference's "
+                         "train.py:63,88 shape is --batch 32 --accumulate 2); profiling aid, not the headline")
     ap.add_argument("--bucketed", type=int, default=0,
                     help="N > 0: cycle N length-bucketed batches (LengthBucketBatchSampler + collate with padding "
                          "quanta) from a synthetic corpus with Ty in [Ty/4, Ty], Tx ~ Ty * tx/ty; --tx/--ty are "
@@ -322,7 +325,8 @@ def main():
     model = MatchaTTS(n_vocab=150, out_channels=80, hidden_channels=192).to(dev)
     model.train()
     graph = not args.no_graph
-    trainer = Trainer(model, TrainConfig(precision=args.precision, graph=graph, graph_cache=max(4, args.bucketed)))
+    trainer = Trainer(model, TrainConfig(precision=args.precision, graph=graph, graph_cache=max(4, args.bucketed),
+                                         accumulate_grad_batches=args.accumulate))
     B, Tx, Ty = args.batch, args.tx, args.ty
     if args.bucketed > 0:
         batches = _bucketed_batches(B, Tx, Ty, args.bucketed, rank, world, dev)
@@ -331,19 +335,27 @@ def main():
     else:
         batch = synthetic_batch(B, Tx, Ty, seed=1000 + rank, device=dev)
         batches = [batch]
+    acc = args.accumulate
+    if acc > 1:  # micro-batches of B / acc (the same synthetic generator, one seed each)
+        if args.bucketed or B % acc:
+            raise SystemExit("bench.py: --accumulate needs --batch divisible by it and no --bucketed")
+        micro = [synthetic_batch(B // acc, Tx, Ty, seed=2000 + i, device=dev) for i in range(acc)]
 
     mas_events: list = []
     real_mp = MA.maximum_path
 
+    def step_batches(i):
+        return micro if acc > 1 else [batches[i % len(batches)]]
+
     for i in range(args.warmup):
-        trainer.step([batches[i % len(batches)]])
+        trainer.step(step_batches(i))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        trainer.step([batches[i % len(batches)]])
+        trainer.step(step_batches(i))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -185,9 +185,10 @@ class BaseConditionalFlowMatching(nn.Module, ABC):
         loss, _, phi_t = self.compute_loss_and_prior(x1, mask, mu, None, t=t, z=z)
         return loss, phi_t
 
-    def compute_loss_and_prior(self, x1, mask, mu, prior_mu, *, t=None, z=None):
+    def compute_loss_and_prior(self, x1, mask, mu, prior_mu, *, t=None, z=None, segments=1):
         """compute_loss plus, when prior_mu is given, MatchaTTS's prior loss on (x1, prior_mu) -- both
-        in one fused pass over the tensors (csrc/losses.hip).  Returns (diff_loss, prior_loss, phi_t)."""
+        in one fused pass over the tensors (csrc/losses.hip).  Returns (diff_loss, prior_loss, phi_t).
+        segments = n > 1: the losses of each of n equal micro-batches stacked along dim 0 ([n] tensors)."""
         b = mu.shape[0]
         if t is None:
             t = torch.rand([b, 1, 1], device=mu.device, dtype=mu.dtype)
@@ -199,6 +200,14 @@ class BaseConditionalFlowMatching(nn.Module, ABC):
         phi_t = packed[..., : x1.shape[1]].transpose(1, 2)
         u_pred = self.estimator.forward_tm_packed(packed, mask[:, 0], t.reshape(b))
         # sum((u_pred - u)^2) / (sum(mask) * n_feats) and the prior loss, fused (flow_matching.py:145-149)
+        if segments > 1:
+            bs = b // segments
+            sl = [slice(i * bs, (i + 1) * bs) for i in range(segments)]
+            parts = [fused_losses(u_pred[q], prior_mu[q] if prior_mu is not None else None, x1[q], z[q], mask[q], s)
+                     for q in sl]
+            loss = torch.stack([lp[0] for lp in parts])
+            prior = torch.stack([lp[1] for lp in parts]) if prior_mu is not None else None
+            return loss, prior, phi_t
         loss, prior = fused_losses(u_pred, prior_mu, x1, z, mask, s)
         return loss, prior, phi_t
 

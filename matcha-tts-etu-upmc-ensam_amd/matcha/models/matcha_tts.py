@@ -119,9 +119,13 @@ class MatchaTTS(BaseLightningClass):
             mu_square = torch.sum(factor * (mu_x ** 2), 1).unsqueeze(-1)
             return y_square - y_mu_double + mu_square + const
 
-    def forward(self, x, x_lengths, y, y_lengths, out_size=None, cond=None, durations=None, *, t=None, z=None):
+    def forward(self, x, x_lengths, y, y_lengths, out_size=None, cond=None, durations=None, *, t=None, z=None,
+                segments=1):
         """Returns (dur_loss, prior_loss, diff_loss, attn) -- matcha_tts.py:247-325.  ``t``/``z``
-        (keyword-only) inject the CFM randomness for parity tests."""
+        (keyword-only) inject the CFM randomness for parity tests.  ``segments`` = n > 1 (keyword-only, the
+        Trainer's merged micro-batches): the batch is n equal micro-batches stacked along dim 0 and each loss
+        is returned per micro-batch (a [n] tensor, every one normalised by its own micro-batch's lengths, as n
+        separate forwards would) -- every other op of the model is per utterance."""
         # the text encoder runs on the same HIP GEMM/attention kernels as the decoder and follows the
         # caller's precision (bf16 MFMA operands inside a bf16 autocast region) unless encoder_precision says
         # otherwise: "bf16x3" / "fp32" take its activations' bf16 rounding -- what is left of the bf16 prior-loss
@@ -168,7 +172,14 @@ class MatchaTTS(BaseLightningClass):
             runs = (col_row, row_start, lens)
         # logw_ = log(1e-8 + dur) * x_mask ; duration_loss(logw, logw_, x_lengths)  (:287-288, model.py:117-135)
         # as one HIP launch each way
-        dur_loss = O.duration_loss_fused(logw, dur, x_lengths)
+        if segments > 1:
+            if x.shape[0] % segments:
+                raise ValueError(f"segments={segments} does not divide the batch {x.shape[0]}")
+            bs = x.shape[0] // segments
+            dur_loss = torch.stack([O.duration_loss_fused(logw[i * bs:(i + 1) * bs], dur[i * bs:(i + 1) * bs],
+                                                          x_lengths[i * bs:(i + 1) * bs]) for i in range(segments)])
+        else:
+            dur_loss = O.duration_loss_fused(logw, dur, x_lengths)
         if out_size is not None:  # :290-312 (host-side random crop, as the reference)
             max_offset = (y_lengths - out_size).clamp(0)
             offset_ranges = list(zip([0] * max_offset.shape[0], max_offset.cpu().numpy()))
@@ -192,7 +203,8 @@ class MatchaTTS(BaseLightningClass):
             mu_y = torch.matmul(attn.squeeze(1).transpose(1, 2), mu_x.transpose(1, 2)).transpose(1, 2)
         # CFM loss (:317) and prior loss (:319-323) in one fused HIP pass (components/flow_matching.py)
         diff_loss, prior_loss, _ = self.decoder.compute_loss_and_prior(y, y_mask, mu_y,
-                                                                       mu_y if self.prior_loss else None, t=t, z=z)
+                                                                       mu_y if self.prior_loss else None, t=t, z=z,
+                                                                       segments=segments)
         if not self.prior_loss:
             prior_loss = 0
         return dur_loss, prior_loss, diff_loss, attn

@@ -200,6 +200,12 @@ class TrainConfig:
     # run the data-parallel exchange even at world size 1 (a world-size-1 process group must exist): the
     # bucketed RCCL path's cost on one GPU (bench.py extra_configs.dp_forced_n1); MTTS_FORCE_DP=1 does the same
     force_dp: bool = False
+    # accumulate_grad_batches > 1 with micro-batches of one padded shape: ONE forward / backward of the stacked
+    # micro-batches, each loss normalised per micro-batch (MatchaTTS.forward(segments=n)) -- the gradient of
+    # (1/n) sum_i L_i that accumulation computes; every op but the losses is per utterance (GroupNorm / LayerNorm
+    # statistics per utterance and padded length), so only the weight-gradient reductions' rounding differs.
+    # Micro-batches of different padded shapes take the stashed fresh-gradient path (_fwd_bwd_stash)
+    merge_micro_batches: bool = True
 
 
 class Trainer:
@@ -276,7 +282,10 @@ class Trainer:
 
     def _fwd_bwd(self, batches, sync_ctx=None):
         n = len(batches)
-        if n > 1 and self._stash_ok():
+        if n > 1 and self._merge_ok(batches):
+            batches = [self._merge(batches)]
+            n = 1
+        elif n > 1 and self._stash_ok():
             return self._fwd_bwd_stash(batches)
         # weight gradients on a side stream, overlapping the dgrad chain (components/_ops.py
         # side_stream_wgrad): safe when autograd steals every fresh gradient (graph step, one
@@ -297,6 +306,20 @@ class Trainer:
                              and (self.cfg.graph or self.dp_mode != "ddp"))
         with OPS.deferred_grad_sums(defer), OPS.side_stream_wgrad(side):
             return self._fwd_bwd_body(batches, sync_ctx)
+
+    def _merge_ok(self, batches) -> bool:
+        """TrainConfig.merge_micro_batches and every micro-batch the same padded shapes (CUDA MatchaTTS)."""
+        if not self.cfg.merge_micro_batches or self.dev.type != "cuda" or not isinstance(self.model, MatchaTTS):
+            return False
+        keys = set(batches[0])
+        return all(set(b) == keys and all(b[k].shape == batches[0][k].shape and b[k].dtype == batches[0][k].dtype
+                                          for k in keys) for b in batches[1:]) and "_segments" not in keys
+
+    @staticmethod
+    def _merge(batches):
+        out = {k: torch.cat([b[k] for b in batches], 0) for k in batches[0]}
+        out["_segments"] = len(batches)
+        return out
 
     def _stash_ok(self) -> bool:
         """accumulate_grad_batches > 1 without data parallelism: every micro-batch can take the fresh-gradient
@@ -348,12 +371,20 @@ class Trainer:
                 else contextlib.nullcontext()
             with ctx, first:
                 inject = {k: batch[k] for k in ("t", "z") if k in batch}  # parity tests' CFM randomness
+                seg = batch.get("_segments", 1)
+                if seg > 1:  # merged micro-batches: per-micro-batch losses ([seg] tensors)
+                    inject["segments"] = seg
                 with self._autocast():
                     dur, prior, diff, _ = self.wrapped(x=batch["x"], x_lengths=batch["x_lengths"],
                                                        y=batch["y"], y_lengths=batch["y_lengths"], **inject)
                 # total = dur + prior + diff and the logged [dur, prior, diff, total] in one launch (device
                 # tensors; the CPU data-parallel tests drive this loop with a CPU stand-in model)
-                if dur.device.type == "cuda":
+                if seg > 1:  # the mean over micro-batches of each one's total / logged vector
+                    parts = [OPS.loss_sum(dur[j], prior[j] if torch.is_tensor(prior) else 0, diff[j])
+                             for j in range(seg)]
+                    total = sum(tp[0] for tp in parts) / seg
+                    vals = sum(tp[1] for tp in parts) / seg
+                elif dur.device.type == "cuda":
                     total, vals = OPS.loss_sum(dur, prior, diff)
                 else:
                     total = dur + prior + diff

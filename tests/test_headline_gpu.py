@@ -48,13 +48,15 @@ MODES = {"32-true": (False, False, "bf16"), "bf16-mixed": (True, False, "bf16"),
 PARITY_MODES = ("bf16-parity", "bf16-parity-fp32enc")
 # The at-bar modes' BACKWARD is bf16: their gradients pinned against the reference fixture's
 # per-tensor gradient norms (B=4) and the 32-true step's gradients / AdamW update (B=32, below).  Bounds from
-# the round-5 GPU measurement (profiles/r05/grads/), about 3x the measured value.
-GRAD_NORM_GLOBAL_RTOL = 1e-2
-GRAD_NORM_MEDIAN_RTOL = 1e-2
-GRAD_NORM_MAX_RTOL = 0.1
-B32_GRAD_GLOBAL_RTOL = 5e-2   # ||g - g32|| / ||g32||
-B32_GRAD_NORM_RTOL = 1e-2     # | ||g|| - ||g32|| | / ||g32||
-B32_UPDATE_RTOL = 0.2         # one clip + AdamW step from zero moments (~ lr * sign(g): small entries flip)
+# the round-5 GPU measurement (profiles/r05/grads/), about 3x the measured value.  bf16-parity measured: B=4
+# global norm 3.3e-4, per-tensor norms median 4.3e-4 / max 1.9e-2; B=32 vs 32-true: ||g - g32|| / ||g32|| 3.0e-3,
+# global norm 4.3e-5, update 7.6e-2 (the first Adam step is ~lr * sign(g): near-zero entries flip; bf16-mixed 0.107)
+GRAD_NORM_GLOBAL_RTOL = 1e-3
+GRAD_NORM_MEDIAN_RTOL = 1.5e-3
+GRAD_NORM_MAX_RTOL = 6e-2
+B32_GRAD_GLOBAL_RTOL = 1e-2   # ||g - g32|| / ||g32||
+B32_GRAD_NORM_RTOL = 2e-4     # | ||g|| - ||g32|| | / ||g32||
+B32_UPDATE_RTOL = 0.15        # one clip + AdamW step from zero moments
 
 
 def run_precision(model, precision, fn):

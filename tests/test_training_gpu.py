@@ -251,9 +251,11 @@ def test_accumulate_grad_batches_2_vs_torch(graph):
     z = torch.randn(4, 80, 96, device=DEV)
     _inject(m_tr, t, z)
     _inject(m_ref, t, z)
-    tr = Trainer(m_tr, TrainConfig(accumulate_grad_batches=2, graph=graph))
-    # the Trainer's first micro-batch runs its weight gradients queued and batched (the batched split
-    # plan); the plain-autograd reference takes the same plan, so the gradients stay bitwise comparable
+    # merge_micro_batches=False: each micro-batch on fresh gradients (stashed, summed at the end) -- the
+    # separate micro-batches of the reference, bitwise
+    tr = Trainer(m_tr, TrainConfig(accumulate_grad_batches=2, graph=graph, merge_micro_batches=False))
+    # the Trainer's micro-batches run their weight gradients queued and batched (the batched split plan); the
+    # plain-autograd reference takes the same plan, so the gradients stay bitwise comparable
     from matcha import _native as N
 
     N.lib().mtts_wgrad_plan_mode(1)
@@ -261,6 +263,50 @@ def test_accumulate_grad_batches_2_vs_torch(graph):
         _accumulate2_steps(tr, m_tr, m_ref, b1, b2, graph)
     finally:
         N.lib().mtts_wgrad_plan_mode(0)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_accumulate_merged_micro_batches_vs_torch(graph):
+    """TrainConfig.merge_micro_batches (the default): two micro-batches of one padded shape run as ONE forward /
+    backward with the losses normalised per micro-batch (MatchaTTS.forward(segments=2)).  Same mathematics as the
+    reference's accumulation; the per-utterance forward is unchanged and only the weight-gradient reductions
+    (over 8 utterances at once instead of 4 + 4) round differently: logged losses within 1e-6, parameters after
+    1 and 3 steps within 1e-6 relative, except pure-noise gradients (Adam moves them by up to ~lr per step)."""
+    from matcha.training import TrainConfig, Trainer, synthetic_batch
+
+    b1 = synthetic_batch(4, 24, 96, seed=1, device=DEV)
+    b2 = synthetic_batch(4, 24, 96, seed=2, device=DEV)
+    m_tr, m_ref = _model(7), _model(7)
+    m_ref.load_state_dict(m_tr.state_dict())
+    m_tr.eval()
+    m_ref.eval()
+    t = torch.rand(4, 1, 1, device=DEV)
+    z = torch.randn(4, 80, 96, device=DEV)
+    _inject(m_tr, torch.cat([t, t]), torch.cat([z, z]))  # the merged batch: both micro-batches' t / z
+    _inject(m_ref, t, z)
+    tr = Trainer(m_tr, TrainConfig(accumulate_grad_batches=2, graph=graph))
+    assert tr._merge_ok([b1, b2])
+    params = [p for p in m_ref.parameters() if p.requires_grad]
+    opt = torch.optim.AdamW(params, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-6)
+    for step in range(3):
+        logged = tr.step([b1, b2]).clone()
+        tot = []
+        for b in (b1, b2):
+            dur, prior, diff, _ = m_ref(**b)
+            tot.append((dur + prior + diff).detach())
+            ((dur + prior + diff) / 2).backward()
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(logged[3], (tot[0] + tot[1]) / 2, rtol=2e-6, atol=0.0)
+        worst = []
+        for (n, a), (_, r) in zip(m_tr.named_parameters(), m_ref.named_parameters()):
+            d = (a.detach() - r.detach()).abs()
+            ok = d <= 1e-6 * r.detach().abs() + 1e-9
+            worst.append((d.max().item(), n, int((~ok).sum())))
+            assert ok.all() or d.max().item() <= (step + 1) * 2e-4 * 1.01, (step, n, d.max().item())
+        print("merged", "graph" if graph else "eager", "step", step, "largest parameter differences:", sorted(worst)[-3:])
 
 
 def _accumulate2_steps(tr, m_tr, m_ref, b1, b2, graph):
