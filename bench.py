@@ -113,19 +113,24 @@ def cpu_baseline(B_cpu: int, Tx: int, Ty: int, budget_s: float) -> dict:
 
 
 def mas_chain_bound(Tx: int, Ty: int, mas_ms: float, clock_ghz: float = 2.1) -> dict:
-    """The DP is a Ty-long dependency chain per utterance (one wave each at this Tx, utterances in parallel on
-    their own CUs): per column a lane updates its K = ceil(Tx / 64) rows -- in the interior chunks (round 4:
-    every valid row strictly below the diagonal and inside the band) about 5 VALU per row (compare, select,
-    add, backpointer shift / or), at the band edges about 9 (plus the diagonal and band tests) -- plus one
-    DPP neighbour exchange, each waiting ~8 cycles for its predecessor at one wave per SIMD.  The estimate
-    uses the edge count; measured / estimate near or below 1 means the kernel runs at its chain bound, not at
-    HBM speed (which the 12 B/cell roofline would ask for)."""
-    K = 1
-    while 64 * K < Tx:
-        K *= 2
-    cyc_per_col = (9 * K + 2) * 8
-    est_ms = Ty * cyc_per_col / (clock_ghz * 1e9) * 1e3
-    return {"columns": Ty, "rows_per_lane": K, "model_cycles_per_column": cyc_per_col,
+    """Lower bound of the DP kernel that RUNS at this Tx (csrc/mas.hip ws_layout; VERDICT r4 #9: the round-4
+    model described the one-wave kernel at every Tx, and the multi-wave kernel "beat" it).
+    Tx <= 256 -- one wave per utterance (mas_dp_kernel): a Ty-long dependency chain; per column a lane updates
+    its K = 1, 2, 4 rows (Tx <= 64, 128, 256) at about 9 VALU per row on the band edges (5 in interior chunks)
+    plus a DPP neighbour exchange, each waiting ~8 cycles for its predecessor at one wave per SIMD.
+    Tx > 256 -- eight waves per utterance (mas_dp_mw_kernel), KL = 1, 2, 4, 8 rows per lane (Tx <= 512 ... 4096),
+    pipelined one 32-column chunk apart: per column two waves per SIMD each issue ~(5 KL + 4) instructions
+    (interior cells + exchange / bookkeeping) at ~4 cycles each -- an ISSUE bound, ignoring the per-chunk LDS
+    barrier -- over Ty + 7 * 32 columns (the pipeline fill).  measured / estimate >= 1 by construction; its
+    size says how far the kernel is from the issue bound (the barrier waits)."""
+    if Tx <= 256:
+        K = 1 if Tx <= 64 else 2 if Tx <= 128 else 4
+        cyc_per_col, cols, shape = (9 * K + 2) * 8, Ty, {"waves": 1, "rows_per_lane": K}
+    else:
+        KL = 1 if Tx <= 512 else 2 if Tx <= 1024 else 4 if Tx <= 2048 else 8
+        cyc_per_col, cols, shape = 2 * (5 * KL + 4) * 4, Ty + 7 * 32, {"waves": 8, "rows_per_lane": KL}
+    est_ms = cols * cyc_per_col / (clock_ghz * 1e9) * 1e3
+    return {"columns": Ty, "kernel_shape": shape, "model_cycles_per_column": cyc_per_col,
             "estimate_ms": round(est_ms, 4), "measured_ns_per_column": round(mas_ms * 1e6 / Ty, 1),
             "measured_over_estimate": round(mas_ms / est_ms, 2), "clock_ghz_assumed": clock_ghz}
 
@@ -594,6 +599,8 @@ def main():
             return None, None
         return json.loads(found[-1].read_text())["traffic_bytes_per_launch"], str(found[-1].relative_to(ROOT))
 
+    mas_traffic = traffic_of("mas")  # tools/r5/pmc_mas.sh: maximum_path on the bench batch's lattice
+
     def roofline_of(log, fam, kernel, note):
         """Roofline line of one kernel family: algorithmic FLOPs / bytes per step from the eager launch log
         (the same launches the graph replays), time from the graph-replay profile when it ran (else the
@@ -691,7 +698,9 @@ def main():
             "roofline_mas": {"kernel": "mas_transpose_kernel + mas_dp_kernel + mas_expand_kernel (maximum_path)",
                              "bound": "hbm",
                              "achieved": round(mas_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(mas_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                             "frac": round(mas_gbs / HBM_PEAK_GBS, 4), "traffic": mas_traffic[0],
+                             "traffic_source": mas_traffic[1],
+                             "traffic_unit": "HBM bytes per maximum_path call (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                              "algorithmic_bytes_per_launch": 12 * cells,
                              "chain_bound": mas_chain_bound(Tx, Ty, mas_ms),
                              "note": "12 B/cell (value+mask read, path write); the API premasks + transposes the "

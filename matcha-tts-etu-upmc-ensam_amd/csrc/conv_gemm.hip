@@ -1176,6 +1176,43 @@ static GemmPlan plan_gemm(const mtts_conv_gemm_args &p, bool bf16, int cfg, int 
     return {cfg, splits, ws};
 }
 
+// The schedule a call runs: the operand-driven rewrites of an explicit or heuristic config (three weight planes,
+// split weight planes, bf16 A, split A).  Shared by the launch and mtts_conv_gemm_workspace_size, so the size
+// query plans the schedule -- and the split count -- that will run.  *rc: MTTS_OK or the error.
+static int resolve_cfg(const mtts_conv_gemm_args &p, bool bf16, int cfg, int M, int *rc) {
+    *rc = MTTS_OK;
+    auto err = [&](int code, const char *msg) {
+        *rc = mtts::fail(code, msg);
+        return cfg;
+    };
+    if (p.flags & MTTS_GEMM_F_SPLIT3) {  // bf16x6: LDS-DMA 64 x 64 (fp32 A split in the kernel)
+        if (!bf16 || (p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_GEMM_F_W_SPLIT | MTTS_GEMM_F_A_SPLIT)))
+            return err(MTTS_ERR_INVALID_ARG, "conv_gemm: three weight planes need bf16 precision and an fp32 A");
+        if (!mtts::conv_gemm_glds_applies(p))
+            return err(MTTS_ERR_UNSUPPORTED, "conv_gemm: three weight planes need the LDS-DMA schedules (cin >= 64)");
+        if (cfg < 0) cfg = MTTS_GEMM_GLDS + 12;
+        if (cfg < MTTS_GEMM_GLDS) return err(MTTS_ERR_UNSUPPORTED, "conv_gemm: three weight planes need an LDS-DMA schedule");
+    }
+    static const bool ws_pick = [] { const char *e = getenv("MTTS_GEMM_WS_PICK"); return !(e && e[0] == '0'); }();
+    if (cfg < 0 && bf16 && ws_pick && (p.flags & MTTS_GEMM_F_W_SPLIT) && !(p.flags & MTTS_GEMM_F_A_SPLIT))
+        cfg = pick_cfg_ws(p, M);
+    if (p.flags & MTTS_GEMM_F_A_BF16) {  // bf16 A operands exist only in the LDS-DMA kernels
+        if (!bf16 || !mtts::conv_gemm_glds_applies(p))
+            return err(MTTS_ERR_UNSUPPORTED,
+                              "conv_gemm: a bf16 A needs bf16 precision, cin >= 64, cin / lda % 8 == 0, 0/1 a_scale");
+        if (cfg < 0) {
+            cfg = pick_cfg_a16(p, M);
+        } else if (cfg < MTTS_GEMM_GLDS) {
+            return err(MTTS_ERR_UNSUPPORTED, "conv_gemm: a bf16 A needs an LDS-DMA schedule");
+        }
+    }
+    if (p.flags & MTTS_GEMM_F_A_SPLIT) {  // bf16x3: register-staged schedules only (the staging pass splits A)
+        if (cfg >= MTTS_GEMM_GLDS) return err(MTTS_ERR_UNSUPPORTED, "conv_gemm: a split A needs a register schedule");
+        if (cfg < 0) cfg = p.K >= 384 ? 12 : 7;
+    }
+    return cfg;
+}
+
 static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, int cfg, int splits, void *ws,
                           size_t ws_bytes, void *hip_stream) {
     MTTS_CHECK_ARG(args != nullptr, "conv_gemm: args is null");
@@ -1214,31 +1251,8 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     }
     if (glds_id && (!bf16 || !mtts::conv_gemm_glds_applies(p)))
         return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: LDS-DMA schedule needs bf16, cin >= 64 and a 0/1 a_scale");
-    if (p.flags & MTTS_GEMM_F_SPLIT3) {  // bf16x6: LDS-DMA 64 x 64 (fp32 A split in the kernel)
-        if (!bf16 || (p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_GEMM_F_W_SPLIT | MTTS_GEMM_F_A_SPLIT)))
-            return mtts::fail(MTTS_ERR_INVALID_ARG, "conv_gemm: three weight planes need bf16 precision and an fp32 A");
-        if (!mtts::conv_gemm_glds_applies(p))
-            return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: three weight planes need the LDS-DMA schedules (cin >= 64)");
-        if (cfg < 0) cfg = MTTS_GEMM_GLDS + 12;
-        if (cfg < MTTS_GEMM_GLDS) return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: three weight planes need an LDS-DMA schedule");
-    }
-    static const bool ws_pick = [] { const char *e = getenv("MTTS_GEMM_WS_PICK"); return !(e && e[0] == '0'); }();
-    if (cfg < 0 && bf16 && ws_pick && (p.flags & MTTS_GEMM_F_W_SPLIT) && !(p.flags & MTTS_GEMM_F_A_SPLIT))
-        cfg = pick_cfg_ws(p, M);
-    if (p.flags & MTTS_GEMM_F_A_BF16) {  // bf16 A operands exist only in the LDS-DMA kernels
-        if (!bf16 || !mtts::conv_gemm_glds_applies(p))
-            return mtts::fail(MTTS_ERR_UNSUPPORTED,
-                              "conv_gemm: a bf16 A needs bf16 precision, cin >= 64, cin / lda % 8 == 0, 0/1 a_scale");
-        if (cfg < 0) {
-            cfg = pick_cfg_a16(p, M);
-        } else if (cfg < MTTS_GEMM_GLDS) {
-            return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: a bf16 A needs an LDS-DMA schedule");
-        }
-    }
-    if (p.flags & MTTS_GEMM_F_A_SPLIT) {  // bf16x3: register-staged schedules only (the staging pass splits A)
-        if (cfg >= MTTS_GEMM_GLDS) return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: a split A needs a register schedule");
-        if (cfg < 0) cfg = p.K >= 384 ? 12 : 7;
-    }
+    cfg = resolve_cfg(p, bf16, cfg, M, &rc);
+    if (rc) return rc;
     const GemmPlan pl = plan_gemm(p, bf16, cfg, splits);
     if (pl.cfg >= MTTS_GEMM_GLDS) {
         int s = pl.splits;
@@ -1267,7 +1281,11 @@ extern "C" int mtts_conv_gemm_tile(const mtts_conv_gemm_args *args, int32_t prec
 extern "C" size_t mtts_conv_gemm_workspace_size(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg,
                                                 int32_t splits) {
     if (!args || args->nb * args->To == 0) return 0;
-    return plan_gemm(*args, precision == MTTS_PREC_BF16, tile_cfg, splits).ws;
+    const bool bf16 = precision == MTTS_PREC_BF16;
+    if (tile_cfg >= MTTS_GEMM_PK) return plan_gemm(*args, bf16, tile_cfg, splits).ws;
+    int rc = MTTS_OK;
+    const int cfg = resolve_cfg(*args, bf16, tile_cfg, args->nb * args->To, &rc);
+    return rc ? 0 : plan_gemm(*args, bf16, cfg, splits).ws;
 }
 
 extern "C" int mtts_conv_gemm_ws(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg, int32_t splits,

@@ -26,6 +26,7 @@
 // diagonal (`from_prev >= from_same or x == y`, core.pyx:73), out-of-band cells hold max_neg_val.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -1060,7 +1061,9 @@ bool mw_enabled() {
     return on;
 }
 
-WsLayout ws_layout(int B, int Tx, int Ty, bool with_lat = false) {
+// shape_override: MTTS_MAS_SHAPE may pick the DP shape -- only where the DP reads the transposed lattice (the
+// row-major kernels reject several of the shapes it can name: ADVICE r4)
+WsLayout ws_layout(int B, int Tx, int Ty, bool with_lat = false, bool shape_override = true) {
     WsLayout w{};
     w.W = 1;
     w.KL = 1;
@@ -1071,14 +1074,14 @@ WsLayout ws_layout(int B, int Tx, int Ty, bool with_lat = false) {
     // (120 x 600: 65 vs 72 us; 256 x 2048: 280 vs 319 us) -- the per-column dependency chain, not the rows per
     // lane, bounds both
     if (Tx > 256 && mw_enabled()) {
-        w.W = Tx <= 128 ? 2 : Tx <= 256 ? 4 : 8;
+        w.W = 8;
         w.KL = Tx <= 512 ? 1 : Tx <= 1024 ? 2 : Tx <= 2048 ? 4 : 8;
         w.K = w.W * w.KL;
         w.Txp = kWave * w.K;
     }
     // MTTS_MAS_SHAPE="W,KL" (tuning sweeps, transposed-lattice DP only -- every lattice but the core.pyx API's):
     // W waves x KL rows per lane; W = 1 the one-wave kernel (K from Tx).  Ignored unless it covers Tx.
-    if (const char *e = getenv("MTTS_MAS_SHAPE")) {
+    if (const char *e = shape_override ? getenv("MTTS_MAS_SHAPE") : nullptr) {
         int W = 0, KL = 0;
         if (sscanf(e, "%d,%d", &W, &KL) == 2 && tr_enabled(Tx)) {
             const bool ok1 = W == 1;
@@ -1280,7 +1283,8 @@ int check_shape(int B, int Tx, int Ty) {
 
 extern "C" size_t mtts_maximum_path_workspace_size(int32_t B, int32_t Tx, int32_t Ty) {
     if (B < 0 || Tx < 1 || Ty < 1) return 0;
-    return ws_layout(B, Tx, Ty, true).total;
+    // covers maximum_path (transposed lattice where tr_enabled) and compute_batch_alignments (row-major)
+    return std::max(ws_layout(B, Tx, Ty, true).total, ws_layout(B, Tx, Ty, true, false).total);
 }
 
 extern "C" int mtts_maximum_path_f32(const float *value, const float *mask, float *path, int32_t B,
@@ -1336,9 +1340,13 @@ extern "C" int mtts_maximum_path_f32(const float *value, const float *mask, floa
 
 extern "C" size_t mtts_prior_maximum_path_workspace_size(int32_t B, int32_t Tx, int32_t Ty) {
     if (B < 0 || Tx < 1 || Ty < 1) return 0;
-    const WsLayout w = ws_layout(B, Tx, Ty);  // lattice: row-major [B,Tx,Ty] or transposed [B,Ty,Txp]
-    return mtts::align_up(w.total, 256) + mtts::align_up((size_t)B * 2 * 4, 256) +
-           (size_t)B * Ty * (Tx > w.Txp ? Tx : w.Txp) * 4;
+    size_t n = 0;
+    for (const bool tr : {true, false}) {  // the layout of either lattice (the call may pass lattice_out or not)
+        const WsLayout w = ws_layout(B, Tx, Ty, false, tr);  // lattice: row-major [B,Tx,Ty] or transposed [B,Ty,Txp]
+        n = std::max(n, mtts::align_up(w.total, 256) + mtts::align_up((size_t)B * 2 * 4, 256) +
+                            (size_t)B * Ty * (Tx > w.Txp ? Tx : w.Txp) * 4);
+    }
+    return n;
 }
 
 extern "C" int mtts_prior_maximum_path(const float *mu_x, const float *y, const int64_t *x_lengths,
@@ -1351,7 +1359,7 @@ extern "C" int mtts_prior_maximum_path(const float *mu_x, const float *y, const 
     if (B == 0) return MTTS_OK;
     MTTS_CHECK_ARG(mu_x && y && x_lengths && y_lengths && C >= 1, "prior_maximum_path: null input or C < 1");
     MTTS_CHECK_ARG(B <= 65535, "prior_maximum_path: B > 65535");
-    const WsLayout w = ws_layout(B, Tx, Ty);
+    const WsLayout w = ws_layout(B, Tx, Ty, false, !lattice_out);  // a caller lattice_out is row-major
     if (!workspace || workspace_bytes < mtts_prior_maximum_path_workspace_size(B, Tx, Ty))
         return mtts::fail(MTTS_ERR_WORKSPACE, "prior_maximum_path: workspace too small");
     char *ws = static_cast<char *>(workspace);
@@ -1441,7 +1449,7 @@ extern "C" int mtts_compute_batch_alignments(int32_t *paths, float *values, cons
     if (rc) return rc;
     if (B == 0) return MTTS_OK;
     MTTS_CHECK_ARG(paths && values && t_xs && t_ys, "compute_batch_alignments: null pointer");
-    const WsLayout w = ws_layout(B, Tx, Ty);
+    const WsLayout w = ws_layout(B, Tx, Ty, false, false);  // row-major lattice (the in-place core.pyx API)
     if (!workspace || workspace_bytes < w.total)
         return mtts::fail(MTTS_ERR_WORKSPACE, "compute_batch_alignments: workspace too small");
     char *ws = static_cast<char *>(workspace);

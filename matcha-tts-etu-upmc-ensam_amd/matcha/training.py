@@ -27,11 +27,12 @@ Two execution modes:
 N>1 graph step: every replay issues the same collective sequence (the buckets of one fixed layout -- rank
 0's recorded backward order, broadcast once -- in bucket order), whatever shape a rank's batch has; a
 capture's warm-up passes never communicate (the reducer packs only), and the communicator's connections
-are set up once by an eager all-reduce per bucket on every rank when the reducer is built.  So each rank
-pads its batch to its own length, as the reference's DDP would, and captures new shapes on its own.
-(TrainConfig.agree_shapes=True instead pads every rank to the MAX padded Tx / Ty over ranks -- one host
-all-reduce per step -- so all ranks share one shape key; the extra padding changes the padded-length
-dependent parts of the arithmetic: GroupNorm statistics, conv bias leaking into padded frames.)
+are set up once by an eager all-reduce per bucket on every rank when the reducer is built.  By default
+(TrainConfig.agree_shapes=True) every rank pads to the MAX padded Tx / Ty over ranks -- one host-side gloo
+all-reduce per step, no GPU sync -- so all ranks capture and replay the same graph together; the extra padding
+changes the padded-length dependent parts of the arithmetic (GroupNorm statistics, conv bias leaking into padded
+frames).  agree_shapes=False lets each rank pad to its own length, as the reference's DDP would, and capture new
+shapes on its own (tested over gloo; not yet run with the in-graph RCCL transport on a multi-GPU box).
 
 Synthetic LJSpeech-shaped batches: token ids ~ U{1..149}, lengths ~ U[0.7 max, max]
 with element 0 = max, mels ~ N(0, 1) zeroed past the length.  A batch dict may carry "t" [B, 1, 1] and
@@ -194,9 +195,12 @@ class TrainConfig:
     graph_cache: int = 4
     dp: str = "auto"  # N>1 exchange: "ddp" (eager only), "buckets" (GradBucketReducer), "auto"
     comm: str = "auto"  # bucket reducer transport: "rccl" (capturable, libmtts_hip), "torch", "auto"
-    # N>1 graph step: pad every rank's batch to the MAX padded shape over ranks (see the module docstring);
-    # off by default -- each rank keeps its own padding, as DDP in the reference's setup would
-    agree_shapes: bool = False
+    # N>1 graph step: pad every rank's batch to the MAX padded shape over ranks (see the module docstring), so
+    # every rank captures and replays the same graph and issues the same in-graph RCCL collectives.  ON by default
+    # (ADVICE r4): rank-local captures beside peers that replay in-graph RCCL all-reduces have never run on a
+    # multi-GPU box; False keeps each rank's own padding (as DDP in the reference's setup) -- exercised over gloo
+    # by tests/test_dp_multirank_gpu.py
+    agree_shapes: bool = True
     # run the data-parallel exchange even at world size 1 (a world-size-1 process group must exist): the
     # bucketed RCCL path's cost on one GPU (bench.py extra_configs.dp_forced_n1); MTTS_FORCE_DP=1 does the same
     force_dp: bool = False
@@ -553,7 +557,7 @@ class Trainer:
         return e
 
     def _agree_shapes(self, batches):
-        """TrainConfig.agree_shapes (N>1 graph step, opt-in): MAX over ranks of each micro-batch's padded Tx /
+        """TrainConfig.agree_shapes (N>1 graph step, on by default): MAX over ranks of each micro-batch's padded Tx /
         Ty (and one batch size), then zero padding up to it, so every rank looks up the same key.  The padded
         frames are masked, but the decoder's arithmetic depends on the padded length (GroupNorm statistics
         over the whole padded length, conv bias leaking into padded frames -- SURVEY 0.6), so a rank's losses

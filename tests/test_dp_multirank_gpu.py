@@ -68,7 +68,7 @@ def _worker(rank, world, port, precision, q):
         from matcha.training import TrainConfig, Trainer
 
         m = _model(dev, seed=rank)  # different init per rank: the Trainer broadcasts rank 0's weights
-        tr = Trainer(m, TrainConfig(graph=True, precision=precision, bucket_mb=4.0))
+        tr = Trainer(m, TrainConfig(graph=True, precision=precision, bucket_mb=4.0, agree_shapes=False))
         b = _shard(rank, dev)
         logs = [tr.step([b]).cpu() for _ in range(STEPS)]
         torch.cuda.synchronize()

@@ -69,3 +69,24 @@ def test_product_path_refuses_cpu_tensors():
 
     with pytest.raises(N.NativeError):
         maximum_path(torch.zeros(1, 2, 3), torch.ones(1, 2, 3))
+
+
+def test_gemm_workspace_query_plans_the_schedule_that_runs():
+    """mtts_conv_gemm_workspace_size resolves the operand-driven schedule rewrites the launch applies:
+    the bf16x6 text-encoder prenet (3840 x 192, k = 5 over 192 channels, three weight planes) runs the LDS-DMA
+    64 x 64 schedule with split K, so its size query must ask for the split slabs (it returned 0 when it planned
+    the raw heuristic's register config, and the launch then ran unsplit)."""
+    from matcha.models.components import _ops as O
+
+    a = O.ConvGemmArgs()
+    a.A, a.W, a.C = 4096, 8192, 12288  # 16-byte aligned placeholders: size queries dereference nothing
+    a.lda, a.Ti, a.To, a.nb, a.in_stride, a.ntaps, a.cin = 192, 120, 120, 32, 1, 5, 192
+    for j in range(5):
+        a.off[j] = j - 2
+    a.N, a.K, a.Kp = 192, 960, 960
+    a.ldc, a.To_full, a.out_stride = 192, 120, 1
+    a.flags = O.GEMM_F_SPLIT3
+    ws = N.lib().mtts_conv_gemm_workspace_size(ctypes.byref(a), O.PREC_BF16, -1, 0)
+    assert ws == 2 * 3840 * 192 * 4, ws  # two fp32 partial slabs of M x N
+    a.flags = 0  # one plane: the register schedule, no split
+    assert N.lib().mtts_conv_gemm_workspace_size(ctypes.byref(a), O.PREC_BF16, -1, 0) == 0

@@ -11,9 +11,12 @@ from pathlib import Path
 from pmc_regex import REGEX  # noqa: E402  (tools/r3/pmc_regex.py)
 
 src, dst = Path(sys.argv[1]), Path(sys.argv[2])
+only = sys.argv[3:] or ["gemm", "wgrad", "attn"]  # family names (default: the step families)
 algo = json.loads((src / "algo.json").read_text())
 dst.mkdir(parents=True, exist_ok=True)
 for fam, rx in REGEX.items():
+    if only and fam not in only:
+        continue
     tot = {}
     for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         files = sorted((src / f"{fam}_{sub}").rglob("*counter_collection.csv"))
@@ -31,8 +34,10 @@ for fam, rx in REGEX.items():
     write_b = 1024 * tot["WRITE_SIZE"][0] / n
     algo_b = algo[fam]["algorithmic_bytes"] / n
     out = {"family": fam, "kernels_regex": rx,
-           "workload": f"tools/r3/pmc_families.py: two eager {algo.get('precision', 'bf16-mixed')} fwd+bwd passes of "
-                       "the bench batch (B=32, 120x600)",
+           "workload": ("tools/r5/pmc_mas.py: two maximum_path calls on the bench batch's lattice (B=32, 120x600)"
+                        if fam == "mas" else
+                        f"tools/r3/pmc_families.py: two eager {algo.get('precision', 'bf16-mixed')} fwd+bwd passes of "
+                        "the bench batch (B=32, 120x600)"),
            "launches": n, "dispatches": tot["FETCH_SIZE"][1], "warmup_dispatches_dropped": True, "fetch_bytes_per_launch": round(fetch_b),
            "write_bytes_per_launch": round(write_b), "traffic_bytes_per_launch": round(fetch_b + write_b),
            "algorithmic_bytes_per_launch": round(algo_b), "traffic_over_algorithmic": round((fetch_b + write_b) / algo_b, 3),

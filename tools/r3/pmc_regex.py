@@ -3,4 +3,5 @@ REGEX = {
     "gemm": "conv_gemm_kernel|conv_gemm_glds_kernel|splitk_epilogue_kernel",
     "wgrad": "conv_wgrad_kernel|reduce_partials_kernel",
     "attn": "attn_fwd|attn_bwd|attn_drow",
+    "mas": "mas_",  # maximum_path: mas_transpose_kernel + mas_dp(_mw)_kernel + mas_expand_kernel (tools/r5/pmc_mas.sh)
 }
