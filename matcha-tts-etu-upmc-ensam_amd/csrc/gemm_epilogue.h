@@ -133,60 +133,125 @@ __device__ __forceinline__ void gemm_epilogue(const mtts_conv_gemm_args &p, f32x
     }
 }
 
-// Everything after the bias for 4 consecutive columns n..n+3 of output row crow (float4 I/O).
-__device__ __forceinline__ void epilogue_row4(const mtts_conv_gemm_args &p, int crow, int n, float (&e)[4],
-                                              uint32_t s0, uint32_t s1, float keep_scale) {
+// V (4 or 8) consecutive bf16 values from / to 16-byte-aligned memory as one uint2 / uint4 access
+template <int V>
+__device__ __forceinline__ void store_bf16v(void *dst, const float (&e)[V]) {
     typedef float f32x2_ __attribute__((ext_vector_type(2)));
     typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
+    uint32_t w[V / 2];
+#pragma unroll
+    for (int q = 0; q < V / 2; ++q)
+        w[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_){e[2 * q], e[2 * q + 1]}, bf16x2_));
+    if constexpr (V == 4) *reinterpret_cast<uint2 *>(dst) = make_uint2(w[0], w[1]);
+    else *reinterpret_cast<uint4 *>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+template <int V>
+__device__ __forceinline__ void load_bf16v(const void *src, float (&a)[V]) {  // bf16 -> fp32 is exact
+    uint32_t w[V / 2];
+    if constexpr (V == 4) {
+        const uint2 h = *reinterpret_cast<const uint2 *>(src);
+        w[0] = h.x, w[1] = h.y;
+    } else {
+        const uint4 h = *reinterpret_cast<const uint4 *>(src);
+        w[0] = h.x, w[1] = h.y, w[2] = h.z, w[3] = h.w;
+    }
+#pragma unroll
+    for (int q = 0; q < V / 2; ++q) {
+        a[2 * q] = __uint_as_float(w[q] << 16);
+        a[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+    }
+}
+template <int V>
+__device__ __forceinline__ void load_f32v(const float *src, float (&a)[V]) {
+#pragma unroll
+    for (int q = 0; q < V / 4; ++q) {
+        const float4 x = reinterpret_cast<const float4 *>(src)[q];
+        a[4 * q] = x.x, a[4 * q + 1] = x.y, a[4 * q + 2] = x.z, a[4 * q + 3] = x.w;
+    }
+}
+template <int V>
+__device__ __forceinline__ void store_f32v(float *dst, const float (&e)[V]) {
+#pragma unroll
+    for (int q = 0; q < V / 4; ++q)
+        reinterpret_cast<float4 *>(dst)[q] = make_float4(e[4 * q], e[4 * q + 1], e[4 * q + 2], e[4 * q + 3]);
+}
+
+// Epilogue kinds fixed at compile time (EK > 0: the weight-stationary kernel classifies each launch on the host,
+// mtts::gemm_epilogue_kind): the per-element tests of p.act / p.flags / null pointers become constants and the
+// branches drop out.  EK_RT reads everything at run time (every other caller).
+enum : int {
+    EK_RT = 0,
+    EK_LIN_C16 = 1,  // no activation, C bf16; bias / dropout / residual / c_scale at run time; no C_pre
+    EK_LIN_C32 = 2,  // the same with an fp32 C
+    EK_GELU = 3,     // fast GELU, bf16 C_pre and C; bias / dropout at run time; no residual / c_scale
+    EK_DGELU = 4,    // fast GELU' on a bf16 aux, bf16 C; bias / dropout at run time; no C_pre / residual / c_scale
+};
+
+__host__ __device__ inline int gemm_epilogue_kind(const mtts_conv_gemm_args &p) {
+    const bool fast = p.flags & MTTS_GEMM_F_FAST_ACT, pre16 = p.flags & MTTS_GEMM_F_PRE_BF16,
+               c16 = p.flags & MTTS_GEMM_F_C_BF16;
+    if (p.act == MTTS_ACT_NONE && !p.C_pre) return c16 ? EK_LIN_C16 : EK_LIN_C32;
+    if (p.act == MTTS_ACT_GELU && fast && pre16 && c16 && p.C_pre && !p.residual && !p.c_scale) return EK_GELU;
+    if (p.act == MTTS_ACT_DGELU && fast && pre16 && c16 && !p.C_pre && p.aux && !p.residual && !p.c_scale)
+        return EK_DGELU;
+    return EK_RT;
+}
+
+// Everything after the bias for V (4 or 8) consecutive columns n.. of output row crow (16-byte I/O: V = 8
+// writes a bf16 C / C_pre as one dwordx4 per lane -- the dwordx2 stores of V = 4 are issue-bound at about
+// half the bytes per cycle, MI355X_MICROARCH.md's epilogue store-tail row).
+template <int V, int EK = EK_RT>
+__device__ __forceinline__ void epilogue_rowv(const mtts_conv_gemm_args &p, int crow, int n, float (&e)[V],
+                                              uint32_t s0, uint32_t s1, float keep_scale) {
+    constexpr bool RT = EK == EK_RT;
+    const int act = RT ? p.act : EK == EK_GELU ? MTTS_ACT_GELU : EK == EK_DGELU ? MTTS_ACT_DGELU : MTTS_ACT_NONE;
+    const bool fast = RT ? (p.flags & MTTS_GEMM_F_FAST_ACT) != 0 : true;
+    const bool pre16 = RT ? (p.flags & MTTS_GEMM_F_PRE_BF16) != 0 : true;
+    const bool c16 = RT ? (p.flags & MTTS_GEMM_F_C_BF16) != 0 : EK != EK_LIN_C32;
+    const bool has_pre = RT ? p.C_pre != nullptr : EK == EK_GELU;
+    const bool has_drop = p.dropout_p > 0.f;
+    const bool has_res = (RT || EK == EK_LIN_C16 || EK == EK_LIN_C32) && p.residual;
+    const bool has_cs = (RT || EK == EK_LIN_C16 || EK == EK_LIN_C32) && p.c_scale;
     const size_t off = (size_t)crow * p.ldc + n;
-    const bool pre16 = p.flags & MTTS_GEMM_F_PRE_BF16;
-    if (p.C_pre) {
-        if (pre16) {
-            const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_){e[0], e[1]}, bf16x2_));
-            const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_){e[2], e[3]}, bf16x2_));
-            *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(p.C_pre) + off) = make_uint2(lo, hi);
-        } else {
-            *reinterpret_cast<float4 *>(p.C_pre + off) = make_float4(e[0], e[1], e[2], e[3]);
-        }
+    if (has_pre) {
+        if (pre16) store_bf16v<V>(reinterpret_cast<uint16_t *>(p.C_pre) + off, e);
+        else store_f32v<V>(p.C_pre + off, e);
     }
-    if (p.act) {
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (p.act == MTTS_ACT_DGELU || p.act == MTTS_ACT_DRELU) {
+    if (act) {
+        float av[V];
+#pragma unroll
+        for (int q = 0; q < V; ++q) av[q] = 0.f;
+        if (act == MTTS_ACT_DGELU || act == MTTS_ACT_DRELU) {
             const size_t ao = (size_t)crow * p.ldaux + n;
-            if (pre16) {  // bf16 -> fp32 is exact: the bits move to the high half
-                const uint2 h = *reinterpret_cast<const uint2 *>(reinterpret_cast<const uint16_t *>(p.aux) + ao);
-                a = make_float4(__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xffff0000u),
-                                __uint_as_float(h.y << 16), __uint_as_float(h.y & 0xffff0000u));
-            } else {
-                a = *reinterpret_cast<const float4 *>(p.aux + ao);
-            }
+            if (pre16) load_bf16v<V>(reinterpret_cast<const uint16_t *>(p.aux) + ao, av);
+            else load_f32v<V>(p.aux + ao, av);
         }
-        const float av[4] = {a.x, a.y, a.z, a.w};
-        const bool fast = p.flags & MTTS_GEMM_F_FAST_ACT;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) e[q] = epi_act(p.act, e[q], &av[q], fast);
+        for (int q = 0; q < V; ++q) e[q] = epi_act(act, e[q], &av[q], fast);
     }
-    if (p.dropout_p > 0.f) {
+    if (has_drop) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < V; ++q)
             e[q] = dropout_keep(s0, s1, (uint32_t)crow, (uint32_t)(n + q), p.dropout_p) ? e[q] * keep_scale : 0.f;
     }
-    if (p.residual) {
-        const float4 r = *reinterpret_cast<const float4 *>(p.residual + (size_t)crow * p.ldr + n);
-        e[0] += r.x; e[1] += r.y; e[2] += r.z; e[3] += r.w;
+    if (has_res) {
+        float r[V];
+        load_f32v<V>(p.residual + (size_t)crow * p.ldr + n, r);
+#pragma unroll
+        for (int q = 0; q < V; ++q) e[q] += r[q];
     }
-    if (p.c_scale) {
+    if (has_cs) {
         const float cs = p.c_scale[crow];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) e[q] *= cs;
+        for (int q = 0; q < V; ++q) e[q] *= cs;
     }
-    if (p.flags & MTTS_GEMM_F_C_BF16) {
-        const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_){e[0], e[1]}, bf16x2_));
-        const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_){e[2], e[3]}, bf16x2_));
-        *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(p.C) + off) = make_uint2(lo, hi);
-    } else {
-        *reinterpret_cast<float4 *>(p.C + off) = make_float4(e[0], e[1], e[2], e[3]);
-    }
+    if (c16) store_bf16v<V>(reinterpret_cast<uint16_t *>(p.C) + off, e);
+    else store_f32v<V>(p.C + off, e);
+}
+
+__device__ __forceinline__ void epilogue_row4(const mtts_conv_gemm_args &p, int crow, int n, float (&e)[4],
+                                              uint32_t s0, uint32_t s1, float keep_scale) {
+    epilogue_rowv<4>(p, crow, n, e, s0, s1, keep_scale);
 }
 
 // Split-K partial store: the raw accumulators of a wave's tiles into part[M][N] (row = GEMM row),
@@ -227,9 +292,17 @@ __host__ __device__ inline bool gemm_epilogue_vec_ok(const mtts_conv_gemm_args &
            (!p.aux || (p.ldaux % 4 == 0 && al(p.aux)));
 }
 
-template <int TM, int TN>
-__device__ __forceinline__ void gemm_epilogue_vec(const mtts_conv_gemm_args &p, f32x16 (&acc)[TM][TN], float *stage,
-                                                  int row0, int col0, int lane) {
+// 8 columns per lane (16-byte bf16 stores) when N, ldc and a bf16 aux row are multiples of 8
+__host__ __device__ inline bool gemm_epilogue_vec8_ok(const mtts_conv_gemm_args &p) {
+    return p.N % 8 == 0 && p.ldc % 8 == 0 && (!p.aux || p.ldaux % 8 == 0);
+}
+
+// EK: epilogue kind (above); ROWMASK: zero the accumulators of the rows whose a_scale is 0 (a one-tap GEMM that
+// did not mask its A rows: A row = GEMM row)
+template <int V, int TM, int TN, int EK = EK_RT, bool ROWMASK = false>
+__device__ __forceinline__ void gemm_epilogue_vec_v(const mtts_conv_gemm_args &p, f32x16 (&acc)[TM][TN], float *stage,
+                                                    int row0, int col0, int lane) {
+    constexpr int L = 32 / V, RP = 64 / L;  // lanes per 32-column row; rows per pass
     const int M = p.nb * p.To;
     const float inv_to = 1.0f / (float)p.To;
     const int lr = lane & 31, lh = lane >> 5;
@@ -240,35 +313,49 @@ __device__ __forceinline__ void gemm_epilogue_vec(const mtts_conv_gemm_args &p, 
         s1 = p.seed[1];
     }
     const float keep_scale = drop ? 1.0f / (1.0f - p.dropout_p) : 1.0f;
-    const int rsub = lane >> 3, c4 = lane & 7;  // this lane's row within an 8-row slab and its column chunk
+    const int rsub = lane / L, cv = lane % L;  // this lane's row within an RP-row slab and its column chunk
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-        // output rows of the 4 slabs this lane finishes in tile row i (same for every j)
-        int crow[4];
+        // output rows of the slabs this lane finishes in tile row i (same for every j)
+        int crow[32 / RP];
+        bool live[32 / RP];
 #pragma unroll
-        for (int it = 0; it < 4; ++it) {
-            const int m = row0 + i * 32 + it * 8 + rsub;
+        for (int it = 0; it < 32 / RP; ++it) {
+            const int m = row0 + i * 32 + it * RP + rsub;
             int b, u;
             divmod_fast(m, p.To, inv_to, b, u);
             crow[it] = m < M ? b * p.To_full + u * p.out_stride + p.out_off : -1;
+            live[it] = true;
+            if (ROWMASK && m < M) live[it] = p.a_scale[m] != 0.f;
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
 #pragma unroll
             for (int v = 0; v < 16; ++v) stage[((v & 3) + 8 * (v >> 2) + 4 * lh) * 32 + lr] = acc[i][j][v];
-            const int n = col0 + j * 32 + 4 * c4;
+            const int n = col0 + j * 32 + V * cv;
             const bool nok = n < p.N;
-            float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (p.bias && nok) bn = *reinterpret_cast<const float4 *>(p.bias + n);
+            float bn[V];
 #pragma unroll
-            for (int it = 0; it < 4; ++it) {
-                float4 x = reinterpret_cast<const float4 *>(stage)[(it * 8 + rsub) * 8 + c4];
+            for (int q = 0; q < V; ++q) bn[q] = 0.f;
+            if (p.bias && nok) load_f32v<V>(p.bias + n, bn);
+#pragma unroll
+            for (int it = 0; it < 32 / RP; ++it) {
+                float e[V];
+                load_f32v<V>(stage + (it * RP + rsub) * 32 + V * cv, e);
                 if (crow[it] < 0 || !nok) continue;
-                float e[4] = {x.x + bn.x, x.y + bn.y, x.z + bn.z, x.w + bn.w};
-                epilogue_row4(p, crow[it], n, e, s0, s1, keep_scale);
+#pragma unroll
+                for (int q = 0; q < V; ++q) e[q] = (live[it] ? e[q] : 0.f) + bn[q];
+                epilogue_rowv<V, EK>(p, crow[it], n, e, s0, s1, keep_scale);
             }
         }
     }
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void gemm_epilogue_vec(const mtts_conv_gemm_args &p, f32x16 (&acc)[TM][TN], float *stage,
+                                                  int row0, int col0, int lane) {
+    if (gemm_epilogue_vec8_ok(p)) gemm_epilogue_vec_v<8>(p, acc, stage, row0, col0, lane);
+    else gemm_epilogue_vec_v<4>(p, acc, stage, row0, col0, lane);
 }
 
 }  // namespace mtts

@@ -100,6 +100,9 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--only-bf16", action="store_true")
     ap.add_argument("--only-fp32", action="store_true")
+    ap.add_argument("--match", default=None, help="M,N,K,flags,act: replay only this launch shape")
+    ap.add_argument("--plain", type=int, default=0, help="with --match: N plain (ungraphed) launches per schedule "
+                    "instead of the timing, for rocprofv3 counter passes")
     args = ap.parse_args()
     rows = [json.loads(l) for l in open(args.log) if l.startswith("{")]
     uniq = {}
@@ -115,6 +118,16 @@ def main():
     for r in cases:
         if (args.only_bf16 and r["prec"] != 1) or (args.only_fp32 and r["prec"] != 0):
             continue
+        if args.match and [int(x) for x in args.match.split(",")] != [r[k] for k in ("M", "N", "K", "flags", "act")]:
+            continue
+        if args.match and args.plain:
+            A, Wp, C, kw = make_case(r)
+            for cfg in cfgs:
+                for _ in range(args.plain):
+                    run(r, A, Wp, C, kw, cfg)
+                torch.cuda.synchronize()
+            print(json.dumps(dict(match=args.match, cfgs=cfgs, launches=args.plain)), flush=True)
+            break
         A, Wp, C, kw = make_case(r)
         res = {}
         ref = None
