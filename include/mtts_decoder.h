@@ -332,6 +332,13 @@ size_t mtts_clip_adamw_workspace_size(int32_t nchunks);
 int mtts_clip_adamw(const mtts_adamw_chunk *chunks, int32_t nchunks, float *params, float *exp_avg,
                     float *exp_avg_sq, const double *lr, float *step, float max_norm, double beta1, double beta2,
                     double eps, double weight_decay, void *workspace, size_t workspace_bytes, void *hip_stream);
+/* The same on g * grad_scale: the data-parallel step all-reduces gradient SUMS (ncclSum: RCCL's one-rank
+ * all-reduce is then no kernel at all, and no pre-multiply pass at N > 1) and folds DDP's mean, 1 / world, in
+ * here -- exact for a power-of-two world (the norm is sqrt(sum g^2) * grad_scale, the same value). */
+int mtts_clip_adamw_scaled(const mtts_adamw_chunk *chunks, int32_t nchunks, float *params, float *exp_avg,
+                           float *exp_avg_sq, const double *lr, float *step, float max_norm, double beta1,
+                           double beta2, double eps, double weight_decay, float grad_scale, void *workspace,
+                           size_t workspace_bytes, void *hip_stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Partial-sum reductions of the parameter gradients, batched.

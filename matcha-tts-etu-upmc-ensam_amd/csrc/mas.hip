@@ -33,7 +33,7 @@
 #include <cstdlib>
 #include <type_traits>
 
-#include "mtts_common.h"
+#include "mtts_base.h"
 
 namespace {
 

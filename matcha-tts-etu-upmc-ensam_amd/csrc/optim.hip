@@ -85,12 +85,14 @@ __global__ __launch_bounds__(kThreads) void adamw_update_kernel(const mtts_adamw
                                                                 const double *__restrict__ lr_ptr,
                                                                 const float *__restrict__ t_next,
                                                                 float *__restrict__ step, float max_norm, double b1,
-                                                                double b2, double eps_d, double wd) {
+                                                                double b2, double eps_d, double wd, float gscale) {
     __shared__ float red[kThreads / 64];
     // total squared norm: every block sums the same partials in the same order
     float s = 0.f;
     for (int i = threadIdx.x; i < nchunks; i += kThreads) s += partial[i];
-    const float total = sqrtf(block_reduce_sum(s, red));
+    // (the partials are sums of the raw g^2; g * gscale has norm sqrt(sum g^2) * gscale -- the same fp32
+    // value for a power-of-two gscale, which scales exactly)
+    const float total = sqrtf(block_reduce_sum(s, red)) * gscale;
     // clip_grad_norm_: coef = clamp(max_norm / (total + 1e-6), max=1), fp32 tensor arithmetic
     float coef = 1.f;
     if (max_norm > 0.f) coef = fminf(max_norm / (total + 1e-6f), 1.f);
@@ -111,7 +113,7 @@ __global__ __launch_bounds__(kThreads) void adamw_update_kernel(const mtts_adamw
     // _foreach_lerp_(m, g, 1 - b1) (weight < 0.5: m + w (g - m)), _foreach_mul_(v, b2),
     // _foreach_addcmul_(v, g, g, 1 - b2), sqrt(v) / sqrt(bc2) + eps, _foreach_addcdiv_(p, m, denom, -lr / bc1)
     auto upd = [&](float g, float &pi, float &mi, float &vi) {
-        g = __fmul_rn(g, coef);
+        g = __fmul_rn(__fmul_rn(g, gscale), coef);
         pi = __fmul_rn(pi, decay);
         mi = __fadd_rn(mi, __fmul_rn(w1, __fsub_rn(g, mi)));
         vi = __fmul_rn(vi, b2f);
@@ -159,12 +161,13 @@ extern "C" size_t mtts_clip_adamw_workspace_size(int32_t nchunks) {
     return (size_t)(nchunks > 0 ? nchunks + 1 : 0) * sizeof(float);
 }
 
-extern "C" int mtts_clip_adamw(const mtts_adamw_chunk *chunks, int32_t nchunks, float *params, float *exp_avg,
-                               float *exp_avg_sq, const double *lr, float *step, float max_norm, double beta1,
-                               double beta2, double eps, double weight_decay, void *workspace,
-                               size_t workspace_bytes, void *hip_stream) {
+extern "C" int mtts_clip_adamw_scaled(const mtts_adamw_chunk *chunks, int32_t nchunks, float *params,
+                                      float *exp_avg, float *exp_avg_sq, const double *lr, float *step, float max_norm,
+                                      double beta1, double beta2, double eps, double weight_decay, float grad_scale,
+                                      void *workspace, size_t workspace_bytes, void *hip_stream) {
     MTTS_CHECK_ARG(chunks && params && exp_avg && exp_avg_sq && lr && step && nchunks >= 0,
                    "clip_adamw: null pointer");
+    MTTS_CHECK_ARG(grad_scale > 0.f, "clip_adamw: grad_scale must be positive");
     if (nchunks == 0) return MTTS_OK;
     if (!workspace || workspace_bytes < mtts_clip_adamw_workspace_size(nchunks))
         return mtts::fail(MTTS_ERR_WORKSPACE, "clip_adamw: workspace too small");
@@ -176,6 +179,14 @@ extern "C" int mtts_clip_adamw(const mtts_adamw_chunk *chunks, int32_t nchunks, 
     if (rc) return rc;
     hipLaunchKernelGGL(adamw_update_kernel, dim3(nchunks), dim3(kThreads), 0, st, chunks, nchunks,
                        (const float *)partial, params, exp_avg, exp_avg_sq, lr, (const float *)t_next, step, max_norm,
-                       beta1, beta2, eps, weight_decay);
+                       beta1, beta2, eps, weight_decay, grad_scale);
     return mtts::check_launch("adamw_update_kernel");
+}
+
+extern "C" int mtts_clip_adamw(const mtts_adamw_chunk *chunks, int32_t nchunks, float *params, float *exp_avg,
+                               float *exp_avg_sq, const double *lr, float *step, float max_norm, double beta1,
+                               double beta2, double eps, double weight_decay, void *workspace,
+                               size_t workspace_bytes, void *hip_stream) {
+    return mtts_clip_adamw_scaled(chunks, nchunks, params, exp_avg, exp_avg_sq, lr, step, max_norm, beta1, beta2, eps,
+                                  weight_decay, 1.0f, workspace, workspace_bytes, hip_stream);
 }

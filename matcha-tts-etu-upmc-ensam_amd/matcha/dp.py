@@ -8,9 +8,12 @@ collectives INSIDE its HIP graph, which torch's ProcessGroupNCCL cannot provide 
 
 * ``GradBucketReducer`` lays every differentiated parameter's gradient out in one flat fp32 buffer,
   in the order backward produces them (recorded in a warm-up pass), cut into ~``bucket_mb`` buckets.
-  A post-accumulate-grad hook counts each bucket's gradients; when the last one lands, the queued
-  weight-gradient GEMMs / sums that produce them are flushed onto the deferral's side stream and the
-  bucket is packed (one ``torch.cat`` into its flat slice) and reduced on the reducer's stream after
+  The armed backward writes the gradients of the conv / linear / FeedForward weights straight into their
+  flat views (``_ops.set_grad_slots``: the producers allocate their output there, AccumulateGrad adopts
+  it as ``.grad``).  A post-accumulate-grad hook counts each bucket's gradients; when the last one lands,
+  the queued weight-gradient GEMMs / sums that produce them are flushed onto the deferral's side stream and
+  the bucket is packed (one multi-tensor copy of the gradients that are not already in place -- norms,
+  embeddings, the time MLP) and reduced on the reducer's stream after
   both the main and the side stream -- captured, that is a forked branch of the graph, so the reduction
   of bucket k runs while backward computes bucket k+1, and the main stream never waits for the side
   stream's weight gradients (the N=1 step's decoder / encoder seam overlap is kept).
@@ -22,8 +25,13 @@ collectives INSIDE its HIP graph, which torch's ProcessGroupNCCL cannot provide 
   or any backend eagerly); it cannot be captured, so a graph step with it reduces the whole flat
   buffer once after the graph (no overlap) -- the shared-GPU gloo rehearsal uses that.
 
-Gradient averaging (mean over ranks) happens in the collective (ncclAvg) or right after it
-(TorchComm: sum then divide), before clipping -- DDP's semantics.
+Gradient averaging (mean over ranks, DDP's semantics) happens before clipping: TorchComm sums then divides;
+RcclComm SUMS (ncclSum) and leaves the factor ``post_scale = 1 / world`` to the consumer -- the Trainer's
+fused clip + AdamW multiplies by it (``mtts_clip_adamw_scaled``: exact for a power-of-two world, so the
+update equals the ncclAvg one bit for bit), any other consumer gets the flat buffer scaled in place by
+``finish()``.  Why: RCCL's ncclAvg is a pre-multiply-sum, and at one rank it still launches a read-modify-write
+kernel over the whole 76 MB buffer (oneRankReduce, ~143 us of the forced-DP N=1 step, profiles/r05/dp/);
+an in-place ncclSum at one rank launches nothing.
 """
 from __future__ import annotations
 
@@ -50,6 +58,7 @@ class TorchComm:
     """torch.distributed all-reduce (sum, then / world): eager only."""
 
     capturable = False
+    post_scale = 1.0  # all_reduce_ leaves the mean
 
     def __init__(self, group=None):
         self.group = group
@@ -57,7 +66,7 @@ class TorchComm:
         self.ranks = self.world  # the ranks the collective spans
         self.backend = dist.get_backend(group)
 
-    def all_reduce_mean_(self, t: torch.Tensor) -> None:
+    def all_reduce_(self, t: torch.Tensor) -> None:
         dist.all_reduce(t, group=self.group)
         t.div_(self.world)
 
@@ -86,11 +95,12 @@ class RcclComm:
             raise RuntimeError(f"RCCL communicator spans {n.value} ranks as rank {me.value}; torch.distributed "
                                f"has {self.world} / {self.rank}")
         self.ranks = n.value  # as RCCL itself reports it (ncclCommCount)
+        self.post_scale = 1.0 / self.world  # all_reduce_ leaves the SUM
         self.version = int(N.lib().mtts_dp_rccl_version())
         self.backend = "rccl"
 
-    def all_reduce_mean_(self, t: torch.Tensor) -> None:
-        N.check(N.lib().mtts_dp_allreduce_f32(self._comm, t.data_ptr(), t.numel(), 1,
+    def all_reduce_(self, t: torch.Tensor) -> None:
+        N.check(N.lib().mtts_dp_allreduce_f32(self._comm, t.data_ptr(), t.numel(), 0,
                                               torch.cuda.current_stream(t.device).cuda_stream),
                 "mtts_dp_allreduce_f32")
 
@@ -167,6 +177,10 @@ class GradBucketReducer:
         self._ready = [0] * len(self.buckets)
         self._issued = 0
         self.grad_refs = None  # the gradient tensors packed in the last armed pass
+        # True: the optimizer applies comm.post_scale itself (Trainer + fused AdamW); False: finish() /
+        # reduce_now() scale the flat buffer in place when the comm leaves sums
+        self.grad_scale_applied = False
+        self.copied = {}  # bucket -> shapes of the gradients its last pack copied (not written in place)
 
     # -------------------------------------------------------------------- per step
     def arm(self, scalars: torch.Tensor, overlap: bool, comm: bool = True) -> None:
@@ -174,7 +188,10 @@ class GradBucketReducer:
         (already the micro-batch mean).  overlap=False packs only; the caller reduces after.  comm=False
         packs only and never communicates (a graph capture's warm-up passes: a rank may capture a new
         shape while its peers replay, so only replays may issue collectives)."""
+        from matcha.models.components import _ops as OPS
+
         self.armed = True
+        OPS.set_grad_slots({p.data_ptr(): v for p, v in zip(self.params, self.views)})
         capturing = self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
         self.overlap = (comm and overlap and self.comm is not None and (self.comm.capturable or not capturing))
         self._pending_scalars = scalars
@@ -199,11 +216,16 @@ class GradBucketReducer:
 
     def _pack(self, k: int) -> None:
         s, e = self.buckets[k]
-        lo, _ = self.spans[k]
-        grads = [self.grad_refs[i].reshape(-1) for i in range(s, e)]
-        n = self.offsets[e] - lo if e < len(self.params) else self.n_grad - lo
-        if grads:
-            torch.cat(grads, out=self.flat[lo:lo + n])
+        dst, src = [], []
+        for i in range(s, e):  # gradients written in place (grad slots) need no copy
+            g, v = self.grad_refs[i], self.views[i]
+            if g.data_ptr() != v.data_ptr():
+                dst.append(v)
+                src.append(g.view_as(v) if g.shape != v.shape else g)
+        self.copied[k] = [self.params[i].shape for i in range(s, e)
+                          if self.grad_refs[i].data_ptr() != self.views[i].data_ptr()]
+        if dst:
+            torch._foreach_copy_(dst, src)
         if k == len(self.buckets) - 1:
             self.flat[self.n_grad:].copy_(self._pending_scalars)
 
@@ -220,19 +242,19 @@ class GradBucketReducer:
                 self.stream.wait_stream(side)
             with torch.cuda.stream(self.stream):
                 self._pack(k)
-                self.comm.all_reduce_mean_(self.flat[lo:hi])
+                self.comm.all_reduce_(self.flat[lo:hi])
             return
         OPS.flush_deferred_grad_sums()  # on the current stream (joins the side stream first)
         self._pack(k)
         if self.overlap:  # CPU (gloo): eager, in order
-            self.comm.all_reduce_mean_(self.flat[lo:hi])
+            self.comm.all_reduce_(self.flat[lo:hi])
 
     def warm(self) -> None:
         """One eager all-reduce per bucket span on every rank (all ranks call this together, when the
         reducer is built): RCCL sets up its connections for each message size on first use, which must not
         happen later inside one rank's graph capture while its peers replay."""
         for lo, hi in self.spans:
-            self.comm.all_reduce_mean_(self.flat[lo:hi])
+            self.comm.all_reduce_(self.flat[lo:hi])
         self.flat.zero_()
 
     def finish(self) -> None:
@@ -240,7 +262,10 @@ class GradBucketReducer:
         (overlap) or the whole buffer reduced now (no overlap), parameters' .grad -> flat views."""
         if not self.armed:
             return
+        from matcha.models.components import _ops as OPS
+
         self.armed = False
+        OPS.set_grad_slots(None)
         if self._issued != len(self.buckets):
             # a parameter got no gradient on this rank.  Its peers issue every bucket, so the remaining
             # ones are issued here too (missing gradients as zeros) before raising: the ranks stay in
@@ -258,20 +283,29 @@ class GradBucketReducer:
         if self.overlap:
             if self.stream is not None:
                 torch.cuda.current_stream(self.device).wait_stream(self.stream)
+            self._post_scale()
         self.attach_views()
+
+    def _post_scale(self) -> None:
+        ps = getattr(self.comm, "post_scale", 1.0)
+        if ps != 1.0 and not self.grad_scale_applied:
+            self.flat[:self.n_grad].mul_(ps)
 
     def reduce_now(self) -> None:
         """No-overlap mode: one all-reduce of the packed buffer (eager, e.g. after a graph replay)."""
-        self.comm.all_reduce_mean_(self.flat)
+        self.comm.all_reduce_(self.flat)
+        self._post_scale()
 
     def attach_views(self) -> None:
         for p, v in zip(self.params, self.views):
             p.grad = v
 
     def scalars(self) -> torch.Tensor:
-        """A VIEW of the averaged logged values in the flat buffer: the next step overwrites it (callers
-        that keep it clone it -- Trainer does)."""
-        return self.flat[self.n_grad:]
+        """The averaged logged values: a VIEW of the flat buffer's tail when the comm leaves the mean (the next
+        step overwrites it: callers that keep it clone it -- Trainer does), else the tail times post_scale."""
+        ps = getattr(self.comm, "post_scale", 1.0)
+        tail = self.flat[self.n_grad:]
+        return tail if ps == 1.0 else tail * ps
 
     def remove(self) -> None:
         for h in self._hooks:

@@ -874,6 +874,57 @@ def _grad_sums(backward):
     return run
 
 
+# Data-parallel gradient slots: GradBucketReducer.arm() hands the flat all-reduce buffer's per-parameter views to
+# the gradient producers (keyed by the parameter's data pointer), so a weight-gradient kernel writes straight into
+# its bucket and the bucket's pack copy has nothing left to move.  A slot is handed out once per
+# armed backward: a parameter used twice gets its second gradient in a fresh buffer, which AccumulateGrad adds
+# into the slot (the first one, already its .grad) -- the same arithmetic as two fresh buffers.
+_GRAD_SLOTS = {"map": None, "used": set()}
+
+
+def set_grad_slots(mapping) -> None:
+    """{parameter data_ptr: fp32 view} for the next backward, or None (fresh gradient buffers)."""
+    _GRAD_SLOTS["map"] = mapping
+    _GRAD_SLOTS["used"] = set()
+
+
+def _pkey(t):
+    """The slot key of a parameter (its data pointer), None for a non-leaf / absent tensor."""
+    return t.data_ptr() if (t is not None and t.is_leaf and t.requires_grad) else None
+
+
+def _grad_buf(key, shape, device) -> torch.Tensor:
+    """The output buffer of one parameter gradient: its armed slot (a flat-buffer view of the same shape), else
+    a fresh fp32 tensor."""
+    m = _GRAD_SLOTS["map"]
+    if m is not None and key is not None and key not in _GRAD_SLOTS["used"]:
+        v = m.get(key)
+        if v is not None and tuple(v.shape) == tuple(shape):
+            _GRAD_SLOTS["used"].add(key)
+            # a NEW tensor object on the slot's memory: AccumulateGrad steals a gradient only when nothing else
+            # references it -- handed the map's own view it would clone it, on the stream, before the deferred
+            # weight-gradient kernels have written it
+            return v.view(v.shape)
+    return torch.empty(tuple(shape), device=device, dtype=torch.float32)
+
+
+def _grad_buf_stacked(keys, shapes, rows, K, device):
+    """[sum(rows), K] buffer for weights stacked along N (q|k|v): one region of the flat buffer when every
+    weight has a slot and the slots lie back to back in stacking order, else a fresh tensor."""
+    m = _GRAD_SLOTS["map"]
+    if m is not None and all(k is not None and k not in _GRAD_SLOTS["used"] and k in m for k in keys):
+        vs = [m[k] for k in keys]
+        ok = all(tuple(v.shape) == tuple(sh) for v, sh in zip(vs, shapes))
+        off = vs[0].data_ptr()
+        for v, r in zip(vs, rows):
+            ok = ok and v.data_ptr() == off
+            off += r * K * 4
+        if ok:
+            _GRAD_SLOTS["used"].update(keys)
+            return vs[0].as_strided((sum(rows), K), (K, 1))
+    return torch.empty(sum(rows), K, device=device, dtype=torch.float32)
+
+
 def _wgrad(dY, To_full, out_stride, out_off, A, Ti, To, nb, in_stride, offs, cin, N_, dw, strides, *, prec,
            a_scale=None, db=None, rows_per_step=-1, target_blocks=-1, depth=-1):
     if _SIDE_WGRAD["on"] and dY.is_cuda:
@@ -968,6 +1019,7 @@ class _ConvTM(torch.autograd.Function):
               residual=_f32c(residual))
         ctx.save_for_backward(x, weight, mask, out_scale, y if act != ACT_NONE else None)
         ctx.leaf = _leaves(weight, bias)
+        ctx.keys = (_pkey(weight), _pkey(bias))
         ctx.cfg = (stride, padding, prec, bias is not None, act, dropout_p, seed, residual is not None)
         return y
 
@@ -1022,8 +1074,8 @@ class _ConvTM(torch.autograd.Function):
             if other is not None and not fuse:  # bf16 x or an unusual layout: autograd's sum, done here
                 dx = dx + other
         if ctx.needs_input_grad[1] or (has_bias and ctx.needs_input_grad[2]):
-            dw = torch.empty(weight.shape, device=x.device, dtype=torch.float32)
-            db = torch.empty(Cout, device=x.device, dtype=torch.float32) if has_bias else None
+            dw = _grad_buf(ctx.keys[0], weight.shape, x.device)
+            db = _grad_buf(ctx.keys[1], (Cout,), x.device) if has_bias else None
             _wgrad(dy, To, 1, 0, x, Ti, To, B, stride, [j - pad for j in range(k)], Cin, Cout, dw,
                    (Cin * k, k, 1), prec=prec, a_scale=mask, db=db)
         if role == "give" and dx is not None:  # handed to the "take" conv of the same x (GradLink)
@@ -1057,6 +1109,7 @@ class _ConvTransposeTM(torch.autograd.Function):
         ctx.wd = packed(spec_convT_dgrad(weight), prec) if ctx.needs_input_grad[0] else None
         ctx.save_for_backward(x, weight, mask)
         ctx.leaf = _leaves(weight, bias)
+        ctx.keys = (_pkey(weight), _pkey(bias))
         ctx.cfg = (prec, bias is not None)
         return y
 
@@ -1079,14 +1132,14 @@ class _ConvTransposeTM(torch.autograd.Function):
             _gemm(dy, T2, T, B, s, offs, Cout, Wd, Kp, Cin, dx, T, prec=prec, c_scale=mask)
         if ctx.needs_input_grad[1]:
             xm = x * mask.unsqueeze(-1) if mask is not None else x
-            dw = torch.empty(weight.shape, device=x.device, dtype=torch.float32)
+            dw = _grad_buf(ctx.keys[0], weight.shape, x.device)
             # dW[c, n, j] = sum_s xm[s, c] dy[2s + j - pad, n]
             _wgrad(xm, T, 1, 0, dy, T2, T, B, s, offs, Cout, Cin, dw,
                    (weight.stride(0), weight.stride(1), weight.stride(2)), prec=prec)
         if has_bias and ctx.needs_input_grad[2]:
             # column sums of dy (rows may be strided: a slice of the concat gradient) in a fixed order:
             # 128-row partials + a job in the step's batched gradient sums (torch's reduction: 26 us)
-            db = torch.empty(Cout, device=dy.device, dtype=torch.float32)
+            db = _grad_buf(ctx.keys[1], (Cout,), dy.device)
             rows = B * T2
             ws = torch.empty(int(N.lib().mtts_colsum_workspace_size(rows, Cout)) // 4, device=dy.device,
                              dtype=torch.float32)
@@ -1121,6 +1174,7 @@ class _LinearTM(torch.autograd.Function):
               dropout_p=dropout_p, seed=seed, a_scale=ins, c_scale=outs)
         ctx.save_for_backward(x2, ins, outs)
         ctx.leaf = _leaves(bias, *weights)
+        ctx.keys = (_pkey(bias), [_pkey(w) for w in weights])
         ctx.cfg = (prec, bias is not None, residual is not None, shp, dropout_p, seed,
                    [w.shape[0] for w in weights], K)
         ctx.wshapes = [w.shape for w in weights]
@@ -1166,8 +1220,11 @@ class _LinearTM(torch.autograd.Function):
             if other is not None and not fuse:
                 dx = dx + other
         if any(ctx.needs_input_grad[6:]) or (has_bias and ctx.needs_input_grad[1]):
-            dw = torch.empty(Np, K, device=dy2.device, dtype=torch.float32)
-            db = torch.empty(Np, device=dy2.device, dtype=torch.float32) if has_bias else None
+            bkey, wkeys = ctx.keys
+            dw = _grad_buf_stacked(wkeys, ctx.wshapes, rows, K, dy2.device) if Np == Nout else \
+                torch.empty(Np, K, device=dy2.device, dtype=torch.float32)
+            db = (_grad_buf(bkey, (Np,), dy2.device) if Np == Nout else
+                  torch.empty(Np, device=dy2.device, dtype=torch.float32)) if has_bias else None
             _wgrad(dy2, M, 1, 0, x2, M, M, 1, 1, [0], K, Np, dw, (K, 1, 0), prec=prec, db=db, a_scale=ins)
             dws = [d.view(w_shape) for d, w_shape in zip(dw[:Nout].split(rows, dim=0), ctx.wshapes)]
             db = db[:Nout] if db is not None else None
@@ -1206,6 +1263,7 @@ class _FeedForwardTM(torch.autograd.Function):
         _gemm(h, M, M, 1, 1, [0], H, W2p, K2p, Nout, y, M, prec=prec, bias=_f32c(b2), residual=res2)
         ctx.save_for_backward(x2, z, h, w1, w2)
         ctx.leaf = _leaves(w1, b1, w2, b2)
+        ctx.keys = (_pkey(w1), _pkey(b1), _pkey(w2), _pkey(b2))
         ctx.cfg = (prec, shp, residual is not None, dropout_p, seed, b1 is not None, b2 is not None)
         return y.reshape(*shp[:-1], Nout)
 
@@ -1219,15 +1277,16 @@ class _FeedForwardTM(torch.autograd.Function):
         dy2 = _f32c(dy).reshape(-1, Nout)
         M = dy2.shape[0]
         dev = dy2.device
-        dw2 = torch.empty(w2.shape, device=dev, dtype=torch.float32)
-        db2 = torch.empty(Nout, device=dev, dtype=torch.float32)
+        kw1, kb1, kw2, kb2 = ctx.keys
+        dw2 = _grad_buf(kw2, w2.shape, dev)
+        db2 = _grad_buf(kb2 if has_b2 else None, (Nout,), dev)
         _wgrad(dy2, M, 1, 0, h, M, M, 1, 1, [0], H, Nout, dw2, (H, 1, 0), prec=prec, db=db2)
         W2t, K2p = ctx.w2t
         dz = torch.empty(M, H, device=dev, dtype=torch.float32)
         _gemm(dy2, M, M, 1, 1, [0], Nout, W2t, K2p, H, dz, M, prec=prec, act=ACT_DGELU, aux=z, dropout_p=p,
               seed=seed)
-        dw1 = torch.empty(w1.shape, device=dev, dtype=torch.float32)
-        db1 = torch.empty(H, device=dev, dtype=torch.float32)
+        dw1 = _grad_buf(kw1, w1.shape, dev)
+        db1 = _grad_buf(kb1 if has_b1 else None, (H,), dev)
         _wgrad(dz, M, 1, 0, x2, M, M, 1, 1, [0], K, H, dw1, (K, 1, 0), prec=prec, db=db1)
         dx = None
         if ctx.needs_input_grad[0]:
@@ -1277,6 +1336,7 @@ class _ConvFFNTM(torch.autograd.Function):
               seed=s2, residual=_f32c(residual), c_scale=m)
         ctx.save_for_backward(x, h, m)
         ctx.leaf = _leaves(w1, b1, w2, b2)
+        ctx.keys = (_pkey(w1), _pkey(b1), _pkey(w2), _pkey(b2))
         ctx.cfg = (prec, k, p_in, p_out, s1, s2, residual is not None, w1.shape, w2.shape)
         return y
 
@@ -1308,15 +1368,16 @@ class _ConvFFNTM(torch.autograd.Function):
                 N.check(N.lib().mtts_act_dropout_bwd(g.data_ptr(), None, dz2.data_ptr(), B * T, Cout, Cout, ACT_NONE,
                                                      float(p_out), s2.data_ptr(), _stream(g)), "mtts_act_dropout_bwd")
         dres = g if has_res else None
-        dw2 = torch.empty(w2s, device=x.device, dtype=torch.float32)
-        db2 = torch.empty(Cout, device=x.device, dtype=torch.float32)
+        kw1, kb1, kw2, kb2 = ctx.keys
+        dw2 = _grad_buf(kw2, w2s, x.device)
+        db2 = _grad_buf(kb2, (Cout,), x.device)
         _wgrad(dz2, T, 1, 0, h, T, T, B, 1, offs, F_, Cout, dw2, (F_ * k, k, 1), prec=prec, db=db2)
         W2d, K2d = ctx.w2d
         dz1 = torch.empty_like(h)  # d(conv1 pre-activation) = dgrad * [h > 0] * keep_in / (1 - p_in)
         _gemm(dz2, T, T, B, 1, doffs, Cout, W2d, K2d, F_, dz1, T, prec=prec, act=ACT_DRELU, aux=h,
               dropout_p=p_in, seed=s1)
-        dw1 = torch.empty(w1s, device=x.device, dtype=torch.float32)
-        db1 = torch.empty(F_, device=x.device, dtype=torch.float32)
+        dw1 = _grad_buf(kw1, w1s, x.device)
+        db1 = _grad_buf(kb1, (F_,), x.device)
         _wgrad(dz1, T, 1, 0, x, T, T, B, 1, offs, Cin, F_, dw1, (Cin * k, k, 1), prec=prec, a_scale=m, db=db1)
         dx = None
         if ctx.needs_input_grad[0]:
@@ -1358,6 +1419,7 @@ class _GroupNormMishTM(torch.autograd.Function):
                                             groups, float(eps), flags, _stream(h)), "mtts_gn_mish_fwd")
         ctx.save_for_backward(h, gamma_c, beta_c, mask_c, mean, rstd)
         ctx.leaf = _leaves(gamma, beta)
+        ctx.keys = (_pkey(gamma), _pkey(beta))
         ctx.cfg = (groups, add is not None)
         return y
 
@@ -1370,8 +1432,8 @@ class _GroupNormMishTM(torch.autograd.Function):
         dy = dy.contiguous() if (h16 and dy.dtype == torch.bfloat16) else _f32c(dy)
         B, T, C = h.shape
         dh = torch.empty_like(h)
-        dg = torch.empty(C, device=h.device, dtype=torch.float32)
-        dbt = torch.empty_like(dg)
+        dg = _grad_buf(ctx.keys[0], (C,), h.device)
+        dbt = _grad_buf(ctx.keys[1], (C,), h.device)
         dadd = torch.empty(B, C, device=h.device, dtype=torch.float32) if has_add else None
         flags = (NORM_F_X_BF16 | NORM_F_Y_BF16 if h16 else 0) | (NORM_F_DY_BF16 if dy.dtype == torch.bfloat16 else 0)
         lib = N.lib()
@@ -1404,6 +1466,7 @@ class _LayerNormTM(torch.autograd.Function):
                                            N.ptr(seed), _stream(x2)), "mtts_layernorm_fwd")
         ctx.save_for_backward(x2, w_c, b_c, mean, rstd)
         ctx.leaf = _leaves(w, b)
+        ctx.keys = (_pkey(w), _pkey(b))
         ctx.cfg = (shp, act, float(dropout_p), seed)
         return y.reshape(shp)
 
@@ -1415,8 +1478,8 @@ class _LayerNormTM(torch.autograd.Function):
         M, C = x2.shape
         dy2 = _f32c(dy).reshape(M, C)
         dx = torch.empty_like(x2)
-        dw = torch.empty(C, device=x2.device, dtype=torch.float32)
-        db = torch.empty_like(dw)
+        dw = _grad_buf(ctx.keys[0], (C,), x2.device)
+        db = _grad_buf(ctx.keys[1], (C,), x2.device)
         lib = N.lib()
         ws = torch.empty(max(int(lib.mtts_layernorm_bwd_workspace_size(M, C)), 1), dtype=torch.uint8,
                          device=x2.device)
@@ -1639,11 +1702,11 @@ def _ln_fwd(h2, w, b, eps, y16):
     return n, mean, rstd
 
 
-def _ln_bwd_res(dn, h2, w, b, mean, rstd, dres):
+def _ln_bwd_res(dn, h2, w, b, mean, rstd, dres, keys=(None, None)):
     M, C = h2.shape
     dh = torch.empty_like(h2)
-    dw = torch.empty(C, device=h2.device, dtype=torch.float32)
-    db = torch.empty_like(dw)
+    dw = _grad_buf(keys[0], (C,), h2.device)
+    db = _grad_buf(keys[1], (C,), h2.device)
     lib = N.lib()
     ws = torch.empty(max(int(lib.mtts_layernorm_bwd_workspace_size(M, C)), 1), dtype=torch.uint8, device=h2.device)
     _keep_partials(ws)
@@ -1687,6 +1750,7 @@ class _PreLNAttentionTM(torch.autograd.Function):
               residual=h2, dropout_p=dropout_p, seed=seed)
         ctx.save_for_backward(h2, lnw, lnb, mean, rstd, n, qkv, bias, o, lse)
         ctx.leaf = _leaves(ln_w, ln_b, w_out, b_out, wq, wk, wv)
+        ctx.keys = (_pkey(ln_w), _pkey(ln_b), _pkey(w_out), _pkey(b_out), [_pkey(w) for w in (wq, wk, wv)])
         ctx.cfg = (prec, shp, heads, float(dropout_p), seed, [w.shape for w in (wq, wk, wv)], b_out is not None)
         return y.reshape(shp)
 
@@ -1706,8 +1770,9 @@ class _PreLNAttentionTM(torch.autograd.Function):
             N.check(N.lib().mtts_dropout_apply(dres.data_ptr(), g.data_ptr(), M, C, C, float(p), seed.data_ptr(),
                                                _stream(g)), "mtts_dropout_apply")
         # to_out: weight + bias gradient, dgrad -> dO
-        dwo = torch.empty(C, Ci, device=dev, dtype=torch.float32)
-        dbo = torch.empty(C, device=dev, dtype=torch.float32) if has_bout else None
+        klw, klb, kwo, kbo, kqkv = ctx.keys
+        dwo = _grad_buf(kwo, (C, Ci), dev)
+        dbo = _grad_buf(kbo, (C,), dev) if has_bout else None
         _wgrad(g, M, 1, 0, o.view(M, Ci), M, M, 1, 1, [0], Ci, C, dwo, (Ci, 1, 0), prec=prec, db=dbo)
         Wot, Kot = ctx.wo_t
         do = torch.empty(B, T, Ci, device=dev, dtype=qkv.dtype)  # stored like q|k|v
@@ -1716,12 +1781,12 @@ class _PreLNAttentionTM(torch.autograd.Function):
         dqkv = _attn_bwd(do, qkv, bias, o, lse, heads, prec)
         # stacked q|k|v projection: weight gradients (A = the bf16 / fp32 LayerNorm output), dgrad -> dn
         dq2 = dqkv.view(M, C3)
-        dwqkv = torch.empty(C3, C, device=dev, dtype=torch.float32)
+        dwqkv = _grad_buf_stacked(kqkv, qshapes, [s_[0] for s_ in qshapes], C, dev)
         _wgrad(dq2, M, 1, 0, n, M, M, 1, 1, [0], C, C3, dwqkv, (C, 1, 0), prec=prec)
         Wqt, Kqt = ctx.wqkv_t
         dn = torch.empty(M, C, device=dev, dtype=torch.float32)
         _gemm(dq2, M, M, 1, 1, [0], C3, Wqt, Kqt, C, dn, M, prec=prec)
-        dh, dlnw, dlnb = _ln_bwd_res(dn, h2, lnw, lnb, mean, rstd, dres)
+        dh, dlnw, dlnb = _ln_bwd_res(dn, h2, lnw, lnb, mean, rstd, dres, (klw, klb))
         dwq, dwk, dwv = (d.view(s_) for d, s_ in zip(dwqkv.split([s_[0] for s_ in qshapes], dim=0), qshapes))
         return dh.reshape(shp), dlnw, dlnb, None, None, None, None, dwo, dbo, dwq, dwk, dwv
 
@@ -1758,6 +1823,7 @@ class _PreLNFeedForwardTM(torch.autograd.Function):
         _gemm(hid, M, M, 1, 1, [0], H, W2p, K2p, C, y, M, prec=prec, bias=_f32c(b2), residual=h2)
         ctx.save_for_backward(h2, lnw, lnb, mean, rstd, n, z, hid)
         ctx.leaf = _leaves(ln_w, ln_b, w1, b1, w2, b2)
+        ctx.keys = tuple(_pkey(t) for t in (ln_w, ln_b, w1, b1, w2, b2))
         ctx.cfg = (prec, shp, float(dropout_p), seed, w1.shape, w2.shape, b1 is not None, b2 is not None)
         return y.reshape(shp)
 
@@ -1770,20 +1836,21 @@ class _PreLNFeedForwardTM(torch.autograd.Function):
         H = w1s[0]
         dev = h2.device
         dy2 = _f32c(dy).reshape(M, C)  # also the residual branch's gradient
-        dw2 = torch.empty(w2s, device=dev, dtype=torch.float32)
-        db2 = torch.empty(C, device=dev, dtype=torch.float32) if has_b2 else None
+        klw, klb, kw1, kb1, kw2, kb2 = ctx.keys
+        dw2 = _grad_buf(kw2, w2s, dev)
+        db2 = _grad_buf(kb2, (C,), dev) if has_b2 else None
         _wgrad(dy2, M, 1, 0, hid, M, M, 1, 1, [0], H, C, dw2, (H, 1, 0), prec=prec, db=db2)
         W2t, K2p = ctx.w2t
         # d(pre-activation): bf16 in bf16-mixed -- only the next dgrad GEMM and dW1 read it
         dz = torch.empty(M, H, device=dev, dtype=torch.bfloat16 if prec == PREC_BF16 else torch.float32)
         _gemm(dy2, M, M, 1, 1, [0], C, W2t, K2p, H, dz, M, prec=prec, act=ACT_DGELU, aux=z, dropout_p=p, seed=seed)
-        dw1 = torch.empty(w1s, device=dev, dtype=torch.float32)
-        db1 = torch.empty(H, device=dev, dtype=torch.float32) if has_b1 else None
+        dw1 = _grad_buf(kw1, w1s, dev)
+        db1 = _grad_buf(kb1, (H,), dev) if has_b1 else None
         _wgrad(dz, M, 1, 0, n, M, M, 1, 1, [0], C, H, dw1, (C, 1, 0), prec=prec, db=db1)
         W1t, K1p = ctx.w1t
         dn = torch.empty(M, C, device=dev, dtype=torch.float32)
         _gemm(dz, M, M, 1, 1, [0], H, W1t, K1p, C, dn, M, prec=prec)
-        dh, dlnw, dlnb = _ln_bwd_res(dn, h2, lnw, lnb, mean, rstd, dy2)
+        dh, dlnw, dlnb = _ln_bwd_res(dn, h2, lnw, lnb, mean, rstd, dy2, (klw, klb))
         return dh.reshape(shp), dlnw, dlnb, None, dw1, db1, dw2, db2, None
 
 

@@ -104,6 +104,8 @@ class _FlatClipAdamW:
         self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)
         self.lr, self.max_norm = lr, float(max_norm or 0.0)
         self.betas, self.eps, self.wd = betas, eps, weight_decay
+        # gradients are SUMS over grad_scale^-1 data-parallel ranks (RcclComm: ncclSum); the mean is taken here
+        self.grad_scale = 1.0
         self._table = None
         self._key = None
         self._ws = None
@@ -144,10 +146,12 @@ class _FlatClipAdamW:
         else:
             self._build()
         b1, b2 = self.betas
-        N.check(N.lib().mtts_clip_adamw(N.ptr(self._table), self._n, N.ptr(self.flat), N.ptr(self.exp_avg),
-                                        N.ptr(self.exp_avg_sq), N.ptr(self.lr), N.ptr(self.step_t), self.max_norm,
-                                        b1, b2, self.eps, self.wd, N.ptr(self._ws), self._ws.numel(),
-                                        torch.cuda.current_stream(self.flat.device).cuda_stream), "mtts_clip_adamw")
+        N.check(N.lib().mtts_clip_adamw_scaled(N.ptr(self._table), self._n, N.ptr(self.flat), N.ptr(self.exp_avg),
+                                               N.ptr(self.exp_avg_sq), N.ptr(self.lr), N.ptr(self.step_t),
+                                               self.max_norm, b1, b2, self.eps, self.wd, self.grad_scale,
+                                               N.ptr(self._ws), self._ws.numel(),
+                                               torch.cuda.current_stream(self.flat.device).cuda_stream),
+                "mtts_clip_adamw_scaled")
 
     def state_snapshot(self):
         return [t.clone() for t in (self.exp_avg, self.exp_avg_sq, self.step_t)]
@@ -166,6 +170,10 @@ N.register("mtts_clip_adamw", ctypes.c_int,
            [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_void_p, ctypes.c_float, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
             ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p])
+N.register("mtts_clip_adamw_scaled", ctypes.c_int,
+           [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_float, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+            ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p])
 
 
 @dataclass
@@ -411,6 +419,28 @@ class Trainer:
             torch.nn.utils.clip_grad_norm_(self.params, self.cfg.gradient_clip_val, foreach=True)
         self.optimizer.step()
 
+    def _group_stacked(self, order):
+        """The recorded backward order with the weights that one stacked GEMM produces (q|k|v of the decoder's
+        attention and of the text encoder's) placed back to back in stacking order, so that their flat-buffer
+        views form one region the stacked weight-gradient GEMM writes in place (_ops._grad_buf_stacked)."""
+        groups = []
+        for m in self.model.modules():
+            for names in (("to_q", "to_k", "to_v"), ("query_conv", "key_conv", "value_conv")):
+                if all(isinstance(getattr(m, n, None), torch.nn.Module) for n in names):
+                    groups.append([getattr(m, n).weight for n in names])
+        member = {id(p): g for g in groups for p in g}
+        present = {id(p) for p in order}
+        out, done = [], set()
+        for p in order:
+            g = member.get(id(p))
+            if g is not None and all(id(q) in present for q in g):
+                if id(p) not in done:
+                    out.extend(g)
+                    done.update(id(q) for q in g)
+            else:
+                out.append(p)
+        return out
+
     def _ensure_reducer(self, batches, run_step):
         """First DP step: one pass with an arrival recorder fixes the bucket layout (backward order)."""
         if self.reducer is not None:
@@ -422,7 +452,7 @@ class Trainer:
             logged = run_step()
         finally:
             rec.remove()
-        order = rec.order
+        order = self._group_stacked(rec.order)
         if self.world > 1:  # one bucket layout on every rank: rank 0's recorded backward order
             index = {id(p): i for i, p in enumerate(self.params)}
             box = [[index[id(p)] for p in order]]
@@ -439,6 +469,9 @@ class Trainer:
             if first_enc is not None:
                 seams, mb = (first_enc,), max(mb, self.cfg.seam_bucket_mb)
         self.reducer = DP.GradBucketReducer(order, comm, mb, self.dev, seams=seams)
+        if isinstance(self.optimizer, _FlatClipAdamW):  # the mean over ranks rides in the fused optimizer step
+            self.optimizer.grad_scale = comm.post_scale
+            self.reducer.grad_scale_applied = True
         if comm.capturable:
             self.reducer.warm()  # every rank, now: later captures run without any collective
         return logged
@@ -466,6 +499,7 @@ class Trainer:
                 self._fwd_bwd(batches)
             finally:
                 self._arm = None
+                OPS.set_grad_slots(None)  # an aborted backward leaves no slots armed
             self.reducer.finish()
             logged = self.reducer.scalars().clone()
         else:
@@ -508,6 +542,7 @@ class Trainer:
                         self._fwd_bwd(static)
                     finally:
                         self._arm = None
+                        OPS.set_grad_slots(None)  # an aborted backward leaves no slots armed
                     self.reducer.finish()
                 else:
                     self._fwd_bwd(static)
@@ -539,6 +574,7 @@ class Trainer:
                     e["logged"] = self._fwd_bwd(static)
                 finally:
                     self._arm = None
+                    OPS.set_grad_slots(None)  # an aborted backward leaves no slots armed
                 self.reducer.finish()  # joins the forked all-reduces; .grad -> flat views
                 if overlap:
                     self._clip_and_update()
