@@ -169,7 +169,7 @@ def _bucketed_batches(B, Tx, Ty, n, rank, world, dev):
 
 # kernel families of the step, by the kernel's own name in a rocprofv3 trace
 FAMILIES = {
-    "gemm": ("conv_gemm_kernel", "conv_gemm_glds_kernel", "splitk_epilogue_kernel"),
+    "gemm": ("conv_gemm_kernel", "conv_gemm_glds_kernel", "conv_gemm_wreg_kernel", "splitk_epilogue_kernel"),
     # weight-gradient GEMMs + the step's batched fixed-order partial sums (reduce_partials_kernel: the split
     # slabs, and the LayerNorm / GroupNorm / bias partials that ride in the same launches)
     "wgrad": ("conv_wgrad_kernel", "reduce_partials_kernel"),
@@ -639,8 +639,8 @@ def main():
                 "frac": round(tf / gemm_peak, 4), **line}
 
     gemm_roofline = roofline_of(
-        gemm_log, "gemm", "conv_gemm_kernel + conv_gemm_glds_kernel (+ splitk_epilogue_kernel): decoder + encoder "
-        "implicit-GEMM conv / linear, forward and dgrad",
+        gemm_log, "gemm", "conv_gemm_kernel + conv_gemm_glds_kernel + conv_gemm_wreg_kernel (+ splitk_epilogue_kernel): "
+        "decoder + encoder implicit-GEMM conv / linear, forward and dgrad",
         "time = the family's kernel time in one graph-replayed step (rocprofv3 trace of this command's child) / "
         "launches; bytes = A rows read once + packed W (both planes when split) + C written (+ aux / residual / "
         "pre-activation streams) per launch; FLOP = 2 M N K")
