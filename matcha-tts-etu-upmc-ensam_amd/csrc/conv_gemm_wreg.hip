@@ -190,7 +190,8 @@ int launch_wreg_e(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
 template <bool ABF16, int NPL, int KS>
 int launch_wreg_t(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
     const bool rm = p.a_scale != nullptr;
-    switch (mtts::gemm_epilogue_kind(p)) {
+    static const bool rt_only = [] { const char *e = getenv("MTTS_WREG_EK_RT"); return e && e[0] == '1'; }();
+    switch (rt_only ? (int)mtts::EK_RT : mtts::gemm_epilogue_kind(p)) {
         case mtts::EK_LIN_C16:
             return rm ? launch_wreg_e<ABF16, NPL, KS, mtts::EK_LIN_C16, true>(p, M, st)
                       : launch_wreg_e<ABF16, NPL, KS, mtts::EK_LIN_C16, false>(p, M, st);

@@ -351,11 +351,24 @@ __device__ __forceinline__ void gemm_epilogue_vec_v(const mtts_conv_gemm_args &p
     }
 }
 
+// The kind is classified once per call (wave-uniform) and each kind runs its own compile-time-specialised
+// epilogue: the generic one spent ~300 scalar instructions per 32 x 32 tile re-testing p.act / p.flags / null
+// pointers (PMC SQ_INSTS_SALU, profiles/r05/wreg/pmc_ff1_first/); specialised, the weight-stationary kernel's
+// launches ran 13 % faster (964 vs 1114 us per step, profiles/r05/wreg/replay_ek_*.jsonl).
 template <int TM, int TN>
 __device__ __forceinline__ void gemm_epilogue_vec(const mtts_conv_gemm_args &p, f32x16 (&acc)[TM][TN], float *stage,
                                                   int row0, int col0, int lane) {
-    if (gemm_epilogue_vec8_ok(p)) gemm_epilogue_vec_v<8>(p, acc, stage, row0, col0, lane);
-    else gemm_epilogue_vec_v<4>(p, acc, stage, row0, col0, lane);
+    if (!gemm_epilogue_vec8_ok(p)) {
+        gemm_epilogue_vec_v<4>(p, acc, stage, row0, col0, lane);
+        return;
+    }
+    switch (gemm_epilogue_kind(p)) {
+        case EK_LIN_C16: gemm_epilogue_vec_v<8, TM, TN, EK_LIN_C16>(p, acc, stage, row0, col0, lane); break;
+        case EK_LIN_C32: gemm_epilogue_vec_v<8, TM, TN, EK_LIN_C32>(p, acc, stage, row0, col0, lane); break;
+        case EK_GELU: gemm_epilogue_vec_v<8, TM, TN, EK_GELU>(p, acc, stage, row0, col0, lane); break;
+        case EK_DGELU: gemm_epilogue_vec_v<8, TM, TN, EK_DGELU>(p, acc, stage, row0, col0, lane); break;
+        default: gemm_epilogue_vec_v<8, TM, TN, EK_RT>(p, acc, stage, row0, col0, lane); break;
+    }
 }
 
 }  // namespace mtts
