@@ -44,7 +44,7 @@ extern "C" {
 #define MTTS_CONV_MAX_TAPS 8
 #define MTTS_GEMM_GLDS 32  /* schedule ids 32.. : bf16 LDS-DMA kernels (csrc/conv_gemm_glds.hip)   */
 #define MTTS_GEMM_PK 64    /* schedule ids 64.. : bf16 persistent big-tile LDS-DMA kernels (csrc/conv_gemm_pk.hip) */
-#define MTTS_GEMM_WREG 96  /* schedule id 96    : bf16 weight-stationary kernel, K <= 256 linears (csrc/conv_gemm_wreg.hip) */
+#define MTTS_GEMM_WREG 96  /* schedule ids 96, 97: bf16 weight-stationary kernels, K <= 256 linears (csrc/conv_gemm_wreg.hip) and K = 512..1024 convs / linears (csrc/conv_gemm_wreg16.hip) */
 
 /*
  * Implicit GEMM  C[row(b,u), n] = epi( sum_{j<ntaps} sum_{c<cin} A[b*Ti + u*in_stride + off[j], c]

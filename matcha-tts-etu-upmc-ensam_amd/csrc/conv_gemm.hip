@@ -1165,7 +1165,7 @@ struct GemmPlan {
 static GemmPlan plan_gemm(const mtts_conv_gemm_args &p, bool bf16, int cfg, int splits) {
     const int M = p.nb * p.To;
     if (cfg < 0) cfg = pick_cfg(p, M, bf16);
-    if (cfg == MTTS_GEMM_WREG) return {cfg, 1, 0};
+    if (cfg == MTTS_GEMM_WREG || cfg == MTTS_GEMM_WREG + 1) return {cfg, 1, 0};
     if (cfg >= MTTS_GEMM_PK) return {cfg, 1, mtts::conv_gemm_pk_workspace_bytes(cfg - MTTS_GEMM_PK, p, !bf16)};
     splits = pick_splits(p, M, cfg, splits, bf16);
     size_t ws = 0;
@@ -1201,6 +1201,8 @@ static int resolve_cfg(const mtts_conv_gemm_args &p, bool bf16, int cfg, int M, 
     static const bool wreg_pick = [] { const char *e = getenv("MTTS_GEMM_WREG_PICK"); return !(e && e[0] == '0'); }();
     if (cfg < 0 && bf16 && wreg_pick && mtts::conv_gemm_wreg_applies(p) && mtts::conv_gemm_wreg_preferred(p, M))
         return MTTS_GEMM_WREG;
+    if (cfg < 0 && bf16 && wreg_pick && mtts::conv_gemm_wreg16_applies(p) && mtts::conv_gemm_wreg16_preferred(p, M))
+        return MTTS_GEMM_WREG + 1;
     static const bool ws_pick = [] { const char *e = getenv("MTTS_GEMM_WS_PICK"); return !(e && e[0] == '0'); }();
     if (cfg < 0 && bf16 && ws_pick && (p.flags & MTTS_GEMM_F_W_SPLIT) && !(p.flags & MTTS_GEMM_F_A_SPLIT))
         cfg = pick_cfg_ws(p, M);
@@ -1246,8 +1248,9 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
                    "conv_gemm: a split A needs split weight planes and an fp32 A");
     const bool glds_id = cfg >= MTTS_GEMM_GLDS && cfg < MTTS_GEMM_GLDS + mtts::conv_gemm_glds_num_cfgs();
     const bool pk_id = cfg >= MTTS_GEMM_PK && cfg < MTTS_GEMM_PK + mtts::conv_gemm_pk_num_cfgs();
-    const bool wreg_id = cfg == MTTS_GEMM_WREG;
-    MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || glds_id || pk_id || wreg_id, "conv_gemm: bad tile config");
+    const bool wreg_id = cfg == MTTS_GEMM_WREG, wreg16_id = cfg == MTTS_GEMM_WREG + 1;
+    MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || glds_id || pk_id || wreg_id || wreg16_id,
+                   "conv_gemm: bad tile config");
     MTTS_CHECK_ARG(splits >= 0, "conv_gemm: bad split count");
     const int M = p.nb * p.To;
     if (M == 0) return MTTS_OK;
@@ -1264,12 +1267,19 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
                               "conv_gemm: weight-stationary schedule needs bf16, one stride-1 tap, K in {80,160,192,256}");
         return mtts::conv_gemm_wreg_launch(p, M, st);
     }
+    if (wreg16_id) {
+        if (!bf16 || !mtts::conv_gemm_wreg16_applies(p))
+            return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: 16-column weight-stationary schedule needs bf16, a bf16 A "
+                                                    "and (taps, cin) in {(3, 256), (1, 512), (1, 1024)}");
+        return mtts::conv_gemm_wreg16_launch(p, M, st);
+    }
     if (glds_id && (!bf16 || !mtts::conv_gemm_glds_applies(p)))
         return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: LDS-DMA schedule needs bf16, cin >= 64 and a 0/1 a_scale");
     cfg = resolve_cfg(p, bf16, cfg, M, &rc);
     if (rc) return rc;
     const GemmPlan pl = plan_gemm(p, bf16, cfg, splits);
     if (pl.cfg == MTTS_GEMM_WREG) return mtts::conv_gemm_wreg_launch(p, M, st);
+    if (pl.cfg == MTTS_GEMM_WREG + 1) return mtts::conv_gemm_wreg16_launch(p, M, st);
     if (pl.cfg >= MTTS_GEMM_GLDS) {
         int s = pl.splits;
         if (pl.ws > 0 && (!ws || ws_bytes < pl.ws || (uintptr_t)ws % 16)) s = 1;  // no workspace: unsplit

@@ -1,0 +1,300 @@
+// Weight-stationary bf16 GEMM for the longer reductions (round 5): K = 512 / 768 / 1024 -- the decoder's k = 3
+// convs over 256 channels (forward and dgrad), the FeedForward down-projection (K = 1024) and its dgrad -- behind
+// mtts_conv_gemm (include/mtts_decoder.h), schedule id MTTS_GEMM_WREG + 1.
+//
+// conv_gemm_wreg.hip holds a wave's W slice as 32x32x16 B fragments (32 columns x K <= 256); here the slice is 16
+// columns x K as v_mfma_f32_16x16x32_bf16 B fragments: K / 32 x 4 VGPRs per plane, 256 registers for K = 1024 on
+// two planes -- one wave per SIMD, the accumulators in AGPRs.  A workgroup (4 waves, 64 columns) walks 32-row
+// tiles of A through an LDS-DMA ring; a k = 3 conv stages ONE image of 32 + 2 input rows per tile and reads it at
+// the three tap offsets (the implicit GEMM's gather costs no extra fill), zeroing the fragments whose tap row falls
+// outside the utterance or on a masked row (the 0/1 row mask is staged beside the image).  Per output element the
+// MFMAs run 32-wide K steps ascending, hi plane before lo plane: deterministic, but NOT the 32x32x16 kernels' order
+// (tests/test_gemm_wreg_gpu.py: against float64 and run to run).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+
+#include "conv_gemm_wreg.h"
+#include "gemm_epilogue.h"
+#include "lds_dma.h"
+#include "mtts_common.h"
+#include "mtts_decoder.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+using mtts::u32x4;
+
+constexpr int kNW = 4, kNT = 64 * kNW;  // 4 waves x 16 columns = 64 columns per workgroup
+constexpr int kBM = 32;                  // rows per A tile (two 16-row MFMA blocks)
+constexpr uint32_t kOob = mtts::kDmaOob;
+
+// One tile's image: rows kBM + NTAP - 1 of CIN bf16 channels (16-byte chunk c of row i at c ^ (i & 15): the 16
+// rows of a fragment read spread over the banks), padded to whole 4 KiB (one 1 KiB piece per wave), then the
+// per-wave 0/1 row-mask slots (64 floats each).
+template <int NTAP, int CIN>
+struct G16 {
+    static constexpr int K = NTAP * CIN, KS = K / 32;
+    static constexpr int ROWB = CIN * 2;
+    static constexpr int ROWS = kBM + NTAP - 1;
+    static constexpr int IMG = (ROWS * ROWB + 4095) / 4096 * 4096;
+    static constexpr int PER_WAVE = IMG / 1024 / kNW;
+    static constexpr int MASKB = kNW * 256;
+    static constexpr int STAGE = IMG + MASKB;
+    static constexpr int S = STAGE <= 40 * 1024 ? 3 : 2;
+    static_assert(ROWB >= 256 && ROWB % 16 == 0, "at least 16 chunks per image row");
+    static_assert(2 * STAGE + kNW * 2048 <= 160 * 1024, "LDS");
+};
+
+template <int NPL, int NTAP, int CIN, int EK, bool MASK>
+__global__ __launch_bounds__(kNT, 1) void conv_gemm_wreg16_kernel(mtts_conv_gemm_args p, int ncg, int mtiles,
+                                                                   int off0, int dstep) {
+    using G = G16<NTAP, CIN>;
+    constexpr int S = G::S, PW = G::PER_WAVE + (MASK ? 1 : 0);
+    __shared__ __attribute__((aligned(1024))) unsigned char sst[S * G::STAGE];
+    __shared__ __attribute__((aligned(16))) float sepi[kNW * 512];
+    __shared__ __attribute__((aligned(16))) uint32_t szero[4];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l16 = lane & 15, lq = lane >> 4;
+    const int M = p.nb * p.To;
+    const int nwg = gridDim.x, R = nwg / ncg;
+    const int g = mtts::xcd_relabel(blockIdx.x, nwg);
+    const int cg = g % ncg, r = g / ncg;
+    const int n0 = cg * (16 * kNW) + 16 * wave;  // this wave's 16 columns
+    const int ntl = r < mtiles ? (mtiles - 1 - r) / R + 1 : 0;
+    // taps: off_j = off0 + dstep * j (dstep = +-1); the image starts at input row m0 + off_lo
+    const int off_lo = dstep > 0 ? off0 : off0 + dstep * (NTAP - 1);
+
+    // ---- W: 16 columns x K as B fragments, every plane (lane: column n0 + l16, k = 32 s + 8 lq .. + 8)
+    bf16x8 wf[NPL][G::KS];
+    {
+        const int n = n0 + l16;
+        const bool nok = n < p.N;
+        const uint16_t *wb = static_cast<const uint16_t *>(p.W) + (size_t)(nok ? n : 0) * p.Kp + 8 * lq;
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl)
+#pragma unroll
+            for (int s = 0; s < G::KS; ++s) {
+                const uint4 v = nok ? *reinterpret_cast<const uint4 *>(wb + (size_t)pl * p.N * p.Kp + 32 * s)
+                                    : make_uint4(0u, 0u, 0u, 0u);
+                wf[pl][s] = __builtin_bit_cast(bf16x8, v);
+            }
+    }
+    mtts::wait_vmcnt<0>();  // retire the W loads before the tile loop (else a vmcnt(0) at its head)
+
+    const long long arows = (long long)p.nb * p.Ti;  // A rows (Ti == To: A row = GEMM row)
+    const u32x4 rsa = mtts::make_rsrc(p.A, (uint32_t)(arows * p.lda * 2));
+    const u32x4 rsm = mtts::make_rsrc(MASK ? p.a_scale : p.A, MASK ? (uint32_t)(arows * 4) : 0u);
+    const uint32_t lds0 = mtts::lds_addr(sst);
+    auto issue = [&](int ti, int stage) {
+        const int gi0 = (r + ti * R) * kBM + off_lo;  // input row of image row 0
+        const bool tv = ti < ntl;
+#pragma unroll
+        for (int i = 0; i < G::PER_WAVE; ++i) {
+            const int q = wave * G::PER_WAVE + i;
+            const int o = q * 1024 + 16 * lane;
+            const int row = o / G::ROWB, slot = (o % G::ROWB) >> 4;
+            const int c = slot ^ (row & 15);
+            const long long gi = (long long)gi0 + row;
+            const uint32_t vo = tv && row < G::ROWS && gi >= 0 && gi < arows
+                                    ? (uint32_t)((gi * p.lda + c * 8) * 2)
+                                    : kOob;
+            mtts::bload16(vo, rsa, 0u, __builtin_amdgcn_readfirstlane(lds0 + stage * G::STAGE + q * 1024));
+        }
+        if constexpr (MASK) {  // this wave's copy of the image rows' 0/1 mask (64 rows >= ROWS)
+            const long long gi = (long long)gi0 + lane;
+            const uint32_t vo = tv && lane < G::ROWS && gi >= 0 && gi < arows ? (uint32_t)(gi * 4) : kOob;
+            mtts::bload4(vo, rsm, 0u, __builtin_amdgcn_readfirstlane(lds0 + stage * G::STAGE + G::IMG + wave * 256));
+        }
+    };
+
+    if (tid < 4) szero[tid] = 0u;  // (visible after the first tile's barrier)
+    for (int s0 = 0; s0 < S - 1; ++s0) issue(s0, s0);
+
+    const float inv_to = 1.0f / (float)p.To;
+    int cur = 0;
+    for (int ti = 0; ti < ntl; ++ti) {
+        mtts::wait_vmcnt<PW * (S - 2)>();
+        mtts::lds_barrier();
+        issue(ti + S - 1, cur == 0 ? S - 1 : cur - 1);
+        const unsigned char *img = sst + cur * G::STAGE;
+        const float *msk = reinterpret_cast<const float *>(img + G::IMG + wave * 256);
+        const int m0 = (r + ti * R) * kBM;
+        // valid taps of this lane's two rows (bit j: tap j's input row lies inside the utterance, unmasked)
+        uint32_t tvb[2];
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk) {
+            const int m = m0 + 16 * blk + l16;
+            int b, u;
+            mtts::divmod_fast(m, p.To, inv_to, b, u);
+            uint32_t bits = 0;
+#pragma unroll
+            for (int j = 0; j < NTAP; ++j) {
+                const int uj = u + off0 + dstep * j;
+                bool ok = m < M && uj >= 0 && uj < p.Ti;
+                if constexpr (MASK) ok = ok && msk[16 * blk + l16 + off0 + dstep * j - off_lo] != 0.f;
+                bits |= ok ? 1u << j : 0u;
+            }
+            tvb[blk] = bits;
+        }
+        f32x4 acc[2];
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) acc[blk][v] = 0.f;
+        // A fragments of k-step s (both 16-row blocks), zeroed where the tap row is invalid
+        auto frag = [&](int s, int blk) {
+            const int j = (32 * s) / CIN, c0 = (32 * s) % CIN;
+            const int ir = 16 * blk + l16 + off0 + dstep * j - off_lo;  // image row of tap j
+            const int ch = (c0 >> 3) + lq;
+            // an invalid tap row reads the zero chunk: no select on the loaded value (which would wait for it
+            // right after the read and defeat the prefetch)
+            const unsigned char *src = ((tvb[blk] >> j) & 1u) ? img + ir * G::ROWB + ((ch ^ (ir & 15)) << 4)
+                                                               : reinterpret_cast<const unsigned char *>(szero);
+            return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4 *>(src));
+        };
+        // software pipeline, two k-steps of fragment reads in flight: with one wave per SIMD nothing else hides
+        // an LDS read's latency (the compiler's own schedule waited on every read before its two MFMAs)
+        constexpr int PD = 2;
+        bf16x8 af[PD + 1][2];
+#pragma unroll
+        for (int s = 0; s < PD && s < G::KS; ++s) {
+            af[s][0] = frag(s, 0);
+            af[s][1] = frag(s, 1);
+        }
+#pragma unroll
+        for (int s = 0; s < G::KS; ++s) {
+            if (s + PD < G::KS) {
+                af[(s + PD) % (PD + 1)][0] = frag(s + PD, 0);
+                af[(s + PD) % (PD + 1)][1] = frag(s + PD, 1);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
+#pragma unroll
+            for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+                for (int pl = 0; pl < NPL; ++pl)
+                    acc[blk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s % (PD + 1)][blk], wf[pl][s], acc[blk], 0,
+                                                                       0, 0);
+        }
+        // ---- epilogue: the wave's 32 x 16 tile through its LDS image (C[row 4 lq + v][col l16] per block), then
+        // one row's 8 columns per lane (16-byte I/O)
+        float *st = sepi + wave * 512;
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) st[(16 * blk + 4 * lq + v) * 16 + l16] = acc[blk][v];
+        {
+            const int row = lane >> 1, half = lane & 1;
+            const int m = m0 + row, n = n0 + 8 * half;
+            float e[8];
+            mtts::load_f32v<8>(st + row * 16 + 8 * half, e);
+            if (m < M && n < p.N) {
+                int b, u;
+                mtts::divmod_fast(m, p.To, inv_to, b, u);
+                const int crow = b * p.To_full + u * p.out_stride + p.out_off;
+                float bn[8];
+#pragma unroll
+                for (int qq = 0; qq < 8; ++qq) bn[qq] = 0.f;
+                if (p.bias) mtts::load_f32v<8>(p.bias + n, bn);
+#pragma unroll
+                for (int qq = 0; qq < 8; ++qq) e[qq] += bn[qq];
+                const bool drop = p.dropout_p > 0.f;
+                const uint32_t s0 = drop ? p.seed[0] : 0u, s1 = drop ? p.seed[1] : 0u;
+                mtts::epilogue_rowv<8, EK>(p, crow, n, e, s0, s1, drop ? 1.0f / (1.0f - p.dropout_p) : 1.0f);
+            }
+        }
+        cur = cur == S - 1 ? 0 : cur + 1;
+    }
+    mtts::wait_vmcnt<0>();
+}
+
+struct Grid16 {
+    int ncg, mtiles, R;
+};
+
+Grid16 grid16(const mtts_conv_gemm_args &p, int M) {
+    static const int cus = [] {
+        int dev = 0, n = 256;
+        hipDeviceProp_t pr;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0)
+            n = pr.multiProcessorCount;
+        return n;
+    }();
+    Grid16 g;
+    g.ncg = (p.N + 16 * kNW - 1) / (16 * kNW);
+    g.mtiles = (M + kBM - 1) / kBM;
+    g.R = std::max(1, std::min(g.mtiles, cus / g.ncg));
+    return g;
+}
+
+template <int NPL, int NTAP, int CIN, int EK, bool MASK>
+int launch16_e(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    const Grid16 g = grid16(p, M);
+    const int dstep = p.ntaps > 1 ? p.off[1] - p.off[0] : 1;
+    hipLaunchKernelGGL((conv_gemm_wreg16_kernel<NPL, NTAP, CIN, EK, MASK>), dim3((unsigned)(g.ncg * g.R)), dim3(kNT), 0,
+                       st, p, g.ncg, g.mtiles, p.off[0], dstep);
+    return mtts::check_launch("conv_gemm_wreg16_kernel");
+}
+
+template <int NPL, int NTAP, int CIN>
+int launch16_t(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    const bool rm = p.a_scale != nullptr;
+    switch (mtts::gemm_epilogue_kind(p)) {
+        case mtts::EK_LIN_C16:
+            return rm ? launch16_e<NPL, NTAP, CIN, mtts::EK_LIN_C16, true>(p, M, st)
+                      : launch16_e<NPL, NTAP, CIN, mtts::EK_LIN_C16, false>(p, M, st);
+        case mtts::EK_LIN_C32:
+            return rm ? launch16_e<NPL, NTAP, CIN, mtts::EK_LIN_C32, true>(p, M, st)
+                      : launch16_e<NPL, NTAP, CIN, mtts::EK_LIN_C32, false>(p, M, st);
+        default:
+            return rm ? launch16_e<NPL, NTAP, CIN, mtts::EK_RT, true>(p, M, st)
+                      : launch16_e<NPL, NTAP, CIN, mtts::EK_RT, false>(p, M, st);
+    }
+}
+
+template <int NPL>
+int launch16_shape(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    if (p.ntaps == 3 && p.cin == 256) return launch16_t<NPL, 3, 256>(p, M, st);
+    if (p.ntaps == 1 && p.cin == 256) return launch16_t<NPL, 1, 256>(p, M, st);
+    if (p.ntaps == 1 && p.cin == 512) return launch16_t<NPL, 1, 512>(p, M, st);
+    if (p.ntaps == 1 && p.cin == 1024) return launch16_t<NPL, 1, 1024>(p, M, st);
+    return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: 16-column weight-stationary schedule: shape not instantiated");
+}
+
+}  // namespace
+
+namespace mtts {
+
+// (taps, cin) in {(3, 256), (1, 256), (1, 512), (1, 1024)} with unit tap steps at stride 1 and Ti == To; bf16 A (16-byte
+// rows); bf16 MFMA on one or two planes; a 0/1 row mask or none; the 16-byte epilogue (N, ldc % 8)
+bool conv_gemm_wreg16_applies(const mtts_conv_gemm_args &p) {
+    const bool shape = (p.ntaps == 3 && p.cin == 256) || (p.ntaps == 1 && (p.cin == 256 || p.cin == 512 || p.cin == 1024));
+    if (!shape || p.K != p.ntaps * p.cin || p.in_stride != 1 || p.Ti != p.To) return false;
+    if (p.ntaps == 3 && (p.off[1] - p.off[0] != p.off[2] - p.off[1] || std::abs(p.off[1] - p.off[0]) != 1)) return false;
+    if (!(p.flags & MTTS_GEMM_F_A_BF16) || (p.flags & (MTTS_GEMM_F_A_SPLIT | MTTS_GEMM_F_SPLIT3))) return false;
+    if (p.a_scale && !(p.flags & MTTS_GEMM_F_BINARY_SCALE)) return false;
+    if (p.lda % 8 || (uintptr_t)p.A % 16 || (uintptr_t)p.W % 16 || p.Kp % 8) return false;
+    const int npl = (p.flags & MTTS_GEMM_F_W_SPLIT) ? 2 : 1;
+    if ((long long)p.nb * p.Ti * p.lda * 2 >= (1ll << 31) - (1ll << 20)) return false;
+    if ((long long)npl * p.N * p.Kp >= (1ll << 31)) return false;
+    return gemm_epilogue_vec_ok(p) && gemm_epilogue_vec8_ok(p);
+}
+
+bool conv_gemm_wreg16_preferred(const mtts_conv_gemm_args &p, int M) {
+    static const bool on = [] { const char *e = getenv("MTTS_GEMM_WREG16_PICK"); return !(e && e[0] == '0'); }();
+    if (!on) return false;
+    // measured (tools/r5/gemm_replay.py, profiles/r05/wreg/replay_wreg16.jsonl): ahead of the LDS-DMA schedules only on
+    // the 19200-row FeedForward down-projection (two planes); one wave per SIMD leaves its LDS reads exposed elsewhere
+    return p.ntaps == 1 && p.cin == 1024 && M >= 16384 && (p.flags & MTTS_GEMM_F_W_SPLIT);
+}
+
+int conv_gemm_wreg16_launch(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    return (p.flags & MTTS_GEMM_F_W_SPLIT) ? launch16_shape<2>(p, M, st) : launch16_shape<1>(p, M, st);
+}
+
+}  // namespace mtts

@@ -57,6 +57,21 @@ __device__ __forceinline__ void bload16(uint32_t voff, u32x4 rsrc, uint32_t soff
         : "memory");
 }
 
+// One buffer_load_dword ... lds: 4 bytes per lane into LDS at lds_base + 4*lane (per-element bounds: a lane
+// whose voff lies past num_records reads a zero)
+__device__ __forceinline__ void bload4(uint32_t voff, u32x4 rsrc, uint32_t soff, uint32_t lds) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dword %1, %2, %3 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
+        : "memory");
+}
+
 // LDS byte address of a __shared__ pointer, wave-uniform (the M0 operand of the DMA loads)
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void *)p);

@@ -110,3 +110,72 @@ def test_wreg_heuristic_and_unsupported_shapes():
     y = torch.empty(2, 50, 128, device=DEV)
     with pytest.raises(N.NativeError):
         O._gemm(x3, 50, 50, 2, 1, [-1, 0, 1], 256, Wp3, Kp3, 128, y, 50, prec=O.PREC_BF16, tile_cfg=WREG)
+
+
+WREG16 = 97  # MTTS_GEMM_WREG + 1: 16 columns per wave, K = 768 (3 taps x 256) / 512 / 1024
+
+
+@pytest.mark.parametrize("kind", ["lin16", "lin32", "runtime"])
+@pytest.mark.parametrize("B,T,cin,N,taps,split,masked", [
+    (3, 301, 256, 256, [-1, 0, 1], True, True),     # decoder k = 3 conv, two planes, ragged rows + mask
+    (2, 150, 256, 160, [1, 0, -1], True, False),    # the dgrad's descending taps; N not a multiple of 64
+    (4, 77, 256, 512, [-1, 0, 1], False, True),
+    (2, 300, 1024, 256, [0], True, False),          # FeedForward down-projection, K = 1024
+    (5, 61, 512, 192, [0], False, True),            # K = 512
+])
+def test_wreg16_vs_float64_and_lds_dma(kind, B, T, cin, N, taps, split, masked):
+    """Schedule 97 against a float64 product of the same bf16 operands (the row mask and the per-utterance tap
+    zero padding included) and against the LDS-DMA schedule 41 on the whole epilogue: not bitwise (16x16x32
+    MFMAs sum 32 products per instruction, the 32x32x16 kernels 16), so within fp32 accumulation error; and
+    deterministic run to run."""
+    from matcha.models.components import _ops as O
+
+    g = torch.Generator(device="cpu").manual_seed(B * T + cin + N)
+    K = cin * len(taps)
+    x = torch.randn(B, T, cin, generator=g).bfloat16().float()
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV)
+    if split:
+        hi = w.bfloat16()
+        Wp = torch.cat([hi, (w - hi.float()).bfloat16()]).contiguous()
+        Wp._mtts_w_split = True
+        Kp = K
+        wq = hi.float() + (w - hi.float()).bfloat16().float()
+    else:
+        Wp, Kp = O.pack_weight(w, O.PREC_BF16)
+        wq = w.bfloat16().float()
+    kw = dict(act=O.ACT_NONE)
+    msk = (torch.rand(B * T, generator=g) > 0.25).float() if masked else torch.ones(B * T)
+    if masked:
+        kw["a_scale"] = msk.to(DEV)
+    c16 = kind == "lin16"
+    if kind in ("lin32", "runtime"):
+        kw["bias"] = torch.randn(N, generator=g).to(DEV)
+        kw["residual"] = torch.randn(B, T, N, generator=g).to(DEV)
+    if kind == "runtime":
+        kw["act"] = O.ACT_RELU
+    A = x.to(DEV).bfloat16()
+    outs = []
+    for cfg in (WREG16, WREG16, 41):
+        C = torch.full((B, T, N), float("nan"), device=DEV, dtype=torch.bfloat16 if c16 else torch.float32)
+        O._gemm(A, T, T, B, 1, taps, cin, Wp, Kp, N, C, T, prec=O.PREC_BF16, tile_cfg=cfg, **kw)
+        torch.cuda.synchronize()
+        outs.append(C.float())
+    assert torch.equal(outs[0], outs[1])  # deterministic
+    # float64 reference: implicit GEMM over the taps with per-utterance zero padding and the row mask on A
+    xm = (x.double() * msk.double().view(B, T, 1))
+    ref = torch.zeros(B, T, N, dtype=torch.float64)
+    wr = wq.double().cpu().view(N, len(taps), cin)
+    for j, o in enumerate(taps):
+        src = torch.zeros_like(xm)
+        lo, hi_ = max(0, -o), min(T, T - o)
+        src[:, lo:hi_] = xm[:, lo + o:hi_ + o]
+        ref += src @ wr[:, j].T
+    if kind in ("lin32", "runtime"):
+        ref += kw["bias"].double().cpu()
+        if kind == "runtime":
+            ref = ref.clamp_min(0)
+        ref += kw["residual"].double().cpu()
+    scale = ref.abs().max().item()
+    tol = (2 ** -7 if c16 else 1e-5) * scale
+    assert (outs[0].double().cpu() - ref).abs().max().item() <= tol
+    assert (outs[0] - outs[2]).abs().max().item() <= (2 ** -7 if c16 else 1e-5) * scale
