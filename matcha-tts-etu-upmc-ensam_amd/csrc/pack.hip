@@ -160,9 +160,17 @@ extern "C" int mtts_pack_weights(const mtts_pack_job *jobs, int32_t njobs, int32
     }
     if (njobs == 0 || max_groups == 0) return MTTS_OK;
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
-    const int gx = (int)((max_groups + kThreads - 1) / kThreads < 256 ? (max_groups + kThreads - 1) / kThreads : 256);
     for (int base = 0; base < njobs; base += kJobsPerLaunch) {
         const int n = njobs - base < kJobsPerLaunch ? njobs - base : kJobsPerLaunch;
+        // blocks per job: one per 256 groups of the launch's largest job, up to ~4096 workgroups per launch (the
+        // old cap of 256 per job left a launch of small jobs at <1 workgroup per CU and a large job grid-striding)
+        long mg = 0;
+        for (int i = 0; i < n; ++i) {
+            const long g = (long)jobs[base + i].rows * (jobs[base + i].Kp / 8);
+            mg = g > mg ? g : mg;
+        }
+        const long cap = 4096 / n > 256 ? 4096 / n : 256;
+        const int gx = (int)((mg + kThreads - 1) / kThreads < cap ? (mg + kThreads - 1) / kThreads : cap);
         JobBatch jb;
         for (int i = 0; i < n; ++i) jb.job[i] = jobs[base + i];
         if (precision == MTTS_PREC_BF16)
