@@ -288,9 +288,12 @@ bool conv_gemm_wreg16_applies(const mtts_conv_gemm_args &p) {
 bool conv_gemm_wreg16_preferred(const mtts_conv_gemm_args &p, int M) {
     static const bool on = [] { const char *e = getenv("MTTS_GEMM_WREG16_PICK"); return !(e && e[0] == '0'); }();
     if (!on) return false;
-    // measured (tools/r5/gemm_replay.py, profiles/r05/wreg/replay_wreg16.jsonl): ahead of the LDS-DMA schedules only on
-    // the 19200-row FeedForward down-projection (two planes); one wave per SIMD leaves its LDS reads exposed elsewhere
-    return p.ntaps == 1 && p.cin == 1024 && M >= 16384 && (p.flags & MTTS_GEMM_F_W_SPLIT);
+    // measured (tools/r5/gemm_replay.py, profiles/r05/wreg/replay_wreg16.jsonl, profiles/r05/sweep/): behind the best
+    // LDS-DMA schedule on every step shape (one wave per SIMD leaves its LDS reads exposed), so explicit id only --
+    // and a heuristic pick here would also keep the schedule tuner (bitwise-equal candidates) from the faster ones
+    (void)p;
+    (void)M;
+    return false;
 }
 
 int conv_gemm_wreg16_launch(const mtts_conv_gemm_args &p, int M, hipStream_t st) {

@@ -179,3 +179,18 @@ def test_wreg16_vs_float64_and_lds_dma(kind, B, T, cin, N, taps, split, masked):
     tol = (2 ** -7 if c16 else 1e-5) * scale
     assert (outs[0].double().cpu() - ref).abs().max().item() <= tol
     assert (outs[0] - outs[2]).abs().max().item() <= (2 ** -7 if c16 else 1e-5) * scale
+
+
+def test_schedule_tuning_keeps_results_bitwise():
+    """With MTTS_GEMM_TUNE=1 the heuristic's first eager call of a shape times the bitwise-equal schedules and
+    caches the fastest (csrc/conv_gemm.hip tune_plan); without it the heuristic runs.  Either way the first call,
+    the later calls and an explicit bitwise-equal schedule give identical outputs, the whole epilogue included."""
+    from matcha.models.components import _ops as O
+
+    B, T, K, N = 4, 333, 256, 320  # a shape no other test uses (a fresh tuning key)
+    A, Wp, Kp, C, kw, x, w = _case("lin32", B, T, K, N, True, True, True, seed=11)
+    first, _ = _run(A, Wp, Kp, C, kw, B, T, K, N, -1)
+    again, _ = _run(A, Wp, Kp, C, kw, B, T, K, N, -1)
+    ref, _ = _run(A, Wp, Kp, C, kw, B, T, K, N, 41)
+    assert torch.equal(first, again)
+    assert torch.equal(first, ref)
