@@ -1545,7 +1545,9 @@ static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks,
     static const int min_blocks16 = [] { const char *e = getenv("MTTS_WGRAD_MINBLK16"); return e ? atoi(e) : 512; }();
     static const int split_rows = [] { const char *e = getenv("MTTS_WGRAD_ROWS"); return e && atoi(e) > 0 ? atoi(e) : 768; }();
     static const int b_min_blocks = [] { const char *e = getenv("MTTS_WGRAD_BMINBLK"); return e ? atoi(e) : 128; }();
-    static const int b_split_rows = [] { const char *e = getenv("MTTS_WGRAD_BROWS"); return e && atoi(e) > 0 ? atoi(e) : 1536; }();
+    // round 5: 3072 rows per split in the batched launches (same-box step A/B, tools/r5/gpu_ab_wgrad.sh: 7.604 / 7.583
+    // vs 7.611 / 7.631 ms at 1536; 1024 and 4608 slower; profiles/r05/wgrad_split_ab.txt) -- fewer slabs to sum
+    static const int b_split_rows = [] { const char *e = getenv("MTTS_WGRAD_BROWS"); return e && atoi(e) > 0 ? atoi(e) : 3072; }();
     // hv = 2: two-half workgroups (twice the waves each): half the workgroups, rows in whole double steps
     const int mb = (batched ? b_min_blocks
                             : (p.flags & (MTTS_GEMM_F_A_BF16 | MTTS_WGRAD_F_DY_BF16)) ? min_blocks16 : min_blocks) / hv;
