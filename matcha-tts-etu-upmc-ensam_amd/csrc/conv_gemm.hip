@@ -1205,7 +1205,9 @@ static int resolve_cfg(const mtts_conv_gemm_args &p, bool bf16, int cfg, int M, 
     if (cfg < 0 && bf16 && wreg_pick && mtts::conv_gemm_wreg16_applies(p) && mtts::conv_gemm_wreg16_preferred(p, M))
         return MTTS_GEMM_WREG + 1;
     static const bool ws_pick = [] { const char *e = getenv("MTTS_GEMM_WS_PICK"); return !(e && e[0] == '0'); }();
-    if (cfg < 0 && bf16 && ws_pick && (p.flags & MTTS_GEMM_F_W_SPLIT) && !(p.flags & MTTS_GEMM_F_A_SPLIT))
+    // (a bf16 A goes to the LDS-DMA pick below: pick_cfg_ws may answer a register-staged schedule)
+    if (cfg < 0 && bf16 && ws_pick && (p.flags & MTTS_GEMM_F_W_SPLIT) &&
+        !(p.flags & (MTTS_GEMM_F_A_SPLIT | MTTS_GEMM_F_A_BF16)))
         cfg = pick_cfg_ws(p, M);
     if (p.flags & MTTS_GEMM_F_A_BF16) {  // bf16 A operands exist only in the LDS-DMA kernels
         if (!bf16 || !mtts::conv_gemm_glds_applies(p))

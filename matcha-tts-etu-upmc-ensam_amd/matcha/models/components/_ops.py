@@ -1688,6 +1688,10 @@ N.register("mtts_layernorm_bwd_res", ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, 
 NORM_F_Y_BF16 = 0x100  # include/mtts_decoder.h MTTS_NORM_F_Y_BF16
 _PRELN_N16 = os.environ.get("MTTS_PRELN_N16", "1") != "0"  # attention block's LN output as bf16 (A/B switch)
 _ATTN_IO16 = os.environ.get("MTTS_ATTN_IO16", "1") != "0"  # bf16 q|k|v / o / dO / dq|dk|dv (A/B switch)
+# the FeedForward block's LN output as bf16 (round 5; same-box step A/B 7.546 / 7.531 -> 7.465 / 7.456 ms, bitwise
+# the same losses, profiles/r05/ab_preln_ff_n16.txt): the up-projection (now the weight-stationary
+# kernel, which rounds an fp32 A to bf16 at the fragment read anyway) and dW1 read it
+_PRELN_FF_N16 = os.environ.get("MTTS_PRELN_FF_N16", "1") != "0"
 
 
 def _ln_fwd(h2, w, b, eps, y16):
@@ -1805,10 +1809,10 @@ class _PreLNFeedForwardTM(torch.autograd.Function):
         M, C = h2.shape
         H = w1.shape[0]
         lnw, lnb = _f32c(ln_w), _f32c(ln_b)
-        # fp32 LayerNorm output here: with it bf16 the GELU GEMM runs the 64 x 256 LDS-DMA tiles, faster
-        # in isolation (53.3 vs 61.0 us at 19200 x 1024 x 256, tools/ff_epilogue_cost.py) but the step
-        # measured slower (9.22 vs 8.92 ms); the register-staged schedule hides the GELU epilogue
-        n, mean, rstd = _ln_fwd(h2, lnw, lnb, eps, False)
+        # bf16 LayerNorm output (round 5, _PRELN_FF_N16): the GELU up-projection runs on the weight-stationary
+        # kernel, which rounds an fp32 A to bf16 at its fragment read anyway -- the same products, half the bytes
+        # (rounds 2-4 kept it fp32: the register-staged schedule then hid the GELU epilogue better)
+        n, mean, rstd = _ln_fwd(h2, lnw, lnb, eps, prec == PREC_BF16 and _PRELN_FF_N16)
         W1p, K1p = packed(spec_linear((w1,), one_plane=not _FF1_SPLIT), prec)
         W2p, K2p = packed(spec_linear((w2,), one_plane=not _FF2_SPLIT), prec)
         ctx.w2t = packed(spec_linear((w2,), dgrad=True), prec)
