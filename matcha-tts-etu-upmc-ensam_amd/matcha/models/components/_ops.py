@@ -2062,6 +2062,8 @@ class _TimeMLP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, e, w1, b1, w2, b2, n_proj, pre, *wb):
         N.require_device(e, w1)
+        ctx.keys = ([_pkey(t) for t in (w1, b1, w2, b2)], [_pkey(w) for w in wb[:n_proj]],
+                    [_pkey(b) for b in wb[n_proj:]])
         ws = [_f32c(w) for w in wb[:n_proj]]
         bs = [_f32c(b) for b in wb[n_proj:]]
         e, w1, b1, w2, b2 = _f32c(e), _f32c(w1), _f32c(b1), _f32c(w2), _f32c(b2)
@@ -2082,11 +2084,12 @@ class _TimeMLP(torch.autograd.Function):
         new = functools.partial(torch.empty, dtype=torch.float32, device=e.device)
         dys = [_f32c(g) if g is not None else torch.zeros(B, w.shape[0], device=e.device) for g, w in zip(g_tps, ws)]
         d_temb = new(B, D)
-        dws = [torch.empty_like(w) for w in ws]
-        dbs = [new(w.shape[0]) for w in ws]
-        dh1, dw2, db2 = new(B, D), torch.empty_like(w2), new(D)
+        (k1, kb1, k2, kb2), kws, kbs = ctx.keys  # data-parallel grad slots (else fresh buffers)
+        dws = [_grad_buf(k, w.shape, e.device) for k, w in zip(kws, ws)]
+        dbs = [_grad_buf(k, (w.shape[0],), e.device) for k, w in zip(kbs, ws)]
+        dh1, dw2, db2 = new(B, D), _grad_buf(k2, w2.shape, e.device), _grad_buf(kb2, (D,), e.device)
         de = new(*e.shape) if ctx.e_grad else None
-        dw1, db1 = torch.empty_like(w1), new(D)
+        dw1, db1 = _grad_buf(k1, w1.shape, e.device), _grad_buf(kb1, (D,), e.device)
         # on the decoder's path (t carries no gradient) every output is a parameter gradient: the five
         # launches leave the critical path for the deferral's side stream (joined before the optimizer)
         # -- only when autograd takes EVERY output as a parameter gradient: it then steals each tensor (no
