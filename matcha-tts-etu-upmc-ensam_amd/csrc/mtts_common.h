@@ -10,6 +10,22 @@
 
 namespace mtts {
 
+// Counter-based dropout keep test shared by the GEMM epilogues, the norms, the attention probabilities
+// and mtts_dropout_apply: one murmur3 finalizer over a (row, column pair, seed) key, whose two 16-bit halves
+// are the uniforms of the pair's even and odd column.  32-bit integer multiplies run at a quarter of the VALU
+// rate on CDNA; the row product is loop-invariant in the epilogues (hoisted) and the 16-byte epilogues hand
+// adjacent column pairs to one hash (the compiler merges the identical calls): one finalizer per two elements
+// (round 5: the FeedForward GELU epilogue spent ~35 % of its VALU cycles in the per-element hash).  The keep
+// probability is 1 - p up to the 2^-16 grid (p = 0.1: 0.100006).  Every site that regenerates a mask calls
+// this with the same (row, col), so forward and backward agree.
+__device__ __forceinline__ bool dropout_keep(uint32_t seed_lo, uint32_t seed_hi, uint32_t row, uint32_t col,
+                                             float p) {
+    uint32_t x = ((row * 0x9E3779B1u) ^ (((col >> 1) + 0x7F4A7C15u) * 0x85EBCA77u) ^ seed_lo) + seed_hi;
+    x ^= x >> 16; x *= 0x85EBCA6Bu; x ^= x >> 13; x *= 0xC2B2AE35u; x ^= x >> 16;
+    const uint32_t u = (col & 1u) ? (x >> 16) : (x & 0xFFFFu);
+    return (float)u * (1.0f / 65536.0f) >= p;
+}
+
 // Tap offset j of a conv argument struct (static indexing only: no private-memory copy of off[]).
 template <class P>
 __device__ __forceinline__ int tap_off(const P &p, int j) {
