@@ -110,7 +110,9 @@ typedef struct mtts_conv_gemm_args {
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
 /* Same, with an explicit schedule: 0..17 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;
  * 8..17 bf16-only: 64-wide K steps, two K steps in flight), MTTS_GEMM_GLDS + i = the bf16 LDS-DMA schedules
- * (csrc/conv_gemm_glds.hip), -1 = heuristic.
+ * (csrc/conv_gemm_glds.hip), MTTS_GEMM_PK + i = the persistent big-tile schedules (csrc/conv_gemm_pk.hip),
+ * MTTS_GEMM_WREG / + 1 = the weight-stationary schedules (csrc/conv_gemm_wreg.hip, conv_gemm_wreg16.hip),
+ * -1 = heuristic (MTTS_GEMM_TUNE=1: plus the bitwise-safe schedule tuner).
  * For tuning and tests; mtts_conv_gemm picks the configuration itself. */
 int mtts_conv_gemm_tile(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg, void *hip_stream);
 /* With a caller-owned workspace: lets the bf16 LDS-DMA schedules split K over several workgroups
