@@ -57,6 +57,12 @@ __device__ __forceinline__ bf16x8 tr_read8(const uint16_t *p, int row_stride) {
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
+// -DMTTS_PIN_PREFETCH=0 builds the register-staged loops without the scheduling fence (A/B builds)
+#ifndef MTTS_PIN_PREFETCH
+#define MTTS_PIN_PREFETCH 1
+#endif
+constexpr bool g_pin_prefetch = MTTS_PIN_PREFETCH != 0;
+
 __device__ __forceinline__ uint16_t to_bf16(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -358,6 +364,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
         }
     };
 
+    // The scheduling fence after each prefetch keeps its global loads ahead of the step's MFMAs: without it
+    // the machine scheduler sank them behind all but the last few MFMAs (ISA of the fp32 64 x 64 schedule,
+    // round 5), so the vmcnt wait before store_tile exposed the whole global round trip every step.
     if constexpr (DEPTH == 2) {
         // two K steps in flight: the loads of step kt+2 are issued before computing step kt, stored to
         // LDS after computing step kt+1 -- two compute phases cover each global round trip
@@ -367,11 +376,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
         mtts::lds_barrier();
         for (int kt = 0; kt < nk; kt += 2) {
             load_tile(R0, kbase + (kt + 2) * KB);
+            if (g_pin_prefetch) __builtin_amdgcn_sched_barrier(0);
             compute(0);
             store_tile(R1, 1);
             mtts::lds_barrier();
             if (kt + 1 >= nk) break;
             load_tile(R1, kbase + (kt + 3) * KB);
+            if (g_pin_prefetch) __builtin_amdgcn_sched_barrier(0);
             compute(1);
             store_tile(R0, 0);
             mtts::lds_barrier();
@@ -384,6 +395,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
         mtts::lds_barrier();
         for (int kt = 0; kt < nk; ++kt) {
             load_tile(R0, kbase + (kt + 1) * KB);
+            if (g_pin_prefetch) __builtin_amdgcn_sched_barrier(0);
             compute(kt & 1);
             store_tile(R0, (kt + 1) & 1);
             mtts::lds_barrier();
@@ -836,6 +848,7 @@ __device__ __forceinline__ void wgrad_block(const WgradBatch &wb, const int vb) 
             store(R0, buf);
             mtts::lds_barrier();
             load(R0, rb + KB);
+            if (g_pin_prefetch) __builtin_amdgcn_sched_barrier(0);
             compute(buf);
             buf ^= 1;
         }
@@ -867,11 +880,13 @@ __device__ __forceinline__ void wgrad_block(const WgradBatch &wb, const int vb) 
             mtts::lds_barrier();
             for (int rb = r_begin; rb < r_end; rb += 2 * KB) {
                 load(R0, rb + 2 * KB);
+                if (g_pin_prefetch) __builtin_amdgcn_sched_barrier(0);
                 compute(0);
                 store(R1, 1);
                 mtts::lds_barrier();
                 if (rb + KB >= r_end) break;
                 load(R1, rb + 3 * KB);
+                if (g_pin_prefetch) __builtin_amdgcn_sched_barrier(0);
                 compute(1);
                 store(R0, 0);
                 mtts::lds_barrier();
@@ -883,6 +898,7 @@ __device__ __forceinline__ void wgrad_block(const WgradBatch &wb, const int vb) 
                 store(R0, buf);  // buf was last read two steps ago, before the previous barrier
                 mtts::lds_barrier();
                 load(R0, rb + KB);  // unconditional: past r_end every row is masked off (branch-free body)
+                if (g_pin_prefetch) __builtin_amdgcn_sched_barrier(0);
                 compute(buf);
                 buf ^= 1;
             }

@@ -11,7 +11,7 @@ for f in sorted(d.glob("pass*/*counter_collection.csv")):
         if "gemm" not in r["Kernel_Name"]:
             continue
         import re
-        k = re.search(r"conv_gemm_\w+_kernel<[^>]*>", r["Kernel_Name"]).group(0)
+        k = re.search(r"conv_gemm(?:_\w+)?_kernel<[^>]*>", r["Kernel_Name"]).group(0)
         key = (f.parent.name, r["Dispatch_Id"])
         agg[k][r["Counter_Name"]][key] = agg[k][r["Counter_Name"]].get(key, 0.0) + float(r["Counter_Value"])
 for k, cs in agg.items():
