@@ -63,6 +63,27 @@ __device__ __forceinline__ bf16x8 tr_read8(const uint16_t *p, int row_stride) {
 #endif
 constexpr bool g_pin_prefetch = MTTS_PIN_PREFETCH != 0;
 
+// -DMTTS_GEMM_TIMELINE=1 (diagnostic builds only, tools/r5/gemm_timeline.py): lane 0 of every wave of the
+// register-staged one-step schedule stamps the 100 MHz wall clock at each phase of each K step into g_tl
+// ([wave][kTlSlots]: HW ids, start, prologue, then per step: loads issued / MFMAs issued / LDS stored /
+// barrier passed, loop end, epilogue end); read back by mtts_gemm_timeline_read.
+#ifndef MTTS_GEMM_TIMELINE
+#define MTTS_GEMM_TIMELINE 0
+#endif
+#if MTTS_GEMM_TIMELINE
+constexpr int kTlSlots = 128, kTlWaves = 16384, kTlSteps = 30;
+__device__ long long g_tl[kTlWaves * kTlSlots];
+#define MTTS_TL(slot)                                                                                    \
+    do {                                                                                                 \
+        const int tl_w = (int)blockIdx.x * (WM * WN) + wave;                                            \
+        if (lane == 0 && tl_w < kTlWaves && (slot) < kTlSlots) g_tl[tl_w * kTlSlots + (slot)] = wall_clock64(); \
+    } while (0)
+#else
+#define MTTS_TL(slot) \
+    do {              \
+    } while (0)
+#endif
+
 __device__ __forceinline__ uint16_t to_bf16(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -390,16 +411,37 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
     } else {
         // branch-free body (no phi copies of in-flight registers): the step after the last one loads
         // clamped addresses with every chunk masked off and stores into the unused buffer
+#if MTTS_GEMM_TIMELINE
+        if (lane == 0 && (int)blockIdx.x * (WM * WN) + wave < kTlWaves)
+            g_tl[((int)blockIdx.x * (WM * WN) + wave) * kTlSlots] =
+                ((long long)__smid() << 32) | (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        MTTS_TL(1);
+#endif
         load_tile(R0, kbase);
         store_tile(R0, 0);
         mtts::lds_barrier();
+        MTTS_TL(2);
         for (int kt = 0; kt < nk; ++kt) {
             load_tile(R0, kbase + (kt + 1) * KB);
             if (g_pin_prefetch) __builtin_amdgcn_sched_barrier(0);
+#if MTTS_GEMM_TIMELINE
+            if (kt < kTlSteps) MTTS_TL(3 + 4 * kt);
+#endif
             compute(kt & 1);
+#if MTTS_GEMM_TIMELINE
+            __builtin_amdgcn_sched_barrier(0);
+            if (kt < kTlSteps) MTTS_TL(4 + 4 * kt);
+#endif
             store_tile(R0, (kt + 1) & 1);
+#if MTTS_GEMM_TIMELINE
+            if (kt < kTlSteps) MTTS_TL(5 + 4 * kt);
+#endif
             mtts::lds_barrier();
+#if MTTS_GEMM_TIMELINE
+            if (kt < kTlSteps) MTTS_TL(6 + 4 * kt);
+#endif
         }
+        MTTS_TL(kTlSlots - 2);
     }
 
     // ---- epilogue ---- (the K loop ended with a barrier after every wave's last LDS access: Bs is free
@@ -409,11 +451,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_kernel(mtts_conv_gemm_
             mtts::gemm_store_partial<TM, TN>(p, acc, reinterpret_cast<float *>(reinterpret_cast<unsigned char *>(&Bs[0][0]) + wave * 4096),
                                              part + (size_t)(kstep0 / ksteps) * M * p.N, m0 + wr * 32 * TM, n0 + wc * 32 * TN,
                                              lane);
+            MTTS_TL(kTlSlots - 1);
             return;
         }
         if (mtts::gemm_epilogue_vec_ok(p)) {
             mtts::gemm_epilogue_vec<TM, TN>(p, acc, reinterpret_cast<float *>(reinterpret_cast<unsigned char *>(&Bs[0][0]) + wave * 4096),
                                             m0 + wr * 32 * TM, n0 + wc * 32 * TN, lane);
+            MTTS_TL(kTlSlots - 1);
             return;
         }
     }
@@ -1461,6 +1505,20 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
     if (heuristic && splits <= 0 && bf16 && tune_on()) pl = tune_plan(p, bf16, pl, M, ws, ws_bytes, st);
     return launch_plan(p, bf16, pl, M, ws, ws_bytes, st);
 }
+
+#if MTTS_GEMM_TIMELINE
+// diagnostic builds: copy (or zero, host == NULL) the timeline buffer; returns its size in bytes
+extern "C" long long mtts_gemm_timeline_read(void *host) {
+    const size_t bytes = sizeof(long long) * kTlWaves * kTlSlots;
+    if (host) {
+        if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tl), bytes) != hipSuccess) return -1;
+    } else {
+        void *d = nullptr;
+        if (hipGetSymbolAddress(&d, HIP_SYMBOL(g_tl)) != hipSuccess || hipMemset(d, 0, bytes) != hipSuccess) return -1;
+    }
+    return (long long)bytes;
+}
+#endif
 
 extern "C" int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream) {
     return conv_gemm_impl(args, precision, -1, 1, nullptr, 0, hip_stream);
