@@ -1620,7 +1620,10 @@ static void wgrad_plan(const mtts_conv_wgrad_args &p, int kb, int target_blocks,
     static const int min_blocks = [] { const char *e = getenv("MTTS_WGRAD_MINBLK"); return e ? atoi(e) : 384; }();
     static const int min_blocks16 = [] { const char *e = getenv("MTTS_WGRAD_MINBLK16"); return e ? atoi(e) : 512; }();
     static const int split_rows = [] { const char *e = getenv("MTTS_WGRAD_ROWS"); return e && atoi(e) > 0 ? atoi(e) : 768; }();
-    static const int b_min_blocks = [] { const char *e = getenv("MTTS_WGRAD_BMINBLK"); return e ? atoi(e) : 128; }();
+    // round 5, with the prefetch fence: 64 minimum blocks per batched job (same box, three alternating rounds:
+    // 7.410 / 7.409 / 7.383 vs 7.457 / 7.452 / 7.455 ms at 128; profiles/r05/ab/wgrad_min_blocks_ab.txt) -- the
+    // side-stream batch crowds the encoder's backward less
+    static const int b_min_blocks = [] { const char *e = getenv("MTTS_WGRAD_BMINBLK"); return e ? atoi(e) : 64; }();
     // round 5: 3072 rows per split in the batched launches (same-box step A/B, tools/r5/gpu_ab_wgrad.sh: 7.604 / 7.583
     // vs 7.611 / 7.631 ms at 1536; 1024 and 4608 slower; profiles/r05/wgrad_split_ab.txt) -- fewer slabs to sum
     static const int b_split_rows = [] { const char *e = getenv("MTTS_WGRAD_BROWS"); return e && atoi(e) > 0 ? atoi(e) : 3072; }();
