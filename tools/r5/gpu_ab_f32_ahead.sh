@@ -1,7 +1,9 @@
 #!/bin/bash
 # round 5: exact-fp32 register schedules with every fragment of a K step read ahead of its MFMAs
 # (MTTS_F32_FRAG_AHEAD; the noahead build: MTTS_BUILD_VARIANT=noahead MTTS_EXTRA_HIPCC_FLAGS=-DMTTS_F32_FRAG_AHEAD=0): GEMM tests,
-# the step A/B alternating on one box -> gpurun_out/$TAG
+# the step A/B alternating on one box -> gpurun_out/$TAG.  The read-ahead variant was measured slower and removed
+#  without being committed: re-apply it (the fp32 branch of compute() reading all 16 fragment
+# pairs, then a sched_barrier, the 16 MFMAs, another sched_barrier) to rerun this A/B.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/${TAG:-r5ahead}; mkdir -p $O; cd $R
 NOAHEAD=matcha-tts-etu-upmc-ensam_amd/lib/libmtts_hip_noahead.so
 PIN=matcha-tts-etu-upmc-ensam_amd/lib/libmtts_hip.so

@@ -1,7 +1,8 @@
 #!/bin/bash
 # round 5: the register-staged GEMM / weight-gradient loops with and without the prefetch scheduling fence
 # (MTTS_PIN_PREFETCH): GEMM tests on the fenced build, replay of the step's GEMM launches on both builds, then
-# the step A/B alternating on one box -> gpurun_out/$TAG
+# the step A/B alternating on one box -> gpurun_out/$TAG.  The unfenced build, beside the default one:
+#   MTTS_BUILD_VARIANT=nopin MTTS_EXTRA_HIPCC_FLAGS=-DMTTS_PIN_PREFETCH=0 python matcha-tts-etu-upmc-ensam_amd/build_native.py
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/${TAG:-r5pin}; mkdir -p $O; cd $R
 NOPIN=matcha-tts-etu-upmc-ensam_amd/lib/libmtts_hip_nopin.so
 PIN=matcha-tts-etu-upmc-ensam_amd/lib/libmtts_hip.so
