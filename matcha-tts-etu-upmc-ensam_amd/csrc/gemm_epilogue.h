@@ -185,8 +185,14 @@ enum : int {
     EK_LIN_C32 = 2,  // the same with an fp32 C
     EK_GELU = 3,     // fast GELU, bf16 C_pre and C; bias / dropout at run time; no residual / c_scale
     EK_DGELU = 4,    // fast GELU' on a bf16 aux, bf16 C; bias / dropout at run time; no C_pre / residual / c_scale
+    EK_RELU32 = 5,   // ReLU, fp32 C; bias / dropout / residual / c_scale at run time; no C_pre (the text encoder's FFN)
+    EK_DRELU32 = 6,  // ReLU' on an fp32 aux, fp32 C; the same run-time terms; no C_pre (its backward)
 };
 
+// -DMTTS_EK_RELU=0: the ReLU / ReLU' launches keep the run-time epilogue (A/B builds)
+#ifndef MTTS_EK_RELU
+#define MTTS_EK_RELU 1
+#endif
 __host__ __device__ inline int gemm_epilogue_kind(const mtts_conv_gemm_args &p) {
     const bool fast = p.flags & MTTS_GEMM_F_FAST_ACT, pre16 = p.flags & MTTS_GEMM_F_PRE_BF16,
                c16 = p.flags & MTTS_GEMM_F_C_BF16;
@@ -194,6 +200,10 @@ __host__ __device__ inline int gemm_epilogue_kind(const mtts_conv_gemm_args &p) 
     if (p.act == MTTS_ACT_GELU && fast && pre16 && c16 && p.C_pre && !p.residual && !p.c_scale) return EK_GELU;
     if (p.act == MTTS_ACT_DGELU && fast && pre16 && c16 && !p.C_pre && p.aux && !p.residual && !p.c_scale)
         return EK_DGELU;
+#if MTTS_EK_RELU
+    if (p.act == MTTS_ACT_RELU && !p.C_pre && !c16) return EK_RELU32;
+    if (p.act == MTTS_ACT_DRELU && !p.C_pre && !c16 && !pre16 && p.aux) return EK_DRELU32;
+#endif
     return EK_RT;
 }
 
@@ -204,14 +214,19 @@ template <int V, int EK = EK_RT>
 __device__ __forceinline__ void epilogue_rowv(const mtts_conv_gemm_args &p, int crow, int n, float (&e)[V],
                                               uint32_t s0, uint32_t s1, float keep_scale) {
     constexpr bool RT = EK == EK_RT;
-    const int act = RT ? p.act : EK == EK_GELU ? MTTS_ACT_GELU : EK == EK_DGELU ? MTTS_ACT_DGELU : MTTS_ACT_NONE;
+    constexpr bool RELU = EK == EK_RELU32 || EK == EK_DRELU32;
+    const int act = RT ? p.act
+                       : EK == EK_GELU ? MTTS_ACT_GELU
+                       : EK == EK_DGELU ? MTTS_ACT_DGELU
+                       : EK == EK_RELU32 ? MTTS_ACT_RELU
+                       : EK == EK_DRELU32 ? MTTS_ACT_DRELU : MTTS_ACT_NONE;
     const bool fast = RT ? (p.flags & MTTS_GEMM_F_FAST_ACT) != 0 : true;
-    const bool pre16 = RT ? (p.flags & MTTS_GEMM_F_PRE_BF16) != 0 : true;
-    const bool c16 = RT ? (p.flags & MTTS_GEMM_F_C_BF16) != 0 : EK != EK_LIN_C32;
+    const bool pre16 = RT ? (p.flags & MTTS_GEMM_F_PRE_BF16) != 0 : EK != EK_DRELU32;
+    const bool c16 = RT ? (p.flags & MTTS_GEMM_F_C_BF16) != 0 : EK != EK_LIN_C32 && !RELU;
     const bool has_pre = RT ? p.C_pre != nullptr : EK == EK_GELU;
     const bool has_drop = p.dropout_p > 0.f;
-    const bool has_res = (RT || EK == EK_LIN_C16 || EK == EK_LIN_C32) && p.residual;
-    const bool has_cs = (RT || EK == EK_LIN_C16 || EK == EK_LIN_C32) && p.c_scale;
+    const bool has_res = (RT || EK == EK_LIN_C16 || EK == EK_LIN_C32 || RELU) && p.residual;
+    const bool has_cs = (RT || EK == EK_LIN_C16 || EK == EK_LIN_C32 || RELU) && p.c_scale;
     const size_t off = (size_t)crow * p.ldc + n;
     if (has_pre) {
         if (pre16) store_bf16v<V>(reinterpret_cast<uint16_t *>(p.C_pre) + off, e);
@@ -367,6 +382,8 @@ __device__ __forceinline__ void gemm_epilogue_vec(const mtts_conv_gemm_args &p, 
         case EK_LIN_C32: gemm_epilogue_vec_v<8, TM, TN, EK_LIN_C32>(p, acc, stage, row0, col0, lane); break;
         case EK_GELU: gemm_epilogue_vec_v<8, TM, TN, EK_GELU>(p, acc, stage, row0, col0, lane); break;
         case EK_DGELU: gemm_epilogue_vec_v<8, TM, TN, EK_DGELU>(p, acc, stage, row0, col0, lane); break;
+        case EK_RELU32: gemm_epilogue_vec_v<8, TM, TN, EK_RELU32>(p, acc, stage, row0, col0, lane); break;
+        case EK_DRELU32: gemm_epilogue_vec_v<8, TM, TN, EK_DRELU32>(p, acc, stage, row0, col0, lane); break;
         default: gemm_epilogue_vec_v<8, TM, TN, EK_RT>(p, acc, stage, row0, col0, lane); break;
     }
 }
