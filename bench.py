@@ -315,6 +315,19 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    # N>1: a host watchdog per rank (matcha/watchdog.py) -- a step that makes no progress within
+    # the phase's bound prints rank, phase, graph key, last issued bucket and the device's last completed step /
+    # bucket to stderr and ends the rank with exit code 3 (torch.distributed.run then stops its peers)
+    wd = None
+    wd_bounds = {"init_s": float(os.environ.get("MTTS_WATCHDOG_INIT_S", "600")),
+                 "warmup_step_s": float(os.environ.get("MTTS_WATCHDOG_WARMUP_S", "300")),
+                 "step_s": float(os.environ.get("MTTS_WATCHDOG_S", "60")),
+                 "post_s": float(os.environ.get("MTTS_WATCHDOG_POST_S", "900"))}
+    if world > 1:
+        from matcha.watchdog import StepWatchdog
+
+        wd = StepWatchdog(rank, wd_bounds["init_s"])
+        wd.beat("init: process group up")
     if world == 1 and os.environ.get("MTTS_FORCE_DP") == "1":
         # rehearsal of the data-parallel step on one GPU: a world-size-1 RCCL group, so the bucketed
         # all-reduces run (as copies) exactly as at N>1; never used for reported numbers
@@ -332,6 +345,13 @@ def main():
     graph = not args.no_graph
     trainer = Trainer(model, TrainConfig(precision=args.precision, graph=graph, graph_cache=max(4, args.bucketed),
                                          accumulate_grad_batches=args.accumulate))
+    if wd is not None:
+        from matcha.watchdog import DeviceProgress
+
+        trainer.progress = wd.device = DeviceProgress()
+        trainer.watchdog = wd
+        wd.beat("warm-up (step 0: backward order, bucket layout, RCCL communicator, graph capture)",
+                bound_s=wd_bounds["warmup_step_s"])
     B, Tx, Ty = args.batch, args.tx, args.ty
     if args.bucketed > 0:
         batches = _bucketed_batches(B, Tx, Ty, args.bucketed, rank, world, dev)
@@ -354,10 +374,15 @@ def main():
 
     for i in range(args.warmup):
         trainer.step(step_batches(i))
+        if wd is not None:  # untimed: each warm-up step completes before the next (a hang names its step)
+            torch.cuda.synchronize()
+            wd.beat("warm-up", last_step_done=i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if wd is not None:
+        wd.beat("timed", bound_s=wd_bounds["step_s"])
     t0 = time.perf_counter()
     for i in range(args.steps):
         trainer.step(step_batches(i))
@@ -365,10 +390,19 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    elapsed = torch.tensor([t1 - t0, -(t1 - t0)], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    rank_spread = {"step_ms_max_over_ranks": round(float(elapsed[0]) / args.steps * 1e3, 3),
+                   "step_ms_min_over_ranks": round(-float(elapsed[1]) / args.steps * 1e3, 3)}
+    rank_spread["max_over_min"] = round(float(elapsed[0]) / max(-float(elapsed[1]), 1e-12), 4)
+    elapsed = float(elapsed[0].item())
+    if wd is not None:
+        wd.beat("data-parallel tail measurement", last_step_done=args.warmup + args.steps - 1)
+    # the exposed tail bucket: one extra eager fwd+bwd with the reducer armed (every rank, no update)
+    dp_tail = trainer.measure_dp_tail(step_batches(0)) if trainer.reducer is not None else None
+    if wd is not None:
+        wd.beat("after the data-parallel legs (rank-local measurements)", bound_s=wd_bounds["post_s"])
     if args.profile_child:  # under rocprofv3 (graph_replay_profile): the trace is all that is wanted
         return
     losses = trainer.last_losses.tolist()
@@ -704,7 +738,9 @@ def main():
                              "algorithmic_bytes_per_launch": 12 * cells,
                              "chain_bound": mas_chain_bound(Tx, Ty, mas_ms),
                              "note": "12 B/cell (value+mask read, path write); the API premasks + transposes the "
-                                     "lattice once (column-major DP loads); chain-bound: one wave per utterance"},
+                                     "lattice once (column-major DP loads) from Tx > 128; the DP is chain / issue "
+                                     "bound: one wave per utterance up to Tx = 256, eight pipelined waves beyond "
+                                     "(chain_bound names the kernel shape that ran)"},
             "decoder_mfma": {"train_flops_per_step": flops,
                              "achieved_tflops_step": round(flops / (step_ms * 1e-3) / 1e12, 2),
                              "peak_tflops": FP32_MFMA_TFLOPS if args.precision == "32-true" else BF16_DENSE_TFLOPS},
@@ -716,15 +752,28 @@ def main():
                 "shared_gpu": os.environ.get("MTTS_BENCH_SHARED_GPU") == "1",
                 "buckets": len(trainer.reducer.buckets), "bucket_mb": trainer.cfg.bucket_mb,
                 "flat_floats": trainer.reducer.flat.numel(),
-                "overlapped_in_graph": bool(next(iter(trainer._graphs.values()))["overlap"]) if trainer._graphs else None},
+                "overlapped_in_graph": bool(next(iter(trainer._graphs.values()))["overlap"]) if trainer._graphs else None,
+                "rank_step_time": rank_spread,
+                "tail": dp_tail,
+                "agree_shapes": trainer.cfg.agree_shapes,
+                "agree_shapes_note": "on (default): every rank pads to the max padded Tx / Ty over ranks, so all ranks "
+                                     "replay one graph; a rank's losses then depend on its peers' padded lengths "
+                                     "(GroupNorm statistics, conv bias in padded frames -- SURVEY 0.6)",
+                "grad_semantics": "after a step each .grad holds the SUM over ranks; the fused clip + AdamW applies "
+                                  "the 1 / world mean (GradBucketReducer.mean_grads() gives DDP's means)",
+                "watchdog": None if wd is None else dict(wd_bounds, exit_code=wd.exit_code)},
             "precision_check": precision_check,
             "synthesise": synth,
         }
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(B, Tx, Ty, args.cpu_budget)
         print(json.dumps(rec), flush=True)
+    if wd is not None:
+        wd.beat("teardown", bound_s=120.0)
     if dist.is_initialized():
         dist.destroy_process_group()
+    if wd is not None:
+        wd.stop()
 
 
 if __name__ == "__main__":

@@ -43,8 +43,7 @@ extern "C" {
 
 #define MTTS_CONV_MAX_TAPS 8
 #define MTTS_GEMM_GLDS 32  /* schedule ids 32.. : bf16 LDS-DMA kernels (csrc/conv_gemm_glds.hip)   */
-#define MTTS_GEMM_PK 64    /* schedule ids 64.. : bf16 persistent big-tile LDS-DMA kernels (csrc/conv_gemm_pk.hip) */
-#define MTTS_GEMM_WREG 96  /* schedule ids 96, 97: bf16 weight-stationary kernels, K <= 256 linears (csrc/conv_gemm_wreg.hip) and K = 512..1024 convs / linears (csrc/conv_gemm_wreg16.hip) */
+#define MTTS_GEMM_WREG 96  /* schedule id 96: bf16 weight-stationary kernel, K <= 256 linears (csrc/conv_gemm_wreg.hip) */
 
 /*
  * Implicit GEMM  C[row(b,u), n] = epi( sum_{j<ntaps} sum_{c<cin} A[b*Ti + u*in_stride + off[j], c]
@@ -110,9 +109,8 @@ typedef struct mtts_conv_gemm_args {
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
 /* Same, with an explicit schedule: 0..17 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;
  * 8..17 bf16-only: 64-wide K steps, two K steps in flight), MTTS_GEMM_GLDS + i = the bf16 LDS-DMA schedules
- * (csrc/conv_gemm_glds.hip), MTTS_GEMM_PK + i = the persistent big-tile schedules (csrc/conv_gemm_pk.hip),
- * MTTS_GEMM_WREG / + 1 = the weight-stationary schedules (csrc/conv_gemm_wreg.hip, conv_gemm_wreg16.hip),
- * -1 = heuristic (MTTS_GEMM_TUNE=1: plus the bitwise-safe schedule tuner).
+ * (csrc/conv_gemm_glds.hip), MTTS_GEMM_WREG = the weight-stationary schedule (csrc/conv_gemm_wreg.hip),
+ * -1 = heuristic.
  * For tuning and tests; mtts_conv_gemm picks the configuration itself. */
 int mtts_conv_gemm_tile(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg, void *hip_stream);
 /* With a caller-owned workspace: lets the bf16 LDS-DMA schedules split K over several workgroups

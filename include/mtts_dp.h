@@ -33,6 +33,16 @@ int mtts_dp_comm_destroy(void *comm);
 /* the loaded RCCL's version code, -1 if RCCL cannot be loaded */
 int mtts_dp_rccl_version(void);
 
+/* Device-side progress for a host watchdog (bench.py's N>1 path): *host_out = nslots int32 in coherent
+ * host-mapped memory, zeroed, readable at any time without synchronising the device.
+ * mtts_dp_progress_mark is stream-ordered and capturable: tag < 0 adds one to the device's step count and
+ * writes it to host[0]; tag >= 0 writes steps * 256 + tag to host[slot] (slot >= 1; the reducer marks
+ * bucket k done with tag k + 1 after its all-reduce).  No reference counterpart (the reference has no
+ * multi-GPU step; DDP's own watchdog is torch's ProcessGroupNCCL timeout). */
+int mtts_dp_progress_create(int32_t nslots, void **handle_out, int32_t **host_out);
+int mtts_dp_progress_mark(void *handle, int32_t slot, int32_t tag, void *hip_stream);
+int mtts_dp_progress_destroy(void *handle);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

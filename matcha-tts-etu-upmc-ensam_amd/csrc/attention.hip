@@ -445,7 +445,7 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<BF16, D, TI, DROP>())) vo
         s0 = p.seed[0];
         s1 = p.seed[1];
     }
-    const float inv_keep = 1.f / (1.f - p.dropout_p);
+    const float inv_keep = mtts::dropout_scale(p.dropout_p);
     const uint32_t prow = (uint32_t)(((size_t)b * p.H + h) * T + q);  // dropout row key of this query
     auto body = [&](int buf, int k0, auto has_bias) __attribute__((always_inline)) {
         constexpr bool TB = decltype(has_bias)::value;
@@ -622,7 +622,7 @@ __device__ __forceinline__ void bwd_dq_body(const mtts_attn_args &p, const mtts_
         s0 = p.seed[0];
         s1 = p.seed[1];
     }
-    const float inv_keep = 1.f / (1.f - p.dropout_p);
+    const float inv_keep = mtts::dropout_scale(p.dropout_p);
     const uint32_t prow = (uint32_t)srow;
     // bf16 without dropout: the row constants start the accumulators (S^T - lse, dP^T - D), so the
     // chains end ready for exp2 and the product
@@ -751,7 +751,7 @@ __device__ __forceinline__ void bwd_dkv_body(const mtts_attn_args &p, const mtts
         s0 = p.seed[0];
         s1 = p.seed[1];
     }
-    const float inv_keep = 1.f / (1.f - p.dropout_p);
+    const float inv_keep = mtts::dropout_scale(p.dropout_p);
     const bool fold = BF16 && !drop;  // row constants start the accumulators (as in the dQ kernel)
     auto compute = [&](int buf, int q0) __attribute__((always_inline)) {
         const ST *Q_ = Qs + buf * Gm::RE, *G_ = Gs + buf * Gm::RE;
@@ -999,7 +999,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_short_kernel(mtts_attn_args
         if (p.dropout_p > 0.f) {
             const uint32_t s0 = p.seed[0], s1 = p.seed[1];
             const uint32_t prow = (uint32_t)(((size_t)b * p.H + h) * T + q);
-            const float inv_keep = 1.f / (1.f - p.dropout_p);
+            const float inv_keep = mtts::dropout_scale(p.dropout_p);
 #pragma unroll
             for (int v = 0; v < 16; ++v)
                 s[v] = mtts::dropout_keep(s0, s1, prow, (uint32_t)(wave * 32 + crow(v, lh)), p.dropout_p)
@@ -1111,7 +1111,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_short_kernel(mtts_attn_a
         const bool tb = flag_s[buf];
         if (tb) crow_load16(bias_s + buf * kTile + sub * 32, lh, bv);
         const uint32_t s0 = drop ? p.seed[0] : 0u, s1 = drop ? p.seed[1] : 0u;
-        const float inv_keep = 1.f / (1.f - p.dropout_p);
+        const float inv_keep = mtts::dropout_scale(p.dropout_p);
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
             float x = BF16 ? sacc[v] : sacc[v] * sl2 - lse2;
@@ -1213,7 +1213,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkv_short_kernel(mtts_attn_
         mma_rows<BF16, D>(sacc, Q_, sub * 32 + lr, lh, kf);  // S (rows q, col = this key)
         mma_rows<BF16, D>(pacc, G_, sub * 32 + lr, lh, vf);  // dP
         const uint32_t s0 = drop ? p.seed[0] : 0u, s1 = drop ? p.seed[1] : 0u;
-        const float inv_keep = 1.f / (1.f - p.dropout_p);
+        const float inv_keep = mtts::dropout_scale(p.dropout_p);
         float pr[16], ds[16];
 #pragma unroll
         for (int v = 0; v < 16; ++v) {

@@ -34,7 +34,6 @@
 #include <cstdint>
 
 #include "gemm_epilogue.h"
-#include "conv_gemm_pk.h"
 #include "conv_gemm_wreg.h"
 #include "mtts_common.h"
 #include "mtts_decoder.h"
@@ -1226,8 +1225,7 @@ struct GemmPlan {
 static GemmPlan plan_gemm(const mtts_conv_gemm_args &p, bool bf16, int cfg, int splits) {
     const int M = p.nb * p.To;
     if (cfg < 0) cfg = pick_cfg(p, M, bf16);
-    if (cfg == MTTS_GEMM_WREG || cfg == MTTS_GEMM_WREG + 1) return {cfg, 1, 0};
-    if (cfg >= MTTS_GEMM_PK) return {cfg, 1, mtts::conv_gemm_pk_workspace_bytes(cfg - MTTS_GEMM_PK, p, !bf16)};
+    if (cfg == MTTS_GEMM_WREG) return {cfg, 1, 0};
     splits = pick_splits(p, M, cfg, splits, bf16);
     size_t ws = 0;
     if (cfg >= MTTS_GEMM_GLDS) {
@@ -1262,8 +1260,6 @@ static int resolve_cfg(const mtts_conv_gemm_args &p, bool bf16, int cfg, int M, 
     static const bool wreg_pick = [] { const char *e = getenv("MTTS_GEMM_WREG_PICK"); return !(e && e[0] == '0'); }();
     if (cfg < 0 && bf16 && wreg_pick && mtts::conv_gemm_wreg_applies(p) && mtts::conv_gemm_wreg_preferred(p, M))
         return MTTS_GEMM_WREG;
-    if (cfg < 0 && bf16 && wreg_pick && mtts::conv_gemm_wreg16_applies(p) && mtts::conv_gemm_wreg16_preferred(p, M))
-        return MTTS_GEMM_WREG + 1;
     static const bool ws_pick = [] { const char *e = getenv("MTTS_GEMM_WS_PICK"); return !(e && e[0] == '0'); }();
     // (a bf16 A goes to the LDS-DMA pick below: pick_cfg_ws may answer a register-staged schedule)
     if (cfg < 0 && bf16 && ws_pick && (p.flags & MTTS_GEMM_F_W_SPLIT) &&
@@ -1289,7 +1285,6 @@ static int resolve_cfg(const mtts_conv_gemm_args &p, bool bf16, int cfg, int M, 
 static int launch_plan(const mtts_conv_gemm_args &p, bool bf16, const GemmPlan &pl, int M, void *ws, size_t ws_bytes,
                        hipStream_t st) {
     if (pl.cfg == MTTS_GEMM_WREG) return mtts::conv_gemm_wreg_launch(p, M, st);
-    if (pl.cfg == MTTS_GEMM_WREG + 1) return mtts::conv_gemm_wreg16_launch(p, M, st);
     if (pl.cfg >= MTTS_GEMM_GLDS) {
         int s = pl.splits;
         if (pl.ws > 0 && (!ws || ws_bytes < pl.ws || (uintptr_t)ws % 16)) s = 1;  // no workspace: unsplit
@@ -1303,147 +1298,6 @@ static int launch_plan(const mtts_conv_gemm_args &p, bool bf16, const GemmPlan &
         launch_by_id<false>(pl.cfg, p, M, st, s, static_cast<float *>(ws));
     }
     return mtts::check_launch("conv_gemm_kernel");
-}
-
-// ------------------------------------------------------------------------------------------------
-// Schedule tuning (round 5): the first eager call of a heuristic-scheduled bf16 GEMM shape times the heuristic's
-// schedule against the unsplit LDS-DMA / weight-stationary schedules and keeps the fastest of those whose output is
-// BITWISE equal to the heuristic's (compared on the device) -- so the choice, which depends on timing, never changes
-// a result.  Calls inside a stream capture (and calls whose output aliases an input) use the cache or the
-// heuristic; the captured train step replays the tuned launches.  Per-shape replay sweep that motivated it:
-// 2566 -> 2438 us of the step's bf16 GEMM launches (profiles/r05/sweep/).  Opt-in (MTTS_GEMM_TUNE=1): the
-// eager-timed choices did not move the graph-replayed step (7.643 / 7.637 vs 7.641 / 7.643 ms, alternating runs on
-// one box, profiles/r05/sweep/ab_tune.txt) -- the heuristic is already the bitwise class's best in replay.
-__global__ void bytes_differ_kernel(const unsigned char *a, const unsigned char *b, size_t n, int *neq) {
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        if (a[i] != b[i]) atomicOr(neq, 1);
-}
-
-namespace {
-std::mutex g_tune_mu;
-std::vector<std::pair<std::vector<long long>, int>> g_tune;  // shape key -> schedule id
-
-std::vector<long long> tune_key(const mtts_conv_gemm_args &p, bool bf16) {
-    std::vector<long long> k = {bf16, p.lda, p.Ti, p.To, p.nb, p.in_stride, p.ntaps, p.cin, p.N, p.K, p.Kp, p.act,
-                                p.ldr, p.ldc, p.To_full, p.out_stride, p.out_off, p.ldaux, p.flags,
-                                p.a_scale != nullptr, p.bias != nullptr, p.residual != nullptr, p.c_scale != nullptr,
-                                p.C_pre != nullptr, p.aux != nullptr, p.dropout_p > 0.f};
-    for (int j = 0; j < p.ntaps; ++j) k.push_back(p.off[j]);
-    return k;
-}
-
-bool tune_on() {
-    static const bool on = [] { const char *e = getenv("MTTS_GEMM_TUNE"); return e && e[0] == '1'; }();
-    return on;
-}
-
-size_t out_bytes(const mtts_conv_gemm_args &p, bool pre) {
-    const bool b16 = pre ? (p.flags & MTTS_GEMM_F_PRE_BF16) : (p.flags & MTTS_GEMM_F_C_BF16);
-    return (size_t)p.nb * p.To_full * p.ldc * (b16 ? 2 : 4);
-}
-
-bool overlaps(const void *a, size_t na, const void *b, size_t nb) {
-    if (!a || !b) return false;
-    const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
-    return x < y + nb && y < x + na;
-}
-}  // namespace
-
-static GemmPlan tune_plan(const mtts_conv_gemm_args &p, bool bf16, const GemmPlan &base, int M, void *ws,
-                          size_t ws_bytes, hipStream_t st) {
-    const auto key = tune_key(p, bf16);
-    {
-        std::lock_guard<std::mutex> lk(g_tune_mu);
-        for (const auto &e : g_tune)
-            if (e.first == key) return e.second == base.cfg ? base : GemmPlan{e.second, 1, 0};
-    }
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return base;
-    auto remember = [&](int cfg) {
-        std::lock_guard<std::mutex> lk(g_tune_mu);
-        g_tune.emplace_back(key, cfg);
-    };
-    std::vector<int> cands;
-    if (bf16 && !(p.flags & (MTTS_GEMM_F_A_SPLIT | MTTS_GEMM_F_SPLIT3))) {
-        if (mtts::conv_gemm_glds_applies(p))
-            for (int id : {36, 38, 40, 41, 42, 44, 45, 47})
-                if (MTTS_GEMM_GLDS + id - 32 != base.cfg) cands.push_back(MTTS_GEMM_GLDS + id - 32);
-        if (base.cfg != MTTS_GEMM_WREG && mtts::conv_gemm_wreg_applies(p)) cands.push_back(MTTS_GEMM_WREG);
-    }
-    const size_t cb = out_bytes(p, false), pb = p.C_pre ? out_bytes(p, true) : 0;
-    const size_t ab = (size_t)p.nb * p.Ti * p.lda * ((p.flags & MTTS_GEMM_F_A_BF16) ? 2 : 4);
-    const size_t rb = p.residual ? (size_t)p.nb * p.To_full * p.ldr * 4 : 0;
-    const size_t xb = p.aux ? (size_t)p.nb * p.To_full * p.ldaux * 4 : 0;
-    const bool alias = overlaps(p.C, cb, p.A, ab) || overlaps(p.C, cb, p.residual, rb) || overlaps(p.C, cb, p.aux, xb) ||
-                       overlaps(p.C_pre, pb, p.A, ab) || overlaps(p.C_pre, pb, p.residual, rb) ||
-                       overlaps(p.C_pre, pb, p.aux, xb) || overlaps(p.C, cb, p.C_pre, pb);
-    if (cands.empty() || alias) {
-        remember(base.cfg);
-        return base;
-    }
-    unsigned char *ref = nullptr;
-    int *neq = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    GemmPlan best = base;
-    bool ok = hipMalloc(reinterpret_cast<void **>(&ref), cb + pb + 16) == hipSuccess &&
-              hipMalloc(reinterpret_cast<void **>(&neq), sizeof(int)) == hipSuccess &&
-              hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess;
-    auto timed = [&](const GemmPlan &pl, float *us) {  // one warm launch, then the mean of 3
-        if (launch_plan(p, bf16, pl, M, ws, ws_bytes, st) != MTTS_OK) return false;
-        hipEventRecord(e0, st);
-        for (int i = 0; i < 3; ++i)
-            if (launch_plan(p, bf16, pl, M, ws, ws_bytes, st) != MTTS_OK) return false;
-        hipEventRecord(e1, st);
-        if (hipEventSynchronize(e1) != hipSuccess) return false;
-        float ms = 0.f;
-        hipEventElapsedTime(&ms, e0, e1);
-        *us = ms * 1000.f / 3.f;
-        return true;
-    };
-    auto equal_to_ref = [&]() {
-        hipMemsetAsync(neq, 0, sizeof(int), st);
-        hipLaunchKernelGGL(bytes_differ_kernel, dim3(1024), dim3(256), 0, st, static_cast<const unsigned char *>((void *)p.C),
-                           ref, cb, neq);
-        if (pb)
-            hipLaunchKernelGGL(bytes_differ_kernel, dim3(1024), dim3(256), 0, st,
-                               static_cast<const unsigned char *>((void *)p.C_pre), ref + cb, pb, neq);
-        int h = 1;
-        hipMemcpyAsync(&h, neq, sizeof(int), hipMemcpyDeviceToHost, st);
-        hipStreamSynchronize(st);
-        return h == 0;
-    };
-    float best_us = 0.f;
-    ok = ok && timed(base, &best_us);
-    if (ok) {
-        hipMemcpyAsync(ref, p.C, cb, hipMemcpyDeviceToDevice, st);
-        if (pb) hipMemcpyAsync(ref + cb, p.C_pre, pb, hipMemcpyDeviceToDevice, st);
-        for (int c : cands) {
-            const GemmPlan pl{c, 1, 0};
-            float us = 0.f;
-            if (!timed(pl, &us)) {
-                hipGetLastError();  // an unsupported combination: not a candidate
-                continue;
-            }
-            if (us < 0.97f * best_us && equal_to_ref()) {
-                best = pl;
-                best_us = us;
-            }
-        }
-        // leave the output exactly as the chosen schedule writes it (bitwise the reference's anyway)
-        launch_plan(p, bf16, best, M, ws, ws_bytes, st);
-    }
-    hipStreamSynchronize(st);
-    static const bool log = [] { const char *e = getenv("MTTS_GEMM_TUNE_LOG"); return e && e[0] == '1'; }();
-    if (log)
-        fprintf(stderr, "[mtts tune] M=%d N=%d K=%d taps=%d flags=0x%x act=%d: base %d -> %d (%.2f us, ok=%d, %zu candidates)\n",
-                M, p.N, p.K, p.ntaps, p.flags, p.act, base.cfg, best.cfg, best_us, (int)ok, cands.size());
-    if (e0) hipEventDestroy(e0);
-    if (e1) hipEventDestroy(e1);
-    if (ref) hipFree(ref);
-    if (neq) hipFree(neq);
-    hipGetLastError();
-    remember(ok ? best.cfg : base.cfg);
-    return ok ? best : base;
 }
 
 static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, int cfg, int splits, void *ws,
@@ -1470,39 +1324,25 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
                        ((p.flags & MTTS_GEMM_F_W_SPLIT) && !(p.flags & MTTS_GEMM_F_A_BF16)),
                    "conv_gemm: a split A needs split weight planes and an fp32 A");
     const bool glds_id = cfg >= MTTS_GEMM_GLDS && cfg < MTTS_GEMM_GLDS + mtts::conv_gemm_glds_num_cfgs();
-    const bool pk_id = cfg >= MTTS_GEMM_PK && cfg < MTTS_GEMM_PK + mtts::conv_gemm_pk_num_cfgs();
-    const bool wreg_id = cfg == MTTS_GEMM_WREG, wreg16_id = cfg == MTTS_GEMM_WREG + 1;
-    MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || glds_id || pk_id || wreg_id || wreg16_id,
+    const bool wreg_id = cfg == MTTS_GEMM_WREG;
+    MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || glds_id || wreg_id,
                    "conv_gemm: bad tile config");
     MTTS_CHECK_ARG(splits >= 0, "conv_gemm: bad split count");
     const int M = p.nb * p.To;
     if (M == 0) return MTTS_OK;
     hipStream_t st = static_cast<hipStream_t>(hip_stream);
     const bool bf16 = precision == MTTS_PREC_BF16;
-    if (pk_id) {  // persistent big-tile schedule, explicit id
-        if (!mtts::conv_gemm_pk_applies(cfg - MTTS_GEMM_PK, p, !bf16))
-            return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: persistent schedule needs whole-tap K steps and 16-byte rows");
-        return mtts::conv_gemm_pk_launch(cfg - MTTS_GEMM_PK, p, M, ws, ws_bytes, st, !bf16);
-    }
     if (wreg_id) {  // weight-stationary schedule, explicit id
         if (!bf16 || !mtts::conv_gemm_wreg_applies(p))
             return mtts::fail(MTTS_ERR_UNSUPPORTED,
                               "conv_gemm: weight-stationary schedule needs bf16, one stride-1 tap, K in {80,160,192,256}");
         return mtts::conv_gemm_wreg_launch(p, M, st);
     }
-    if (wreg16_id) {
-        if (!bf16 || !mtts::conv_gemm_wreg16_applies(p))
-            return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: 16-column weight-stationary schedule needs bf16, a bf16 A "
-                                                    "and (taps, cin) in {(3, 256), (1, 512), (1, 1024)}");
-        return mtts::conv_gemm_wreg16_launch(p, M, st);
-    }
     if (glds_id && (!bf16 || !mtts::conv_gemm_glds_applies(p)))
         return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: LDS-DMA schedule needs bf16, cin >= 64 and a 0/1 a_scale");
-    const bool heuristic = cfg < 0;
     cfg = resolve_cfg(p, bf16, cfg, M, &rc);
     if (rc) return rc;
-    GemmPlan pl = plan_gemm(p, bf16, cfg, splits);
-    if (heuristic && splits <= 0 && bf16 && tune_on()) pl = tune_plan(p, bf16, pl, M, ws, ws_bytes, st);
+    const GemmPlan pl = plan_gemm(p, bf16, cfg, splits);
     return launch_plan(p, bf16, pl, M, ws, ws_bytes, st);
 }
 
@@ -1533,7 +1373,6 @@ extern "C" size_t mtts_conv_gemm_workspace_size(const mtts_conv_gemm_args *args,
                                                 int32_t splits) {
     if (!args || args->nb * args->To == 0) return 0;
     const bool bf16 = precision == MTTS_PREC_BF16;
-    if (tile_cfg >= MTTS_GEMM_PK) return plan_gemm(*args, bf16, tile_cfg, splits).ws;
     int rc = MTTS_OK;
     const int cfg = resolve_cfg(*args, bf16, tile_cfg, args->nb * args->To, &rc);
     return rc ? 0 : plan_gemm(*args, bf16, cfg, splits).ws;
@@ -1551,7 +1390,7 @@ __global__ void dropout_apply_kernel(const float *__restrict__ x, float *__restr
     const uint32_t s0 = seed[0], s1 = seed[1];
     const int r = (int)(idx / cols), c = (int)(idx - (int64_t)r * cols);
     const float v = x[(size_t)r * ld + c];
-    y[(size_t)r * ld + c] = mtts::dropout_keep(s0, s1, (uint32_t)r, (uint32_t)c, p) ? v * (1.0f / (1.0f - p)) : 0.f;
+    y[(size_t)r * ld + c] = mtts::dropout_keep(s0, s1, (uint32_t)r, (uint32_t)c, p) ? v * mtts::dropout_scale(p) : 0.f;
 }
 
 extern "C" int mtts_dropout_apply(const float *x, float *y, int32_t rows, int32_t cols, int32_t ld, float p,
@@ -1577,7 +1416,7 @@ __global__ void act_dropout_bwd_kernel(const float *__restrict__ dy, const float
     float v = dy[o];
     if (row_scale) v = v * row_scale[r];
     if (act == MTTS_ACT_RELU && !(y[o] > 0.f)) v = 0.f;
-    if (p > 0.f) v = mtts::dropout_keep(seed[0], seed[1], (uint32_t)r, (uint32_t)c, p) ? v * (1.0f / (1.0f - p)) : 0.f;
+    if (p > 0.f) v = mtts::dropout_keep(seed[0], seed[1], (uint32_t)r, (uint32_t)c, p) ? v * mtts::dropout_scale(p) : 0.f;
     dx[o] = v;
 }
 

@@ -437,7 +437,7 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(mtts_conv_gemm_arg
     if (p.dropout_p > 0.f) {
         s0 = p.seed[0];
         s1 = p.seed[1];
-        keep = 1.0f / (1.0f - p.dropout_p);
+        keep = mtts::dropout_scale(p.dropout_p);
     }
     mtts::epilogue_row4(p, b * p.To_full + u * p.out_stride + p.out_off, n, e, s0, s1, keep);
 }

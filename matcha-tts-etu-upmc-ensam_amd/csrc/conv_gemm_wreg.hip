@@ -238,7 +238,8 @@ bool conv_gemm_wreg_applies(const mtts_conv_gemm_args &p) {
     if (p.lda % (16 / es) || (uintptr_t)p.A % 16 || (uintptr_t)p.W % 16 || p.Kp % 8) return false;
     if ((long long)p.nb * p.Ti * p.lda * es >= (1ll << 31) - (1ll << 20)) return false;
     if ((long long)npl * p.N * p.Kp >= (1ll << 31)) return false;
-    return gemm_epilogue_vec_ok(p);
+    // the kernel always finishes 8 columns per lane (gemm_epilogue_vec_v<8>): N % 8 == 4 would write past the row
+    return gemm_epilogue_vec_ok(p) && gemm_epilogue_vec8_ok(p);
 }
 
 bool conv_gemm_wreg_preferred(const mtts_conv_gemm_args &p, int M) {

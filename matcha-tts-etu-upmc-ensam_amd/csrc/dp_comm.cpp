@@ -140,3 +140,68 @@ extern "C" int mtts_dp_rccl_version(void) {
     if (!r || !r->get_version || r->get_version(&v) != ncclSuccess) return -1;
     return v;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Device-side progress markers for the host watchdog of the data-parallel bench: a coherent,
+// host-mapped int32 array the host reads at any time without synchronising, written by a one-lane kernel that is
+// stream-ordered and capturable -- inside the step's graph after each bucket's all-reduce (reducer stream) and at
+// the end of the step (main stream).  Slot 0 = steps the device has completed (a device-side counter incremented
+// by the step-end mark), slot s > 0 = steps * 256 + tag of the last mark on that slot (tag = bucket index + 1).
+namespace {
+struct Progress {
+    int32_t *host = nullptr;  // hipHostMalloc(mapped | coherent): the watchdog reads it
+    int32_t *dev = nullptr;   // device step counter
+    int32_t nslots = 0;
+};
+
+// vector stores only (the store address is lane-dependent; one lane is active)
+__global__ void progress_mark_kernel(int32_t *__restrict__ dev, int32_t *host, int32_t slot, int32_t tag) {
+    const int l = threadIdx.x;
+    if (l != 0) return;
+    int32_t steps = dev[l];
+    if (tag < 0) {
+        steps += 1;
+        dev[l] = steps;
+        __hip_atomic_store(host + l, steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        __hip_atomic_store(host + slot + l, steps * 256 + tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+}  // namespace
+
+extern "C" int mtts_dp_progress_create(int32_t nslots, void **handle_out, int32_t **host_out) {
+    MTTS_CHECK_ARG(handle_out && host_out && nslots >= 1 && nslots <= 64, "dp_progress_create: bad args");
+    Progress *pr = new Progress();
+    pr->nslots = nslots;
+    if (hipHostMalloc(reinterpret_cast<void **>(&pr->host), sizeof(int32_t) * nslots,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&pr->dev), sizeof(int32_t)) != hipSuccess ||
+        hipMemset(pr->dev, 0, sizeof(int32_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        if (pr->host) hipHostFree(pr->host);
+        if (pr->dev) hipFree(pr->dev);
+        delete pr;
+        return mtts::fail(MTTS_ERR_HIP, "dp_progress_create: allocation failed");
+    }
+    std::memset(pr->host, 0, sizeof(int32_t) * nslots);
+    *handle_out = pr;
+    *host_out = pr->host;
+    return MTTS_OK;
+}
+
+extern "C" int mtts_dp_progress_mark(void *handle, int32_t slot, int32_t tag, void *hip_stream) {
+    Progress *pr = static_cast<Progress *>(handle);
+    MTTS_CHECK_ARG(pr && slot >= 0 && slot < pr->nslots && (tag < 0 || slot > 0), "dp_progress_mark: bad args");
+    hipLaunchKernelGGL(progress_mark_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(hip_stream), pr->dev,
+                       pr->host, slot, tag);
+    return mtts::check_launch("progress_mark_kernel");
+}
+
+extern "C" int mtts_dp_progress_destroy(void *handle) {
+    Progress *pr = static_cast<Progress *>(handle);
+    if (!pr) return MTTS_OK;
+    hipDeviceSynchronize();
+    hipHostFree(pr->host);
+    hipFree(pr->dev);
+    delete pr;
+    return MTTS_OK;
+}

@@ -120,7 +120,7 @@ __device__ __forceinline__ void gemm_epilogue(const mtts_conv_gemm_args &p, f32x
                 }
                 if (p.dropout_p > 0.f)
                     val = dropout_keep(s0, s1, (uint32_t)crow, (uint32_t)n, p.dropout_p)
-                              ? val * (1.0f / (1.0f - p.dropout_p))
+                              ? val * dropout_scale(p.dropout_p)
                               : 0.f;
                 if (p.residual) val += p.residual[crow * p.ldr + n];
                 if (p.c_scale) val *= p.c_scale[crow];
@@ -327,7 +327,7 @@ __device__ __forceinline__ void gemm_epilogue_vec_v(const mtts_conv_gemm_args &p
         s0 = p.seed[0];
         s1 = p.seed[1];
     }
-    const float keep_scale = drop ? 1.0f / (1.0f - p.dropout_p) : 1.0f;
+    const float keep_scale = drop ? dropout_scale(p.dropout_p) : 1.0f;
     const int rsub = lane / L, cv = lane % L;  // this lane's row within an RP-row slab and its column chunk
 #pragma unroll
     for (int i = 0; i < TM; ++i) {

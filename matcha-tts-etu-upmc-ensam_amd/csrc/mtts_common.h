@@ -16,14 +16,21 @@ namespace mtts {
 // rate on CDNA; the row product is loop-invariant in the epilogues (hoisted) and the 16-byte epilogues hand
 // adjacent column pairs to one hash (the compiler merges the identical calls): one finalizer per two elements
 // (round 5: the FeedForward GELU epilogue spent ~35 % of its VALU cycles in the per-element hash).  The keep
-// probability is 1 - p up to the 2^-16 grid (p = 0.1: 0.100006).  Every site that regenerates a mask calls
-// this with the same (row, col), so forward and backward agree.
+// probability is quantised to the 2^-16 grid: an element is kept iff u >= ceil(p * 65536), so P(keep) =
+// (65536 - ceil(p * 65536)) / 65536 (p = 0.1: 0.899994), and dropout_scale() rescales by exactly its inverse --
+// E[kept * scale] = 1 with no grid bias.  Every site that regenerates a mask calls this with the same
+// (row, col), so forward and backward agree.
 __device__ __forceinline__ bool dropout_keep(uint32_t seed_lo, uint32_t seed_hi, uint32_t row, uint32_t col,
                                              float p) {
     uint32_t x = ((row * 0x9E3779B1u) ^ (((col >> 1) + 0x7F4A7C15u) * 0x85EBCA77u) ^ seed_lo) + seed_hi;
     x ^= x >> 16; x *= 0x85EBCA6Bu; x ^= x >> 13; x *= 0xC2B2AE35u; x ^= x >> 16;
     const uint32_t u = (col & 1u) ? (x >> 16) : (x & 0xFFFFu);
     return (float)u * (1.0f / 65536.0f) >= p;
+}
+
+// 1 / P(keep) of dropout_keep: 65536 / (65536 - ceil(p * 65536)) (p * 65536 is exact in fp32); 1 at p <= 0
+__host__ __device__ __forceinline__ float dropout_scale(float p) {
+    return p > 0.f ? 65536.0f / (65536.0f - ceilf(p * 65536.0f)) : 1.0f;
 }
 
 // Tap offset j of a conv argument struct (static indexing only: no private-memory copy of off[]).

@@ -448,7 +448,7 @@ __global__ __launch_bounds__(kThreads) void layernorm_fwd_kernel(const float *__
         sd0 = seed[0];
         sd1 = seed[1];
     }
-    const float inv_keep = 1.f / (1.f - p);
+    const float inv_keep = mtts::dropout_scale(p);
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int row = row0 + q;
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(kThreads) void layernorm_bwd_kernel(const float *__
         sd0 = seed[0];
         sd1 = seed[1];
     }
-    const float inv_keep = 1.f / (1.f - p);
+    const float inv_keep = mtts::dropout_scale(p);
     const int rbeg = blockIdx.x * rows_per_block;
     const int rend = min(M, rbeg + rows_per_block);
     for (int r0 = rbeg + wv * R; r0 < rend; r0 += (kThreads / 64) * R) {

@@ -29,7 +29,9 @@ Gradient averaging (mean over ranks, DDP's semantics) happens before clipping: T
 RcclComm SUMS (ncclSum) and leaves the factor ``post_scale = 1 / world`` to the consumer -- the Trainer's
 fused clip + AdamW multiplies by it (``mtts_clip_adamw_scaled``: exact for a power-of-two world, so the
 update equals the ncclAvg one bit for bit), any other consumer gets the flat buffer scaled in place by
-``finish()``.  Why: RCCL's ncclAvg is a pre-multiply-sum, and at one rank it still launches a read-modify-write
+``finish()``.  So with RcclComm under the Trainer's graph step, each parameter's ``.grad`` after the step holds
+the SUM over ranks, not DDP's mean (``GradBucketReducer.grad_scale_applied``; ``mean_grads()`` returns the
+means): anything that reads ``.grad`` after a step (norm logging, comparisons with DDP) must use that.  Why: RCCL's ncclAvg is a pre-multiply-sum, and at one rank it still launches a read-modify-write
 kernel over the whole 76 MB buffer (oneRankReduce, ~143 us of the forced-DP N=1 step, profiles/r05/dp/);
 an in-place ncclSum at one rank launches nothing.
 """
@@ -181,6 +183,12 @@ class GradBucketReducer:
         # reduce_now() scale the flat buffer in place when the comm leaves sums
         self.grad_scale_applied = False
         self.copied = {}  # bucket -> shapes of the gradients its last pack copied (not written in place)
+        # bench.py's N>1 path (matcha/watchdog.py): the host watchdog hears of every bucket issue; the device
+        # marks each bucket's completed all-reduce (a graph node after it on the reducer stream)
+        self.watchdog = None
+        self.progress = None
+        # measure_tail(): HIP events around the last bucket's pack + all-reduce on the reducer stream
+        self.tail_events = None
 
     # -------------------------------------------------------------------- per step
     def arm(self, scalars: torch.Tensor, overlap: bool, comm: bool = True) -> None:
@@ -233,6 +241,8 @@ class GradBucketReducer:
         from matcha.models.components import _ops as OPS
 
         lo, hi = self.spans[k]
+        if self.watchdog is not None:
+            self.watchdog.note(bucket_issued=k, buckets=len(self.buckets))
         if self.overlap and self.stream is not None:
             # the bucket's weight gradients may still be queued: they run on the deferral's side stream
             # (joined at the deferral's exit); pack + all-reduce here wait for the main and the side stream
@@ -241,13 +251,22 @@ class GradBucketReducer:
             if side is not None:
                 self.stream.wait_stream(side)
             with torch.cuda.stream(self.stream):
+                tail = self.tail_events is not None and k == len(self.buckets) - 1
+                if tail:
+                    self.tail_events["start"].record(self.stream)
                 self._pack(k)
                 self.comm.all_reduce_(self.flat[lo:hi])
-            return
-        OPS.flush_deferred_grad_sums()  # on the current stream (joins the side stream first)
-        self._pack(k)
-        if self.overlap:  # CPU (gloo): eager, in order
-            self.comm.all_reduce_(self.flat[lo:hi])
+                if tail:
+                    self.tail_events["end"].record(self.stream)
+                if self.progress is not None:
+                    self.progress.mark_bucket(k, self.stream)
+        else:
+            OPS.flush_deferred_grad_sums()  # on the current stream (joins the side stream first)
+            self._pack(k)
+            if self.overlap:  # CPU (gloo): eager, in order
+                self.comm.all_reduce_(self.flat[lo:hi])
+        if self.watchdog is not None:
+            self.watchdog.beat(bucket_returned=k)
 
     def warm(self) -> None:
         """One eager all-reduce per bucket span on every rank (all ranks call this together, when the
@@ -282,6 +301,8 @@ class GradBucketReducer:
                                f"(first: index {missing[:3]}); the bucket layout assumes a fixed set")
         if self.overlap:
             if self.stream is not None:
+                if self.tail_events is not None:  # the backward's end on the main stream, before the join
+                    self.tail_events["bwd_end"].record(torch.cuda.current_stream(self.device))
                 torch.cuda.current_stream(self.device).wait_stream(self.stream)
             self._post_scale()
         self.attach_views()
@@ -295,6 +316,14 @@ class GradBucketReducer:
         """No-overlap mode: one all-reduce of the packed buffer (eager, e.g. after a graph replay)."""
         self.comm.all_reduce_(self.flat)
         self._post_scale()
+
+    def mean_grads(self) -> list:
+        """The parameters' gradients as DDP's means over ranks (``.grad`` holds sums when the optimizer applies
+        the 1 / world factor itself)."""
+        ps = getattr(self.comm, "post_scale", 1.0)
+        if ps == 1.0 or not self.grad_scale_applied:
+            return list(self.views)
+        return [v * ps for v in self.views]
 
     def attach_views(self) -> None:
         for p, v in zip(self.params, self.views):

@@ -1733,7 +1733,8 @@ class _PreLNAttentionTM(torch.autograd.Function):
         M, C = h2.shape
         B, T = shp[0], shp[1]
         lnw, lnb = _f32c(ln_w), _f32c(ln_b)
-        n, mean, rstd = _ln_fwd(h2, lnw, lnb, eps, prec == PREC_BF16 and _PRELN_N16)
+        # (not under precise_forward: its bf16x3 / fp32 GEMMs read the fp32 A's low bits -- ADVICE r5)
+        n, mean, rstd = _ln_fwd(h2, lnw, lnb, eps, prec == PREC_BF16 and _PRELN_N16 and not _PRECISE.get())
         Wqkv, Kq = packed(spec_linear((wq, wk, wv)), prec)
         Wo, Ko = packed(spec_linear((w_out,)), prec)
         ctx.wqkv_t = packed(spec_linear((wq, wk, wv), dgrad=True), prec)
@@ -1812,7 +1813,8 @@ class _PreLNFeedForwardTM(torch.autograd.Function):
         # bf16 LayerNorm output (round 5, _PRELN_FF_N16): the GELU up-projection runs on the weight-stationary
         # kernel, which rounds an fp32 A to bf16 at its fragment read anyway -- the same products, half the bytes
         # (rounds 2-4 kept it fp32: the register-staged schedule then hid the GELU epilogue better)
-        n, mean, rstd = _ln_fwd(h2, lnw, lnb, eps, prec == PREC_BF16 and _PRELN_FF_N16)
+        # (not under precise_forward, whose split-A GEMMs need the fp32 LN output -- ADVICE r5)
+        n, mean, rstd = _ln_fwd(h2, lnw, lnb, eps, prec == PREC_BF16 and _PRELN_FF_N16 and not _PRECISE.get())
         W1p, K1p = packed(spec_linear((w1,), one_plane=not _FF1_SPLIT), prec)
         W2p, K2p = packed(spec_linear((w2,), one_plane=not _FF2_SPLIT), prec)
         ctx.w2t = packed(spec_linear((w2,), dgrad=True), prec)

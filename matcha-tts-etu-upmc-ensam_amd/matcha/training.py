@@ -248,6 +248,10 @@ class Trainer:
         self._recorder = None
         self._arm = None  # (overlap,) while the reducer is to be armed in the next backward
         self._graphs = collections.OrderedDict()
+        # bench.py's N>1 path (matcha/watchdog.py): a host watchdog told of every step / graph key / bucket issue,
+        # and device progress markers captured into the step (one after each bucket's all-reduce, one at its end)
+        self.watchdog = None
+        self.progress = None
         # a gloo group for the host-side agreements (padded shapes, bucket layout): never syncs the GPU
         self._host_group = None
         if self.dp and self.world > 1:
@@ -469,6 +473,7 @@ class Trainer:
             if first_enc is not None:
                 seams, mb = (first_enc,), max(mb, self.cfg.seam_bucket_mb)
         self.reducer = DP.GradBucketReducer(order, comm, mb, self.dev, seams=seams)
+        self.reducer.watchdog, self.reducer.progress = self.watchdog, self.progress
         if isinstance(self.optimizer, _FlatClipAdamW):  # the mean over ranks rides in the fused optimizer step
             self.optimizer.grad_scale = comm.post_scale
             self.reducer.grad_scale_applied = True
@@ -508,6 +513,8 @@ class Trainer:
                 dist.all_reduce(logged)
                 logged = logged / self.world
         self._clip_and_update()
+        if self.progress is not None and self.dev.type == "cuda":
+            self.progress.mark_step(torch.cuda.current_stream(self.dev))
         self.optimizer.zero_grad(set_to_none=True)
         return logged
 
@@ -578,6 +585,8 @@ class Trainer:
                 self.reducer.finish()  # joins the forked all-reduces; .grad -> flat views
                 if overlap:
                     self._clip_and_update()
+                    if self.progress is not None:  # the device's "step done" marker, a node of the graph
+                        self.progress.mark_step(torch.cuda.current_stream(self.dev))
             else:
                 e["logged"] = self._fwd_bwd(static)
         e["fb_grads"] = [p.grad for p in gparams]  # graph-pool outputs, kept alive with the graph
@@ -593,11 +602,13 @@ class Trainer:
         return e
 
     def _agree_shapes(self, batches):
-        """TrainConfig.agree_shapes (N>1 graph step, on by default): MAX over ranks of each micro-batch's padded Tx /
+        """TrainConfig.agree_shapes (N>1 graph step, ON by default): MAX over ranks of each micro-batch's padded Tx /
         Ty (and one batch size), then zero padding up to it, so every rank looks up the same key.  The padded
         frames are masked, but the decoder's arithmetic depends on the padded length (GroupNorm statistics
-        over the whole padded length, conv bias leaking into padded frames -- SURVEY 0.6), so a rank's losses
-        then depend on its peers' lengths; the default keeps each rank's own padding."""
+        over the whole padded length, conv bias leaking into padded frames -- SURVEY 0.6), so with the default a
+        rank's losses depend on its peers' padded lengths (tests/test_distributed_cpu.py measures the difference
+        against per-rank padding); agree_shapes=False keeps each rank's own padding, as the reference's DDP
+        would."""
         if not (self.cfg.agree_shapes and self.dp and self.world > 1 and self.cfg.graph):
             return batches
         dims = torch.tensor([[b["x"].shape[1], b["y"].shape[2], b["x"].shape[0], -b["x"].shape[0]] for b in batches],
@@ -620,6 +631,9 @@ class Trainer:
     def _graph_step(self, batches):
         batches = self._agree_shapes(batches)
         key = tuple(tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(b.items())) for b in batches)
+        if self.watchdog is not None:
+            self.watchdog.note(graph_key="|".join(f"B{b['x'].shape[0]}xTx{b['x'].shape[1]}xTy{b['y'].shape[-1]}"
+                                                  for b in batches), graph_cached=key in self._graphs)
         e = self._graphs.get(key)
         if e is None:
             e = self._graph_capture(batches)
@@ -639,7 +653,40 @@ class Trainer:
         if not e["overlap"]:  # torch.distributed transport: one eager all-reduce of the packed buffer
             self.reducer.reduce_now()
             e["g_opt"].replay()
+            if self.progress is not None:
+                self.progress.mark_step(torch.cuda.current_stream(self.dev))
         return self.reducer.scalars().clone()  # the flat buffer is overwritten by the next replay
+
+    def measure_dp_tail(self, batches) -> dict | None:
+        """The data-parallel step's exposed tail: ONE extra eager forward + backward with the
+        reducer armed exactly as in the graph step (every rank calls it together; no optimizer update, results
+        discarded), with HIP events on the main stream at the end of the backward and on the reducer stream
+        around the last bucket's pack + all-reduce.  Returns the all-reduce's own time and the part of it the
+        main stream waits for (exposed = end of the last all-reduce - end of the backward, >= 0).  None unless a
+        capturable (RCCL) reducer runs on a GPU."""
+        r = self.reducer
+        if r is None or not self.dp or self.dev.type != "cuda" or not r.comm.capturable:
+            return None
+        ev = {k: torch.cuda.Event(enable_timing=True) for k in ("start", "end", "bwd_end")}
+        r.tail_events = ev
+        for p in self.params:
+            p.grad = None
+        self._arm = True
+        try:
+            self._fwd_bwd(self._agree_shapes(batches))
+        finally:
+            self._arm = None
+            OPS.set_grad_slots(None)
+            r.tail_events = None
+        r.finish()
+        torch.cuda.synchronize(self.dev)
+        ar = ev["start"].elapsed_time(ev["end"])
+        exposed = max(0.0, ev["bwd_end"].elapsed_time(ev["end"]))
+        return {"tail_bucket": len(r.buckets) - 1, "tail_bucket_mb": round((r.spans[-1][1] - r.spans[-1][0]) * 4 / 2 ** 20, 3),
+                "tail_pack_allreduce_us": round(ar * 1e3, 1), "tail_exposed_us": round(exposed * 1e3, 1),
+                "note": "one eager fwd+bwd after the timed region, reducer armed as in the graph step: HIP events "
+                        "around the last bucket's pack + all-reduce (reducer stream) and at the backward's end "
+                        "(main stream); exposed = all-reduce end - backward end"}
 
     # ------------------------------------------------------------------------------------ api
     def step(self, batches: list[dict]) -> torch.Tensor:
@@ -647,9 +694,13 @@ class Trainer:
         device tensor [dur, prior, diff, total] (mean over micro-batches and ranks); nothing here
         synchronises with the host."""
         assert len(batches) == self.cfg.accumulate_grad_batches
+        if self.watchdog is not None:
+            self.watchdog.beat(step_enqueueing=self.global_step)
         logged = self._graph_step(batches) if self.cfg.graph else self._eager_step(batches)
         self.global_step += 1
         self.last_losses = logged
+        if self.watchdog is not None:
+            self.watchdog.beat(last_step_enqueued=self.global_step - 1)
         return logged
 
     def on_epoch_end(self):

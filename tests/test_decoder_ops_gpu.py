@@ -678,3 +678,38 @@ def test_conv_transpose_tm_row_strided_grad(prec):
     ref = lambda x, w, b: torch.cat(  # noqa: E731
         [F.conv_transpose1d((x * m[..., None]).transpose(1, 2), w, b, 2, 1).transpose(1, 2), other], -1)
     _run(lambda x, w, b: torch.cat([conv_transpose_tm(x, w, b, m), other], -1), ref, [x, w, b], prec)
+
+
+@pytest.mark.parametrize("p", [0.1, 0.05, 0.3])
+def test_dropout_keep_rate_unbiased_and_pairs_independent(p):
+    """the counter-based mask (mtts_common.h dropout_keep: one hash per column pair, 16-bit uniforms) keeps
+    an element with probability (65536 - ceil(p * 65536)) / 65536 and dropout_scale rescales by exactly its inverse,
+    so the mean of dropout(ones) is 1 up to sampling noise (no 2^-16 grid bias); the even / odd columns of a pair
+    (the two halves of one hash) and adjacent rows are uncorrelated."""
+    from matcha import _native as N
+    from matcha.models.components import _ops as O
+
+    rows, cols = 4096, 4096
+    x = torch.ones(rows, cols, device=DEV)
+    y = torch.empty_like(x)
+    seed = torch.tensor([987654321, 12345], dtype=torch.int32, device=DEV)
+    N.check(N.lib().mtts_dropout_apply(x.data_ptr(), y.data_ptr(), rows, cols, cols, float(p), seed.data_ptr(),
+                                       O._stream(y)), "mtts_dropout_apply")
+    torch.cuda.synchronize()
+    keep = (y != 0).double()
+    n = keep.numel()
+    want_keep = (65536 - math.ceil(p * 65536)) / 65536
+    sd = math.sqrt(want_keep * (1 - want_keep) / n)
+    assert abs(keep.mean().item() - want_keep) < 5 * sd
+    scale = y[y != 0].unique()
+    assert scale.numel() == 1 and scale.item() == pytest.approx(1.0 / want_keep, rel=1e-7)
+    assert abs(y.double().mean().item() - 1.0) < 5 * sd / want_keep  # unbiased
+    k = keep - keep.mean()
+
+    def corr(a, b):
+        return ((a * b).mean() / (a.std() * b.std())).item()
+
+    lim = 5.0 / math.sqrt(n / 2)
+    assert abs(corr(k[:, 0::2], k[:, 1::2])) < lim  # the two halves of one hash
+    assert abs(corr(k[:, 1:-1:2], k[:, 2::2])) < lim  # across adjacent pairs
+    assert abs(corr(k[:-1], k[1:])) < lim  # adjacent rows

@@ -51,7 +51,15 @@ def _model(dev, seed):
     return m
 
 
-def _worker(rank, world, port, precision, q):
+def _pad_to(b, ty):
+    """Trainer._agree_shapes' zero padding of a batch (and its injected z) to ty frames."""
+    b = dict(b)
+    for k in ("y", "z"):
+        b[k] = torch.nn.functional.pad(b[k], (0, ty - b[k].shape[2]))
+    return b
+
+
+def _worker(rank, world, port, precision, q, agree=False):
     import sys
 
     from pathlib import Path
@@ -68,7 +76,7 @@ def _worker(rank, world, port, precision, q):
         from matcha.training import TrainConfig, Trainer
 
         m = _model(dev, seed=rank)  # different init per rank: the Trainer broadcasts rank 0's weights
-        tr = Trainer(m, TrainConfig(graph=True, precision=precision, bucket_mb=4.0, agree_shapes=False))
+        tr = Trainer(m, TrainConfig(graph=True, precision=precision, bucket_mb=4.0, agree_shapes=agree))
         b = _shard(rank, dev)
         logs = [tr.step([b]).cpu() for _ in range(STEPS)]
         torch.cuda.synchronize()
@@ -82,12 +90,16 @@ def _worker(rank, world, port, precision, q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("precision", ["bf16-mixed"])
-def test_two_ranks_real_model_graph_step_equals_mean_gradient(precision):
+@pytest.mark.parametrize("precision,agree", [("bf16-mixed", False), ("bf16-mixed", True)])
+def test_two_ranks_real_model_graph_step_equals_mean_gradient(precision, agree):
+    """agree=False: each rank keeps its own padding (the reference's DDP semantics).  agree=True (the Trainer's
+    default): every rank pads to the max padded length over ranks (Ty 96), so the result equals one
+    process over the shards padded to 96; its distance from per-rank padding -- the cost of the default -- is
+    measured and printed (the padded frames enter the decoder's GroupNorm statistics)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, precision, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, precision, q, agree)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -102,18 +114,35 @@ def test_two_ranks_real_model_graph_step_equals_mean_gradient(precision):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert res[0][2] == res[1][2] == 2  # the communicator spans both ranks
     assert res[0][3] >= 3  # several buckets exercised
-    assert res[0][4] != res[1][4]  # each rank captured its own padded shape
+    assert (res[0][4] == res[1][4]) == agree  # own padded shapes, or one agreed shape
 
     # one process, the mean gradient: accumulate_grad_batches=2 over the two shards, each at its own length
+    # (agree: both padded to the max, as the ranks did); micro-batches not merged, so each shard's backward runs
+    # alone exactly as on its rank
     from matcha.training import TrainConfig, Trainer
 
     dev = torch.device("cuda:0")
-    m = _model(dev, seed=0)
-    tr = Trainer(m, TrainConfig(graph=True, precision=precision, accumulate_grad_batches=2))
-    b0, b1 = _shard(0, dev), _shard(1, dev)
-    logs = torch.stack([tr.step([b0, b1]).cpu() for _ in range(STEPS)])
-    torch.cuda.synchronize()
-    want = {n: p.detach().cpu() for n, p in m.named_parameters()}
+
+    def one_process(pad):
+        m = _model(dev, seed=0)
+        tr = Trainer(m, TrainConfig(graph=True, precision=precision, accumulate_grad_batches=2,
+                                    merge_micro_batches=False))
+        b0, b1 = _shard(0, dev), _shard(1, dev)
+        if pad:
+            ty = max(TY.values())
+            b0, b1 = _pad_to(b0, ty), _pad_to(b1, ty)
+        lg = torch.stack([tr.step([b0, b1]).cpu() for _ in range(STEPS)])
+        torch.cuda.synchronize()
+        return {n: p.detach().cpu() for n, p in m.named_parameters()}, lg
+
+    want, logs = one_process(agree)
+    if agree:  # the default's cost against the reference's per-rank padding, measured
+        own, own_logs = one_process(False)
+        dl = ((logs - own_logs).abs() / own_logs.abs().clamp_min(1e-12)).max(0).values
+        dp = max(((want[n] - own[n]).norm() / own[n].norm().clamp_min(1e-12)).item() for n in own)
+        print(f"\nagree_shapes=True vs per-rank padding after {STEPS} steps: logged [dur, prior, diff, total] max rel "
+              f"diff {[f'{v:.3e}' for v in dl.tolist()]}, max per-tensor parameter rel diff {dp:.3e}")
+        assert torch.isfinite(dl).all()
 
     for n in want:
         assert torch.equal(res[0][0][n], res[1][0][n]), n  # replicas identical

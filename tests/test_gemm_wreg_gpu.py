@@ -112,85 +112,30 @@ def test_wreg_heuristic_and_unsupported_shapes():
         O._gemm(x3, 50, 50, 2, 1, [-1, 0, 1], 256, Wp3, Kp3, 128, y, 50, prec=O.PREC_BF16, tile_cfg=WREG)
 
 
-WREG16 = 97  # MTTS_GEMM_WREG + 1: 16 columns per wave, K = 768 (3 taps x 256) / 512 / 1024
-
-
-@pytest.mark.parametrize("kind", ["lin16", "lin32", "runtime"])
-@pytest.mark.parametrize("B,T,cin,N,taps,split,masked", [
-    (3, 301, 256, 256, [-1, 0, 1], True, True),     # decoder k = 3 conv, two planes, ragged rows + mask
-    (2, 150, 256, 160, [1, 0, -1], True, False),    # the dgrad's descending taps; N not a multiple of 64
-    (4, 77, 256, 512, [-1, 0, 1], False, True),
-    (2, 300, 1024, 256, [0], True, False),          # FeedForward down-projection, K = 1024
-    (5, 61, 512, 192, [0], False, True),            # K = 512
-])
-def test_wreg16_vs_float64_and_lds_dma(kind, B, T, cin, N, taps, split, masked):
-    """Schedule 97 against a float64 product of the same bf16 operands (the row mask and the per-utterance tap
-    zero padding included) and against the LDS-DMA schedule 41 on the whole epilogue: not bitwise (16x16x32
-    MFMAs sum 32 products per instruction, the 32x32x16 kernels 16), so within fp32 accumulation error; and
-    deterministic run to run."""
+@pytest.mark.parametrize("kind", ["lin16", "lin32", "dgelu"])
+def test_wreg_refuses_n_mod_8_eq_4(kind):
+    """the kernel finishes 8 columns per lane, so N % 8 == 4 (here N = 196 in rows of ldc = 200) must
+    not reach it: the heuristic picks another schedule (bitwise equal to schedule 41, the 4 columns past N left
+    untouched) and an explicit request fails loudly."""
+    from matcha import _native as N
     from matcha.models.components import _ops as O
 
-    g = torch.Generator(device="cpu").manual_seed(B * T + cin + N)
-    K = cin * len(taps)
-    x = torch.randn(B, T, cin, generator=g).bfloat16().float()
-    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV)
-    if split:
-        hi = w.bfloat16()
-        Wp = torch.cat([hi, (w - hi.float()).bfloat16()]).contiguous()
-        Wp._mtts_w_split = True
-        Kp = K
-        wq = hi.float() + (w - hi.float()).bfloat16().float()
-    else:
-        Wp, Kp = O.pack_weight(w, O.PREC_BF16)
-        wq = w.bfloat16().float()
-    kw = dict(act=O.ACT_NONE)
-    msk = (torch.rand(B * T, generator=g) > 0.25).float() if masked else torch.ones(B * T)
-    if masked:
-        kw["a_scale"] = msk.to(DEV)
-    c16 = kind == "lin16"
-    if kind in ("lin32", "runtime"):
-        kw["bias"] = torch.randn(N, generator=g).to(DEV)
-        kw["residual"] = torch.randn(B, T, N, generator=g).to(DEV)
-    if kind == "runtime":
-        kw["act"] = O.ACT_RELU
-    A = x.to(DEV).bfloat16()
+    B, T, K, Nn, ld = 2, 150, 256, 196, 200
+    A, Wp, Kp, _, kw, x, w = _case(kind, B, T, K, Nn, True, False, True, seed=5)
+    for k in ("residual", "aux"):  # epilogue streams with the output's row pitch
+        if k in kw:
+            t = torch.zeros(B, T, ld, device=DEV, dtype=kw[k].dtype)
+            t[..., :Nn] = kw[k]
+            kw[k] = t
+    dt = torch.bfloat16 if kind in ("lin16", "dgelu") else torch.float32
     outs = []
-    for cfg in (WREG16, WREG16, 41):
-        C = torch.full((B, T, N), float("nan"), device=DEV, dtype=torch.bfloat16 if c16 else torch.float32)
-        O._gemm(A, T, T, B, 1, taps, cin, Wp, Kp, N, C, T, prec=O.PREC_BF16, tile_cfg=cfg, **kw)
+    for cfg in (-1, 41):
+        C = torch.full((B, T, ld), float("nan"), device=DEV, dtype=dt)
+        O._gemm(A, T, T, B, 1, [0], K, Wp, Kp, Nn, C, T, prec=O.PREC_BF16, tile_cfg=cfg, **kw)
         torch.cuda.synchronize()
-        outs.append(C.float())
-    assert torch.equal(outs[0], outs[1])  # deterministic
-    # float64 reference: implicit GEMM over the taps with per-utterance zero padding and the row mask on A
-    xm = (x.double() * msk.double().view(B, T, 1))
-    ref = torch.zeros(B, T, N, dtype=torch.float64)
-    wr = wq.double().cpu().view(N, len(taps), cin)
-    for j, o in enumerate(taps):
-        src = torch.zeros_like(xm)
-        lo, hi_ = max(0, -o), min(T, T - o)
-        src[:, lo:hi_] = xm[:, lo + o:hi_ + o]
-        ref += src @ wr[:, j].T
-    if kind in ("lin32", "runtime"):
-        ref += kw["bias"].double().cpu()
-        if kind == "runtime":
-            ref = ref.clamp_min(0)
-        ref += kw["residual"].double().cpu()
-    scale = ref.abs().max().item()
-    tol = (2 ** -7 if c16 else 1e-5) * scale
-    assert (outs[0].double().cpu() - ref).abs().max().item() <= tol
-    assert (outs[0] - outs[2]).abs().max().item() <= (2 ** -7 if c16 else 1e-5) * scale
-
-
-def test_schedule_tuning_keeps_results_bitwise():
-    """With MTTS_GEMM_TUNE=1 the heuristic's first eager call of a shape times the bitwise-equal schedules and
-    caches the fastest (csrc/conv_gemm.hip tune_plan); without it the heuristic runs.  Either way the first call,
-    the later calls and an explicit bitwise-equal schedule give identical outputs, the whole epilogue included."""
-    from matcha.models.components import _ops as O
-
-    B, T, K, N = 4, 333, 256, 320  # a shape no other test uses (a fresh tuning key)
-    A, Wp, Kp, C, kw, x, w = _case("lin32", B, T, K, N, True, True, True, seed=11)
-    first, _ = _run(A, Wp, Kp, C, kw, B, T, K, N, -1)
-    again, _ = _run(A, Wp, Kp, C, kw, B, T, K, N, -1)
-    ref, _ = _run(A, Wp, Kp, C, kw, B, T, K, N, 41)
-    assert torch.equal(first, again)
-    assert torch.equal(first, ref)
+        assert torch.isnan(C[..., Nn:].float()).all(), "columns past N written"
+        outs.append(C[..., :Nn].float())
+    assert torch.equal(outs[0], outs[1])
+    C = torch.empty(B, T, ld, device=DEV, dtype=dt)
+    with pytest.raises(N.NativeError):
+        O._gemm(A, T, T, B, 1, [0], K, Wp, Kp, Nn, C, T, prec=O.PREC_BF16, tile_cfg=WREG, **kw)

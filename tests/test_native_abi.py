@@ -33,6 +33,7 @@ def test_every_declared_symbol_has_a_python_signature():
     import matcha.models.components._ops  # noqa: F401  (registers the decoder entry points)
     import matcha.training  # noqa: F401  (registers the clip + AdamW entry points)
     import matcha.dp  # noqa: F401  (registers the RCCL data-parallel entry points)
+    import matcha.watchdog  # noqa: F401  (registers the device progress markers)
     import matcha.models.components.text_encoder  # noqa: F401  (registers the embedding entry points)
 
     missing = [s for s in declared_symbols() if s not in N._SIGNATURES]

@@ -222,6 +222,40 @@ def test_clip_norm_independent_of_gradient_alignment():
     assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])
 
 
+@pytest.mark.parametrize("world", [4, 8, 3])
+def test_clip_adamw_grad_scale_is_the_rank_mean(world):
+    """the data-parallel step hands the fused optimizer gradient SUMS over `world` ranks with
+    grad_scale = 1 / world (matcha/dp.py RcclComm: ncclSum, the mean folded into mtts_clip_adamw_scaled).  For a
+    power-of-two world that is bitwise the unscaled step on the mean gradients (g * 2^-k is exact); for world = 3
+    the scale rounds, and the parameters stay within 2 ulp of the step on the fp32 means.  Three steps, clipping
+    active and inactive."""
+    from matcha.training import _FlatClipAdamW
+
+    g = torch.Generator().manual_seed(13)
+    shapes = [(256, 80, 3), (17,), (1003,), (1,)]
+    init = [torch.randn(s, generator=g) for s in shapes]
+    # per-rank gradients whose fp32 sum is exact (multiples of 2^-12 well inside 24 bits)
+    ranks = [[[torch.round(torch.randn(s, generator=g) * sc * 4096) / 4096 for s in shapes] for _ in range(world)]
+             for sc in (3.0, 0.01, 0.5)]
+    runs = {}
+    for mode in ("sum_scaled", "mean"):
+        ps = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+        opt = _FlatClipAdamW(ps, torch.tensor(1e-4, device=DEV, dtype=torch.float64), 1.0)
+        for step_grads in ranks:
+            sums = [torch.stack([r[i] for r in step_grads]).sum(0) for i in range(len(shapes))]
+            for p, s in zip(ps, sums):
+                p.grad = (s if mode == "sum_scaled" else s / world).to(DEV).contiguous()
+            opt.grad_scale = 1.0 / world if mode == "sum_scaled" else 1.0
+            opt.step()
+        torch.cuda.synchronize()
+        runs[mode] = opt.flat.clone()
+    a, b = runs["sum_scaled"], runs["mean"]
+    if world & (world - 1) == 0:
+        assert torch.equal(a, b)
+    else:
+        assert ((a - b).abs() / _ulp2(b)).max().item() <= 1.0
+
+
 def _inject(m, t, z):
     m.decoder.compute_loss_and_prior = (lambda f: (lambda *a, **k: f(*a, **{**k, "t": t, "z": z})))(
         m.decoder.compute_loss_and_prior)
