@@ -1,0 +1,321 @@
+// Weight-resident bf16 implicit GEMM (round 6): the decoder's k = 1 / 2 / 3 convs and linears with K <= 768 --
+// Resnet1D's Block1D convs, the transposed conv's phases, their dgrads, the q|k|v dgrad -- behind mtts_conv_gemm
+// (include/mtts_decoder.h), schedule id MTTS_GEMM_WLDS.
+//
+// Why: the LDS-DMA kernels (conv_gemm_glds.hip) stream the packed weights through LDS again for every 64-row tile.
+// On the decoder's 256-column convs that is most of what a workgroup loads (W 256 x 768 x 2 B per tile per plane
+// against 64 x 768 x 2 B of A), and the per-CU L2 -> LDS fill (~70 GB/s, MI355X_MICROARCH.md 'gather into LDS';
+// round-5 fill probe) bounds them at 0.13 of HBM / 5 % of MFMA peak.  Here a workgroup owns 64 weight rows -- 64
+// output columns (one plane) or 32 columns x two planes (the parity policy's split weights) -- over the whole
+// reduction K <= 768: 96 KiB of LDS, loaded ONCE; it then walks its 128-row tiles and only A streams.  A k = 3 conv
+// stages each tile's input rows once (130 rows for 128 outputs) and reads them at the three tap offsets, so A is
+// not re-read per tap either.  Per 128-row tile the workgroup moves ~66 KiB (bf16 A, 256 channels) for 25 MFLOP.
+//
+// Layout: both LDS images are CHUNK-major -- 16-byte chunk c of row r at c * rows + r -- so a fragment read (16
+// lanes on 16 consecutive rows of one chunk) is bank-conflict free at any row shift, with no swizzle.  One LDS-DMA
+// wave instruction fills 64 consecutive (chunk, row) slots.  The K loop runs over 64-byte channel chunks of the
+// staged rows (32 bf16 / 16 fp32 channels: "steps"), tap-major inside a step; steps of consecutive tiles form one
+// pipeline, S stages deep, so the next tile's first chunks are in flight during a tile's epilogue.
+// Validity: a staged input row outside [0, nb * Ti) or whose 0/1 mask is 0 is DMA'd as zeros (per-tile lane bits,
+// computed for ALL of the workgroup's tiles in the prologue: no mask load inside the DMA pipeline, whose wait would
+// drain it); a tap that falls outside its utterance reads the stage's zero row instead.
+// Numerics: fp32 accumulation of bf16 products in (channel chunk, tap, 16-channel substep) order -- not bitwise the
+// LDS-DMA kernels' tap-major order; within fp32 accumulation error of them (tests/test_gemm_wlds_gpu.py).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+
+#include "conv_gemm_wreg.h"
+#include "gemm_epilogue.h"
+#include "lds_dma.h"
+#include "mtts_common.h"
+#include "mtts_decoder.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+using mtts::f32x16;
+using mtts::u32x4;
+
+constexpr int kNW = 4, kNT = 64 * kNW;  // 4 waves, each 32 output rows of the 128-row tile
+constexpr int kBM = 32 * kNW;           // rows per tile
+constexpr int kKMax = 768;              // the W image: 64 rows x K bf16, chunk-major
+constexpr int kMaxTiles = 8;            // tiles per workgroup (validity bits precomputed for all of them)
+constexpr uint32_t kOob = mtts::kDmaOob;
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
+
+// NTAP taps at stride 1: a tile's staged input rows NR = 128 + NTAP - 1, NI one-KiB DMA instructions per stage (4
+// chunk columns x NRP rows), PW of them per wave (those past NI write the junk KiB); the zero row is NRP - 1 (rows
+// past NR are DMA'd from out of range: zeros)
+template <int NTAP>
+struct WlGeom {
+    static constexpr int NR = kBM + NTAP - 1;
+    static constexpr int NRP = (NR + (NTAP > 1 ? 1 : 0) + 15) / 16 * 16;  // + a zero row when taps can fall outside
+    static constexpr int NI = 4 * NRP / 64;
+    static constexpr int PW = (NI + kNW - 1) / kNW;
+    static constexpr int STAGE = NI * 1024;
+    static_assert((4 * NRP) % 64 == 0, "whole DMA instructions per stage");
+};
+
+template <bool ABF16, int NPL, int NTAP, int S, int EK>
+__global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_args p, int ncg, int mtiles, int off_min) {
+    using G = WlGeom<NTAP>;
+    constexpr int ES = ABF16 ? 2 : 4;
+    constexpr int CPC = 64 / ES;         // channels per staged 64-byte row chunk (one pipeline step)
+    constexpr int SUB = CPC / 16;        // 16-channel MFMA substeps per step
+    constexpr int TN = NPL == 2 ? 1 : 2; // 32-column accumulator blocks per wave
+    constexpr int NRP = G::NRP, PW = G::PW, NI = G::NI;
+    __shared__ __attribute__((aligned(1024))) unsigned char sw[64 * kKMax * 2];
+    __shared__ __attribute__((aligned(1024))) unsigned char sa[S * G::STAGE];
+    __shared__ __attribute__((aligned(1024))) unsigned char sjunk[1024];
+    __shared__ __attribute__((aligned(16))) float sepi[kNW * 1024];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31, lh = lane >> 5;
+    const int M = p.nb * p.To, K = p.K, cin = p.cin;
+    const int nch = cin / CPC;  // steps per tile
+    const int nwg = gridDim.x, R = nwg / ncg;
+    const int g = mtts::xcd_relabel(blockIdx.x, nwg);
+    const int cg = g % ncg, r = g / ncg;
+    const int n0 = cg * (NPL == 2 ? 32 : 64);
+    const int ntl = r < mtiles ? (mtiles - 1 - r) / R + 1 : 0;
+    const int nsteps = ntl * nch;
+    const int arows = p.nb * p.Ti;  // Ti == To (stride 1): input row of output row m at tap offset o is m + o
+    // the bias of this lane's accumulator columns, loaded now and added to the finished accumulators (the same fp32
+    // add the epilogue does): an epilogue load would wait for -- drain -- the DMAs in flight behind it
+    float bias[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + 32 * j + lr;
+        bias[j] = p.bias && n < p.N ? p.bias[n] : 0.f;
+    }
+    mtts_conv_gemm_args pe = p;
+    pe.bias = nullptr;
+
+    // ---- per-tile staging validity (bit i * PW + k: this lane's slot of DMA instruction k of tile i), all tiles
+    // now: the mask loads are retired before the first DMA is issued
+    uint32_t vbits = 0;
+    for (int i = 0; i < ntl; ++i) {
+        const int m0 = (r + i * R) * kBM;
+#pragma unroll
+        for (int k = 0; k < PW; ++k) {
+            const int q = wave + kNW * k;
+            const int t = 64 * q + lane, row = t % NRP;
+            const int gr = m0 + off_min + row;
+            bool v = q < NI && row < G::NR && gr >= 0 && gr < arows;
+            if (v && p.a_scale) v = p.a_scale[gr] != 0.f;
+            vbits |= (uint32_t)v << (i * PW + k);
+        }
+    }
+
+    // ---- W image: chunk column c (16 bytes = 8 k) x 64 rows; row w = plane * 32 + column (two planes) or column
+    const u32x4 rsw = mtts::make_rsrc(p.W, (uint32_t)((long long)NPL * p.N * p.Kp * 2));
+    {
+        const int pl = NPL == 2 ? lane >> 5 : 0, nl = NPL == 2 ? lane & 31 : lane;
+        const int n = n0 + nl;
+        const uint32_t vw = n < p.N ? (uint32_t)(((long long)pl * p.N + n) * p.Kp * 2) : kOob;
+        const uint32_t lw = mtts::lds_addr(sw);
+        for (int q = wave; q < K / 8; q += kNW)
+            mtts::bload16(vw, rsw, (uint32_t)(q * 16), __builtin_amdgcn_readfirstlane(lw + q * 1024));
+    }
+
+    // ---- A staging: DMA instruction q of a stage covers slots 64q .. 64q + 63 = (chunk t / NRP, row t % NRP)
+    const u32x4 rsa = mtts::make_rsrc(p.A, (uint32_t)((long long)arows * p.lda * ES));
+    const uint32_t la0 = mtts::lds_addr(sa), ljunk = mtts::lds_addr(sjunk);
+    uint32_t av[PW];  // this lane's source byte offsets for the current issue tile (channel chunk 0)
+    int atile = -1;
+    auto issue = [&](int st, int stage) {
+        if (st >= nsteps) return;  // past the end: nothing (the waits below count only real issues... see loop)
+        const int ti = st / nch, ch = st - ti * nch;
+        if (ti != atile) {
+            atile = ti;
+            const int m0 = (r + ti * R) * kBM;
+#pragma unroll
+            for (int k = 0; k < PW; ++k) {
+                const int q = wave + kNW * k;
+                const int t = 64 * q + lane, c = t / NRP, row = t % NRP;
+                const bool v = (vbits >> (ti * PW + k)) & 1u;
+                av[k] = v ? (uint32_t)(((long long)(m0 + off_min + row) * p.lda + c * (16 / ES)) * ES) : kOob;
+            }
+        }
+        const uint32_t soff = (uint32_t)(ch * CPC * ES);
+#pragma unroll
+        for (int k = 0; k < PW; ++k) {
+            const int q = wave + kNW * k;
+            const uint32_t dst = q < NI ? la0 + stage * G::STAGE + q * 1024 : ljunk;
+            mtts::bload16(av[k], rsa, soff, __builtin_amdgcn_readfirstlane(dst));
+        }
+    };
+
+    // ---- per-lane fragment rows of the current compute tile: staged row of output row 32 * wave + lr at tap j,
+    // or the zero row when the tap leaves the utterance
+    int arow16[NTAP];
+    auto tile_rows = [&](int ti) {
+        const int m = (r + ti * R) * kBM + 32 * wave + lr;
+        int b = 0, u = 0;
+        mtts::divmod_fast(m < M ? m : 0, p.To, 1.0f / (float)p.To, b, u);
+#pragma unroll
+        for (int j = 0; j < NTAP; ++j) {
+            const int o = p.off[0] + j * (NTAP > 1 ? p.off[1] - p.off[0] : 0);
+            const int ui = u + o;
+            const bool v = ui >= 0 && ui < p.Ti;
+            arow16[j] = (v ? 32 * wave + lr + (o - off_min) : NRP - 1) * 16;
+        }
+    };
+
+    for (int s0 = 0; s0 < S - 1; ++s0) issue(s0, s0);
+
+    f32x16 acc[1][TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[0][j][v] = 0.f;
+
+    int cur = 0, ctile = -1;
+    for (int st = 0; st < nsteps; ++st) {
+        // steps issued so far beyond st: min(S - 2, nsteps - 1 - st); with W's loads all older than step 0's
+        if (st + S - 2 < nsteps) mtts::wait_vmcnt<PW * (S - 2)>();
+        else mtts::wait_vmcnt<0>();
+        mtts::lds_barrier();
+        issue(st + S - 1, cur == 0 ? S - 1 : cur - 1);
+        const int ti = st / nch, ch = st - ti * nch;
+        if (ti != ctile) {
+            ctile = ti;
+            tile_rows(ti);
+        }
+        const unsigned char *sb = sa + cur * G::STAGE;
+#pragma unroll
+        for (int j = 0; j < NTAP; ++j) {
+#pragma unroll
+            for (int s = 0; s < SUB; ++s) {
+                bf16x8 af;
+                if constexpr (ABF16) {
+                    af = *reinterpret_cast<const bf16x8 *>(sb + (2 * s + lh) * (NRP * 16) + arow16[j]);
+                } else {
+                    const float4 x0 = *reinterpret_cast<const float4 *>(sb + (2 * lh) * (NRP * 16) + arow16[j]);
+                    const float4 x1 = *reinterpret_cast<const float4 *>(sb + (2 * lh + 1) * (NRP * 16) + arow16[j]);
+                    af = __builtin_bit_cast(bf16x8, make_uint4(pack2(x0.x, x0.y), pack2(x0.z, x0.w), pack2(x1.x, x1.y),
+                                                               pack2(x1.z, x1.w)));
+                }
+                // W chunk column of k = j * cin + ch * CPC + 16 s + 8 lh
+                const int cw = (j * cin + ch * CPC + 16 * s) / 8 + lh;
+                const unsigned char *wb = sw + cw * 1024 + lr * 16;
+                const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(wb);
+                const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(wb + 32 * 16);
+                if constexpr (NPL == 2) {
+                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc[0][0], 0, 0, 0);
+                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc[0][0], 0, 0, 0);
+                } else {
+                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc[0][0], 0, 0, 0);
+                    acc[0][TN - 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc[0][TN - 1], 0, 0, 0);
+                }
+            }
+        }
+        if (ch == nch - 1) {
+            if (p.bias) {
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) acc[0][j][v] += bias[j];
+            }
+            mtts::gemm_epilogue_vec_v<8, 1, TN, EK, false>(pe, acc, sepi + wave * 1024, (r + ti * R) * kBM + 32 * wave, n0,
+                                                           lane);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int v = 0; v < 16; ++v) acc[0][j][v] = 0.f;
+        }
+        cur = cur == S - 1 ? 0 : cur + 1;
+    }
+    mtts::wait_vmcnt<0>();  // no DMA may still target this workgroup's LDS when it retires
+}
+
+struct WlGrid {
+    int ncg, mtiles, R;
+};
+
+WlGrid wlds_grid(const mtts_conv_gemm_args &p, int M) {
+    static const int cus = [] {
+        int dev = 0, n = 256;
+        hipDeviceProp_t pr;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0)
+            n = pr.multiProcessorCount;
+        return n;
+    }();
+    const int npl = (p.flags & MTTS_GEMM_F_W_SPLIT) ? 2 : 1;
+    WlGrid g;
+    g.ncg = (p.N + (npl == 2 ? 31 : 63)) / (npl == 2 ? 32 : 64);
+    g.mtiles = (M + kBM - 1) / kBM;
+    g.R = std::max(1, std::min(g.mtiles, cus / g.ncg));
+    // every stream's tiles must fit the precomputed validity bits
+    g.R = std::max(g.R, (g.mtiles + kMaxTiles - 1) / kMaxTiles);
+    return g;
+}
+
+template <bool ABF16, int NPL, int NTAP, int EK>
+int launch_wlds_e(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    constexpr int S = 4;
+    using G = WlGeom<NTAP>;
+    static_assert(64 * kKMax * 2 + S * G::STAGE + 1024 + kNW * 4096 <= 160 * 1024, "LDS");
+    static_assert(kMaxTiles * G::PW <= 32, "validity bits: kMaxTiles * PW <= 32");
+    const WlGrid g = wlds_grid(p, M);
+    const int o0 = p.off[0], o1 = p.off[p.ntaps - 1];
+    hipLaunchKernelGGL((conv_gemm_wlds_kernel<ABF16, NPL, NTAP, S, EK>), dim3((unsigned)(g.ncg * g.R)), dim3(kNT), 0, st, p,
+                       g.ncg, g.mtiles, std::min(o0, o1));
+    return mtts::check_launch("conv_gemm_wlds_kernel");
+}
+
+template <bool ABF16, int NPL, int NTAP>
+int launch_wlds_t(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    return mtts::gemm_epilogue_kind(p) == mtts::EK_LIN_C16 ? launch_wlds_e<ABF16, NPL, NTAP, mtts::EK_LIN_C16>(p, M, st)
+                                                            : launch_wlds_e<ABF16, NPL, NTAP, mtts::EK_LIN_C32>(p, M, st);
+}
+
+template <bool ABF16, int NPL>
+int launch_wlds_n(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    switch (p.ntaps) {
+        case 1: return launch_wlds_t<ABF16, NPL, 1>(p, M, st);
+        case 2: return launch_wlds_t<ABF16, NPL, 2>(p, M, st);
+        default: return launch_wlds_t<ABF16, NPL, 3>(p, M, st);
+    }
+}
+
+}  // namespace
+
+namespace mtts {
+
+// bf16 MFMA on one or two weight planes; 1..3 taps at stride 1 over whole utterances (Ti == To); K = taps * cin <= 768
+// with whole 64-byte channel chunks (cin % 32 bf16 / % 16 fp32); a 0/1 row mask or none; no activation / pre-activation
+// (the plain bf16 / fp32 C epilogue kinds: bias, dropout, residual, c_scale at run time); 16-byte epilogue (N % 8)
+bool conv_gemm_wlds_applies(const mtts_conv_gemm_args &p) {
+    if (p.ntaps < 1 || p.ntaps > 3 || p.in_stride != 1 || p.Ti != p.To) return false;
+    if (p.ntaps > 1 && p.off[1] - p.off[0] != 1 && p.off[1] - p.off[0] != -1) return false;
+    if (p.K != p.ntaps * p.cin || p.K > kKMax || p.K % 32) return false;
+    if (p.flags & (MTTS_GEMM_F_A_SPLIT | MTTS_GEMM_F_SPLIT3)) return false;
+    if (p.a_scale && !(p.flags & MTTS_GEMM_F_BINARY_SCALE)) return false;
+    const bool a16 = p.flags & MTTS_GEMM_F_A_BF16;
+    const int es = a16 ? 2 : 4;
+    if (p.cin % (64 / es) || p.lda % (16 / es) || (uintptr_t)p.A % 16 || (uintptr_t)p.W % 16 || p.Kp % 8) return false;
+    const int k = gemm_epilogue_kind(p);
+    if (k != EK_LIN_C16 && k != EK_LIN_C32) return false;
+    if ((long long)p.nb * p.Ti * p.lda * es >= (1ll << 31) - (1ll << 20)) return false;
+    const int npl = (p.flags & MTTS_GEMM_F_W_SPLIT) ? 2 : 1;
+    if ((long long)npl * p.N * p.Kp * 2 >= (1ll << 31) - (1ll << 20)) return false;
+    return gemm_epilogue_vec_ok(p) && gemm_epilogue_vec8_ok(p);
+}
+
+int conv_gemm_wlds_launch(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    const bool a16 = p.flags & MTTS_GEMM_F_A_BF16, w2 = p.flags & MTTS_GEMM_F_W_SPLIT;
+    if (a16) return w2 ? launch_wlds_n<true, 2>(p, M, st) : launch_wlds_n<true, 1>(p, M, st);
+    return w2 ? launch_wlds_n<false, 2>(p, M, st) : launch_wlds_n<false, 1>(p, M, st);
+}
+
+}  // namespace mtts
