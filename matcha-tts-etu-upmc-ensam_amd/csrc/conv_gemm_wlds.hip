@@ -11,11 +11,12 @@
 // stages each tile's input rows once (130 rows for 128 outputs) and reads them at the three tap offsets, so A is
 // not re-read per tap either.  Per 128-row tile the workgroup moves ~66 KiB (bf16 A, 256 channels) for 25 MFLOP.
 //
-// Layout: both LDS images are CHUNK-major -- 16-byte chunk c of row r at c * rows + r -- so a fragment read (16
-// lanes on 16 consecutive rows of one chunk) is bank-conflict free at any row shift, with no swizzle.  One LDS-DMA
-// wave instruction fills 64 consecutive (chunk, row) slots.  The K loop runs over 64-byte channel chunks of the
-// staged rows (32 bf16 / 16 fp32 channels: "steps"), tap-major inside a step; steps of consecutive tiles form one
-// pipeline, S stages deep, so the next tile's first chunks are in flight during a tile's epilogue.
+// Layout: row-major LDS images with XOR-swizzled 16-byte chunks (a_swz / w_swz), conflict-free fragment reads at any
+// row shift.  The K loop runs over 64-byte channel chunks of the staged rows (32 bf16 / 16 fp32 channels: "steps"),
+// tap-major inside a step; steps of consecutive tiles form one pipeline, S = 5 stages deep (~36 KiB in flight: an
+// LDS-DMA fill takes ~1.5 us from issue to landing, so the bytes in flight, not the instruction count, set the
+// rate), and the next tile's first chunks are in flight during a tile's epilogue.  (The first version's chunk-major
+// images -- 64 rows x 16 bytes per DMA instruction -- and 3 stages of 9 KiB ran each step at ~14 GB/s per CU.)
 // Validity: a staged input row outside [0, nb * Ti) or whose 0/1 mask is 0 is DMA'd as zeros (per-tile lane bits,
 // computed for ALL of the workgroup's tiles in the prologue: no mask load inside the DMA pipeline, whose wait would
 // drain it); a tap that falls outside its utterance reads the stage's zero row instead.
@@ -51,30 +52,46 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
 }
 
-// NTAP taps at stride 1: a tile's staged input rows NR = 128 + NTAP - 1, NI one-KiB DMA instructions per stage (4
-// chunk columns x NRP rows), PW of them per wave (those past NI write the junk KiB); the zero row is NRP - 1 (rows
-// past NR are DMA'd from out of range: zeros)
+// NTAP taps at stride 1: a tile's staged input rows NR = 128 + NTAP - 1 (+ a zero row when a tap can leave its
+// utterance), NRP rounded to 16 rows = NI one-KiB DMA instructions per stage (16 rows x 64 bytes each), wave w
+// issuing instructions w, w + 4, ... (PWV(w) of them); rows past NR are DMA'd from out of range: zeros
 template <int NTAP>
 struct WlGeom {
     static constexpr int NR = kBM + NTAP - 1;
-    static constexpr int NRP = (NR + (NTAP > 1 ? 1 : 0) + 15) / 16 * 16;  // + a zero row when taps can fall outside
-    static constexpr int NI = 4 * NRP / 64;
-    static constexpr int PW = (NI + kNW - 1) / kNW;
+    static constexpr int NRP = (NR + (NTAP > 1 ? 1 : 0) + 15) / 16 * 16;
+    static constexpr int NI = NRP / 16;
+    static constexpr int PW = (NI + kNW - 1) / kNW;  // the most any wave issues per stage
     static constexpr int STAGE = NI * 1024;
-    static_assert((4 * NRP) % 64 == 0, "whole DMA instructions per stage");
+    static constexpr int pwv(int w) { return (NI - w + kNW - 1) / kNW; }
 };
+
+// counted wait for wave w: its DMAs of the last `steps` issued pipeline steps may stay in flight
+template <int NTAP, int STEPS>
+__device__ __forceinline__ void wait_steps(int wave) {
+    using G = WlGeom<NTAP>;
+    if (wave == 0) mtts::wait_vmcnt<G::pwv(0) * STEPS>();
+    else if (wave == 1) mtts::wait_vmcnt<G::pwv(1) * STEPS>();
+    else if (wave == 2) mtts::wait_vmcnt<G::pwv(2) * STEPS>();
+    else mtts::wait_vmcnt<G::pwv(3) * STEPS>();
+}
+
+// LDS images, row-major with 16-byte chunks XOR-swizzled so that 16 lanes reading one logical chunk of 16
+// consecutive rows hit distinct banks: A rows are 64 bytes (chunk c of row r at c ^ ((r >> 2) & 3)), W rows are
+// K * 2 bytes (chunk c at c ^ (row & 15) inside its aligned group of 16).  The DMA fills 16 A rows (4 lanes per row:
+// 64 contiguous source bytes) or 1 KiB of W rows (contiguous) per wave instruction.
+__device__ __forceinline__ int a_swz(int row, int c) { return row * 64 + ((c ^ ((row >> 2) & 3)) << 4); }
+__device__ __forceinline__ int w_swz(int row, int c) { return ((c & ~15) | ((c & 15) ^ (row & 15))) << 4; }
 
 template <bool ABF16, int NPL, int NTAP, int S, int EK>
 __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_args p, int ncg, int mtiles, int off_min) {
     using G = WlGeom<NTAP>;
     constexpr int ES = ABF16 ? 2 : 4;
-    constexpr int CPC = 64 / ES;         // channels per staged 64-byte row chunk (one pipeline step)
+    constexpr int CPC = 64 / ES;         // channels per staged 64-byte row (one pipeline step)
     constexpr int SUB = CPC / 16;        // 16-channel MFMA substeps per step
     constexpr int TN = NPL == 2 ? 1 : 2; // 32-column accumulator blocks per wave
     constexpr int NRP = G::NRP, PW = G::PW, NI = G::NI;
     __shared__ __attribute__((aligned(1024))) unsigned char sw[64 * kKMax * 2];
     __shared__ __attribute__((aligned(1024))) unsigned char sa[S * G::STAGE];
-    __shared__ __attribute__((aligned(1024))) unsigned char sjunk[1024];
     __shared__ __attribute__((aligned(16))) float sepi[kNW * 1024];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -100,7 +117,7 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
     mtts_conv_gemm_args pe = p;
     pe.bias = nullptr;
 
-    // ---- per-tile staging validity (bit i * PW + k: this lane's slot of DMA instruction k of tile i), all tiles
+    // ---- per-tile staging validity (bit i * PW + k: this lane's row of DMA instruction k of tile i), all tiles
     // now: the mask loads are retired before the first DMA is issued
     uint32_t vbits = 0;
     for (int i = 0; i < ntl; ++i) {
@@ -108,7 +125,7 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
 #pragma unroll
         for (int k = 0; k < PW; ++k) {
             const int q = wave + kNW * k;
-            const int t = 64 * q + lane, row = t % NRP;
+            const int row = 16 * q + (lane >> 2);
             const int gr = m0 + off_min + row;
             bool v = q < NI && row < G::NR && gr >= 0 && gr < arows;
             if (v && p.a_scale) v = p.a_scale[gr] != 0.f;
@@ -116,24 +133,29 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
         }
     }
 
-    // ---- W image: chunk column c (16 bytes = 8 k) x 64 rows; row w = plane * 32 + column (two planes) or column
+    // ---- W image: 64 rows x K bf16, row w = plane * 32 + column (two planes) or column; instruction q fills bytes
+    // 1024 q .. of the image
     const u32x4 rsw = mtts::make_rsrc(p.W, (uint32_t)((long long)NPL * p.N * p.Kp * 2));
     {
-        const int pl = NPL == 2 ? lane >> 5 : 0, nl = NPL == 2 ? lane & 31 : lane;
-        const int n = n0 + nl;
-        const uint32_t vw = n < p.N ? (uint32_t)(((long long)pl * p.N + n) * p.Kp * 2) : kOob;
         const uint32_t lw = mtts::lds_addr(sw);
-        for (int q = wave; q < K / 8; q += kNW)
-            mtts::bload16(vw, rsw, (uint32_t)(q * 16), __builtin_amdgcn_readfirstlane(lw + q * 1024));
+        const int cpr = K / 8;  // 16-byte chunks per W row
+        for (int q = wave; q < K / 8; q += kNW) {
+            const int t = 64 * q + lane, w = t / cpr, pc = t - w * cpr;
+            const int c = (pc & ~15) | ((pc & 15) ^ (w & 15));
+            const int pl = NPL == 2 ? w >> 5 : 0, n = n0 + (NPL == 2 ? w & 31 : w);
+            const uint32_t vw = n < p.N ? (uint32_t)((((long long)pl * p.N + n) * p.Kp + c * 8) * 2) : kOob;
+            mtts::bload16(vw, rsw, 0u, __builtin_amdgcn_readfirstlane(lw + q * 1024));
+        }
     }
 
-    // ---- A staging: DMA instruction q of a stage covers slots 64q .. 64q + 63 = (chunk t / NRP, row t % NRP)
+    // ---- A staging: instruction q of a stage fills image rows 16 q .. 16 q + 15 (lane: row 16 q + lane / 4, slot
+    // lane % 4 <- logical chunk (lane % 4) ^ ((row >> 2) & 3))
     const u32x4 rsa = mtts::make_rsrc(p.A, (uint32_t)((long long)arows * p.lda * ES));
-    const uint32_t la0 = mtts::lds_addr(sa), ljunk = mtts::lds_addr(sjunk);
+    const uint32_t la0 = mtts::lds_addr(sa);
     uint32_t av[PW];  // this lane's source byte offsets for the current issue tile (channel chunk 0)
     int atile = -1;
     auto issue = [&](int st, int stage) {
-        if (st >= nsteps) return;  // past the end: nothing (the waits below count only real issues... see loop)
+        if (st >= nsteps) return;
         const int ti = st / nch, ch = st - ti * nch;
         if (ti != atile) {
             atile = ti;
@@ -141,7 +163,7 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
 #pragma unroll
             for (int k = 0; k < PW; ++k) {
                 const int q = wave + kNW * k;
-                const int t = 64 * q + lane, c = t / NRP, row = t % NRP;
+                const int row = 16 * q + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 3);
                 const bool v = (vbits >> (ti * PW + k)) & 1u;
                 av[k] = v ? (uint32_t)(((long long)(m0 + off_min + row) * p.lda + c * (16 / ES)) * ES) : kOob;
             }
@@ -150,14 +172,14 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
 #pragma unroll
         for (int k = 0; k < PW; ++k) {
             const int q = wave + kNW * k;
-            const uint32_t dst = q < NI ? la0 + stage * G::STAGE + q * 1024 : ljunk;
-            mtts::bload16(av[k], rsa, soff, __builtin_amdgcn_readfirstlane(dst));
+            if (q < NI)  // wave-uniform
+                mtts::bload16(av[k], rsa, soff, __builtin_amdgcn_readfirstlane(la0 + stage * G::STAGE + q * 1024));
         }
     };
 
-    // ---- per-lane fragment rows of the current compute tile: staged row of output row 32 * wave + lr at tap j,
-    // or the zero row when the tap leaves the utterance
-    int arow16[NTAP];
+    // ---- per-lane fragment rows of the current compute tile: image row of output row 32 * wave + lr at tap j, or
+    // the zero row when the tap leaves the utterance
+    int arow[NTAP];
     auto tile_rows = [&](int ti) {
         const int m = (r + ti * R) * kBM + 32 * wave + lr;
         int b = 0, u = 0;
@@ -167,7 +189,7 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
             const int o = p.off[0] + j * (NTAP > 1 ? p.off[1] - p.off[0] : 0);
             const int ui = u + o;
             const bool v = ui >= 0 && ui < p.Ti;
-            arow16[j] = (v ? 32 * wave + lr + (o - off_min) : NRP - 1) * 16;
+            arow[j] = v ? 32 * wave + lr + (o - off_min) : NRP - 1;
         }
     };
 
@@ -179,10 +201,11 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
 #pragma unroll
         for (int v = 0; v < 16; ++v) acc[0][j][v] = 0.f;
 
+    const int wrow0 = lr * K * 2, wrow1 = (32 + lr) * K * 2;  // this lane's two W rows (w & 15 == lr & 15)
     int cur = 0, ctile = -1;
     for (int st = 0; st < nsteps; ++st) {
-        // steps issued so far beyond st: min(S - 2, nsteps - 1 - st); with W's loads all older than step 0's
-        if (st + S - 2 < nsteps) mtts::wait_vmcnt<PW * (S - 2)>();
+        // steps issued after st: min(S - 2, nsteps - 1 - st); W's loads are all older than step 0's
+        if (st + S - 2 < nsteps) wait_steps<NTAP, S - 2>(wave);
         else mtts::wait_vmcnt<0>();
         mtts::lds_barrier();
         issue(st + S - 1, cur == 0 ? S - 1 : cur - 1);
@@ -198,18 +221,18 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
             for (int s = 0; s < SUB; ++s) {
                 bf16x8 af;
                 if constexpr (ABF16) {
-                    af = *reinterpret_cast<const bf16x8 *>(sb + (2 * s + lh) * (NRP * 16) + arow16[j]);
+                    af = *reinterpret_cast<const bf16x8 *>(sb + a_swz(arow[j], 2 * s + lh));
                 } else {
-                    const float4 x0 = *reinterpret_cast<const float4 *>(sb + (2 * lh) * (NRP * 16) + arow16[j]);
-                    const float4 x1 = *reinterpret_cast<const float4 *>(sb + (2 * lh + 1) * (NRP * 16) + arow16[j]);
+                    const float4 x0 = *reinterpret_cast<const float4 *>(sb + a_swz(arow[j], 2 * lh));
+                    const float4 x1 = *reinterpret_cast<const float4 *>(sb + a_swz(arow[j], 2 * lh + 1));
                     af = __builtin_bit_cast(bf16x8, make_uint4(pack2(x0.x, x0.y), pack2(x0.z, x0.w), pack2(x1.x, x1.y),
                                                                pack2(x1.z, x1.w)));
                 }
-                // W chunk column of k = j * cin + ch * CPC + 16 s + 8 lh
+                // W chunk of k = j * cin + ch * CPC + 16 s + 8 lh
                 const int cw = (j * cin + ch * CPC + 16 * s) / 8 + lh;
-                const unsigned char *wb = sw + cw * 1024 + lr * 16;
-                const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(wb);
-                const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(wb + 32 * 16);
+                const int so = w_swz(lr, cw);
+                const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(sw + wrow0 + so);
+                const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(sw + wrow1 + so);
                 if constexpr (NPL == 2) {
                     acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc[0][0], 0, 0, 0);
                     acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc[0][0], 0, 0, 0);
@@ -262,9 +285,9 @@ WlGrid wlds_grid(const mtts_conv_gemm_args &p, int M) {
 
 template <bool ABF16, int NPL, int NTAP, int EK>
 int launch_wlds_e(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
-    constexpr int S = 4;
+    constexpr int S = 5;
     using G = WlGeom<NTAP>;
-    static_assert(64 * kKMax * 2 + S * G::STAGE + 1024 + kNW * 4096 <= 160 * 1024, "LDS");
+    static_assert(64 * kKMax * 2 + S * G::STAGE + kNW * 4096 <= 160 * 1024, "LDS");
     static_assert(kMaxTiles * G::PW <= 32, "validity bits: kMaxTiles * PW <= 32");
     const WlGrid g = wlds_grid(p, M);
     const int o0 = p.off[0], o1 = p.off[p.ntaps - 1];
@@ -298,7 +321,7 @@ namespace mtts {
 bool conv_gemm_wlds_applies(const mtts_conv_gemm_args &p) {
     if (p.ntaps < 1 || p.ntaps > 3 || p.in_stride != 1 || p.Ti != p.To) return false;
     if (p.ntaps > 1 && p.off[1] - p.off[0] != 1 && p.off[1] - p.off[0] != -1) return false;
-    if (p.K != p.ntaps * p.cin || p.K > kKMax || p.K % 32) return false;
+    if (p.K != p.ntaps * p.cin || p.K > kKMax || p.K % 128) return false;  // (the W swizzle: 16-chunk groups)
     if (p.flags & (MTTS_GEMM_F_A_SPLIT | MTTS_GEMM_F_SPLIT3)) return false;
     if (p.a_scale && !(p.flags & MTTS_GEMM_F_BINARY_SCALE)) return false;
     const bool a16 = p.flags & MTTS_GEMM_F_A_BF16;

@@ -36,7 +36,7 @@ def _weights(N, K, split, g):
     (2, 300, 256, 512, [1, 0, -1], True, False, False, 1),    # N = 512 dgrad
     (3, 300, 256, 256, [0, -1], False, True, True, 2),        # ConvTranspose phase: 2 taps, strided output
     (2, 77, 768, 256, [0], True, False, False, 1),            # q|k|v dgrad (one tap, K = 768)
-    (1, 4800, 128, 192, [-1, 0, 1], False, False, True, 1),   # K = 384, one long utterance
+    (1, 4800, 256, 192, [-1, 0, 1], False, False, True, 1),   # one long utterance, N = 192
 ])
 def test_wlds_vs_float64_and_lds_dma(kind, B, T, cin, N, taps, a16, split, masked, ostride):
     from matcha.models.components import _ops as O
@@ -65,7 +65,8 @@ def test_wlds_vs_float64_and_lds_dma(kind, B, T, cin, N, taps, a16, split, maske
                 prec=O.PREC_BF16, tile_cfg=cfg, **kw)
         torch.cuda.synchronize()
         outs.append(C.float())
-    assert torch.equal(outs[0], outs[1], equal_nan=True)  # deterministic
+    nan = torch.isnan(outs[0])
+    assert torch.equal(nan, torch.isnan(outs[1])) and torch.equal(outs[0][~nan], outs[1][~nan])  # deterministic
     # float64 reference: implicit GEMM over the taps with per-utterance zero padding and the row mask on A
     xm = x.double() * msk.double().view(B, T, 1)
     ref = torch.zeros(B, T, N, dtype=torch.float64)
