@@ -114,8 +114,16 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
         const int n = n0 + 32 * j + lr;
         bias[j] = p.bias && n < p.N ? p.bias[n] : 0.f;
     }
+    // the epilogue's arguments with every stream it could load made compile-time absent (conv_gemm_wlds_applies
+    // refuses them): no load, and no wait for one, can sit in the tile loop
     mtts_conv_gemm_args pe = p;
     pe.bias = nullptr;
+    pe.residual = nullptr;
+    pe.c_scale = nullptr;
+    pe.aux = nullptr;
+    pe.C_pre = nullptr;
+    pe.seed = nullptr;
+    pe.dropout_p = 0.f;
 
     // ---- per-tile staging validity (bit i * PW + k: this lane's row of DMA instruction k of tile i), all tiles
     // now: the mask loads are retired before the first DMA is issued
@@ -132,6 +140,9 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
             vbits |= (uint32_t)v << (i * PW + k);
         }
     }
+    // retire the bias / mask loads here: left pending, the compiler's wait before their first use (the first
+    // tile's epilogue) is a vmcnt(0) that would also drain the DMAs in flight by then
+    mtts::wait_vmcnt<0>();
 
     // ---- W image: 64 rows x K bf16, row w = plane * 32 + column (two planes) or column; instruction q fills bytes
     // 1024 q .. of the image
@@ -195,68 +206,63 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
 
     for (int s0 = 0; s0 < S - 1; ++s0) issue(s0, s0);
 
-    f32x16 acc[1][TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) acc[0][j][v] = 0.f;
-
     const int wrow0 = lr * K * 2, wrow1 = (32 + lr) * K * 2;  // this lane's two W rows (w & 15 == lr & 15)
-    int cur = 0, ctile = -1;
-    for (int st = 0; st < nsteps; ++st) {
-        // steps issued after st: min(S - 2, nsteps - 1 - st); W's loads are all older than step 0's
-        if (st + S - 2 < nsteps) wait_steps<NTAP, S - 2>(wave);
-        else mtts::wait_vmcnt<0>();
-        mtts::lds_barrier();
-        issue(st + S - 1, cur == 0 ? S - 1 : cur - 1);
-        const int ti = st / nch, ch = st - ti * nch;
-        if (ti != ctile) {
-            ctile = ti;
-            tile_rows(ti);
-        }
-        const unsigned char *sb = sa + cur * G::STAGE;
+    int cur = 0, st = 0;
+    for (int ti = 0; ti < ntl; ++ti) {
+        tile_rows(ti);
+        // the tile's accumulators live only inside its chunk loop (loop-carried across tiles, the register
+        // allocator copied them out of the AGPRs at every step, behind a vmcnt(0) that drained the DMAs in flight)
+        f32x16 acc[1][TN];
 #pragma unroll
-        for (int j = 0; j < NTAP; ++j) {
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int s = 0; s < SUB; ++s) {
-                bf16x8 af;
-                if constexpr (ABF16) {
-                    af = *reinterpret_cast<const bf16x8 *>(sb + a_swz(arow[j], 2 * s + lh));
-                } else {
-                    const float4 x0 = *reinterpret_cast<const float4 *>(sb + a_swz(arow[j], 2 * lh));
-                    const float4 x1 = *reinterpret_cast<const float4 *>(sb + a_swz(arow[j], 2 * lh + 1));
-                    af = __builtin_bit_cast(bf16x8, make_uint4(pack2(x0.x, x0.y), pack2(x0.z, x0.w), pack2(x1.x, x1.y),
-                                                               pack2(x1.z, x1.w)));
-                }
-                // W chunk of k = j * cin + ch * CPC + 16 s + 8 lh
-                const int cw = (j * cin + ch * CPC + 16 * s) / 8 + lh;
-                const int so = w_swz(lr, cw);
-                const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(sw + wrow0 + so);
-                const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(sw + wrow1 + so);
-                if constexpr (NPL == 2) {
-                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc[0][0], 0, 0, 0);
-                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc[0][0], 0, 0, 0);
-                } else {
-                    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc[0][0], 0, 0, 0);
-                    acc[0][TN - 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc[0][TN - 1], 0, 0, 0);
+            for (int v = 0; v < 16; ++v) acc[0][j][v] = 0.f;
+        for (int ch = 0; ch < nch; ++ch, ++st) {
+            // steps issued after st: min(S - 2, nsteps - 1 - st); W's loads are all older than step 0's
+            if (st + S - 2 < nsteps) wait_steps<NTAP, S - 2>(wave);
+            else mtts::wait_vmcnt<0>();
+            mtts::lds_barrier();
+            issue(st + S - 1, cur == 0 ? S - 1 : cur - 1);
+            const unsigned char *sb = sa + cur * G::STAGE;
+#pragma unroll
+            for (int j = 0; j < NTAP; ++j) {
+#pragma unroll
+                for (int s = 0; s < SUB; ++s) {
+                    bf16x8 af;
+                    if constexpr (ABF16) {
+                        af = *reinterpret_cast<const bf16x8 *>(sb + a_swz(arow[j], 2 * s + lh));
+                    } else {
+                        const float4 x0 = *reinterpret_cast<const float4 *>(sb + a_swz(arow[j], 2 * lh));
+                        const float4 x1 = *reinterpret_cast<const float4 *>(sb + a_swz(arow[j], 2 * lh + 1));
+                        af = __builtin_bit_cast(bf16x8, make_uint4(pack2(x0.x, x0.y), pack2(x0.z, x0.w),
+                                                                   pack2(x1.x, x1.y), pack2(x1.z, x1.w)));
+                    }
+                    // W chunk of k = j * cin + ch * CPC + 16 s + 8 lh
+                    const int cw = (j * cin + ch * CPC + 16 * s) / 8 + lh;
+                    const int so = w_swz(lr, cw);
+                    const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(sw + wrow0 + so);
+                    const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(sw + wrow1 + so);
+                    if constexpr (NPL == 2) {
+                        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc[0][0], 0, 0, 0);
+                        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc[0][0], 0, 0, 0);
+                    } else {
+                        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc[0][0], 0, 0, 0);
+                        acc[0][TN - 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc[0][TN - 1], 0, 0, 0);
+                    }
                 }
             }
+            cur = cur == S - 1 ? 0 : cur + 1;
         }
-        if (ch == nch - 1) {
-            if (p.bias) {
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int v = 0; v < 16; ++v) acc[0][j][v] += bias[j];
-            }
-            mtts::gemm_epilogue_vec_v<8, 1, TN, EK, false>(pe, acc, sepi + wave * 1024, (r + ti * R) * kBM + 32 * wave, n0,
-                                                           lane);
+        if (p.bias) {
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
-                for (int v = 0; v < 16; ++v) acc[0][j][v] = 0.f;
+                for (int v = 0; v < 16; ++v) acc[0][j][v] += bias[j];
         }
-        cur = cur == S - 1 ? 0 : cur + 1;
+        // (no global load in this epilogue -- conv_gemm_wlds_applies refuses residual / c_scale / dropout: its
+        // wait would drain the DMAs in flight)
+        mtts::gemm_epilogue_vec_v<8, 1, TN, EK, false>(pe, acc, sepi + wave * 1024, (r + ti * R) * kBM + 32 * wave, n0,
+                                                       lane);
     }
     mtts::wait_vmcnt<0>();  // no DMA may still target this workgroup's LDS when it retires
 }
@@ -317,7 +323,7 @@ namespace mtts {
 
 // bf16 MFMA on one or two weight planes; 1..3 taps at stride 1 over whole utterances (Ti == To); K = taps * cin <= 768
 // with whole 64-byte channel chunks (cin % 32 bf16 / % 16 fp32); a 0/1 row mask or none; no activation / pre-activation
-// (the plain bf16 / fp32 C epilogue kinds: bias, dropout, residual, c_scale at run time); 16-byte epilogue (N % 8)
+// (the plain bf16 / fp32 C epilogue kinds, with a bias at most: no residual / c_scale / dropout); 16-byte epilogue
 bool conv_gemm_wlds_applies(const mtts_conv_gemm_args &p) {
     if (p.ntaps < 1 || p.ntaps > 3 || p.in_stride != 1 || p.Ti != p.To) return false;
     if (p.ntaps > 1 && p.off[1] - p.off[0] != 1 && p.off[1] - p.off[0] != -1) return false;
@@ -329,6 +335,8 @@ bool conv_gemm_wlds_applies(const mtts_conv_gemm_args &p) {
     if (p.cin % (64 / es) || p.lda % (16 / es) || (uintptr_t)p.A % 16 || (uintptr_t)p.W % 16 || p.Kp % 8) return false;
     const int k = gemm_epilogue_kind(p);
     if (k != EK_LIN_C16 && k != EK_LIN_C32) return false;
+    // no epilogue stream but the output: a global load inside the DMA pipeline waits for (drains) every DMA in flight
+    if (p.residual || p.c_scale || p.dropout_p > 0.f) return false;
     if ((long long)p.nb * p.Ti * p.lda * es >= (1ll << 31) - (1ll << 20)) return false;
     const int npl = (p.flags & MTTS_GEMM_F_W_SPLIT) ? 2 : 1;
     if ((long long)npl * p.N * p.Kp * 2 >= (1ll << 31) - (1ll << 20)) return false;

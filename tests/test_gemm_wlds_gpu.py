@@ -28,7 +28,7 @@ def _weights(N, K, split, g):
     return Wp, Kp, w.bfloat16().float()
 
 
-@pytest.mark.parametrize("kind", ["c16", "c32_bias_res", "c32_cscale"])
+@pytest.mark.parametrize("kind", ["c16", "c16_bias", "c32_bias"])
 @pytest.mark.parametrize("B,T,cin,N,taps,a16,split,masked,ostride", [
     (3, 301, 256, 256, [-1, 0, 1], True, True, True, 1),      # Block1D conv, split planes, ragged rows + mask
     (2, 600, 256, 256, [1, 0, -1], True, False, False, 1),    # its dgrad (descending taps)
@@ -49,14 +49,10 @@ def test_wlds_vs_float64_and_lds_dma(kind, B, T, cin, N, taps, a16, split, maske
     msk = (torch.rand(B * T, generator=g) > 0.25).float() if masked else torch.ones(B * T)
     if masked:
         kw["a_scale"] = msk.to(DEV)
-    c16 = kind == "c16"
+    c16 = kind.startswith("c16")
     To_full = T * ostride
-    if kind == "c32_bias_res":
+    if kind.endswith("bias"):
         kw["bias"] = torch.randn(N, generator=g).to(DEV)
-        kw["residual"] = torch.randn(B, To_full, N, generator=g).to(DEV)
-    if kind == "c32_cscale":
-        kw["bias"] = torch.randn(N, generator=g).to(DEV)
-        kw["c_scale"] = (torch.rand(B * To_full, generator=g) > 0.2).float().to(DEV)
     A = x.to(DEV).bfloat16() if a16 else x.to(DEV)
     outs = []
     for cfg in (WLDS, WLDS, 41):
@@ -78,12 +74,8 @@ def test_wlds_vs_float64_and_lds_dma(kind, B, T, cin, N, taps, a16, split, maske
         ref += src @ wr[:, j].T
     full = torch.full((B, To_full, N), float("nan"), dtype=torch.float64)
     rows = slice(ostride - 1, None, ostride)
-    if kind in ("c32_bias_res", "c32_cscale"):
+    if kind.endswith("bias"):
         ref += kw["bias"].double().cpu()
-    if kind == "c32_bias_res":
-        ref += kw["residual"].double().cpu()[:, rows]
-    if kind == "c32_cscale":
-        ref *= kw["c_scale"].double().cpu().view(B, To_full, 1)[:, rows]
     full[:, rows] = ref
     got = outs[0].double().cpu()
     assert torch.equal(torch.isnan(got), torch.isnan(full))  # every output row written, nothing else
@@ -95,8 +87,8 @@ def test_wlds_vs_float64_and_lds_dma(kind, B, T, cin, N, taps, a16, split, maske
 
 
 def test_wlds_refuses_unsupported_shapes():
-    """No silent fallback: an explicit request for a shape the kernel does not cover (K > 768, a GELU epilogue,
-    stride 2) fails loudly; the heuristic keeps the other schedules there."""
+    """No silent fallback: an explicit request for a shape the kernel does not cover (K > 768, an activation, a
+    residual / row-scale epilogue stream, stride 2) fails loudly; the heuristic keeps the other schedules there."""
     from matcha import _native as N
     from matcha.models.components import _ops as O
 
@@ -109,6 +101,12 @@ def test_wlds_refuses_unsupported_shapes():
     Wp, Kp = O.pack_weight(torch.randn(128, 256, device=DEV), O.PREC_BF16)
     with pytest.raises(N.NativeError):
         O._gemm(x, 50, 50, 2, 1, [0], 256, Wp, Kp, 128, y, 50, prec=O.PREC_BF16, tile_cfg=WLDS, act=O.ACT_RELU)
+    with pytest.raises(N.NativeError):
+        O._gemm(x, 50, 50, 2, 1, [0], 256, Wp, Kp, 128, y, 50, prec=O.PREC_BF16, tile_cfg=WLDS,
+                residual=torch.randn(2, 50, 128, device=DEV))
+    with pytest.raises(N.NativeError):
+        O._gemm(x, 50, 50, 2, 1, [0], 256, Wp, Kp, 128, y, 50, prec=O.PREC_BF16, tile_cfg=WLDS,
+                c_scale=torch.ones(100, device=DEV))
     x2 = torch.randn(2, 100, 256, device=DEV)  # the stride-2 Downsample conv
     Wp3, Kp3 = O.pack_weight(torch.randn(128, 3 * 256, device=DEV), O.PREC_BF16)
     with pytest.raises(N.NativeError):
