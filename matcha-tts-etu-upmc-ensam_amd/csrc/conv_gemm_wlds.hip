@@ -224,30 +224,40 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
             mtts::lds_barrier();
             issue(st + S - 1, cur == 0 ? S - 1 : cur - 1);
             const unsigned char *sb = sa + cur * G::STAGE;
+            // every fragment of the step is read first, then the MFMAs run back to back: with one wave per SIMD
+            // nothing else hides an LDS read, and read-MFMA pairs exposed its latency at every MFMA
+            bf16x8 af[NTAP][SUB], bw[NTAP][SUB][2];
 #pragma unroll
             for (int j = 0; j < NTAP; ++j) {
 #pragma unroll
                 for (int s = 0; s < SUB; ++s) {
-                    bf16x8 af;
                     if constexpr (ABF16) {
-                        af = *reinterpret_cast<const bf16x8 *>(sb + a_swz(arow[j], 2 * s + lh));
+                        af[j][s] = *reinterpret_cast<const bf16x8 *>(sb + a_swz(arow[j], 2 * s + lh));
                     } else {
                         const float4 x0 = *reinterpret_cast<const float4 *>(sb + a_swz(arow[j], 2 * lh));
                         const float4 x1 = *reinterpret_cast<const float4 *>(sb + a_swz(arow[j], 2 * lh + 1));
-                        af = __builtin_bit_cast(bf16x8, make_uint4(pack2(x0.x, x0.y), pack2(x0.z, x0.w),
-                                                                   pack2(x1.x, x1.y), pack2(x1.z, x1.w)));
+                        af[j][s] = __builtin_bit_cast(bf16x8, make_uint4(pack2(x0.x, x0.y), pack2(x0.z, x0.w),
+                                                                         pack2(x1.x, x1.y), pack2(x1.z, x1.w)));
                     }
                     // W chunk of k = j * cin + ch * CPC + 16 s + 8 lh
                     const int cw = (j * cin + ch * CPC + 16 * s) / 8 + lh;
                     const int so = w_swz(lr, cw);
-                    const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(sw + wrow0 + so);
-                    const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(sw + wrow1 + so);
+                    bw[j][s][0] = *reinterpret_cast<const bf16x8 *>(sw + wrow0 + so);
+                    bw[j][s][1] = *reinterpret_cast<const bf16x8 *>(sw + wrow1 + so);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < NTAP; ++j) {
+#pragma unroll
+                for (int s = 0; s < SUB; ++s) {
                     if constexpr (NPL == 2) {
-                        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc[0][0], 0, 0, 0);
-                        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc[0][0], 0, 0, 0);
+                        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[j][s], bw[j][s][0], acc[0][0], 0, 0, 0);
+                        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[j][s], bw[j][s][1], acc[0][0], 0, 0, 0);
                     } else {
-                        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc[0][0], 0, 0, 0);
-                        acc[0][TN - 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc[0][TN - 1], 0, 0, 0);
+                        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[j][s], bw[j][s][0], acc[0][0], 0, 0, 0);
+                        acc[0][TN - 1] =
+                            __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[j][s], bw[j][s][1], acc[0][TN - 1], 0, 0, 0);
                     }
                 }
             }
