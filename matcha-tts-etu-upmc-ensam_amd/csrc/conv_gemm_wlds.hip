@@ -83,7 +83,7 @@ __device__ __forceinline__ int a_swz(int row, int c) { return row * 64 + ((c ^ (
 __device__ __forceinline__ int w_swz(int row, int c) { return ((c & ~15) | ((c & 15) ^ (row & 15))) << 4; }
 
 template <bool ABF16, int NPL, int NTAP, int S, int EK>
-__global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_args p, int ncg, int mtiles, int off_min) {
+__global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_args p, int ncg, int mtiles, int off_min, int dbg) {
     using G = WlGeom<NTAP>;
     constexpr int ES = ABF16 ? 2 : 4;
     constexpr int CPC = 64 / ES;         // channels per staged 64-byte row (one pipeline step)
@@ -180,6 +180,7 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
             }
         }
         const uint32_t soff = (uint32_t)(ch * CPC * ES);
+        if (dbg & 2) return;  // diagnostic: no A staging
 #pragma unroll
         for (int k = 0; k < PW; ++k) {
             const int q = wave + kNW * k;
@@ -247,6 +248,12 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
+            if (dbg & 1) {  // diagnostic: reads, no MFMAs (keep the reads alive)
+#pragma unroll
+                for (int j = 0; j < NTAP; ++j)
+#pragma unroll
+                    for (int s = 0; s < SUB; ++s) acc[0][0][0] += (float)af[j][s][0] + (float)bw[j][s][0][1] + (float)bw[j][s][1][2];
+            } else
 #pragma unroll
             for (int j = 0; j < NTAP; ++j) {
 #pragma unroll
@@ -307,8 +314,10 @@ int launch_wlds_e(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
     static_assert(kMaxTiles * G::PW <= 32, "validity bits: kMaxTiles * PW <= 32");
     const WlGrid g = wlds_grid(p, M);
     const int o0 = p.off[0], o1 = p.off[p.ntaps - 1];
+    // MTTS_WLDS_DBG (diagnostics only): bit 0 = no MFMAs, bit 1 = no A staging
+    static const int dbg = [] { const char *e = getenv("MTTS_WLDS_DBG"); return e ? atoi(e) : 0; }();
     hipLaunchKernelGGL((conv_gemm_wlds_kernel<ABF16, NPL, NTAP, S, EK>), dim3((unsigned)(g.ncg * g.R)), dim3(kNT), 0, st, p,
-                       g.ncg, g.mtiles, std::min(o0, o1));
+                       g.ncg, g.mtiles, std::min(o0, o1), dbg);
     return mtts::check_launch("conv_gemm_wlds_kernel");
 }
 
