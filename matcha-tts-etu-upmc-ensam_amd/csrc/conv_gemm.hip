@@ -1260,8 +1260,8 @@ static int resolve_cfg(const mtts_conv_gemm_args &p, bool bf16, int cfg, int M, 
     static const bool wreg_pick = [] { const char *e = getenv("MTTS_GEMM_WREG_PICK"); return !(e && e[0] == '0'); }();
     if (cfg < 0 && bf16 && wreg_pick && mtts::conv_gemm_wreg_applies(p) && mtts::conv_gemm_wreg_preferred(p, M))
         return MTTS_GEMM_WREG;
-    // the weight-resident kernel (W in LDS, loaded once per workgroup): the decoder's k <= 3 convs and linears with
-    // K <= 768 (csrc/conv_gemm_wlds.hip); MTTS_GEMM_WLDS_PICK=1 turns the heuristic's pick on
+    // the weight-resident kernel (W in LDS, loaded once per workgroup; A straight to registers): the decoder's k <= 3
+    // convs and linears with K <= 768 (csrc/conv_gemm_wlds.hip); MTTS_GEMM_WLDS_PICK=1 turns the heuristic's pick on
     static const bool wlds_pick = [] { const char *e = getenv("MTTS_GEMM_WLDS_PICK"); return e && e[0] == '1'; }();
     if (cfg < 0 && bf16 && wlds_pick && M >= 4096 && mtts::conv_gemm_wlds_applies(p)) return MTTS_GEMM_WLDS;
     static const bool ws_pick = [] { const char *e = getenv("MTTS_GEMM_WS_PICK"); return !(e && e[0] == '0'); }();

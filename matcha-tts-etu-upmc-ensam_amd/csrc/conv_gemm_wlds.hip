@@ -5,23 +5,20 @@
 // Why: the LDS-DMA kernels (conv_gemm_glds.hip) stream the packed weights through LDS again for every 64-row tile.
 // On the decoder's 256-column convs that is most of what a workgroup loads (W 256 x 768 x 2 B per tile per plane
 // against 64 x 768 x 2 B of A), and the per-CU L2 -> LDS fill (~70 GB/s, MI355X_MICROARCH.md 'gather into LDS';
-// round-5 fill probe) bounds them at 0.13 of HBM / 5 % of MFMA peak.  Here a workgroup owns 64 weight rows -- 64
-// output columns (one plane) or 32 columns x two planes (the parity policy's split weights) -- over the whole
-// reduction K <= 768: 96 KiB of LDS, loaded ONCE; it then walks its 128-row tiles and only A streams.  A k = 3 conv
-// stages each tile's input rows once (130 rows for 128 outputs) and reads them at the three tap offsets, so A is
-// not re-read per tap either.  Per 128-row tile the workgroup moves ~66 KiB (bf16 A, 256 channels) for 25 MFLOP.
+// round-5 fill probe) bounds them.  Here a workgroup owns 64 weight rows -- 64 output columns (one plane) or 32
+// columns x two planes (the parity policy's split weights) -- over the whole reduction K <= 768: 96 KiB of LDS,
+// loaded ONCE.  Its four waves then walk their own blocks of 32 * TM rows independently (no barrier after the W
+// load): A goes straight to registers through a compiler-tracked prefetch ring PD substeps deep (a k = 3 conv reads
+// each 16-channel chunk at the three tap offsets back to back, so the shifted rows come from L1), W fragments come
+// from LDS, and the next block's first loads are issued during the current block's tail.
 //
-// Layout: row-major LDS images with XOR-swizzled 16-byte chunks (a_swz / w_swz), conflict-free fragment reads at any
-// row shift.  The K loop runs over 64-byte channel chunks of the staged rows (32 bf16 / 16 fp32 channels: "steps"),
-// tap-major inside a step; steps of consecutive tiles form one pipeline, S = 5 stages deep (~36 KiB in flight: an
-// LDS-DMA fill takes ~1.5 us from issue to landing, so the bytes in flight, not the instruction count, set the
-// rate), and the next tile's first chunks are in flight during a tile's epilogue.  (The first version's chunk-major
-// images -- 64 rows x 16 bytes per DMA instruction -- and 3 stages of 9 KiB ran each step at ~14 GB/s per CU.)
-// Validity: a staged input row outside [0, nb * Ti) or whose 0/1 mask is 0 is DMA'd as zeros (per-tile lane bits,
-// computed for ALL of the workgroup's tiles in the prologue: no mask load inside the DMA pipeline, whose wait would
-// drain it); a tap that falls outside its utterance reads the stage's zero row instead.
-// Numerics: fp32 accumulation of bf16 products in (channel chunk, tap, 16-channel substep) order -- not bitwise the
-// LDS-DMA kernels' tap-major order; within fp32 accumulation error of them (tests/test_gemm_wlds_gpu.py).
+// History (round 6, tools/r6/gpu_wlds*.sh): a first version staged A through an LDS-DMA ring shared by the four
+// waves; the W image leaves only ~50 KiB of LDS for that ring, each step was barrier- and latency-bound at ~0.5-1 us
+// whatever it carried (diagnostic switches: 24.8 of 29.7 us without MFMAs and without A staging), and it ran 20-90 %
+// slower than the LDS-DMA kernels on every step shape.
+//
+// Numerics: fp32 accumulation of bf16 products in (16-channel chunk, tap) order -- not bitwise the LDS-DMA kernels'
+// tap-major order; within fp32 accumulation error of them (tests/test_gemm_wlds_gpu.py).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -42,253 +39,209 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 using mtts::f32x16;
 using mtts::u32x4;
 
-constexpr int kNW = 4, kNT = 64 * kNW;  // 4 waves, each 32 output rows of the 128-row tile
-constexpr int kBM = 32 * kNW;           // rows per tile
-constexpr int kKMax = 768;              // the W image: 64 rows x K bf16, chunk-major
-constexpr int kMaxTiles = 8;            // tiles per workgroup (validity bits precomputed for all of them)
+constexpr int kNW = 4, kNT = 64 * kNW;
+constexpr int kKMax = 768;  // the W image: 64 rows x K bf16
 constexpr uint32_t kOob = mtts::kDmaOob;
+
+__device__ float g_wl_zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // never written: invalid tap rows
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
 }
 
-// NTAP taps at stride 1: a tile's staged input rows NR = 128 + NTAP - 1 (+ a zero row when a tap can leave its
-// utterance), NRP rounded to 16 rows = NI one-KiB DMA instructions per stage (16 rows x 64 bytes each), wave w
-// issuing instructions w, w + 4, ... (PWV(w) of them); rows past NR are DMA'd from out of range: zeros
-template <int NTAP>
-struct WlGeom {
-    static constexpr int NR = kBM + NTAP - 1;
-    static constexpr int NRP = (NR + (NTAP > 1 ? 1 : 0) + 15) / 16 * 16;
-    static constexpr int NI = NRP / 16;
-    static constexpr int PW = (NI + kNW - 1) / kNW;  // the most any wave issues per stage
-    static constexpr int STAGE = NI * 1024;
-    static constexpr int pwv(int w) { return (NI - w + kNW - 1) / kNW; }
-};
-
-// counted wait for wave w: its DMAs of the last `steps` issued pipeline steps may stay in flight
-template <int NTAP, int STEPS>
-__device__ __forceinline__ void wait_steps(int wave) {
-    using G = WlGeom<NTAP>;
-    if (wave == 0) mtts::wait_vmcnt<G::pwv(0) * STEPS>();
-    else if (wave == 1) mtts::wait_vmcnt<G::pwv(1) * STEPS>();
-    else if (wave == 2) mtts::wait_vmcnt<G::pwv(2) * STEPS>();
-    else mtts::wait_vmcnt<G::pwv(3) * STEPS>();
-}
-
-// LDS images, row-major with 16-byte chunks XOR-swizzled so that 16 lanes reading one logical chunk of 16
-// consecutive rows hit distinct banks: A rows are 64 bytes (chunk c of row r at c ^ ((r >> 2) & 3)), W rows are
-// K * 2 bytes (chunk c at c ^ (row & 15) inside its aligned group of 16).  The DMA fills 16 A rows (4 lanes per row:
-// 64 contiguous source bytes) or 1 KiB of W rows (contiguous) per wave instruction.
-__device__ __forceinline__ int a_swz(int row, int c) { return row * 64 + ((c ^ ((row >> 2) & 3)) << 4); }
+// W image row-major, 16-byte chunk c of row w at ((c & ~15) | ((c & 15) ^ (w & 15))): 16 lanes reading one logical
+// chunk of 16 consecutive rows hit distinct banks
 __device__ __forceinline__ int w_swz(int row, int c) { return ((c & ~15) | ((c & 15) ^ (row & 15))) << 4; }
 
-template <bool ABF16, int NPL, int NTAP, int S, int EK>
-__global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_args p, int ncg, int mtiles, int off_min, int dbg) {
-    using G = WlGeom<NTAP>;
+// One A fragment slot of the prefetch ring: TM row blocks x (bf16: 8 values in one uint4 | fp32: 8 values in two)
+template <bool ABF16, int TM>
+struct AFrag {
+    uint4 v[TM][ABF16 ? 1 : 2];
+};
+
+// ABF16: A storage; NPL: weight planes; NTAP taps (stride 1); KS = K / 16 substeps; TM: 32-row blocks per wave block;
+// PD: prefetch distance in substeps (PD + 1 divides KS: ring slots are compile-time per substep in every block)
+template <bool ABF16, int NPL, int NTAP, int KS, int TM, int PD, int EK>
+__global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_args p, int ncg, int nblk) {
+    static_assert(KS % (PD + 1) == 0, "ring slots repeat every block");
     constexpr int ES = ABF16 ? 2 : 4;
-    constexpr int CPC = 64 / ES;         // channels per staged 64-byte row (one pipeline step)
-    constexpr int SUB = CPC / 16;        // 16-channel MFMA substeps per step
-    constexpr int TN = NPL == 2 ? 1 : 2; // 32-column accumulator blocks per wave
-    constexpr int NRP = G::NRP, PW = G::PW, NI = G::NI;
-    __shared__ __attribute__((aligned(1024))) unsigned char sw[64 * kKMax * 2];
-    __shared__ __attribute__((aligned(1024))) unsigned char sa[S * G::STAGE];
+    constexpr int K = 16 * KS, CIN = K / NTAP, NC = CIN / 16;  // NC 16-channel chunks per tap
+    constexpr int TN = NPL == 2 ? 1 : 2;                       // 32-column accumulator blocks per wave
+    constexpr int BMW = 32 * TM;                                // rows per wave block
+    constexpr int NS = PD + 1;
+    static_assert(CIN % 16 == 0 && K <= kKMax, "shape");
+    __shared__ __attribute__((aligned(1024))) unsigned char sw[64 * K * 2];
     __shared__ __attribute__((aligned(16))) float sepi[kNW * 1024];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lr = lane & 31, lh = lane >> 5;
-    const int M = p.nb * p.To, K = p.K, cin = p.cin;
-    const int nch = cin / CPC;  // steps per tile
+    const int M = p.nb * p.To;
     const int nwg = gridDim.x, R = nwg / ncg;
     const int g = mtts::xcd_relabel(blockIdx.x, nwg);
     const int cg = g % ncg, r = g / ncg;
     const int n0 = cg * (NPL == 2 ? 32 : 64);
-    const int ntl = r < mtiles ? (mtiles - 1 - r) / R + 1 : 0;
-    const int nsteps = ntl * nch;
-    const int arows = p.nb * p.Ti;  // Ti == To (stride 1): input row of output row m at tap offset o is m + o
-    // the bias of this lane's accumulator columns, loaded now and added to the finished accumulators (the same fp32
-    // add the epilogue does): an epilogue load would wait for -- drain -- the DMAs in flight behind it
-    float bias[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int n = n0 + 32 * j + lr;
-        bias[j] = p.bias && n < p.N ? p.bias[n] : 0.f;
-    }
-    // the epilogue's arguments with every stream it could load made compile-time absent (conv_gemm_wlds_applies
-    // refuses them): no load, and no wait for one, can sit in the tile loop
-    mtts_conv_gemm_args pe = p;
-    pe.bias = nullptr;
-    pe.residual = nullptr;
-    pe.c_scale = nullptr;
-    pe.aux = nullptr;
-    pe.C_pre = nullptr;
-    pe.seed = nullptr;
-    pe.dropout_p = 0.f;
+    const int dstep = NTAP > 1 ? p.off[1] - p.off[0] : 0;
+    const float inv_to = 1.0f / (float)p.To;
 
-    // ---- per-tile staging validity (bit i * PW + k: this lane's row of DMA instruction k of tile i), all tiles
-    // now: the mask loads are retired before the first DMA is issued
-    uint32_t vbits = 0;
-    for (int i = 0; i < ntl; ++i) {
-        const int m0 = (r + i * R) * kBM;
-#pragma unroll
-        for (int k = 0; k < PW; ++k) {
-            const int q = wave + kNW * k;
-            const int row = 16 * q + (lane >> 2);
-            const int gr = m0 + off_min + row;
-            bool v = q < NI && row < G::NR && gr >= 0 && gr < arows;
-            if (v && p.a_scale) v = p.a_scale[gr] != 0.f;
-            vbits |= (uint32_t)v << (i * PW + k);
-        }
-    }
-    // retire the bias / mask loads here: left pending, the compiler's wait before their first use (the first
-    // tile's epilogue) is a vmcnt(0) that would also drain the DMAs in flight by then
-    mtts::wait_vmcnt<0>();
-
-    // ---- W image: 64 rows x K bf16, row w = plane * 32 + column (two planes) or column; instruction q fills bytes
-    // 1024 q .. of the image
-    const u32x4 rsw = mtts::make_rsrc(p.W, (uint32_t)((long long)NPL * p.N * p.Kp * 2));
+    // ---- W image by LDS-DMA (64 rows x K; row w = plane * 32 + column, or column), then the bias of this lane's
+    // accumulator columns (added to the finished accumulators: the epilogue's own bias load would wait, in order,
+    // for every prefetch load issued before it)
     {
+        const u32x4 rsw = mtts::make_rsrc(p.W, (uint32_t)((long long)NPL * p.N * p.Kp * 2));
         const uint32_t lw = mtts::lds_addr(sw);
-        const int cpr = K / 8;  // 16-byte chunks per W row
+        constexpr int CPR = K / 8;  // 16-byte chunks per W row
         for (int q = wave; q < K / 8; q += kNW) {
-            const int t = 64 * q + lane, w = t / cpr, pc = t - w * cpr;
+            const int t = 64 * q + lane, w = t / CPR, pc = t - w * CPR;
             const int c = (pc & ~15) | ((pc & 15) ^ (w & 15));
             const int pl = NPL == 2 ? w >> 5 : 0, n = n0 + (NPL == 2 ? w & 31 : w);
             const uint32_t vw = n < p.N ? (uint32_t)((((long long)pl * p.N + n) * p.Kp + c * 8) * 2) : kOob;
             mtts::bload16(vw, rsw, 0u, __builtin_amdgcn_readfirstlane(lw + q * 1024));
         }
     }
-
-    // ---- A staging: instruction q of a stage fills image rows 16 q .. 16 q + 15 (lane: row 16 q + lane / 4, slot
-    // lane % 4 <- logical chunk (lane % 4) ^ ((row >> 2) & 3))
-    const u32x4 rsa = mtts::make_rsrc(p.A, (uint32_t)((long long)arows * p.lda * ES));
-    const uint32_t la0 = mtts::lds_addr(sa);
-    uint32_t av[PW];  // this lane's source byte offsets for the current issue tile (channel chunk 0)
-    int atile = -1;
-    auto issue = [&](int st, int stage) {
-        if (st >= nsteps) return;
-        const int ti = st / nch, ch = st - ti * nch;
-        if (ti != atile) {
-            atile = ti;
-            const int m0 = (r + ti * R) * kBM;
+    float bias[TN];
 #pragma unroll
-            for (int k = 0; k < PW; ++k) {
-                const int q = wave + kNW * k;
-                const int row = 16 * q + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 3);
-                const bool v = (vbits >> (ti * PW + k)) & 1u;
-                av[k] = v ? (uint32_t)(((long long)(m0 + off_min + row) * p.lda + c * (16 / ES)) * ES) : kOob;
-            }
-        }
-        const uint32_t soff = (uint32_t)(ch * CPC * ES);
-        if (dbg & 2) return;  // diagnostic: no A staging
-#pragma unroll
-        for (int k = 0; k < PW; ++k) {
-            const int q = wave + kNW * k;
-            if (q < NI)  // wave-uniform
-                mtts::bload16(av[k], rsa, soff, __builtin_amdgcn_readfirstlane(la0 + stage * G::STAGE + q * 1024));
-        }
-    };
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + 32 * j + lr;
+        bias[j] = p.bias && n < p.N ? p.bias[n] : 0.f;
+    }
+    mtts::wait_vmcnt<0>();
+    __syncthreads();  // the W image is complete and read-only from here on
 
-    // ---- per-lane fragment rows of the current compute tile: image row of output row 32 * wave + lr at tap j, or
-    // the zero row when the tap leaves the utterance
-    int arow[NTAP];
-    auto tile_rows = [&](int ti) {
-        const int m = (r + ti * R) * kBM + 32 * wave + lr;
+    mtts_conv_gemm_args pe = p;
+    pe.bias = nullptr;
+
+    // ---- A addressing: the lane's source of block row i (row 32 i + lr of the wave block) at tap j, substep chunk 0,
+    // and the byte step per 16-channel chunk (0 for an invalid tap row: it reads the zero buffer at every chunk)
+    const unsigned char *abase = reinterpret_cast<const unsigned char *>(p.A);
+    const unsigned char *zero = reinterpret_cast<const unsigned char *>(g_wl_zero);
+    auto row_ok = [&](int m, int j, int &src) {  // tap j of output row m: in its utterance (and m < M)
         int b = 0, u = 0;
-        mtts::divmod_fast(m < M ? m : 0, p.To, 1.0f / (float)p.To, b, u);
+        mtts::divmod_fast(m < M ? m : 0, p.To, inv_to, b, u);
+        const int o = p.off[0] + j * dstep;
+        src = m + o;
+        return m < M && u + o >= 0 && u + o < p.Ti;
+    };
+    const unsigned char *base[TM][NTAP], *nbase[TM][NTAP];
+    int stp[TM][NTAP], nstp[TM][NTAP];
+    float mk[TM][NTAP];
+    auto load_masks = [&](int blk) {  // the next block's input-row masks (used NS substeps before it starts)
 #pragma unroll
-        for (int j = 0; j < NTAP; ++j) {
-            const int o = p.off[0] + j * (NTAP > 1 ? p.off[1] - p.off[0] : 0);
-            const int ui = u + o;
-            const bool v = ui >= 0 && ui < p.Ti;
-            arow[j] = v ? 32 * wave + lr + (o - off_min) : NRP - 1;
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < NTAP; ++j) {
+                int src = 0;
+                const bool ok = blk < nblk && row_ok(blk * BMW + 32 * i + lr, j, src);
+                mk[i][j] = p.a_scale ? p.a_scale[ok ? src : 0] : 1.f;
+            }
+    };
+    auto set_bases = [&](int blk, const unsigned char *(&bs)[TM][NTAP], int (&sp)[TM][NTAP]) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < NTAP; ++j) {
+                int src = 0;
+                const bool ok = blk < nblk && row_ok(blk * BMW + 32 * i + lr, j, src) && mk[i][j] != 0.f;
+                bs[i][j] = ok ? abase + ((long long)src * p.lda + 8 * lh) * ES : zero;
+                sp[i][j] = ok ? 16 * ES : 0;
+            }
+    };
+    // substep t of a block: chunk t / NTAP at tap t % NTAP (the taps of one chunk back to back: L1 serves the
+    // shifted rows)
+    auto load = [&](const unsigned char *(&bs)[TM][NTAP], int (&sp)[TM][NTAP], int t, AFrag<ABF16, TM> &f) {
+        const int c = t / NTAP, j = t % NTAP;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const unsigned char *q = bs[i][j] + c * sp[i][j];
+            f.v[i][0] = *reinterpret_cast<const uint4 *>(q);
+            if constexpr (!ABF16) f.v[i][1] = *reinterpret_cast<const uint4 *>(q + 16);
         }
     };
 
-    for (int s0 = 0; s0 < S - 1; ++s0) issue(s0, s0);
+    int blk = r + R * wave;  // this wave's blocks: r + R * (wave + 4 i)
+    AFrag<ABF16, TM> ring[NS];
+    load_masks(blk);
+    set_bases(blk, base, stp);
+#pragma unroll
+    for (int t = 0; t < PD; ++t) load(base, stp, t, ring[t]);
 
     const int wrow0 = lr * K * 2, wrow1 = (32 + lr) * K * 2;  // this lane's two W rows (w & 15 == lr & 15)
-    int cur = 0, st = 0;
-    for (int ti = 0; ti < ntl; ++ti) {
-        tile_rows(ti);
-        // the tile's accumulators live only inside its chunk loop (loop-carried across tiles, the register
-        // allocator copied them out of the AGPRs at every step, behind a vmcnt(0) that drained the DMAs in flight)
-        f32x16 acc[1][TN];
+    for (; blk < nblk; blk += kNW * R) {
+        const int nxt = blk + kNW * R;
+        load_masks(nxt);  // (always issued: a zero-step base for a missing next block reads the zero buffer)
+        f32x16 acc[TM][TN];
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int v = 0; v < 16; ++v) acc[0][j][v] = 0.f;
-        for (int ch = 0; ch < nch; ++ch, ++st) {
-            // steps issued after st: min(S - 2, nsteps - 1 - st); W's loads are all older than step 0's
-            if (st + S - 2 < nsteps) wait_steps<NTAP, S - 2>(wave);
-            else mtts::wait_vmcnt<0>();
-            mtts::lds_barrier();
-            issue(st + S - 1, cur == 0 ? S - 1 : cur - 1);
-            const unsigned char *sb = sa + cur * G::STAGE;
-            // every fragment of the step is read first, then the MFMAs run back to back: with one wave per SIMD
-            // nothing else hides an LDS read, and read-MFMA pairs exposed its latency at every MFMA
-            bf16x8 af[NTAP][SUB], bw[NTAP][SUB][2];
-#pragma unroll
-            for (int j = 0; j < NTAP; ++j) {
-#pragma unroll
-                for (int s = 0; s < SUB; ++s) {
-                    if constexpr (ABF16) {
-                        af[j][s] = *reinterpret_cast<const bf16x8 *>(sb + a_swz(arow[j], 2 * s + lh));
-                    } else {
-                        const float4 x0 = *reinterpret_cast<const float4 *>(sb + a_swz(arow[j], 2 * lh));
-                        const float4 x1 = *reinterpret_cast<const float4 *>(sb + a_swz(arow[j], 2 * lh + 1));
-                        af[j][s] = __builtin_bit_cast(bf16x8, make_uint4(pack2(x0.x, x0.y), pack2(x0.z, x0.w),
-                                                                         pack2(x1.x, x1.y), pack2(x1.z, x1.w)));
-                    }
-                    // W chunk of k = j * cin + ch * CPC + 16 s + 8 lh
-                    const int cw = (j * cin + ch * CPC + 16 * s) / 8 + lh;
-                    const int so = w_swz(lr, cw);
-                    bw[j][s][0] = *reinterpret_cast<const bf16x8 *>(sw + wrow0 + so);
-                    bw[j][s][1] = *reinterpret_cast<const bf16x8 *>(sw + wrow1 + so);
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if (dbg & 1) {  // diagnostic: reads, no MFMAs (keep the reads alive)
-#pragma unroll
-                for (int j = 0; j < NTAP; ++j)
-#pragma unroll
-                    for (int s = 0; s < SUB; ++s) acc[0][0][0] += (float)af[j][s][0] + (float)bw[j][s][0][1] + (float)bw[j][s][1][2];
-            } else
-#pragma unroll
-            for (int j = 0; j < NTAP; ++j) {
-#pragma unroll
-                for (int s = 0; s < SUB; ++s) {
-                    if constexpr (NPL == 2) {
-                        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[j][s], bw[j][s][0], acc[0][0], 0, 0, 0);
-                        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[j][s], bw[j][s][1], acc[0][0], 0, 0, 0);
-                    } else {
-                        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[j][s], bw[j][s][0], acc[0][0], 0, 0, 0);
-                        acc[0][TN - 1] =
-                            __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[j][s], bw[j][s][1], acc[0][TN - 1], 0, 0, 0);
-                    }
-                }
-            }
-            cur = cur == S - 1 ? 0 : cur + 1;
-        }
-        if (p.bias) {
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
-                for (int v = 0; v < 16; ++v) acc[0][j][v] += bias[j];
+                for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+        // W fragments of substep t (k = j * CIN + 16 c + 8 lh), read one substep ahead; a scheduling barrier per
+        // substep keeps the compiler from hoisting every read of the unrolled block (it spilled at two planes)
+        auto wread = [&](int t, bf16x8 (&b)[2]) {
+            const int c = t / NTAP, j = t % NTAP;
+            const int so = w_swz(lr, (j * CIN + 16 * c) / 8 + lh);
+            b[0] = *reinterpret_cast<const bf16x8 *>(sw + wrow0 + so);
+            b[1] = *reinterpret_cast<const bf16x8 *>(sw + wrow1 + so);
+        };
+        bf16x8 wb[2][2];
+        wread(0, wb[0]);
+#pragma unroll
+        for (int t = 0; t < KS; ++t) {
+            if (t == KS - PD) set_bases(nxt, nbase, nstp);
+            if (t + PD < KS) load(base, stp, t + PD, ring[(t + PD) % NS]);
+            else load(nbase, nstp, t + PD - KS, ring[(t + PD) % NS]);
+            if (t + 1 < KS) wread(t + 1, wb[(t + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            const bf16x8 b0 = wb[t & 1][0], b1 = wb[t & 1][1];
+            const AFrag<ABF16, TM> &f = ring[t % NS];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                bf16x8 af;
+                if constexpr (ABF16) {
+                    af = __builtin_bit_cast(bf16x8, f.v[i][0]);
+                } else {
+                    const uint4 x0 = f.v[i][0], x1 = f.v[i][1];
+                    af = __builtin_bit_cast(
+                        bf16x8, make_uint4(pack2(__uint_as_float(x0.x), __uint_as_float(x0.y)),
+                                           pack2(__uint_as_float(x0.z), __uint_as_float(x0.w)),
+                                           pack2(__uint_as_float(x1.x), __uint_as_float(x1.y)),
+                                           pack2(__uint_as_float(x1.z), __uint_as_float(x1.w))));
+                }
+                if constexpr (NPL == 2) {
+                    acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc[i][0], 0, 0, 0);
+                    acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc[i][0], 0, 0, 0);
+                } else {
+                    acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc[i][0], 0, 0, 0);
+                    acc[i][TN - 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc[i][TN - 1], 0, 0, 0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
-        // (no global load in this epilogue -- conv_gemm_wlds_applies refuses residual / c_scale / dropout: its
-        // wait would drain the DMAs in flight)
-        mtts::gemm_epilogue_vec_v<8, 1, TN, EK, false>(pe, acc, sepi + wave * 1024, (r + ti * R) * kBM + 32 * wave, n0,
-                                                       lane);
+        if (p.bias) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) acc[i][j][v] += bias[j];
+        }
+        mtts::gemm_epilogue_vec_v<8, TM, TN, EK, false>(pe, acc, sepi + wave * 1024, blk * BMW, n0, lane);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < NTAP; ++j) {
+                base[i][j] = nbase[i][j];
+                stp[i][j] = nstp[i][j];
+            }
     }
-    mtts::wait_vmcnt<0>();  // no DMA may still target this workgroup's LDS when it retires
 }
 
 struct WlGrid {
-    int ncg, mtiles, R;
+    int ncg, nblk, R;
 };
 
-WlGrid wlds_grid(const mtts_conv_gemm_args &p, int M) {
+WlGrid wlds_grid(const mtts_conv_gemm_args &p, int M, int bmw) {
     static const int cus = [] {
         int dev = 0, n = 256;
         hipDeviceProp_t pr;
@@ -299,63 +252,61 @@ WlGrid wlds_grid(const mtts_conv_gemm_args &p, int M) {
     const int npl = (p.flags & MTTS_GEMM_F_W_SPLIT) ? 2 : 1;
     WlGrid g;
     g.ncg = (p.N + (npl == 2 ? 31 : 63)) / (npl == 2 ? 32 : 64);
-    g.mtiles = (M + kBM - 1) / kBM;
-    g.R = std::max(1, std::min(g.mtiles, cus / g.ncg));
-    // every stream's tiles must fit the precomputed validity bits
-    g.R = std::max(g.R, (g.mtiles + kMaxTiles - 1) / kMaxTiles);
+    g.nblk = (M + bmw - 1) / bmw;
+    g.R = std::max(1, std::min((g.nblk + kNW - 1) / kNW, cus / g.ncg));
     return g;
 }
 
-template <bool ABF16, int NPL, int NTAP, int EK>
+template <bool ABF16, int NPL, int NTAP, int KS, int EK>
 int launch_wlds_e(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
-    constexpr int S = 5;
-    using G = WlGeom<NTAP>;
-    static_assert(64 * kKMax * 2 + S * G::STAGE + kNW * 4096 <= 160 * 1024, "LDS");
-    static_assert(kMaxTiles * G::PW <= 32, "validity bits: kMaxTiles * PW <= 32");
-    const WlGrid g = wlds_grid(p, M);
-    const int o0 = p.off[0], o1 = p.off[p.ntaps - 1];
-    // MTTS_WLDS_DBG (diagnostics only): bit 0 = no MFMAs, bit 1 = no A staging
-    static const int dbg = [] { const char *e = getenv("MTTS_WLDS_DBG"); return e ? atoi(e) : 0; }();
-    hipLaunchKernelGGL((conv_gemm_wlds_kernel<ABF16, NPL, NTAP, S, EK>), dim3((unsigned)(g.ncg * g.R)), dim3(kNT), 0, st, p,
-                       g.ncg, g.mtiles, std::min(o0, o1), dbg);
+    constexpr int TM = 2;
+    constexpr int PD = ABF16 ? 15 : 7;
+    const WlGrid g = wlds_grid(p, M, 32 * TM);
+    hipLaunchKernelGGL((conv_gemm_wlds_kernel<ABF16, NPL, NTAP, KS, TM, PD, EK>), dim3((unsigned)(g.ncg * g.R)), dim3(kNT),
+                       0, st, p, g.ncg, g.nblk);
     return mtts::check_launch("conv_gemm_wlds_kernel");
 }
 
-template <bool ABF16, int NPL, int NTAP>
-int launch_wlds_t(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
-    return mtts::gemm_epilogue_kind(p) == mtts::EK_LIN_C16 ? launch_wlds_e<ABF16, NPL, NTAP, mtts::EK_LIN_C16>(p, M, st)
-                                                            : launch_wlds_e<ABF16, NPL, NTAP, mtts::EK_LIN_C32>(p, M, st);
+template <bool ABF16, int NPL, int NTAP, int KS>
+int launch_wlds_k(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
+    switch (mtts::gemm_epilogue_kind(p)) {
+        case mtts::EK_LIN_C16: return launch_wlds_e<ABF16, NPL, NTAP, KS, mtts::EK_LIN_C16>(p, M, st);
+        case mtts::EK_LIN_C32: return launch_wlds_e<ABF16, NPL, NTAP, KS, mtts::EK_LIN_C32>(p, M, st);
+        default: return launch_wlds_e<ABF16, NPL, NTAP, KS, mtts::EK_RT>(p, M, st);
+    }
 }
 
+// (taps, K) instantiated: (3, 768) the k = 3 convs over 256 channels; (2, 512) the transposed conv's phases; (1, 768)
+// the q|k|v dgrad; (1, 512), (1, 256) the other 256 / 512-wide linears
 template <bool ABF16, int NPL>
 int launch_wlds_n(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
-    switch (p.ntaps) {
-        case 1: return launch_wlds_t<ABF16, NPL, 1>(p, M, st);
-        case 2: return launch_wlds_t<ABF16, NPL, 2>(p, M, st);
-        default: return launch_wlds_t<ABF16, NPL, 3>(p, M, st);
-    }
+    if (p.ntaps == 3 && p.K == 768) return launch_wlds_k<ABF16, NPL, 3, 48>(p, M, st);
+    if (p.ntaps == 2 && p.K == 512) return launch_wlds_k<ABF16, NPL, 2, 32>(p, M, st);
+    if (p.ntaps == 1 && p.K == 768) return launch_wlds_k<ABF16, NPL, 1, 48>(p, M, st);
+    if (p.ntaps == 1 && p.K == 512) return launch_wlds_k<ABF16, NPL, 1, 32>(p, M, st);
+    if (p.ntaps == 1 && p.K == 256) return launch_wlds_k<ABF16, NPL, 1, 16>(p, M, st);
+    return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: weight-resident schedule: (taps, K) not instantiated");
 }
 
 }  // namespace
 
 namespace mtts {
 
-// bf16 MFMA on one or two weight planes; 1..3 taps at stride 1 over whole utterances (Ti == To); K = taps * cin <= 768
-// with whole 64-byte channel chunks (cin % 32 bf16 / % 16 fp32); a 0/1 row mask or none; no activation / pre-activation
-// (the plain bf16 / fp32 C epilogue kinds, with a bias at most: no residual / c_scale / dropout); 16-byte epilogue
+// bf16 MFMA on one or two weight planes; (taps, K) in {(3, 768), (2, 512), (1, 768), (1, 512), (1, 256)} at stride 1
+// over whole utterances (Ti == To); a 0/1 row mask or none; 16-byte aligned A rows; any epilogue without an
+// activation / pre-activation (the 16-byte epilogue: N % 8)
 bool conv_gemm_wlds_applies(const mtts_conv_gemm_args &p) {
     if (p.ntaps < 1 || p.ntaps > 3 || p.in_stride != 1 || p.Ti != p.To) return false;
     if (p.ntaps > 1 && p.off[1] - p.off[0] != 1 && p.off[1] - p.off[0] != -1) return false;
-    if (p.K != p.ntaps * p.cin || p.K > kKMax || p.K % 128) return false;  // (the W swizzle: 16-chunk groups)
+    const bool kok = (p.ntaps == 3 && p.K == 768) || (p.ntaps == 2 && p.K == 512) ||
+                     (p.ntaps == 1 && (p.K == 768 || p.K == 512 || p.K == 256));
+    if (!kok || p.K != p.ntaps * p.cin) return false;
     if (p.flags & (MTTS_GEMM_F_A_SPLIT | MTTS_GEMM_F_SPLIT3)) return false;
     if (p.a_scale && !(p.flags & MTTS_GEMM_F_BINARY_SCALE)) return false;
     const bool a16 = p.flags & MTTS_GEMM_F_A_BF16;
     const int es = a16 ? 2 : 4;
-    if (p.cin % (64 / es) || p.lda % (16 / es) || (uintptr_t)p.A % 16 || (uintptr_t)p.W % 16 || p.Kp % 8) return false;
-    const int k = gemm_epilogue_kind(p);
-    if (k != EK_LIN_C16 && k != EK_LIN_C32) return false;
-    // no epilogue stream but the output: a global load inside the DMA pipeline waits for (drains) every DMA in flight
-    if (p.residual || p.c_scale || p.dropout_p > 0.f) return false;
+    if (p.lda % (16 / es) || (uintptr_t)p.A % 16 || (uintptr_t)p.W % 16 || p.Kp % 8) return false;
+    if (p.act != MTTS_ACT_NONE || p.C_pre) return false;
     if ((long long)p.nb * p.Ti * p.lda * es >= (1ll << 31) - (1ll << 20)) return false;
     const int npl = (p.flags & MTTS_GEMM_F_W_SPLIT) ? 2 : 1;
     if ((long long)npl * p.N * p.Kp * 2 >= (1ll << 31) - (1ll << 20)) return false;

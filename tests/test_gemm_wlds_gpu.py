@@ -28,7 +28,7 @@ def _weights(N, K, split, g):
     return Wp, Kp, w.bfloat16().float()
 
 
-@pytest.mark.parametrize("kind", ["c16", "c16_bias", "c32_bias"])
+@pytest.mark.parametrize("kind", ["c16", "c16_bias", "c32_bias", "c32_bias_res", "c32_cscale"])
 @pytest.mark.parametrize("B,T,cin,N,taps,a16,split,masked,ostride", [
     (3, 301, 256, 256, [-1, 0, 1], True, True, True, 1),      # Block1D conv, split planes, ragged rows + mask
     (2, 600, 256, 256, [1, 0, -1], True, False, False, 1),    # its dgrad (descending taps)
@@ -37,6 +37,8 @@ def _weights(N, K, split, g):
     (3, 300, 256, 256, [0, -1], False, True, True, 2),        # ConvTranspose phase: 2 taps, strided output
     (2, 77, 768, 256, [0], True, False, False, 1),            # q|k|v dgrad (one tap, K = 768)
     (1, 4800, 256, 192, [-1, 0, 1], False, False, True, 1),   # one long utterance, N = 192
+    (3, 333, 512, 256, [0], True, True, True, 1),             # one tap, K = 512
+    (2, 100, 256, 256, [0], False, False, False, 1),          # one tap, K = 256, few blocks
 ])
 def test_wlds_vs_float64_and_lds_dma(kind, B, T, cin, N, taps, a16, split, masked, ostride):
     from matcha.models.components import _ops as O
@@ -51,8 +53,12 @@ def test_wlds_vs_float64_and_lds_dma(kind, B, T, cin, N, taps, a16, split, maske
         kw["a_scale"] = msk.to(DEV)
     c16 = kind.startswith("c16")
     To_full = T * ostride
-    if kind.endswith("bias"):
+    if "bias" in kind or kind == "c32_cscale":
         kw["bias"] = torch.randn(N, generator=g).to(DEV)
+    if kind == "c32_bias_res":
+        kw["residual"] = torch.randn(B, To_full, N, generator=g).to(DEV)
+    if kind == "c32_cscale":
+        kw["c_scale"] = (torch.rand(B * To_full, generator=g) > 0.2).float().to(DEV)
     A = x.to(DEV).bfloat16() if a16 else x.to(DEV)
     outs = []
     for cfg in (WLDS, WLDS, 41):
@@ -74,8 +80,12 @@ def test_wlds_vs_float64_and_lds_dma(kind, B, T, cin, N, taps, a16, split, maske
         ref += src @ wr[:, j].T
     full = torch.full((B, To_full, N), float("nan"), dtype=torch.float64)
     rows = slice(ostride - 1, None, ostride)
-    if kind.endswith("bias"):
+    if "bias" in kind or kind == "c32_cscale":
         ref += kw["bias"].double().cpu()
+    if kind == "c32_bias_res":
+        ref += kw["residual"].double().cpu()[:, rows]
+    if kind == "c32_cscale":
+        ref *= kw["c_scale"].double().cpu().view(B, To_full, 1)[:, rows]
     full[:, rows] = ref
     got = outs[0].double().cpu()
     assert torch.equal(torch.isnan(got), torch.isnan(full))  # every output row written, nothing else
@@ -87,8 +97,8 @@ def test_wlds_vs_float64_and_lds_dma(kind, B, T, cin, N, taps, a16, split, maske
 
 
 def test_wlds_refuses_unsupported_shapes():
-    """No silent fallback: an explicit request for a shape the kernel does not cover (K > 768, an activation, a
-    residual / row-scale epilogue stream, stride 2) fails loudly; the heuristic keeps the other schedules there."""
+    """No silent fallback: an explicit request for a shape the kernel does not cover (K > 768, an activation, stride 2)
+    fails loudly; the heuristic keeps the other schedules there."""
     from matcha import _native as N
     from matcha.models.components import _ops as O
 
@@ -101,12 +111,6 @@ def test_wlds_refuses_unsupported_shapes():
     Wp, Kp = O.pack_weight(torch.randn(128, 256, device=DEV), O.PREC_BF16)
     with pytest.raises(N.NativeError):
         O._gemm(x, 50, 50, 2, 1, [0], 256, Wp, Kp, 128, y, 50, prec=O.PREC_BF16, tile_cfg=WLDS, act=O.ACT_RELU)
-    with pytest.raises(N.NativeError):
-        O._gemm(x, 50, 50, 2, 1, [0], 256, Wp, Kp, 128, y, 50, prec=O.PREC_BF16, tile_cfg=WLDS,
-                residual=torch.randn(2, 50, 128, device=DEV))
-    with pytest.raises(N.NativeError):
-        O._gemm(x, 50, 50, 2, 1, [0], 256, Wp, Kp, 128, y, 50, prec=O.PREC_BF16, tile_cfg=WLDS,
-                c_scale=torch.ones(100, device=DEV))
     x2 = torch.randn(2, 100, 256, device=DEV)  # the stride-2 Downsample conv
     Wp3, Kp3 = O.pack_weight(torch.randn(128, 3 * 256, device=DEV), O.PREC_BF16)
     with pytest.raises(N.NativeError):
