@@ -17,8 +17,8 @@
 // whatever it carried (diagnostic switches: 24.8 of 29.7 us without MFMAs and without A staging), and it ran 20-90 %
 // slower than the LDS-DMA kernels on every step shape.
 //
-// Numerics: fp32 accumulation of bf16 products in (16-channel chunk, tap) order -- not bitwise the LDS-DMA kernels'
-// tap-major order; within fp32 accumulation error of them (tests/test_gemm_wlds_gpu.py).
+// Numerics: fp32 accumulation of bf16 products in (64-channel chunk, tap, permuted 16-k substep) order -- not bitwise
+// the LDS-DMA kernels' tap-major order; within fp32 accumulation error of them (tests/test_gemm_wlds_gpu.py).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -65,11 +65,11 @@ template <bool ABF16, int NPL, int NTAP, int KS, int TM, int PD, int EK>
 __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_args p, int ncg, int nblk) {
     static_assert(KS % (PD + 1) == 0, "ring slots repeat every block");
     constexpr int ES = ABF16 ? 2 : 4;
-    constexpr int K = 16 * KS, CIN = K / NTAP, NC = CIN / 16;  // NC 16-channel chunks per tap
+    constexpr int K = 16 * KS, CIN = K / NTAP;
     constexpr int TN = NPL == 2 ? 1 : 2;                       // 32-column accumulator blocks per wave
     constexpr int BMW = 32 * TM;                                // rows per wave block
     constexpr int NS = PD + 1;
-    static_assert(CIN % 16 == 0 && K <= kKMax, "shape");
+    static_assert(CIN % 64 == 0 && K <= kKMax, "shape: whole 64-channel chunks per tap");
     __shared__ __attribute__((aligned(1024))) unsigned char sw[64 * K * 2];
     __shared__ __attribute__((aligned(16))) float sepi[kNW * 1024];
 
@@ -111,8 +111,14 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
     mtts_conv_gemm_args pe = p;
     pe.bias = nullptr;
 
-    // ---- A addressing: the lane's source of block row i (row 32 i + lr of the wave block) at tap j, substep chunk 0,
-    // and the byte step per 16-channel chunk (0 for an invalid tap row: it reads the zero buffer at every chunk)
+    // ---- A addressing.  The reduction runs over 64-channel chunks c, tap j inside a chunk, 4 substeps s inside a
+    // tap, and a substep's 16 k are NOT 16 consecutive channels: lane half lh takes channels 64 c + 32 lh + 8 s ..
+    // + 8 (W's fragments follow the same permutation).  So a lane's 4 substeps read 32 contiguous channels of its
+    // row and the 64 lanes of 4 consecutive loads cover whole 128-byte lines: with 16 consecutive channels per
+    // substep (the MFMA's natural k order) every load touched 32 lines for 32 bytes each, and with four waves'
+    // blocks L1 could not hold the lines until the next chunk came back -- ~4x the bytes from L2.
+    // base: the lane's row of block row i at tap j (+ its 32-channel half), ok: 0 when the tap row is invalid
+    // (every load of it then reads the zero buffer)
     const unsigned char *abase = reinterpret_cast<const unsigned char *>(p.A);
     const unsigned char *zero = reinterpret_cast<const unsigned char *>(g_wl_zero);
     auto row_ok = [&](int m, int j, int &src) {  // tap j of output row m: in its utterance (and m < M)
@@ -123,7 +129,7 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
         return m < M && u + o >= 0 && u + o < p.Ti;
     };
     const unsigned char *base[TM][NTAP], *nbase[TM][NTAP];
-    int stp[TM][NTAP], nstp[TM][NTAP];
+    int stp[TM][NTAP], nstp[TM][NTAP];  // 1: valid, 0: zero buffer
     float mk[TM][NTAP];
     auto load_masks = [&](int blk) {  // the next block's input-row masks (used NS substeps before it starts)
 #pragma unroll
@@ -142,17 +148,17 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
             for (int j = 0; j < NTAP; ++j) {
                 int src = 0;
                 const bool ok = blk < nblk && row_ok(blk * BMW + 32 * i + lr, j, src) && mk[i][j] != 0.f;
-                bs[i][j] = ok ? abase + ((long long)src * p.lda + 8 * lh) * ES : zero;
-                sp[i][j] = ok ? 16 * ES : 0;
+                bs[i][j] = ok ? abase + ((long long)src * p.lda + 32 * lh) * ES : zero;
+                sp[i][j] = ok ? 1 : 0;
             }
     };
-    // substep t of a block: chunk t / NTAP at tap t % NTAP (the taps of one chunk back to back: L1 serves the
-    // shifted rows)
+    // substep t of a block = (chunk t / (4 NTAP), tap (t / 4) % NTAP, s = t % 4): the taps of one chunk back to back
+    // (the shifted rows come from L1)
     auto load = [&](const unsigned char *(&bs)[TM][NTAP], int (&sp)[TM][NTAP], int t, AFrag<ABF16, TM> &f) {
-        const int c = t / NTAP, j = t % NTAP;
+        const int c = t / (4 * NTAP), j = (t / 4) % NTAP, sub = t % 4;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-            const unsigned char *q = bs[i][j] + c * sp[i][j];
+            const unsigned char *q = bs[i][j] + sp[i][j] * ((64 * c + 8 * sub) * ES);
             f.v[i][0] = *reinterpret_cast<const uint4 *>(q);
             if constexpr (!ABF16) f.v[i][1] = *reinterpret_cast<const uint4 *>(q + 16);
         }
@@ -176,11 +182,12 @@ __global__ __launch_bounds__(kNT, 1) void conv_gemm_wlds_kernel(mtts_conv_gemm_a
             for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
-        // W fragments of substep t (k = j * CIN + 16 c + 8 lh), read one substep ahead; a scheduling barrier per
-        // substep keeps the compiler from hoisting every read of the unrolled block (it spilled at two planes)
+        // W fragments of substep t (k = j * CIN + 64 c + 32 lh + 8 s, the permutation above), read one substep ahead;
+        // a scheduling barrier per substep keeps the compiler from hoisting every read of the unrolled block (it
+        // spilled at two planes)
         auto wread = [&](int t, bf16x8 (&b)[2]) {
-            const int c = t / NTAP, j = t % NTAP;
-            const int so = w_swz(lr, (j * CIN + 16 * c) / 8 + lh);
+            const int c = t / (4 * NTAP), j = (t / 4) % NTAP, sub = t % 4;
+            const int so = w_swz(lr, (j * CIN + 64 * c + 8 * sub) / 8 + 4 * lh);
             b[0] = *reinterpret_cast<const bf16x8 *>(sw + wrow0 + so);
             b[1] = *reinterpret_cast<const bf16x8 *>(sw + wrow1 + so);
         };
@@ -282,7 +289,9 @@ template <bool ABF16, int NPL>
 int launch_wlds_n(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
     if (p.ntaps == 3 && p.K == 768) return launch_wlds_k<ABF16, NPL, 3, 48>(p, M, st);
     if (p.ntaps == 2 && p.K == 512) return launch_wlds_k<ABF16, NPL, 2, 32>(p, M, st);
-    if (p.ntaps == 1 && p.K == 768) return launch_wlds_k<ABF16, NPL, 1, 48>(p, M, st);
+    if constexpr (ABF16) {  // (an fp32 A at K = 768, one tap, spilled; no step launch has it)
+        if (p.ntaps == 1 && p.K == 768) return launch_wlds_k<ABF16, NPL, 1, 48>(p, M, st);
+    }
     if (p.ntaps == 1 && p.K == 512) return launch_wlds_k<ABF16, NPL, 1, 32>(p, M, st);
     if (p.ntaps == 1 && p.K == 256) return launch_wlds_k<ABF16, NPL, 1, 16>(p, M, st);
     return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: weight-resident schedule: (taps, K) not instantiated");
@@ -292,7 +301,7 @@ int launch_wlds_n(const mtts_conv_gemm_args &p, int M, hipStream_t st) {
 
 namespace mtts {
 
-// bf16 MFMA on one or two weight planes; (taps, K) in {(3, 768), (2, 512), (1, 768), (1, 512), (1, 256)} at stride 1
+// bf16 MFMA on one or two weight planes; (taps, K) in {(3, 768), (2, 512), (1, 768; bf16 A), (1, 512), (1, 256)} at stride 1
 // over whole utterances (Ti == To); a 0/1 row mask or none; 16-byte aligned A rows; any epilogue without an
 // activation / pre-activation (the 16-byte epilogue: N % 8)
 bool conv_gemm_wlds_applies(const mtts_conv_gemm_args &p) {
@@ -301,6 +310,7 @@ bool conv_gemm_wlds_applies(const mtts_conv_gemm_args &p) {
     const bool kok = (p.ntaps == 3 && p.K == 768) || (p.ntaps == 2 && p.K == 512) ||
                      (p.ntaps == 1 && (p.K == 768 || p.K == 512 || p.K == 256));
     if (!kok || p.K != p.ntaps * p.cin) return false;
+    if (!(p.flags & MTTS_GEMM_F_A_BF16) && p.ntaps == 1 && p.K == 768) return false;  // not instantiated
     if (p.flags & (MTTS_GEMM_F_A_SPLIT | MTTS_GEMM_F_SPLIT3)) return false;
     if (p.a_scale && !(p.flags & MTTS_GEMM_F_BINARY_SCALE)) return false;
     const bool a16 = p.flags & MTTS_GEMM_F_A_BF16;
