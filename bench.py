@@ -502,7 +502,7 @@ def main():
                  ("split_weights", True, True, "bf16"), ("parity_policy", True, True, OPS.encoder_precision_for_parity()),
                  ("parity_bf16x3_encoder", True, True, "bf16x3"), ("parity_bf16x6_encoder", True, True, "bf16x6"),
                  ("parity_fp32fwd_encoder", True, True, "fp32fwd"), ("parity_fp32_encoder", True, True, "fp32"))
-        from matcha.precision import grad_errors, loss_and_grads, precision_context
+        from matcha.precision import error_attribution, grad_errors, loss_and_grads, precision_context
 
         trainer_modes = {"32-true": "32-true", "one_plane": "bf16-mixed", "parity_policy": "bf16-parity"}
         with torch.no_grad():
@@ -527,6 +527,9 @@ def main():
             _, gm, _ = loss_and_grads(pm, pb, trainer_modes[name], t=t_inj, z=z_inj)
             grads_check[name] = {k: (round(v, 7) if isinstance(v, float) else v)
                                  for k, v in grad_errors(gm, g32, params).items()}
+        # which module family's bf16 arithmetic the benched precision's gradient error comes from
+        run_mode = "parity_policy" if args.precision == "bf16-parity" else "one_plane"
+        grads_check["attribution"] = error_attribution(pm, pb, trainer_modes[run_mode], g32, t=t_inj, z=z_inj)
         del pm, g32, gm
         l32, a32 = res["32-true"]
 
@@ -535,7 +538,6 @@ def main():
             return {"loss_rel_err": [round(abs(a - b) / abs(b), 7) for a, b in zip(l16, l32)],
                     "alignment_cell_agreement": round(float((a16 == a32).float().mean().item()), 6)}
 
-        run_mode = "parity_policy" if args.precision == "bf16-parity" else "one_plane"
         precision_check = {
             "bf16_loss_rel_err": errs(run_mode)["loss_rel_err"],
             "run_mode": run_mode,
@@ -545,7 +547,9 @@ def main():
             "grads_note": "fwd + bwd of the same batch (eval mode) in each precision: gradient vs 32-true's "
                           "(global and per-tensor relative L2 error, the global norm's relative error) and one "
                           "clip(1.0) + AdamW(1e-4) update from zero moments (train.py:85 32-true is the reference "
-                          "precision; the bf16 modes' backward runs in bf16)",
+                          "precision; the bf16 modes' backward runs in bf16).  attribution: the benched precision "
+                          "with one module family held in 32-true at a time (matcha/precision.py hold_fp32): "
+                          "source_share = 1 - (e_held / e)^2; lands_share = where the squared error sits",
             "losses": ["dur", "prior", "diff"],
             "bar": "alignment bit-exact (agreement 1.0), mel / flow-matching loss within 1e-4 relative (north star)",
             "note": "bf16 modes vs 32-true (= the oracle at this batch) with the parity tests' recipe weights and "

@@ -48,15 +48,16 @@ MODES = {"32-true": (False, False, "bf16"), "bf16-mixed": (True, False, "bf16"),
 PARITY_MODES = ("bf16-parity", "bf16-parity-fp32enc")
 # The at-bar modes' BACKWARD is bf16: their gradients pinned against the reference fixture's
 # per-tensor gradient norms (B=4) and the 32-true step's gradients / AdamW update (B=32, below).  Bounds from
-# the round-5 GPU measurement (profiles/r05/grads/), about 3x the measured value.  bf16-parity measured: B=4
-# global norm 3.3e-4, per-tensor norms median 4.3e-4 / max 1.9e-2; B=32 vs 32-true: ||g - g32|| / ||g32|| 3.0e-3,
-# global norm 4.3e-5, update 7.6e-2 (the first Adam step is ~lr * sign(g): near-zero entries flip; bf16-mixed 0.107)
+# the round-5 GPU measurement (profiles/r05/grads/); the B=32 bounds at measured + 50 % (round 6, VERDICT r5 #4:
+# re-measured unchanged on HEAD, profiles/r06/).  bf16-parity measured: B=4 global norm 3.3e-4, per-tensor norms
+# median 4.3e-4 / max 1.9e-2; B=32 vs 32-true: ||g - g32|| / ||g32|| 2.99e-3, global norm 4.28e-5, update 7.58e-2
+# (the first Adam step is ~lr * sign(g): near-zero entries flip; bf16-mixed 0.107)
 GRAD_NORM_GLOBAL_RTOL = 1e-3
 GRAD_NORM_MEDIAN_RTOL = 1.5e-3
 GRAD_NORM_MAX_RTOL = 6e-2
-B32_GRAD_GLOBAL_RTOL = 1e-2   # ||g - g32|| / ||g32||
-B32_GRAD_NORM_RTOL = 2e-4     # | ||g|| - ||g32|| | / ||g32||
-B32_UPDATE_RTOL = 0.15        # one clip + AdamW step from zero moments
+B32_GRAD_GLOBAL_RTOL = 4.5e-3  # ||g - g32|| / ||g32||
+B32_GRAD_NORM_RTOL = 6.5e-5    # | ||g|| - ||g32|| | / ||g32||
+B32_UPDATE_RTOL = 0.114        # one clip + AdamW step from zero moments
 
 
 def run_precision(model, precision, fn):
@@ -234,3 +235,28 @@ def test_bench_batch_b32_grads_vs_32true(precision):
         assert e["norm_rel_err"] <= B32_GRAD_NORM_RTOL, e
         assert e["update_rel_err"] <= B32_UPDATE_RTOL, e
     assert e["global_rel_err"] < 0.5, e  # one plane: measured, finite and in range
+
+
+def test_bench_batch_b32_grad_error_attribution():
+    """Where the bf16-parity gradient error comes from (matcha/precision.py error_attribution): holding one module
+    family in 32-true removes that family's share.  Measured (round 6, B=32 bench batch): global 2.99e-3; held
+    decoder 1.50e-3 (source 75 %), text encoder 2.60e-3 (24 %), decoder Resnet1D blocks 2.62e-3 (23 %), FeedForward
+    2.81e-3 (12 %), attention 2.83e-3 (10 %) -- diffuse: no family carries a majority but the decoder as a whole."""
+    from matcha.precision import HOLD_FAMILIES, error_attribution, loss_and_grads
+
+    o = _oracle_b32()
+    model = _product(43)
+    b = {k: v.to(DEV) for k, v in o["batch"].items()}
+    t, z = o["t"].to(DEV), o["z"].to(DEV)
+    _, g32, _ = loss_and_grads(model, b, "32-true", t=t, z=z)
+    a = error_attribution(model, b, "bf16-parity", g32, t=t, z=z)
+    print(f"B=32 bf16-parity gradient error attribution: {a}")
+    assert a["global_rel_err"] <= B32_GRAD_GLOBAL_RTOL
+    assert set(a["held"]) == set(HOLD_FAMILIES)
+    assert abs(sum(a["lands_share"].values()) - 1.0) < 1e-3
+    held = {k: v["global_rel_err"] for k, v in a["held"].items()}
+    for fam in HOLD_FAMILIES:  # holding any family in 32-true never makes the error worse (beyond noise)
+        assert held[fam] <= a["global_rel_err"] * 1.02, (fam, held[fam], a["global_rel_err"])
+    assert held["decoder"] <= 0.7 * a["global_rel_err"]  # the decoder's bf16 backward is the largest source
+    sub = sum(a["held"][f]["source_share"] for f in ("decoder_resnets", "decoder_attention", "decoder_ff"))
+    assert sub <= a["held"]["decoder"]["source_share"] + 0.05  # the decoder's parts do not exceed the whole
