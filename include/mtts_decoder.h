@@ -43,7 +43,6 @@ extern "C" {
 
 #define MTTS_CONV_MAX_TAPS 8
 #define MTTS_GEMM_GLDS 32  /* schedule ids 32.. : bf16 LDS-DMA kernels (csrc/conv_gemm_glds.hip)   */
-#define MTTS_GEMM_WLDS 64  /* schedule id 64: bf16 weight-resident kernel, W in LDS, K <= 768 convs / linears (csrc/conv_gemm_wlds.hip) */
 #define MTTS_GEMM_WREG 96  /* schedule id 96: bf16 weight-stationary kernel, K <= 256 linears (csrc/conv_gemm_wreg.hip) */
 
 /*
@@ -110,8 +109,7 @@ typedef struct mtts_conv_gemm_args {
 int mtts_conv_gemm(const mtts_conv_gemm_args *args, int32_t precision, void *hip_stream);
 /* Same, with an explicit schedule: 0..17 = register-staged tile configs (csrc/conv_gemm.hip kCfgs;
  * 8..17 bf16-only: 64-wide K steps, two K steps in flight), MTTS_GEMM_GLDS + i = the bf16 LDS-DMA schedules
- * (csrc/conv_gemm_glds.hip), MTTS_GEMM_WLDS = the weight-resident schedule (csrc/conv_gemm_wlds.hip),
- * MTTS_GEMM_WREG = the weight-stationary schedule (csrc/conv_gemm_wreg.hip), -1 = heuristic.
+ * (csrc/conv_gemm_glds.hip), MTTS_GEMM_WREG = the weight-stationary schedule (csrc/conv_gemm_wreg.hip), -1 = heuristic.
  * For tuning and tests; mtts_conv_gemm picks the configuration itself. */
 int mtts_conv_gemm_tile(const mtts_conv_gemm_args *args, int32_t precision, int32_t tile_cfg, void *hip_stream);
 /* With a caller-owned workspace: lets the bf16 LDS-DMA schedules split K over several workgroups

@@ -1225,7 +1225,7 @@ struct GemmPlan {
 static GemmPlan plan_gemm(const mtts_conv_gemm_args &p, bool bf16, int cfg, int splits) {
     const int M = p.nb * p.To;
     if (cfg < 0) cfg = pick_cfg(p, M, bf16);
-    if (cfg == MTTS_GEMM_WREG || cfg == MTTS_GEMM_WLDS) return {cfg, 1, 0};
+    if (cfg == MTTS_GEMM_WREG) return {cfg, 1, 0};
     splits = pick_splits(p, M, cfg, splits, bf16);
     size_t ws = 0;
     if (cfg >= MTTS_GEMM_GLDS) {
@@ -1260,10 +1260,6 @@ static int resolve_cfg(const mtts_conv_gemm_args &p, bool bf16, int cfg, int M, 
     static const bool wreg_pick = [] { const char *e = getenv("MTTS_GEMM_WREG_PICK"); return !(e && e[0] == '0'); }();
     if (cfg < 0 && bf16 && wreg_pick && mtts::conv_gemm_wreg_applies(p) && mtts::conv_gemm_wreg_preferred(p, M))
         return MTTS_GEMM_WREG;
-    // the weight-resident kernel (W in LDS, loaded once per workgroup; A straight to registers): the decoder's k <= 3
-    // convs and linears with K <= 768 (csrc/conv_gemm_wlds.hip); MTTS_GEMM_WLDS_PICK=1 turns the heuristic's pick on
-    static const bool wlds_pick = [] { const char *e = getenv("MTTS_GEMM_WLDS_PICK"); return e && e[0] == '1'; }();
-    if (cfg < 0 && bf16 && wlds_pick && M >= 4096 && mtts::conv_gemm_wlds_applies(p)) return MTTS_GEMM_WLDS;
     static const bool ws_pick = [] { const char *e = getenv("MTTS_GEMM_WS_PICK"); return !(e && e[0] == '0'); }();
     // (a bf16 A goes to the LDS-DMA pick below: pick_cfg_ws may answer a register-staged schedule)
     if (cfg < 0 && bf16 && ws_pick && (p.flags & MTTS_GEMM_F_W_SPLIT) &&
@@ -1289,7 +1285,6 @@ static int resolve_cfg(const mtts_conv_gemm_args &p, bool bf16, int cfg, int M, 
 static int launch_plan(const mtts_conv_gemm_args &p, bool bf16, const GemmPlan &pl, int M, void *ws, size_t ws_bytes,
                        hipStream_t st) {
     if (pl.cfg == MTTS_GEMM_WREG) return mtts::conv_gemm_wreg_launch(p, M, st);
-    if (pl.cfg == MTTS_GEMM_WLDS) return mtts::conv_gemm_wlds_launch(p, M, st);
     if (pl.cfg >= MTTS_GEMM_GLDS) {
         int s = pl.splits;
         if (pl.ws > 0 && (!ws || ws_bytes < pl.ws || (uintptr_t)ws % 16)) s = 1;  // no workspace: unsplit
@@ -1329,8 +1324,8 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
                        ((p.flags & MTTS_GEMM_F_W_SPLIT) && !(p.flags & MTTS_GEMM_F_A_BF16)),
                    "conv_gemm: a split A needs split weight planes and an fp32 A");
     const bool glds_id = cfg >= MTTS_GEMM_GLDS && cfg < MTTS_GEMM_GLDS + mtts::conv_gemm_glds_num_cfgs();
-    const bool wreg_id = cfg == MTTS_GEMM_WREG, wlds_id = cfg == MTTS_GEMM_WLDS;
-    MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || glds_id || wreg_id || wlds_id,
+    const bool wreg_id = cfg == MTTS_GEMM_WREG;
+    MTTS_CHECK_ARG((cfg >= -1 && cfg < kNumCfgs) || glds_id || wreg_id,
                    "conv_gemm: bad tile config");
     MTTS_CHECK_ARG(splits >= 0, "conv_gemm: bad split count");
     const int M = p.nb * p.To;
@@ -1342,12 +1337,6 @@ static int conv_gemm_impl(const mtts_conv_gemm_args *args, int32_t precision, in
             return mtts::fail(MTTS_ERR_UNSUPPORTED,
                               "conv_gemm: weight-stationary schedule needs bf16, one stride-1 tap, K in {80,160,192,256}");
         return mtts::conv_gemm_wreg_launch(p, M, st);
-    }
-    if (wlds_id) {  // weight-resident schedule, explicit id
-        if (!bf16 || !mtts::conv_gemm_wlds_applies(p))
-            return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: weight-resident schedule needs bf16, 1..3 stride-1 taps, "
-                                                    "K <= 768, whole 64-byte channel chunks, no activation, N % 8 == 0");
-        return mtts::conv_gemm_wlds_launch(p, M, st);
     }
     if (glds_id && (!bf16 || !mtts::conv_gemm_glds_applies(p)))
         return mtts::fail(MTTS_ERR_UNSUPPORTED, "conv_gemm: LDS-DMA schedule needs bf16, cin >= 64 and a 0/1 a_scale");

@@ -39,6 +39,26 @@ using mtts::f32x16;
 
 __device__ uint4 g_zero16 = {0u, 0u, 0u, 0u};  // never written: source of every masked / out-of-range chunk
 
+// -DMTTS_GEMM_TIMELINE=1 (diagnostic builds only, tools/r6/glds_timeline.py): lane 0 of every wave stamps the
+// 100 MHz wall clock into g_tlg ([wave][kTlSlots]: HW ids, start, prologue issued, then per K step: data landed +
+// barrier passed / MFMAs issued, loop end, epilogue end); read back by mtts_glds_timeline_read.
+#ifndef MTTS_GEMM_TIMELINE
+#define MTTS_GEMM_TIMELINE 0
+#endif
+#if MTTS_GEMM_TIMELINE
+constexpr int kTlSlots = 128, kTlWaves = 16384, kTlSteps = 60;
+__device__ long long g_tlg[kTlWaves * kTlSlots];
+#define MTTS_TLG(slot)                                                                                   \
+    do {                                                                                                 \
+        const int tl_w = (int)blockIdx.x * NW + wave;                                                    \
+        if (lane == 0 && tl_w < kTlWaves && (slot) < kTlSlots) g_tlg[tl_w * kTlSlots + (slot)] = wall_clock64(); \
+    } while (0)
+#else
+#define MTTS_TLG(slot) \
+    do {               \
+    } while (0)
+#endif
+
 constexpr int kBK = 64;
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
@@ -379,16 +399,33 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
         }
     };
 
+#if MTTS_GEMM_TIMELINE
+    if (lane == 0 && (int)blockIdx.x * NW + wave < kTlWaves)
+        g_tlg[((int)blockIdx.x * NW + wave) * kTlSlots] =
+            ((long long)__smid() << 32) | (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    MTTS_TLG(1);
+#endif
     // prologue: steps 0 .. STAGES-2 in flight (steps past nk DMA zeros into their buffer: harmless)
     issue(std::integral_constant<int, 0>{});
     if constexpr (STAGES > 2) issue(std::integral_constant<int, 1>{});
+    MTTS_TLG(2);
     // step kt uses buffer kt % STAGES and refills buffer (kt + STAGES - 1) % STAGES, which step kt-1 read
+    int tl_k = 0;
+    (void)tl_k;
     auto step = [&](auto S) {
         constexpr int cur = decltype(S)::value, nxt = (cur + STAGES - 1) % STAGES;
         wait_vmcnt<(GA + GW) * (STAGES - 2)>();  // this wave's DMAs for step kt have landed
         mtts::lds_barrier();                       // ... everyone's, and step kt-1's reads are done
+#if MTTS_GEMM_TIMELINE
+        if (tl_k < kTlSteps) MTTS_TLG(3 + 2 * tl_k);
+#endif
         issue(std::integral_constant<int, nxt>{});
         compute(S);
+#if MTTS_GEMM_TIMELINE
+        __builtin_amdgcn_sched_barrier(0);
+        if (tl_k < kTlSteps) MTTS_TLG(4 + 2 * tl_k);
+        ++tl_k;
+#endif
     };
     for (int kt = 0; kt < nk; kt += STAGES) {
         step(std::integral_constant<int, 0>{});
@@ -400,6 +437,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
         }
     }
     wait_vmcnt<0>();  // no DMA may still target this workgroup's LDS when it retires
+    MTTS_TLG(kTlSlots - 2);
     if (part || mtts::gemm_epilogue_vec_ok(p)) {
         mtts::lds_barrier();  // every wave is past its last fragment read: the buffers are free
         unsigned char *stage = wave % 4 == 0 ? sA0 : wave % 4 == 1 ? sW0 : wave % 4 == 2 ? sA1 : sW1;
@@ -412,6 +450,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_gemm_glds_kernel(mtts_conv_
     } else {
         mtts::gemm_epilogue<TM, TN>(p, acc, m0 + wr * 32 * TM, n0 + wc * 32 * TN, lr, lh);
     }
+    MTTS_TLG(kTlSlots - 1);
 }
 
 // Split-K combine: out = epilogue(sum_s part[s][m][n..n+3]) summed in split order (deterministic).
@@ -579,5 +618,18 @@ int splitk_combine(const mtts_conv_gemm_args &p, int M, const float *part, int S
 int conv_gemm_glds_launch(int id, const mtts_conv_gemm_args &p, int M, int splits, float *part, hipStream_t st) {
     return launch_glds_id(id, p, M, splits, part, st, std::make_integer_sequence<int, kNumGlds>{});
 }
-
 }  // namespace mtts
+
+#if MTTS_GEMM_TIMELINE
+// diagnostic builds: copy (or zero, host == NULL) the LDS-DMA kernels' timeline buffer; returns its size in bytes
+extern "C" long long mtts_glds_timeline_read(void *host) {
+    const size_t bytes = sizeof(long long) * kTlWaves * kTlSlots;
+    if (host) {
+        if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tlg), bytes) != hipSuccess) return -1;
+    } else {
+        void *d = nullptr;
+        if (hipGetSymbolAddress(&d, HIP_SYMBOL(g_tlg)) != hipSuccess || hipMemset(d, 0, bytes) != hipSuccess) return -1;
+    }
+    return (long long)bytes;
+}
+#endif

@@ -10,5 +10,5 @@ tail -2 $O/smoke.log
 timeout -k 10 700 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench rc=$?"; tail -20 $O/bench.err; exit 1; }
 python tools/r5/bench_summary.py $O/bench.json > $O/summary.txt; head -5 $O/summary.txt
 MTTS_BENCH_SHARED_GPU=1 timeout -k 10 400 python bench.py --gpus 2 --steps 6 --warmup 2 --no-synth > $O/bench_shared2.json 2> $O/bench_shared2.err; rc=$?
-echo "shared-gpu 2-rank bench rc=$rc"; tail -c 1500 $O/bench_shared2.json | python -c "import json,sys; s=sys.stdin.read(); d=json.loads(s[s.index('{'):]); print(json.dumps(d['dp']))" || tail -20 $O/bench_shared2.err
+echo "shared-gpu 2-rank bench rc=$rc"; python -c "import json,sys; s=open(sys.argv[1]).read(); d=json.loads(s[s.index('{'):]); print(json.dumps(d['dp']))" $O/bench_shared2.json || tail -20 $O/bench_shared2.err
 exit $rc
