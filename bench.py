@@ -733,7 +733,7 @@ def main():
             "roofline_attn": roofline_attn,
             "graph_replay_profile": gprof,
             "extra_configs": extra,
-            "roofline_mas": {"kernel": "mas_transpose_kernel + mas_dp_kernel + mas_expand_kernel (maximum_path)",
+            "roofline_mas": {"kernel": "mas_transpose_kernel + mas_dp_kernel (Tx <= 256) / mas_dp_mw_kernel + mas_expand_kernel (maximum_path)",
                              "bound": "hbm",
                              "achieved": round(mas_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(mas_gbs / HBM_PEAK_GBS, 4), "traffic": mas_traffic[0],

@@ -54,6 +54,7 @@ struct MasArgs {
     int premasked;
     float neg;
     int tr_ld;  // > 0: `value` is the premasked lattice TRANSPOSED, [B][Ty][tr_ld] (x contiguous; tr_ld = Txp)
+    int bt_bufs;  // multi-wave kernel, global-bits mode: backtrack slot buffers in LDS (2, 1; 0: walk from global)
 };
 
 // K consecutive floats at p (the text rows x0 .. x0+K-1 of one column of a transposed lattice): one wave
@@ -127,6 +128,20 @@ __device__ __forceinline__ float cell_tr(float fp, float dp, float sc, int d, un
     const float v = __builtin_amdgcn_fmed3f(fp, fs, INFINITY) + sc;
     const bool band = (unsigned)d <= span;
     return __builtin_amdgcn_fmed3f(v, band ? -INFINITY : neg, band ? INFINITY : neg);
+}
+
+// R = 2 R + (fp >= fs): the backpointer bit shifted in by v_cmp + v_addc (the compiler builds it from a cndmask, an or
+// and a shift per column pair)
+__device__ __forceinline__ void shift_in_ge(uint32_t &R, float fp, float fs) {
+    asm("v_cmp_ge_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc" : "+v"(R) : "v"(fp), "v"(fs) : "vcc");
+}
+
+// max(a, b) as one v_max_f32: the compiler lowers fmaxf / a med3 against +inf to a canonicalising v_max_f32 x, x per
+// operand first (IEEE mode), an extra instruction on the column chain; the DP's operands are never NaN
+__device__ __forceinline__ float vmax_raw(float a, float b) {
+    float r;
+    asm("v_max_f32_e32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 
 template <int B, int E, class F>
@@ -422,8 +437,18 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
 // the chain per column shrinks from K = Tx/64 rows per lane (one wave) to KL (e.g. Tx = 512: 8 -> 1)
 // at the price of one barrier per 32 columns and W - 1 fill phases.  The backtrack is mas_dp_kernel's
 // (wave 0), with the next backpointer word column prefetched while the current one is walked.
+// MTTS_MAS_STAMPS (the probe harness tools/r6/mas_probe.py only, never the product): block b's thread 0 writes the
+// 100 MHz clock at kernel start, after the forward DP and after the backtrack to mas_probe_stamps[b][0..2]
+#ifdef MTTS_MAS_STAMPS
+__device__ long long mas_probe_stamps[4096 * 4];
+#define MAS_STAMP(i) \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) mas_probe_stamps[blockIdx.x * 4 + (i)] = wall_clock64()
+#else
+#define MAS_STAMP(i)
+#endif
 template <int KL, int W, bool PM, bool VEC, bool LDS_BITS, bool DP_OUT, bool TR = false>
 __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
+    MAS_STAMP(0);
     static_assert(!TR || (PM && !DP_OUT), "the transposed lattice is premasked, and dp_out is row-major");
     constexpr int CC = 32;       // columns per chunk (one backpointer word)
     constexpr int C = CC / KL;   // columns per ring sub-chunk: KL * C = 32 cells per lane
@@ -490,9 +515,33 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
         constexpr int RING = PM ? 3 : 2;
         constexpr int MD = PM ? 1 : RING;
         float vbuf[RING][KL][C], mbuf[MD][KL][C];
+        // TR, KL <= 2 rows per lane: buffer loads -- the column offset a wave-uniform scalar advanced by the column
+        // stride, the lane's rows a fixed vector offset, columns past Ty out of the descriptor's range (zeros: they feed
+        // nothing the backtrack reads) -- one scalar add and KL loads per column; the clamped 64-bit vector address of
+        // the first version took ~6 issue slots per column of the issue-bound chain.  KL >= 4: float4 global loads.
+        constexpr bool TRB = TR && KL <= 2;
+        const auto tr_rsrc = [&] {
+            if constexpr (TRB)
+                return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.value + (size_t)b * Ty * a.tr_ld), 0,
+                                                         (int)((size_t)Ty * a.tr_ld * 4), 0x00020000);
+            else
+                return 0;
+        }();
+        const int tr_lane = x0 * 4, tr_ld4 = a.tr_ld * 4;
         auto load_sub = [&](auto slot, int y0) {
             constexpr int sl = decltype(slot)::value;
-            if constexpr (TR) {  // column-major: one KL-row vector per column
+            if constexpr (TRB) {
+                int soff = y0 * tr_ld4;
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+#pragma unroll
+                    for (int i = 0; i < KL; ++i)
+                        vbuf[sl][i][j] = __builtin_bit_cast(
+                            float, __builtin_amdgcn_raw_buffer_load_b32(tr_rsrc, tr_lane + 4 * i, soff, 0));
+                    soff += tr_ld4;
+                }
+                return;
+            } else if constexpr (TR) {  // column-major: one KL-row vector per column
 #pragma unroll
                 for (int j = 0; j < C; ++j) {
                     float col[KL];
@@ -517,6 +566,32 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
         auto chunk = [&](auto phase3, int c) {
             constexpr int P = decltype(phase3)::value;
             const int r3 = c % 3, p3 = (c + 2) % 3;
+            // TR: the lane-0 neighbours of the whole chunk, read once (broadcast ds_read_b128: every lane the same
+            // address) -- column y needs the previous wave's last row after column y - 1 (ring slot of chunk c, or of
+            // chunk c - 1 for the chunk's first column); wave 0 has none (0 before column 0, else max_neg_val)
+            float nbc[TR ? CC : 1];
+            float eoc[TR ? CC : 1];
+            if constexpr (TR) {
+                if (wave == 0) {
+#pragma unroll
+                    for (int j = 0; j < CC; ++j) nbc[j] = (c == 0 && j == 0) ? 0.0f : neg;
+                } else {
+                    const float4 *src = reinterpret_cast<const float4 *>(ein + r3 * W * CC);
+#pragma unroll
+                    for (int q = 0; q < CC / 4 - 1; ++q) {
+                        const float4 v = src[q];
+                        nbc[4 * q + 1] = v.x;
+                        nbc[4 * q + 2] = v.y;
+                        nbc[4 * q + 3] = v.z;
+                        nbc[4 * q + 4] = v.w;
+                    }
+                    const float4 v = src[CC / 4 - 1];
+                    nbc[CC - 3] = v.x;
+                    nbc[CC - 2] = v.y;
+                    nbc[CC - 1] = v.z;
+                    nbc[0] = c == 0 ? neg : edge[(p3 * W) * CC + (wave - 1) * CC + CC - 1];
+                }
+            }
             static_for<0, KL>([&](auto sv) {
                 constexpr int s = decltype(sv)::value;
                 constexpr int sl = (P * KL + s) % RING;
@@ -528,6 +603,10 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
 #pragma unroll
                 for (int j = 0; j < C; ++j) {
                     const int jc = s * C + j;  // column within the chunk
+                    if constexpr (TR) {
+                        nbl[j] = nbc[jc];
+                        continue;
+                    }
                     const int y = y0 + j;
                     // read unconditionally (wave 0 reads a valid slot and ignores it): selects, no branches
                     const float prev = jc == 0 ? edge[(p3 * W) * CC + (wave > 0 ? wave - 1 : 0) * CC + CC - 1]
@@ -551,9 +630,14 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
                             if constexpr (PM) sc = vbuf[sl][i][j];
                             else sc = vbuf[sl][i][j] * mbuf[sl][i][j];  // __init__.py:45
                             const float fp = i == 0 ? nb : dp[i - 1], fs = dp[i];
-                            const bool diag = fp >= fs;
-                            ndp[i] = (TR ? __builtin_amdgcn_fmed3f(fp, fs, INFINITY) : (diag ? fp : fs)) + sc;
-                            R[i] = (R[i] << 1) | (diag ? 1u : 0u);
+                            if constexpr (TR) {
+                                ndp[i] = vmax_raw(fp, fs) + sc;
+                                shift_in_ge(R[i], fp, fs);
+                            } else {
+                                const bool diag = fp >= fs;
+                                ndp[i] = (diag ? fp : fs) + sc;
+                                R[i] = (R[i] << 1) | (diag ? 1u : 0u);
+                            }
                         }
 #pragma unroll
                         for (int i = 0; i < KL; ++i) dp[i] = ndp[i];
@@ -615,11 +699,22 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
                         eo[j] = dp[KL - 1];
                     }
                 }
-                if (lane == 63) {
+                if constexpr (TR) {
+#pragma unroll
+                    for (int j = 0; j < C; ++j) eoc[s * C + j] = eo[j];
+                } else if (lane == 63) {
 #pragma unroll
                     for (int j = 0; j < C; ++j) eout[r3 * W * CC + s * C + j] = eo[j];
                 }
             });
+            if constexpr (TR) {
+                if (lane == 63) {
+                    float4 *dst = reinterpret_cast<float4 *>(eout + r3 * W * CC);
+#pragma unroll
+                    for (int q = 0; q < CC / 4; ++q)
+                        dst[q] = make_float4(eoc[4 * q], eoc[4 * q + 1], eoc[4 * q + 2], eoc[4 * q + 3]);
+                }
+            }
             // the chunk's backpointer word per row (a partial last chunk left-aligned like mas_dp_kernel's)
             const int sh = (!TR && c == nchunks - 1 && (t_y & 31)) ? 32 - (t_y & 31) : 0;  // TR: all 32 columns ran
 #pragma unroll
@@ -649,37 +744,78 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
     if constexpr (!LDS_BITS) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     if constexpr (!LDS_BITS) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    MAS_STAMP(1);
 
-    if (valid && wave == 0) {
-        // backtrack (mas_dp_kernel's walk): registers hold one word column slot-major, W[r] lane l = row
-        // r*64 + l; in global-bits mode the next column (c - 1) is requested while column c is walked
-        int idx = t_x - 1;
-        int y = t_y - 1;
-        int cur_c = -1;
-        uint32_t Wc[KB], Wn[LDS_BITS ? 1 : KB];
-        bool have_next = false;
+    if constexpr (LDS_BITS) {
+        if (valid && wave == 0) {
+            // backtrack (mas_dp_kernel's walk): registers hold one word column slot-major, W[r] lane l = row r*64 + l
+            int idx = t_x - 1;
+            int y = t_y - 1;
+            int cur_c = -1;
+            uint32_t Wc[KB];
 #pragma unroll
-        for (int r = 0; r < KB; ++r) Wc[r] = 0u;
-        bool done = false;
+            for (int r = 0; r < KB; ++r) Wc[r] = 0u;
+            bool done = false;
 #pragma unroll
-        for (int r = KB - 1; r >= 0; --r) {
-            while (!done && idx >= kWave * r) {
-                if (idx == 0) {
-                    if (lane == 0) rs[0] = 0;
-                    done = true;
-                    break;
-                }
-                if (idx >= y) {
-                    for (int x = lane; x <= idx; x += kWave) rs[x] = x;
-                    done = true;
-                    break;
-                }
-                const int c = y >> 5;
-                if (c != cur_c) {
-                    if constexpr (LDS_BITS) {
+            for (int r = KB - 1; r >= 0; --r) {
+                while (!done && idx >= kWave * r) {
+                    if (idx == 0) {
+                        if (lane == 0) rs[0] = 0;
+                        done = true;
+                        break;
+                    }
+                    if (idx >= y) {
+                        for (int x = lane; x <= idx; x += kWave) rs[x] = x;
+                        done = true;
+                        break;
+                    }
+                    const int c = y >> 5;
+                    if (c != cur_c) {
 #pragma unroll
                         for (int rr = 0; rr < KB; ++rr) Wc[rr] = bits_l[c * Txp + rr * kWave + lane];
+                        cur_c = c;
+                    }
+                    const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)Wc[r], idx & (kWave - 1));
+                    const int base = c << 5;
+                    uint32_t m = word & (0xFFFFFFFFu << (31 - (y - base)));
+                    if (idx >= base) m &= 0xFFFFFFFFu >> (idx - base);
+                    int ydec;
+                    if (m) {
+                        ydec = base + 31 - __builtin_ctz(m);
+                    } else if (idx >= base) {
+                        ydec = idx;
                     } else {
+                        y = base - 1;
+                        continue;
+                    }
+                    if (lane == 0) rs[idx] = ydec;
+                    idx -= 1;
+                    y = ydec - 1;
+                }
+            }
+        }
+    } else if (valid && a.bt_bufs == 0) {
+        if (wave == 0) {
+            // backtrack from global bits (a Ty too long for the LDS slot buffers below): registers hold one word column
+            // slot-major, W[r] lane l = row r*64 + l; the next column (c - 1) is requested while column c is walked
+            int idx = t_x - 1;
+            int y = t_y - 1;
+            int cur_c = -1;
+            uint32_t Wc[KB], Wn[KB];
+            bool have_next = false;
+#pragma unroll
+            for (int r = 0; r < KB; ++r) Wc[r] = 0u;
+            bool done = false;
+#pragma unroll
+            for (int r = KB - 1; r >= 0; --r) {
+                while (!done && idx >= kWave * r) {
+                    if (idx == 0 || idx >= y) {
+                        for (int x = lane; x <= idx; x += kWave) rs[x] = x;
+                        done = true;
+                        break;
+                    }
+                    const int c = y >> 5;
+                    if (c != cur_c) {
                         if (have_next && c == cur_c - 1) {
 #pragma unroll
                             for (int rr = 0; rr < KB; ++rr) Wc[rr] = Wn[rr];
@@ -691,29 +827,89 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
                         const int cn = c > 0 ? c - 1 : 0;
 #pragma unroll
                         for (int rr = 0; rr < KB; ++rr) Wn[rr] = bits_g[(size_t)cn * Txp + rr * kWave + lane];
+                        cur_c = c;
                     }
-                    cur_c = c;
+                    const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)Wc[r], idx & (kWave - 1));
+                    const int base = c << 5;
+                    uint32_t m = word & (0xFFFFFFFFu << (31 - (y - base)));
+                    if (idx >= base) m &= 0xFFFFFFFFu >> (idx - base);
+                    int ydec;
+                    if (m) {
+                        ydec = base + 31 - __builtin_ctz(m);
+                    } else if (idx >= base) {
+                        ydec = idx;
+                    } else {
+                        y = base - 1;
+                        continue;
+                    }
+                    if (lane == 0) rs[idx] = ydec;
+                    idx -= 1;
+                    y = ydec - 1;
                 }
-                const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)Wc[r], idx & (kWave - 1));
-                const int base = c << 5;
-                uint32_t m = word & (0xFFFFFFFFu << (31 - (y - base)));
-                if (idx >= base) m &= 0xFFFFFFFFu >> (idx - base);
-                int ydec;
-                if (m) {
-                    ydec = base + 31 - __builtin_ctz(m);
-                } else if (idx >= base) {
-                    ydec = idx;
-                } else {
-                    y = base - 1;
-                    continue;
-                }
-                if (lane == 0) rs[idx] = ydec;
-                idx -= 1;
-                y = ydec - 1;
             }
+        }
+    } else if (valid) {
+        // backtrack, global-bits mode (round 6): the walk of row slot r (rows 64 r .. 64 r + 63) reads only that slot's
+        // word of each column, so the slot's words of all columns are copied into LDS (nch x 256 B, coalesced) and wave 0
+        // walks them from there -- with two buffers the other waves copy slot r - 1 while wave 0 walks slot r.  The
+        // first version loaded all KB words of a column from HBM / L2 whenever the walk entered it, one column ahead.
+        const int nbuf = a.bt_bufs;
+        const int slot_words = a.nch * kWave;
+        int idx = t_x - 1;
+        int y = t_y - 1;
+        int cur_c = -1;
+        uint32_t Wc = 0u;  // lane l: the word of row 64 r + l in column cur_c (one LDS read per column change)
+        bool done = false;
+        const int r0 = (t_x - 1) / kWave;
+        auto copy_slot = [&](int r, int t0, int nt) {
+            uint32_t *dst = bits_l + (nbuf == 2 ? (r & 1) * slot_words : 0);
+            for (int i = t0; i < slot_words; i += nt) dst[i] = bits_g[(size_t)(i >> 6) * Txp + r * kWave + (i & (kWave - 1))];
+        };
+        if (nbuf == 2) copy_slot(r0, threadIdx.x, 64 * W);
+#pragma unroll 1
+        for (int r = r0; r >= 0; --r) {  // block-uniform
+            cur_c = -1;
+            if (nbuf == 1) {
+                __syncthreads();  // the previous slot's walk has finished reading the buffer
+                copy_slot(r, threadIdx.x, 64 * W);
+            }
+            __syncthreads();  // slot r is in LDS
+            const uint32_t *slot = bits_l + (nbuf == 2 ? (r & 1) * slot_words : 0);
+            if (wave == 0) {
+                // the slot's row starts gather in lane (row & 63) of rsv (a lane select) and go to LDS once per slot; the
+                // step's decisions are selects, not branches (the first version spent ~40 scalar instructions and six
+                // branches per row step)
+                int rsv = -1;
+                while (!done && idx >= kWave * r) {
+                    if (idx == 0 || idx >= y) {  // the rest of the path is the diagonal x == y (or row 0 at column 0)
+                        for (int x = lane; x <= idx; x += kWave) rs[x] = x;
+                        done = true;
+                        break;
+                    }
+                    const int c = y >> 5;
+                    if (c != cur_c) {
+                        Wc = slot[c * kWave + lane];
+                        cur_c = c;
+                    }
+                    const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)Wc, idx & (kWave - 1));
+                    const int base = c << 5;
+                    const uint32_t m = word & (0xFFFFFFFFu << (31 - (y - base))) &
+                                       (idx >= base ? 0xFFFFFFFFu >> (idx - base) : 0xFFFFFFFFu);
+                    const bool found = m != 0u || idx >= base;
+                    const int ydec = m ? base + 31 - __builtin_ctz(m) : idx;
+                    rsv = (found && lane == (idx & (kWave - 1))) ? ydec : rsv;
+                    y = found ? ydec - 1 : base - 1;
+                    idx = found ? idx - 1 : idx;
+                }
+                if (rsv >= 0) rs[r * kWave + lane] = rsv;
+            } else if (nbuf == 2 && r > 0) {
+                copy_slot(r - 1, threadIdx.x - 64, 64 * (W - 1));  // beside the walk
+            }
+            if (nbuf == 2) __syncthreads();  // slot r - 1 copied; slot r's buffer is free for slot r - 2
         }
     }
     __syncthreads();
+    MAS_STAMP(2);
     int32_t *rs_out = a.row_start + (size_t)b * Tx;
     for (int x = threadIdx.x; x < Tx; x += 64 * W) rs_out[x] = rs[x];
 }
@@ -1114,11 +1310,32 @@ WsLayout ws_layout(int B, int Tx, int Ty, bool with_lat = false, bool shape_over
     return w;
 }
 
+// dynamic LDS past 64 KiB needs the kernel attribute (a long Ty's backtrack slot copy: nch x 256 B)
+constexpr size_t kMwLdsMax = 160 * 1024;
+// global-bits mode: as many backtrack slot buffers (nch x 256 B each, at most 2) as the LDS holds beside `shmem`;
+// sets a.bt_bufs and returns the launch's LDS bytes
+size_t mw_backtrack_bufs(MasArgs &a, size_t shmem) {
+    const size_t slot = (size_t)a.nch * kWave * 4;
+    a.bt_bufs = shmem + 2 * slot <= kMwLdsMax ? 2 : shmem + slot <= kMwLdsMax ? 1 : 0;
+    return shmem + a.bt_bufs * slot;
+}
+template <typename K>
+bool mw_lds_attr(K kernel, size_t bytes) {
+    if (bytes <= 64 * 1024) return true;
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bytes) == hipSuccess;
+}
+
 template <int KL, int W, bool PM>
-int launch_dp_mw(const MasArgs &a, int B, bool vec, bool lds_bits, bool dp_out, size_t shmem, hipStream_t st) {
+int launch_dp_mw(MasArgs a, int B, bool vec, bool lds_bits, bool dp_out, size_t shmem, hipStream_t st) {
     dim3 grid(B), block(64 * W);
-#define MTTS_MAS_MW_LAUNCH(V, L, DO) \
-    hipLaunchKernelGGL((mas_dp_mw_kernel<KL, W, PM, V, L, DO && PM>), grid, block, shmem, st, a)
+    if (!lds_bits) shmem = mw_backtrack_bufs(a, shmem);
+#define MTTS_MAS_MW_LAUNCH(V, L, DO)                                                                  \
+    do {                                                                                              \
+        if (!mw_lds_attr(mas_dp_mw_kernel<KL, W, PM, V, L, DO && PM>, shmem))                         \
+            return mtts::fail(MTTS_ERR_HIP, "maximum_path: LDS attribute");                           \
+        hipLaunchKernelGGL((mas_dp_mw_kernel<KL, W, PM, V, L, DO && PM>), grid, block, shmem, st, a); \
+    } while (0)
     if (vec) {
         if (lds_bits) {
             if (dp_out) MTTS_MAS_MW_LAUNCH(true, true, true); else MTTS_MAS_MW_LAUNCH(true, true, false);
@@ -1192,11 +1409,17 @@ int launch_dp_kc(const MasArgs &a, int B, bool vec, bool lds_bits, bool dp_out, 
 }
 
 template <int KL, int W>
-int launch_dp_mw_tr(const MasArgs &a, int B, bool lds_bits, size_t shmem, hipStream_t st) {
-    if (lds_bits)
+int launch_dp_mw_tr(MasArgs a, int B, bool lds_bits, size_t shmem, hipStream_t st) {
+    if (!lds_bits) shmem = mw_backtrack_bufs(a, shmem);
+    if (lds_bits) {
+        if (!mw_lds_attr(mas_dp_mw_kernel<KL, W, true, false, true, false, true>, shmem))
+            return mtts::fail(MTTS_ERR_HIP, "maximum_path: LDS attribute");
         hipLaunchKernelGGL((mas_dp_mw_kernel<KL, W, true, false, true, false, true>), dim3(B), dim3(64 * W), shmem, st, a);
-    else
+    } else {
+        if (!mw_lds_attr(mas_dp_mw_kernel<KL, W, true, false, false, false, true>, shmem))
+            return mtts::fail(MTTS_ERR_HIP, "maximum_path: LDS attribute");
         hipLaunchKernelGGL((mas_dp_mw_kernel<KL, W, true, false, false, false, true>), dim3(B), dim3(64 * W), shmem, st, a);
+    }
     return mtts::check_launch("mas_dp_mw_kernel");
 }
 
