@@ -370,6 +370,9 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
         // Row idx occupies columns [ydec, y]; ydec = the highest column <= y whose diagonal bit is
         // set, or idx itself (forced diagonal at x == y, core.pyx:91).  Registers hold one chunk of
         // words slot-major: W[r] lane l = row r*64 + l, so the row select is static per r-segment.
+        // Round 6: the step's decisions are selects (the branchy first version spent ~40 scalar instructions and six
+        // branches per row step -- ~20 us of the B = 32, 120 x 600 kernel), and a segment's row starts gather in lane
+        // (row & 63) of rsv, written to LDS once per segment.
         int idx = t_x - 1;
         int y = t_y - 1;
         int cur_c = -1;
@@ -379,13 +382,11 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
         bool done = false;
 #pragma unroll
         for (int r = K - 1; r >= 0; --r) {
+            int rsv = -1;
             while (!done && idx >= kWave * r) {
-                if (idx == 0) {  // row 0 runs down to column 0 (core.pyx:89-91: idx > 0 test)
-                    if (lane == 0) rs[0] = 0;
-                    done = true;
-                    break;
-                }
-                if (idx >= y) {  // on the diagonal: every remaining step is forced
+                // row 0 runs down to column 0 (core.pyx:89-91: idx > 0 test); on the diagonal every remaining step is
+                // forced
+                if (idx == 0 || idx >= y) {
                     for (int x = lane; x <= idx; x += kWave) rs[x] = x;
                     done = true;
                     break;
@@ -404,21 +405,16 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
                 }
                 const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)W[r], idx & (kWave - 1));
                 const int base = c << 5;
-                uint32_t m = word & (0xFFFFFFFFu << (31 - (y - base)));  // columns <= y
-                if (idx >= base) m &= 0xFFFFFFFFu >> (idx - base);       // columns >= idx (in band)
-                int ydec;
-                if (m) {
-                    ydec = base + 31 - __builtin_ctz(m);
-                } else if (idx >= base) {
-                    ydec = idx;
-                } else {
-                    y = base - 1;
-                    continue;
-                }
-                if (lane == 0) rs[idx] = ydec;
-                idx -= 1;
-                y = ydec - 1;
+                // columns <= y, and >= idx (in band) when the row's diagonal lies in this word
+                const uint32_t m = word & (0xFFFFFFFFu << (31 - (y - base))) &
+                                   (idx >= base ? 0xFFFFFFFFu >> (idx - base) : 0xFFFFFFFFu);
+                const bool found = m != 0u || idx >= base;  // else: the run continues in the previous word
+                const int ydec = m ? base + 31 - __builtin_ctz(m) : idx;
+                rsv = (found && lane == (idx & (kWave - 1))) ? ydec : rsv;
+                y = found ? ydec - 1 : base - 1;
+                idx = found ? idx - 1 : idx;
             }
+            if (rsv >= 0) rs[r * kWave + lane] = rsv;
         }
     }
     __syncthreads();
@@ -758,13 +754,9 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
             bool done = false;
 #pragma unroll
             for (int r = KB - 1; r >= 0; --r) {
+                int rsv = -1;  // the segment's row starts, lane (row & 63); selects per step (mas_dp_kernel's walk)
                 while (!done && idx >= kWave * r) {
-                    if (idx == 0) {
-                        if (lane == 0) rs[0] = 0;
-                        done = true;
-                        break;
-                    }
-                    if (idx >= y) {
+                    if (idx == 0 || idx >= y) {
                         for (int x = lane; x <= idx; x += kWave) rs[x] = x;
                         done = true;
                         break;
@@ -777,21 +769,15 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
                     }
                     const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)Wc[r], idx & (kWave - 1));
                     const int base = c << 5;
-                    uint32_t m = word & (0xFFFFFFFFu << (31 - (y - base)));
-                    if (idx >= base) m &= 0xFFFFFFFFu >> (idx - base);
-                    int ydec;
-                    if (m) {
-                        ydec = base + 31 - __builtin_ctz(m);
-                    } else if (idx >= base) {
-                        ydec = idx;
-                    } else {
-                        y = base - 1;
-                        continue;
-                    }
-                    if (lane == 0) rs[idx] = ydec;
-                    idx -= 1;
-                    y = ydec - 1;
+                    const uint32_t m = word & (0xFFFFFFFFu << (31 - (y - base))) &
+                                       (idx >= base ? 0xFFFFFFFFu >> (idx - base) : 0xFFFFFFFFu);
+                    const bool found = m != 0u || idx >= base;
+                    const int ydec = m ? base + 31 - __builtin_ctz(m) : idx;
+                    rsv = (found && lane == (idx & (kWave - 1))) ? ydec : rsv;
+                    y = found ? ydec - 1 : base - 1;
+                    idx = found ? idx - 1 : idx;
                 }
+                if (rsv >= 0) rs[r * kWave + lane] = rsv;
             }
         }
     } else if (valid && a.bt_bufs == 0) {
