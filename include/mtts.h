@@ -61,7 +61,9 @@ const char *mtts_last_error(void);
 #define MTTS_MAS_NO_DENSE_PATH 0x2   /* only row_start_out/lengths_out: do not write `path`    */
 
 /* Maximum text length (Tx) the kernels accept. */
-#define MTTS_MAS_MAX_TX 4096 /* 8 waves x 8 text rows per lane of the multi-wave DP (round 4; 2048 with MTTS_MAS_MW=0) */
+#define MTTS_MAS_MAX_TX 8192 /* maximum_path / the fused prior path (transposed lattice): 8 waves x 16 text rows per lane of
+                                the multi-wave DP (round 6; 4096 in rounds 4-5; 2048 with MTTS_MAS_MW=0) */
+#define MTTS_MAS_MAX_TX_ROW_MAJOR 4096 /* mtts_compute_batch_alignments (the row-major lattice it mutates): 8 x 8 rows */
 
 /* Bytes of device workspace mtts_maximum_path_f32 / mtts_compute_batch_alignments need. */
 size_t mtts_maximum_path_workspace_size(int32_t B, int32_t Tx, int32_t Ty);

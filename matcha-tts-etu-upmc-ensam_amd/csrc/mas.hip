@@ -782,18 +782,16 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
         }
     } else if (valid && a.bt_bufs == 0) {
         if (wave == 0) {
-            // backtrack from global bits (a Ty too long for the LDS slot buffers below): registers hold one word column
-            // slot-major, W[r] lane l = row r*64 + l; the next column (c - 1) is requested while column c is walked
+            // backtrack from global bits (a Ty too long for the LDS slot buffers below): lane l holds the word of row
+            // 64 r + l in column cur_c, loaded when the walk enters the column (latency-bound, but registers independent
+            // of KL: the round-5 walk held all KB words of a column, 2 x 128 registers at KL = 16)
             int idx = t_x - 1;
             int y = t_y - 1;
-            int cur_c = -1;
-            uint32_t Wc[KB], Wn[KB];
-            bool have_next = false;
-#pragma unroll
-            for (int r = 0; r < KB; ++r) Wc[r] = 0u;
             bool done = false;
-#pragma unroll
-            for (int r = KB - 1; r >= 0; --r) {
+#pragma unroll 1
+            for (int r = (t_x - 1) / kWave; r >= 0; --r) {
+                int cur_c = -1, rsv = -1;
+                uint32_t Wc = 0u;
                 while (!done && idx >= kWave * r) {
                     if (idx == 0 || idx >= y) {
                         for (int x = lane; x <= idx; x += kWave) rs[x] = x;
@@ -802,36 +800,20 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
                     }
                     const int c = y >> 5;
                     if (c != cur_c) {
-                        if (have_next && c == cur_c - 1) {
-#pragma unroll
-                            for (int rr = 0; rr < KB; ++rr) Wc[rr] = Wn[rr];
-                        } else {
-#pragma unroll
-                            for (int rr = 0; rr < KB; ++rr) Wc[rr] = bits_g[(size_t)c * Txp + rr * kWave + lane];
-                        }
-                        have_next = c > 0;
-                        const int cn = c > 0 ? c - 1 : 0;
-#pragma unroll
-                        for (int rr = 0; rr < KB; ++rr) Wn[rr] = bits_g[(size_t)cn * Txp + rr * kWave + lane];
+                        Wc = bits_g[(size_t)c * Txp + r * kWave + lane];
                         cur_c = c;
                     }
-                    const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)Wc[r], idx & (kWave - 1));
+                    const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)Wc, idx & (kWave - 1));
                     const int base = c << 5;
-                    uint32_t m = word & (0xFFFFFFFFu << (31 - (y - base)));
-                    if (idx >= base) m &= 0xFFFFFFFFu >> (idx - base);
-                    int ydec;
-                    if (m) {
-                        ydec = base + 31 - __builtin_ctz(m);
-                    } else if (idx >= base) {
-                        ydec = idx;
-                    } else {
-                        y = base - 1;
-                        continue;
-                    }
-                    if (lane == 0) rs[idx] = ydec;
-                    idx -= 1;
-                    y = ydec - 1;
+                    const uint32_t m = word & (0xFFFFFFFFu << (31 - (y - base))) &
+                                       (idx >= base ? 0xFFFFFFFFu >> (idx - base) : 0xFFFFFFFFu);
+                    const bool found = m != 0u || idx >= base;
+                    const int ydec = m ? base + 31 - __builtin_ctz(m) : idx;
+                    rsv = (found && lane == (idx & (kWave - 1))) ? ydec : rsv;
+                    y = found ? ydec - 1 : base - 1;
+                    idx = found ? idx - 1 : idx;
                 }
+                if (rsv >= 0) rs[r * kWave + lane] = rsv;
             }
         }
     } else if (valid) {
@@ -1257,7 +1239,7 @@ WsLayout ws_layout(int B, int Tx, int Ty, bool with_lat = false, bool shape_over
     // lane, bounds both
     if (Tx > 256 && mw_enabled()) {
         w.W = 8;
-        w.KL = Tx <= 512 ? 1 : Tx <= 1024 ? 2 : Tx <= 2048 ? 4 : 8;
+        w.KL = Tx <= 512 ? 1 : Tx <= 1024 ? 2 : Tx <= 2048 ? 4 : Tx <= 4096 ? 8 : 16;  // (16: transposed lattice only)
         w.K = w.W * w.KL;
         w.Txp = kWave * w.K;
     }
@@ -1397,11 +1379,15 @@ int launch_dp_kc(const MasArgs &a, int B, bool vec, bool lds_bits, bool dp_out, 
 template <int KL, int W>
 int launch_dp_mw_tr(MasArgs a, int B, bool lds_bits, size_t shmem, hipStream_t st) {
     if (!lds_bits) shmem = mw_backtrack_bufs(a, shmem);
-    if (lds_bits) {
-        if (!mw_lds_attr(mas_dp_mw_kernel<KL, W, true, false, true, false, true>, shmem))
-            return mtts::fail(MTTS_ERR_HIP, "maximum_path: LDS attribute");
-        hipLaunchKernelGGL((mas_dp_mw_kernel<KL, W, true, false, true, false, true>), dim3(B), dim3(64 * W), shmem, st, a);
-    } else {
+    if constexpr (KL <= 8) {  // (KL = 16: Txp = 8192 rows never fit the LDS-bits budget)
+        if (lds_bits) {
+            if (!mw_lds_attr(mas_dp_mw_kernel<KL, W, true, false, true, false, true>, shmem))
+                return mtts::fail(MTTS_ERR_HIP, "maximum_path: LDS attribute");
+            hipLaunchKernelGGL((mas_dp_mw_kernel<KL, W, true, false, true, false, true>), dim3(B), dim3(64 * W), shmem, st, a);
+            return mtts::check_launch("mas_dp_mw_kernel");
+        }
+    }
+    {
         if (!mw_lds_attr(mas_dp_mw_kernel<KL, W, true, false, false, false, true>, shmem))
             return mtts::fail(MTTS_ERR_HIP, "maximum_path: LDS attribute");
         hipLaunchKernelGGL((mas_dp_mw_kernel<KL, W, true, false, false, false, true>), dim3(B), dim3(64 * W), shmem, st, a);
@@ -1439,7 +1425,8 @@ int launch_dp_tr(const MasArgs &a, int B, const WsLayout &w, hipStream_t st) {
             case 1: return launch_dp_mw_tr<1, 8>(a, B, w.lds_bits, shmem, st);
             case 2: return launch_dp_mw_tr<2, 8>(a, B, w.lds_bits, shmem, st);
             case 4: return launch_dp_mw_tr<4, 8>(a, B, w.lds_bits, shmem, st);
-            default: return launch_dp_mw_tr<8, 8>(a, B, w.lds_bits, shmem, st);
+            case 8: return launch_dp_mw_tr<8, 8>(a, B, w.lds_bits, shmem, st);
+            default: return launch_dp_mw_tr<16, 8>(a, B, false, shmem, st);  // Tx <= 8192 (global bits)
         }
     }
     const size_t shmem = (size_t)w.Txp * 4 + (w.lds_bits ? (size_t)w.Txp * w.nch * 4 : 0);
@@ -1459,6 +1446,9 @@ int launch_dp(MasArgs a, int B, const WsLayout &w, bool vec, bool dp_out, hipStr
     if (w.W > 1) {
         const size_t shmem = (size_t)w.Txp * 4 + (size_t)3 * w.W * 32 * 4 + (w.lds_bits ? (size_t)w.Txp * w.nch * 4 : 0);
         if (w.W < 8 && w.KL != 1) return mtts::fail(MTTS_ERR_UNSUPPORTED, "maximum_path: DP shape needs the transposed lattice");
+        if (w.KL > 8)
+            return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: Tx > 4096 needs the transposed lattice (compute_batch_alignments / "
+                                              "dp_out and MTTS_MAS_TR=0 keep the row-major lattice: Tx <= 4096)");
         if (w.W == 2) return launch_dp_mw_pm<1, 2>(a, B, vec, w.lds_bits, dp_out, shmem, st);
         if (w.W == 4) return launch_dp_mw_pm<1, 4>(a, B, vec, w.lds_bits, dp_out, shmem, st);
         switch (w.KL) {
@@ -1482,7 +1472,7 @@ int launch_dp(MasArgs a, int B, const WsLayout &w, bool vec, bool dp_out, hipStr
 int check_shape(int B, int Tx, int Ty) {
     if (B < 0 || Tx < 1 || Ty < 1) return mtts::fail(MTTS_ERR_INVALID_ARG, "maximum_path: bad shape");
     if (Tx > MTTS_MAS_MAX_TX || (Tx > 2048 && !mw_enabled()))
-        return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: Tx > MTTS_MAS_MAX_TX (4096) is not supported");
+        return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: Tx > MTTS_MAS_MAX_TX (8192) is not supported");
     if ((int64_t)Tx * Ty * 4 >= (int64_t)1 << 31)
         return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: one utterance's lattice exceeds 2 GiB");
     return MTTS_OK;

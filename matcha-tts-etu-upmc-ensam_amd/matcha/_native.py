@@ -18,7 +18,8 @@ LIB_PATH = Path(os.environ.get("MTTS_LIB", _PKG_ROOT / "lib" / "libmtts_hip.so")
 MTTS_OK = 0
 MTTS_MAS_VALUE_PREMASKED = 0x1
 MTTS_MAS_NO_DENSE_PATH = 0x2
-MTTS_MAS_MAX_TX = 4096  # include/mtts.h
+MTTS_MAS_MAX_TX = 8192  # include/mtts.h (maximum_path, prior_maximum_path)
+MTTS_MAS_MAX_TX_ROW_MAJOR = 4096  # include/mtts.h (compute_batch_alignments)
 
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32

@@ -16,14 +16,17 @@ import torch
 from matcha import _native as N
 
 
-def _check_tx(Tx: int) -> None:
-    """The DP keeps one utterance's text rows in one workgroup's registers (8 waves x 8 rows per lane at
-    most, csrc/mas.hip mas_dp_mw_kernel): t_x <= 4096.  The reference Cython (core.pyx:14-96) has no cap;
-    LJSpeech tops out near 190 tokens and BASELINE config 5 uses 512, so the limit is a documented shape
-    error, not a silent truncation."""
-    if Tx > N.MTTS_MAS_MAX_TX:
+def _check_tx(Tx: int, limit: int | None = None) -> None:
+    """The DP keeps one utterance's text rows in one workgroup's registers (8 waves x 16 rows per lane at
+    most, csrc/mas.hip mas_dp_mw_kernel): t_x <= 8192 (round 6; 4096 before), and 4096 for the row-major
+    lattice compute_batch_alignments mutates.  The reference Cython (core.pyx:14-96) has no cap; LJSpeech tops
+    out near 190 tokens and BASELINE config 5 uses 512, so the limit is a documented shape error, not a silent
+    truncation."""
+    limit = N.MTTS_MAS_MAX_TX if limit is None else limit
+    if Tx > limit:
         raise ValueError(f"maximum_path: text length {Tx} exceeds the GPU kernel's limit of "
-                         f"{N.MTTS_MAS_MAX_TX} rows (MTTS_MAS_MAX_TX, include/mtts.h)")
+                         f"{limit} rows (MTTS_MAS_MAX_TX{'' if limit == N.MTTS_MAS_MAX_TX else '_ROW_MAJOR'}, "
+                         f"include/mtts.h)")
 
 
 def _workspace(B: int, Tx: int, Ty: int, device) -> torch.Tensor:
@@ -85,7 +88,7 @@ def maximum_path_c(paths: torch.Tensor, values: torch.Tensor, t_xs: torch.Tensor
     if not (paths.is_contiguous() and values.is_contiguous()):
         raise ValueError("maximum_path_c mutates its arguments in place: they must be C-contiguous")
     B, Tx, Ty = values.shape
-    _check_tx(Tx)
+    _check_tx(Tx, N.MTTS_MAS_MAX_TX_ROW_MAJOR)
     t_xs = t_xs.to(torch.int32).contiguous()
     t_ys = t_ys.to(torch.int32).contiguous()
     dev = values.device

@@ -283,12 +283,33 @@ def test_expand_rows_matches_bmm_and_its_gradient():
 
 
 def test_text_length_limit_is_a_clear_error():
-    """Beyond MTTS_MAS_MAX_TX (4096 rows; the reference Cython has no cap) the wrapper refuses with a
-    ValueError naming the limit instead of a native shape error."""
+    """Beyond MTTS_MAS_MAX_TX (8192 rows; the reference Cython has no cap) the wrapper refuses with a
+    ValueError naming the limit instead of a native shape error; compute_batch_alignments (the row-major
+    lattice it mutates) keeps 4096 and says so."""
     import torch
 
-    from matcha.utils.monotonic_align import maximum_path
+    from matcha.utils.monotonic_align import maximum_path, maximum_path_c
 
-    v = torch.zeros(1, 4097, 4100, device="cuda")
-    with pytest.raises(ValueError, match="4096"):
+    v = torch.zeros(1, 8193, 8200, device="cuda")
+    with pytest.raises(ValueError, match="8192"):
         maximum_path(v, torch.ones_like(v))
+    del v
+    v = torch.zeros(1, 4097, 4100, device="cuda")
+    paths = torch.zeros(1, 4097, 4100, dtype=torch.int32, device="cuda")
+    t = torch.tensor([4097], dtype=torch.int32, device="cuda")
+    with pytest.raises(ValueError, match="4096"):
+        maximum_path_c(paths, v, t, torch.tensor([4100], dtype=torch.int32, device="cuda"))
+
+
+@pytest.mark.parametrize("Tx,Ty", [(4097, 4500), (6000, 6001), (8192, 8192)])
+def test_long_text_vs_oracle(Tx, Ty):
+    """Round 6: maximum_path beyond 4096 text rows (the multi-wave DP at 16 rows per lane, backpointers in HBM, the
+    backtrack from LDS slot copies) is bit-exact with the oracle, ties included."""
+    rng = np.random.default_rng(Tx + 3 * Ty)
+    for ties in (False, True):
+        value, t_x, t_y = _rand_case(rng, 1, Tx, Ty, ties)
+        t_x[0], t_y[0] = Tx, Ty
+        mask = O.lengths_mask(1, Tx, Ty, t_x, t_y)
+        exp_p, _ = O.mas_batch(value, t_x, t_y)
+        path, _, _ = gpu_path(value, mask)
+        np.testing.assert_array_equal(path, exp_p.astype(np.float32))

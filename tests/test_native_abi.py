@@ -46,8 +46,8 @@ def test_abi_version_and_error_slot():
     rc = lib.mtts_maximum_path_f32(None, None, None, 2, 0, 5, 0, None, None, None, 0, None)
     assert rc == -1  # MTTS_ERR_INVALID_ARG, before any HIP call
     assert b"bad shape" in lib.mtts_last_error()
-    rc = lib.mtts_maximum_path_f32(None, None, None, 2, 4097, 5, 0, None, None, None, 0, None)
-    assert rc == -2  # MTTS_ERR_SHAPE: Tx > MTTS_MAS_MAX_TX (4096)
+    rc = lib.mtts_maximum_path_f32(None, None, None, 2, 8193, 5, 0, None, None, None, 0, None)
+    assert rc == -2  # MTTS_ERR_SHAPE: Tx > MTTS_MAS_MAX_TX (8192)
     rc = lib.mtts_maximum_path_f32(None, None, None, 2, 5, 5, 0x80, None, None, None, 0, None)
     assert rc == -1  # unknown flag
     rc = lib.mtts_maximum_path_f32(ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16),

@@ -33,7 +33,7 @@ extern "C" int probe_mw(const float *lat, const int *txs, const int *tys, int *l
     hipStream_t st = (hipStream_t)stream;
     const int KL = Txp / 512;
     if (KL == 1) go<1>(a, B, shmem, st); else if (KL == 2) go<2>(a, B, shmem, st);
-    else if (KL == 4) go<4>(a, B, shmem, st); else go<8>(a, B, shmem, st);
+    else if (KL == 4) go<4>(a, B, shmem, st); else if (KL == 8) go<8>(a, B, shmem, st); else go<16>(a, B, shmem, st);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 extern "C" int probe_stamps(long long *host, int n) {
