@@ -1,4 +1,5 @@
 #!/bin/bash
+# (ran on the weight-resident schedule of round 6, since removed: profiles/r06/wlds/)
 # weight-resident GEMM (csrc/conv_gemm_wlds.hip): its tests, a replay of the step's bf16 GEMM launches on the
 # heuristic vs the new schedule, and bench A/B with the heuristic pick off / on -> gpurun_out/$TAG
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/${TAG:-r6wlds}; mkdir -p $O; cd $R
