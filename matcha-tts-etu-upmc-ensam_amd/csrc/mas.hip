@@ -271,9 +271,14 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
                         if constexpr (PM) sc = vbuf[sl][i][j];
                         else sc = vbuf[sl][i][j] * mbuf[sl][i][j];  // __init__.py:45
                         const float fp = i == 0 ? nb : dp[i - 1], fs = dp[i];
-                        const bool diag = fp >= fs;
-                        ndp[i] = (TR ? __builtin_amdgcn_fmed3f(fp, fs, INFINITY) : (diag ? fp : fs)) + sc;
-                        R[i] = (R[i] << 1) | (diag ? 1u : 0u);
+                        if constexpr (!DP_OUT) {  // round 6: raw max on the chain, bit by v_cmp + v_addc (off it)
+                            ndp[i] = vmax_raw(fp, fs) + sc;
+                            shift_in_ge(R[i], fp, fs);
+                        } else {  // (the mutated lattice is compared bit for bit: keep the select's signed zeros)
+                            const bool diag = fp >= fs;
+                            ndp[i] = (diag ? fp : fs) + sc;
+                            R[i] = (R[i] << 1) | (diag ? 1u : 0u);
+                        }
                     }
 #pragma unroll
                     for (int i = 0; i < K; ++i) dp[i] = ndp[i];
