@@ -488,9 +488,14 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
 
     int32_t *rs = reinterpret_cast<int32_t *>(smem);                // [Txp] row starts
     float *edge = reinterpret_cast<float *>(smem + Txp);            // [3][W][CC] last-row values per column
+    // TR, KL <= 2: chunks each wave has finished (its edge values written): the waves hand over through these instead
+    // of a workgroup barrier per chunk (round 6: the barriers took ~35 % of the forward DP at 8 x 512 x 4096)
+    __shared__ int mw_done[W];
+    if (threadIdx.x < W) mw_done[threadIdx.x] = 0;
     uint32_t *bits_l = smem + Txp + 3 * W * CC;                     // [nch][Txp] (LDS mode)
     uint32_t *bits_g = a.bits + (size_t)b * a.nch * Txp;
     for (int x = threadIdx.x; x < Txp; x += 64 * W) rs[x] = -1;
+    __syncthreads();  // mw_done is zero before any wave reads it
 
     const bool valid = t_x >= 1 && t_y >= 1 && t_x <= t_y && t_x <= Tx && t_y <= Ty;
     if (valid) {
@@ -727,20 +732,55 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
             }
         };
         static_for<0, RING - 1>([&](auto sv) { load_sub(sv, decltype(sv)::value * C); });
-        for (int i = 0; i < wave; ++i) mtts::lds_barrier();  // pipeline fill: wave w starts in phase w
-        for (int c = 0; c < nchunks; c += RING) {
-            bool go = true;
-            static_for<0, RING>([&](auto pv) {
-                constexpr int P = decltype(pv)::value;
-                if (go && c + P < nchunks) {
-                    chunk(pv, c + P);
-                    mtts::lds_barrier();
-                } else {
-                    go = false;
+        // (KL >= 4 keeps the barrier: there the spinning waves measured slower -- they take issue slots from their
+        // SIMD partners -- 2 x 4096 x 4200 DP 1466 -> 1581 us, 1 x 5000 x 5600 3798 -> 4058 us; KL = 1 / 2: 8 x 512 x 4096
+        // 250 -> 227 us, 8 x 1024 x 4096 572 -> 497 us; tools/r6/mas_probe.py)
+        if constexpr (TR && KL <= 2) {
+            // point-to-point hand-over: before chunk c, wave w waits until wave w - 1 has finished chunk c (its edge
+            // values for c and c - 1 are in the ring) and until wave w + 1 has finished chunk c - 2 (the last reader of
+            // the ring slot chunk c overwrites: wave w + 1 reads slot (c - 3) % 3 in its chunk c - 3 and that slot's last
+            // value in its chunk c - 2); after chunk c it publishes c + 1 once its LDS writes have landed.  The spin is
+            // bounded (every wave reaches the end whatever happens); a bound hit would only corrupt the path.
+            auto wait_ge = [&](int w2, int target) {
+                for (int spins = 0; spins < (1 << 22); ++spins) {
+                    if (__hip_atomic_load(&mw_done[w2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+                    __builtin_amdgcn_s_sleep(1);
                 }
-            });
+                asm volatile("" ::: "memory");  // the ring reads stay after the wait
+            };
+            for (int c = 0; c < nchunks; c += RING) {
+                bool go = true;
+                static_for<0, RING>([&](auto pv) {
+                    constexpr int P = decltype(pv)::value;
+                    const int cc = c + P;
+                    if (go && cc < nchunks) {
+                        if (wave > 0) wait_ge(wave - 1, cc + 1);
+                        if (wave < W - 1 && cc >= 2) wait_ge(wave + 1, cc - 1);
+                        chunk(pv, cc);
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's edge writes have landed
+                        if (lane == 0)
+                            __hip_atomic_store(&mw_done[wave], cc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else {
+                        go = false;
+                    }
+                });
+            }
+        } else {
+            for (int i = 0; i < wave; ++i) mtts::lds_barrier();  // pipeline fill: wave w starts in phase w
+            for (int c = 0; c < nchunks; c += RING) {
+                bool go = true;
+                static_for<0, RING>([&](auto pv) {
+                    constexpr int P = decltype(pv)::value;
+                    if (go && c + P < nchunks) {
+                        chunk(pv, c + P);
+                        mtts::lds_barrier();
+                    } else {
+                        go = false;
+                    }
+                });
+            }
+            for (int i = wave; i < W - 1; ++i) mtts::lds_barrier();  // drain: every wave runs nchunks + W - 1 phases
         }
-        for (int i = wave; i < W - 1; ++i) mtts::lds_barrier();  // drain: every wave runs nchunks + W - 1 phases
     }
     if constexpr (!LDS_BITS) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
