@@ -432,7 +432,7 @@ __global__ __launch_bounds__(kWave, 1) void mas_dp_kernel(MasArgs a) {
 // KL text rows t*KL .. t*KL+KL-1.  A column's cells depend only on the previous column, so the waves
 // split the rows and run as a pipeline skewed by one 32-column chunk: in phase p wave w processes chunk
 // p - w; the x-1 neighbour of its first row is the previous wave's last row one column earlier, which
-// that wave's lane 63 wrote to an LDS edge ring (3 chunks deep) one or two phases before; a workgroup
+// that wave's lane 63 wrote to an LDS edge ring (kEdgeRing chunks deep) one or two phases before; a workgroup
 // barrier (LDS-only) ends every phase.  Per chunk a lane flushes one backpointer word per row (the
 // chunk IS one 32-column word).  Same arithmetic per cell as mas_dp_kernel (bit-exact with core.pyx);
 // the chain per column shrinks from K = Tx/64 rows per lane (one wave) to KL (e.g. Tx = 512: 8 -> 1)
@@ -447,6 +447,10 @@ __device__ long long mas_probe_stamps[4096 * 4];
 #else
 #define MAS_STAMP(i)
 #endif
+// edge ring depth in chunks: with the point-to-point hand-over (TR, KL <= 2) a wave may run up to kEdgeRing - 2 chunks
+// ahead of its successor, so the successor's hand-over latency leaves the chunk period once the ring is deep
+// enough: at 3 slots the period was a chunk's compute + one hand-over (round 6, tools/r6/mas_probe.py)
+constexpr int kEdgeRing = 6;
 template <int KL, int W, bool PM, bool VEC, bool LDS_BITS, bool DP_OUT, bool TR = false>
 __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
     MAS_STAMP(0);
@@ -487,12 +491,12 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
     }
 
     int32_t *rs = reinterpret_cast<int32_t *>(smem);                // [Txp] row starts
-    float *edge = reinterpret_cast<float *>(smem + Txp);            // [3][W][CC] last-row values per column
+    float *edge = reinterpret_cast<float *>(smem + Txp);            // [kEdgeRing][W][CC] last-row values per column
     // TR, KL <= 2: chunks each wave has finished (its edge values written): the waves hand over through these instead
     // of a workgroup barrier per chunk (round 6: the barriers took ~35 % of the forward DP at 8 x 512 x 4096)
     __shared__ int mw_done[W];
     if (threadIdx.x < W) mw_done[threadIdx.x] = 0;
-    uint32_t *bits_l = smem + Txp + 3 * W * CC;                     // [nch][Txp] (LDS mode)
+    uint32_t *bits_l = smem + Txp + kEdgeRing * W * CC;                     // [nch][Txp] (LDS mode)
     uint32_t *bits_g = a.bits + (size_t)b * a.nch * Txp;
     for (int x = threadIdx.x; x < Txp; x += 64 * W) rs[x] = -1;
     __syncthreads();  // mw_done is zero before any wave reads it
@@ -571,7 +575,7 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
         // of the sub-chunk RING - 1 ahead issued before each one is processed
         auto chunk = [&](auto phase3, int c) {
             constexpr int P = decltype(phase3)::value;
-            const int r3 = c % 3, p3 = (c + 2) % 3;
+            const int r3 = c % kEdgeRing, p3 = (c + kEdgeRing - 1) % kEdgeRing;  // this chunk's / the previous one's ring slot
             // TR: the lane-0 neighbours of the whole chunk, read once (broadcast ds_read_b128: every lane the same
             // address) -- column y needs the previous wave's last row after column y - 1 (ring slot of chunk c, or of
             // chunk c - 1 for the chunk's first column); wave 0 has none (0 before column 0, else max_neg_val)
@@ -737,9 +741,10 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
         // 250 -> 227 us, 8 x 1024 x 4096 572 -> 497 us; tools/r6/mas_probe.py)
         if constexpr (TR && KL <= 2) {
             // point-to-point hand-over: before chunk c, wave w waits until wave w - 1 has finished chunk c (its edge
-            // values for c and c - 1 are in the ring) and until wave w + 1 has finished chunk c - 2 (the last reader of
-            // the ring slot chunk c overwrites: wave w + 1 reads slot (c - 3) % 3 in its chunk c - 3 and that slot's last
-            // value in its chunk c - 2); after chunk c it publishes c + 1 once its LDS writes have landed.  The spin is
+            // values for c and c - 1 are in the ring) and until wave w + 1 has finished chunk c - kEdgeRing + 1 (the last
+            // reader of the ring slot chunk c overwrites: wave w + 1 reads the slot of chunk c - kEdgeRing in its chunk
+            // c - kEdgeRing and that slot's last value in its next chunk); after chunk c it publishes c + 1 once its LDS
+            // writes have landed.  The spin is
             // bounded (every wave reaches the end whatever happens); a bound hit would only corrupt the path.
             auto wait_ge = [&](int w2, int target) {
                 for (int spins = 0; spins < (1 << 22); ++spins) {
@@ -755,7 +760,7 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
                     const int cc = c + P;
                     if (go && cc < nchunks) {
                         if (wave > 0) wait_ge(wave - 1, cc + 1);
-                        if (wave < W - 1 && cc >= 2) wait_ge(wave + 1, cc - 1);
+                        if (wave < W - 1 && cc >= kEdgeRing - 1) wait_ge(wave + 1, cc - kEdgeRing + 2);
                         chunk(pv, cc);
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's edge writes have landed
                         if (lane == 0)
@@ -891,7 +896,8 @@ __global__ __launch_bounds__(64 * W) void mas_dp_mw_kernel(MasArgs a) {
             if (wave == 0) {
                 // the slot's row starts gather in lane (row & 63) of rsv (a lane select) and go to LDS once per slot; the
                 // step's decisions are selects, not branches (the first version spent ~40 scalar instructions and six
-                // branches per row step)
+                // branches per row step).  (A read-ahead of the previous column's word, round 6, measured slower:
+                // 8 x 512 x 4096 89 -> 100 us, 2 x 4096 x 4200 525 -> 653 us.)
                 int rsv = -1;
                 while (!done && idx >= kWave * r) {
                     if (idx == 0 || idx >= y) {  // the rest of the path is the diagonal x == y (or row 0 at column 0)
@@ -1324,7 +1330,7 @@ WsLayout ws_layout(int B, int Tx, int Ty, bool with_lat = false, bool shape_over
 }
 
 // dynamic LDS past 64 KiB needs the kernel attribute (a long Ty's backtrack slot copy: nch x 256 B)
-constexpr size_t kMwLdsMax = 160 * 1024;
+constexpr size_t kMwLdsMax = 160 * 1024 - 256;  // (the kernel's static hand-over flags take the rest)
 // global-bits mode: as many backtrack slot buffers (nch x 256 B each, at most 2) as the LDS holds beside `shmem`;
 // sets a.bt_bufs and returns the launch's LDS bytes
 size_t mw_backtrack_bufs(MasArgs &a, size_t shmem) {
@@ -1334,7 +1340,7 @@ size_t mw_backtrack_bufs(MasArgs &a, size_t shmem) {
 }
 template <typename K>
 bool mw_lds_attr(K kernel, size_t bytes) {
-    if (bytes <= 64 * 1024) return true;
+    if (bytes + 256 <= 64 * 1024) return true;  // (+ the static hand-over flags)
     return hipFuncSetAttribute(reinterpret_cast<const void *>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)bytes) == hipSuccess;
 }
@@ -1460,7 +1466,7 @@ int launch_dp_kc_tr(const MasArgs &a, int B, bool lds_bits, size_t shmem, hipStr
 // The DP on the transposed premasked lattice (a.tr_ld > 0): same kernels, column-major loads
 int launch_dp_tr(const MasArgs &a, int B, const WsLayout &w, hipStream_t st) {
     if (w.W > 1) {
-        const size_t shmem = (size_t)w.Txp * 4 + (size_t)3 * w.W * 32 * 4 + (w.lds_bits ? (size_t)w.Txp * w.nch * 4 : 0);
+        const size_t shmem = (size_t)w.Txp * 4 + (size_t)kEdgeRing * w.W * 32 * 4 + (w.lds_bits ? (size_t)w.Txp * w.nch * 4 : 0);
         if (w.W == 2) return w.KL == 2 ? launch_dp_mw_tr<2, 2>(a, B, w.lds_bits, shmem, st)
                                        : launch_dp_mw_tr<1, 2>(a, B, w.lds_bits, shmem, st);
         if (w.W == 4) return w.KL == 4   ? launch_dp_mw_tr<4, 4>(a, B, w.lds_bits, shmem, st)
@@ -1489,7 +1495,7 @@ int launch_dp(MasArgs a, int B, const WsLayout &w, bool vec, bool dp_out, hipStr
     if (a.tr_ld > 0) return dp_out ? mtts::fail(MTTS_ERR_INVALID_ARG, "maximum_path: dp_out needs the row-major lattice")
                                    : launch_dp_tr(a, B, w, st);
     if (w.W > 1) {
-        const size_t shmem = (size_t)w.Txp * 4 + (size_t)3 * w.W * 32 * 4 + (w.lds_bits ? (size_t)w.Txp * w.nch * 4 : 0);
+        const size_t shmem = (size_t)w.Txp * 4 + (size_t)kEdgeRing * w.W * 32 * 4 + (w.lds_bits ? (size_t)w.Txp * w.nch * 4 : 0);
         if (w.W < 8 && w.KL != 1) return mtts::fail(MTTS_ERR_UNSUPPORTED, "maximum_path: DP shape needs the transposed lattice");
         if (w.KL > 8)
             return mtts::fail(MTTS_ERR_SHAPE, "maximum_path: Tx > 4096 needs the transposed lattice (compute_batch_alignments / "

@@ -29,7 +29,7 @@ extern "C" int probe_mw(const float *lat, const int *txs, const int *tys, int *l
     MasArgs a{};
     a.value = lat; a.t_xs = txs; a.t_ys = tys; a.lengths = lengths; a.row_start = row_start; a.bits = bits;
     a.Tx = Tx; a.Ty = Ty; a.Txp = Txp; a.nch = nch; a.premasked = 1; a.neg = neg; a.tr_ld = Txp;
-    const size_t shmem = mw_backtrack_bufs(a, (size_t)Txp * 4 + (size_t)3 * 8 * 32 * 4);
+    const size_t shmem = mw_backtrack_bufs(a, (size_t)Txp * 4 + (size_t)kEdgeRing * 8 * 32 * 4);
     hipStream_t st = (hipStream_t)stream;
     const int KL = Txp / 512;
     if (KL == 1) go<1>(a, B, shmem, st); else if (KL == 2) go<2>(a, B, shmem, st);
