@@ -120,9 +120,10 @@ def mas_chain_bound(Tx: int, Ty: int, mas_ms: float, clock_ghz: float = 2.1) -> 
     plus a DPP neighbour exchange, each waiting ~8 cycles for its predecessor at one wave per SIMD.
     Tx > 256 -- eight waves per utterance (mas_dp_mw_kernel), KL = 1, 2, 4, 8 rows per lane (Tx <= 512 ... 4096),
     pipelined one 32-column chunk apart: per column two waves per SIMD each issue ~(5 KL + 4) instructions
-    (interior cells + exchange / bookkeeping) at ~4 cycles each -- an ISSUE bound, ignoring the per-chunk LDS
-    barrier -- over Ty + 7 * 32 columns (the pipeline fill).  measured / estimate >= 1 by construction; its
-    size says how far the kernel is from the issue bound (the barrier waits)."""
+    (interior cells + exchange / bookkeeping) at ~4 cycles each -- an ISSUE bound, ignoring the per-chunk
+    synchronisation (a wave-to-wave LDS hand-over at KL <= 2, a workgroup barrier above) -- over Ty + 7 * 32
+    columns (the pipeline fill).  measured / estimate >= 1 by construction; its size says how far the kernel is
+    from the issue bound (DESIGN.md §3 round 6, §8 #4)."""
     if Tx <= 256:
         K = 1 if Tx <= 64 else 2 if Tx <= 128 else 4
         cyc_per_col, cols, shape = (9 * K + 2) * 8, Ty, {"waves": 1, "rows_per_lane": K}
